@@ -1,0 +1,184 @@
+/* libmrl_hip -- C ABI of the MI355X-native TRPO hot path (gfx950 HIP kernels).
+ *
+ * The reference (ddlau/modular_rl) has no native code and no FFI: its hot path is
+ * Theano-compiled graphs and numpy called from Python.  This
+ * header is the boundary the Python host layer (`modular_rl_amd/_lib.py`, ctypes)
+ * binds; each entry cites the reference interface it replaces.
+ *
+ * Conventions
+ *  - Every function returns 0 on success, <0 on error (MRL_E_*); the message is in
+ *    mrl_last_error().  No C++ exception crosses the ABI.
+ *  - All buffers are caller-owned DEVICE pointers (e.g. torch.Tensor.data_ptr());
+ *    every call is asynchronous on `stream` (a hipStream_t), no host sync, no
+ *    allocation -- so the whole hot path can be captured in a hipGraph.
+ *  - Row n of every [N, ...] batch array is time-major: n = t * n_envs + e.
+ *  - `skip` (may be NULL): device int; when *skip != 0 the kernel returns at once
+ *    (device-side early exit of the conjugate-gradient loop, trpo.py:192-193).
+ */
+#ifndef MRL_HIP_H
+#define MRL_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MRL_OK 0
+#define MRL_E_ARG (-1)
+#define MRL_E_UNSUPPORTED (-2)
+#define MRL_E_HIP (-3)
+
+/* head kinds */
+#define MRL_HEAD_LINEAR 0   /* value net, Dense(1)                 agentzoo.py:58      */
+#define MRL_HEAD_SOFTMAX 1  /* Categorical, Dense(k, softmax)      agentzoo.py:46      */
+#define MRL_HEAD_GAUSS 2    /* DiagGauss, Dense(d) + ConcatFixedStd agentzoo.py:40-43 */
+
+/* tanh MLP shape: n_in -> 64 -> 64 -> n_out (the fast path; hid_sizes=[64,64],
+ * agentzoo.py:20-23).  Other shapes return MRL_E_UNSUPPORTED (no CPU fallback). */
+typedef struct {
+  int32_t n_in;    /* input features (obs dim, +1 for the VF time feature)   */
+  int32_t n_out;   /* k (Categorical), d (DiagGauss) or 1 (value)             */
+  int32_t head;    /* MRL_HEAD_*                                              */
+  int32_t n_hidden;/* must be 64                                              */
+  int32_t n_layers;/* must be 2                                               */
+} mrl_mlp_desc;
+
+const char* mrl_last_error(void);
+int32_t mrl_version(void);
+
+/* number of float parameters (flat theta, Keras trainable_weights order,
+ * core.py:518-557) and of floats in the packed LDS image */
+int64_t mrl_mlp_num_params(const mrl_mlp_desc* d);
+int64_t mrl_mlp_image_floats(const mrl_mlp_desc* d);
+
+/* theta (fp32 flat) -> image.  Replaces SetFromFlat (core.py:527-541): the
+ * kernels read weights only through the image.  fwd_only: skip backward frags. */
+int mrl_mlp_pack(const mrl_mlp_desc* d, const float* theta, float* image, int32_t fwd_only,
+                 const int32_t* skip, void* stream);
+
+/* row epilogues of the fused forward pass (mrl_mlp_rows) */
+#define MRL_EPI_PROB 0      /* out <- prob rows [N,k] / [N,2d] / value [N]     core.py:261-270, 648-650 */
+#define MRL_EPI_LOSSES 1    /* partial <- (sum ratio*adv, sum KL(old,new), sum ent)  trpo.py:60-64    */
+#define MRL_EPI_SURRGRAD 2  /* LOSSES + ghead <- d surr / d head rows              trpo.py:42-43     */
+#define MRL_EPI_VFLOSS 3    /* partial <- sum (y-yhat)^2; ghead <- 2(yhat-y)/N_glob core.py:611-617  */
+#define MRL_EPI_FVP 4       /* forward + JVP(tangent) + KL metric -> ghead rows      trpo.py:45-58   */
+
+typedef struct {
+  const float* x;          /* [N, n_obs] observations                              */
+  const int32_t* ep_t;     /* [N] step index in episode (VF time feature) or NULL  */
+  double timestep_limit;   /* time feature = ep_t / timestep_limit (core.py:660)   */
+  int64_t n;               /* rows                                                 */
+  double inv_n_global;     /* 1 / rows summed over all ranks                       */
+  const void* act;         /* [N] int32 (Categorical) | [N, d] float (DiagGauss)   */
+  const float* adv;        /* [N] standardized advantages                          */
+  const float* oldprob;    /* [N, k] | [N, 2d] rollout-time prob rows              */
+  const float* target;     /* [N] VF regression target                             */
+  float* out;              /* EPI_PROB output                                      */
+  float* ghead;            /* [N, gh] head-gradient rows (gh = k, 2d or 1)         */
+  double* partial;         /* [mrl_partial_rows(n), 4] fp64 per-wave partial sums  */
+} mrl_rows_io;
+
+int64_t mrl_partial_rows(int64_t n);  /* rows of `partial` a call over n rows writes */
+int64_t mrl_slab_rows(int64_t n);     /* rows of the mrl_mlp_vjp slab                */
+
+/* fused forward (+ JVP for EPI_FVP) with a per-row epilogue.
+ * theta: flat fp32 params (for logstd); image: packed primal image;
+ * tangent/image_t: flat fp32 tangent and its packed image (EPI_FVP only). */
+int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epilogue, const float* theta, const float* image,
+                 const float* tangent, const float* image_t, const mrl_rows_io* io,
+                 const int32_t* skip, void* stream);
+
+/* vector-Jacobian product: slab[w, :] <- per-wave partial of sum_n J_n^T ghead_n in
+ * flat theta layout (head columns beyond n_out -- DiagGauss logstd -- are summed
+ * into the logstd slots).  Replaces flatgrad / the VJP half of the Theano Fvp. */
+int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const int32_t* ep_t,
+                double timestep_limit, const float* ghead, int64_t n, float* slab, const int32_t* skip,
+                void* stream);
+
+/* out[c] = sum_r slab[r, c] in fixed order with fp64 accumulation */
+int mrl_reduce_rows_f32(const float* slab, int64_t rows, int64_t cols, float* out, const int32_t* skip, void* stream);
+int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* out, const int32_t* skip, void* stream);
+
+/* ---------------------------------------------------------------- conjugate gradient
+ * Device-resident Demmel CG on flat fp64 vectors (trpo.py:165-200).
+ * state (fp64): [0]=rdotr [1]=last pz [2]=iterations run; flag (int32[2]): [0]=converged.
+ * init:   x=0, r=p=b, rdotr=r.r, p32=(float)p, flag=0.
+ * update: z = fvp + damping*p; v=rdotr/p.z; x+=v p; r-=v z; mu=r.r/rdotr; p=r+mu p;
+ *         flag=1 when rdotr<tol; pass `flag` as the `skip` of the next Fvp kernels. */
+int mrl_cg_init(const double* b, int64_t n, double* x, double* r, double* p, float* p32, double* state,
+                int32_t* flag, void* stream);
+int mrl_cg_update(const float* fvp, double damping, double residual_tol, int64_t n, double* x, double* r,
+                  double* p, float* p32, double* state, int32_t* flag, void* stream);
+/* step scaling (trpo.py:119-124): shs = .5 x.(fvp + damping x), lm = sqrt(shs/max_kl),
+ * fullstep = x/lm, out[0]=shs out[1]=lm out[2]=-g.x out[3]=-g.x/lm (expected rate) */
+int mrl_trpo_step(const float* fvp, const double* x, const float* g, double damping, double max_kl,
+                  int64_t n, double* fullstep, double* out, void* stream);
+/* theta_out = (float)(theta_old + frac * fullstep)   (linesearch, trpo.py:150, core.py:540) */
+int mrl_axpy_cast(const float* theta_old, const double* fullstep, double frac, int64_t n, float* theta_out,
+                  void* stream);
+/* out (fp64) = scale * (double)in ; in-place-safe */
+int mrl_cast_scale_f32_f64(const float* in, double scale, int64_t n, double* out, void* stream);
+
+/* ---------------------------------------------------------------- advantage
+ * GAE + discounted return over time-major [T, E] rows (core.py:63-75 with
+ * misc_utils.py:9-27 discount): flags bit0 = episode ends at this row, bit1 = the
+ * env terminated (bootstrap 0) else bootstrap with the row's own baseline (core.py:73).
+ * moments (fp64 [3]) <- (sum adv, sum adv^2, count)  (for core.py:100-105). */
+int mrl_gae(const float* rew, const float* vpred, const uint8_t* flags, int64_t T, int64_t E, double gamma,
+            double lam, float* adv, float* ret, double* moments, void* workspace, void* stream);
+int64_t mrl_gae_workspace_bytes(int64_t T, int64_t E);
+/* adv <- (adv - mean)/std from global moments (sum, sumsq, n): numpy std, ddof=0, no eps */
+int mrl_standardize(float* adv, int64_t n, const double* moments, void* stream);
+/* y = mixfrac * ret + (1 - mixfrac) * vpred  (NnRegression.fit target, core.py:622-624) */
+int mrl_vf_target(const float* ret, const float* vpred, double mixfrac, int64_t n, float* y, void* stream);
+
+/* ---------------------------------------------------------------- batched rollout
+ * Replaces do_rollouts_serial/rollout (core.py:174-221) + ZFilter (filters.py:17-40)
+ * + StochPolicy.act (core.py:261-267) + gym env.step: E envs step in lock-step on
+ * device for T steps.  Per step the E new observations are merged into the running
+ * stat (Chan merge of per-block Welford partials in block order), then normalised. */
+#define MRL_ENV_CARTPOLE 0  /* CartPole-v0 equations (gym), k = 2            */
+#define MRL_ENV_HOPPER 1    /* Hopper-v2-shaped surrogate, obs 11 / act 3     */
+
+typedef struct {
+  int32_t env_id;          /* MRL_ENV_*                                          */
+  int32_t n_envs;          /* E on this rank                                     */
+  int32_t horizon;         /* T steps per iteration                              */
+  int32_t timestep_limit;  /* episode cut (core.py:190, run_pg.py:103-105)       */
+  int32_t filter;          /* 1: ZFilter obs (clip 5) + reward RunningStat       */
+  int32_t env_offset;      /* rank * E: global env id for the RNG streams         */
+  uint64_t seed;           /* Philox key                                         */
+} mrl_rollout_desc;
+
+typedef struct {
+  double* env_state;       /* [state_doubles, E] SoA                             */
+  int32_t* env_int;        /* [2, E]: steps in episode, episodes started         */
+  double* filter_state;    /* [2, filter_doubles] ping-pong running stats        */
+  double* records;         /* [2, n_blocks, record_doubles] per-block partials   */
+  int64_t* iteration;      /* device iteration counter (RNG step base)           */
+  float* obs;              /* [T*E, obs_dim] filtered observations (core.py:191-192) */
+  void* act;               /* [T*E] int32 | [T*E, d] float                        */
+  float* prob;             /* [T*E, k | 2d]                                       */
+  float* rew;              /* [T*E] raw rewards (core.py:198)                     */
+  uint8_t* flags;          /* [T*E] bit0 last-of-episode, bit1 terminated         */
+  int32_t* ep_t;           /* [T*E] step index of the row inside its episode      */
+  const void* noise;       /* optional injected noise [T*E] u | [T*E, d] z        */
+} mrl_rollout_bufs;
+
+int64_t mrl_env_state_doubles(int32_t env_id);
+int64_t mrl_filter_doubles(int32_t env_id);
+int64_t mrl_record_doubles(int32_t env_id);
+int64_t mrl_rollout_blocks(int32_t n_envs);
+/* reset every env (start of iteration, core.py:186) and publish obs_0 partials */
+int mrl_rollout_reset(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void* stream);
+/* one lock-step env step t (0 <= t < horizon) for all envs */
+int mrl_rollout_step(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta,
+                     const float* image, const mrl_rollout_bufs* b, int32_t t, void* stream);
+/* after step T-1: fold the last reward partials into the reward stat, advance the
+ * iteration counter (obs_T is never pushed: the horizon cuts the episode) */
+int mrl_rollout_finish(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,120 @@
+"""ctypes binding of libmrl_hip.so (the C ABI declared in include/mrl_hip.h).
+
+There is no CPU fallback: if the library is missing or no GPU is visible the
+product path raises ``MrlError`` (the oracle in ``oracle/`` is test-only).
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmrl_hip.so")
+
+OK = 0
+HEAD_LINEAR, HEAD_SOFTMAX, HEAD_GAUSS = 0, 1, 2
+EPI_PROB, EPI_LOSSES, EPI_SURRGRAD, EPI_VFLOSS, EPI_FVP = 0, 1, 2, 3, 4
+ENV_CARTPOLE, ENV_HOPPER = 0, 1
+
+vp = ctypes.c_void_p
+i32 = ctypes.c_int32
+i64 = ctypes.c_int64
+f64 = ctypes.c_double
+
+
+class MrlError(RuntimeError):
+    pass
+
+
+class MlpDesc(ctypes.Structure):
+    _fields_ = [("n_in", i32), ("n_out", i32), ("head", i32), ("n_hidden", i32), ("n_layers", i32)]
+
+
+class RowsIO(ctypes.Structure):
+    _fields_ = [("x", vp), ("ep_t", vp), ("timestep_limit", f64), ("n", i64), ("inv_n_global", f64),
+                ("act", vp), ("adv", vp), ("oldprob", vp), ("target", vp), ("out", vp), ("ghead", vp),
+                ("partial", vp)]
+
+
+class RolloutDesc(ctypes.Structure):
+    _fields_ = [("env_id", i32), ("n_envs", i32), ("horizon", i32), ("timestep_limit", i32), ("filter", i32),
+                ("env_offset", i32), ("seed", ctypes.c_uint64)]
+
+
+class RolloutBufs(ctypes.Structure):
+    _fields_ = [("env_state", vp), ("env_int", vp), ("filter_state", vp), ("records", vp), ("iteration", vp),
+                ("obs", vp), ("act", vp), ("prob", vp), ("rew", vp), ("flags", vp), ("ep_t", vp), ("noise", vp)]
+
+
+# name -> (restype, argtypes); every symbol include/mrl_hip.h declares
+SIGNATURES = {
+    "mrl_last_error": (ctypes.c_char_p, []),
+    "mrl_version": (i32, []),
+    "mrl_mlp_num_params": (i64, [vp]),
+    "mrl_mlp_image_floats": (i64, [vp]),
+    "mrl_mlp_pack": (i32, [vp, vp, vp, i32, vp, vp]),
+    "mrl_partial_rows": (i64, [i64]),
+    "mrl_slab_rows": (i64, [i64]),
+    "mrl_mlp_rows": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, vp]),
+    "mrl_mlp_vjp": (i32, [vp, vp, vp, vp, f64, vp, i64, vp, vp, vp]),
+    "mrl_reduce_rows_f32": (i32, [vp, i64, i64, vp, vp, vp]),
+    "mrl_reduce_rows_f64": (i32, [vp, i64, i64, vp, vp, vp]),
+    "mrl_cg_init": (i32, [vp, i64, vp, vp, vp, vp, vp, vp, vp]),
+    "mrl_cg_update": (i32, [vp, f64, f64, i64, vp, vp, vp, vp, vp, vp, vp]),
+    "mrl_trpo_step": (i32, [vp, vp, vp, f64, f64, i64, vp, vp, vp]),
+    "mrl_axpy_cast": (i32, [vp, vp, f64, i64, vp, vp]),
+    "mrl_cast_scale_f32_f64": (i32, [vp, f64, i64, vp, vp]),
+    "mrl_gae": (i32, [vp, vp, vp, i64, i64, f64, f64, vp, vp, vp, vp, vp]),
+    "mrl_gae_workspace_bytes": (i64, [i64, i64]),
+    "mrl_standardize": (i32, [vp, i64, vp, vp]),
+    "mrl_vf_target": (i32, [vp, vp, f64, i64, vp, vp]),
+    "mrl_env_state_doubles": (i64, [i32]),
+    "mrl_filter_doubles": (i64, [i32]),
+    "mrl_record_doubles": (i64, [i32]),
+    "mrl_rollout_blocks": (i64, [i32]),
+    "mrl_rollout_reset": (i32, [vp, vp, vp]),
+    "mrl_rollout_step": (i32, [vp, vp, vp, vp, vp, i32, vp]),
+    "mrl_rollout_finish": (i32, [vp, vp, vp]),
+}
+
+_lib = None
+
+
+def load(require_gpu=False):
+    """Load libmrl_hip.so once; raise MrlError if it is absent (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MrlError(f"{LIB_PATH} is not built: run `make` (or __graft_entry__.build()); "
+                           "modular_rl_amd has no CPU fallback")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    if require_gpu and not torch.cuda.is_available():
+        raise MrlError("modular_rl_amd needs a ROCm GPU (MI355X); none is visible and there is no CPU fallback")
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != OK:
+        msg = load().mrl_last_error().decode()
+        raise MrlError(f"{what}: rc={rc}: {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    check(rc, name)

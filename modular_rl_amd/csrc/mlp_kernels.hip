@@ -1,0 +1,632 @@
+// Fused MLP kernels of the TRPO hot path on v_mfma_f32_32x32x2_f32 (exact fp32).
+//
+//   mlp_rows_kernel<EPI>  forward (+ JVP) of a 32-row tile per wave with a per-row
+//                         epilogue: prob rows, TRPO losses, surrogate gradient rows,
+//                         VF loss rows, or the KL-metric rows of the Fisher product.
+//   mlp_vjp_kernel        forward recompute + backprop of head-gradient rows and the
+//                         weight-gradient sums  sum_rows act^T * grad  (MFMA with the
+//                         row index as K, operands transposed through LDS).
+//
+// Replaces the Theano-compiled functions of the reference: _act_prob
+// (core.py:269-270), compute_policy_gradient / compute_losses /
+// compute_fisher_vector_product (trpo.py:68-70), NnRegression.predict and
+// LbfgsOptimizer.f_lossgrad (core.py:608, 670-671).  The Fisher product uses the
+// exact Gauss-Newton form of Theano's double backprop:
+// JVP -> per-row KL metric -> VJP.
+#include <math.h>
+
+#include "../../include/mrl_hip.h"
+#include "mlp_device.h"
+
+namespace mrl {
+
+static thread_local std::string g_err;
+void set_error(const std::string& s) { g_err = s; }
+int fail(int code, const std::string& s) {
+  g_err = s;
+  return code;
+}
+int hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    return E_HIP;
+  }
+  return OK;
+}
+
+constexpr int ROWS_BLOCK = 256;
+constexpr int ROWS_MAX_BLOCKS = 1024;
+constexpr int VJP_MAX_BLOCKS = 256;
+constexpr int SCR_FLOATS = 2 * 64 * IMG_PAD;  // per-wave transpose scratch
+
+static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+struct RowsArgs {
+  MlpDims d;
+  int head, n_obs, gh;
+  const float* x;
+  const int32_t* ept;
+  double ts_limit;
+  int64_t n;
+  double inv_ng;
+  const void* act;
+  const float* adv;
+  const float* oldprob;
+  const float* target;
+  float* out;
+  float* ghead;
+  double* partial;
+  const float* logstd;   // theta + tls (DiagGauss) or nullptr
+  const float* dlogstd;  // tangent + tls (EPI_FVP, DiagGauss) or nullptr
+};
+
+constexpr float LOG2PI_F = 1.8378770664093453f;
+constexpr float LOG2PIE_F = 2.8378770664093453f;
+
+template <int EPI>
+__global__ __launch_bounds__(ROWS_BLOCK) void mlp_rows_kernel(RowsArgs a, const float* __restrict__ img,
+                                                               const float* __restrict__ imgt,
+                                                               const int32_t* __restrict__ skip) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (skip != nullptr && *skip != 0) return;
+  const MlpDims& d = a.d;
+  const int fs = d.fwd_size;
+  for (int i = threadIdx.x; i < fs / 4; i += ROWS_BLOCK)
+    reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img)[i];
+  if (EPI == MRL_EPI_FVP)
+    for (int i = threadIdx.x; i < fs / 4; i += ROWS_BLOCK)
+      reinterpret_cast<float4*>(lds + fs)[i] = reinterpret_cast<const float4*>(imgt)[i];
+  __syncthreads();
+  const float* ldt = lds + fs;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int A = d.A;
+  float ls[MAX_OUT], sd[MAX_OUT], dls[MAX_OUT];
+#pragma unroll
+  for (int j = 0; j < MAX_OUT; ++j) {
+    ls[j] = (a.logstd != nullptr && j < A) ? a.logstd[j] : 0.f;
+    sd[j] = expf(ls[j]);
+    dls[j] = (a.dlogstd != nullptr && j < A) ? a.dlogstd[j] : 0.f;
+  }
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+  const int64_t ntiles = (a.n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t row = tile * 32 + (lane & 31);
+    const bool valid = row < a.n;
+    XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
+    Fwd f;
+    forward_tile<true>(lds, d, xl, lane, f);
+    float z[MAX_OUT];
+    head_gather(f.z, lane, z);
+    float dz[MAX_OUT];
+    if (EPI == MRL_EPI_FVP) {
+      const f32x16 dzt = jvp_tile(lds, ldt, d, xl, lane, f);
+      head_gather(dzt, lane, dz);
+    }
+    if (!valid || h != 0) continue;
+
+    if (EPI == MRL_EPI_PROB) {
+      if (a.head == MRL_HEAD_LINEAR) {
+        a.out[row] = z[0];
+      } else if (a.head == MRL_HEAD_SOFTMAX) {
+        float m = z[0];
+        for (int j = 1; j < A; ++j) m = fmaxf(m, z[j]);
+        float e[MAX_OUT], s = 0.f;
+        for (int j = 0; j < A; ++j) { e[j] = expf(z[j] - m); s += e[j]; }
+        for (int j = 0; j < A; ++j) a.out[row * A + j] = e[j] / s;
+      } else {
+        for (int j = 0; j < A; ++j) {
+          a.out[row * 2 * A + j] = z[j];
+          a.out[row * 2 * A + A + j] = sd[j];
+        }
+      }
+    } else if (EPI == MRL_EPI_LOSSES || EPI == MRL_EPI_SURRGRAD) {
+      const float advr = a.adv[row];
+      if (a.head == MRL_HEAD_SOFTMAX) {
+        // Categorical: loglik core.py:349-353, kl 355-356, entropy 358-359
+        float m = z[0];
+        for (int j = 1; j < A; ++j) m = fmaxf(m, z[j]);
+        float p[MAX_OUT], s = 0.f;
+        for (int j = 0; j < A; ++j) { p[j] = expf(z[j] - m); s += p[j]; }
+        for (int j = 0; j < A; ++j) p[j] = p[j] / s;
+        const int act = reinterpret_cast<const int32_t*>(a.act)[row];
+        const float* op = a.oldprob + row * A;
+        float pa = 0.f, opa = 0.f, kl = 0.f, ent = 0.f;
+        for (int j = 0; j < A; ++j) {
+          if (j == act) { pa = p[j]; opa = op[j]; }
+          kl += op[j] * logf(op[j] / p[j]);
+          ent -= p[j] * logf(p[j]);
+        }
+        const float ratio = expf(logf(pa) - logf(opa));
+        acc0 += (double)(ratio * advr);
+        acc1 += (double)kl;
+        acc2 += (double)ent;
+        if (EPI == MRL_EPI_SURRGRAD) {
+          const float w = (float)(-a.inv_ng) * ratio * advr;
+          for (int j = 0; j < A; ++j) a.ghead[row * a.gh + j] = w * ((j == act ? 1.f : 0.f) - p[j]);
+        }
+      } else {
+        // DiagGauss: loglik core.py:412-416, kl 421-426, entropy 428-430
+        const float* ac = reinterpret_cast<const float*>(a.act) + row * A;
+        const float* op = a.oldprob + row * 2 * A;
+        float q = 0.f, q0 = 0.f, sls = 0.f, sls0 = 0.f, kl = 0.f, u[MAX_OUT];
+        for (int j = 0; j < A; ++j) {
+          const float m0 = op[j], s0 = op[A + j];
+          u[j] = (ac[j] - z[j]) / sd[j];
+          const float u0 = (ac[j] - m0) / s0;
+          q += u[j] * u[j];
+          q0 += u0 * u0;
+          sls += ls[j];
+          sls0 += logf(s0);
+          const float dm = m0 - z[j];
+          kl += logf(sd[j] / s0) + (s0 * s0 + dm * dm) / (2.f * sd[j] * sd[j]);
+        }
+        kl -= 0.5f * A;
+        const float logp = -0.5f * q - 0.5f * LOG2PI_F * A - sls;
+        const float oldlogp = -0.5f * q0 - 0.5f * LOG2PI_F * A - sls0;
+        const float ratio = expf(logp - oldlogp);
+        acc0 += (double)(ratio * advr);
+        acc1 += (double)kl;
+        acc2 += (double)(sls + 0.5f * LOG2PIE_F * A);
+        if (EPI == MRL_EPI_SURRGRAD) {
+          const float w = (float)(-a.inv_ng) * ratio * advr;
+          for (int j = 0; j < A; ++j) {
+            a.ghead[row * a.gh + j] = w * u[j] / sd[j];
+            a.ghead[row * a.gh + A + j] = w * (u[j] * u[j] - 1.f);
+          }
+        }
+      }
+    } else if (EPI == MRL_EPI_VFLOSS) {
+      const float err = z[0] - a.target[row];
+      acc0 += (double)err * (double)err;
+      a.ghead[row] = (float)(2.0 * a.inv_ng) * err;
+    } else if (EPI == MRL_EPI_FVP) {
+      const float s = (float)a.inv_ng;
+      if (a.head == MRL_HEAD_SOFTMAX) {
+        float m = z[0];
+        for (int j = 1; j < A; ++j) m = fmaxf(m, z[j]);
+        float p[MAX_OUT], se = 0.f, pd = 0.f;
+        for (int j = 0; j < A; ++j) { p[j] = expf(z[j] - m); se += p[j]; }
+        for (int j = 0; j < A; ++j) { p[j] = p[j] / se; pd += p[j] * dz[j]; }
+        for (int j = 0; j < A; ++j) a.ghead[row * a.gh + j] = p[j] * (dz[j] - pd) * s;
+      } else if (a.head == MRL_HEAD_GAUSS) {
+        for (int j = 0; j < A; ++j) {
+          a.ghead[row * a.gh + j] = dz[j] / (sd[j] * sd[j]) * s;
+          a.ghead[row * a.gh + A + j] = 2.f * dls[j] * s;
+        }
+      } else {
+        a.ghead[row * a.gh] = dz[0] * s;
+      }
+    }
+  }
+  if (a.partial != nullptr) {
+    acc0 = wave_sum(acc0);
+    acc1 = wave_sum(acc1);
+    acc2 = wave_sum(acc2);
+    if (lane == 0) {
+      double* p = a.partial + ((int64_t)blockIdx.x * 4 + wave) * 4;
+      p[0] = acc0;
+      p[1] = acc1;
+      p[2] = acc2;
+      p[3] = 0.0;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ VJP
+struct VjpArgs {
+  MlpDims d;
+  int n_obs, gh, n_sum;
+  const float* x;
+  const int32_t* ept;
+  double ts_limit;
+  int64_t n;
+  const float* ghead;
+  float* slab;
+};
+
+// write a transposed tile (two 32x32 C tiles of 64 units) as img[unit][h'][s'],
+// row j = 2 s' + h', per-unit stride IMG_PAD (conflict-free b32 writes, b128 reads)
+__device__ inline void write_img(float* img, const f32x16* t, int lane) {
+  const int j = lane & 31, h = lane >> 5;
+  const int base = (j & 1) * 16 + (j >> 1);
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) img[(32 * mt + cperm(r, h)) * IMG_PAD + base] = t[mt][r];
+}
+
+__device__ inline float rowsum32(const float* img, int unit) {
+  const float* p = img + unit * IMG_PAD;
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 v = ld4(p + 4 * q);
+    s += (v.x + v.y) + (v.z + v.w);
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __restrict__ img,
+                                                       const int32_t* __restrict__ skip) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (skip != nullptr && *skip != 0) return;
+  const MlpDims& d = a.d;
+  for (int i = threadIdx.x; i < d.total_size / 4; i += 256)
+    reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img)[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
+  float* scrA = lds + d.total_size + wave * SCR_FLOATS;
+  float* scrB = scrA + 64 * IMG_PAD;
+  const int A = d.A;
+
+  f32x16 gW1[2][2], gW2[2], gW0[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    gW2[m] = zero16();
+    gW0[m] = zero16();
+#pragma unroll
+    for (int n = 0; n < 2; ++n) gW1[m][n] = zero16();
+  }
+  float gb0 = 0.f, gb1 = 0.f, gb2 = 0.f;
+  float gls[MAX_OUT];
+#pragma unroll
+  for (int q = 0; q < MAX_OUT; ++q) gls[q] = 0.f;
+
+  const int64_t ntiles = (a.n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t row0 = tile * 32;
+    const int64_t row = row0 + j;
+    const bool valid = row < a.n;
+    XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
+    Fwd f;
+    forward_tile<false>(lds, d, xl, lane, f);
+
+    // head gradient rows in C layout: register r of half h = out r + 4h
+    f32x16 G = zero16();
+    if (valid) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = r + 4 * h;
+        if (o < A) G[r] = a.ghead[row * a.gh + o];
+      }
+      if (h == 0)
+        for (int q = 0; q < a.n_sum; ++q) gls[q] += a.ghead[row * a.gh + A + q];
+    }
+    // gh2 = W2 . G   (K = outs, 4 k-steps)
+    f32x16 g2[2];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      g2[mi] = zero16();
+      const float4 w = frag4(lds, d.ba2, 4, mi, 0, lane);
+      g2[mi] = MFMA32(w.x, G[0], g2[mi]);
+      g2[mi] = MFMA32(w.y, G[1], g2[mi]);
+      g2[mi] = MFMA32(w.z, G[2], g2[mi]);
+      g2[mi] = MFMA32(w.w, G[3], g2[mi]);
+    }
+    // gW2 += H2^T G  (row index as K through LDS)
+    write_img(scrA, f.h2, lane);
+    {
+      const int base = (j & 1) * 16 + (j >> 1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) scrB[(r + 4 * h) * IMG_PAD + base] = G[r];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const float4 bq = ld4(scrB + j * IMG_PAD + h * 16 + 4 * s4);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const float4 aq = ld4(scrA + (32 * mi + j) * IMG_PAD + h * 16 + 4 * s4);
+        gW2[mi] = MFMA32(aq.x, bq.x, gW2[mi]);
+        gW2[mi] = MFMA32(aq.y, bq.y, gW2[mi]);
+        gW2[mi] = MFMA32(aq.z, bq.z, gW2[mi]);
+        gW2[mi] = MFMA32(aq.w, bq.w, gW2[mi]);
+      }
+    }
+    if (lane < A) gb2 += rowsum32(scrB, lane);
+    // ga2 = gh2 * (1 - h2^2)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) g2[m][r] *= (1.f - f.h2[m][r] * f.h2[m][r]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    write_img(scrA, f.h1, lane);
+    write_img(scrB, g2, lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // gW1 += H1^T GA2
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const float4 a0 = ld4(scrA + j * IMG_PAD + h * 16 + 4 * s4);
+      const float4 a1 = ld4(scrA + (32 + j) * IMG_PAD + h * 16 + 4 * s4);
+      const float4 b0 = ld4(scrB + j * IMG_PAD + h * 16 + 4 * s4);
+      const float4 b1 = ld4(scrB + (32 + j) * IMG_PAD + h * 16 + 4 * s4);
+      gW1[0][0] = MFMA32(a0.x, b0.x, gW1[0][0]);
+      gW1[0][1] = MFMA32(a0.x, b1.x, gW1[0][1]);
+      gW1[1][0] = MFMA32(a1.x, b0.x, gW1[1][0]);
+      gW1[1][1] = MFMA32(a1.x, b1.x, gW1[1][1]);
+      gW1[0][0] = MFMA32(a0.y, b0.y, gW1[0][0]);
+      gW1[0][1] = MFMA32(a0.y, b1.y, gW1[0][1]);
+      gW1[1][0] = MFMA32(a1.y, b0.y, gW1[1][0]);
+      gW1[1][1] = MFMA32(a1.y, b1.y, gW1[1][1]);
+      gW1[0][0] = MFMA32(a0.z, b0.z, gW1[0][0]);
+      gW1[0][1] = MFMA32(a0.z, b1.z, gW1[0][1]);
+      gW1[1][0] = MFMA32(a1.z, b0.z, gW1[1][0]);
+      gW1[1][1] = MFMA32(a1.z, b1.z, gW1[1][1]);
+      gW1[0][0] = MFMA32(a0.w, b0.w, gW1[0][0]);
+      gW1[0][1] = MFMA32(a0.w, b1.w, gW1[0][1]);
+      gW1[1][0] = MFMA32(a1.w, b0.w, gW1[1][0]);
+      gW1[1][1] = MFMA32(a1.w, b1.w, gW1[1][1]);
+    }
+    gb1 += rowsum32(scrB, lane);
+    // gh1 = W1 . ga2 ; ga1 = gh1 * (1 - h1^2)
+    f32x16 g1[2];
+    g1[0] = zero16();
+    g1[1] = zero16();
+    chain<2>(lds, d.ba1, g2, lane, g1);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) g1[m][r] *= (1.f - f.h1[m][r] * f.h1[m][r]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    write_img(scrB, g1, lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // gW0 += X^T GA1 : A[i = input j][k = row 2s+h] straight from global x
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const float4 b0 = ld4(scrB + j * IMG_PAD + h * 16 + 4 * s4);
+      const float4 b1 = ld4(scrB + (32 + j) * IMG_PAD + h * 16 + 4 * s4);
+      float av[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int s = 4 * s4 + q;
+        const int64_t xr = row0 + 2 * s + h;
+        XGlobal xq{a.x, a.ept, a.ts_limit, a.n_obs, xr, xr < a.n};
+        av[q] = (j < d.O) ? xq(j) : 0.f;
+      }
+      gW0[0] = MFMA32(av[0], b0.x, gW0[0]);
+      gW0[1] = MFMA32(av[0], b1.x, gW0[1]);
+      gW0[0] = MFMA32(av[1], b0.y, gW0[0]);
+      gW0[1] = MFMA32(av[1], b1.y, gW0[1]);
+      gW0[0] = MFMA32(av[2], b0.z, gW0[0]);
+      gW0[1] = MFMA32(av[2], b1.z, gW0[1]);
+      gW0[0] = MFMA32(av[3], b0.w, gW0[0]);
+      gW0[1] = MFMA32(av[3], b1.w, gW0[1]);
+    }
+    gb0 += rowsum32(scrB, lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+
+  // per-wave partial gradient in flat theta layout
+  float* out = a.slab + ((int64_t)blockIdx.x * 4 + wave) * d.P;
+#pragma unroll
+  for (int mj = 0; mj < 2; ++mj)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = cperm(r, h);
+      if (i < d.O) out[d.tW0 + i * HID + 32 * mj + j] = gW0[mj][r];
+    }
+  out[d.tb0 + lane] = gb0;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int mj = 0; mj < 2; ++mj)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[d.tW1 + (32 * mi + cperm(r, h)) * HID + 32 * mj + j] = gW1[mi][mj][r];
+  out[d.tb1 + lane] = gb1;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (j < A) out[d.tW2 + (32 * mi + cperm(r, h)) * A + j] = gW2[mi][r];
+  if (lane < A) out[d.tb2 + lane] = gb2;
+  for (int q = 0; q < a.n_sum; ++q) {
+    const float s = wave_sumf(gls[q]);
+    if (lane == 0) out[d.tls + q] = s;
+  }
+}
+
+// ------------------------------------------------------------------ pack / reduce
+__global__ void mlp_pack_kernel(MlpDims d, const float* __restrict__ th, float* __restrict__ image, int count,
+                                const int32_t* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) image[i] = image_value(d, th, i);
+}
+
+template <class T, class O>
+__global__ void reduce_rows_kernel(const T* __restrict__ slab, int64_t rows, int64_t cols, O* __restrict__ out,
+                                   const int32_t* __restrict__ skip) {
+  __shared__ double part[4][64];
+  if (skip != nullptr && *skip != 0) return;
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + c;
+  double s = 0.0;
+  if (col < cols)
+    for (int64_t r = g; r < rows; r += 4) s += (double)slab[r * cols + col];
+  part[g][c] = s;
+  __syncthreads();
+  if (g == 0 && col < cols) out[col] = (O)(((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]);
+}
+
+}  // namespace mrl
+
+using namespace mrl;
+
+static int check_desc(const mrl_mlp_desc* d) {
+  if (d == nullptr) return fail(E_ARG, "null mlp desc");
+  if (d->n_hidden != HID || d->n_layers != 2)
+    return fail(E_UNSUPPORTED, "only hid_sizes=[64,64] is implemented on the HIP path (got " +
+                                   std::to_string(d->n_layers) + "x" + std::to_string(d->n_hidden) + ")");
+  if (d->n_in < 1 || d->n_in > MAX_IN) return fail(E_UNSUPPORTED, "n_in must be in [1, 32]");
+  if (d->n_out < 1 || d->n_out > MAX_OUT) return fail(E_UNSUPPORTED, "n_out must be in [1, 8]");
+  if (d->head < 0 || d->head > 2) return fail(E_ARG, "bad head kind");
+  if (d->head == MRL_HEAD_LINEAR && d->n_out != 1) return fail(E_ARG, "linear head needs n_out=1");
+  return OK;
+}
+
+static MlpDims dims_of(const mrl_mlp_desc* d) { return mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS); }
+
+static int64_t rows_blocks(int64_t n) {
+  int64_t b = ceil_div(ceil_div(n, 32), 4);
+  if (b < 1) b = 1;
+  return b > ROWS_MAX_BLOCKS ? ROWS_MAX_BLOCKS : b;
+}
+static int64_t vjp_blocks(int64_t n) {
+  int64_t b = ceil_div(ceil_div(n, 32), 4);
+  if (b < 1) b = 1;
+  return b > VJP_MAX_BLOCKS ? VJP_MAX_BLOCKS : b;
+}
+
+extern "C" {
+
+const char* mrl_last_error(void) { return mrl::g_err.c_str(); }
+int32_t mrl_version(void) { return 1; }
+
+int64_t mrl_mlp_num_params(const mrl_mlp_desc* d) {
+  if (check_desc(d) != OK) return -1;
+  return dims_of(d).P;
+}
+int64_t mrl_mlp_image_floats(const mrl_mlp_desc* d) {
+  if (check_desc(d) != OK) return -1;
+  return dims_of(d).total_size;
+}
+int64_t mrl_partial_rows(int64_t n) { return rows_blocks(n) * 4; }
+int64_t mrl_slab_rows(int64_t n) { return vjp_blocks(n) * 4; }
+
+int mrl_mlp_pack(const mrl_mlp_desc* d, const float* theta, float* image, int32_t fwd_only, const int32_t* skip,
+                 void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (!theta || !image) return fail(E_ARG, "null pointer");
+  MlpDims m = dims_of(d);
+  int count = fwd_only ? m.fwd_size : m.total_size;
+  hipLaunchKernelGGL(mlp_pack_kernel, dim3((count + 255) / 256), dim3(256), 0, (hipStream_t)stream, m, theta, image,
+                     count, skip);
+  return hip_check(hipGetLastError(), "mrl_mlp_pack");
+}
+
+int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const float* image, const float* tangent,
+                 const float* image_t, const mrl_rows_io* io, const int32_t* skip, void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (!io || !image || !io->x) return fail(E_ARG, "null pointer");
+  if (io->n <= 0) return OK;
+  RowsArgs a;
+  a.d = dims_of(d);
+  a.head = d->head;
+  a.n_obs = d->n_in - (io->ep_t ? 1 : 0);
+  a.gh = d->head == MRL_HEAD_GAUSS ? 2 * d->n_out : d->n_out;
+  a.x = io->x;
+  a.ept = io->ep_t;
+  a.ts_limit = io->timestep_limit;
+  a.n = io->n;
+  a.inv_ng = io->inv_n_global;
+  a.act = io->act;
+  a.adv = io->adv;
+  a.oldprob = io->oldprob;
+  a.target = io->target;
+  a.out = io->out;
+  a.ghead = io->ghead;
+  a.partial = io->partial;
+  a.logstd = (d->head == MRL_HEAD_GAUSS && theta) ? theta + a.d.tls : nullptr;
+  a.dlogstd = (d->head == MRL_HEAD_GAUSS && tangent) ? tangent + a.d.tls : nullptr;
+  switch (epi) {
+    case MRL_EPI_PROB:
+      if (!io->out) return fail(E_ARG, "EPI_PROB needs out");
+      if (d->head == MRL_HEAD_GAUSS && !theta) return fail(E_ARG, "DiagGauss needs theta (logstd)");
+      break;
+    case MRL_EPI_LOSSES:
+    case MRL_EPI_SURRGRAD:
+      if (d->head == MRL_HEAD_LINEAR) return fail(E_ARG, "policy epilogue on a value net");
+      if (!io->act || !io->adv || !io->oldprob || !io->partial) return fail(E_ARG, "losses need act/adv/oldprob/partial");
+      if (epi == MRL_EPI_SURRGRAD && !io->ghead) return fail(E_ARG, "SURRGRAD needs ghead");
+      if (d->head == MRL_HEAD_GAUSS && !theta) return fail(E_ARG, "DiagGauss needs theta (logstd)");
+      break;
+    case MRL_EPI_VFLOSS:
+      if (d->head != MRL_HEAD_LINEAR || !io->target || !io->ghead || !io->partial)
+        return fail(E_ARG, "VFLOSS needs a linear head, target, ghead, partial");
+      break;
+    case MRL_EPI_FVP:
+      if (!tangent || !image_t || !io->ghead) return fail(E_ARG, "FVP needs tangent, image_t, ghead");
+      if (d->head == MRL_HEAD_GAUSS && !theta) return fail(E_ARG, "DiagGauss needs theta (logstd)");
+      break;
+    default:
+      return fail(E_ARG, "unknown epilogue");
+  }
+  const int64_t blocks = rows_blocks(io->n);
+  size_t shm = (size_t)a.d.fwd_size * 4 * (epi == MRL_EPI_FVP ? 2 : 1);
+  hipStream_t s = (hipStream_t)stream;
+  switch (epi) {
+    case MRL_EPI_PROB:
+      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_PROB>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t, skip);
+      break;
+    case MRL_EPI_LOSSES:
+      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_LOSSES>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t, skip);
+      break;
+    case MRL_EPI_SURRGRAD:
+      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_SURRGRAD>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t,
+                         skip);
+      break;
+    case MRL_EPI_VFLOSS:
+      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_VFLOSS>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t, skip);
+      break;
+    case MRL_EPI_FVP:
+      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_FVP>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t, skip);
+      break;
+  }
+  return hip_check(hipGetLastError(), "mrl_mlp_rows");
+}
+
+int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const int32_t* ep_t, double ts_limit,
+                const float* ghead, int64_t n, float* slab, const int32_t* skip, void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (!image || !x || !ghead || !slab) return fail(E_ARG, "null pointer");
+  if (n <= 0) return OK;
+  VjpArgs a;
+  a.d = dims_of(d);
+  a.n_obs = d->n_in - (ep_t ? 1 : 0);
+  a.n_sum = d->head == MRL_HEAD_GAUSS ? d->n_out : 0;
+  a.gh = d->n_out + a.n_sum;
+  a.x = x;
+  a.ept = ep_t;
+  a.ts_limit = ts_limit;
+  a.n = n;
+  a.ghead = ghead;
+  a.slab = slab;
+  const int64_t blocks = vjp_blocks(n);
+  size_t shm = ((size_t)a.d.total_size + 4 * (size_t)SCR_FLOATS) * 4;
+  hipLaunchKernelGGL(mlp_vjp_kernel, dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image, skip);
+  return hip_check(hipGetLastError(), "mrl_mlp_vjp");
+}
+
+int mrl_reduce_rows_f32(const float* slab, int64_t rows, int64_t cols, float* out, const int32_t* skip, void* stream) {
+  if (!slab || !out) return fail(E_ARG, "null pointer");
+  if (cols <= 0) return OK;
+  hipLaunchKernelGGL((reduce_rows_kernel<float, float>), dim3(ceil_div(cols, 64)), dim3(256), 0, (hipStream_t)stream,
+                     slab, rows, cols, out, skip);
+  return hip_check(hipGetLastError(), "mrl_reduce_rows_f32");
+}
+int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* out, const int32_t* skip,
+                        void* stream) {
+  if (!slab || !out) return fail(E_ARG, "null pointer");
+  if (cols <= 0) return OK;
+  hipLaunchKernelGGL((reduce_rows_kernel<double, double>), dim3(ceil_div(cols, 64)), dim3(256), 0, (hipStream_t)stream,
+                     slab, rows, cols, out, skip);
+  return hip_check(hipGetLastError(), "mrl_reduce_rows_f64");
+}
+
+}  // extern "C"

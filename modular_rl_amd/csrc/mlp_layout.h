@@ -1,0 +1,124 @@
+// Packed LDS "image" of a tanh MLP with two 64-wide hidden layers, laid out as
+// per-lane MFMA A-operand fragments (v_mfma_f32_32x32x2_f32) so that a kernel
+// copies it linearly into LDS and reads every weight fragment with one
+// conflict-free ds_read_b128 per 4 k-steps.
+//
+// Reference net: Keras Dense(64,tanh) x2 + Dense(out) (`agentzoo.py:34-48,55-58`).
+// Flat theta order (`core.py:518-557`): W0 (in,64) row-major, b0, W1 (64,64),
+// b1, W2 (64,A), b2, [logstd (A) for DiagGauss].
+//
+// Activations are kept TRANSPOSED in MFMA accumulators: a 32-row tile of a
+// 64-unit layer is two 32x32 C tiles D[unit][row] (row on the lane, units in the
+// 16 registers: unit = 32*mt + cperm(r, lane>>5)).  Such a tile is directly the
+// B operand of the next layer (k-step s takes register s&15 of tile s>>4, lane
+// half h supplying unit 32*(s>>4) + cperm(s&15, h)), so layers chain with no data
+// movement; the weight fragments below are permuted to match.
+#pragma once
+#include "mrl_common.h"
+
+namespace mrl {
+
+constexpr int HID = 64;       // hidden width (fast path)
+constexpr int MAX_IN = 32;    // input features (obs [+ time feature])
+constexpr int MAX_OUT = 8;    // head outputs backpropagated
+constexpr int IMG_PAD = 36;   // per-unit stride of LDS transpose scratch (floats)
+
+struct MlpDims {
+  int O, A;        // inputs, head outputs
+  int KS0p;        // input-layer k-steps (ceil(O/2)) rounded up to a multiple of 4
+  int fa0, fa1, fa2, fb0, fb1, fb2, ba1, ba2;  // segment offsets (floats)
+  int fwd_size, total_size;
+  // flat theta offsets
+  int tW0, tb0, tW1, tb1, tW2, tb2, tls, P;
+};
+
+__host__ __device__ inline MlpDims mlp_dims(int O, int A, int gauss) {
+  MlpDims d;
+  d.O = O;
+  d.A = A;
+  int ks0 = (O + 1) / 2;
+  d.KS0p = (ks0 + 3) & ~3;
+  int o = 0;
+  d.fa0 = o; o += 2 * d.KS0p * 64;
+  d.fa1 = o; o += 2 * 32 * 64;
+  d.fa2 = o; o += 1 * 32 * 64;
+  d.fb0 = o; o += 2 * 2 * 16;
+  d.fb1 = o; o += 2 * 2 * 16;
+  d.fb2 = o; o += 1 * 2 * 16;
+  d.fwd_size = o;
+  d.ba1 = o; o += 2 * 32 * 64;
+  d.ba2 = o; o += 2 * 4 * 64;
+  d.total_size = o;
+  d.tW0 = 0;
+  d.tb0 = d.tW0 + O * HID;
+  d.tW1 = d.tb0 + HID;
+  d.tb1 = d.tW1 + HID * HID;
+  d.tW2 = d.tb1 + HID;
+  d.tb2 = d.tW2 + HID * A;
+  d.tls = d.tb2 + A;
+  d.P = d.tls + (gauss ? A : 0);
+  return d;
+}
+
+// fragment slot (mo, s) of a segment with KSp k-steps -> float offset of lane 0
+__host__ __device__ inline int frag_off(int mo, int s, int KSp, int lane) {
+  return ((mo * (KSp / 4) + (s >> 2)) * 64 + lane) * 4 + (s & 3);
+}
+
+// k index (input unit) fed by lane half h at k-step s of a chained (64-unit) layer
+__host__ __device__ inline int chain_k(int s, int h) { return 32 * (s >> 4) + cperm(s & 15, h); }
+
+// value of image element `idx` given flat theta (nullptr => zeros)
+__host__ __device__ inline float image_value(const MlpDims& d, const float* th, int idx) {
+  auto dec = [&](int seg, int KSp, int& mo, int& s, int& lane) {
+    int rel = idx - seg;
+    int q = rel & 3;
+    int l = (rel >> 2) & 63;
+    int blk = rel >> 8;  // mo * (KSp/4) + s4
+    mo = blk / (KSp / 4);
+    s = (blk % (KSp / 4)) * 4 + q;
+    lane = l;
+  };
+  int mo, s, lane;
+  if (idx < d.fa1) {                      // FA0: A[i=out][k=in] = W0[in][out]
+    dec(d.fa0, d.KS0p, mo, s, lane);
+    int k = 2 * s + (lane >> 5);
+    int j = 32 * mo + (lane & 31);
+    return k < d.O ? th[d.tW0 + k * HID + j] : 0.f;
+  } else if (idx < d.fa2) {               // FA1
+    dec(d.fa1, 32, mo, s, lane);
+    int k = chain_k(s, lane >> 5);
+    int j = 32 * mo + (lane & 31);
+    return th[d.tW1 + k * HID + j];
+  } else if (idx < d.fb0) {               // FA2 (head)
+    dec(d.fa2, 32, mo, s, lane);
+    int k = chain_k(s, lane >> 5);
+    int j = lane & 31;
+    return j < d.A ? th[d.tW2 + k * d.A + j] : 0.f;
+  } else if (idx < d.fb1) {               // FB0 [mo][h][r]
+    int rel = idx - d.fb0;
+    int r = rel & 15, h = (rel >> 4) & 1, m = rel >> 5;
+    return th[d.tb0 + 32 * m + cperm(r, h)];
+  } else if (idx < d.fb2) {
+    int rel = idx - d.fb1;
+    int r = rel & 15, h = (rel >> 4) & 1, m = rel >> 5;
+    return th[d.tb1 + 32 * m + cperm(r, h)];
+  } else if (idx < d.fwd_size) {
+    int rel = idx - d.fb2;
+    int r = rel & 15, h = (rel >> 4) & 1;
+    int u = cperm(r, h);
+    return u < d.A ? th[d.tb2 + u] : 0.f;
+  } else if (idx < d.ba2) {               // BA1: A[i=in][k=out] = W1[in][out]
+    dec(d.ba1, 32, mo, s, lane);
+    int i = 32 * mo + (lane & 31);
+    int k = chain_k(s, lane >> 5);
+    return th[d.tW1 + i * HID + k];
+  } else {                                // BA2: A[i=in][k=out] = W2[in][out], out = s + 4h
+    dec(d.ba2, 4, mo, s, lane);
+    int i = 32 * mo + (lane & 31);
+    int o = s + 4 * (lane >> 5);
+    return o < d.A ? th[d.tW2 + i * d.A + o] : 0.f;
+  }
+}
+
+}  // namespace mrl

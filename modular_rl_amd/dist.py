@@ -1,0 +1,63 @@
+"""Data-parallel communication: one process per GPU, torch.distributed over RCCL.
+
+The reference has no distributed path (`parallel` raises NotImplementedError,
+core.py:123-124,175-176).  Here every rank owns E envs, its own trajectories and
+activation work; theta is replicated and the ranks take identical steps because
+every reduction the update consumes is summed over ranks first:
+  * the flat policy gradient g and every conjugate-gradient Fvp (sum, then the
+    kernels' 1/N_global scaling makes them global means),
+  * loss sums (surr / KL / entropy) of the before/after/line-search passes,
+  * advantage moments (sum, sum of squares, count) for the global standardisation,
+  * VF loss and gradient of every L-BFGS evaluation,
+  * the ZFilter running-stat deltas once per iteration (Chan merge, rank order).
+``backend="nccl"`` is RCCL on ROCm; ``gloo`` is used by the CPU tests.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self, group=None):
+        self.group = group
+        self.enabled = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.rank = dist.get_rank(group) if self.enabled else 0
+        self.world = dist.get_world_size(group) if self.enabled else 1
+
+    def allreduce_(self, t):
+        """In-place sum over ranks (no-op on one rank)."""
+        if self.enabled:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def allreduce_int(self, v):
+        if not self.enabled:
+            return int(v)
+        dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
+        t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, group=self.group)
+        return int(t.item())
+
+    def allgather(self, t):
+        if not self.enabled:
+            return [t]
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return out
+
+    def barrier(self):
+        if self.enabled:
+            dist.barrier(group=self.group)
+
+
+def init_from_env(backend=None):
+    """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torchrun) if present."""
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or dist.is_initialized():
+        return Comm()
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dist.init_process_group(backend=backend)
+    return Comm()
