@@ -131,6 +131,16 @@ int64_t mrl_gae_workspace_bytes(int64_t T, int64_t E);
 int mrl_standardize(float* adv, int64_t n, const double* moments, void* stream);
 /* y = mixfrac * ret + (1 - mixfrac) * vpred  (NnRegression.fit target, core.py:622-624) */
 int mrl_vf_target(const float* ret, const float* vpred, double mixfrac, int64_t n, float* y, void* stream);
+/* out (fp64 [3]) <- (sum (a-b), sum (a-b)^2, n); b may be NULL.  For the VF stats
+ * (PredStdev / TargStdev / explained variance, core.py:629-636, misc_utils.py:29-49) */
+int mrl_moments(const float* a, const float* b, int64_t n, double* out, void* workspace, void* stream);
+int64_t mrl_moments_workspace_bytes(int64_t n);
+/* episode statistics of the batch (add_episode_stats, core.py:31-44): out (fp64 [6]) <-
+ * (n_episodes, sum R, sum R^2, max R, sum len, max len); an episode = a row run ending
+ * at a flags&1 row (whole episode, or a horizon-cut one, like a reference path). */
+int mrl_episode_stats(const float* rew, const uint8_t* flags, int64_t T, int64_t E, double* out, void* workspace,
+                      void* stream);
+int64_t mrl_episode_stats_workspace_bytes(int64_t E);
 
 /* ---------------------------------------------------------------- batched rollout
  * Replaces do_rollouts_serial/rollout (core.py:174-221) + ZFilter (filters.py:17-40)

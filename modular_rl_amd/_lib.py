@@ -68,6 +68,10 @@ SIGNATURES = {
     "mrl_gae_workspace_bytes": (i64, [i64, i64]),
     "mrl_standardize": (i32, [vp, i64, vp, vp]),
     "mrl_vf_target": (i32, [vp, vp, f64, i64, vp, vp]),
+    "mrl_moments": (i32, [vp, vp, i64, vp, vp, vp]),
+    "mrl_moments_workspace_bytes": (i64, [i64]),
+    "mrl_episode_stats": (i32, [vp, vp, i64, i64, vp, vp, vp]),
+    "mrl_episode_stats_workspace_bytes": (i64, [i64]),
     "mrl_env_state_doubles": (i64, [i32]),
     "mrl_filter_doubles": (i64, [i32]),
     "mrl_record_doubles": (i64, [i32]),

@@ -1,0 +1,223 @@
+"""Lock-step batched rollout collector (replaces get_paths / do_rollouts_serial /
+rollout, `core.py:174-221`).
+
+E envs per rank advance together for ``horizon`` steps per iteration; each step is
+ONE fused HIP launch (filter merge -> normalise -> policy MLP on MFMA -> sample ->
+env step -> Welford partials).  The T launches (plus reset/finish) can be captured
+once into a hipGraph and replayed every iteration (``use_graph``): the policy
+weights are read through the persistent ``net.image`` buffer and the RNG step base
+from a device iteration counter, so replays need no re-capture.
+
+Semantics vs the reference: every env is reset at the start of
+an iteration (core.py:186); observations are stored filtered, rewards raw; an
+episode ends at env ``done`` (gym TimeLimit included => terminated, bootstrap 0) or
+at the ``timestep_limit`` / horizon cut (not terminated, bootstrap b[-1]).  The
+ZFilter pushes all E observations of a step as one Chan merge (E = 1 reduces
+exactly to RunningStat.push); across ranks the running stats are merged once per
+iteration (rank order), so ranks normalise with identical statistics at every
+iteration start.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream
+from .dist import Comm
+
+
+class Batch:
+    """Device-resident batch of N = T*E time-major rows (row n = t*E + e)."""
+
+    def __init__(self, n, obs, act, prob, rew=None, flags=None, ep_t=None, T=None, E=None):
+        self.n = int(n)
+        self.obs, self.act, self.prob, self.rew, self.flags, self.ep_t = obs, act, prob, rew, flags, ep_t
+        self.T, self.E = T, E
+        self.adv = self.ret = self.vpred = None
+        self.episode = None
+
+    @staticmethod
+    def from_paths(paths, stochpol, device, need_policy=True):
+        """Concatenate per-path dicts (core.py:205-207 schema) into a device batch
+        (one env, paths laid end to end: T = total rows, E = 1)."""
+        cat = np.concatenate
+        dev = torch.device(device)
+        obs = torch.as_tensor(cat([np.asarray(p["observation"], dtype=np.float32) for p in paths])).to(dev)
+        n = obs.shape[0]
+        act = prob = None
+        if need_policy:
+            a = cat([np.asarray(p["action"]) for p in paths])
+            act = torch.as_tensor(a.astype(np.int32) if stochpol.discrete else a.astype(np.float32)).to(dev)
+            prob = torch.as_tensor(cat([np.asarray(p["prob"], dtype=np.float32) for p in paths])).to(dev)
+        ep_t = torch.as_tensor(cat([np.arange(len(p["observation"]), dtype=np.int32) for p in paths])).to(dev)
+        flags = np.zeros(n, dtype=np.uint8)
+        ends = np.cumsum([len(p["observation"]) for p in paths]) - 1
+        for e_, p in zip(ends, paths):
+            flags[e_] = 1 | (2 if p.get("terminated", False) else 0)
+        rew = None
+        if "reward" in paths[0]:
+            rew = torch.as_tensor(cat([np.asarray(p["reward"], dtype=np.float32) for p in paths])).to(dev)
+        b = Batch(n, obs, act, prob, rew, torch.as_tensor(flags).to(dev), ep_t, T=n, E=1)
+        if "advantage" in paths[0]:
+            b.adv = torch.as_tensor(cat([np.asarray(p["advantage"], dtype=np.float32) for p in paths])).to(dev)
+        return b
+
+    def to_paths(self):
+        """Split back into reference-style path dicts (host numpy), env by env."""
+        T, E = self.T, self.E
+        obs = self.obs.view(T, E, -1).cpu().numpy()
+        act = self.act.view(T, E, *self.act.shape[1:]).cpu().numpy()
+        prob = self.prob.view(T, E, -1).cpu().numpy()
+        rew = self.rew.view(T, E).cpu().numpy().astype(np.float64)
+        flags = self.flags.view(T, E).cpu().numpy()
+        paths = []
+        for e in range(E):
+            start = 0
+            for t in range(T):
+                if flags[t, e] & 1:
+                    sl = slice(start, t + 1)
+                    paths.append(dict(observation=obs[sl, e], action=act[sl, e], prob=prob[sl, e],
+                                      reward=rew[sl, e], terminated=bool(flags[t, e] & 2)))
+                    start = t + 1
+        return paths
+
+
+class Collector:
+    def __init__(self, env, policy, n_envs, horizon, timestep_limit, filter=1, seed=0, comm=None, device="cuda",
+                 use_graph=False):
+        lib = _lib.load(require_gpu=True)
+        self.env, self.policy = env, policy
+        self.comm = comm if comm is not None else Comm()
+        self.E, self.T = int(n_envs), int(horizon)
+        self.N = self.E * self.T
+        self.dev = torch.device(device)
+        self.desc = _lib.RolloutDesc(env.kind, self.E, self.T, int(timestep_limit), int(filter),
+                                     self.comm.rank * self.E, int(seed) & 0xFFFFFFFFFFFFFFFF)
+        ns = lib.mrl_env_state_doubles(env.kind)
+        self.FS = int(lib.mrl_filter_doubles(env.kind))
+        self.RS = int(lib.mrl_record_doubles(env.kind))
+        self.NB = int(lib.mrl_rollout_blocks(self.E))
+        f64 = dict(dtype=torch.float64, device=self.dev)
+        self.env_state = torch.zeros(ns * self.E, **f64)
+        self.env_int = torch.zeros(2 * self.E, dtype=torch.int32, device=self.dev)
+        self.filter_state = torch.zeros(2 * self.FS, **f64)
+        self.records = torch.zeros(2 * self.NB * self.RS, **f64)
+        self.iteration = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        O, A = env.obs_dim, env.act_dim
+        self.obs = torch.zeros(self.N, O, dtype=torch.float32, device=self.dev)
+        if env.discrete:
+            self.act = torch.zeros(self.N, dtype=torch.int32, device=self.dev)
+            self.prob = torch.zeros(self.N, A, dtype=torch.float32, device=self.dev)
+        else:
+            self.act = torch.zeros(self.N, A, dtype=torch.float32, device=self.dev)
+            self.prob = torch.zeros(self.N, 2 * A, dtype=torch.float32, device=self.dev)
+        self.rew = torch.zeros(self.N, dtype=torch.float32, device=self.dev)
+        self.flags = torch.zeros(self.N, dtype=torch.uint8, device=self.dev)
+        self.ep_t = torch.zeros(self.N, dtype=torch.int32, device=self.dev)
+        self.noise = None
+        self.use_graph = use_graph
+        self.graph = None
+        self._ep_ws = torch.zeros(int(lib.mrl_episode_stats_workspace_bytes(self.E)) // 8 + 1, **f64)
+        self._ep_out = torch.zeros(8, **f64)
+
+    def _bufs(self):
+        return _lib.RolloutBufs(ptr(self.env_state), ptr(self.env_int), ptr(self.filter_state), ptr(self.records),
+                                ptr(self.iteration), ptr(self.obs), ptr(self.act), ptr(self.prob), ptr(self.rew),
+                                ptr(self.flags), ptr(self.ep_t), ptr(self.noise))
+
+    def _launch_all(self):
+        bufs = self._bufs()
+        net = self.policy.net
+        call("mrl_rollout_reset", ctypes.byref(self.desc), ctypes.byref(bufs), stream())
+        for t in range(self.T):
+            call("mrl_rollout_step", ctypes.byref(self.desc), ctypes.byref(net.desc), ptr(net.theta), ptr(net.image),
+                 ctypes.byref(bufs), int(t), stream())
+        call("mrl_rollout_finish", ctypes.byref(self.desc), ctypes.byref(bufs), stream())
+
+    def set_noise(self, noise):
+        """Inject sampling noise (float64 u[N] or z[N, d]) instead of Philox (parity mode)."""
+        self.noise = None if noise is None else torch.as_tensor(noise, dtype=torch.float64).to(self.dev).contiguous()
+        self.graph = None
+
+    def collect(self):
+        fs_start = self.filter_state[:self.FS].clone() if self.comm.enabled else None
+        if self.use_graph and self.noise is None:
+            if self.graph is None:
+                # captured launches are recorded, not executed: state is untouched by the capture
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph):
+                    self._launch_all()
+            self.graph.replay()
+        else:
+            self._launch_all()
+        if self.comm.enabled:
+            self._merge_filter_across_ranks(fs_start)
+        b = Batch(self.N, self.obs, self.act, self.prob, self.rew, self.flags, self.ep_t, T=self.T, E=self.E)
+        return b
+
+    # ------------------------------------------------------------ filter state
+    def _merge_filter_across_ranks(self, fs_start):
+        """Per-iteration Chan merge of every rank's running-stat delta, in rank order."""
+        D = (self.FS - 2) // 2
+        s0 = fs_start.double().cpu().numpy()
+        s1 = self.filter_state[:self.FS].double().cpu().numpy()
+        delta = np.zeros(self.FS)
+        for which, cols in ((0, range(D - 1)), (1, [D - 1])):
+            n0, n1 = s0[which], s1[which]
+            nd = n1 - n0
+            delta[which] = nd
+            for k in cols:
+                M0, M1, S0, S1 = s0[2 + k], s1[2 + k], s0[2 + D + k], s1[2 + D + k]
+                if nd > 0:
+                    md = (n1 * M1 - n0 * M0) / nd
+                    delta[2 + k] = md
+                    delta[2 + D + k] = S1 - S0 - (md - M0) ** 2 * n0 * nd / n1
+        dev = "cuda" if self.comm.enabled and torch.distributed.get_backend() == "nccl" else "cpu"
+        all_d = self.comm.allgather(torch.as_tensor(delta).to(dev))
+        out = s0.copy()
+        for d in all_d:
+            d = d.cpu().numpy()
+            for which, cols in ((0, range(D - 1)), (1, [D - 1])):
+                nb = d[which]
+                if nb <= 0:
+                    continue
+                na = out[which]
+                n = na + nb
+                for k in cols:
+                    M, S = out[2 + k], out[2 + D + k]
+                    mb, m2b = d[2 + k], d[2 + D + k]
+                    delta_ = mb - M
+                    newM = M + (delta_ * nb) / n
+                    out[2 + D + k] = S + m2b + delta_ * (mb - newM) * nb
+                    out[2 + k] = newM
+                out[which] = n
+        self.filter_state[:self.FS].copy_(torch.as_tensor(out))
+
+    def filter_stats(self):
+        """(n, mean[obs], var[obs]), (n_rew, mean_rew, var_rew) of the running stats."""
+        s = self.filter_state[:self.FS].cpu().numpy()
+        D = (self.FS - 2) // 2
+        n, nr = s[0], s[1]
+        M, S = s[2:2 + D], s[2 + D:2 + 2 * D]
+        var_o = S[:D - 1] / (n - 1) if n > 1 else M[:D - 1] ** 2
+        var_r = S[D - 1] / (nr - 1) if nr > 1 else M[D - 1] ** 2
+        return (n, M[:D - 1].copy(), var_o), (nr, M[D - 1], var_r)
+
+    # ------------------------------------------------------------ episode stats
+    def episode_stats(self, batch):
+        """add_episode_stats scalars (core.py:31-44), reduced on device and over ranks."""
+        call("mrl_episode_stats", ptr(batch.rew), ptr(batch.flags), batch.T, batch.E, ptr(self._ep_out),
+             ptr(self._ep_ws), stream())
+        v = self._ep_out[:6].clone()
+        if self.comm.enabled:
+            mx = v[[3, 5]].clone()
+            self.comm.allreduce_(v)
+            if self.comm.world > 1:
+                torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
+                v[3], v[5] = mx[0], mx[1]
+        cnt, sr, sr2, mr, sl, ml = (float(x) for x in v.cpu().numpy())
+        mean = sr / cnt
+        return dict(NumEpBatch=int(cnt), EpRewMean=mean,
+                    EpRewSEM=float(np.sqrt(max(sr2 / cnt - mean * mean, 0.0)) / np.sqrt(cnt)),
+                    EpRewMax=mr, EpLenMean=sl / cnt, EpLenMax=ml, RewPerStep=sr / sl)

@@ -1,0 +1,248 @@
+"""Training-loop layer with the reference's names (`core.py` of ddlau/modular_rl).
+
+The loop ``run_policy_gradient_algorithm`` (`core.py:118-171`) keeps its contract
+(``callback(stats)`` once per iteration with EpRewMean / vf_* / pol_* /
+TimeElapsed keys) but each stage is device-resident:
+
+  rollouts            Collector.collect()          fused lock-step HIP rollout
+  compute_advantage   NnVf forward + mrl_gae + global standardisation
+  VF update           NnVf.fit_batch               L-BFGS with device loss/grad
+  policy update       TrpoUpdater.update           device CG / line search
+
+The per-path API (``rollout``, ``do_rollouts_serial``, ``compute_advantage(vf,
+paths, ...)``, ``agent.updater(paths)``) is kept for compatibility and runs the
+same kernels on E = 1.
+"""
+import time
+from collections import OrderedDict
+from importlib import import_module
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream
+from .collector import Batch, Collector
+from .dist import Comm
+from .misc_utils import update_default_config
+from .vf import LbfgsOptimizer, NnRegression, NnVf  # noqa: F401  (reference names live in core)
+
+concat = np.concatenate
+
+
+def get_agent_cls(name):
+    """`core.py:20-24`."""
+    p, m = name.rsplit(".", 1)
+    mod = import_module(p)
+    return getattr(mod, m)
+
+
+def add_episode_stats(stats, paths):
+    """`core.py:31-44` (per-path form)."""
+    reward_key = "reward_raw" if "reward_raw" in paths[0] else "reward"
+    episoderewards = np.array([path[reward_key].sum() for path in paths])
+    pathlengths = np.array([pathlength(path) for path in paths])
+    stats["EpisodeRewards"] = episoderewards
+    stats["EpisodeLengths"] = pathlengths
+    stats["NumEpBatch"] = len(episoderewards)
+    stats["EpRewMean"] = episoderewards.mean()
+    stats["EpRewSEM"] = episoderewards.std() / np.sqrt(len(paths))
+    stats["EpRewMax"] = episoderewards.max()
+    stats["EpLenMean"] = pathlengths.mean()
+    stats["EpLenMax"] = pathlengths.max()
+    stats["RewPerStep"] = episoderewards.sum() / pathlengths.sum()
+
+
+def add_prefixed_stats(stats, prefix, d):
+    for k, v in d.items():
+        stats[prefix + "_" + k] = v
+
+
+# ================================================================ advantage
+class _GaeWorkspace:
+    def __init__(self):
+        self.ws = None
+        self.moments = None
+
+    def get(self, T, E, device):
+        nbytes = int(_lib.load().mrl_gae_workspace_bytes(int(T), int(E)))
+        if self.ws is None or self.ws.numel() < nbytes or self.ws.device != device:
+            self.ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            self.moments = torch.zeros(3, dtype=torch.float64, device=device)
+        return self.ws, self.moments
+
+
+_GAE = _GaeWorkspace()
+
+
+def compute_advantage_batch(vf, batch, gamma, lam, comm=None):
+    """Device form of `core.py:63-105` on a time-major batch: baseline forward,
+    GAE + discounted return scan (mrl_gae), then standardisation with the global
+    (all-rank) mean / std (numpy std, ddof=0, no epsilon)."""
+    comm = comm if comm is not None else Comm()
+    dev = batch.obs.device
+    n = batch.n
+    batch.vpred = vf.predict_batch(batch, out=batch.vpred if batch.vpred is not None and batch.vpred.numel() == n
+                                   else torch.empty(n, dtype=torch.float32, device=dev))
+    if batch.adv is None or batch.adv.numel() != n:
+        batch.adv = torch.empty(n, dtype=torch.float32, device=dev)
+        batch.ret = torch.empty(n, dtype=torch.float32, device=dev)
+    ws, moments = _GAE.get(batch.T, batch.E, dev)
+    call("mrl_gae", ptr(batch.rew), ptr(batch.vpred), ptr(batch.flags), int(batch.T), int(batch.E), float(gamma),
+         float(lam), ptr(batch.adv), ptr(batch.ret), ptr(moments), ptr(ws), stream())
+    comm.allreduce_(moments)
+    call("mrl_standardize", ptr(batch.adv), int(n), ptr(moments), stream())
+    return batch
+
+
+def compute_advantage(vf, paths, gamma, lam):
+    """Per-path API of `core.py:63-105`: fills path["return"], ["baseline"],
+    ["advantage"] (standardised over all paths)."""
+    dev = vf.net.device
+    batch = Batch.from_paths(paths, None, device=dev, need_policy=False)
+    compute_advantage_batch(vf, batch, gamma, lam)
+    adv = batch.adv.cpu().numpy().astype(np.float64)
+    ret = batch.ret.cpu().numpy().astype(np.float64)
+    base = batch.vpred.cpu().numpy().astype(np.float64)
+    i = 0
+    for path in paths:
+        L = len(path["reward"])
+        path["return"], path["baseline"], path["advantage"] = ret[i:i + L], base[i:i + L], adv[i:i + L]
+        i += L
+
+
+PG_OPTIONS = [
+    ("timestep_limit", int, 0, "maximum length of trajectories"),
+    ("n_iter", int, 200, "number of batch"),
+    ("parallel", int, 0, "collect trajectories in parallel"),
+    ("timesteps_per_batch", int, 100, ""),
+    ("gamma", float, 0.99, "discount"),
+    ("lam", float, 1.0, "lambda parameter from generalized advantage estimation"),
+    # MI355X build: lock-step batched collection
+    ("n_envs", int, 1, "envs stepped in lock-step per GPU"),
+    ("horizon", int, 0, "steps per env per iteration (0: ceil(timesteps_per_batch / n_envs))"),
+    ("use_graph", int, 1, "replay the rollout's per-step launches from one captured hipGraph"),
+]
+
+
+def horizon_of(cfg):
+    h = int(cfg.get("horizon", 0) or 0)
+    if h <= 0:
+        h = -(-int(cfg["timesteps_per_batch"]) // int(cfg.get("n_envs", 1) or 1))
+    return max(h, 1)
+
+
+def run_policy_gradient_algorithm(env, agent, usercfg=None, callback=None):
+    """`core.py:118-171`: rollouts -> advantage -> VF fit -> TRPO update -> callback(stats)."""
+    cfg = update_default_config(PG_OPTIONS, usercfg)
+    cfg.update(usercfg or {})
+    if cfg["parallel"]:
+        raise NotImplementedError("parallel rollouts: launch one process per GPU with torchrun instead")
+    comm = agent.comm
+    collector = agent.make_collector(env, cfg)
+    tstart = time.time()
+    for _ in range(cfg["n_iter"]):
+        batch = collector.collect()
+        compute_advantage_batch(agent.baseline, batch, cfg["gamma"], cfg["lam"], comm)
+        vf_stats = agent.baseline.fit_batch(batch)
+        pol_stats = agent.updater.update(batch)
+        stats = OrderedDict()
+        stats.update(collector.episode_stats(batch))
+        add_prefixed_stats(stats, "vf", vf_stats)
+        add_prefixed_stats(stats, "pol", pol_stats)
+        stats["TimeElapsed"] = time.time() - tstart
+        if callback:
+            callback(stats)
+
+
+# ================================================================ per-path API
+def get_paths(env, agent, cfg, seed_iter):
+    if cfg["parallel"]:
+        raise NotImplementedError
+    return do_rollouts_serial(env, agent, cfg["timestep_limit"], cfg["timesteps_per_batch"], seed_iter)
+
+
+def rollout(env, agent, timestep_limit):
+    """One episode (`core.py:182-207`) through the device collector with E = 1."""
+    col = agent.path_collector(env, timestep_limit)
+    while True:
+        paths = col.collect().to_paths()
+        if paths:
+            return paths[0]
+
+
+def do_rollouts_serial(env, agent, timestep_limit, n_timesteps, seed_iter):
+    """Whole episodes until more than n_timesteps steps (`core.py:210-221`)."""
+    paths = []
+    timesteps_sofar = 0
+    while True:
+        next(seed_iter)
+        path = rollout(env, agent, timestep_limit)
+        paths.append(path)
+        timesteps_sofar += pathlength(path)
+        if timesteps_sofar > n_timesteps:
+            break
+    return paths
+
+
+def pathlength(path):
+    return len(path["action"])
+
+
+# ================================================================ policies / probtypes
+class ProbType:
+    pass
+
+
+class Categorical(ProbType):
+    """`core.py:339-365` (device math lives in mrl_mlp_rows; this is the host API)."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def sample(self, prob):
+        cs = np.cumsum(prob, axis=1)
+        return np.argmax(cs > np.random.rand(prob.shape[0], 1), axis=1)
+
+    def maxprob(self, prob):
+        return prob.argmax(axis=1)
+
+
+class DiagGauss(ProbType):
+    """`core.py:402-438`."""
+
+    def __init__(self, d):
+        self.d = d
+
+    def sample(self, prob):
+        mean_nd, std_nd = prob[:, :self.d], prob[:, self.d:]
+        return np.random.randn(prob.shape[0], self.d).astype(np.float32) * std_nd + mean_nd
+
+    def maxprob(self, prob):
+        return prob[:, :self.d]
+
+
+class StochPolicyMLP:
+    """Device replacement of StochPolicyKeras (`core.py:296-336`)."""
+
+    def __init__(self, net, probtype):
+        self.net = net
+        self._probtype = probtype
+        self.discrete = isinstance(probtype, Categorical)
+
+    @property
+    def probtype(self):
+        return self._probtype
+
+    def act(self, ob, stochastic=True):
+        """`core.py:261-267`: single-row forward on device."""
+        x = torch.as_tensor(np.asarray(ob, dtype=np.float32)[None]).to(self.net.device)
+        prob = self.net.forward(x, 1).cpu().numpy().reshape(1, -1)
+        a = self.probtype.sample(prob) if stochastic else self.probtype.maxprob(prob)
+        return a[0], {"prob": prob[0]}
+
+    def get_flat(self):
+        return self.net.get_flat()
+
+    def set_from_flat(self, th):
+        self.net.set_flat(th)

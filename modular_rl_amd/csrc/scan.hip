@@ -249,6 +249,90 @@ __global__ void cast_scale_kernel(const float* __restrict__ a, double s, int64_t
     o[i] = s * (double)a[i];
 }
 
+// ------------------------------------------------------------------ moments / episode stats
+// per-block fp64 (sum, sumsq) of (a - b) -> part[block][2]
+__global__ void moments_kernel(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
+                               double* __restrict__ part) {
+  __shared__ double red[2][256];
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = (double)a[i] - (b ? (double)b[i] : 0.0);
+    s1 += v;
+    s2 += v * v;
+  }
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + o];
+      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[blockIdx.x * 2] = red[0][0];
+    part[blockIdx.x * 2 + 1] = red[1][0];
+  }
+}
+
+// episode statistics over time-major rows (core.py:31-44): one thread per env scans
+// its rows in time order; part[block][8] = (n_ep, sum R, sum R^2, max R, sum L, max L, sum r, 0)
+__global__ void episode_stats_kernel(const float* __restrict__ rew, const uint8_t* __restrict__ flags, int64_t T,
+                                     int64_t E, double* __restrict__ part) {
+  __shared__ double red[6][256];
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double cnt = 0, sr = 0, sr2 = 0, mr = -INFINITY, sl = 0, ml = 0;
+  if (e < E) {
+    double ep = 0.0, len = 0.0;
+    for (int64_t t = 0; t < T; ++t) {
+      ep += (double)rew[t * E + e];
+      len += 1.0;
+      if (flags[t * E + e] & 1) {
+        cnt += 1.0;
+        sr += ep;
+        sr2 += ep * ep;
+        mr = fmax(mr, ep);
+        sl += len;
+        ml = fmax(ml, len);
+        ep = 0.0;
+        len = 0.0;
+      }
+    }
+  }
+  red[0][threadIdx.x] = cnt;
+  red[1][threadIdx.x] = sr;
+  red[2][threadIdx.x] = sr2;
+  red[3][threadIdx.x] = mr;
+  red[4][threadIdx.x] = sl;
+  red[5][threadIdx.x] = ml;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      for (int q = 0; q < 6; ++q) {
+        if (q == 3 || q == 5) red[q][threadIdx.x] = fmax(red[q][threadIdx.x], red[q][threadIdx.x + o]);
+        else red[q][threadIdx.x] += red[q][threadIdx.x + o];
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) part[blockIdx.x * 8 + threadIdx.x] = red[threadIdx.x][0];
+  if (threadIdx.x == 6) part[blockIdx.x * 8 + 6] = 0.0;
+  if (threadIdx.x == 7) part[blockIdx.x * 8 + 7] = 0.0;
+}
+
+__global__ void episode_stats_final_kernel(const double* __restrict__ part, int64_t nb, double* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  double a[6] = {0, 0, 0, -INFINITY, 0, 0};
+  for (int64_t b = 0; b < nb; ++b) {
+    for (int q = 0; q < 6; ++q) {
+      const double v = part[b * 8 + q];
+      a[q] = (q == 3 || q == 5) ? fmax(a[q], v) : a[q] + v;
+    }
+  }
+  for (int q = 0; q < 6; ++q) out[q] = a[q];
+}
+
 static inline int64_t grid_for(int64_t n, int64_t bs = 256, int64_t cap = 2048) {
   int64_t g = (n + bs - 1) / bs;
   if (g < 1) g = 1;
@@ -327,6 +411,31 @@ int mrl_axpy_cast(const float* theta_old, const double* fullstep, double frac, i
   hipLaunchKernelGGL(axpy_cast_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, theta_old, fullstep, frac,
                      n, theta_out);
   return hip_check(hipGetLastError(), "mrl_axpy_cast");
+}
+
+int64_t mrl_moments_workspace_bytes(int64_t n) { return grid_for(n, 256, 1024) * 2 * (int64_t)sizeof(double); }
+
+int mrl_moments(const float* a, const float* b, int64_t n, double* out, void* workspace, void* stream) {
+  if (!a || !out || !workspace) return fail(E_ARG, "null pointer");
+  const int64_t g = grid_for(n, 256, 1024);
+  double* part = reinterpret_cast<double*>(workspace);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(moments_kernel, dim3(g), dim3(256), 0, s, a, b, n, part);
+  hipLaunchKernelGGL(moments_final_kernel, dim3(1), dim3(256), 0, s, part, g, (double)n, out);
+  return hip_check(hipGetLastError(), "mrl_moments");
+}
+
+int64_t mrl_episode_stats_workspace_bytes(int64_t E) { return ((E + 255) / 256) * 8 * (int64_t)sizeof(double); }
+
+int mrl_episode_stats(const float* rew, const uint8_t* flags, int64_t T, int64_t E, double* out, void* workspace,
+                      void* stream) {
+  if (!rew || !flags || !out || !workspace) return fail(E_ARG, "null pointer");
+  const int64_t nb = (E + 255) / 256;
+  double* part = reinterpret_cast<double*>(workspace);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(episode_stats_kernel, dim3(nb), dim3(256), 0, s, rew, flags, T, E, part);
+  hipLaunchKernelGGL(episode_stats_final_kernel, dim3(1), dim3(64), 0, s, part, nb, out);
+  return hip_check(hipGetLastError(), "mrl_episode_stats");
 }
 
 int mrl_cast_scale_f32_f64(const float* in, double scale, int64_t n, double* out, void* stream) {

@@ -1,0 +1,218 @@
+"""Trust Region Policy Optimization update on device (`trpo.py:12-200` of the reference).
+
+``TrpoUpdater(stochpol, usercfg)`` keeps the reference constructor, ``options``
+and ``__call__(paths) -> OrderedDict(surr/kl/ent _before/_after)``; it also
+exposes ``update(batch)`` on the device-resident batch of the lock-step
+collector.  The numerics run in libmrl_hip:
+
+  g, losses_before      one fused pass   (mrl_mlp_rows SURRGRAD + mrl_mlp_vjp)
+  cg(F + damping I, -g) device CG vectors (fp64), 10 x [Fvp kernels + cg_update];
+                        the residual-tolerance break is a device flag that turns
+                        the remaining Fvp launches into no-ops (no host sync)
+  shs / lm / fullstep   one more Fvp + mrl_trpo_step (the duplicate diagnostic
+                        Fvp of trpo.py:111 is dropped)
+  linesearch            per candidate: theta = theta_old + frac*fullstep (fp64,
+                        cast to fp32 like SetFromFlat) + one fused loss pass; the
+                        accepted candidate's (surr, kl, ent) are losses_after.
+
+In data-parallel mode every sum above is all-reduced over ranks (dist.Comm)
+before it is used, so all ranks take the identical step.
+"""
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream
+from .dist import Comm
+from .misc_utils import update_default_config
+
+
+class HipTrpoOps:
+    """The device kernels the updater drives (one policy net, one bound batch)."""
+
+    def __init__(self, net):
+        self.net = net
+        P, dev = net.P, net.device
+        self.P = P
+        f32 = dict(dtype=torch.float32, device=dev)
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.g = torch.zeros(P, **f32)
+        self.fv = torch.zeros(P, **f32)
+        self.b = torch.zeros(P, **f64)
+        self.x = torch.zeros(P, **f64)
+        self.r = torch.zeros(P, **f64)
+        self.p = torch.zeros(P, **f64)
+        self.p32 = torch.zeros(P, **f32)
+        self.x32 = torch.zeros(P, **f32)
+        self.zero32 = torch.zeros(P, **f32)
+        self.fullstep = torch.zeros(P, **f64)
+        self.cand = torch.zeros(P, **f32)
+        self.cand_image = torch.zeros_like(net.image)
+        self.tan_image = torch.zeros_like(net.image)
+        self.state = torch.zeros(4, **f64)
+        self.flag = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.step_out = torch.zeros(4, **f64)
+        self.sums = torch.zeros(4, **f64)
+        self.batch = None
+
+    def bind(self, batch, inv_n_global):
+        self.batch = batch
+        self.inv_ng = float(inv_n_global)
+        n = batch.n
+        self.ghead = self.net.ws.get("ghead", n * self.net.gh, torch.float32)
+        self.partial = self.net.ws.get("partial", self.net.partial_rows(n) * 4, torch.float64)
+
+    def surrgrad(self):
+        b, net = self.batch, self.net
+        net.rows(_lib.EPI_SURRGRAD, b.obs, b.n, inv_n_global=self.inv_ng, act=b.act, adv=b.adv, oldprob=b.prob,
+                 ghead=self.ghead, partial=self.partial)
+        net.reduce_partial(self.partial, b.n, self.sums)
+        net.vjp_flat(b.obs, b.n, self.ghead, self.g)
+        return self.g, self.sums
+
+    def losses(self, theta):
+        b, net = self.batch, self.net
+        net.pack(theta=theta, image=self.cand_image, fwd_only=True)
+        net.rows(_lib.EPI_LOSSES, b.obs, b.n, inv_n_global=self.inv_ng, act=b.act, adv=b.adv, oldprob=b.prob,
+                 partial=self.partial, theta=theta, image=self.cand_image)
+        return net.reduce_partial(self.partial, b.n, self.sums)
+
+    def fvp(self, v32, skip=None):
+        b, net = self.batch, self.net
+        net.pack(theta=v32, image=self.tan_image, fwd_only=True, skip=skip)
+        net.rows(_lib.EPI_FVP, b.obs, b.n, inv_n_global=self.inv_ng, ghead=self.ghead, tangent=v32,
+                 image_t=self.tan_image, skip=skip)
+        net.vjp_flat(b.obs, b.n, self.ghead, self.fv, skip=skip)
+        return self.fv
+
+    def neg_g64(self, g):
+        call("mrl_cast_scale_f32_f64", ptr(g), -1.0, self.P, ptr(self.b), stream())
+        return self.b
+
+    def cg_init(self, b):
+        call("mrl_cg_init", ptr(b), self.P, ptr(self.x), ptr(self.r), ptr(self.p), ptr(self.p32), ptr(self.state),
+             ptr(self.flag), stream())
+
+    def cg_update(self, fv, damping, tol):
+        call("mrl_cg_update", ptr(fv), float(damping), float(tol), self.P, ptr(self.x), ptr(self.r), ptr(self.p),
+             ptr(self.p32), ptr(self.state), ptr(self.flag), stream())
+
+    def stepdir32(self):
+        call("mrl_axpy_cast", ptr(self.zero32), ptr(self.x), 1.0, self.P, ptr(self.x32), stream())
+        return self.x32
+
+    def trpo_step(self, fv, g, damping, max_kl):
+        call("mrl_trpo_step", ptr(fv), ptr(self.x), ptr(g), float(damping), float(max_kl), self.P,
+             ptr(self.fullstep), ptr(self.step_out), stream())
+        return self.step_out
+
+    def candidate(self, theta_old, frac):
+        call("mrl_axpy_cast", ptr(theta_old), ptr(self.fullstep), float(frac), self.P, ptr(self.cand), stream())
+        return self.cand
+
+
+def _losses(sums, n_glob):
+    s = sums.detach().double().cpu().numpy()
+    return np.array([-s[0] / n_glob, s[1] / n_glob, s[2] / n_glob])
+
+
+def linesearch(f, fval, expected_improve_rate, max_backtracks=10, accept_ratio=.1):
+    """Backtracking line search on the surrogate only (`trpo.py:143-159`).
+    ``fval`` is the surrogate at x (the reference's ``f(x)``); ``f(stepfrac) ->
+    (newfval, aux)`` evaluates the candidate x + stepfrac*fullstep on device.
+    Returns (success, stepfrac or None, k, aux)."""
+    for k, stepfrac in enumerate(.5 ** np.arange(max_backtracks)):
+        newfval, aux = f(stepfrac)
+        actual_improve = fval - newfval
+        expected_improve = expected_improve_rate * stepfrac
+        ratio = actual_improve / expected_improve
+        if ratio > accept_ratio and actual_improve > 0:
+            return True, stepfrac, k, aux
+    return False, None, -1, None
+
+
+class TrpoUpdater:
+    options = [
+        ("cg_damping", float, 1e-3, "Add multiple of the identity to Fisher matrix during CG"),
+        ("max_kl", float, 1e-2, "KL divergence between old and new policy (averaged over state-space)"),
+    ]
+    CG_ITERS = 10
+    RESIDUAL_TOL = 1e-10
+
+    def __init__(self, stochpol, usercfg, comm=None, ops=None):
+        self.cfg = update_default_config(self.options, usercfg)
+        self.stochpol = stochpol
+        self.comm = comm if comm is not None else Comm()
+        self.ops = ops if ops is not None else HipTrpoOps(stochpol.net)
+        self.loss_names = ["surr", "kl", "ent"]
+        self.last_diag = {}
+
+    # EzFlat surface (core.py:544-554)
+    def get_params_flat(self):
+        return self.stochpol.get_flat()
+
+    def set_params_flat(self, th):
+        self.stochpol.set_from_flat(th)
+
+    def __call__(self, paths):
+        """Per-path API (`trpo.py:72-78`): concatenate, move to device, update."""
+        from .core import Batch
+        batch = Batch.from_paths(paths, self.stochpol, device=self.stochpol.net.device)
+        return self.update(batch)
+
+    def update(self, batch):
+        cfg, ops, comm, net = self.cfg, self.ops, self.comm, self.stochpol.net
+        n_glob = comm.allreduce_int(batch.n)
+        ops.bind(batch, 1.0 / n_glob)
+        thprev = net.theta.clone()
+        g, sums = ops.surrgrad()
+        comm.allreduce_(g)
+        comm.allreduce_(sums)
+        losses_before = _losses(sums, n_glob)
+        diag = {"n_global": n_glob}
+        losses_after = losses_before
+        g_host = g.detach().double().cpu().numpy()
+        if np.allclose(g_host, 0):
+            print("got zero gradient. not updating")
+            diag["skipped"] = True
+        else:
+            damping, max_kl = float(cfg["cg_damping"]), float(cfg["max_kl"])
+            ops.cg_init(ops.neg_g64(g))
+            for _ in range(self.CG_ITERS):
+                fv = ops.fvp(ops.p32, skip=ops.flag)
+                comm.allreduce_(fv)
+                ops.cg_update(fv, damping, self.RESIDUAL_TOL)
+            fv = ops.fvp(ops.stepdir32())
+            comm.allreduce_(fv)
+            out = ops.trpo_step(fv, g, damping, max_kl).cpu().numpy()
+            shs, lm, neggdotstepdir, rate = (float(v) for v in out)
+            fval = losses_before[0]
+
+            def f(stepfrac):
+                l = _losses(self._candidate_losses(thprev, stepfrac), n_glob)
+                return l[0], l
+
+            success, frac, k, laux = linesearch(f, fval, rate)
+            if success:
+                net.theta.copy_(ops.cand)  # the accepted (last evaluated) candidate
+                losses_after = laux
+            else:
+                net.theta.copy_(thprev)
+            net.pack()
+            st = ops.state.cpu().numpy()
+            diag.update(skipped=False, shs=shs, lm=lm, neggdotstepdir=neggdotstepdir, expected_rate=rate,
+                        success=success, k=k, stepfrac=frac, cg_iters=int(st[2]), rdotr=float(st[0]))
+        self.last_diag = diag
+        out = OrderedDict()
+        for (lname, lbefore, lafter) in zip(self.loss_names, losses_before, losses_after):
+            out[lname + "_before"] = lbefore
+            out[lname + "_after"] = lafter
+        return out
+
+    def _candidate_losses(self, thprev, stepfrac):
+        th = self.ops.candidate(thprev, stepfrac)
+        sums = self.ops.losses(th)
+        self.comm.allreduce_(sums)
+        return sums

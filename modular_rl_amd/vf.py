@@ -1,0 +1,177 @@
+"""Value-function baseline on device (`core.py:595-697` of the reference).
+
+``NnVf`` / ``NnRegression`` / ``LbfgsOptimizer`` keep the reference's names and
+semantics: the VF input is ``[obs, t / timestep_limit]`` (`core.py:659-660`), the
+regression target is ``mixfrac * return + (1 - mixfrac) * V_old`` (`core.py:622-
+624`), and the loss ``sum((y - yhat)^2)/N + 1e-3 * sum(theta^2)`` (`core.py:611-617`)
+is minimised by scipy's L-BFGS-B for ``maxiter`` iterations (`core.py:686-687`) on
+the host, while every loss+gradient evaluation is one fused forward pass
+(``mrl_mlp_rows`` VFLOSS) + one VJP (``mrl_mlp_vjp``) on the GPU, all-reduced over
+ranks in data-parallel mode.
+"""
+from collections import OrderedDict
+
+import numpy as np
+import scipy.optimize
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream
+from .dist import Comm
+
+L2_COEF = 1e-3
+
+
+class DeviceMoments:
+    """(sum, sumsq, n) of (a - b) over rows, summed over ranks."""
+
+    def __init__(self, device, comm):
+        self.device, self.comm = device, comm
+        self.out = torch.zeros(3, dtype=torch.float64, device=device)
+        self.ws = None
+
+    def __call__(self, a, b, n):
+        nbytes = int(_lib.load().mrl_moments_workspace_bytes(int(n)))
+        if self.ws is None or self.ws.numel() * 8 < nbytes:
+            self.ws = torch.empty(nbytes // 8 + 1, dtype=torch.float64, device=self.device)
+        call("mrl_moments", ptr(a), ptr(b), int(n), ptr(self.out), ptr(self.ws), stream())
+        self.comm.allreduce_(self.out)
+        s, s2, c = (float(v) for v in self.out.cpu().numpy())
+        return s, s2, c
+
+    def std(self, a, b, n):
+        s, s2, c = self(a, b, n)
+        m = s / c
+        return float(np.sqrt(max(s2 / c - m * m, 0.0)))
+
+
+class LbfgsOptimizer:
+    """scipy L-BFGS-B driver; loss and gradient evaluated on device (`core.py:663-697`)."""
+
+    def __init__(self, net, maxiter=3, comm=None):
+        self.net = net
+        self.maxiter = maxiter
+        self.comm = comm if comm is not None else Comm()
+        self.g = torch.zeros(net.P, dtype=torch.float32, device=net.device)
+        self.sums = torch.zeros(4, dtype=torch.float64, device=net.device)
+        self.n_evals = 0
+
+    def get_params_flat(self):
+        return self.net.get_flat()
+
+    def set_params_flat(self, th):
+        self.net.set_flat(th)
+
+    def _eval(self, data, with_grad):
+        net = self.net
+        x, ep_t, limit, n, target, n_glob = data
+        ghead = net.ws.get("vf_ghead", n, torch.float32)
+        partial = net.ws.get("vf_partial", net.partial_rows(n) * 4, torch.float64)
+        net.rows(_lib.EPI_VFLOSS, x, n, ep_t=ep_t, timestep_limit=limit, inv_n_global=1.0 / n_glob, target=target,
+                 ghead=ghead, partial=partial)
+        net.reduce_partial(partial, n, self.sums)
+        if with_grad:
+            net.vjp_flat(x, n, ghead, self.g, ep_t=ep_t, timestep_limit=limit)
+            self.comm.allreduce_(self.g)
+        self.comm.allreduce_(self.sums)
+        th = net.theta.detach().double().cpu().numpy()
+        mse = float(self.sums[0].item()) / n_glob
+        l2 = L2_COEF * float(np.sum(th * th))
+        g = None
+        if with_grad:
+            g = self.g.detach().double().cpu().numpy() + 2.0 * L2_COEF * th
+        return mse + l2, mse, l2, g
+
+    def update(self, data):
+        thprev = self.get_params_flat()
+
+        def lossandgrad(th):
+            self.set_params_flat(th)
+            self.n_evals += 1
+            l, _, _, g = self._eval(data, True)
+            return l, g.astype("float64")
+
+        self.set_params_flat(thprev)
+        lb, mb, l2b, _ = self._eval(data, False)
+        theta, _, opt_info = scipy.optimize.fmin_l_bfgs_b(lossandgrad, thprev.astype(np.float64), maxiter=self.maxiter)
+        self.set_params_flat(theta)
+        la, ma, l2a, _ = self._eval(data, False)
+        info = OrderedDict()
+        for name, b, a in (("loss", lb, la), ("mse", mb, ma), ("l2", l2b, l2a)):
+            info[name + "_before"] = b
+            info[name + "_after"] = a
+        self.last_opt_info = {k: v for k, v in opt_info.items() if k != "grad"}
+        return info
+
+
+class NnRegression:
+    """`core.py:595-637`: mixfrac target, L-BFGS fit, prediction / EV statistics."""
+
+    def __init__(self, net, mixfrac=1.0, maxiter=2, comm=None):
+        self.net = net
+        self.mixfrac = mixfrac
+        self.comm = comm if comm is not None else Comm()
+        self.opt = LbfgsOptimizer(net, maxiter=maxiter, comm=self.comm)
+        self.moments = DeviceMoments(net.device, self.comm)
+
+    def predict(self, x, n, ep_t=None, timestep_limit=1.0, out=None):
+        return self.net.forward(x, n, ep_t=ep_t, timestep_limit=timestep_limit, out=out)
+
+    def fit(self, x, n, ytarg, ep_t=None, timestep_limit=1.0, ypredold=None):
+        """ytarg: [n] device returns. ypredold: V_old predictions if already computed
+        (compute_advantage evaluates the same net on the same rows, core.py:70)."""
+        net = self.net
+        if ypredold is None:
+            ypredold = self.predict(x, n, ep_t, timestep_limit)
+        target = net.ws.get("vf_target", n, torch.float32)
+        call("mrl_vf_target", ptr(ytarg), ptr(ypredold), float(self.mixfrac), int(n), ptr(target), stream())
+        n_glob = self.comm.allreduce_int(n)
+        out = self.opt.update((x, ep_t, timestep_limit, n, target, n_glob))
+        yprednew = self.predict(x, n, ep_t, timestep_limit, out=net.ws.get("vf_pred_new", n, torch.float32))
+        out["PredStdevBefore"] = self.moments.std(ypredold, None, n)
+        out["PredStdevAfter"] = self.moments.std(yprednew, None, n)
+        vary = self.moments.std(ytarg, None, n) ** 2
+        out["TargStdev"] = float(np.sqrt(vary))
+
+        def ev(yp):  # explained_variance_2d (misc_utils.py:44-49)
+            if vary < 1e-10:
+                return 0.0
+            return 1.0 - self.moments.std(ytarg, yp, n) ** 2 / vary
+
+        out["EV_before"] = ev(ypredold)
+        out["EV_after"] = ev(yprednew)
+        return out
+
+
+class NnVf:
+    """Value baseline with the time feature (`core.py:643-660`)."""
+
+    def __init__(self, net, timestep_limit, regression_params, comm=None):
+        self.reg = NnRegression(net, comm=comm, **regression_params)
+        self.timestep_limit = timestep_limit
+
+    @property
+    def net(self):
+        return self.reg.net
+
+    def preproc(self, ob_no):
+        return np.concatenate([ob_no, np.arange(len(ob_no)).reshape(-1, 1) / float(self.timestep_limit)], axis=1)
+
+    def predict(self, path):
+        ob = torch.as_tensor(np.asarray(path["observation"], dtype=np.float32)).to(self.net.device)
+        n = ob.shape[0]
+        ep_t = torch.arange(n, dtype=torch.int32, device=self.net.device)
+        return self.reg.predict(ob, n, ep_t, self.timestep_limit).cpu().numpy().astype(np.float64)
+
+    def predict_batch(self, batch, out=None):
+        return self.reg.predict(batch.obs, batch.n, batch.ep_t, self.timestep_limit, out=out)
+
+    def fit_batch(self, batch):
+        return self.reg.fit(batch.obs, batch.n, batch.ret, batch.ep_t, self.timestep_limit, ypredold=batch.vpred)
+
+    def fit(self, paths):
+        from .core import Batch
+        batch = Batch.from_paths(paths, None, device=self.net.device, need_policy=False)
+        batch.ret = torch.as_tensor(np.concatenate([p["return"] for p in paths]).astype(np.float32)).to(self.net.device)
+        batch.vpred = None
+        return self.reg.fit(batch.obs, batch.n, batch.ret, batch.ep_t, self.timestep_limit)

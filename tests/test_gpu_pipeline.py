@@ -1,0 +1,200 @@
+"""GPU parity of the rest of the hot path: GAE scan + standardisation, the
+lock-step rollout (envs, filter, sampling), the TRPO update (CG / step / line
+search) and the VF L-BFGS fit, each against the oracle / golden fixtures."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import rollout_np as RO
+from oracle import trpo_np as T
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _dev(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).cuda()
+
+
+@pytest.mark.parametrize("Tn,E", [(1, 1), (33, 5), (100, 37), (257, 64)])
+def test_gae_and_standardize(Tn, E):
+    from modular_rl_amd import core
+    from modular_rl_amd.collector import Batch
+    rng = np.random.default_rng(Tn * 100 + E)
+    rew = rng.standard_normal((Tn, E)).astype(np.float32)
+    v = rng.standard_normal((Tn, E)).astype(np.float32)
+    last = rng.random((Tn, E)) < 0.08
+    last[-1] = True
+    term = last & (rng.random((Tn, E)) < 0.5)
+    flags = (last.astype(np.uint8) | (term.astype(np.uint8) << 1))
+    adv_w, ret_w = T.gae_batched(rew.astype(np.float64), v.astype(np.float64), last, term, 0.995, 0.97)
+
+    class VF:  # baseline predictions injected
+        def predict_batch(self, batch, out=None):
+            return _dev(v.reshape(-1))
+
+    b = Batch(Tn * E, _dev(np.zeros((Tn * E, 1))), None, None, _dev(rew.reshape(-1)), _dev(flags.reshape(-1), torch.uint8),
+              None, T=Tn, E=E)
+    core.compute_advantage_batch(VF(), b, 0.995, 0.97)
+    np.testing.assert_allclose(b.ret.cpu().numpy().reshape(Tn, E), ret_w, rtol=1e-5, atol=1e-5)
+    if Tn * E > 1:
+        np.testing.assert_allclose(b.adv.cpu().numpy().reshape(Tn, E), T.standardize(adv_w), rtol=1e-4, atol=1e-4)
+
+
+def _policy(head, nin, nout, seed):
+    from modular_rl_amd import _lib
+    from modular_rl_amd.core import Categorical, DiagGauss, StochPolicyMLP
+    from modular_rl_amd.nets import MlpNet
+    rng = np.random.default_rng(seed)
+    spec = T.Spec(nin, [64, 64], nout, head)
+    th = T.mlp_init(rng, spec.shapes, head == "gauss") + 0.1 * rng.standard_normal(spec.P)
+    if head == "gauss":
+        th[-nout:] = -0.5 + 0.1 * rng.standard_normal(nout)
+    th = th.astype(np.float32).astype(np.float64)
+    net = MlpNet(nin, nout, _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX)
+    net.set_flat(th)
+    pt = DiagGauss(nout) if head == "gauss" else Categorical(nout)
+    return spec, th, StochPolicyMLP(net, pt)
+
+
+@pytest.mark.parametrize("env_id,E,Tn,limit,inject", [
+    ("CartPole-v0", 200, 48, 200, False), ("CartPole-v0", 7, 30, 12, True),
+    ("Hopper-v2", 150, 24, 1000, False), ("Hopper-v2", 130, 16, 9, True), ("CartPole-v0", 1, 40, 200, False)])
+def test_rollout_matches_oracle(env_id, E, Tn, limit, inject):
+    from modular_rl_amd.collector import Collector
+    from modular_rl_amd.envs import make
+    env = make(env_id)
+    head = "softmax" if env.discrete else "gauss"
+    spec, th, pol = _policy(head, env.obs_dim, env.act_dim, seed=E)
+    seed = 1234 + E
+    col = Collector(env, pol, E, Tn, limit, filter=1, seed=seed, use_graph=False)
+    kind = RO.CARTPOLE if env.discrete else RO.HOPPER
+    envs = RO.Envs(kind, E, seed)
+    fs = RO.FilterState(env.obs_dim + 1)
+    for it in range(2):
+        noise = None
+        if inject:
+            rng = np.random.default_rng(it)
+            noise = rng.random((Tn, E)) if env.discrete else rng.standard_normal((Tn, E, env.act_dim))
+            col.set_noise(noise.reshape(Tn * E, -1) if not env.discrete else noise.reshape(-1))
+        b = col.collect()
+        want, fs = RO.collect(envs, fs, spec, th, Tn, limit, it, filt=True, noise=noise)
+        np.testing.assert_array_equal(b.flags.cpu().numpy().reshape(Tn, E), want["flags"])
+        np.testing.assert_array_equal(b.ep_t.cpu().numpy().reshape(Tn, E), want["ep_t"])
+        np.testing.assert_allclose(b.obs.cpu().numpy().reshape(Tn, E, -1), want["obs"], rtol=1e-5, atol=1e-5)
+        if env.discrete:
+            np.testing.assert_array_equal(b.act.cpu().numpy().reshape(Tn, E), want["act"])
+        else:
+            np.testing.assert_allclose(b.act.cpu().numpy().reshape(Tn, E, -1), want["act"], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(b.prob.cpu().numpy().reshape(Tn, E, -1), want["prob"], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(b.rew.cpu().numpy().reshape(Tn, E), want["rew"], rtol=1e-4, atol=1e-4)
+        (n, m, var), (nr, mr, vr) = col.filter_stats()
+        assert n == fs.n and nr == fs.nr
+        # fp32 actions feed fp64 dynamics: Hopper states drift ~1e-7 relative over the horizon
+        np.testing.assert_allclose(m, fs.M[:-1], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(mr, fs.M[-1], rtol=1e-5, atol=1e-6)
+
+
+def test_rollout_graph_replay_equals_eager():
+    from modular_rl_amd.collector import Collector
+    from modular_rl_amd.envs import make
+    env = make("Hopper-v2")
+    _, _, pol = _policy("gauss", 11, 3, seed=3)
+    outs = []
+    for g in (False, True):
+        col = Collector(env, pol, 256, 20, 1000, seed=9, use_graph=g)
+        for _ in range(3):
+            b = col.collect()
+        outs.append((b.obs.clone(), b.act.clone(), col.filter_state.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("tag", ["gauss1", "cat1", "gauss0"])
+def test_trpo_update_matches_reference_golden(tag):
+    """Device TrpoUpdater on the batch of tests/golden/trpo_update.npz (produced by the
+    reference's own TrpoUpdater.__call__ control flow)."""
+    from modular_rl_amd.collector import Batch
+    from modular_rl_amd.trpo import TrpoUpdater
+    d = np.load(os.path.join(G, "trpo_update.npz"))
+    head = "gauss" if tag.startswith("gauss") else "softmax"
+    nin, nout = (11, 3) if head == "gauss" else (4, 2)
+    _, _, pol = _policy(head, nin, nout, seed=0)
+    th0 = d[f"{tag}_theta0"]
+    pol.net.set_flat(th0)
+    damping, max_kl = d[f"{tag}_cfg"]
+    up = TrpoUpdater(pol, dict(cg_damping=damping, max_kl=max_kl))
+    N = d[f"{tag}_ob"].shape[0]
+    act = d[f"{tag}_act"]
+    b = Batch(N, _dev(d[f"{tag}_ob"]), _dev(act, torch.int32 if head == "softmax" else torch.float32),
+              _dev(d[f"{tag}_oldprob"]))
+    b.adv = _dev(d[f"{tag}_adv"])
+    stats = up.update(b)
+    th1 = pol.get_flat().astype(np.float64)
+    want = d[f"{tag}_theta1"]
+    step = np.abs(want - th0).max()
+    # fp32 device pipeline vs float64 reference: relative to the step it took
+    assert np.abs(th1 - want).max() <= 2e-3 * step, (np.abs(th1 - want).max(), step)
+    got = np.array([stats[k] for k in ("surr_before", "surr_after", "kl_before", "kl_after", "ent_before", "ent_after")])
+    ref = d[f"{tag}_stats"]
+    np.testing.assert_allclose(got, ref, rtol=2e-3, atol=1e-6)
+    assert up.last_diag["success"]
+
+
+def test_trpo_update_matches_oracle_fp32_tolerance():
+    """Well-conditioned Hopper-shaped case: step direction, lm, accepted k and
+    surr/kl after the step within 1e-4 relative of the float64 oracle."""
+    from modular_rl_amd.collector import Batch
+    from modular_rl_amd.trpo import TrpoUpdater
+    rng = np.random.default_rng(11)
+    spec, th, pol = _policy("gauss", 11, 3, seed=4)
+    N = 20000
+    ob = rng.standard_normal((N, 11)).astype(np.float32).astype(np.float64)
+    oldprob = T.policy_prob(spec, th, ob).astype(np.float32).astype(np.float64)
+    act = T.sample(spec, oldprob, rng.standard_normal((N, 3))).astype(np.float32).astype(np.float64)
+    adv = T.standardize(rng.standard_normal(N) + 0.5 * ob[:, 0]).astype(np.float32).astype(np.float64)
+    th_w, stats_w, diag_w = T.trpo_update(spec, th, ob, act, adv, oldprob, cg_damping=0.1, max_kl=0.01)
+    up = TrpoUpdater(pol, dict(cg_damping=0.1, max_kl=0.01))
+    b = Batch(N, _dev(ob), _dev(act), _dev(oldprob))
+    b.adv = _dev(adv)
+    stats = up.update(b)
+    dg = up.last_diag
+    assert dg["k"] == diag_w["k"]
+    np.testing.assert_allclose(dg["lm"], diag_w["lm"], rtol=1e-4)
+    np.testing.assert_allclose(dg["shs"], diag_w["shs"], rtol=1e-4)
+    th1 = pol.get_flat().astype(np.float64)
+    assert np.abs(th1 - th_w).max() <= 1e-4 * np.abs(th_w - th).max() + 1e-7
+    for k in ("surr_before", "surr_after", "kl_after", "ent_before", "ent_after"):
+        np.testing.assert_allclose(stats[k], stats_w[k], rtol=1e-4, atol=1e-7, err_msg=k)
+
+
+def test_vf_fit_matches_oracle():
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import MlpNet
+    from modular_rl_amd.vf import NnVf
+    rng = np.random.default_rng(5)
+    N, O, limit = 5000, 11, 1000.0
+    spec = T.Spec(O + 1, [64, 64], 1, "linear")
+    th = T.mlp_init(rng, spec.shapes, False).astype(np.float32).astype(np.float64)
+    obs = rng.standard_normal((N, O)).astype(np.float32)
+    ep_t = rng.integers(0, 1000, N).astype(np.int32)
+    ret = (3 * obs[:, 0] + np.sin(obs[:, 1]) + ep_t / 500.0).astype(np.float32)
+    X = np.concatenate([obs.astype(np.float64), (ep_t / limit).astype(np.float32).astype(np.float64)[:, None]], 1)
+    th_w, st_w, _, _ = T.vf_fit(spec, th, X, ret.astype(np.float64), mixfrac=0.1, maxiter=2)
+    net = MlpNet(O + 1, 1, _lib.HEAD_LINEAR)
+    net.set_flat(th)
+    vf = NnVf(net, limit, dict(mixfrac=0.1))
+
+    class B:
+        pass
+    b = B()
+    b.obs, b.n, b.ep_t, b.ret = _dev(obs), N, _dev(ep_t, torch.int32), _dev(ret)
+    b.vpred = vf.predict_batch(b)
+    st = vf.fit_batch(b)
+    for k in ("loss_before", "mse_before", "l2_before", "loss_after", "mse_after", "PredStdevBefore",
+              "PredStdevAfter", "TargStdev", "EV_before", "EV_after"):
+        np.testing.assert_allclose(st[k], st_w[k], rtol=2e-4, atol=1e-6, err_msg=k)
+    th1 = net.get_flat().astype(np.float64)
+    assert np.abs(th1 - th_w).max() <= 1e-3 * np.abs(th_w - th).max()
