@@ -1,0 +1,205 @@
+#!/usr/bin/env python
+"""Benchmark: full TRPO iterations on the Hopper-v2-shaped env, 4096 envs x 1024 steps per GPU.
+
+One "step" = one TRPO iteration of run_policy_gradient_algorithm (core.py:135-171):
+lock-step rollout of E x T env steps -> GAE + standardisation -> VF L-BFGS fit ->
+TRPO update (pg, 10-iteration CG on the Fisher product, step scaling, line search).
+Inputs are synthetic (random-init nets, simulator-generated data); all device work
+starts from state already resident in HBM.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
+
+Rank 0 prints ONE JSON line.  value = env-steps/s summed over ranks (weak scaling:
+E x T envs-steps per GPU per iteration).  Also reported: TRPO-iters/s, per-phase
+times, the live HIP-event roofline of the dominant kernel (Fisher-vector product)
+and of the GAE scan, and the CPU oracle timed on a bounded sample of the workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec + TRPO-iters/sec, 4096 envs×1024 steps, 1/2/4/8 MI355X"
+PEAK_FP32_TFLOPS = 157.3     # MI355X dense FP32 (MFMA f32 == VALU rate), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec
+
+
+def flops_per_row(O, A):
+    """Algorithmic FLOP per row of the two Fisher-product kernels (tanh MLP O-64-64-A)."""
+    fwd = 2 * (O * 64 + 64 * 64 + 64 * A)
+    jvp = 2 * (O * 64 + 2 * 64 * 64 + 2 * 64 * A)
+    vjp = 2 * (64 * A + 64 * A + 64 * 64 + 64 * 64 + O * 64)   # gh2, gW2, gW1, gh1, gW0
+    return {"fvp_jvp_rows": fwd + jvp, "fvp_vjp": vjp}
+
+
+GAE_BYTES_PER_ROW = 17  # read r 4 + v 4 + flags 1, write adv 4 + ret 4
+
+
+def cpu_baseline(E, Tn, seed=0):
+    """Time the numpy oracle (CPU restatement of the reference) on one full iteration."""
+    from oracle import rollout_np as RO
+    from oracle import trpo_np as T
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        threads = os.cpu_count()
+    rng = np.random.default_rng(seed)
+    spec = T.Spec(11, [64, 64], 3, "gauss")
+    vspec = T.Spec(12, [64, 64], 1, "linear")
+    th = T.mlp_init(rng, spec.shapes, True)
+    thv = T.mlp_init(rng, vspec.shapes, False)
+    envs = RO.Envs(RO.HOPPER, E, seed)
+    fs = RO.FilterState(12)
+    t0 = time.perf_counter()
+    out, fs = RO.collect(envs, fs, spec, th, Tn, 1000, 0)
+    N = E * Tn
+    ob = out["obs"].reshape(N, 11).astype(np.float64)
+    X = np.concatenate([ob, (out["ep_t"].reshape(N) / 1000.0)[:, None]], axis=1)
+    v = T.mlp_forward(vspec, thv, X, np.float32)[0][:, 0].astype(np.float64).reshape(Tn, E)
+    flags = out["flags"]
+    adv, ret = T.gae_batched(out["rew"].astype(np.float64), v, (flags & 1) > 0, (flags & 2) > 0, 0.995, 0.97)
+    adv = T.standardize(adv).reshape(N)
+    T.vf_fit(vspec, thv, X, ret.reshape(N), mixfrac=0.1, maxiter=2, dtype=np.float32)
+    T.trpo_update(spec, th, ob, out["act"].reshape(N, 3).astype(np.float64), adv,
+                  out["prob"].reshape(N, 6).astype(np.float64), cg_damping=0.1, max_kl=0.01, dtype=np.float32)
+    dt = time.perf_counter() - t0
+    return {"value": N / dt, "unit": "env-steps/s", "cores": int(threads), "kind": "port",
+            "sample": f"one full TRPO iteration (rollout+GAE+VF fit+update) of the numpy oracle on Hopper "
+                      f"{E} envs x {Tn} steps = {N} env-steps, float32 update / float64 rollout, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--env", default="Hopper-v2")
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--horizon", type=int, default=1024)
+    ap.add_argument("--cpu-envs", type=int, default=1024)
+    ap.add_argument("--cpu-horizon", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    from modular_rl_amd import timing
+    from modular_rl_amd.agentzoo import TrpoAgent
+    from modular_rl_amd.core import compute_advantage_batch
+    from modular_rl_amd.dist import init_from_env
+    from modular_rl_amd.envs import make
+
+    comm = init_from_env()
+    if torch.cuda.is_available() and not comm.enabled:
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    rank, world = comm.rank, comm.world
+    env = make(args.env)
+    E, Tn = args.envs, args.horizon
+    cfg = dict(timestep_limit=env.spec.max_episode_steps, gamma=0.995, lam=0.97, max_kl=0.01, cg_damping=0.1,
+               n_envs=E, horizon=Tn, filter=1, seed=0, hid_sizes=[64, 64], activation="tanh", use_graph=1)
+    agent = TrpoAgent(env.observation_space, env.action_space, cfg, comm=comm)
+    collector = agent.make_collector(env, cfg)
+
+    def ev():
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    phases = {"rollout": 0.0, "advantage": 0.0, "vf_fit": 0.0, "trpo_update": 0.0}
+
+    def iteration(record):
+        e0 = ev()
+        batch = collector.collect()
+        e1 = ev()
+        compute_advantage_batch(agent.baseline, batch, cfg["gamma"], cfg["lam"], comm)
+        e2 = ev()
+        agent.baseline.fit_batch(batch)
+        e3 = ev()
+        agent.updater.update(batch)
+        e4 = ev()
+        collector.episode_stats(batch)
+        if record is not None:
+            record.append((e0, e1, e2, e3, e4))
+
+    for _ in range(args.warmup):
+        iteration(None)
+    timing.enable(True)
+    rec = []
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        iteration(rec)
+    torch.cuda.synchronize()
+    comm.barrier()
+    elapsed = time.perf_counter() - t0
+    if comm.enabled:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern = timing.summary()
+    timing.enable(False)
+    for (e0, e1, e2, e3, e4) in rec:
+        phases["rollout"] += e0.elapsed_time(e1)
+        phases["advantage"] += e1.elapsed_time(e2)
+        phases["vf_fit"] += e2.elapsed_time(e3)
+        phases["trpo_update"] += e3.elapsed_time(e4)
+    K = args.steps
+    n_local = E * Tn
+    total_steps = n_local * world * K
+    value = total_steps / elapsed
+    if rank != 0:
+        return
+    fpr = flops_per_row(env.obs_dim, env.act_dim)
+    kinfo = {}
+    for name in ("fvp_jvp_rows", "fvp_vjp"):
+        if name in kern:
+            cnt, mean_ms, tot_ms = kern[name]
+            achieved = fpr[name] * n_local / (mean_ms * 1e-3) / 1e12
+            kinfo[name] = dict(launches=cnt, mean_ms=mean_ms, total_ms=tot_ms, tflops=achieved)
+    dom = max(kinfo, key=lambda k: kinfo[k]["total_ms"])
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+    roofline = {"bound": "mfma", "achieved": round(kinfo[dom]["tflops"], 3), "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(kinfo[dom]["tflops"] / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+                "kernel": dom, "flop_per_row": fpr[dom], "rows_per_launch": n_local,
+                "mean_launch_ms": round(kinfo[dom]["mean_ms"], 4), "launches_timed": kinfo[dom]["launches"]}
+    gae = None
+    if "gae_scan" in kern:
+        cnt, mean_ms, _ = kern["gae_scan"]
+        gbs = GAE_BYTES_PER_ROW * n_local / (mean_ms * 1e-3) / 1e9
+        gae = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+               "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_row": GAE_BYTES_PER_ROW, "mean_launch_ms": round(mean_ms, 4)}
+    line = {
+        "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": K,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1000, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "config": {"workload": f"{args.env} (surrogate dynamics) {E} envs x {Tn} steps per GPU, one TRPO iteration "
+                               "per step (rollout+GAE+VF L-BFGS+TRPO CG/linesearch)",
+                   "envs_per_gpu": E, "horizon": Tn, "global_batch": E * Tn * world, "parallelism": f"dp{world}",
+                   "policy": f"{env.obs_dim}-64-64-{env.act_dim} tanh DiagGauss", "gamma": 0.995, "lam": 0.97,
+                   "max_kl": 0.01, "cg_damping": 0.1},
+        "trpo_iters_per_sec": round(K / elapsed, 4),
+        "rollout_env_steps_per_sec": round(n_local * world * K / (phases["rollout"] * 1e-3), 1),
+        "phase_ms_per_iter": {k: round(v / K, 3) for k, v in phases.items()},
+        "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()} for k, v in kinfo.items()},
+        "roofline": roofline,
+        "roofline_gae": gae,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_envs, args.cpu_horizon)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -20,7 +20,7 @@ from importlib import import_module
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, timing
 from ._lib import call, ptr, stream
 from .collector import Batch, Collector
 from .dist import Comm
@@ -88,8 +88,10 @@ def compute_advantage_batch(vf, batch, gamma, lam, comm=None):
         batch.adv = torch.empty(n, dtype=torch.float32, device=dev)
         batch.ret = torch.empty(n, dtype=torch.float32, device=dev)
     ws, moments = _GAE.get(batch.T, batch.E, dev)
+    timing.start("gae_scan")
     call("mrl_gae", ptr(batch.rew), ptr(batch.vpred), ptr(batch.flags), int(batch.T), int(batch.E), float(gamma),
          float(lam), ptr(batch.adv), ptr(batch.ret), ptr(moments), ptr(ws), stream())
+    timing.stop("gae_scan")
     comm.allreduce_(moments)
     call("mrl_standardize", ptr(batch.adv), int(n), ptr(moments), stream())
     return batch

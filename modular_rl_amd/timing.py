@@ -1,0 +1,43 @@
+"""Optional HIP-event timing of named launch regions on the current stream.
+
+Disabled by default (zero cost); bench.py enables it to measure the average
+device duration of the dominant kernels live inside the timed region.
+"""
+import collections
+
+import torch
+
+_ENABLED = False
+_open = {}
+_events = collections.defaultdict(list)
+
+
+def enable(on=True):
+    global _ENABLED
+    _ENABLED = on
+    _open.clear()
+    _events.clear()
+
+
+def start(name):
+    if _ENABLED:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        _open[name] = e
+
+
+def stop(name):
+    if _ENABLED:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        _events[name].append((_open.pop(name), e))
+
+
+def summary():
+    """{name: (count, mean_ms, total_ms)} -- synchronises."""
+    torch.cuda.synchronize()
+    out = {}
+    for k, v in _events.items():
+        ms = [a.elapsed_time(b) for a, b in v]
+        out[k] = (len(ms), sum(ms) / max(len(ms), 1), sum(ms))
+    return out

@@ -23,7 +23,7 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, timing
 from ._lib import call, ptr, stream
 from .dist import Comm
 from .misc_utils import update_default_config
@@ -82,9 +82,13 @@ class HipTrpoOps:
     def fvp(self, v32, skip=None):
         b, net = self.batch, self.net
         net.pack(theta=v32, image=self.tan_image, fwd_only=True, skip=skip)
+        timing.start("fvp_jvp_rows")
         net.rows(_lib.EPI_FVP, b.obs, b.n, inv_n_global=self.inv_ng, ghead=self.ghead, tangent=v32,
                  image_t=self.tan_image, skip=skip)
+        timing.stop("fvp_jvp_rows")
+        timing.start("fvp_vjp")
         net.vjp_flat(b.obs, b.n, self.ghead, self.fv, skip=skip)
+        timing.stop("fvp_vjp")
         return self.fv
 
     def neg_g64(self, g):
