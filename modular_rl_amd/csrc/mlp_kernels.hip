@@ -64,7 +64,8 @@ constexpr float LOG2PI_F = 1.8378770664093453f;
 constexpr float LOG2PIE_F = 2.8378770664093453f;
 
 template <int EPI>
-__global__ __launch_bounds__(ROWS_BLOCK) void mlp_rows_kernel(RowsArgs a, const float* __restrict__ img,
+// 2 waves/SIMD only where the allocator fits 256 registers without spilling (VFLOSS)
+__global__ __launch_bounds__(ROWS_BLOCK, EPI == MRL_EPI_VFLOSS ? 2 : 1) void mlp_rows_kernel(RowsArgs a, const float* __restrict__ img,
                                                                const float* __restrict__ imgt,
                                                                const int32_t* __restrict__ skip) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -453,12 +454,37 @@ __global__ void reduce_rows_kernel(const T* __restrict__ slab, int64_t rows, int
   if (skip != nullptr && *skip != 0) return;
   const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int64_t col = (int64_t)blockIdx.x * 64 + c;
-  double s = 0.0;
-  if (col < cols)
-    for (int64_t r = g; r < rows; r += 4) s += (double)slab[r * cols + col];
-  part[g][c] = s;
+  // 8 independent accumulators keep 8 loads in flight per lane (latency-bound otherwise)
+  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (col < cols) {
+    int64_t r = g;
+    for (; r + 28 < rows; r += 32) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += (double)slab[(r + 4 * q) * cols + col];
+    }
+    for (; r < rows; r += 4) s[0] += (double)slab[r * cols + col];
+  }
+  part[g][c] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
   if (g == 0 && col < cols) out[col] = (O)(((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]);
+}
+
+// few columns (per-wave loss partials): one block per column, 256 threads over rows
+template <class T, class O>
+__global__ void reduce_rows_narrow_kernel(const T* __restrict__ slab, int64_t rows, int64_t cols, O* __restrict__ out,
+                                          const int32_t* __restrict__ skip) {
+  __shared__ double red[256];
+  if (skip != nullptr && *skip != 0) return;
+  const int64_t col = blockIdx.x;
+  double s = 0.0;
+  for (int64_t r = threadIdx.x; r < rows; r += 256) s += (double)slab[r * cols + col];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[col] = (O)red[0];
 }
 
 }  // namespace mrl
@@ -624,8 +650,12 @@ int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* 
                         void* stream) {
   if (!slab || !out) return fail(E_ARG, "null pointer");
   if (cols <= 0) return OK;
-  hipLaunchKernelGGL((reduce_rows_kernel<double, double>), dim3(ceil_div(cols, 64)), dim3(256), 0, (hipStream_t)stream,
-                     slab, rows, cols, out, skip);
+  if (cols <= 16)
+    hipLaunchKernelGGL((reduce_rows_narrow_kernel<double, double>), dim3(cols), dim3(256), 0, (hipStream_t)stream,
+                       slab, rows, cols, out, skip);
+  else
+    hipLaunchKernelGGL((reduce_rows_kernel<double, double>), dim3(ceil_div(cols, 64)), dim3(256), 0,
+                       (hipStream_t)stream, slab, rows, cols, out, skip);
   return hip_check(hipGetLastError(), "mrl_reduce_rows_f64");
 }
 

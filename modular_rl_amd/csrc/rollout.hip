@@ -67,21 +67,30 @@ __device__ inline void reset_env(const RollArgs& a, int e, double* s) {
   a.b.env_int[e] = 0;
 }
 
-// per-block Welford partial of vals[ENVS_PER_BLOCK][D] (doubles in LDS)
+// sum over the 16 lanes of an aligned 16-lane group (fixed butterfly order)
+__device__ inline double sum16(double v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// per-block two-pass (mean, M2) partial of vals[ENVS_PER_BLOCK][D] (doubles in LDS):
+// thread (k = tid/16, j = tid%16) covers envs j, j+16, ...; 16-lane butterflies.
 __device__ inline void publish_partial(const RollArgs& a, const double* vals, int nvalid, int D, bool with_rew,
                                        double* rec_out) {
-  const int k = threadIdx.x;
-  if (k < D) {
-    double mean = 0.0, m2 = 0.0;
-    if (nvalid > 0) {
-      double s = 0.0;
-      for (int i = 0; i < nvalid; ++i) s += vals[i * D + k];
-      mean = s / (double)nvalid;
-      for (int i = 0; i < nvalid; ++i) {
-        const double dv = vals[i * D + k] - mean;
-        m2 += dv * dv;
-      }
+  const int k = threadIdx.x >> 4, j = threadIdx.x & 15;
+  double s = 0.0;
+  if (k < D)
+    for (int i = j; i < nvalid; i += 16) s += vals[i * D + k];
+  const double mean = nvalid > 0 ? sum16(s) / (double)nvalid : 0.0;
+  double m2 = 0.0;
+  if (k < D)
+    for (int i = j; i < nvalid; i += 16) {
+      const double dv = vals[i * D + k] - mean;
+      m2 += dv * dv;
     }
+  m2 = sum16(m2);
+  if (k < D && j == 0) {
     double* r = rec_out + (int64_t)blockIdx.x * a.RS;
     r[2 + k] = mean;
     r[2 + D + k] = m2;
@@ -90,6 +99,36 @@ __device__ inline void publish_partial(const RollArgs& a, const double* vals, in
       r[1] = with_rew ? (double)nvalid : 0.0;
     }
   }
+}
+
+// combine the per-block records of one column k into a batch (n, mean, M2):
+// mean = sum n_b mean_b / n ; M2 = sum (M2_b + n_b (mean_b - mean)^2).
+// Called by all 16 lanes of thread group k; every lane returns the same values.
+__device__ inline void batch_of_records(const double* rec, int nb, int RS, int D, int O, int k, int j, double& bn,
+                                        double& bm, double& bs) {
+  const bool isr = (k == O);
+  double n = 0.0, sm = 0.0;
+  for (int b = j; b < nb; b += 16) {
+    const double* r = rec + (int64_t)b * RS;
+    const double nb_ = r[isr ? 1 : 0];
+    n += nb_;
+    sm += nb_ * r[2 + k];
+  }
+  n = sum16(n);
+  sm = sum16(sm);
+  const double mean = n > 0.0 ? sm / n : 0.0;
+  double m2 = 0.0;
+  for (int b = j; b < nb; b += 16) {
+    const double* r = rec + (int64_t)b * RS;
+    const double nb_ = r[isr ? 1 : 0];
+    if (nb_ > 0.0) {
+      const double dm = r[2 + k] - mean;
+      m2 += r[2 + D + k] + nb_ * dm * dm;
+    }
+  }
+  bn = n;
+  bm = mean;
+  bs = sum16(m2);
 }
 
 // Chan merge of (nb, mb, m2b) into (n, M, S); for nb == 1 this is RunningStat.push
@@ -138,24 +177,22 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, MlpDims md
   double* fs_out = a.b.filter_state + ((t + 1) & 1) * a.FS;
   const double* rec_in = a.b.records + (int64_t)(t & 1) * a.nb * a.RS;
   double* rec_out = a.b.records + (int64_t)((t + 1) & 1) * a.nb * a.RS;
-  if ((int)threadIdx.x < D) {
-    const int k = threadIdx.x;
+  if ((int)(threadIdx.x >> 4) < D) {
+    const int k = threadIdx.x >> 4, j = threadIdx.x & 15;
     const bool isr = (k == O);
     double n = fs_in[isr ? 1 : 0], M = fs_in[2 + k], S = fs_in[2 + D + k];
-    // combine the block partials in block order, then merge the batch
-    double bn = 0.0, bm = 0.0, bs = 0.0;
-    for (int b = 0; b < a.nb; ++b) {
-      const double* r = rec_in + (int64_t)b * a.RS;
-      chan_merge(bn, bm, bs, r[isr ? 1 : 0], r[2 + k], r[2 + D + k]);
-    }
+    // combine the block partials into one batch, then one Chan merge into the stat
+    double bn, bm, bs;
+    batch_of_records(rec_in, a.nb, a.RS, D, O, k, j, bn, bm, bs);
     chan_merge(n, M, S, bn, bm, bs);
-    if (blockIdx.x == 0) {
+    if (j != 0) {
+    } else if (blockIdx.x == 0) {
       if (k == 0) fs_out[0] = n;
       if (isr) fs_out[1] = n;
       fs_out[2 + k] = M;
       fs_out[2 + D + k] = S;
     }
-    if (!isr) {
+    if (!isr && j == 0) {
       const double var = n > 1.0 ? S / (n - 1.0) : M * M;  // running_stat.py:27
       fmean[k] = M;
       fden[k] = sqrt(var) + 1e-8;
@@ -295,7 +332,7 @@ __global__ void rollout_finish_kernel(RollArgs a) {
   const double* fs_in = a.b.filter_state + (T & 1) * a.FS;
   double* fs_out = a.b.filter_state;
   const double* rec_in = a.b.records + (int64_t)(T & 1) * a.nb * a.RS;
-  const int k = threadIdx.x;
+  const int k = threadIdx.x >> 4, j = threadIdx.x & 15;
   const bool isr = (k == O);
   double n = 0.0, M = 0.0, S = 0.0;
   if (k < D) {
@@ -303,16 +340,13 @@ __global__ void rollout_finish_kernel(RollArgs a) {
     M = fs_in[2 + k];
     S = fs_in[2 + D + k];
     if (isr) {  // the last step's rewards still go through rewfilt (core.py:199)
-      double bn = 0.0, bm = 0.0, bs = 0.0;
-      for (int b = 0; b < a.nb; ++b) {
-        const double* r = rec_in + (int64_t)b * a.RS;
-        chan_merge(bn, bm, bs, r[1], r[2 + k], r[2 + D + k]);
-      }
+      double bn, bm, bs;
+      batch_of_records(rec_in, a.nb, a.RS, D, O, k, j, bn, bm, bs);
       chan_merge(n, M, S, bn, bm, bs);
     }
   }
   __syncthreads();  // fs_in may alias fs_out (T even)
-  if (k < D) {
+  if (k < D && j == 0) {
     if (k == 0) fs_out[0] = n;
     if (isr) fs_out[1] = n;
     fs_out[2 + k] = M;
@@ -382,7 +416,7 @@ int mrl_rollout_finish(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, voi
   int rc = check_roll(d, b);
   if (rc) return rc;
   RollArgs a = make_args(d, b);
-  hipLaunchKernelGGL(rollout_finish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(rollout_finish_kernel, dim3(1), dim3(RB), 0, (hipStream_t)stream, a);
   return hip_check(hipGetLastError(), "mrl_rollout_finish");
 }
 

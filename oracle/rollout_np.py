@@ -62,15 +62,22 @@ def _block_partials(vals):
     return out
 
 
+def _batch(recs, col_sel, count_of):
+    """Combine block records into one batch: n = sum n_b, mean = sum n_b mean_b / n,
+    M2 = sum (M2_b + n_b (mean_b - mean)^2) -- the parallel form of Chan's merge."""
+    n = sum(count_of(r) for r in recs)
+    if n <= 0:
+        return 0.0, 0.0, 0.0
+    mean = sum(count_of(r) * col_sel(r[1]) for r in recs) / n
+    m2 = sum(col_sel(r[2]) + count_of(r) * (col_sel(r[1]) - mean) ** 2 for r in recs if count_of(r) > 0)
+    return n, mean, m2
+
+
 def _merge_records(fs, recs, with_obs=True, with_rew=True):
     D = len(fs.M)
     O = D - 1
-    bn, bm, bs = 0.0, np.zeros(D), np.zeros(D)
-    bnr, bmr, bsr = 0.0, 0.0, 0.0
-    for (n, mean, m2, has_rew) in recs:
-        bn, bm, bs = _merge(bn, bm, bs, n, mean, m2)
-        if has_rew:
-            bnr, bmr, bsr = _merge(bnr, bmr, bsr, n, mean[O], m2[O])
+    bn, bm, bs = _batch(recs, lambda v: v, lambda r: r[0])
+    bnr, bmr, bsr = _batch(recs, lambda v: v[O], lambda r: r[0] if r[3] else 0.0)
     if with_obs:
         n, M, S = _merge(fs.n, fs.M[:O], fs.S[:O], bn, bm[:O], bs[:O])
         fs.n, fs.M[:O], fs.S[:O] = n, M, S
