@@ -110,8 +110,8 @@ class TrpoAgent(AgentWithPolicy):
         limit = int(timestep_limit or cfg["timestep_limit"] or env.spec.max_episode_steps)
         key = (env.spec.id, E, T, limit)
         if key not in self._collectors:
-            col = Collector(env, self.policy, E, T, limit, filter=cfg["filter"], seed=self.seed, comm=self.comm,
-                            use_graph=bool(cfg.get("use_graph", 1)))
+            col = Collector(env, self.policy, E, T, limit, filter=self.cfg["filter"], seed=self.seed, comm=self.comm,
+                            use_graph=bool(cfg.get("use_graph", self.cfg.get("use_graph", 1))))
             shared = self._filter_owner()
             if shared is not None:  # one running stat per agent
                 col.filter_state = shared.filter_state

@@ -27,6 +27,47 @@ from ._lib import call, ptr, stream
 from .dist import Comm
 
 
+def merge_filter_deltas(s0, s1, comm):
+    """Per-iteration cross-rank merge of the running stats.  Every rank started the
+    iteration from the same state s0 = [n_obs, n_rew, M[D], S[D]] and ended at its
+    local s1 = s0 (+) its own pushes.  Each rank's delta (n, mean, M2) is recovered by
+    inverting Chan's formula, all deltas are gathered and merged into s0 in rank
+    order, so all ranks leave with the identical global statistics."""
+    FS = len(s0)
+    D = (FS - 2) // 2
+    delta = np.zeros(FS)
+    for which, cols in ((0, range(D - 1)), (1, [D - 1])):
+        n0, n1 = s0[which], s1[which]
+        nd = n1 - n0
+        delta[which] = nd
+        if nd <= 0:
+            continue
+        for k in cols:
+            M0, M1, S0, S1 = s0[2 + k], s1[2 + k], s0[2 + D + k], s1[2 + D + k]
+            md = (n1 * M1 - n0 * M0) / nd
+            delta[2 + k] = md
+            delta[2 + D + k] = S1 - S0 - (md - M0) ** 2 * n0 * nd / n1
+    dev = "cuda" if comm.enabled and torch.distributed.get_backend() == "nccl" else "cpu"
+    all_d = comm.allgather(torch.as_tensor(delta).to(dev))
+    out = np.array(s0, dtype=np.float64).copy()
+    for d in all_d:
+        d = d.cpu().numpy()
+        for which, cols in ((0, range(D - 1)), (1, [D - 1])):
+            nb = d[which]
+            if nb <= 0:
+                continue
+            n = out[which] + nb
+            for k in cols:
+                M, S = out[2 + k], out[2 + D + k]
+                mb, m2b = d[2 + k], d[2 + D + k]
+                dl = mb - M
+                newM = M + (dl * nb) / n
+                out[2 + D + k] = S + m2b + dl * (mb - newM) * nb
+                out[2 + k] = newM
+            out[which] = n
+    return out
+
+
 class Batch:
     """Device-resident batch of N = T*E time-major rows (row n = t*E + e)."""
 
@@ -158,40 +199,9 @@ class Collector:
 
     # ------------------------------------------------------------ filter state
     def _merge_filter_across_ranks(self, fs_start):
-        """Per-iteration Chan merge of every rank's running-stat delta, in rank order."""
-        D = (self.FS - 2) // 2
         s0 = fs_start.double().cpu().numpy()
         s1 = self.filter_state[:self.FS].double().cpu().numpy()
-        delta = np.zeros(self.FS)
-        for which, cols in ((0, range(D - 1)), (1, [D - 1])):
-            n0, n1 = s0[which], s1[which]
-            nd = n1 - n0
-            delta[which] = nd
-            for k in cols:
-                M0, M1, S0, S1 = s0[2 + k], s1[2 + k], s0[2 + D + k], s1[2 + D + k]
-                if nd > 0:
-                    md = (n1 * M1 - n0 * M0) / nd
-                    delta[2 + k] = md
-                    delta[2 + D + k] = S1 - S0 - (md - M0) ** 2 * n0 * nd / n1
-        dev = "cuda" if self.comm.enabled and torch.distributed.get_backend() == "nccl" else "cpu"
-        all_d = self.comm.allgather(torch.as_tensor(delta).to(dev))
-        out = s0.copy()
-        for d in all_d:
-            d = d.cpu().numpy()
-            for which, cols in ((0, range(D - 1)), (1, [D - 1])):
-                nb = d[which]
-                if nb <= 0:
-                    continue
-                na = out[which]
-                n = na + nb
-                for k in cols:
-                    M, S = out[2 + k], out[2 + D + k]
-                    mb, m2b = d[2 + k], d[2 + D + k]
-                    delta_ = mb - M
-                    newM = M + (delta_ * nb) / n
-                    out[2 + D + k] = S + m2b + delta_ * (mb - newM) * nb
-                    out[2 + k] = newM
-                out[which] = n
+        out = merge_filter_deltas(s0, s1, self.comm)
         self.filter_state[:self.FS].copy_(torch.as_tensor(out))
 
     def filter_stats(self):

@@ -1,4 +1,5 @@
 import os
+import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -8,3 +9,7 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP library + device)")
+    # the HIP library is a build artefact (git-ignored): build it in-tree if absent
+    lib = os.path.join(ROOT, "modular_rl_amd", "libmrl_hip.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-C", ROOT, "-j8"], check=True, stdout=subprocess.DEVNULL)

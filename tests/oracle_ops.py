@@ -1,0 +1,95 @@
+"""Oracle-backed stand-in for modular_rl_amd.trpo.HipTrpoOps -- TEST ONLY.
+
+Lets the real TrpoUpdater.update orchestration (collective placement, global-N
+scaling, CG control flow, line search) run on CPU under gloo: every device
+kernel the updater calls is replaced by the float64 numpy oracle on this rank's
+local rows, returning LOCAL sums scaled by 1/N_global exactly like the kernels.
+"""
+import types
+
+import numpy as np
+import torch
+
+from oracle import trpo_np as T
+
+
+def fake_policy(spec, theta):
+    net = types.SimpleNamespace(theta=torch.tensor(theta, dtype=torch.float64), pack=lambda *a, **k: None,
+                                device=torch.device("cpu"), P=spec.P)
+    return types.SimpleNamespace(net=net, get_flat=lambda: net.theta.numpy().copy(),
+                                 set_from_flat=lambda th: net.theta.copy_(torch.as_tensor(th)))
+
+
+class OracleOps:
+    def __init__(self, spec, net):
+        self.spec, self.net, self.P = spec, net, spec.P
+        z = lambda: torch.zeros(self.P, dtype=torch.float64)  # noqa: E731
+        self.x, self.r, self.p, self.p32, self.fullstep, self.cand = z(), z(), z(), z(), z(), z()
+        self.state = torch.zeros(4, dtype=torch.float64)
+        self.flag = torch.zeros(2, dtype=torch.int32)
+        self.fv = z()
+
+    def bind(self, batch, inv_ng):
+        self.b, self.inv_ng = batch, inv_ng
+
+    def _scale(self):
+        return self.b.n * self.inv_ng  # oracle divides by local n; kernels by N_global
+
+    def surrgrad(self):
+        b, th = self.b, self.net.theta.numpy()
+        g = T.policy_gradient(self.spec, th, b.obs, b.act, b.adv, b.prob) * self._scale()
+        return torch.tensor(g), self.losses(self.net.theta)
+
+    def losses(self, theta):
+        b = self.b
+        s, kl, ent = T.surr_kl_ent(self.spec, theta.numpy(), b.obs, b.act, b.adv, b.prob)
+        return torch.tensor([-s * b.n, kl * b.n, ent * b.n, 0.0])
+
+    def fvp(self, v, skip=None):
+        if skip is not None and int(skip[0]) != 0:
+            return self.fv
+        fv = T.fisher_vector_product(self.spec, self.net.theta.numpy(), v.numpy(), self.b.obs) * self._scale()
+        self.fv = torch.tensor(fv)
+        return self.fv
+
+    def neg_g64(self, g):
+        return -g.double()
+
+    def cg_init(self, b):
+        self.x.zero_()
+        self.r.copy_(b)
+        self.p.copy_(b)
+        self.p32.copy_(b)
+        self.state[0] = float(b.dot(b))
+        self.state[2] = 0
+        self.flag[0] = 0
+
+    def cg_update(self, fv, damping, tol):
+        if int(self.flag[0]) != 0:
+            return
+        rdotr = float(self.state[0])
+        z = fv + damping * self.p
+        v = rdotr / float(self.p.dot(z))
+        self.x += v * self.p
+        self.r -= v * z
+        newr = float(self.r.dot(self.r))
+        self.p.copy_(self.r + (newr / rdotr) * self.p)
+        self.p32.copy_(self.p)
+        self.state[0] = newr
+        self.state[2] += 1
+        if newr < tol:
+            self.flag[0] = 1
+
+    def stepdir32(self):
+        return self.x.clone()
+
+    def trpo_step(self, fv, g, damping, max_kl):
+        shs = 0.5 * float(self.x.dot(fv + damping * self.x))
+        lm = np.sqrt(shs / max_kl)
+        self.fullstep.copy_(self.x / lm)
+        ngx = -float(g.double().dot(self.x))
+        return torch.tensor([shs, lm, ngx, ngx / lm])
+
+    def candidate(self, theta_old, frac):
+        self.cand.copy_(theta_old + frac * self.fullstep)
+        return self.cand

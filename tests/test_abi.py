@@ -1,0 +1,100 @@
+"""The C-ABI boundary without a GPU: libmrl_hip.so loads, exports every function
+include/mrl_hip.h declares, the ctypes binding matches the C struct layouts
+(compiled probe with gcc), host-only queries answer, and the product path refuses
+to run without a GPU (no CPU fallback)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mrl_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mrl_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from modular_rl_amd import _lib
+    lib = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 30
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (mrl_[a-z0-9_]+)", nm))
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    unbound = [n for n in names if n not in _lib.SIGNATURES]
+    assert not unbound, unbound
+    for n in names:
+        assert getattr(lib, n) is not None
+
+
+def test_ctypes_struct_layout_matches_c(tmp_path):
+    from modular_rl_amd import _lib
+    probe = tmp_path / "probe.c"
+    probe.write_text("""
+#include <stdio.h>
+#include <stddef.h>
+#include "mrl_hip.h"
+#define P(T, F) printf(#T "." #F " %zu\\n", offsetof(T, F));
+int main(void) {
+  printf("mrl_mlp_desc %zu\\nmrl_rows_io %zu\\nmrl_rollout_desc %zu\\nmrl_rollout_bufs %zu\\n",
+         sizeof(mrl_mlp_desc), sizeof(mrl_rows_io), sizeof(mrl_rollout_desc), sizeof(mrl_rollout_bufs));
+  P(mrl_rows_io, timestep_limit) P(mrl_rows_io, n) P(mrl_rows_io, inv_n_global) P(mrl_rows_io, partial)
+  P(mrl_rollout_desc, seed) P(mrl_rollout_bufs, noise)
+  return 0;
+}
+""")
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(probe), "-o", str(exe)], check=True)
+    out = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split("\n") if l)
+    assert int(out["mrl_mlp_desc"]) == ctypes.sizeof(_lib.MlpDesc)
+    assert int(out["mrl_rows_io"]) == ctypes.sizeof(_lib.RowsIO)
+    assert int(out["mrl_rollout_desc"]) == ctypes.sizeof(_lib.RolloutDesc)
+    assert int(out["mrl_rollout_bufs"]) == ctypes.sizeof(_lib.RolloutBufs)
+    assert int(out["mrl_rows_io.timestep_limit"]) == _lib.RowsIO.timestep_limit.offset
+    assert int(out["mrl_rows_io.n"]) == _lib.RowsIO.n.offset
+    assert int(out["mrl_rows_io.inv_n_global"]) == _lib.RowsIO.inv_n_global.offset
+    assert int(out["mrl_rows_io.partial"]) == _lib.RowsIO.partial.offset
+    assert int(out["mrl_rollout_desc.seed"]) == _lib.RolloutDesc.seed.offset
+    assert int(out["mrl_rollout_bufs.noise"]) == _lib.RolloutBufs.noise.offset
+
+
+def test_host_queries_match_the_reference_parameter_layout():
+    from modular_rl_amd import _lib
+    from oracle import trpo_np as T
+    lib = _lib.load()
+    for (n_in, n_out, head, name) in [(11, 3, _lib.HEAD_GAUSS, "gauss"), (4, 2, _lib.HEAD_SOFTMAX, "softmax"),
+                                      (12, 1, _lib.HEAD_LINEAR, "linear")]:
+        d = _lib.MlpDesc(n_in, n_out, head, 64, 2)
+        assert lib.mrl_mlp_num_params(ctypes.byref(d)) == T.Spec(n_in, [64, 64], n_out, name).P
+        assert lib.mrl_mlp_image_floats(ctypes.byref(d)) > 0
+    # Hopper 5,126 / CartPole 4,610 / VF 5,057 params
+    assert lib.mrl_mlp_num_params(ctypes.byref(_lib.MlpDesc(11, 3, _lib.HEAD_GAUSS, 64, 2))) == 5126
+    bad = _lib.MlpDesc(11, 3, _lib.HEAD_GAUSS, 128, 2)
+    assert lib.mrl_mlp_num_params(ctypes.byref(bad)) < 0
+    assert b"hid_sizes" in lib.mrl_last_error()
+    assert lib.mrl_env_state_doubles(_lib.ENV_HOPPER) == 12
+    assert lib.mrl_filter_doubles(_lib.ENV_CARTPOLE) == 2 + 2 * 5
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU refusal")
+def test_product_path_refuses_without_gpu():
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import MlpNet
+    with pytest.raises(_lib.MrlError):
+        MlpNet(11, 3, _lib.HEAD_GAUSS)
+
+
+def test_unsupported_hidden_sizes_fail_loudly():
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import check_hid_sizes
+    check_hid_sizes([64, 64])
+    with pytest.raises(_lib.MrlError):
+        check_hid_sizes([128, 128])

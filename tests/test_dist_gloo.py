@@ -1,0 +1,108 @@
+"""Data-parallel orchestration on CPU with torch.distributed gloo, world_size 2.
+
+* TrpoUpdater.update with the rows split over 2 ranks takes the same step as one
+  rank holding all rows, and as the float64 oracle (the collectives are placed and
+  scaled correctly: g, every CG Fvp, loss sums, line-search losses).
+* merge_filter_deltas: 2 ranks pushing different observations from a common start
+  end with the running stat of one process pushing all of them (rank order).
+"""
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import trpo_np as T
+
+
+def _data(seed=0, N=600):
+    rng = np.random.default_rng(seed)
+    spec = T.Spec(11, [64, 64], 3, "gauss")
+    th = T.mlp_init(rng, spec.shapes, True) + 0.02 * rng.standard_normal(spec.P)
+    ob = rng.standard_normal((N, 11))
+    oldprob = T.policy_prob(spec, th + 0.01 * rng.standard_normal(spec.P), ob)
+    act = T.sample(spec, oldprob, rng.standard_normal((N, 3)))
+    adv = T.standardize(rng.standard_normal(N) + 0.4 * ob[:, 1])
+    return spec, th, ob, act, adv, oldprob
+
+
+def _update(rank_rows, comm):
+    from modular_rl_amd.trpo import TrpoUpdater
+    from tests.oracle_ops import OracleOps, fake_policy
+    spec, th, ob, act, adv, oldprob = _data()
+    sl = rank_rows
+    pol = fake_policy(spec, th)
+    up = TrpoUpdater(pol, dict(cg_damping=0.1, max_kl=0.01), comm=comm, ops=OracleOps(spec, pol.net))
+    b = types.SimpleNamespace(n=len(ob[sl]), obs=ob[sl], act=act[sl], adv=adv[sl], prob=oldprob[sl])
+    stats = up.update(b)
+    return pol.net.theta.numpy().copy(), stats, up.last_diag
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from modular_rl_amd.collector import merge_filter_deltas
+    from modular_rl_amd.dist import Comm
+    comm = Comm()
+    N = 600
+    rows = slice(rank * N // world, (rank + 1) * N // world)
+    th, stats, diag = _update(rows, comm)
+    # filter merge: common start state (from pushes of `pre`), then rank-local pushes
+    rng = np.random.default_rng(1)
+    pre = rng.standard_normal((30, 4)) * 2 + 1
+    local = [rng.standard_normal((17 + 5 * r, 4)) * (r + 1) for r in range(world)]
+    lrew = [rng.standard_normal(17 + 5 * r) for r in range(world)]
+    rs, rr = T.RunningStat((4,)), T.RunningStat(())
+    for x in pre:
+        rs.push(x)
+        rr.push(x[0])
+    s0 = np.concatenate([[rs.n, rr.n], np.append(rs.M, rr.M), np.append(rs.S, rr.S)])
+    for x, r in zip(local[rank], lrew[rank]):
+        rs.push(x)
+        rr.push(r)
+    s1 = np.concatenate([[rs.n, rr.n], np.append(rs.M, rr.M), np.append(rs.S, rr.S)])
+    merged = merge_filter_deltas(s0, s1, comm)
+    if rank == 0:
+        q.put((th, dict(stats), diag["k"], merged))
+    dist.destroy_process_group()
+
+
+def test_two_rank_update_equals_single_rank_and_oracle():
+    from modular_rl_amd.dist import Comm
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    th2, stats2, k2, merged = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    th1, stats1, diag1 = _update(slice(0, 600), Comm())
+    spec, th, ob, act, adv, oldprob = _data()
+    th_w, stats_w, diag_w = T.trpo_update(spec, th, ob, act, adv, oldprob, cg_damping=0.1, max_kl=0.01)
+    step = np.abs(th_w - th).max()
+    assert np.abs(th2 - th1).max() <= 1e-9 * step
+    assert np.abs(th1 - th_w).max() <= 1e-9 * step
+    assert k2 == diag1["k"] == diag_w["k"]
+    for k in stats_w:
+        np.testing.assert_allclose(stats2[k], stats_w[k], rtol=1e-9, atol=1e-13)
+    # filter: all pushes in rank order from the common start
+    rng = np.random.default_rng(1)
+    pre = rng.standard_normal((30, 4)) * 2 + 1
+    local = [rng.standard_normal((17 + 5 * r, 4)) * (r + 1) for r in range(2)]
+    lrew = [rng.standard_normal(17 + 5 * r) for r in range(2)]
+    rs, rr = T.RunningStat((4,)), T.RunningStat(())
+    for x in pre:
+        rs.push(x)
+        rr.push(x[0])
+    for r in range(2):
+        for x, rw in zip(local[r], lrew[r]):
+            rs.push(x)
+            rr.push(rw)
+    want = np.concatenate([[rs.n, rr.n], np.append(rs.M, rr.M), np.append(rs.S, rr.S)])
+    np.testing.assert_allclose(merged, want, rtol=1e-10, atol=1e-10)

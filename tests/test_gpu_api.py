@@ -1,0 +1,75 @@
+"""End-to-end use of the reference-shaped API on the GPU: run_pg.py's loop,
+TrpoAgent's per-path methods, and learning progress on CartPole."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import trpo_np as T
+
+pytestmark = pytest.mark.gpu
+
+
+def _agent(env_id, **kw):
+    from modular_rl_amd.agentzoo import TrpoAgent
+    from modular_rl_amd.envs import make
+    env = make(env_id)
+    cfg = dict(timestep_limit=env.spec.max_episode_steps, gamma=0.99, lam=0.97, max_kl=0.01, cg_damping=0.1,
+               n_envs=128, horizon=200, seed=1)
+    cfg.update(kw)
+    return env, TrpoAgent(env.observation_space, env.action_space, cfg), cfg
+
+
+def test_run_policy_gradient_algorithm_learns_cartpole():
+    from modular_rl_amd.core import run_policy_gradient_algorithm
+    env, agent, cfg = _agent("CartPole-v0", n_iter=12)
+    seen = []
+    run_policy_gradient_algorithm(env, agent, usercfg=cfg, callback=seen.append)
+    assert len(seen) == 12
+    for k in ("EpRewMean", "EpLenMean", "NumEpBatch", "vf_loss_before", "vf_EV_after", "pol_surr_before",
+              "pol_kl_after", "pol_ent_after", "TimeElapsed"):
+        assert k in seen[-1]
+    assert all(s["pol_kl_after"] <= 2.0 * 0.01 for s in seen)  # trust region held
+    assert seen[-1]["EpRewMean"] > 1.5 * seen[0]["EpRewMean"], (seen[0]["EpRewMean"], seen[-1]["EpRewMean"])
+
+
+def test_run_pg_cli_hopper_two_iterations(capsys):
+    import run_pg
+    run_pg.main(["--env", "Hopper-v2", "--n_iter", "2", "--n_envs", "256", "--horizon", "64", "--json",
+                 "--gamma", "0.995", "--lam", "0.97"])
+    lines = [l for l in capsys.readouterr().out.splitlines() if l.startswith("{")]
+    assert len(lines) == 2
+
+
+def test_per_path_api_matches_oracle():
+    """agent.updater(paths) / compute_advantage(vf, paths) on reference-style path dicts."""
+    from modular_rl_amd.core import compute_advantage, do_rollouts_serial
+    env, agent, cfg = _agent("CartPole-v0")
+    import itertools
+    paths = do_rollouts_serial(env, agent, 200, 300, itertools.count())
+    assert sum(len(p["reward"]) for p in paths) > 300 and all(p["terminated"] or len(p["reward"]) == 200 for p in paths)
+    vf_th = agent.baseline.net.get_flat().astype(np.float64)
+    compute_advantage(agent.baseline, paths, 0.99, 0.97)
+    vspec = T.Spec(5, [64, 64], 1, "linear")
+    ref = [dict(reward=p["reward"], terminated=p["terminated"], observation=p["observation"]) for p in paths]
+
+    def pred(p):
+        X = np.concatenate([p["observation"].astype(np.float64),
+                            (np.arange(len(p["observation"])) / 200.0).astype(np.float32).astype(np.float64)[:, None]], 1)
+        return T.mlp_forward(vspec, vf_th, X)[0][:, 0]
+
+    T.compute_advantage(pred, ref, 0.99, 0.97)
+    for p, r in zip(paths, ref):
+        np.testing.assert_allclose(p["advantage"], r["advantage"], rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(p["return"], r["return"], rtol=1e-5, atol=1e-4)
+    spec = T.Spec(4, [64, 64], 2, "softmax")
+    th0 = agent.get_flat().astype(np.float64)
+    cat = np.concatenate
+    th_w, st_w, dg_w = T.trpo_update(spec, th0, cat([p["observation"] for p in paths]).astype(np.float64),
+                                     cat([p["action"] for p in paths]), cat([p["advantage"] for p in paths]),
+                                     cat([p["prob"] for p in paths]).astype(np.float64), cg_damping=0.1, max_kl=0.01)
+    stats = agent.updater(paths)
+    assert agent.updater.last_diag["k"] == dg_w["k"]
+    np.testing.assert_allclose(stats["kl_after"], st_w["kl_after"], rtol=5e-3)
+    ob = torch.as_tensor(np.zeros(4, np.float32))
+    a, info = agent.act(ob.numpy())
+    assert a in (0, 1) and info["prob"].shape == (2,)
