@@ -4,6 +4,10 @@
 #pragma once
 #include "mlp_layout.h"
 
+// Cross-lane hand-off through LDS inside ONE wave: a wave's LDS instructions execute
+// in issue order, so only the compiler must be kept from moving loads above stores.
+#define WAVE_LDS_ORDER() asm volatile("" ::: "memory")
+
 namespace mrl {
 
 // ------------------------------------------------------------------ device helpers
@@ -103,8 +107,141 @@ __device__ inline void tanh16(f32x16& a) {
   for (int r = 0; r < 16; ++r) a[r] = tanh_fast(a[r]);
 }
 
+// Head (A <= 8 outputs) on VALU: a 32-wide MFMA tile would be >= 75 % padding.
+// Lane half h holds 32 of the 64 units of its row; z[o] += sum_i hv[h][o][i]*src_i
+// (broadcast ds_read_b128 within the half); head_finish adds the other half and the
+// bias, so every lane of the row ends with all outputs.
+__device__ inline void head_partial(const float* lds, const MlpDims& d, const f32x16* src, int h, float* z) {
+  const float* w = lds + d.hv + h * (MAX_OUT * 32);
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    if (o < d.A) {
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float4 wv = ld4(w + o * 32 + 4 * q);
+        const int mt = q >> 2, r0 = 4 * (q & 3);
+        acc += wv.x * src[mt][r0] + wv.y * src[mt][r0 + 1] + wv.z * src[mt][r0 + 2] + wv.w * src[mt][r0 + 3];
+      }
+      z[o] += acc;
+    }
+  }
+}
+
+__device__ inline void head_finish(const float* lds, const MlpDims& d, float* z) {
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o)
+    if (o < d.A) z[o] = (z[o] + __shfl_xor(z[o], 32)) + lds[d.hb + o];
+}
+
+// head partial from ONE 32-unit M-tile (mt) of a layer-2 activation
+__device__ inline void head_partial_mt(const float* lds, const MlpDims& d, const f32x16& src, int mt, int h,
+                                       float* z) {
+  const float* w = lds + d.hv + h * (MAX_OUT * 32) + mt * 16;
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    if (o < d.A) {
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 wv = ld4(w + o * 32 + 4 * q);
+        acc += wv.x * src[4 * q] + wv.y * src[4 * q + 1] + wv.z * src[4 * q + 2] + wv.w * src[4 * q + 3];
+      }
+      z[o] += acc;
+    }
+  }
+}
+
+// acc += sum_s frag(seg, mo, s) * src[s>>4][s&15] for ONE output M-tile
+__device__ inline void chain1(const float* lds, int seg, int mo, const f32x16* src, int lane, f32x16& acc) {
+#pragma unroll
+  for (int s4 = 0; s4 < 8; ++s4) {
+    const float4 w = frag4(lds, seg, 32, mo, s4, lane);
+    const int s = 4 * s4;
+    acc = MFMA32(w.x, src[(s + 0) >> 4][(s + 0) & 15], acc);
+    acc = MFMA32(w.y, src[(s + 1) >> 4][(s + 1) & 15], acc);
+    acc = MFMA32(w.z, src[(s + 2) >> 4][(s + 2) & 15], acc);
+    acc = MFMA32(w.w, src[(s + 3) >> 4][(s + 3) & 15], acc);
+  }
+}
+
+// forward to the head outputs only, layer 2 one M-tile at a time (h2 never fully live)
+template <class XL>
+__device__ inline void forward_head_lowreg(const float* lds, const MlpDims& d, const XL& xl, int lane, float* z) {
+  const int h = lane >> 5;
+  f32x16 h1[2];
+  h1[0] = load_bias16(lds, d.fb0, 0, h);
+  h1[1] = load_bias16(lds, d.fb0, 1, h);
+  layer0(lds, d, xl, lane, h1);
+  tanh16(h1[0]);
+  tanh16(h1[1]);
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) z[o] = 0.f;
+#pragma unroll
+  for (int mo = 0; mo < 2; ++mo) {
+    f32x16 a = load_bias16(lds, d.fb1, mo, h);
+    chain1(lds, d.fa1, mo, h1, lane, a);
+    __builtin_amdgcn_sched_barrier(0);
+    tanh16(a);
+    head_partial_mt(lds, d, a, mo, h, z);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  head_finish(lds, d, z);
+}
+
+// forward + JVP to the head, layer 2 one M-tile at a time (peak: h1, dh1 + 2 tiles)
+template <class XL>
+__device__ inline void forward_jvp_head_lowreg(const float* lds, const float* ldt, const MlpDims& d, const XL& xl,
+                                               int lane, float* z, float* dz) {
+  const int h = lane >> 5;
+  f32x16 h1[2], dh1[2];
+  h1[0] = load_bias16(lds, d.fb0, 0, h);
+  h1[1] = load_bias16(lds, d.fb0, 1, h);
+  layer0(lds, d, xl, lane, h1);
+  dh1[0] = load_bias16(ldt, d.fb0, 0, h);
+  dh1[1] = load_bias16(ldt, d.fb0, 1, h);
+  layer0(ldt, d, xl, lane, dh1);
+  tanh16(h1[0]);
+  tanh16(h1[1]);
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dh1[m][r] *= (1.f - h1[m][r] * h1[m][r]);
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    z[o] = 0.f;
+    dz[o] = 0.f;
+  }
+  float dzt[MAX_OUT];
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) dzt[o] = 0.f;
+#pragma unroll
+  for (int mo = 0; mo < 2; ++mo) {
+    f32x16 a = load_bias16(lds, d.fb1, mo, h);
+    f32x16 da = load_bias16(ldt, d.fb1, mo, h);
+    // scheduling fences keep each chain's fragment prefetch within 32 registers
+    chain1(lds, d.fa1, mo, h1, lane, a);
+    __builtin_amdgcn_sched_barrier(0);
+    chain1(lds, d.fa1, mo, dh1, lane, da);
+    __builtin_amdgcn_sched_barrier(0);
+    chain1(ldt, d.fa1, mo, h1, lane, da);
+    __builtin_amdgcn_sched_barrier(0);
+    tanh16(a);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) da[r] *= (1.f - a[r] * a[r]);
+    head_partial_mt(lds, d, a, mo, h, z);
+    head_partial_mt(lds, d, da, mo, h, dz);
+    head_partial_mt(ldt, d, a, mo, h, dzt);
+  }
+  head_finish(lds, d, z);
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) dz[o] += dzt[o];
+  head_finish(ldt, d, dz);
+}
+
 struct Fwd {
-  f32x16 h1[2], h2[2], z;
+  f32x16 h1[2], h2[2];
+  float z[MAX_OUT];
 };
 
 template <bool HEAD, class XL>
@@ -121,48 +258,57 @@ __device__ inline void forward_tile(const float* lds, const MlpDims& d, const XL
   tanh16(f.h2[0]);
   tanh16(f.h2[1]);
   if (HEAD) {
-    f.z = load_bias16(lds, d.fb2, 0, h);
-    chain<1>(lds, d.fa2, f.h2, lane, &f.z);
+#pragma unroll
+    for (int o = 0; o < MAX_OUT; ++o) f.z[o] = 0.f;
+    head_partial(lds, d, f.h2, h, f.z);
+    head_finish(lds, d, f.z);
   }
 }
 
-// JVP along the tangent image `ldt` (same layout), primal activations in f
+// forward + JVP along the tangent image `ldt` (same layout), interleaved layer by
+// layer so h1/dh1 die before layer 2's accumulators are live.  Leaves h2 in f.h2,
+// the outputs in f.z and their directional derivative in dz.
 template <class XL>
-__device__ inline f32x16 jvp_tile(const float* lds, const float* ldt, const MlpDims& d, const XL& xl, int lane,
-                                  const Fwd& f) {
+__device__ inline void forward_jvp_tile(const float* lds, const float* ldt, const MlpDims& d, const XL& xl, int lane,
+                                        Fwd& f, float* dz) {
   const int h = lane >> 5;
-  f32x16 dh1[2], dh2[2];
-  dh1[0] = load_bias16(ldt, d.fb0, 0, h);
-  dh1[1] = load_bias16(ldt, d.fb0, 1, h);
-  layer0(ldt, d, xl, lane, dh1);
+  f32x16 dh[2];
+  f.h1[0] = load_bias16(lds, d.fb0, 0, h);
+  f.h1[1] = load_bias16(lds, d.fb0, 1, h);
+  layer0(lds, d, xl, lane, f.h1);
+  dh[0] = load_bias16(ldt, d.fb0, 0, h);
+  dh[1] = load_bias16(ldt, d.fb0, 1, h);
+  layer0(ldt, d, xl, lane, dh);
+  tanh16(f.h1[0]);
+  tanh16(f.h1[1]);
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dh1[m][r] *= (1.f - f.h1[m][r] * f.h1[m][r]);
-  dh2[0] = load_bias16(ldt, d.fb1, 0, h);
-  dh2[1] = load_bias16(ldt, d.fb1, 1, h);
-  chain<2>(lds, d.fa1, dh1, lane, dh2);
-  chain<2>(ldt, d.fa1, f.h1, lane, dh2);
+    for (int r = 0; r < 16; ++r) dh[m][r] *= (1.f - f.h1[m][r] * f.h1[m][r]);
+  f32x16 da[2];
+  f.h2[0] = load_bias16(lds, d.fb1, 0, h);
+  f.h2[1] = load_bias16(lds, d.fb1, 1, h);
+  chain<2>(lds, d.fa1, f.h1, lane, f.h2);
+  da[0] = load_bias16(ldt, d.fb1, 0, h);
+  da[1] = load_bias16(ldt, d.fb1, 1, h);
+  chain<2>(lds, d.fa1, dh, lane, da);
+  chain<2>(ldt, d.fa1, f.h1, lane, da);
+  tanh16(f.h2[0]);
+  tanh16(f.h2[1]);
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dh2[m][r] *= (1.f - f.h2[m][r] * f.h2[m][r]);
-  f32x16 dz = load_bias16(ldt, d.fb2, 0, h);
-  chain<1>(lds, d.fa2, dh2, lane, &dz);
-  chain<1>(ldt, d.fa2, f.h2, lane, &dz);
-  return dz;
-}
-
-// head outputs o < 8 live in register o&3 of lane half o>>2: give every lane all 8
-__device__ inline void head_gather(const f32x16& z, int lane, float* out) {
-  const int h = lane >> 5;
+    for (int r = 0; r < 16; ++r) da[m][r] *= (1.f - f.h2[m][r] * f.h2[m][r]);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float mine = z[r];
-    const float other = __shfl_xor(mine, 32);
-    out[r] = h ? other : mine;
-    out[4 + r] = h ? mine : other;
+  for (int o = 0; o < MAX_OUT; ++o) {
+    f.z[o] = 0.f;
+    dz[o] = 0.f;
   }
+  head_partial(lds, d, f.h2, h, f.z);
+  head_finish(lds, d, f.z);
+  head_partial(lds, d, da, h, dz);
+  head_partial(ldt, d, f.h2, h, dz);
+  head_finish(ldt, d, dz);
 }
 
 __device__ inline double wave_sum(double v) {

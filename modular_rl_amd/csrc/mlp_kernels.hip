@@ -64,8 +64,8 @@ constexpr float LOG2PI_F = 1.8378770664093453f;
 constexpr float LOG2PIE_F = 2.8378770664093453f;
 
 template <int EPI>
-// 2 waves/SIMD only where the allocator fits 256 registers without spilling (VFLOSS)
-__global__ __launch_bounds__(ROWS_BLOCK, EPI == MRL_EPI_VFLOSS ? 2 : 1) void mlp_rows_kernel(RowsArgs a, const float* __restrict__ img,
+// 2 waves/SIMD: layer 2 is evaluated one M-tile at a time so the chain fits 256 registers
+__global__ __launch_bounds__(ROWS_BLOCK, 2) void mlp_rows_kernel(RowsArgs a, const float* __restrict__ img,
                                                                const float* __restrict__ imgt,
                                                                const int32_t* __restrict__ skip) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -95,15 +95,9 @@ __global__ __launch_bounds__(ROWS_BLOCK, EPI == MRL_EPI_VFLOSS ? 2 : 1) void mlp
     const int64_t row = tile * 32 + (lane & 31);
     const bool valid = row < a.n;
     XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
-    Fwd f;
-    forward_tile<true>(lds, d, xl, lane, f);
-    float z[MAX_OUT];
-    head_gather(f.z, lane, z);
-    float dz[MAX_OUT];
-    if (EPI == MRL_EPI_FVP) {
-      const f32x16 dzt = jvp_tile(lds, ldt, d, xl, lane, f);
-      head_gather(dzt, lane, dz);
-    }
+    float z[MAX_OUT], dz[MAX_OUT];
+    if (EPI == MRL_EPI_FVP) forward_jvp_head_lowreg(lds, ldt, d, xl, lane, z, dz);
+    else forward_head_lowreg(lds, d, xl, lane, z);
     if (!valid || h != 0) continue;
 
     if (EPI == MRL_EPI_PROB) {
@@ -312,9 +306,7 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
 #pragma unroll
       for (int r = 0; r < 4; ++r) scrB[(r + 4 * h) * IMG_PAD + base] = G[r];
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    WAVE_LDS_ORDER();
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       const float4 bq = ld4(scrB + j * IMG_PAD + h * 16 + 4 * s4);
@@ -333,14 +325,10 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int r = 0; r < 16; ++r) g2[m][r] *= (1.f - f.h2[m][r] * f.h2[m][r]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    WAVE_LDS_ORDER();
     write_img(scrA, f.h1, lane);
     write_img(scrB, g2, lane);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    WAVE_LDS_ORDER();
     // gW1 += H1^T GA2
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
@@ -375,13 +363,9 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int r = 0; r < 16; ++r) g1[m][r] *= (1.f - f.h1[m][r] * f.h1[m][r]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    WAVE_LDS_ORDER();
     write_img(scrB, g1, lane);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    WAVE_LDS_ORDER();
     // gW0 += X^T GA1 : A[i = input j][k = row 2s+h] straight from global x
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
@@ -405,9 +389,7 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
       gW0[1] = MFMA32(av[3], b1.w, gW0[1]);
     }
     gb0 += rowsum32(scrB, lane);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    WAVE_LDS_ORDER();
   }
 
   // per-wave partial gradient in flat theta layout

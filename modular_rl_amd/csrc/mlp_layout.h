@@ -26,7 +26,7 @@ constexpr int IMG_PAD = 36;   // per-unit stride of LDS transpose scratch (float
 struct MlpDims {
   int O, A;        // inputs, head outputs
   int KS0p;        // input-layer k-steps (ceil(O/2)) rounded up to a multiple of 4
-  int fa0, fa1, fa2, fb0, fb1, fb2, ba1, ba2;  // segment offsets (floats)
+  int fa0, fa1, fb0, fb1, hv, hb, ba1, ba2;  // segment offsets (floats)
   int fwd_size, total_size;
   // flat theta offsets
   int tW0, tb0, tW1, tb1, tW2, tb2, tls, P;
@@ -41,10 +41,10 @@ __host__ __device__ inline MlpDims mlp_dims(int O, int A, int gauss) {
   int o = 0;
   d.fa0 = o; o += 2 * d.KS0p * 64;
   d.fa1 = o; o += 2 * 32 * 64;
-  d.fa2 = o; o += 1 * 32 * 64;
   d.fb0 = o; o += 2 * 2 * 16;
   d.fb1 = o; o += 2 * 2 * 16;
-  d.fb2 = o; o += 1 * 2 * 16;
+  d.hv = o; o += 2 * MAX_OUT * 32;   // head weights for VALU: [h][o][mt*16 + r] = W2[32mt + cperm(r,h)][o]
+  d.hb = o; o += 16;                 // head bias (A <= 8, padded)
   d.fwd_size = o;
   d.ba1 = o; o += 2 * 32 * 64;
   d.ba2 = o; o += 2 * 4 * 64;
@@ -85,29 +85,27 @@ __host__ __device__ inline float image_value(const MlpDims& d, const float* th, 
     int k = 2 * s + (lane >> 5);
     int j = 32 * mo + (lane & 31);
     return k < d.O ? th[d.tW0 + k * HID + j] : 0.f;
-  } else if (idx < d.fa2) {               // FA1
+  } else if (idx < d.fb0) {               // FA1
     dec(d.fa1, 32, mo, s, lane);
     int k = chain_k(s, lane >> 5);
     int j = 32 * mo + (lane & 31);
     return th[d.tW1 + k * HID + j];
-  } else if (idx < d.fb0) {               // FA2 (head)
-    dec(d.fa2, 32, mo, s, lane);
-    int k = chain_k(s, lane >> 5);
-    int j = lane & 31;
-    return j < d.A ? th[d.tW2 + k * d.A + j] : 0.f;
   } else if (idx < d.fb1) {               // FB0 [mo][h][r]
     int rel = idx - d.fb0;
     int r = rel & 15, h = (rel >> 4) & 1, m = rel >> 5;
     return th[d.tb0 + 32 * m + cperm(r, h)];
-  } else if (idx < d.fb2) {
+  } else if (idx < d.hv) {                // FB1
     int rel = idx - d.fb1;
     int r = rel & 15, h = (rel >> 4) & 1, m = rel >> 5;
     return th[d.tb1 + 32 * m + cperm(r, h)];
-  } else if (idx < d.fwd_size) {
-    int rel = idx - d.fb2;
-    int r = rel & 15, h = (rel >> 4) & 1;
-    int u = cperm(r, h);
-    return u < d.A ? th[d.tb2 + u] : 0.f;
+  } else if (idx < d.hb) {                // HV [h][o][mt*16 + r] = W2[32mt + cperm(r,h)][o]
+    int rel = idx - d.hv;
+    int i = rel & 31, o = (rel >> 5) % MAX_OUT, h = rel / (32 * MAX_OUT);
+    int u = 32 * (i >> 4) + cperm(i & 15, h);
+    return o < d.A ? th[d.tW2 + u * d.A + o] : 0.f;
+  } else if (idx < d.fwd_size) {          // HB
+    int o = idx - d.hb;
+    return o < d.A ? th[d.tb2 + o] : 0.f;
   } else if (idx < d.ba2) {               // BA1: A[i=in][k=out] = W1[in][out]
     dec(d.ba1, 32, mo, s, lane);
     int i = 32 * mo + (lane & 31);

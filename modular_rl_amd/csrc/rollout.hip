@@ -225,9 +225,7 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, MlpDims md
       xt[wave][j][k] = vf;
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  WAVE_LDS_ORDER();
 
   // 3. policy forward
   struct XL {
@@ -236,25 +234,8 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, MlpDims md
     bool valid;
     __device__ inline float operator()(int k) const { return (valid && k < O) ? p[k] : 0.f; }
   } xl{&xt[wave][j][0], O, valid};
-  struct Fwd2 {
-    f32x16 h1[2], h2[2], z;
-  };
-  f32x16 acc[2];
-  acc[0] = load_bias16(lds, md.fb0, 0, h);
-  acc[1] = load_bias16(lds, md.fb0, 1, h);
-  layer0(lds, md, xl, lane, acc);
-  tanh16(acc[0]);
-  tanh16(acc[1]);
-  f32x16 h2[2];
-  h2[0] = load_bias16(lds, md.fb1, 0, h);
-  h2[1] = load_bias16(lds, md.fb1, 1, h);
-  chain<2>(lds, md.fa1, acc, lane, h2);
-  tanh16(h2[0]);
-  tanh16(h2[1]);
-  f32x16 zt = load_bias16(lds, md.fb2, 0, h);
-  chain<1>(lds, md.fa2, h2, lane, &zt);
   float z[MAX_OUT];
-  head_gather(zt, lane, z);
+  forward_head_lowreg(lds, md, xl, lane, z);
 
   bool done = false, last = false, term = false;
   double rew = 0.0;
