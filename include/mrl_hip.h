@@ -173,6 +173,7 @@ typedef struct {
   uint8_t* flags;          /* [T*E] bit0 last-of-episode, bit1 terminated         */
   int32_t* ep_t;           /* [T*E] step index of the row inside its episode      */
   const void* noise;       /* optional injected noise [T*E] u | [T*E, d] z        */
+  int64_t* stamps;         /* optional diagnostic: [T, 8] s_memtime of block 0 phases (NULL in production) */
 } mrl_rollout_bufs;
 
 int64_t mrl_env_state_doubles(int32_t env_id);

@@ -43,7 +43,8 @@ class RolloutDesc(ctypes.Structure):
 
 class RolloutBufs(ctypes.Structure):
     _fields_ = [("env_state", vp), ("env_int", vp), ("filter_state", vp), ("records", vp), ("iteration", vp),
-                ("obs", vp), ("act", vp), ("prob", vp), ("rew", vp), ("flags", vp), ("ep_t", vp), ("noise", vp)]
+                ("obs", vp), ("act", vp), ("prob", vp), ("rew", vp), ("flags", vp), ("ep_t", vp), ("noise", vp),
+                ("stamps", vp)]
 
 
 # name -> (restype, argtypes); every symbol include/mrl_hip.h declares

@@ -157,6 +157,7 @@ class Collector:
         self.flags = torch.zeros(self.N, dtype=torch.uint8, device=self.dev)
         self.ep_t = torch.zeros(self.N, dtype=torch.int32, device=self.dev)
         self.noise = None
+        self.stamps = None  # diagnostic [T, 8] int64 phase stamps (see rollout.hip); None in production
         self.use_graph = use_graph
         self.graph = None
         self._ep_ws = torch.zeros(int(lib.mrl_episode_stats_workspace_bytes(self.E)) // 8 + 1, **f64)
@@ -165,7 +166,7 @@ class Collector:
     def _bufs(self):
         return _lib.RolloutBufs(ptr(self.env_state), ptr(self.env_int), ptr(self.filter_state), ptr(self.records),
                                 ptr(self.iteration), ptr(self.obs), ptr(self.act), ptr(self.prob), ptr(self.rew),
-                                ptr(self.flags), ptr(self.ep_t), ptr(self.noise))
+                                ptr(self.flags), ptr(self.ep_t), ptr(self.noise), ptr(self.stamps))
 
     def _launch_all(self):
         bufs = self._bufs()

@@ -73,9 +73,10 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau) {
   const double p2 = p1 + a2;
   const double w1 = var_ + v1;
   const double w2 = w1 + v2;
-  const double s0 = sin(ar), c0 = cos(ar);
-  const double s1 = sin(p1), c1 = cos(p1);
-  const double s2 = sin(p2), c2 = cos(p2);
+  double s0, c0, s1, c1, s2, c2;  // one shared range reduction per angle
+  sincos(ar, &s0, &c0);
+  sincos(p1, &s1, &c1);
+  sincos(p2, &s2, &c2);
   const double fx = x + HP_L_TORSO * s0 + HP_L_THIGH * s1 + HP_L_LEG * s2;
   const double fz = z - HP_L_TORSO * c0 - HP_L_THIGH * c1 - HP_L_LEG * c2;
   const double fvx = vx + HP_L_TORSO * c0 * var_ + HP_L_THIGH * c1 * w1 + HP_L_LEG * c2 * w2;

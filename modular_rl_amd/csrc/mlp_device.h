@@ -244,6 +244,40 @@ struct Fwd {
   float z[MAX_OUT];
 };
 
+// input layer from preloaded operands x0[s] = x[row][2s+h] (KS0p <= 16)
+__device__ inline void layer0_pre(const float* lds, const MlpDims& d, const float* x0, int lane, f32x16* acc) {
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {
+    if (s4 < d.KS0p / 4) {
+      const float4 w0 = frag4(lds, d.fa0, d.KS0p, 0, s4, lane);
+      const float4 w1 = frag4(lds, d.fa0, d.KS0p, 1, s4, lane);
+      acc[0] = MFMA32(w0.x, x0[4 * s4 + 0], acc[0]);
+      acc[1] = MFMA32(w1.x, x0[4 * s4 + 0], acc[1]);
+      acc[0] = MFMA32(w0.y, x0[4 * s4 + 1], acc[0]);
+      acc[1] = MFMA32(w1.y, x0[4 * s4 + 1], acc[1]);
+      acc[0] = MFMA32(w0.z, x0[4 * s4 + 2], acc[0]);
+      acc[1] = MFMA32(w1.z, x0[4 * s4 + 2], acc[1]);
+      acc[0] = MFMA32(w0.w, x0[4 * s4 + 3], acc[0]);
+      acc[1] = MFMA32(w1.w, x0[4 * s4 + 3], acc[1]);
+    }
+  }
+}
+
+// forward to h1, h2 (no head) from preloaded input operands
+__device__ inline void forward_tile_pre(const float* lds, const MlpDims& d, const float* x0, int lane, Fwd& f) {
+  const int h = lane >> 5;
+  f.h1[0] = load_bias16(lds, d.fb0, 0, h);
+  f.h1[1] = load_bias16(lds, d.fb0, 1, h);
+  layer0_pre(lds, d, x0, lane, f.h1);
+  tanh16(f.h1[0]);
+  tanh16(f.h1[1]);
+  f.h2[0] = load_bias16(lds, d.fb1, 0, h);
+  f.h2[1] = load_bias16(lds, d.fb1, 1, h);
+  chain<2>(lds, d.fa1, f.h1, lane, f.h2);
+  tanh16(f.h2[0]);
+  tanh16(f.h2[1]);
+}
+
 template <bool HEAD, class XL>
 __device__ inline void forward_tile(const float* lds, const MlpDims& d, const XL& xl, int lane, Fwd& f) {
   const int h = lane >> 5;

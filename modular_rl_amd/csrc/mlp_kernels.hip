@@ -242,6 +242,37 @@ __device__ inline float rowsum32(const float* img, int unit) {
   return s;
 }
 
+// every global operand one tile needs, loaded ahead of use
+struct VjpIn {
+  float x0[16];       // layer-0 B operands x[row][2s+h]
+  float xg[16];       // gW0 A operands x[row0+2s+h][j]
+  float g[4];         // head-gradient rows ghead[row][r+4h]
+  float gs[MAX_OUT];  // summed head columns (DiagGauss logstd), lane half 0 only
+};
+
+__device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn& in) {
+  const int h = lane >> 5, j = lane & 31;
+  const int64_t row0 = tile * 32, row = row0 + j;
+  const bool valid = row < a.n;
+  XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
+#pragma unroll
+  for (int s = 0; s < 16; ++s) in.x0[s] = (s < a.d.KS0p) ? xl(2 * s + h) : 0.f;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int64_t xr = row0 + 2 * s + h;
+    XGlobal xq{a.x, a.ept, a.ts_limit, a.n_obs, xr, xr < a.n};
+    in.xg[s] = (j < a.d.O) ? xq(j) : 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int o = r + 4 * h;
+    in.g[r] = (valid && o < a.d.A) ? a.ghead[row * a.gh + o] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < MAX_OUT; ++q)
+    in.gs[q] = (valid && h == 0 && q < a.n_sum) ? a.ghead[row * a.gh + a.d.A + q] : 0.f;
+}
+
 __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __restrict__ img,
                                                        const int32_t* __restrict__ skip) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -269,25 +300,23 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
   for (int q = 0; q < MAX_OUT; ++q) gls[q] = 0.f;
 
   const int64_t ntiles = (a.n + 31) / 32;
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  // software pipeline: every global operand of tile i+1 is in flight while tile i computes
+  VjpIn cur, nxt;
+  int64_t tile = (int64_t)blockIdx.x * 4 + wave;
+  if (tile < ntiles) vjp_load(a, tile, lane, cur);
+  for (; tile < ntiles; tile += stride) {
+    if (tile + stride < ntiles) vjp_load(a, tile + stride, lane, nxt);
     const int64_t row0 = tile * 32;
-    const int64_t row = row0 + j;
-    const bool valid = row < a.n;
-    XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
     Fwd f;
-    forward_tile<false>(lds, d, xl, lane, f);
+    forward_tile_pre(lds, d, cur.x0, lane, f);
 
     // head gradient rows in C layout: register r of half h = out r + 4h
     f32x16 G = zero16();
-    if (valid) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int o = r + 4 * h;
-        if (o < A) G[r] = a.ghead[row * a.gh + o];
-      }
-      if (h == 0)
-        for (int q = 0; q < a.n_sum; ++q) gls[q] += a.ghead[row * a.gh + A + q];
-    }
+    for (int r = 0; r < 4; ++r) G[r] = cur.g[r];
+#pragma unroll
+    for (int q = 0; q < MAX_OUT; ++q) gls[q] += cur.gs[q];
     // gh2 = W2 . G   (K = outs, 4 k-steps)
     f32x16 g2[2];
 #pragma unroll
@@ -371,14 +400,7 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
     for (int s4 = 0; s4 < 4; ++s4) {
       const float4 b0 = ld4(scrB + j * IMG_PAD + h * 16 + 4 * s4);
       const float4 b1 = ld4(scrB + (32 + j) * IMG_PAD + h * 16 + 4 * s4);
-      float av[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int s = 4 * s4 + q;
-        const int64_t xr = row0 + 2 * s + h;
-        XGlobal xq{a.x, a.ept, a.ts_limit, a.n_obs, xr, xr < a.n};
-        av[q] = (j < d.O) ? xq(j) : 0.f;
-      }
+      const float* av = cur.xg + 4 * s4;
       gW0[0] = MFMA32(av[0], b0.x, gW0[0]);
       gW0[1] = MFMA32(av[0], b1.x, gW0[1]);
       gW0[0] = MFMA32(av[1], b0.y, gW0[0]);
@@ -390,6 +412,8 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
     }
     gb0 += rowsum32(scrB, lane);
     WAVE_LDS_ORDER();
+    (void)row0;
+    cur = nxt;
   }
 
   // per-wave partial gradient in flat theta layout

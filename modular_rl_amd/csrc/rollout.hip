@@ -8,14 +8,16 @@
 // Per launch (step t) every block
 //   1. merges the per-block Welford partials of the E raw observations of step t
 //      (and rewards of step t-1) -- published by launch t-1 -- into the running
-//      stat, in block order (so every block derives the identical state; block 0
-//      stores it; ping-pong buffers by step parity),
+//      stat (every block derives the identical state; block 0 stores it; ping-pong
+//      buffers by step parity),
 //   2. normalises its envs' observations (x - mean)/(std + 1e-8), clip +-5, stores
 //      them as the trajectory rows (fp32) and in LDS,
 //   3. runs the policy MLP forward on MFMA (32 envs per wave, image in LDS),
 //   4. samples the action (Philox counter stream or injected noise),
 //   5. steps the env (fp64), auto-resets finished episodes, writes reward/flags,
 //   6. publishes the block's Welford partial of the new raw obs and the reward.
+// Kernels are templated on the env so every per-env array has a compile-time size
+// (registers, no scratch).
 #include <math.h>
 
 #include "../../include/mrl_hip.h"
@@ -24,9 +26,24 @@
 
 namespace mrl {
 
-constexpr int RB = 256;          // threads per block
+constexpr int RB = 256;  // threads per block
 constexpr int ENVS_PER_BLOCK = 128;
-constexpr int MAXD = 16;         // obs dims + 1 (reward)
+constexpr int MAXD = 16;  // obs dims + 1 (reward)
+
+template <int ENV>
+struct EnvC;
+template <>
+struct EnvC<MRL_ENV_CARTPOLE> {
+  static constexpr int NS = CP_NS, OBS = CP_OBS, ACT = 2, DISCRETE = 1, MAX_STEPS = 200, NU = 4;
+  __device__ static void reset(const double* u, double* s) { cartpole_reset(u, s); }
+  __device__ static void obs(const double* s, double* o) { cartpole_obs(s, o); }
+};
+template <>
+struct EnvC<MRL_ENV_HOPPER> {
+  static constexpr int NS = HP_NS, OBS = HP_OBS, ACT = HP_ACT, DISCRETE = 0, MAX_STEPS = 1000, NU = 12;
+  __device__ static void reset(const double* u, double* s) { hopper_reset(u, s); }
+  __device__ static void obs(const double* s, double* o) { hopper_obs(s, o); }
+};
 
 struct EnvInfo {
   int ns, obs, act, discrete, max_steps;
@@ -37,32 +54,23 @@ __host__ __device__ inline EnvInfo env_info(int id) {
 }
 __host__ __device__ inline int filt_doubles(int obs) { return 2 + 2 * (obs + 1); }
 
-__device__ inline void env_reset(int id, const double* u, double* s) {
-  if (id == MRL_ENV_CARTPOLE) cartpole_reset(u, s);
-  else hopper_reset(u, s);
-}
-__device__ inline void env_obs(int id, const double* s, double* o) {
-  if (id == MRL_ENV_CARTPOLE) cartpole_obs(s, o);
-  else hopper_obs(s, o);
-}
-
 struct RollArgs {
   mrl_rollout_desc d;
   mrl_rollout_bufs b;
-  EnvInfo ei;
   int nb;      // blocks
   int FS, RS;  // filter / record doubles
 };
 
 // reset-noise uniforms for one env: (gid, episode counter) on domain 1
+template <int ENV>
 __device__ inline void reset_env(const RollArgs& a, int e, double* s) {
   const int E = a.d.n_envs;
   const uint32_t gid = (uint32_t)(a.d.env_offset + e);
   const uint64_t w = (uint64_t)(uint32_t)a.b.env_int[E + e];
-  double u[HP_NS];
-  const int nu = a.ei.discrete ? 4 : 12;
-  for (int c = 0; c < nu / 2; ++c) philox_uniform2(a.d.seed, 1, gid, w, (uint32_t)c, u[2 * c], u[2 * c + 1]);
-  env_reset(a.d.env_id, u, s);
+  double u[EnvC<ENV>::NU];
+#pragma unroll
+  for (int c = 0; c < EnvC<ENV>::NU / 2; ++c) philox_uniform2(a.d.seed, 1, gid, w, (uint32_t)c, u[2 * c], u[2 * c + 1]);
+  EnvC<ENV>::reset(u, s);
   a.b.env_int[E + e] = (int32_t)(w + 1);
   a.b.env_int[e] = 0;
 }
@@ -107,28 +115,43 @@ __device__ inline void publish_partial(const RollArgs& a, const double* vals, in
 __device__ inline void batch_of_records(const double* rec, int nb, int RS, int D, int O, int k, int j, double& bn,
                                         double& bm, double& bs) {
   const bool isr = (k == O);
-  double n = 0.0, sm = 0.0;
-  for (int b = j; b < nb; b += 16) {
-    const double* r = rec + (int64_t)b * RS;
-    const double nb_ = r[isr ? 1 : 0];
-    n += nb_;
-    sm += nb_ * r[2 + k];
+  // all record fields in one round of loads (up to RB_MAX records per lane), then combine
+  constexpr int RB_MAX = 4;  // 16 lanes x 4 = 64 blocks (8192 envs) per round
+  double rn[RB_MAX], rm[RB_MAX], rs[RB_MAX];
+  double n = 0.0, sm = 0.0, raw = 0.0;
+  for (int b0 = 0; b0 < nb; b0 += 16 * RB_MAX) {
+#pragma unroll
+    for (int q = 0; q < RB_MAX; ++q) {
+      const int b = b0 + j + 16 * q;
+      const double* r = rec + (int64_t)b * RS;
+      rn[q] = b < nb ? r[isr ? 1 : 0] : 0.0;
+      rm[q] = b < nb ? r[2 + k] : 0.0;
+      rs[q] = b < nb ? r[2 + D + k] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < RB_MAX; ++q) {
+      n += rn[q];
+      sm += rn[q] * rm[q];
+      raw += rs[q] + rn[q] * rm[q] * rm[q];
+    }
   }
   n = sum16(n);
   sm = sum16(sm);
   const double mean = n > 0.0 ? sm / n : 0.0;
-  double m2 = 0.0;
-  for (int b = j; b < nb; b += 16) {
-    const double* r = rec + (int64_t)b * RS;
-    const double nb_ = r[isr ? 1 : 0];
-    if (nb_ > 0.0) {
-      const double dm = r[2 + k] - mean;
-      m2 += r[2 + D + k] + nb_ * dm * dm;
-    }
-  }
   bn = n;
   bm = mean;
-  bs = sum16(m2);
+  if (nb <= 16 * RB_MAX) {  // one round (<= 8192 envs): exact two-pass form from registers
+    double m2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < RB_MAX; ++q)
+      if (rn[q] > 0.0) {
+        const double dm = rm[q] - mean;
+        m2 += rs[q] + rn[q] * dm * dm;
+      }
+    bs = sum16(m2);
+  } else {  // many rounds: sum (M2_b + n_b mean_b^2) - n mean^2
+    bs = sum16(raw) - n * mean * mean;
+  }
 }
 
 // Chan merge of (nb, mb, m2b) into (n, M, S); for nb == 1 this is RunningStat.push
@@ -143,16 +166,21 @@ __device__ inline void chan_merge(double& n, double& M, double& S, double nb, do
   n = nn;
 }
 
+template <int ENV>
 __global__ __launch_bounds__(RB) void rollout_reset_kernel(RollArgs a) {
+  using EC = EnvC<ENV>;
+  constexpr int O = EC::OBS, D = O + 1;
   __shared__ double vals[ENVS_PER_BLOCK * MAXD];
-  const int E = a.d.n_envs, O = a.ei.obs, D = O + 1;
+  const int E = a.d.n_envs;
   const int le = threadIdx.x;
   const int e = blockIdx.x * ENVS_PER_BLOCK + le;
   if (le < ENVS_PER_BLOCK && e < E) {
-    double s[HP_NS], o[HP_OBS];
-    reset_env(a, e, s);
-    for (int i = 0; i < a.ei.ns; ++i) a.b.env_state[(int64_t)i * E + e] = s[i];
-    env_obs(a.d.env_id, s, o);
+    double s[EC::NS], o[O];
+    reset_env<ENV>(a, e, s);
+#pragma unroll
+    for (int i = 0; i < EC::NS; ++i) a.b.env_state[(int64_t)i * E + e] = s[i];
+    EC::obs(s, o);
+#pragma unroll
     for (int k = 0; k < O; ++k) vals[le * D + k] = o[k];
     vals[le * D + O] = 0.0;
   }
@@ -161,16 +189,37 @@ __global__ __launch_bounds__(RB) void rollout_reset_kernel(RollArgs a) {
   publish_partial(a, vals, nvalid, D, false, a.b.records);
 }
 
+template <int ENV>
 __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, MlpDims md, const float* __restrict__ theta,
                                                           const float* __restrict__ img, int t) {
+  using EC = EnvC<ENV>;
+  constexpr int O = EC::OBS, D = O + 1, NS = EC::NS, A = EC::ACT;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ double vals[ENVS_PER_BLOCK * MAXD];
   __shared__ double fmean[MAXD], fden[MAXD];
   __shared__ float xt[4][32][MAX_IN];
+  // diagnostic phase stamps (100 MHz realtime) of block 0 / thread 0 -- never set in production
+#define STAMP(k)                                                                    \
+  do {                                                                              \
+    if (a.b.stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0)               \
+      a.b.stamps[(int64_t)t * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  STAMP(0);
+  const int E = a.d.n_envs;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
+  const int le = wave * 32 + j;
+  const int e = blockIdx.x * ENVS_PER_BLOCK + le;
+  const bool valid = e < E;
+  const int64_t row = (int64_t)t * E + e;
 
-  const int E = a.d.n_envs, O = a.ei.obs, D = O + 1, A = md.A;
+  // env state loads first: they overlap the image copy and the filter merge below
+  double s[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) s[i] = valid ? a.b.env_state[(int64_t)i * E + e] : 0.0;
+
   for (int i = threadIdx.x; i < md.fwd_size / 4; i += RB)
     reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img)[i];
+  STAMP(1);
 
   // 1. running-stat merge (filters.py:30-31 push, per step over all envs)
   const double* fs_in = a.b.filter_state + (t & 1) * a.FS;
@@ -178,41 +227,33 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, MlpDims md
   const double* rec_in = a.b.records + (int64_t)(t & 1) * a.nb * a.RS;
   double* rec_out = a.b.records + (int64_t)((t + 1) & 1) * a.nb * a.RS;
   if ((int)(threadIdx.x >> 4) < D) {
-    const int k = threadIdx.x >> 4, j = threadIdx.x & 15;
+    const int k = threadIdx.x >> 4, jj = threadIdx.x & 15;
     const bool isr = (k == O);
     double n = fs_in[isr ? 1 : 0], M = fs_in[2 + k], S = fs_in[2 + D + k];
     // combine the block partials into one batch, then one Chan merge into the stat
     double bn, bm, bs;
-    batch_of_records(rec_in, a.nb, a.RS, D, O, k, j, bn, bm, bs);
+    batch_of_records(rec_in, a.nb, a.RS, D, O, k, jj, bn, bm, bs);
     chan_merge(n, M, S, bn, bm, bs);
-    if (j != 0) {
-    } else if (blockIdx.x == 0) {
+    if (jj == 0 && blockIdx.x == 0) {
       if (k == 0) fs_out[0] = n;
       if (isr) fs_out[1] = n;
       fs_out[2 + k] = M;
       fs_out[2 + D + k] = S;
     }
-    if (!isr && j == 0) {
+    if (!isr && jj == 0) {
       const double var = n > 1.0 ? S / (n - 1.0) : M * M;  // running_stat.py:27
       fmean[k] = M;
       fden[k] = sqrt(var) + 1e-8;
     }
   }
   __syncthreads();
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
-  const int le = wave * 32 + j;
-  const int e = blockIdx.x * ENVS_PER_BLOCK + le;
-  const bool valid = e < E;
-  const int64_t row = (int64_t)t * E + e;
-  double s[HP_NS];
-  if (valid)
-    for (int i = 0; i < a.ei.ns; ++i) s[i] = a.b.env_state[(int64_t)i * E + e];
+  STAMP(2);
 
   // 2. filtered observation (core.py:191-192)
-  if (valid) {
-    double o[HP_OBS];
-    env_obs(a.d.env_id, s, o);
+  {
+    double o[O];
+    EC::obs(s, o);
+#pragma unroll
     for (int k = 0; k < O; ++k) {
       double v = o[k];
       if (a.d.filter) {
@@ -221,62 +262,87 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, MlpDims md
         v = v < -5.0 ? -5.0 : (v > 5.0 ? 5.0 : v);
       }
       const float vf = (float)v;
-      if (h == 0) a.b.obs[row * O + k] = vf;
+      if (valid && h == 0) a.b.obs[row * O + k] = vf;
       xt[wave][j][k] = vf;
     }
   }
   WAVE_LDS_ORDER();
+  STAMP(3);
 
   // 3. policy forward
   struct XL {
     const float* p;
-    int O;
     bool valid;
     __device__ inline float operator()(int k) const { return (valid && k < O) ? p[k] : 0.f; }
-  } xl{&xt[wave][j][0], O, valid};
+  } xl{&xt[wave][j][0], valid};
+  // sampling noise does not depend on the policy output: draw it first so its VALU
+  // work overlaps the MFMA chain of the forward
+  const uint32_t gid = (uint32_t)(a.d.env_offset + e);
+  const uint64_t w = (uint64_t)(*a.b.iteration) * (uint64_t)a.d.horizon + (uint64_t)t;
+  double zn[A + 1];
+  if (a.b.noise != nullptr) {
+    if (valid) {
+      if constexpr (EC::DISCRETE) zn[0] = reinterpret_cast<const double*>(a.b.noise)[row];
+      else
+#pragma unroll
+        for (int q = 0; q < A; ++q) zn[q] = reinterpret_cast<const double*>(a.b.noise)[row * A + q];
+    }
+  } else if constexpr (EC::DISCRETE) {
+    double u1;
+    philox_uniform2(a.d.seed, 0, gid, w, 0, zn[0], u1);
+  } else {
+#pragma unroll
+    for (int c = 0; c < (A + 1) / 2; ++c) {
+      double u0, u1;
+      philox_uniform2(a.d.seed, 0, gid, w, (uint32_t)c, u0, u1);
+      const double rad = sqrt(-2.0 * log(1.0 - u0));
+      double sn, cn;
+      sincos(2.0 * 3.141592653589793 * u1, &sn, &cn);
+      zn[2 * c] = rad * cn;
+      zn[2 * c + 1] = rad * sn;
+    }
+  }
+
   float z[MAX_OUT];
   forward_head_lowreg(lds, md, xl, lane, z);
 
   bool done = false, last = false, term = false;
   double rew = 0.0;
   if (valid && h == 0) {
-    const uint32_t gid = (uint32_t)(a.d.env_offset + e);
-    const uint64_t w = (uint64_t)(*a.b.iteration) * (uint64_t)a.d.horizon + (uint64_t)t;
+    STAMP(4);
     // 4. sample (core.py:261-267; distributions.py:3-13 / core.py:432-435)
-    if (a.ei.discrete) {
+    if constexpr (EC::DISCRETE) {
       float m = z[0];
+#pragma unroll
       for (int q = 1; q < A; ++q) m = fmaxf(m, z[q]);
-      float p[MAX_OUT], se = 0.f;
-      for (int q = 0; q < A; ++q) { p[q] = expf(z[q] - m); se += p[q]; }
+      float p[A], se = 0.f;
+#pragma unroll
+      for (int q = 0; q < A; ++q) {
+        p[q] = expf(z[q] - m);
+        se += p[q];
+      }
+#pragma unroll
       for (int q = 0; q < A; ++q) p[q] = p[q] / se;
-      double u, u1;
-      if (a.b.noise != nullptr) u = reinterpret_cast<const double*>(a.b.noise)[row];
-      else philox_uniform2(a.d.seed, 0, gid, w, 0, u, u1);
+      const double u = zn[0];
       int act = 0;
       float cs = 0.f;
+      bool found = false;
+#pragma unroll
       for (int q = 0; q < A; ++q) {
         cs += p[q];
-        if ((double)cs > u) { act = q; break; }
+        if (!found && (double)cs > u) {
+          act = q;
+          found = true;
+        }
       }
       reinterpret_cast<int32_t*>(a.b.act)[row] = act;
+#pragma unroll
       for (int q = 0; q < A; ++q) a.b.prob[row * A + q] = p[q];
       cartpole_step(s, act, rew, done);
     } else {
       const float* logstd = theta + md.tls;
-      float av[MAX_OUT];
-      double zn[MAX_OUT + 1];
-      if (a.b.noise != nullptr) {
-        for (int q = 0; q < A; ++q) zn[q] = reinterpret_cast<const double*>(a.b.noise)[row * A + q];
-      } else {
-        for (int c = 0; c < (A + 1) / 2; ++c) {
-          double u0, u1;
-          philox_uniform2(a.d.seed, 0, gid, w, (uint32_t)c, u0, u1);
-          const double rad = sqrt(-2.0 * log(1.0 - u0));
-          const double ang = 2.0 * 3.141592653589793 * u1;
-          zn[2 * c] = rad * cos(ang);
-          zn[2 * c + 1] = rad * sin(ang);
-        }
-      }
+      float av[A];
+#pragma unroll
       for (int q = 0; q < A; ++q) {
         const float sd = expf(logstd[q]);
         av[q] = __fadd_rn(__fmul_rn((float)zn[q], sd), z[q]);
@@ -286,30 +352,36 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, MlpDims md
       }
       hopper_step(s, av, rew, done);
     }
+    STAMP(5);
     // 5. episode bookkeeping: gym TimeLimit => done (terminated, bootstrap 0);
     //    the rollout loop limit / horizon cut => not terminated (core.py:190-207, 73)
     const int ept = a.b.env_int[e];
     a.b.ep_t[row] = ept;
-    term = done || (ept + 1 >= a.ei.max_steps);
+    term = done || (ept + 1 >= EC::MAX_STEPS);
     last = term || (ept + 1 >= a.d.timestep_limit) || (t == a.d.horizon - 1);
     a.b.rew[row] = (float)rew;
     a.b.flags[row] = (uint8_t)((last ? 1 : 0) | (term ? 2 : 0));
-    if (last && t < a.d.horizon - 1) reset_env(a, e, s);
+    if (last && t < a.d.horizon - 1) reset_env<ENV>(a, e, s);
     else a.b.env_int[e] = ept + 1;
-    for (int i = 0; i < a.ei.ns; ++i) a.b.env_state[(int64_t)i * E + e] = s[i];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) a.b.env_state[(int64_t)i * E + e] = s[i];
     // 6. raw next observation + reward into the block partial
-    double o[HP_OBS];
-    env_obs(a.d.env_id, s, o);
+    double o[O];
+    EC::obs(s, o);
+#pragma unroll
     for (int k = 0; k < O; ++k) vals[le * D + k] = o[k];
     vals[le * D + O] = rew;
   }
   __syncthreads();
+  STAMP(6);
   const int nvalid = min(ENVS_PER_BLOCK, E - (int)blockIdx.x * ENVS_PER_BLOCK);
   publish_partial(a, vals, nvalid, D, true, rec_out);
+  STAMP(7);
+#undef STAMP
 }
 
-__global__ void rollout_finish_kernel(RollArgs a) {
-  const int O = a.ei.obs, D = O + 1, T = a.d.horizon;
+__global__ void rollout_finish_kernel(RollArgs a, int O) {
+  const int D = O + 1, T = a.d.horizon;
   const double* fs_in = a.b.filter_state + (T & 1) * a.FS;
   double* fs_out = a.b.filter_state;
   const double* rec_in = a.b.records + (int64_t)(T & 1) * a.nb * a.RS;
@@ -333,7 +405,7 @@ __global__ void rollout_finish_kernel(RollArgs a) {
     fs_out[2 + k] = M;
     fs_out[2 + D + k] = S;
   }
-  if (k == 0) *a.b.iteration += 1;
+  if (threadIdx.x == 0) *a.b.iteration += 1;
 }
 
 }  // namespace mrl
@@ -352,9 +424,8 @@ static RollArgs make_args(const mrl_rollout_desc* d, const mrl_rollout_bufs* b) 
   RollArgs a;
   a.d = *d;
   a.b = *b;
-  a.ei = env_info(d->env_id);
   a.nb = (d->n_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
-  a.FS = filt_doubles(a.ei.obs);
+  a.FS = filt_doubles(env_info(d->env_id).obs);
   a.RS = a.FS;
   return a;
 }
@@ -370,7 +441,10 @@ int mrl_rollout_reset(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void
   int rc = check_roll(d, b);
   if (rc) return rc;
   RollArgs a = make_args(d, b);
-  hipLaunchKernelGGL(rollout_reset_kernel, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a);
+  if (d->env_id == MRL_ENV_CARTPOLE)
+    hipLaunchKernelGGL(rollout_reset_kernel<MRL_ENV_CARTPOLE>, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(rollout_reset_kernel<MRL_ENV_HOPPER>, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a);
   return hip_check(hipGetLastError(), "mrl_rollout_reset");
 }
 
@@ -389,7 +463,12 @@ int mrl_rollout_step(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const f
   RollArgs a = make_args(d, b);
   MlpDims md = mlp_dims(pol->n_in, pol->n_out, gauss);
   size_t shm = (size_t)md.fwd_size * 4;
-  hipLaunchKernelGGL(rollout_step_kernel, dim3(a.nb), dim3(RB), shm, (hipStream_t)stream, a, md, theta, image, t);
+  if (d->env_id == MRL_ENV_CARTPOLE)
+    hipLaunchKernelGGL(rollout_step_kernel<MRL_ENV_CARTPOLE>, dim3(a.nb), dim3(RB), shm, (hipStream_t)stream, a, md,
+                       theta, image, t);
+  else
+    hipLaunchKernelGGL(rollout_step_kernel<MRL_ENV_HOPPER>, dim3(a.nb), dim3(RB), shm, (hipStream_t)stream, a, md,
+                       theta, image, t);
   return hip_check(hipGetLastError(), "mrl_rollout_step");
 }
 
@@ -397,7 +476,7 @@ int mrl_rollout_finish(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, voi
   int rc = check_roll(d, b);
   if (rc) return rc;
   RollArgs a = make_args(d, b);
-  hipLaunchKernelGGL(rollout_finish_kernel, dim3(1), dim3(RB), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(rollout_finish_kernel, dim3(1), dim3(RB), 0, (hipStream_t)stream, a, env_info(d->env_id).obs);
   return hip_check(hipGetLastError(), "mrl_rollout_finish");
 }
 
