@@ -99,6 +99,54 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
 int mrl_reduce_rows_f32(const float* slab, int64_t rows, int64_t cols, float* out, const int32_t* skip, void* stream);
 int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* out, const int32_t* skip, void* stream);
 
+/* ---------------------------------------------------------------- layered (wide) MLP path
+ * Any hid_sizes (e.g. Humanoid 376-512-512-512-17): each Dense layer
+ * is one tiled fp32-MFMA GEMM over all rows (forward, JVP, input-grad, weight-grad)
+ * and the head epilogue is a per-row kernel; the host sequences them
+ * (modular_rl_amd/nets.py LayeredMlpNet).  Replaces the same Theano functions as
+ * mrl_mlp_rows / mrl_mlp_vjp for nets the fused 64-wide kernels do not cover. */
+#define MRL_LAYERED_MAX_OUT 32
+
+#define MRL_GEMM_STORE 0  /* C = AB (+ bias)                                         */
+#define MRL_GEMM_TANH 1   /* C = tanh(AB + bias)                  Dense + tanh forward */
+#define MRL_GEMM_DTANH 2  /* C = (AB + bias) * (1 - H^2)          JVP / input-grad    */
+#define MRL_GEMM_SLAB 3   /* c + z*slab_stride = sum over K-split z of AB  (weight grads) */
+
+typedef struct {
+  int64_t m, n, k;
+  const float* a;       /* op(a)(i,k) = a[i*lda+k] (a_trans 0) | a[k*lda+i] (a_trans 1)  */
+  int64_t lda;
+  int32_t a_trans;
+  int32_t ones_row;     /* 1: row m-1 of op(a) is all ones (bias grad rides the weight-grad GEMM) */
+  const float* b;       /* op(b)(k,j) = b[k*ldb+j] (b_trans 0) | b[j*ldb+k] (b_trans 1)  */
+  int64_t ldb;
+  int32_t b_trans;
+  int32_t epilogue;     /* MRL_GEMM_*                                                    */
+  const float* a2;      /* optional second product a2.b2 (same shapes/layout) added to C  */
+  const float* b2;
+  float* c;
+  int64_t ldc;
+  const float* bias;    /* [n] or NULL                                                   */
+  const float* h;       /* MRL_GEMM_DTANH: [m, ldh] activations                          */
+  int64_t ldh;
+  int32_t splits;       /* MRL_GEMM_SLAB: requested K splits (see mrl_gemm_slab_splits)  */
+  int32_t pad_;
+  int64_t slab_stride;  /* MRL_GEMM_SLAB: floats between consecutive split slabs         */
+} mrl_gemm_desc;
+
+int mrl_gemm(const mrl_gemm_desc* g, const int32_t* skip, void* stream);
+/* slabs a MRL_GEMM_SLAB call over k rows with `max_splits` requested actually writes */
+int64_t mrl_gemm_slab_splits(int64_t k, int32_t max_splits);
+/* per-row head epilogue (same semantics as mrl_mlp_rows' epilogues) on head rows
+ * z [N, n_out] (and tangent rows dz for EPI_FVP); logstd/dlogstd for DiagGauss;
+ * io->x / ep_t unused; partial has mrl_partial_rows(n) rows. */
+int mrl_head_rows(int32_t head, int32_t n_out, int32_t epilogue, const float* z, const float* dz,
+                  const float* logstd, const float* dlogstd, const mrl_rows_io* io, const int32_t* skip,
+                  void* stream);
+/* X[N, n_obs+1] = [obs, ep_t/timestep_limit]  (value-net input, core.py:659-660) */
+int mrl_concat_time(const float* obs, const int32_t* ep_t, int64_t n, int32_t n_obs, double timestep_limit,
+                    float* x, void* stream);
+
 /* ---------------------------------------------------------------- conjugate gradient
  * Device-resident Demmel CG on flat fp64 vectors (trpo.py:165-200).
  * state (fp64): [0]=rdotr [1]=last pz [2]=iterations run; flag (int32[2]): [0]=converged.

@@ -15,6 +15,7 @@ OK = 0
 HEAD_LINEAR, HEAD_SOFTMAX, HEAD_GAUSS = 0, 1, 2
 EPI_PROB, EPI_LOSSES, EPI_SURRGRAD, EPI_VFLOSS, EPI_FVP = 0, 1, 2, 3, 4
 ENV_CARTPOLE, ENV_HOPPER = 0, 1
+GEMM_STORE, GEMM_TANH, GEMM_DTANH, GEMM_SLAB = 0, 1, 2, 3
 
 vp = ctypes.c_void_p
 i32 = ctypes.c_int32
@@ -34,6 +35,13 @@ class RowsIO(ctypes.Structure):
     _fields_ = [("x", vp), ("ep_t", vp), ("timestep_limit", f64), ("n", i64), ("inv_n_global", f64),
                 ("act", vp), ("adv", vp), ("oldprob", vp), ("target", vp), ("out", vp), ("ghead", vp),
                 ("partial", vp)]
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [("m", i64), ("n", i64), ("k", i64), ("a", vp), ("lda", i64), ("a_trans", i32), ("ones_row", i32),
+                ("b", vp), ("ldb", i64), ("b_trans", i32), ("epilogue", i32), ("a2", vp), ("b2", vp), ("c", vp),
+                ("ldc", i64), ("bias", vp), ("h", vp), ("ldh", i64), ("splits", i32), ("pad_", i32),
+                ("slab_stride", i64)]
 
 
 class RolloutDesc(ctypes.Structure):
@@ -60,6 +68,10 @@ SIGNATURES = {
     "mrl_mlp_vjp": (i32, [vp, vp, vp, vp, f64, vp, i64, vp, vp, vp]),
     "mrl_reduce_rows_f32": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_reduce_rows_f64": (i32, [vp, i64, i64, vp, vp, vp]),
+    "mrl_gemm": (i32, [vp, vp, vp]),
+    "mrl_gemm_slab_splits": (i64, [i64, i32]),
+    "mrl_head_rows": (i32, [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
+    "mrl_concat_time": (i32, [vp, vp, i64, i32, f64, vp, vp]),
     "mrl_cg_init": (i32, [vp, i64, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_cg_update": (i32, [vp, f64, f64, i64, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_trpo_step": (i32, [vp, vp, vp, f64, f64, i64, vp, vp, vp]),

@@ -1,0 +1,329 @@
+// Tiled fp32 GEMM on v_mfma_f32_32x32x2_f32 for the wide ("layered") MLP path
+// (Humanoid 376-512-512-512-17 and any hid_sizes the fused 64-wide kernels do not
+// cover).  One kernel, three operand orientations, fused epilogues:
+//
+//   C[M,N] = sum_p op(A_p)[M,K] . op(B_p)[K,N]        p = 1 or 2 products (JVP: dX.W + X.dW)
+//   op(A)(i,k) = A[i*lda + k]  (a_trans = 0)   or  A[k*lda + i]  (a_trans = 1)
+//   op(B)(k,j) = B[k*ldb + j]  (b_trans = 0)   or  B[j*ldb + k]  (b_trans = 1)
+//   epilogue: store | +bias | tanh(. + bias) | . * (1 - H^2) | split-K partial slab
+//
+// Layer forward  Y = tanh(X W + b)        NN, EPI_TANH
+// JVP            dY = (1-Y^2)(dX W + X dW + db)    NN dual + bias, then rows-scale
+// VJP input grad dX = (G W^T) (1 - X^2)    NT, EPI_DTANH
+// weight grad    dW = X^T G  (K = rows)    TN, EPI_SLAB (split-K over rows, slabs reduced
+//                                          by mrl_reduce_rows_f32 in fixed order)
+//
+// Block 128x128x32, 256 threads = 4 waves, each wave a 64x64 tile = 2x2 MFMA tiles.
+// Global->LDS with coalesced loads; LDS tiles are k-major with an odd row pitch (129)
+// so both the staging writes and the MFMA operand reads are bank-conflict free.
+#include <math.h>
+
+#include "../../include/mrl_hip.h"
+#include "mlp_device.h"
+#include "rows_epilogue.h"
+
+namespace mrl {
+
+constexpr int GBM = 128, GBN = 128, GBK = 32, GLD = 129;
+
+struct GemmArgs {
+  int64_t M, N, K;
+  const float* A;
+  const float* B;
+  const float* A2;
+  const float* B2;
+  int64_t lda, ldb;
+  float* C;
+  int64_t ldc;
+  const float* bias;
+  const float* H;
+  int64_t ldh;
+  int epi;
+  int64_t m_real;       // rows of op(A) read from memory; rows >= m_real are the ones-row
+  int64_t k_chunk;      // split-K: K rows per blockIdx.z
+  int64_t slab_stride;  // split-K: floats between the slabs of consecutive splits
+  const int32_t* skip;
+};
+
+// stage one [GBK x 128] operand tile: dst[k][c] (pitch GLD), c = tile row (A) or col (B)
+// contig_c: the source is contiguous along c (else along k)
+template <bool CONTIG_C>
+__device__ inline void stage_tile(float* dst, const float* src, int64_t ld, int64_t c0, int64_t k0, int64_t C,
+                                  int64_t Kend, int64_t Creal) {
+  const int t = threadIdx.x;
+  if (CONTIG_C) {
+    // element (c, k) at src[k*ld + c]; lanes along c
+    const int c = t & 127;
+    const int kb = t >> 7;  // 0..1
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = kb + 2 * q;
+      const int64_t gc = c0 + c, gk = k0 + k;
+      const bool in = gc < C && gk < Kend;
+      dst[k * GLD + c] = (in && gc < Creal) ? src[gk * ld + gc] : (in ? 1.f : 0.f);
+    }
+  } else {
+    // element (c, k) at src[c*ld + k]; 4 lanes per c, 8 consecutive k each
+    const int c = t >> 1;     // 0..127
+    const int kq = t & 1;     // 0..1 -> k in [16kq, 16kq+16)
+    const int64_t gc = c0 + c;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = kq * 16 + q;
+      const int64_t gk = k0 + k;
+      const bool in = gc < C && gk < Kend;
+      dst[k * GLD + c] = (in && gc < Creal) ? src[gc * ld + gk] : (in ? 1.f : 0.f);
+    }
+  }
+}
+
+template <bool AT, bool BT>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
+  __shared__ float As[GBK * GLD];
+  __shared__ float Bs[GBK * GLD];
+  if (g.skip != nullptr && *g.skip != 0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t m0 = (int64_t)blockIdx.y * GBM, n0 = (int64_t)blockIdx.x * GBN;
+  int64_t kbeg = 0, kend = g.K;
+  if (g.epi == MRL_GEMM_SLAB) {
+    kbeg = (int64_t)blockIdx.z * g.k_chunk;
+    kend = min(g.K, kbeg + g.k_chunk);
+  }
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = zero16();
+  const int npairs = g.A2 != nullptr ? 2 : 1;
+  for (int p = 0; p < npairs; ++p) {
+    const float* Ap = p == 0 ? g.A : g.A2;
+    const float* Bp = p == 0 ? g.B : g.B2;
+    for (int64_t k0 = kbeg; k0 < kend; k0 += GBK) {
+      __syncthreads();
+      // A tile: c = row i in [m0, m0+128), contiguous along i iff a_trans
+      stage_tile<AT>(As, Ap, g.lda, m0, k0, g.M, kend, g.m_real);
+      // B tile: c = col j in [n0, n0+128), contiguous along j iff !b_trans
+      stage_tile<!BT>(Bs, Bp, g.ldb, n0, k0, g.N, kend, g.N);
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < GBK / 2; ++s) {
+        const int k = 2 * s + h;
+        const float a0 = As[k * GLD + wm * 64 + j];
+        const float a1 = As[k * GLD + wm * 64 + 32 + j];
+        const float b0 = Bs[k * GLD + wn * 64 + j];
+        const float b1 = Bs[k * GLD + wn * 64 + 32 + j];
+        acc[0][0] = MFMA32(a0, b0, acc[0][0]);
+        acc[0][1] = MFMA32(a0, b1, acc[0][1]);
+        acc[1][0] = MFMA32(a1, b0, acc[1][0]);
+        acc[1][1] = MFMA32(a1, b1, acc[1][1]);
+      }
+    }
+  }
+  // epilogue: lane holds column j, rows cperm(r, h) of each 32x32 tile
+  float* C = g.C;
+  if (g.epi == MRL_GEMM_SLAB) C += (int64_t)blockIdx.z * g.slab_stride;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int64_t col = n0 + wn * 64 + ni * 32 + j;
+      if (col >= g.N) continue;
+      const float bv = g.bias != nullptr ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * 64 + mi * 32 + cperm(r, h);
+        if (row >= g.M) continue;
+        float v = acc[mi][ni][r] + bv;
+        if (g.epi == MRL_GEMM_TANH) v = tanh_fast(v);
+        else if (g.epi == MRL_GEMM_DTANH) {
+          const float hv = g.H[row * g.ldh + col];
+          v *= (1.f - hv * hv);
+        }
+        C[row * g.ldc + col] = v;
+      }
+    }
+}
+
+// X = [obs, ep_t / limit] for the value net's time feature (core.py:659-660)
+__global__ void concat_time_kernel(const float* __restrict__ obs, const int32_t* __restrict__ ept, int64_t n, int O,
+                                   double limit, float* __restrict__ X) {
+  const int64_t total = n * (O + 1);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / (O + 1);
+    const int c = (int)(i % (O + 1));
+    X[i] = c < O ? obs[r * O + c] : (float)((double)ept[r] / limit);
+  }
+}
+
+// Per-row head epilogue of the layered path: z (and dz) rows come from the last GEMM.
+template <int EPI, int MA>
+__global__ __launch_bounds__(256) void head_rows_kernel(RowsArgs a, const float* __restrict__ zr,
+                                                        const float* __restrict__ dzr, const int32_t* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int A = a.A;
+  float ls[MA], sd[MA], dls[MA];
+#pragma unroll
+  for (int j = 0; j < MA; ++j) {
+    ls[j] = (a.logstd != nullptr && j < A) ? a.logstd[j] : 0.f;
+    sd[j] = expf(ls[j]);
+    dls[j] = (a.dlogstd != nullptr && j < A) ? a.dlogstd[j] : 0.f;
+  }
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+  for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < a.n; row += (int64_t)gridDim.x * 256) {
+    float z[MA], dz[MA];
+#pragma unroll
+    for (int j = 0; j < MA; ++j) {
+      z[j] = j < A ? zr[row * A + j] : 0.f;
+      dz[j] = (EPI == MRL_EPI_FVP && j < A) ? dzr[row * A + j] : 0.f;
+    }
+    row_epilogue<EPI, MA>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+  }
+  if (a.partial != nullptr) {
+    acc0 = wave_sum(acc0);
+    acc1 = wave_sum(acc1);
+    acc2 = wave_sum(acc2);
+    if (lane == 0) {
+      double* p = a.partial + ((int64_t)blockIdx.x * 4 + wave) * 4;
+      p[0] = acc0;
+      p[1] = acc1;
+      p[2] = acc2;
+      p[3] = 0.0;
+    }
+  }
+}
+
+template <int MA>
+static void launch_head(int epi, dim3 grid, hipStream_t s, const RowsArgs& a, const float* z, const float* dz,
+                        const int32_t* skip) {
+  switch (epi) {
+    case MRL_EPI_PROB: hipLaunchKernelGGL((head_rows_kernel<MRL_EPI_PROB, MA>), grid, dim3(256), 0, s, a, z, dz, skip); break;
+    case MRL_EPI_LOSSES: hipLaunchKernelGGL((head_rows_kernel<MRL_EPI_LOSSES, MA>), grid, dim3(256), 0, s, a, z, dz, skip); break;
+    case MRL_EPI_SURRGRAD: hipLaunchKernelGGL((head_rows_kernel<MRL_EPI_SURRGRAD, MA>), grid, dim3(256), 0, s, a, z, dz, skip); break;
+    case MRL_EPI_VFLOSS: hipLaunchKernelGGL((head_rows_kernel<MRL_EPI_VFLOSS, MA>), grid, dim3(256), 0, s, a, z, dz, skip); break;
+    default: hipLaunchKernelGGL((head_rows_kernel<MRL_EPI_FVP, MA>), grid, dim3(256), 0, s, a, z, dz, skip); break;
+  }
+}
+
+}  // namespace mrl
+
+using namespace mrl;
+
+extern "C" {
+
+static int64_t slab_chunk(int64_t K, int64_t splits) {
+  if (splits < 1) splits = 1;
+  int64_t chunk = ((K + splits - 1) / splits + GBK - 1) / GBK * GBK;
+  return chunk < GBK ? GBK : chunk;
+}
+
+int64_t mrl_gemm_slab_splits(int64_t k, int32_t max_splits) {
+  if (k <= 0) return 1;
+  const int64_t chunk = slab_chunk(k, max_splits);
+  return (k + chunk - 1) / chunk;
+}
+
+int mrl_gemm(const mrl_gemm_desc* d, const int32_t* skip, void* stream) {
+  if (!d || !d->b || !d->c || (!d->a && d->m > (d->ones_row ? 1 : 0))) return fail(E_ARG, "mrl_gemm: null pointer");
+  if ((d->a2 == nullptr) != (d->b2 == nullptr)) return fail(E_ARG, "mrl_gemm: a2/b2 must be both set or both null");
+  if (d->epilogue < MRL_GEMM_STORE || d->epilogue > MRL_GEMM_SLAB) return fail(E_ARG, "mrl_gemm: bad epilogue");
+  if (d->epilogue == MRL_GEMM_DTANH && !d->h) return fail(E_ARG, "mrl_gemm: DTANH needs h");
+  if (d->m <= 0 || d->n <= 0) return OK;
+  GemmArgs g;
+  g.M = d->m;
+  g.N = d->n;
+  g.K = d->k;
+  g.A = d->a;
+  g.B = d->b;
+  g.A2 = d->a2;
+  g.B2 = d->b2;
+  g.lda = d->lda;
+  g.ldb = d->ldb;
+  g.C = d->c;
+  g.ldc = d->ldc;
+  g.bias = d->bias;
+  g.H = d->h;
+  g.ldh = d->ldh;
+  g.epi = d->epilogue;
+  g.m_real = d->m - (d->ones_row ? 1 : 0);
+  g.k_chunk = d->k;
+  g.slab_stride = d->slab_stride;
+  g.skip = skip;
+  int64_t splits = 1;
+  if (g.epi == MRL_GEMM_SLAB) {
+    g.k_chunk = slab_chunk(d->k, d->splits);
+    splits = d->k > 0 ? (d->k + g.k_chunk - 1) / g.k_chunk : 1;
+  }
+  if (splits > 65535) return fail(E_ARG, "mrl_gemm: too many splits");
+  dim3 grid((unsigned)((g.N + GBN - 1) / GBN), (unsigned)((g.M + GBM - 1) / GBM), (unsigned)splits);
+  hipStream_t s = (hipStream_t)stream;
+  if (!d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(256), 0, s, g);
+  else if (!d->a_trans && d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(256), 0, s, g);
+  else if (d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(256), 0, s, g);
+  return hip_check(hipGetLastError(), "mrl_gemm");
+}
+
+int mrl_head_rows(int32_t head, int32_t n_out, int32_t epi, const float* z, const float* dz, const float* logstd,
+                  const float* dlogstd, const mrl_rows_io* io, const int32_t* skip, void* stream) {
+  if (!io || !z) return fail(E_ARG, "mrl_head_rows: null pointer");
+  if (head < MRL_HEAD_LINEAR || head > MRL_HEAD_GAUSS) return fail(E_ARG, "bad head kind");
+  if (n_out < 1 || n_out > MRL_LAYERED_MAX_OUT) return fail(E_UNSUPPORTED, "n_out must be in [1, 32]");
+  if (head == MRL_HEAD_LINEAR && n_out != 1) return fail(E_ARG, "linear head needs n_out=1");
+  if (head == MRL_HEAD_GAUSS && !logstd) return fail(E_ARG, "DiagGauss needs logstd");
+  switch (epi) {
+    case MRL_EPI_PROB:
+      if (!io->out) return fail(E_ARG, "EPI_PROB needs out");
+      break;
+    case MRL_EPI_LOSSES:
+    case MRL_EPI_SURRGRAD:
+      if (head == MRL_HEAD_LINEAR) return fail(E_ARG, "policy epilogue on a value net");
+      if (!io->act || !io->adv || !io->oldprob || !io->partial) return fail(E_ARG, "losses need act/adv/oldprob/partial");
+      if (epi == MRL_EPI_SURRGRAD && !io->ghead) return fail(E_ARG, "SURRGRAD needs ghead");
+      break;
+    case MRL_EPI_VFLOSS:
+      if (head != MRL_HEAD_LINEAR || !io->target || !io->ghead || !io->partial)
+        return fail(E_ARG, "VFLOSS needs a linear head, target, ghead, partial");
+      break;
+    case MRL_EPI_FVP:
+      if (!dz || !io->ghead) return fail(E_ARG, "FVP needs dz, ghead");
+      if (head == MRL_HEAD_GAUSS && !dlogstd) return fail(E_ARG, "DiagGauss FVP needs dlogstd");
+      break;
+    default:
+      return fail(E_ARG, "unknown epilogue");
+  }
+  if (io->n <= 0) return OK;
+  RowsArgs a{};
+  a.head = head;
+  a.A = n_out;
+  a.gh = head == MRL_HEAD_GAUSS ? 2 * n_out : n_out;
+  a.n = io->n;
+  a.inv_ng = io->inv_n_global;
+  a.act = io->act;
+  a.adv = io->adv;
+  a.oldprob = io->oldprob;
+  a.target = io->target;
+  a.out = io->out;
+  a.ghead = io->ghead;
+  a.partial = io->partial;
+  a.logstd = head == MRL_HEAD_GAUSS ? logstd : nullptr;
+  a.dlogstd = head == MRL_HEAD_GAUSS ? dlogstd : nullptr;
+  const dim3 grid((unsigned)(mrl_partial_rows(io->n) / 4));
+  if (n_out <= 8) launch_head<8>(epi, grid, (hipStream_t)stream, a, z, dz, skip);
+  else launch_head<MRL_LAYERED_MAX_OUT>(epi, grid, (hipStream_t)stream, a, z, dz, skip);
+  return hip_check(hipGetLastError(), "mrl_head_rows");
+}
+
+int mrl_concat_time(const float* obs, const int32_t* ep_t, int64_t n, int32_t n_obs, double timestep_limit, float* X,
+                    void* stream) {
+  if (!obs || !ep_t || !X) return fail(E_ARG, "null pointer");
+  if (n <= 0) return OK;
+  int64_t g = (n * (n_obs + 1) + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(concat_time_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, ep_t, n, n_obs,
+                     timestep_limit, X);
+  return hip_check(hipGetLastError(), "mrl_concat_time");
+}
+
+}  // extern "C"

@@ -17,6 +17,7 @@
 
 #include "../../include/mrl_hip.h"
 #include "mlp_device.h"
+#include "rows_epilogue.h"
 
 namespace mrl {
 
@@ -41,28 +42,6 @@ constexpr int SCR_FLOATS = 2 * 64 * IMG_PAD;  // per-wave transpose scratch
 
 static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-struct RowsArgs {
-  MlpDims d;
-  int head, n_obs, gh;
-  const float* x;
-  const int32_t* ept;
-  double ts_limit;
-  int64_t n;
-  double inv_ng;
-  const void* act;
-  const float* adv;
-  const float* oldprob;
-  const float* target;
-  float* out;
-  float* ghead;
-  double* partial;
-  const float* logstd;   // theta + tls (DiagGauss) or nullptr
-  const float* dlogstd;  // tangent + tls (EPI_FVP, DiagGauss) or nullptr
-};
-
-constexpr float LOG2PI_F = 1.8378770664093453f;
-constexpr float LOG2PIE_F = 2.8378770664093453f;
-
 template <int EPI>
 // 2 waves/SIMD: layer 2 is evaluated one M-tile at a time so the chain fits 256 registers
 __global__ __launch_bounds__(ROWS_BLOCK, 2) void mlp_rows_kernel(RowsArgs a, const float* __restrict__ img,
@@ -81,7 +60,7 @@ __global__ __launch_bounds__(ROWS_BLOCK, 2) void mlp_rows_kernel(RowsArgs a, con
   const float* ldt = lds + fs;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
-  const int A = d.A;
+  const int A = a.A;
   float ls[MAX_OUT], sd[MAX_OUT], dls[MAX_OUT];
 #pragma unroll
   for (int j = 0; j < MAX_OUT; ++j) {
@@ -100,99 +79,7 @@ __global__ __launch_bounds__(ROWS_BLOCK, 2) void mlp_rows_kernel(RowsArgs a, con
     else forward_head_lowreg(lds, d, xl, lane, z);
     if (!valid || h != 0) continue;
 
-    if (EPI == MRL_EPI_PROB) {
-      if (a.head == MRL_HEAD_LINEAR) {
-        a.out[row] = z[0];
-      } else if (a.head == MRL_HEAD_SOFTMAX) {
-        float m = z[0];
-        for (int j = 1; j < A; ++j) m = fmaxf(m, z[j]);
-        float e[MAX_OUT], s = 0.f;
-        for (int j = 0; j < A; ++j) { e[j] = expf(z[j] - m); s += e[j]; }
-        for (int j = 0; j < A; ++j) a.out[row * A + j] = e[j] / s;
-      } else {
-        for (int j = 0; j < A; ++j) {
-          a.out[row * 2 * A + j] = z[j];
-          a.out[row * 2 * A + A + j] = sd[j];
-        }
-      }
-    } else if (EPI == MRL_EPI_LOSSES || EPI == MRL_EPI_SURRGRAD) {
-      const float advr = a.adv[row];
-      if (a.head == MRL_HEAD_SOFTMAX) {
-        // Categorical: loglik core.py:349-353, kl 355-356, entropy 358-359
-        float m = z[0];
-        for (int j = 1; j < A; ++j) m = fmaxf(m, z[j]);
-        float p[MAX_OUT], s = 0.f;
-        for (int j = 0; j < A; ++j) { p[j] = expf(z[j] - m); s += p[j]; }
-        for (int j = 0; j < A; ++j) p[j] = p[j] / s;
-        const int act = reinterpret_cast<const int32_t*>(a.act)[row];
-        const float* op = a.oldprob + row * A;
-        float pa = 0.f, opa = 0.f, kl = 0.f, ent = 0.f;
-        for (int j = 0; j < A; ++j) {
-          if (j == act) { pa = p[j]; opa = op[j]; }
-          kl += op[j] * logf(op[j] / p[j]);
-          ent -= p[j] * logf(p[j]);
-        }
-        const float ratio = expf(logf(pa) - logf(opa));
-        acc0 += (double)(ratio * advr);
-        acc1 += (double)kl;
-        acc2 += (double)ent;
-        if (EPI == MRL_EPI_SURRGRAD) {
-          const float w = (float)(-a.inv_ng) * ratio * advr;
-          for (int j = 0; j < A; ++j) a.ghead[row * a.gh + j] = w * ((j == act ? 1.f : 0.f) - p[j]);
-        }
-      } else {
-        // DiagGauss: loglik core.py:412-416, kl 421-426, entropy 428-430
-        const float* ac = reinterpret_cast<const float*>(a.act) + row * A;
-        const float* op = a.oldprob + row * 2 * A;
-        float q = 0.f, q0 = 0.f, sls = 0.f, sls0 = 0.f, kl = 0.f, u[MAX_OUT];
-        for (int j = 0; j < A; ++j) {
-          const float m0 = op[j], s0 = op[A + j];
-          u[j] = (ac[j] - z[j]) / sd[j];
-          const float u0 = (ac[j] - m0) / s0;
-          q += u[j] * u[j];
-          q0 += u0 * u0;
-          sls += ls[j];
-          sls0 += logf(s0);
-          const float dm = m0 - z[j];
-          kl += logf(sd[j] / s0) + (s0 * s0 + dm * dm) / (2.f * sd[j] * sd[j]);
-        }
-        kl -= 0.5f * A;
-        const float logp = -0.5f * q - 0.5f * LOG2PI_F * A - sls;
-        const float oldlogp = -0.5f * q0 - 0.5f * LOG2PI_F * A - sls0;
-        const float ratio = expf(logp - oldlogp);
-        acc0 += (double)(ratio * advr);
-        acc1 += (double)kl;
-        acc2 += (double)(sls + 0.5f * LOG2PIE_F * A);
-        if (EPI == MRL_EPI_SURRGRAD) {
-          const float w = (float)(-a.inv_ng) * ratio * advr;
-          for (int j = 0; j < A; ++j) {
-            a.ghead[row * a.gh + j] = w * u[j] / sd[j];
-            a.ghead[row * a.gh + A + j] = w * (u[j] * u[j] - 1.f);
-          }
-        }
-      }
-    } else if (EPI == MRL_EPI_VFLOSS) {
-      const float err = z[0] - a.target[row];
-      acc0 += (double)err * (double)err;
-      a.ghead[row] = (float)(2.0 * a.inv_ng) * err;
-    } else if (EPI == MRL_EPI_FVP) {
-      const float s = (float)a.inv_ng;
-      if (a.head == MRL_HEAD_SOFTMAX) {
-        float m = z[0];
-        for (int j = 1; j < A; ++j) m = fmaxf(m, z[j]);
-        float p[MAX_OUT], se = 0.f, pd = 0.f;
-        for (int j = 0; j < A; ++j) { p[j] = expf(z[j] - m); se += p[j]; }
-        for (int j = 0; j < A; ++j) { p[j] = p[j] / se; pd += p[j] * dz[j]; }
-        for (int j = 0; j < A; ++j) a.ghead[row * a.gh + j] = p[j] * (dz[j] - pd) * s;
-      } else if (a.head == MRL_HEAD_GAUSS) {
-        for (int j = 0; j < A; ++j) {
-          a.ghead[row * a.gh + j] = dz[j] / (sd[j] * sd[j]) * s;
-          a.ghead[row * a.gh + A + j] = 2.f * dls[j] * s;
-        }
-      } else {
-        a.ghead[row * a.gh] = dz[0] * s;
-      }
-    }
+    row_epilogue<EPI, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
   }
   if (a.partial != nullptr) {
     acc0 = wave_sum(acc0);
@@ -561,6 +448,7 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
   a.head = d->head;
   a.n_obs = d->n_in - (io->ep_t ? 1 : 0);
   a.gh = d->head == MRL_HEAD_GAUSS ? 2 * d->n_out : d->n_out;
+  a.A = d->n_out;
   a.x = io->x;
   a.ept = io->ep_t;
   a.ts_limit = io->timestep_limit;

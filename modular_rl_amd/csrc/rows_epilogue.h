@@ -1,0 +1,134 @@
+// Per-row epilogues shared by the fused 64-wide rows kernel (mlp_kernels.hip) and the
+// layered-path head kernel (gemm.hip): given the head pre-activation z (and its
+// tangent dz for the Fisher product) of one row, produce prob rows, the surrogate /
+// KL / entropy partial sums, the head-gradient row, or the VF squared error.
+#pragma once
+#include "../../include/mrl_hip.h"
+#include "mlp_layout.h"
+
+namespace mrl {
+
+struct RowsArgs {
+  MlpDims d;
+  int head, n_obs, gh, A;
+  const float* x;
+  const int32_t* ept;
+  double ts_limit;
+  int64_t n;
+  double inv_ng;
+  const void* act;
+  const float* adv;
+  const float* oldprob;
+  const float* target;
+  float* out;
+  float* ghead;
+  double* partial;
+  const float* logstd;   // theta + tls (DiagGauss) or nullptr
+  const float* dlogstd;  // tangent + tls (EPI_FVP, DiagGauss) or nullptr
+};
+
+constexpr float LOG2PI_F = 1.8378770664093453f;
+constexpr float LOG2PIE_F = 2.8378770664093453f;
+
+template <int EPI, int MA>
+__device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, const float (&z)[MA],
+                                             const float (&dz)[MA], const float (&ls)[MA], const float (&sd)[MA],
+                                             const float (&dls)[MA], double& acc0, double& acc1, double& acc2) {
+  const int A = a.A;
+  if (EPI == MRL_EPI_PROB) {
+    if (a.head == MRL_HEAD_LINEAR) {
+      a.out[row] = z[0];
+    } else if (a.head == MRL_HEAD_SOFTMAX) {
+      float m = z[0];
+      for (int j = 1; j < A; ++j) m = fmaxf(m, z[j]);
+      float e[MA], s = 0.f;
+      for (int j = 0; j < A; ++j) { e[j] = expf(z[j] - m); s += e[j]; }
+      for (int j = 0; j < A; ++j) a.out[row * A + j] = e[j] / s;
+    } else {
+      for (int j = 0; j < A; ++j) {
+        a.out[row * 2 * A + j] = z[j];
+        a.out[row * 2 * A + A + j] = sd[j];
+      }
+    }
+  } else if (EPI == MRL_EPI_LOSSES || EPI == MRL_EPI_SURRGRAD) {
+    const float advr = a.adv[row];
+    if (a.head == MRL_HEAD_SOFTMAX) {
+      // Categorical: loglik core.py:349-353, kl 355-356, entropy 358-359
+      float m = z[0];
+      for (int j = 1; j < A; ++j) m = fmaxf(m, z[j]);
+      float p[MA], s = 0.f;
+      for (int j = 0; j < A; ++j) { p[j] = expf(z[j] - m); s += p[j]; }
+      for (int j = 0; j < A; ++j) p[j] = p[j] / s;
+      const int act = reinterpret_cast<const int32_t*>(a.act)[row];
+      const float* op = a.oldprob + row * A;
+      float pa = 0.f, opa = 0.f, kl = 0.f, ent = 0.f;
+      for (int j = 0; j < A; ++j) {
+        if (j == act) { pa = p[j]; opa = op[j]; }
+        kl += op[j] * logf(op[j] / p[j]);
+        ent -= p[j] * logf(p[j]);
+      }
+      const float ratio = expf(logf(pa) - logf(opa));
+      acc0 += (double)(ratio * advr);
+      acc1 += (double)kl;
+      acc2 += (double)ent;
+      if (EPI == MRL_EPI_SURRGRAD) {
+        const float w = (float)(-a.inv_ng) * ratio * advr;
+        for (int j = 0; j < A; ++j) a.ghead[row * a.gh + j] = w * ((j == act ? 1.f : 0.f) - p[j]);
+      }
+    } else {
+      // DiagGauss: loglik core.py:412-416, kl 421-426, entropy 428-430
+      const float* ac = reinterpret_cast<const float*>(a.act) + row * A;
+      const float* op = a.oldprob + row * 2 * A;
+      float q = 0.f, q0 = 0.f, sls = 0.f, sls0 = 0.f, kl = 0.f, u[MA];
+      for (int j = 0; j < A; ++j) {
+        const float m0 = op[j], s0 = op[A + j];
+        u[j] = (ac[j] - z[j]) / sd[j];
+        const float u0 = (ac[j] - m0) / s0;
+        q += u[j] * u[j];
+        q0 += u0 * u0;
+        sls += ls[j];
+        sls0 += logf(s0);
+        const float dm = m0 - z[j];
+        kl += logf(sd[j] / s0) + (s0 * s0 + dm * dm) / (2.f * sd[j] * sd[j]);
+      }
+      kl -= 0.5f * A;
+      const float logp = -0.5f * q - 0.5f * LOG2PI_F * A - sls;
+      const float oldlogp = -0.5f * q0 - 0.5f * LOG2PI_F * A - sls0;
+      const float ratio = expf(logp - oldlogp);
+      acc0 += (double)(ratio * advr);
+      acc1 += (double)kl;
+      acc2 += (double)(sls + 0.5f * LOG2PIE_F * A);
+      if (EPI == MRL_EPI_SURRGRAD) {
+        const float w = (float)(-a.inv_ng) * ratio * advr;
+        for (int j = 0; j < A; ++j) {
+          a.ghead[row * a.gh + j] = w * u[j] / sd[j];
+          a.ghead[row * a.gh + A + j] = w * (u[j] * u[j] - 1.f);
+        }
+      }
+    }
+  } else if (EPI == MRL_EPI_VFLOSS) {
+    const float err = z[0] - a.target[row];
+    acc0 += (double)err * (double)err;
+    a.ghead[row] = (float)(2.0 * a.inv_ng) * err;
+  } else if (EPI == MRL_EPI_FVP) {
+    // GGN metric of the KL at the old policy (== Theano's double backprop, trpo.py:45-58)
+    const float s = (float)a.inv_ng;
+    if (a.head == MRL_HEAD_SOFTMAX) {
+      float m = z[0];
+      for (int j = 1; j < A; ++j) m = fmaxf(m, z[j]);
+      float p[MA], se = 0.f, pd = 0.f;
+      for (int j = 0; j < A; ++j) { p[j] = expf(z[j] - m); se += p[j]; }
+      for (int j = 0; j < A; ++j) { p[j] = p[j] / se; pd += p[j] * dz[j]; }
+      for (int j = 0; j < A; ++j) a.ghead[row * a.gh + j] = p[j] * (dz[j] - pd) * s;
+    } else if (a.head == MRL_HEAD_GAUSS) {
+      for (int j = 0; j < A; ++j) {
+        a.ghead[row * a.gh + j] = dz[j] / (sd[j] * sd[j]) * s;
+        a.ghead[row * a.gh + A + j] = 2.f * dls[j] * s;
+      }
+    } else {
+      a.ghead[row * a.gh] = dz[0] * s;
+    }
+  }
+}
+
+}  // namespace mrl

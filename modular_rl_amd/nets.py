@@ -1,9 +1,19 @@
-"""Device MLP nets: flat fp32 theta + packed LDS image, driven through libmrl_hip.
+"""Device MLP nets: flat fp32 theta driven through libmrl_hip.
 
 Replaces the Keras ``Sequential`` + Theano function machinery of the reference
 (`agentzoo.py:25-60`, `core.py:296-336`, `core.py:518-557`): parameters live in
-one flat device vector in Keras ``trainable_weights`` order, and every pass over
-a batch is one fused HIP launch (``mrl_mlp_rows`` / ``mrl_mlp_vjp``).
+one flat device vector in Keras ``trainable_weights`` order.  Two device
+implementations share one interface (``rows`` / ``vjp_flat`` / ``forward``):
+
+* ``MlpNet`` -- hid_sizes [64, 64], n_in <= 32, n_out <= 8 (CartPole, Hopper):
+  every pass over a batch is one fused launch (``mrl_mlp_rows`` / ``mrl_mlp_vjp``)
+  with the weights resident in LDS as a packed image.
+* ``LayeredMlpNet`` -- any hid_sizes / widths (Humanoid 376-512-512-512-17): each
+  Dense layer is one tiled MFMA GEMM over all rows (``mrl_gemm``), the head
+  epilogue is ``mrl_head_rows``; the forward activations of the last recording pass
+  are kept as a tape so the Fisher products of one update reuse them.
+
+``make_net`` picks the fused path whenever the shape allows it.
 """
 import ctypes
 
@@ -17,17 +27,37 @@ HIDDEN = 64
 N_LAYERS = 2
 
 
+MAX_OUT_LAYERED = 32
+FUSED_MAX_IN, FUSED_MAX_OUT = 32, 8
+
+
 def check_hid_sizes(hid_sizes):
-    hid = list(hid_sizes)
-    if hid != [HIDDEN] * N_LAYERS:
-        raise MrlError(f"hid_sizes={hid} is not implemented on the HIP path (only [64, 64]); "
-                       "there is no CPU fallback")
+    hid = [int(h) for h in hid_sizes]
+    if len(hid) < 1 or min(hid) < 1:
+        raise MrlError(f"hid_sizes={hid}: need at least one hidden layer of positive width")
+    return hid
 
 
-def glorot_init(rng, n_in, n_out, head):
+def fused_ok(n_in, n_out, hid_sizes):
+    return list(hid_sizes) == [HIDDEN] * N_LAYERS and n_in <= FUSED_MAX_IN and n_out <= FUSED_MAX_OUT
+
+
+def make_net(n_in, n_out, head, hid_sizes=(HIDDEN,) * N_LAYERS, impl="auto", device="cuda"):
+    """Fused 64-wide net when the shape allows it (impl="auto"), else the layered net."""
+    hid = check_hid_sizes(hid_sizes)
+    if impl not in ("auto", "fused", "layered"):
+        raise MrlError(f"mlp impl {impl!r}: expected auto, fused or layered")
+    if impl == "fused" or (impl == "auto" and fused_ok(n_in, n_out, hid)):
+        if not fused_ok(n_in, n_out, hid):
+            raise MrlError(f"fused MLP path needs hid_sizes=[64, 64], n_in<=32, n_out<=8 (got {hid}, {n_in}, {n_out})")
+        return MlpNet(n_in, n_out, head, device=device)
+    return LayeredMlpNet(n_in, n_out, head, hid, device=device)
+
+
+def glorot_init(rng, n_in, n_out, head, hid_sizes=(HIDDEN,) * N_LAYERS):
     """Keras glorot-uniform kernels, zero biases, last kernel x0.1, logstd 0 (`agentzoo.py:34-48`)."""
     arrs = []
-    dims = [n_in] + [HIDDEN] * N_LAYERS + [n_out]
+    dims = [n_in] + list(hid_sizes) + [n_out]
     for i in range(len(dims) - 1):
         lim = np.sqrt(6.0 / (dims[i] + dims[i + 1]))
         W = rng.uniform(-lim, lim, size=(dims[i], dims[i + 1]))
@@ -57,6 +87,8 @@ class Workspace:
 class MlpNet:
     """tanh MLP n_in -> 64 -> 64 -> n_out with a linear / softmax / DiagGauss head."""
 
+    layered = False
+
     def __init__(self, n_in, n_out, head, device="cuda"):
         self.lib = _lib.load(require_gpu=True)
         self.desc = _lib.MlpDesc(n_in, n_out, head, HIDDEN, N_LAYERS)
@@ -70,6 +102,7 @@ class MlpNet:
         self.theta = torch.zeros(self.P, dtype=torch.float32, device=self.device)
         self.image = torch.zeros(self.image_floats, dtype=torch.float32, device=self.device)
         self.gh = 2 * n_out if head == _lib.HEAD_GAUSS else n_out
+        self.hid_sizes = [HIDDEN] * N_LAYERS
         self.ws = Workspace(self.device)
 
     # ---- flat parameter plumbing (GetFlat / SetFromFlat, core.py:518-557)
@@ -117,6 +150,211 @@ class MlpNet:
 
     def forward(self, x, n, ep_t=None, timestep_limit=1.0, out=None):
         """prob rows (policy) or values (VF) for n rows of x."""
+        width = 1 if self.head == _lib.HEAD_LINEAR else self.gh
+        if out is None:
+            out = torch.empty((int(n), width) if width > 1 else (int(n),), dtype=torch.float32, device=self.device)
+        self.rows(_lib.EPI_PROB, x, n, ep_t=ep_t, timestep_limit=timestep_limit, out=out)
+        return out
+
+
+def layer_offsets(dims, gauss):
+    """Flat-theta offsets of each Dense layer's W [d_in, d_out] and b, of logstd, and P."""
+    w_off, b_off, off = [], [], 0
+    for i in range(len(dims) - 1):
+        w_off.append(off)
+        off += dims[i] * dims[i + 1]
+        b_off.append(off)
+        off += dims[i + 1]
+    tls = off
+    return w_off, b_off, tls, off + (dims[-1] if gauss else 0)
+
+
+class LayeredMlpNet:
+    """tanh MLP n_in -> hid_sizes... -> n_out on the layered GEMM path (any widths).
+
+    Flat theta layout (Keras trainable_weights order, core.py:518-557): for each Dense
+    layer W [d_in, d_out] row-major then b [d_out]; DiagGauss appends logstd [n_out].
+    ``image`` is a placeholder (the layered kernels read theta directly), so callers
+    that pack images (HipTrpoOps) work unchanged."""
+
+    layered = True
+    SLAB_SPLITS = 64
+
+    def __init__(self, n_in, n_out, head, hid_sizes, device="cuda"):
+        self.lib = _lib.load(require_gpu=True)
+        if not 1 <= n_out <= MAX_OUT_LAYERED:
+            raise MrlError(f"n_out={n_out}: the layered head supports 1..{MAX_OUT_LAYERED} outputs")
+        if head == _lib.HEAD_LINEAR and n_out != 1:
+            raise MrlError("linear head needs n_out=1")
+        self.n_in, self.n_out, self.head = int(n_in), int(n_out), head
+        self.hid_sizes = check_hid_sizes(hid_sizes)
+        self.dims = [self.n_in] + self.hid_sizes + [self.n_out]
+        self.w_off, self.b_off, self.tls, self.P = layer_offsets(self.dims, head == _lib.HEAD_GAUSS)
+        self.device = torch.device(device)
+        self.theta = torch.zeros(self.P, dtype=torch.float32, device=self.device)
+        self.image = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.gh = 2 * n_out if head == _lib.HEAD_GAUSS else n_out
+        self.ws = Workspace(self.device)
+        self.desc = None
+        self._tape = None  # (key, X, ldx, [H_1..H_L], Z)
+
+    # ---- flat parameter plumbing
+    def get_flat(self):
+        return self.theta.detach().cpu().numpy().copy()
+
+    def set_flat(self, th):
+        th = torch.as_tensor(np.asarray(th), dtype=torch.float32)
+        self.theta.copy_(th.to(self.device))
+        self._tape = None
+
+    def pack(self, theta=None, image=None, fwd_only=False, skip=None):
+        """No image on the layered path: the GEMMs read theta directly."""
+
+    def partial_rows(self, n):
+        return int(self.lib.mrl_partial_rows(int(n)))
+
+    def reduce_partial(self, partial, n, out):
+        call("mrl_reduce_rows_f64", ptr(partial), self.partial_rows(n), 4, ptr(out), None, stream())
+        return out
+
+    # ---- GEMM helpers
+    @staticmethod
+    def _addr(t, off=0):
+        return None if t is None else ctypes.c_void_p(t.data_ptr() + 4 * off)
+
+    def _gemm(self, m, n, k, a, lda, b, ldb, c, ldc, a_trans=0, b_trans=0, epi=0, a2=None, b2=None, bias=None,
+              h=None, ldh=0, ones_row=0, splits=1, slab_stride=0, skip=None):
+        g = _lib.GemmDesc(m=m, n=n, k=k, a=a, lda=lda, a_trans=a_trans, ones_row=ones_row, b=b, ldb=ldb,
+                          b_trans=b_trans, epilogue=epi, a2=a2, b2=b2, c=c, ldc=ldc, bias=bias, h=h, ldh=ldh,
+                          splits=splits, slab_stride=slab_stride)
+        call("mrl_gemm", ctypes.byref(g), ptr(skip), stream())
+
+    def _input(self, x, n, ep_t, timestep_limit, name="x_time"):
+        """(X, ldx): obs rows, or [obs, t/limit] materialised for a value net."""
+        if ep_t is None:
+            return x, self.n_in
+        X = self.ws.get(name, n * self.n_in, torch.float32)
+        call("mrl_concat_time", ptr(x), ptr(ep_t), int(n), self.n_in - 1, float(timestep_limit), ptr(X), stream())
+        return X, self.n_in
+
+    def _forward(self, X, ldx, n, theta, bufs, zbuf, skip=None):
+        """H_l = tanh(H_{l-1} W + b) ... Z = H_L W + b into bufs[l] / zbuf."""
+        L = len(self.dims) - 1
+        a, lda = self._addr(X), ldx
+        for l in range(L):
+            din, dout = self.dims[l], self.dims[l + 1]
+            last = l == L - 1
+            out = zbuf if last else bufs[l]
+            self._gemm(n, dout, din, a, lda, self._addr(theta, self.w_off[l]), dout, self._addr(out), dout,
+                       epi=_lib.GEMM_STORE if last else _lib.GEMM_TANH, bias=self._addr(theta, self.b_off[l]),
+                       skip=skip)
+            a, lda = self._addr(out), dout
+
+    def _key(self, theta, x, n, ep_t):
+        return (theta.data_ptr(), theta._version, x.data_ptr(), int(n), None if ep_t is None else ep_t.data_ptr())
+
+    def _record(self, x, n, ep_t, timestep_limit, theta):
+        """Forward pass at theta kept as the tape the next vjp_flat / FVP uses."""
+        key = self._key(theta, x, n, ep_t)
+        X, ldx = self._input(x, n, ep_t, timestep_limit, name="tape_x")
+        H = [self.ws.get(f"tape_h{l}", n * d, torch.float32) for l, d in enumerate(self.hid_sizes)]
+        Z = self.ws.get("tape_z", n * self.n_out, torch.float32)
+        self._forward(X, ldx, n, theta, H, Z)
+        self._tape = (key, X, ldx, H, Z, theta)
+        return self._tape
+
+    def _scratch(self, n):
+        w = max(self.hid_sizes)
+        return [self.ws.get(f"scr{i}", n * w, torch.float32) for i in range(2)]
+
+    def rows(self, epi, x, n, ep_t=None, timestep_limit=1.0, inv_n_global=1.0, act=None, adv=None, oldprob=None,
+             target=None, out=None, ghead=None, partial=None, theta=None, image=None, tangent=None, image_t=None,
+             skip=None):
+        n = int(n)
+        theta = self.theta if theta is None else theta
+        io = _lib.RowsIO(ptr(x), ptr(ep_t), float(timestep_limit), n, float(inv_n_global), ptr(act), ptr(adv),
+                         ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial))
+        dz = None
+        if epi == _lib.EPI_FVP:
+            if tangent is None:
+                raise MrlError("EPI_FVP needs a tangent")
+            tape = self._tape
+            if tape is None or tape[0] != self._key(theta, x, n, ep_t):
+                tape = self._record(x, n, ep_t, timestep_limit, theta)
+            _, X, ldx, H, Z, _ = tape
+            dz = self.ws.get("tape_dz", n * self.n_out, torch.float32)
+            self._jvp(X, ldx, n, theta, tangent, H, dz, skip)
+        elif epi in (_lib.EPI_SURRGRAD, _lib.EPI_VFLOSS):
+            _, X, ldx, H, Z, _ = self._record(x, n, ep_t, timestep_limit, theta)
+        else:
+            if n == 0:
+                return
+            X, ldx = self._input(x, n, ep_t, timestep_limit)
+            Z = self.ws.get("fwd_z", n * self.n_out, torch.float32)
+            s0, s1 = self._scratch(n)
+            bufs = [s0 if l % 2 == 0 else s1 for l in range(len(self.hid_sizes))]
+            self._forward(X, ldx, n, theta, bufs, Z, skip)
+        gauss = self.head == _lib.HEAD_GAUSS
+        call("mrl_head_rows", int(self.head), self.n_out, int(epi), ptr(Z), ptr(dz),
+             self._addr(theta, self.tls) if gauss else None,
+             self._addr(tangent, self.tls) if (gauss and tangent is not None) else None,
+             ctypes.byref(io), ptr(skip), stream())
+
+    def _jvp(self, X, ldx, n, theta, tangent, H, dz, skip):
+        """dH_1 = (X dW0 + db0)(1-H_1^2); dH_l = (dH W + H dW + db)(1-H_l^2); dZ = dH_L W + H_L dW + db."""
+        L = len(self.dims) - 1
+        scr = self._scratch(n)
+        prev_d = None  # dH of the previous layer
+        for l in range(L):
+            din, dout = self.dims[l], self.dims[l + 1]
+            last = l == L - 1
+            outb = dz if last else scr[l % 2]
+            epi = _lib.GEMM_STORE if last else _lib.GEMM_DTANH
+            W = self._addr(theta, self.w_off[l])
+            dW = self._addr(tangent, self.w_off[l])
+            db = self._addr(tangent, self.b_off[l])
+            h = None if last else self._addr(H[l])
+            if l == 0:
+                self._gemm(n, dout, din, self._addr(X), ldx, dW, dout, self._addr(outb), dout, epi=epi, bias=db,
+                           h=h, ldh=dout, skip=skip)
+            else:
+                self._gemm(n, dout, din, self._addr(prev_d), din, W, dout, self._addr(outb), dout, epi=epi,
+                           a2=self._addr(H[l - 1]), b2=dW, bias=db, h=h, ldh=dout, skip=skip)
+            prev_d = outb
+
+    def vjp_flat(self, x, n, ghead, out, ep_t=None, timestep_limit=1.0, image=None, skip=None):
+        """out[P] (fp32) <- sum_n J_n^T ghead_n at the tape's theta (split-K slabs + fixed-order reduce)."""
+        n = int(n)
+        tape = self._tape
+        if tape is None or tape[0][2:] != (x.data_ptr(), n, None if ep_t is None else ep_t.data_ptr()):
+            raise MrlError("LayeredMlpNet.vjp_flat needs a preceding recording rows() pass on the same rows")
+        _, X, ldx, H, Z, theta = tape
+        S = int(self.lib.mrl_gemm_slab_splits(n, self.SLAB_SPLITS))
+        slab = self.ws.get("slab", S * self.P, torch.float32)
+        L = len(self.dims) - 1
+        scr = self._scratch(n)
+        G, ldg = ghead, self.gh
+        for l in reversed(range(L)):
+            din, dout = self.dims[l], self.dims[l + 1]
+            inp = X if l == 0 else H[l - 1]
+            # [dW; db] = [inp, 1]^T G  (K = rows, split over S slabs)
+            self._gemm(din + 1, dout, n, self._addr(inp), din if l else ldx, self._addr(G), ldg,
+                       self._addr(slab, self.w_off[l]), dout, a_trans=1, epi=_lib.GEMM_SLAB, ones_row=1,
+                       splits=self.SLAB_SPLITS, slab_stride=self.P, skip=skip)
+            if l > 0:
+                Gn = scr[l % 2]
+                self._gemm(n, din, dout, self._addr(G), ldg, self._addr(theta, self.w_off[l]), dout,
+                           self._addr(Gn), din, b_trans=1, epi=_lib.GEMM_DTANH, h=self._addr(H[l - 1]), ldh=din,
+                           skip=skip)
+                G, ldg = Gn, din
+        if self.head == _lib.HEAD_GAUSS:
+            A = self.n_out
+            self._gemm(1, A, n, None, 0, self._addr(ghead, A), self.gh, self._addr(slab, self.tls), A, a_trans=1,
+                       epi=_lib.GEMM_SLAB, ones_row=1, splits=self.SLAB_SPLITS, slab_stride=self.P, skip=skip)
+        call("mrl_reduce_rows_f32", ptr(slab), S, self.P, ptr(out), ptr(skip), stream())
+        return out
+
+    def forward(self, x, n, ep_t=None, timestep_limit=1.0, out=None):
         width = 1 if self.head == _lib.HEAD_LINEAR else self.gh
         if out is None:
             out = torch.empty((int(n), width) if width > 1 else (int(n),), dtype=torch.float32, device=self.device)

@@ -7,6 +7,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 import torch
 
@@ -44,8 +45,10 @@ def test_ctypes_struct_layout_matches_c(tmp_path):
 #include "mrl_hip.h"
 #define P(T, F) printf(#T "." #F " %zu\\n", offsetof(T, F));
 int main(void) {
-  printf("mrl_mlp_desc %zu\\nmrl_rows_io %zu\\nmrl_rollout_desc %zu\\nmrl_rollout_bufs %zu\\n",
-         sizeof(mrl_mlp_desc), sizeof(mrl_rows_io), sizeof(mrl_rollout_desc), sizeof(mrl_rollout_bufs));
+  printf("mrl_mlp_desc %zu\\nmrl_rows_io %zu\\nmrl_rollout_desc %zu\\nmrl_rollout_bufs %zu\\nmrl_gemm_desc %zu\\n",
+         sizeof(mrl_mlp_desc), sizeof(mrl_rows_io), sizeof(mrl_rollout_desc), sizeof(mrl_rollout_bufs),
+         sizeof(mrl_gemm_desc));
+  P(mrl_gemm_desc, ones_row) P(mrl_gemm_desc, epilogue) P(mrl_gemm_desc, ldh) P(mrl_gemm_desc, slab_stride)
   P(mrl_rows_io, timestep_limit) P(mrl_rows_io, n) P(mrl_rows_io, inv_n_global) P(mrl_rows_io, partial)
   P(mrl_rollout_desc, seed) P(mrl_rollout_bufs, noise)
   return 0;
@@ -64,6 +67,9 @@ int main(void) {
     assert int(out["mrl_rows_io.partial"]) == _lib.RowsIO.partial.offset
     assert int(out["mrl_rollout_desc.seed"]) == _lib.RolloutDesc.seed.offset
     assert int(out["mrl_rollout_bufs.noise"]) == _lib.RolloutBufs.noise.offset
+    assert int(out["mrl_gemm_desc"]) == ctypes.sizeof(_lib.GemmDesc)
+    for f in ("ones_row", "epilogue", "ldh", "slab_stride"):
+        assert int(out["mrl_gemm_desc." + f]) == getattr(_lib.GemmDesc, f).offset, f
 
 
 def test_host_queries_match_the_reference_parameter_layout():
@@ -92,9 +98,45 @@ def test_product_path_refuses_without_gpu():
         MlpNet(11, 3, _lib.HEAD_GAUSS)
 
 
-def test_unsupported_hidden_sizes_fail_loudly():
+def test_hidden_sizes_validation_and_path_choice():
     from modular_rl_amd import _lib
-    from modular_rl_amd.nets import check_hid_sizes
-    check_hid_sizes([64, 64])
-    with pytest.raises(_lib.MrlError):
-        check_hid_sizes([128, 128])
+    from modular_rl_amd.nets import check_hid_sizes, fused_ok
+    assert check_hid_sizes([64, 64]) == [64, 64]
+    assert check_hid_sizes(["512", 512, 512]) == [512, 512, 512]
+    for bad in ([], [64, 0]):
+        with pytest.raises(_lib.MrlError):
+            check_hid_sizes(bad)
+    assert fused_ok(11, 3, [64, 64]) and fused_ok(4, 2, [64, 64])
+    assert not fused_ok(376, 17, [512, 512, 512]) and not fused_ok(11, 3, [128, 128])
+    assert not fused_ok(40, 3, [64, 64]) and not fused_ok(11, 9, [64, 64])
+
+
+def test_layered_parameter_layout_matches_the_reference():
+    """LayeredMlpNet offsets follow Keras trainable_weights order (W, b per layer, logstd),
+    checked against the oracle's unflatten without touching the GPU."""
+    from modular_rl_amd.nets import layer_offsets
+    from oracle import trpo_np as T
+    for (nin, nout, name, hid) in [(376, 17, "gauss", [512, 512, 512]), (377, 1, "linear", [512, 512, 512]),
+                                   (6, 5, "softmax", [100, 50, 30])]:
+        spec = T.Spec(nin, hid, nout, name)
+        dims = [nin] + hid + [nout]
+        w_off, b_off, tls, P = layer_offsets(dims, name == "gauss")
+        assert P == spec.P
+        th = np.arange(spec.P, dtype=np.float64)
+        Ws, bs, logstd = spec.split(th)
+        for l in range(len(dims) - 1):
+            assert Ws[l].shape == (dims[l], dims[l + 1])
+            assert Ws[l].ravel()[0] == w_off[l] and bs[l].ravel()[0] == b_off[l]
+        if name == "gauss":
+            assert logstd.ravel()[0] == tls
+    # Humanoid policy 376-512-512-512-17 (+logstd): SURVEY §8 C5
+    assert T.Spec(376, [512, 512, 512], 17, "gauss").P == 376 * 512 + 512 + 2 * (512 * 512 + 512) + 512 * 17 + 17 + 17
+
+
+def test_gemm_refuses_bad_descriptors():
+    from modular_rl_amd import _lib
+    lib = _lib.load()
+    d = _lib.GemmDesc(m=4, n=4, k=4)
+    rc = lib.mrl_gemm(ctypes.byref(d), None, None)
+    assert rc < 0 and b"null" in lib.mrl_last_error()
+    assert lib.mrl_gemm_slab_splits(1000, 4) == 4 and lib.mrl_gemm_slab_splits(10, 64) == 1

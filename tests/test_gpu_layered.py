@@ -1,0 +1,226 @@
+"""GPU parity of the layered (tiled MFMA GEMM) MLP path against the float64 oracle:
+forward / losses / policy gradient / Fisher product / VF loss-grad for shapes the
+fused 64-wide kernels do not cover -- Humanoid 376-512-512-512-17,
+odd widths, one hidden layer, n_out > 8 -- plus the [64, 64] shape both paths run."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import trpo_np as T
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ("gauss", 11, 3, [64, 64]),
+    ("gauss", 376, 17, [512, 512, 512]),
+    ("softmax", 6, 5, [100, 50, 30]),
+    ("gauss", 20, 9, [130]),
+    ("softmax", 40, 12, [256, 96]),
+]
+IDS = ["hopper64", "humanoid512", "odd", "onelayer", "cat12"]
+
+
+def _net(head, nin, nout, hid):
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import LayeredMlpNet
+    h = {"gauss": _lib.HEAD_GAUSS, "softmax": _lib.HEAD_SOFTMAX, "linear": _lib.HEAD_LINEAR}[head]
+    return LayeredMlpNet(nin, nout, h, hid)
+
+
+def _setup(head, nin, nout, hid, N, seed=0):
+    rng = np.random.default_rng(seed)
+    spec = T.Spec(nin, hid, nout, head)
+    th = T.mlp_init(rng, spec.shapes, head == "gauss") + 0.02 * rng.standard_normal(spec.P)
+    if head == "gauss":
+        th[-nout:] = 0.3 * rng.standard_normal(nout)
+    th = th.astype(np.float32).astype(np.float64)
+    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
+    oldth = th + 0.005 * rng.standard_normal(spec.P)
+    oldprob = T.policy_prob(spec, oldth, ob).astype(np.float32).astype(np.float64)
+    noise = rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N)
+    act = T.sample(spec, oldprob, noise)
+    if head == "gauss":
+        act = act.astype(np.float32).astype(np.float64)
+    adv = rng.standard_normal(N).astype(np.float32).astype(np.float64)
+    return spec, th, ob, act, adv, oldprob
+
+
+def _dev(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).cuda()
+
+
+def _rel(a, b):
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+def test_make_net_dispatch():
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import LayeredMlpNet, MlpNet, make_net
+    assert isinstance(make_net(11, 3, _lib.HEAD_GAUSS, [64, 64]), MlpNet)
+    assert isinstance(make_net(376, 17, _lib.HEAD_GAUSS, [512, 512, 512]), LayeredMlpNet)
+    assert isinstance(make_net(11, 3, _lib.HEAD_GAUSS, [64, 64], impl="layered"), LayeredMlpNet)
+    assert isinstance(make_net(11, 3, _lib.HEAD_GAUSS, [32]), LayeredMlpNet)
+
+
+@pytest.mark.parametrize("head,nin,nout,hid", CASES, ids=IDS)
+@pytest.mark.parametrize("N", [1, 77, 1000])
+def test_forward_prob(head, nin, nout, hid, N):
+    spec, th, ob, *_ = _setup(head, nin, nout, hid, N)
+    net = _net(head, nin, nout, hid)
+    net.set_flat(th)
+    got = net.forward(_dev(ob), N).cpu().numpy().astype(np.float64)
+    want = T.policy_prob(spec, th, ob)
+    np.testing.assert_allclose(got, want, rtol=5e-5, atol=5e-6)
+
+
+@pytest.mark.parametrize("head,nin,nout,hid", CASES, ids=IDS)
+def test_losses_and_policy_gradient(head, nin, nout, hid):
+    from modular_rl_amd import _lib
+    N = 700
+    spec, th, ob, act, adv, oldprob = _setup(head, nin, nout, hid, N, seed=1)
+    net = _net(head, nin, nout, hid)
+    net.set_flat(th)
+    x = _dev(ob)
+    a = _dev(act, torch.int32 if head == "softmax" else torch.float32)
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    ghead = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(adv), oldprob=_dev(oldprob),
+             ghead=ghead, partial=partial)
+    sums = torch.zeros(4, dtype=torch.float64, device="cuda")
+    net.reduce_partial(partial, N, sums)
+    g = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(x, N, ghead, g)
+    s = sums.cpu().numpy()
+    losses = np.array([-s[0] / N, s[1] / N, s[2] / N])
+    want = T.surr_kl_ent(spec, th, ob, act, adv, oldprob)
+    np.testing.assert_allclose(losses, want, rtol=1e-4, atol=1e-6)
+    gw = T.policy_gradient(spec, th, ob, act, adv, oldprob)
+    assert _rel(g.cpu().numpy(), gw) < 1e-4
+    # LOSSES-only pass (line search) at another theta leaves the tape alone
+    partial.zero_()
+    th2 = torch.as_tensor(th * 1.01, dtype=torch.float32).cuda()
+    net.rows(_lib.EPI_LOSSES, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(adv), oldprob=_dev(oldprob),
+             partial=partial, theta=th2)
+    net.reduce_partial(partial, N, sums)
+    s = sums.cpu().numpy()
+    want2 = T.surr_kl_ent(spec, th2.double().cpu().numpy(), ob, act, adv, oldprob)
+    np.testing.assert_allclose(np.array([-s[0] / N, s[1] / N, s[2] / N]), want2, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("head,nin,nout,hid", CASES, ids=IDS)
+def test_fisher_vector_product(head, nin, nout, hid):
+    from modular_rl_amd import _lib
+    N = 600
+    spec, th, ob, *_ = _setup(head, nin, nout, hid, N, seed=2)
+    rng = np.random.default_rng(5)
+    net = _net(head, nin, nout, hid)
+    net.set_flat(th)
+    x = _dev(ob)
+    ghead = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+    fv = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    for rep in range(2):  # the second product reuses the recorded forward tape
+        v = rng.standard_normal(spec.P).astype(np.float32)
+        vt = _dev(v)
+        net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=ghead, tangent=vt)
+        net.vjp_flat(x, N, ghead, fv)
+        want = T.fisher_vector_product(spec, th, v.astype(np.float64), ob)
+        assert _rel(fv.cpu().numpy(), want) < 1e-4, rep
+
+
+def test_fvp_tape_follows_theta_updates():
+    from modular_rl_amd import _lib
+    head, nin, nout, hid = "gauss", 11, 3, [96, 48]
+    N = 300
+    spec, th, ob, *_ = _setup(head, nin, nout, hid, N, seed=4)
+    net = _net(head, nin, nout, hid)
+    net.set_flat(th)
+    x = _dev(ob)
+    ghead = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+    fv = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    v = np.random.default_rng(1).standard_normal(spec.P).astype(np.float32)
+    net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=ghead, tangent=_dev(v))
+    th3 = (th * 0.9).astype(np.float32).astype(np.float64)
+    net.theta.copy_(_dev(th3))  # in-place update, as TrpoUpdater does
+    net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=ghead, tangent=_dev(v))
+    net.vjp_flat(x, N, ghead, fv)
+    want = T.fisher_vector_product(spec, th3, v.astype(np.float64), ob)
+    assert _rel(fv.cpu().numpy(), want) < 1e-4
+
+
+@pytest.mark.parametrize("nin,hid", [(377, [512, 512, 512]), (12, [64, 64]), (30, [200])])
+def test_value_forward_and_loss_grad_with_time_feature(nin, hid):
+    from modular_rl_amd import _lib
+    N, limit = 900, 1000.0
+    rng = np.random.default_rng(3)
+    spec = T.Spec(nin, hid, 1, "linear")
+    th = (T.mlp_init(rng, spec.shapes, False) + 0.02 * rng.standard_normal(spec.P)).astype(np.float32).astype(np.float64)
+    obs = rng.standard_normal((N, nin - 1)).astype(np.float32)
+    ept = rng.integers(0, 1000, size=N).astype(np.int32)
+    X = np.concatenate([obs.astype(np.float64), (ept / limit).astype(np.float32).astype(np.float64)[:, None]], axis=1)
+    y = rng.standard_normal(N).astype(np.float32)
+    net = _net("linear", nin, 1, hid)
+    net.set_flat(th)
+    xo, et = _dev(obs), _dev(ept, torch.int32)
+    v = net.forward(xo, N, ep_t=et, timestep_limit=limit).cpu().numpy()
+    want_v = T.mlp_forward(spec, th, X)[0][:, 0]
+    np.testing.assert_allclose(v, want_v, rtol=5e-5, atol=5e-6)
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    ghead = torch.zeros(N, dtype=torch.float32, device="cuda")
+    net.rows(_lib.EPI_VFLOSS, xo, N, ep_t=et, timestep_limit=limit, inv_n_global=1.0 / N, target=_dev(y),
+             ghead=ghead, partial=partial)
+    sums = torch.zeros(4, dtype=torch.float64, device="cuda")
+    net.reduce_partial(partial, N, sums)
+    g = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(xo, N, ghead, g, ep_t=et, timestep_limit=limit)
+    loss, gw, mse, l2 = T.vf_loss_grad(spec, th, X, y.astype(np.float64))
+    np.testing.assert_allclose(sums[0].item() / N, mse, rtol=1e-5)
+    assert _rel(g.cpu().numpy() + 2e-3 * th, gw) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (130, 70, 33), (257, 129, 300)])
+def test_gemm_orientations_and_epilogues(M, N, K):
+    """mrl_gemm against torch fp64 for every operand orientation and epilogue."""
+    import ctypes
+    from modular_rl_amd import _lib
+    from modular_rl_amd._lib import call, stream
+    _lib.load(require_gpu=True)
+    g = torch.Generator().manual_seed(M * 7 + N)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(K, N, generator=g)
+    A2 = torch.randn(M, K, generator=g)
+    B2 = torch.randn(K, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    H = torch.rand(M, N, generator=g)
+    addr = lambda t: ctypes.c_void_p(t.data_ptr())
+    for at in (0, 1):
+        for bt in (0, 1):
+            Ad = (A.t().contiguous() if at else A).cuda()
+            Bd = (B.t().contiguous() if bt else B).cuda()
+            A2d = (A2.t().contiguous() if at else A2).cuda()
+            B2d = (B2.t().contiguous() if bt else B2).cuda()
+            lda = M if at else K
+            ldb = K if bt else N
+            for epi in (_lib.GEMM_STORE, _lib.GEMM_TANH, _lib.GEMM_DTANH):
+                C = torch.zeros(M, N, device="cuda")
+                d = _lib.GemmDesc(m=M, n=N, k=K, a=addr(Ad), lda=lda, a_trans=at, b=addr(Bd), ldb=ldb, b_trans=bt,
+                                  epilogue=epi, a2=addr(A2d), b2=addr(B2d), c=addr(C), ldc=N, bias=addr(bias.cuda()),
+                                  h=addr(H.cuda()), ldh=N)
+                call("mrl_gemm", ctypes.byref(d), None, stream())
+                ref = (A.double() @ B.double() + A2.double() @ B2.double() + bias.double())
+                if epi == _lib.GEMM_TANH:
+                    ref = torch.tanh(ref)
+                elif epi == _lib.GEMM_DTANH:
+                    ref = ref * (1 - H.double() ** 2)
+                err = (C.cpu().double() - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
+                assert err < 1e-5, (at, bt, epi, err)
+    # split-K slabs with the ones-row (bias grad) and stride
+    Ad = A.t().contiguous()  # [K, M]: op(A)(i,k) = Ad[k*M + i]  (a_trans = 1)
+    S = int(_lib.load().mrl_gemm_slab_splits(K, 4))
+    stride = (M + 1) * N + 5
+    slab = torch.zeros(S * stride, device="cuda")
+    d = _lib.GemmDesc(m=M + 1, n=N, k=K, a=addr(Ad.cuda()), lda=M, a_trans=1, ones_row=1, b=addr(B.cuda()), ldb=N,
+                      epilogue=_lib.GEMM_SLAB, c=addr(slab), ldc=N, splits=4, slab_stride=stride)
+    call("mrl_gemm", ctypes.byref(d), None, stream())
+    got = slab.view(S, stride)[:, :(M + 1) * N].sum(0).view(M + 1, N).cpu().double()
+    ref = torch.cat([A.double(), torch.ones(1, K, dtype=torch.float64)], 0) @ B.double()
+    assert (got - ref).abs().max().item() < 1e-4 * max(ref.abs().max().item(), 1.0)
