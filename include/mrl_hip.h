@@ -137,6 +137,10 @@ typedef struct {
 int mrl_gemm(const mrl_gemm_desc* g, const int32_t* skip, void* stream);
 /* slabs a MRL_GEMM_SLAB call over k rows with `max_splits` requested actually writes */
 int64_t mrl_gemm_slab_splits(int64_t k, int32_t max_splits);
+/* bias / logstd gradients: slab[z*slab_stride + c] = sum of g[r, c] (ld ldg) over the
+ * z-th of `splits` equal row chunks, z < splits (empty chunks write 0) */
+int mrl_colsum(const float* g, int64_t m, int64_t n, int64_t ldg, int32_t splits, float* slab, int64_t slab_stride,
+               const int32_t* skip, void* stream);
 /* per-row head epilogue (same semantics as mrl_mlp_rows' epilogues) on head rows
  * z [N, n_out] (and tangent rows dz for EPI_FVP); logstd/dlogstd for DiagGauss;
  * io->x / ep_t unused; partial has mrl_partial_rows(n) rows. */
@@ -197,6 +201,7 @@ int64_t mrl_episode_stats_workspace_bytes(int64_t E);
  * stat (Chan merge of per-block Welford partials in block order), then normalised. */
 #define MRL_ENV_CARTPOLE 0  /* CartPole-v0 equations (gym), k = 2            */
 #define MRL_ENV_HOPPER 1    /* Hopper-v2-shaped surrogate, obs 11 / act 3     */
+#define MRL_ENV_HUMANOID 2  /* Humanoid-v2-shaped surrogate, obs 376 / act 17 (layered rollout only) */
 
 typedef struct {
   int32_t env_id;          /* MRL_ENV_*                                          */
@@ -222,6 +227,7 @@ typedef struct {
   int32_t* ep_t;           /* [T*E] step index of the row inside its episode      */
   const void* noise;       /* optional injected noise [T*E] u | [T*E, d] z        */
   int64_t* stamps;         /* optional diagnostic: [T, 8] s_memtime of block 0 phases (NULL in production) */
+  double* raw_obs;         /* layered rollout: [obs_dim+1, E] raw next obs + reward (SoA) */
 } mrl_rollout_bufs;
 
 int64_t mrl_env_state_doubles(int32_t env_id);
@@ -233,6 +239,15 @@ int mrl_rollout_reset(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void
 /* one lock-step env step t (0 <= t < horizon) for all envs */
 int mrl_rollout_step(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta,
                      const float* image, const mrl_rollout_bufs* b, int32_t t, void* stream);
+/* Layered-policy rollout (any policy net; required for Humanoid): step t is
+ *   mrl_rollout_obs(t)            filter merge + normalised obs rows of step t -> b->obs
+ *   <policy forward over the E rows of step t, e.g. LayeredMlpNet GEMMs> -> z [E, n_out]
+ *   mrl_rollout_act(z, t)         sample, env step, raw next obs/reward, block partials
+ * mrl_rollout_reset_rows replaces mrl_rollout_reset; mrl_rollout_finish is shared. */
+int mrl_rollout_reset_rows(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void* stream);
+int mrl_rollout_obs(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, int32_t t, void* stream);
+int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const float* z, const float* logstd,
+                    const mrl_rollout_bufs* b, int32_t t, void* stream);
 /* after step T-1: fold the last reward partials into the reward stat, advance the
  * iteration counter (obs_T is never pushed: the horizon cuts the episode) */
 int mrl_rollout_finish(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void* stream);

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libmrl_hip.so")
 OK = 0
 HEAD_LINEAR, HEAD_SOFTMAX, HEAD_GAUSS = 0, 1, 2
 EPI_PROB, EPI_LOSSES, EPI_SURRGRAD, EPI_VFLOSS, EPI_FVP = 0, 1, 2, 3, 4
-ENV_CARTPOLE, ENV_HOPPER = 0, 1
+ENV_CARTPOLE, ENV_HOPPER, ENV_HUMANOID = 0, 1, 2
 GEMM_STORE, GEMM_TANH, GEMM_DTANH, GEMM_SLAB = 0, 1, 2, 3
 
 vp = ctypes.c_void_p
@@ -52,7 +52,7 @@ class RolloutDesc(ctypes.Structure):
 class RolloutBufs(ctypes.Structure):
     _fields_ = [("env_state", vp), ("env_int", vp), ("filter_state", vp), ("records", vp), ("iteration", vp),
                 ("obs", vp), ("act", vp), ("prob", vp), ("rew", vp), ("flags", vp), ("ep_t", vp), ("noise", vp),
-                ("stamps", vp)]
+                ("stamps", vp), ("raw_obs", vp)]
 
 
 # name -> (restype, argtypes); every symbol include/mrl_hip.h declares
@@ -70,6 +70,7 @@ SIGNATURES = {
     "mrl_reduce_rows_f64": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_gemm": (i32, [vp, vp, vp]),
     "mrl_gemm_slab_splits": (i64, [i64, i32]),
+    "mrl_colsum": (i32, [vp, i64, i64, i64, i32, vp, i64, vp, vp]),
     "mrl_head_rows": (i32, [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_concat_time": (i32, [vp, vp, i64, i32, f64, vp, vp]),
     "mrl_cg_init": (i32, [vp, i64, vp, vp, vp, vp, vp, vp, vp]),
@@ -92,6 +93,9 @@ SIGNATURES = {
     "mrl_rollout_reset": (i32, [vp, vp, vp]),
     "mrl_rollout_step": (i32, [vp, vp, vp, vp, vp, i32, vp]),
     "mrl_rollout_finish": (i32, [vp, vp, vp]),
+    "mrl_rollout_reset_rows": (i32, [vp, vp, vp]),
+    "mrl_rollout_obs": (i32, [vp, vp, i32, vp]),
+    "mrl_rollout_act": (i32, [vp, i32, i32, vp, vp, vp, i32, vp]),
 }
 
 _lib = None

@@ -17,13 +17,14 @@ from .dist import Comm
 from .envs import Box, Discrete
 from .filters import DeviceZFilter
 from .misc_utils import IDENTITY, comma_sep_ints, update_default_config
-from .nets import MlpNet, check_hid_sizes, glorot_init
+from .nets import check_hid_sizes, glorot_init, make_net
 from .trpo import TrpoUpdater
 from .vf import NnVf
 
 MLP_OPTIONS = [
     ("hid_sizes", comma_sep_ints, [64, 64], "Sizes of hidden layers of MLP"),
     ("activation", str, "tanh", "nonlinearity"),
+    ("mlp_impl", str, "auto", "HIP MLP path: auto (fused 64-wide kernels when the shape allows), fused, layered"),
 ]
 
 FILTER_OPTIONS = [
@@ -37,18 +38,19 @@ def make_mlps(ob_space, ac_space, cfg, comm=None, seed=0):
     assert isinstance(ob_space, Box)
     if cfg["activation"] != "tanh":
         raise _lib.MrlError("only activation=tanh is implemented on the HIP path")
-    check_hid_sizes(cfg["hid_sizes"])
+    hid = check_hid_sizes(cfg["hid_sizes"])
+    impl = cfg.get("mlp_impl", "auto")
     rng = np.random.default_rng(seed)
     if isinstance(ac_space, Box):
         outdim, head, probtype = ac_space.shape[0], _lib.HEAD_GAUSS, DiagGauss(ac_space.shape[0])
     else:
         outdim, head, probtype = ac_space.n, _lib.HEAD_SOFTMAX, Categorical(ac_space.n)
     nin = ob_space.shape[0]
-    net = MlpNet(nin, outdim, head)
-    net.set_flat(glorot_init(rng, nin, outdim, head))
+    net = make_net(nin, outdim, head, hid, impl=impl)
+    net.set_flat(glorot_init(rng, nin, outdim, head, hid))
     policy = StochPolicyMLP(net, probtype)
-    vfnet = MlpNet(nin + 1, 1, _lib.HEAD_LINEAR)
-    vfnet.set_flat(glorot_init(rng, nin + 1, 1, _lib.HEAD_LINEAR))
+    vfnet = make_net(nin + 1, 1, _lib.HEAD_LINEAR, hid, impl=impl)
+    vfnet.set_flat(glorot_init(rng, nin + 1, 1, _lib.HEAD_LINEAR, hid))
     baseline = NnVf(vfnet, cfg["timestep_limit"], dict(mixfrac=0.1), comm=comm)
     return policy, baseline
 

@@ -1,9 +1,11 @@
 """Lock-step batched rollout collector (replaces get_paths / do_rollouts_serial /
 rollout, `core.py:174-221`).
 
-E envs per rank advance together for ``horizon`` steps per iteration; each step is
-ONE fused HIP launch (filter merge -> normalise -> policy MLP on MFMA -> sample ->
-env step -> Welford partials).  The T launches (plus reset/finish) can be captured
+E envs per rank advance together for ``horizon`` steps per iteration.  With the
+fused 64-wide policy each step is ONE HIP launch (filter merge -> normalise ->
+policy MLP on MFMA -> sample -> env step -> Welford partials).  With a layered
+policy (wide nets, Humanoid's 376-d obs) a step is mrl_rollout_obs -> the policy's
+GEMM forward over the E rows -> mrl_rollout_act.  The T launches (plus reset/finish) can be captured
 once into a hipGraph and replayed every iteration (``use_graph``): the policy
 weights are read through the persistent ``net.image`` buffer and the RNG step base
 from a device iteration counter, so replays need no re-capture.
@@ -158,6 +160,17 @@ class Collector:
         self.ep_t = torch.zeros(self.N, dtype=torch.int32, device=self.dev)
         self.noise = None
         self.stamps = None  # diagnostic [T, 8] int64 phase stamps (see rollout.hip); None in production
+        net = policy.net
+        self.layered = bool(getattr(net, "layered", False))
+        if env.kind == _lib.ENV_HUMANOID and not self.layered:
+            raise _lib.MrlError("Humanoid-v2 needs a layered policy net (its 376-d obs exceeds the fused kernel)")
+        self.raw_obs = None
+        if self.layered:
+            # persistent per-step buffers (their addresses are baked into the captured graph)
+            self.raw_obs = torch.zeros((O + 1) * self.E, **f64)
+            self._zrows = torch.zeros(self.E * A, dtype=torch.float32, device=self.dev)
+            w = max(net.hid_sizes)
+            self._fwd_bufs = [torch.zeros(self.E * w, dtype=torch.float32, device=self.dev) for _ in range(2)]
         self.use_graph = use_graph
         self.graph = None
         self._ep_ws = torch.zeros(int(lib.mrl_episode_stats_workspace_bytes(self.E)) // 8 + 1, **f64)
@@ -166,16 +179,31 @@ class Collector:
     def _bufs(self):
         return _lib.RolloutBufs(ptr(self.env_state), ptr(self.env_int), ptr(self.filter_state), ptr(self.records),
                                 ptr(self.iteration), ptr(self.obs), ptr(self.act), ptr(self.prob), ptr(self.rew),
-                                ptr(self.flags), ptr(self.ep_t), ptr(self.noise), ptr(self.stamps))
+                                ptr(self.flags), ptr(self.ep_t), ptr(self.noise), ptr(self.stamps),
+                                ptr(self.raw_obs))
 
     def _launch_all(self):
         bufs = self._bufs()
         net = self.policy.net
+        if self.layered:
+            return self._launch_all_layered(bufs, net)
         call("mrl_rollout_reset", ctypes.byref(self.desc), ctypes.byref(bufs), stream())
         for t in range(self.T):
             call("mrl_rollout_step", ctypes.byref(self.desc), ctypes.byref(net.desc), ptr(net.theta), ptr(net.image),
                  ctypes.byref(bufs), int(t), stream())
         call("mrl_rollout_finish", ctypes.byref(self.desc), ctypes.byref(bufs), stream())
+
+    def _launch_all_layered(self, bufs, net):
+        E, O = self.E, self.env.obs_dim
+        d = ctypes.byref(self.desc)
+        logstd = net._addr(net.theta, net.tls) if net.head == _lib.HEAD_GAUSS else None
+        call("mrl_rollout_reset_rows", d, ctypes.byref(bufs), stream())
+        for t in range(self.T):
+            call("mrl_rollout_obs", d, ctypes.byref(bufs), int(t), stream())
+            net.forward_rows(self.obs[t * E:(t + 1) * E], E, self._zrows, self._fwd_bufs)
+            call("mrl_rollout_act", d, int(net.head), int(net.n_out), ptr(self._zrows), logstd, ctypes.byref(bufs),
+                 int(t), stream())
+        call("mrl_rollout_finish", d, ctypes.byref(bufs), stream())
 
     def set_noise(self, noise):
         """Inject sampling noise (float64 u[N] or z[N, d]) instead of Philox (parity mode)."""

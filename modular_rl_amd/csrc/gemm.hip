@@ -45,94 +45,138 @@ struct GemmArgs {
   const int32_t* skip;
 };
 
-// stage one [GBK x 128] operand tile: dst[k][c] (pitch GLD), c = tile row (A) or col (B)
-// contig_c: the source is contiguous along c (else along k)
-template <bool CONTIG_C>
-__device__ inline void stage_tile(float* dst, const float* src, int64_t ld, int64_t c0, int64_t k0, int64_t C,
-                                  int64_t Kend, int64_t Creal) {
+// One [GBK x TW] operand tile per K step (TW = 128, or 32 for the narrow head tiles),
+// staged global -> registers -> LDS as dst[k][c] (pitch TW+1: conflict-free);
+// c = tile row (A) or col (B).  CONTIG_C: the source is contiguous along c (lanes along
+// c, coalesced), else along k (each thread reads TW/8 consecutive k of one c, 16 B at
+// a time when aligned).  Rows c >= Creal of an in-range tile read as 1 (the ones-row
+// of the bias gradient).
+template <bool CONTIG_C, int TW>
+__device__ inline void load_tile(float (&r)[TW / 8], const float* __restrict__ src, int64_t ld, int64_t c0,
+                                 int64_t k0, int64_t C, int64_t Kend, int64_t Creal, bool vec) {
+  constexpr int TPC = 256 / TW;  // threads per c (!CONTIG_C) or k rows per pass (CONTIG_C)
+  constexpr int PER = TW / 8;    // values per thread
   const int t = threadIdx.x;
   if (CONTIG_C) {
-    // element (c, k) at src[k*ld + c]; lanes along c
-    const int c = t & 127;
-    const int kb = t >> 7;  // 0..1
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int k = kb + 2 * q;
-      const int64_t gc = c0 + c, gk = k0 + k;
-      const bool in = gc < C && gk < Kend;
-      dst[k * GLD + c] = (in && gc < Creal) ? src[gk * ld + gc] : (in ? 1.f : 0.f);
-    }
-  } else {
-    // element (c, k) at src[c*ld + k]; 4 lanes per c, 8 consecutive k each
-    const int c = t >> 1;     // 0..127
-    const int kq = t & 1;     // 0..1 -> k in [16kq, 16kq+16)
+    const int c = t % TW, kb = t / TW;
     const int64_t gc = c0 + c;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int k = kq * 16 + q;
-      const int64_t gk = k0 + k;
+    for (int q = 0; q < PER; ++q) {
+      const int64_t gk = k0 + kb + TPC * q;
       const bool in = gc < C && gk < Kend;
-      dst[k * GLD + c] = (in && gc < Creal) ? src[gc * ld + gk] : (in ? 1.f : 0.f);
+      r[q] = (in && gc < Creal) ? src[gk * ld + gc] : (in ? 1.f : 0.f);
+    }
+  } else {
+    const int c = t / TPC, kq = t % TPC;
+    const int64_t gc = c0 + c, gk0 = k0 + kq * PER;
+    if (vec && gc < Creal && gk0 + PER <= Kend) {
+      const float4* p = reinterpret_cast<const float4*>(src + gc * ld + gk0);
+#pragma unroll
+      for (int i = 0; i < PER / 4; ++i) {
+        const float4 v = p[i];
+        r[4 * i] = v.x;
+        r[4 * i + 1] = v.y;
+        r[4 * i + 2] = v.z;
+        r[4 * i + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int64_t gk = gk0 + q;
+        const bool in = gc < C && gk < Kend;
+        r[q] = (in && gc < Creal) ? src[gc * ld + gk] : (in ? 1.f : 0.f);
+      }
     }
   }
 }
 
-template <bool AT, bool BT>
+template <bool CONTIG_C, int TW>
+__device__ inline void store_tile(float* dst, const float (&r)[TW / 8]) {
+  constexpr int TPC = 256 / TW, PER = TW / 8, LD = TW + 1;
+  const int t = threadIdx.x;
+  if (CONTIG_C) {
+    const int c = t % TW, kb = t / TW;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) dst[(kb + TPC * q) * LD + c] = r[q];
+  } else {
+    const int c = t / TPC, kq = t % TPC;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) dst[(kq * PER + q) * LD + c] = r[q];
+  }
+}
+
+constexpr int GEMM_LDS_FLOATS = 4 * GBK * GLD;  // double-buffered A and B tiles (BN = 128)
+
+// BN = 128: 2x2 waves, each a 64x64 tile (2x2 MFMA tiles).  BN = 32 (narrow heads,
+// n <= 32): 4x1 waves, each a 32x32 tile.
+template <bool AT, bool BT, int BN>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
-  __shared__ float As[GBK * GLD];
-  __shared__ float Bs[GBK * GLD];
+  constexpr int MI = BN == 128 ? 2 : 1, NI = BN == 128 ? 2 : 1, BLD = BN + 1;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   if (g.skip != nullptr && *g.skip != 0) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int64_t m0 = (int64_t)blockIdx.y * GBM, n0 = (int64_t)blockIdx.x * GBN;
+  const int wm = BN == 128 ? wave >> 1 : wave, wn = BN == 128 ? wave & 1 : 0;
+  const int64_t m0 = (int64_t)blockIdx.y * GBM, n0 = (int64_t)blockIdx.x * BN;
   int64_t kbeg = 0, kend = g.K;
   if (g.epi == MRL_GEMM_SLAB) {
     kbeg = (int64_t)blockIdx.z * g.k_chunk;
     kend = min(g.K, kbeg + g.k_chunk);
   }
-  f32x16 acc[2][2];
+  f32x16 acc[MI][NI];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < MI; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = zero16();
+    for (int b = 0; b < NI; ++b) acc[a][b] = zero16();
   const int npairs = g.A2 != nullptr ? 2 : 1;
-  for (int p = 0; p < npairs; ++p) {
-    const float* Ap = p == 0 ? g.A : g.A2;
-    const float* Bp = p == 0 ? g.B : g.B2;
-    for (int64_t k0 = kbeg; k0 < kend; k0 += GBK) {
-      __syncthreads();
-      // A tile: c = row i in [m0, m0+128), contiguous along i iff a_trans
-      stage_tile<AT>(As, Ap, g.lda, m0, k0, g.M, kend, g.m_real);
-      // B tile: c = col j in [n0, n0+128), contiguous along j iff !b_trans
-      stage_tile<!BT>(Bs, Bp, g.ldb, n0, k0, g.N, kend, g.N);
-      __syncthreads();
+  const int64_t ntk = kend > kbeg ? (kend - kbeg + GBK - 1) / GBK : 0;
+  const int64_t nt = npairs * ntk;
+  // 16-byte loads along k need ld % 4 == 0 and 16 B aligned bases
+  const bool va = !AT && (g.lda & 3) == 0 && ((reinterpret_cast<uintptr_t>(g.A) | reinterpret_cast<uintptr_t>(g.A2)) & 15) == 0;
+  const bool vb = BT && (g.ldb & 3) == 0 && ((reinterpret_cast<uintptr_t>(g.B) | reinterpret_cast<uintptr_t>(g.B2)) & 15) == 0;
+  float ra[16], rb[BN / 8];
+  auto load = [&](int64_t t) {
+    const int p = t >= ntk ? 1 : 0;
+    const int64_t k0 = kbeg + (t - p * ntk) * GBK;
+    // A tile: c = row i in [m0, m0+128), contiguous along i iff a_trans
+    load_tile<AT, GBM>(ra, p ? g.A2 : g.A, g.lda, m0, k0, g.M, kend, g.m_real, va);
+    // B tile: c = col j in [n0, n0+BN), contiguous along j iff !b_trans
+    load_tile<!BT, BN>(rb, p ? g.B2 : g.B, g.ldb, n0, k0, g.N, kend, g.N, vb);
+  };
+  if (nt > 0) load(0);
+  for (int64_t t = 0; t < nt; ++t) {
+    float* As = smem + (t & 1) * GBK * (GLD + BLD);
+    float* Bs = As + GBK * GLD;
+    store_tile<AT, GBM>(As, ra);
+    store_tile<!BT, BN>(Bs, rb);
+    __syncthreads();
+    if (t + 1 < nt) load(t + 1);  // next tile's global loads overlap this tile's MFMAs
 #pragma unroll
-      for (int s = 0; s < GBK / 2; ++s) {
-        const int k = 2 * s + h;
-        const float a0 = As[k * GLD + wm * 64 + j];
-        const float a1 = As[k * GLD + wm * 64 + 32 + j];
-        const float b0 = Bs[k * GLD + wn * 64 + j];
-        const float b1 = Bs[k * GLD + wn * 64 + 32 + j];
-        acc[0][0] = MFMA32(a0, b0, acc[0][0]);
-        acc[0][1] = MFMA32(a0, b1, acc[0][1]);
-        acc[1][0] = MFMA32(a1, b0, acc[1][0]);
-        acc[1][1] = MFMA32(a1, b1, acc[1][1]);
-      }
+    for (int s = 0; s < GBK / 2; ++s) {
+      const int k = 2 * s + h;
+      float av[MI], bv[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) av[mi] = As[k * GLD + wm * 32 * MI + 32 * mi + j];
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) bv[ni] = Bs[k * BLD + wn * 32 * NI + 32 * ni + j];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA32(av[mi], bv[ni], acc[mi][ni]);
     }
   }
   // epilogue: lane holds column j, rows cperm(r, h) of each 32x32 tile
   float* C = g.C;
   if (g.epi == MRL_GEMM_SLAB) C += (int64_t)blockIdx.z * g.slab_stride;
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      const int64_t col = n0 + wn * 64 + ni * 32 + j;
+    for (int ni = 0; ni < NI; ++ni) {
+      const int64_t col = n0 + wn * 32 * NI + ni * 32 + j;
       if (col >= g.N) continue;
       const float bv = g.bias != nullptr ? g.bias[col] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * 64 + mi * 32 + cperm(r, h);
+        const int64_t row = m0 + wm * 32 * MI + mi * 32 + cperm(r, h);
         if (row >= g.M) continue;
         float v = acc[mi][ni][r] + bv;
         if (g.epi == MRL_GEMM_TANH) v = tanh_fast(v);
@@ -143,6 +187,34 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
         C[row * g.ldc + col] = v;
       }
     }
+}
+
+// Bias gradients: slab[z*stride + c] = sum over row chunk z of G[r, c].  64 columns per
+// block (one per lane, coalesced 256 B row segments), 4 waves interleave the rows.
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ G, int64_t M, int64_t N, int64_t ldg,
+                                                     int64_t chunk, float* __restrict__ slab, int64_t stride,
+                                                     const int32_t* __restrict__ skip) {
+  __shared__ float red[4][64];
+  if (skip != nullptr && *skip != 0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t r0 = (int64_t)blockIdx.y * chunk, r1 = min(M, r0 + chunk);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (col < N) {
+    const float* p = G + col;
+    int64_t r = r0 + wave;
+    for (; r + 12 < r1; r += 16) {
+      s0 += p[r * ldg];
+      s1 += p[(r + 4) * ldg];
+      s2 += p[(r + 8) * ldg];
+      s3 += p[(r + 12) * ldg];
+    }
+    for (; r < r1; r += 4) s0 += p[r * ldg];
+  }
+  red[wave][lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (wave == 0 && col < N)
+    slab[(int64_t)blockIdx.y * stride + col] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 // X = [obs, ep_t / limit] for the value net's time feature (core.py:659-660)
@@ -256,12 +328,26 @@ int mrl_gemm(const mrl_gemm_desc* d, const int32_t* skip, void* stream) {
     splits = d->k > 0 ? (d->k + g.k_chunk - 1) / g.k_chunk : 1;
   }
   if (splits > 65535) return fail(E_ARG, "mrl_gemm: too many splits");
-  dim3 grid((unsigned)((g.N + GBN - 1) / GBN), (unsigned)((g.M + GBM - 1) / GBM), (unsigned)splits);
   hipStream_t s = (hipStream_t)stream;
-  if (!d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(256), 0, s, g);
-  else if (!d->a_trans && d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(256), 0, s, g);
-  else if (d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(256), 0, s, g);
-  else hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(256), 0, s, g);
+  const unsigned gm = (unsigned)((g.M + GBM - 1) / GBM);
+  const int64_t wide_blocks = (g.N + GBN - 1) / GBN * (int64_t)gm * splits;
+  if (g.N <= 32 || wide_blocks < 160) {
+    // narrow 128x32 tiles: head layers (n_out <= 32) without 128-wide MFMA waste, and
+    // small-M launches (the rollout's per-step forward over E rows) with 4x the blocks
+    const dim3 grid((unsigned)((g.N + 31) / 32), gm, (unsigned)splits);
+    const size_t shm = 2 * GBK * (GLD + 33) * sizeof(float);
+    if (!d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, false, 32>), grid, dim3(256), shm, s, g);
+    else if (!d->a_trans && d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, true, 32>), grid, dim3(256), shm, s, g);
+    else if (d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<true, false, 32>), grid, dim3(256), shm, s, g);
+    else hipLaunchKernelGGL((gemm_f32_kernel<true, true, 32>), grid, dim3(256), shm, s, g);
+  } else {
+    const dim3 grid((unsigned)((g.N + GBN - 1) / GBN), gm, (unsigned)splits);
+    const size_t shm = GEMM_LDS_FLOATS * sizeof(float);
+    if (!d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, false, 128>), grid, dim3(256), shm, s, g);
+    else if (!d->a_trans && d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, true, 128>), grid, dim3(256), shm, s, g);
+    else if (d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<true, false, 128>), grid, dim3(256), shm, s, g);
+    else hipLaunchKernelGGL((gemm_f32_kernel<true, true, 128>), grid, dim3(256), shm, s, g);
+  }
   return hip_check(hipGetLastError(), "mrl_gemm");
 }
 
@@ -313,6 +399,18 @@ int mrl_head_rows(int32_t head, int32_t n_out, int32_t epi, const float* z, cons
   if (n_out <= 8) launch_head<8>(epi, grid, (hipStream_t)stream, a, z, dz, skip);
   else launch_head<MRL_LAYERED_MAX_OUT>(epi, grid, (hipStream_t)stream, a, z, dz, skip);
   return hip_check(hipGetLastError(), "mrl_head_rows");
+}
+
+int mrl_colsum(const float* g, int64_t m, int64_t n, int64_t ldg, int32_t splits, float* slab, int64_t slab_stride,
+               const int32_t* skip, void* stream) {
+  if (!g || !slab) return fail(E_ARG, "mrl_colsum: null pointer");
+  if (n <= 0) return OK;
+  const int64_t S = splits < 1 ? 1 : splits;
+  if (S > 65535) return fail(E_ARG, "mrl_colsum: too many splits");
+  const int64_t chunk = m > 0 ? (m + S - 1) / S : 0;
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((n + 63) / 64), (unsigned)S), dim3(256), 0, (hipStream_t)stream,
+                     g, m, n, ldg, chunk, slab, slab_stride, skip);
+  return hip_check(hipGetLastError(), "mrl_colsum");
 }
 
 int mrl_concat_time(const float* obs, const int32_t* ep_t, int64_t n, int32_t n_obs, double timestep_limit, float* X,

@@ -37,12 +37,43 @@ struct EnvC<MRL_ENV_CARTPOLE> {
   static constexpr int NS = CP_NS, OBS = CP_OBS, ACT = 2, DISCRETE = 1, MAX_STEPS = 200, NU = 4;
   __device__ static void reset(const double* u, double* s) { cartpole_reset(u, s); }
   __device__ static void obs(const double* s, double* o) { cartpole_obs(s, o); }
+  __device__ static void step_disc(double* s, int a, double& rew, bool& done) { cartpole_step(s, a, rew, done); }
+  __device__ static void step_cont(double*, const float*, double&, bool&) {}
+  template <class Out>
+  __device__ static void obs_out(const double* s, Out out) {
+    double o[OBS];
+    cartpole_obs(s, o);
+#pragma unroll
+    for (int k = 0; k < OBS; ++k) out(k, o[k]);
+  }
 };
 template <>
 struct EnvC<MRL_ENV_HOPPER> {
   static constexpr int NS = HP_NS, OBS = HP_OBS, ACT = HP_ACT, DISCRETE = 0, MAX_STEPS = 1000, NU = 12;
   __device__ static void reset(const double* u, double* s) { hopper_reset(u, s); }
   __device__ static void obs(const double* s, double* o) { hopper_obs(s, o); }
+  __device__ static void step_disc(double*, int, double&, bool&) {}
+  __device__ static void step_cont(double* s, const float* a, double& rew, bool& done) { hopper_step(s, a, rew, done); }
+  template <class Out>
+  __device__ static void obs_out(const double* s, Out out) {
+    double o[OBS];
+    hopper_obs(s, o);
+#pragma unroll
+    for (int k = 0; k < OBS; ++k) out(k, o[k]);
+  }
+};
+template <>
+struct EnvC<MRL_ENV_HUMANOID> {
+  static constexpr int NS = HM_NS, OBS = HM_OBS, ACT = HM_ACT, DISCRETE = 0, MAX_STEPS = 1000, NU = HM_NU;
+  __device__ static void reset(const double* u, double* s) { humanoid_reset(u, s); }
+  __device__ static void step_disc(double*, int, double&, bool&) {}
+  __device__ static void step_cont(double* s, const float* a, double& rew, bool& done) {
+    humanoid_step(s, a, rew, done);
+  }
+  template <class Out>
+  __device__ static void obs_out(const double* s, Out out) {
+    humanoid_obs(s, out);
+  }
 };
 
 struct EnvInfo {
@@ -50,6 +81,7 @@ struct EnvInfo {
 };
 __host__ __device__ inline EnvInfo env_info(int id) {
   if (id == MRL_ENV_CARTPOLE) return EnvInfo{CP_NS, CP_OBS, 2, 1, 200};
+  if (id == MRL_ENV_HUMANOID) return EnvInfo{HM_NS, HM_OBS, HM_ACT, 0, 1000};
   return EnvInfo{HP_NS, HP_OBS, HP_ACT, 0, 1000};
 }
 __host__ __device__ inline int filt_doubles(int obs) { return 2 + 2 * (obs + 1); }
@@ -166,6 +198,103 @@ __device__ inline void chan_merge(double& n, double& M, double& S, double nb, do
   n = nn;
 }
 
+// sampling noise of env e at step t: Philox (gid, iteration*T + t) on domain 0, or the
+// injected noise rows.  zn[0] = uniform (Categorical) | zn[q] = standard normals (Gauss)
+template <int ENV>
+__device__ inline void draw_noise(const RollArgs& a, int e, int64_t row, int t, double* zn) {
+  using EC = EnvC<ENV>;
+  constexpr int A = EC::ACT;
+  const uint32_t gid = (uint32_t)(a.d.env_offset + e);
+  const uint64_t w = (uint64_t)(*a.b.iteration) * (uint64_t)a.d.horizon + (uint64_t)t;
+  if (a.b.noise != nullptr) {
+    if constexpr (EC::DISCRETE) zn[0] = reinterpret_cast<const double*>(a.b.noise)[row];
+    else
+#pragma unroll
+      for (int q = 0; q < A; ++q) zn[q] = reinterpret_cast<const double*>(a.b.noise)[row * A + q];
+  } else if constexpr (EC::DISCRETE) {
+    double u1;
+    philox_uniform2(a.d.seed, 0, gid, w, 0, zn[0], u1);
+  } else {
+#pragma unroll
+    for (int c = 0; c < (A + 1) / 2; ++c) {
+      double u0, u1;
+      philox_uniform2(a.d.seed, 0, gid, w, (uint32_t)c, u0, u1);
+      const double rad = sqrt(-2.0 * log(1.0 - u0));
+      double sn, cn;
+      sincos(2.0 * 3.141592653589793 * u1, &sn, &cn);
+      zn[2 * c] = rad * cn;
+      if (2 * c + 1 < A) zn[2 * c + 1] = rad * sn;
+    }
+  }
+}
+
+// sample the action from the head rows z (core.py:261-267; distributions.py:3-13 /
+// core.py:432-435), write act/prob rows, step the env (fp64)
+template <int ENV>
+__device__ inline void sample_and_step(const RollArgs& a, int64_t row, const float* z, const float* logstd,
+                                       const double* zn, double* s, double& rew, bool& done) {
+  using EC = EnvC<ENV>;
+  constexpr int A = EC::ACT;
+  if constexpr (EC::DISCRETE) {
+    float m = z[0];
+#pragma unroll
+    for (int q = 1; q < A; ++q) m = fmaxf(m, z[q]);
+    float p[A], se = 0.f;
+#pragma unroll
+    for (int q = 0; q < A; ++q) {
+      p[q] = expf(z[q] - m);
+      se += p[q];
+    }
+#pragma unroll
+    for (int q = 0; q < A; ++q) p[q] = p[q] / se;
+    const double u = zn[0];
+    int act = 0;
+    float cs = 0.f;
+    bool found = false;
+#pragma unroll
+    for (int q = 0; q < A; ++q) {
+      cs += p[q];
+      if (!found && (double)cs > u) {
+        act = q;
+        found = true;
+      }
+    }
+    reinterpret_cast<int32_t*>(a.b.act)[row] = act;
+#pragma unroll
+    for (int q = 0; q < A; ++q) a.b.prob[row * A + q] = p[q];
+    EC::step_disc(s, act, rew, done);
+  } else {
+    float av[A];
+#pragma unroll
+    for (int q = 0; q < A; ++q) {
+      const float sd = expf(logstd[q]);
+      av[q] = __fadd_rn(__fmul_rn((float)zn[q], sd), z[q]);
+      reinterpret_cast<float*>(a.b.act)[row * A + q] = av[q];
+      a.b.prob[row * 2 * A + q] = z[q];
+      a.b.prob[row * 2 * A + A + q] = sd;
+    }
+    EC::step_cont(s, av, rew, done);
+  }
+}
+
+// episode bookkeeping: gym TimeLimit => done (terminated, bootstrap 0); the rollout
+// loop limit / horizon cut => not terminated (core.py:190-207, 73); auto-reset; store
+template <int ENV>
+__device__ inline void finish_env_step(const RollArgs& a, int e, int64_t row, int t, double* s, double rew, bool done) {
+  using EC = EnvC<ENV>;
+  const int E = a.d.n_envs;
+  const int ept = a.b.env_int[e];
+  a.b.ep_t[row] = ept;
+  const bool term = done || (ept + 1 >= EC::MAX_STEPS);
+  const bool last = term || (ept + 1 >= a.d.timestep_limit) || (t == a.d.horizon - 1);
+  a.b.rew[row] = (float)rew;
+  a.b.flags[row] = (uint8_t)((last ? 1 : 0) | (term ? 2 : 0));
+  if (last && t < a.d.horizon - 1) reset_env<ENV>(a, e, s);
+  else a.b.env_int[e] = ept + 1;
+#pragma unroll
+  for (int i = 0; i < EC::NS; ++i) a.b.env_state[(int64_t)i * E + e] = s[i];
+}
+
 template <int ENV>
 __global__ __launch_bounds__(RB) void rollout_reset_kernel(RollArgs a) {
   using EC = EnvC<ENV>;
@@ -277,94 +406,19 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, MlpDims md
   } xl{&xt[wave][j][0], valid};
   // sampling noise does not depend on the policy output: draw it first so its VALU
   // work overlaps the MFMA chain of the forward
-  const uint32_t gid = (uint32_t)(a.d.env_offset + e);
-  const uint64_t w = (uint64_t)(*a.b.iteration) * (uint64_t)a.d.horizon + (uint64_t)t;
   double zn[A + 1];
-  if (a.b.noise != nullptr) {
-    if (valid) {
-      if constexpr (EC::DISCRETE) zn[0] = reinterpret_cast<const double*>(a.b.noise)[row];
-      else
-#pragma unroll
-        for (int q = 0; q < A; ++q) zn[q] = reinterpret_cast<const double*>(a.b.noise)[row * A + q];
-    }
-  } else if constexpr (EC::DISCRETE) {
-    double u1;
-    philox_uniform2(a.d.seed, 0, gid, w, 0, zn[0], u1);
-  } else {
-#pragma unroll
-    for (int c = 0; c < (A + 1) / 2; ++c) {
-      double u0, u1;
-      philox_uniform2(a.d.seed, 0, gid, w, (uint32_t)c, u0, u1);
-      const double rad = sqrt(-2.0 * log(1.0 - u0));
-      double sn, cn;
-      sincos(2.0 * 3.141592653589793 * u1, &sn, &cn);
-      zn[2 * c] = rad * cn;
-      zn[2 * c + 1] = rad * sn;
-    }
-  }
+  if (valid) draw_noise<ENV>(a, e, row, t, zn);
 
   float z[MAX_OUT];
   forward_head_lowreg(lds, md, xl, lane, z);
 
-  bool done = false, last = false, term = false;
   double rew = 0.0;
   if (valid && h == 0) {
     STAMP(4);
-    // 4. sample (core.py:261-267; distributions.py:3-13 / core.py:432-435)
-    if constexpr (EC::DISCRETE) {
-      float m = z[0];
-#pragma unroll
-      for (int q = 1; q < A; ++q) m = fmaxf(m, z[q]);
-      float p[A], se = 0.f;
-#pragma unroll
-      for (int q = 0; q < A; ++q) {
-        p[q] = expf(z[q] - m);
-        se += p[q];
-      }
-#pragma unroll
-      for (int q = 0; q < A; ++q) p[q] = p[q] / se;
-      const double u = zn[0];
-      int act = 0;
-      float cs = 0.f;
-      bool found = false;
-#pragma unroll
-      for (int q = 0; q < A; ++q) {
-        cs += p[q];
-        if (!found && (double)cs > u) {
-          act = q;
-          found = true;
-        }
-      }
-      reinterpret_cast<int32_t*>(a.b.act)[row] = act;
-#pragma unroll
-      for (int q = 0; q < A; ++q) a.b.prob[row * A + q] = p[q];
-      cartpole_step(s, act, rew, done);
-    } else {
-      const float* logstd = theta + md.tls;
-      float av[A];
-#pragma unroll
-      for (int q = 0; q < A; ++q) {
-        const float sd = expf(logstd[q]);
-        av[q] = __fadd_rn(__fmul_rn((float)zn[q], sd), z[q]);
-        reinterpret_cast<float*>(a.b.act)[row * A + q] = av[q];
-        a.b.prob[row * 2 * A + q] = z[q];
-        a.b.prob[row * 2 * A + A + q] = sd;
-      }
-      hopper_step(s, av, rew, done);
-    }
+    bool done = false;
+    sample_and_step<ENV>(a, row, z, theta + md.tls, zn, s, rew, done);
     STAMP(5);
-    // 5. episode bookkeeping: gym TimeLimit => done (terminated, bootstrap 0);
-    //    the rollout loop limit / horizon cut => not terminated (core.py:190-207, 73)
-    const int ept = a.b.env_int[e];
-    a.b.ep_t[row] = ept;
-    term = done || (ept + 1 >= EC::MAX_STEPS);
-    last = term || (ept + 1 >= a.d.timestep_limit) || (t == a.d.horizon - 1);
-    a.b.rew[row] = (float)rew;
-    a.b.flags[row] = (uint8_t)((last ? 1 : 0) | (term ? 2 : 0));
-    if (last && t < a.d.horizon - 1) reset_env<ENV>(a, e, s);
-    else a.b.env_int[e] = ept + 1;
-#pragma unroll
-    for (int i = 0; i < NS; ++i) a.b.env_state[(int64_t)i * E + e] = s[i];
+    finish_env_step<ENV>(a, e, row, t, s, rew, done);
     // 6. raw next observation + reward into the block partial
     double o[O];
     EC::obs(s, o);
@@ -380,30 +434,203 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, MlpDims md
 #undef STAMP
 }
 
+
+// ------------------------------------------------------------------ layered-policy rollout
+// For policies the fused step kernel does not cover (wide nets, Humanoid's 376-d obs),
+// step t is three launches: lrollout_obs (filter merge + normalised obs rows) ->
+// the policy's GEMM forward over the E rows (LayeredMlpNet) -> lrollout_act (sample,
+// env step, raw next obs + reward as SoA rows [O+1][E] fp64, block partials).
+constexpr int MAXD_L = 384;  // obs dims + 1 on the layered path
+
+// per-block two-pass partial of the SoA rows raw[k][e0 .. e0+nvalid) for k < D
+__device__ inline void publish_partial_raw(const RollArgs& a, int e0, int nvalid, int D, bool with_rew,
+                                           double* rec_out) {
+  const int E = a.d.n_envs;
+  const int g = threadIdx.x >> 4, j = threadIdx.x & 15;
+  double* r = rec_out + (int64_t)blockIdx.x * a.RS;
+  for (int k = g; k < D; k += RB / 16) {
+    const double* col = a.b.raw_obs + (int64_t)k * E + e0;
+    double sm = 0.0;
+    for (int i = j; i < nvalid; i += 16) sm += col[i];
+    const double mean = nvalid > 0 ? sum16(sm) / (double)nvalid : 0.0;
+    double m2 = 0.0;
+    for (int i = j; i < nvalid; i += 16) {
+      const double dv = col[i] - mean;
+      m2 += dv * dv;
+    }
+    m2 = sum16(m2);
+    if (j == 0) {
+      r[2 + k] = mean;
+      r[2 + D + k] = m2;
+    }
+  }
+  if (threadIdx.x == 0) {
+    r[0] = (double)nvalid;
+    r[1] = with_rew ? (double)nvalid : 0.0;
+  }
+}
+
+template <int ENV>
+__global__ __launch_bounds__(RB) void lrollout_reset_kernel(RollArgs a) {
+  using EC = EnvC<ENV>;
+  constexpr int O = EC::OBS, D = O + 1;
+  const int E = a.d.n_envs;
+  const int e0 = blockIdx.x * ENVS_PER_BLOCK;
+  const int e = e0 + threadIdx.x;
+  if (threadIdx.x < ENVS_PER_BLOCK && e < E) {
+    double s[EC::NS];
+    reset_env<ENV>(a, e, s);
+#pragma unroll
+    for (int i = 0; i < EC::NS; ++i) a.b.env_state[(int64_t)i * E + e] = s[i];
+    double* raw = a.b.raw_obs;
+    EC::obs_out(s, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
+    raw[(int64_t)O * E + e] = 0.0;
+  }
+  __threadfence_block();
+  __syncthreads();
+  publish_partial_raw(a, e0, min(ENVS_PER_BLOCK, E - e0), D, false, a.b.records);
+}
+
+template <int ENV>
+__global__ __launch_bounds__(RB) void lrollout_obs_kernel(RollArgs a, int t) {
+  using EC = EnvC<ENV>;
+  constexpr int O = EC::OBS, D = O + 1;
+  __shared__ double fmean[MAXD_L], fden[MAXD_L];
+  __shared__ float tile[32 * 129];
+  const int E = a.d.n_envs;
+  // 1. running-stat merge of step t's raw obs (and step t-1's rewards), as the fused kernel
+  const double* fs_in = a.b.filter_state + (t & 1) * a.FS;
+  double* fs_out = a.b.filter_state + ((t + 1) & 1) * a.FS;
+  const double* rec_in = a.b.records + (int64_t)(t & 1) * a.nb * a.RS;
+  const int g = threadIdx.x >> 4, jj = threadIdx.x & 15;
+  for (int k = g; k < D; k += RB / 16) {
+    const bool isr = (k == O);
+    double n = fs_in[isr ? 1 : 0], M = fs_in[2 + k], S = fs_in[2 + D + k];
+    double bn, bm, bs;
+    batch_of_records(rec_in, a.nb, a.RS, D, O, k, jj, bn, bm, bs);
+    chan_merge(n, M, S, bn, bm, bs);
+    if (jj == 0 && blockIdx.x == 0) {
+      if (k == 0) fs_out[0] = n;
+      if (isr) fs_out[1] = n;
+      fs_out[2 + k] = M;
+      fs_out[2 + D + k] = S;
+    }
+    if (!isr && jj == 0) {
+      const double var = n > 1.0 ? S / (n - 1.0) : M * M;  // running_stat.py:27
+      fmean[k] = M;
+      fden[k] = sqrt(var) + 1e-8;
+    }
+  }
+  __syncthreads();
+  // 2. normalised obs rows (core.py:191-192): SoA raw -> LDS tile -> row-major fp32 rows
+  const int e0 = blockIdx.x * ENVS_PER_BLOCK;
+  const int nvalid = min(ENVS_PER_BLOCK, E - e0);
+  const int64_t row0 = (int64_t)t * E + e0;
+  for (int c0 = 0; c0 < O; c0 += 32) {
+    {
+      const int el = threadIdx.x & 127, kb = threadIdx.x >> 7;
+#pragma unroll 4
+      for (int q = 0; q < 16; ++q) {
+        const int k = c0 + kb + 2 * q;
+        float vf = 0.f;
+        if (k < O && el < nvalid) {
+          double v = a.b.raw_obs[(int64_t)k * E + e0 + el];
+          if (a.d.filter) {
+            v = v - fmean[k];
+            v = v / fden[k];
+            v = v < -5.0 ? -5.0 : (v > 5.0 ? 5.0 : v);
+          }
+          vf = (float)v;
+        }
+        tile[(kb + 2 * q) * 129 + el] = vf;
+      }
+    }
+    __syncthreads();
+    {
+      const int el = threadIdx.x >> 1, half = threadIdx.x & 1;
+      if (el < nvalid) {
+        float* dst = a.b.obs + (row0 + el) * O;
+#pragma unroll 4
+        for (int q = 0; q < 16; ++q) {
+          const int k = c0 + half * 16 + q;
+          if (k < O) dst[k] = tile[(half * 16 + q) * 129 + el];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int ENV>
+__global__ __launch_bounds__(RB) void lrollout_act_kernel(RollArgs a, const float* __restrict__ zrows,
+                                                          const float* __restrict__ logstd, int t) {
+  using EC = EnvC<ENV>;
+  constexpr int O = EC::OBS, D = O + 1, NS = EC::NS, A = EC::ACT;
+  const int E = a.d.n_envs;
+  const int e0 = blockIdx.x * ENVS_PER_BLOCK;
+  const int e = e0 + threadIdx.x;
+  double* rec_out = a.b.records + (int64_t)((t + 1) & 1) * a.nb * a.RS;
+  if (threadIdx.x < ENVS_PER_BLOCK && e < E) {
+    const int64_t row = (int64_t)t * E + e;
+    double s[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) s[i] = a.b.env_state[(int64_t)i * E + e];
+    float z[A];
+#pragma unroll
+    for (int q = 0; q < A; ++q) z[q] = zrows[(int64_t)e * A + q];
+    double zn[A + 1];
+    draw_noise<ENV>(a, e, row, t, zn);
+    double rew = 0.0;
+    bool done = false;
+    sample_and_step<ENV>(a, row, z, logstd, zn, s, rew, done);
+    finish_env_step<ENV>(a, e, row, t, s, rew, done);
+    double* raw = a.b.raw_obs;
+    EC::obs_out(s, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
+    raw[(int64_t)O * E + e] = rew;
+  }
+  __threadfence_block();
+  __syncthreads();
+  publish_partial_raw(a, e0, min(ENVS_PER_BLOCK, E - e0), D, true, rec_out);
+}
+
 __global__ void rollout_finish_kernel(RollArgs a, int O) {
   const int D = O + 1, T = a.d.horizon;
   const double* fs_in = a.b.filter_state + (T & 1) * a.FS;
   double* fs_out = a.b.filter_state;
   const double* rec_in = a.b.records + (int64_t)(T & 1) * a.nb * a.RS;
-  const int k = threadIdx.x >> 4, j = threadIdx.x & 15;
-  const bool isr = (k == O);
+  const int g = threadIdx.x >> 4, j = threadIdx.x & 15;
+  // the last step's rewards still go through rewfilt (core.py:199); obs_T is never pushed
   double n = 0.0, M = 0.0, S = 0.0;
-  if (k < D) {
-    n = fs_in[isr ? 1 : 0];
-    M = fs_in[2 + k];
-    S = fs_in[2 + D + k];
-    if (isr) {  // the last step's rewards still go through rewfilt (core.py:199)
-      double bn, bm, bs;
-      batch_of_records(rec_in, a.nb, a.RS, D, O, k, j, bn, bm, bs);
-      chan_merge(n, M, S, bn, bm, bs);
-    }
+  if (g == 0) {
+    n = fs_in[1];
+    M = fs_in[2 + O];
+    S = fs_in[2 + D + O];
+    double bn, bm, bs;
+    batch_of_records(rec_in, a.nb, a.RS, D, O, O, j, bn, bm, bs);
+    chan_merge(n, M, S, bn, bm, bs);
   }
+  // copy the obs stat when fs_in is the other buffer (T odd)
+  double cp[(MAXD_L + RB - 1) / RB * 2 + 1];
+  int nc = 0;
+  if ((T & 1) != 0)
+    for (int k = threadIdx.x; k < O; k += RB) {
+      cp[nc++] = fs_in[2 + k];
+      cp[nc++] = fs_in[2 + D + k];
+    }
+  const double n_obs = fs_in[0];
   __syncthreads();  // fs_in may alias fs_out (T even)
-  if (k < D && j == 0) {
-    if (k == 0) fs_out[0] = n;
-    if (isr) fs_out[1] = n;
-    fs_out[2 + k] = M;
-    fs_out[2 + D + k] = S;
+  if ((T & 1) != 0) {
+    nc = 0;
+    for (int k = threadIdx.x; k < O; k += RB) {
+      fs_out[2 + k] = cp[nc++];
+      fs_out[2 + D + k] = cp[nc++];
+    }
+    if (threadIdx.x == 0) fs_out[0] = n_obs;
+  }
+  if (g == 0 && j == 0) {
+    fs_out[1] = n;
+    fs_out[2 + O] = M;
+    fs_out[2 + D + O] = S;
   }
   if (threadIdx.x == 0) *a.b.iteration += 1;
 }
@@ -414,7 +641,8 @@ using namespace mrl;
 
 static int check_roll(const mrl_rollout_desc* d, const mrl_rollout_bufs* b) {
   if (!d || !b) return fail(E_ARG, "null desc/bufs");
-  if (d->env_id != MRL_ENV_CARTPOLE && d->env_id != MRL_ENV_HOPPER) return fail(E_UNSUPPORTED, "unknown env_id");
+  if (d->env_id != MRL_ENV_CARTPOLE && d->env_id != MRL_ENV_HOPPER && d->env_id != MRL_ENV_HUMANOID)
+    return fail(E_UNSUPPORTED, "unknown env_id");
   if (d->n_envs <= 0 || d->horizon <= 0 || d->timestep_limit <= 0) return fail(E_ARG, "bad sizes");
   if (!b->env_state || !b->env_int || !b->filter_state || !b->records || !b->iteration) return fail(E_ARG, "null state");
   return OK;
@@ -440,6 +668,7 @@ int64_t mrl_rollout_blocks(int32_t n_envs) { return (n_envs + ENVS_PER_BLOCK - 1
 int mrl_rollout_reset(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void* stream) {
   int rc = check_roll(d, b);
   if (rc) return rc;
+  if (d->env_id == MRL_ENV_HUMANOID) return fail(E_UNSUPPORTED, "Humanoid runs on the layered rollout (mrl_rollout_reset_rows)");
   RollArgs a = make_args(d, b);
   if (d->env_id == MRL_ENV_CARTPOLE)
     hipLaunchKernelGGL(rollout_reset_kernel<MRL_ENV_CARTPOLE>, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a);
@@ -448,11 +677,61 @@ int mrl_rollout_reset(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void
   return hip_check(hipGetLastError(), "mrl_rollout_reset");
 }
 
+#define MRL_DISPATCH_ENV(id, KERNEL, ...)                                                    \
+  do {                                                                                      \
+    if ((id) == MRL_ENV_CARTPOLE) hipLaunchKernelGGL(KERNEL<MRL_ENV_CARTPOLE>, __VA_ARGS__); \
+    else if ((id) == MRL_ENV_HOPPER) hipLaunchKernelGGL(KERNEL<MRL_ENV_HOPPER>, __VA_ARGS__); \
+    else hipLaunchKernelGGL(KERNEL<MRL_ENV_HUMANOID>, __VA_ARGS__);                         \
+  } while (0)
+
+static int check_rows(const mrl_rollout_desc* d, const mrl_rollout_bufs* b) {
+  int rc = check_roll(d, b);
+  if (rc) return rc;
+  if (!b->raw_obs) return fail(E_ARG, "the layered rollout needs raw_obs [(obs_dim+1) * n_envs] doubles");
+  if (env_info(d->env_id).obs + 1 > MAXD_L) return fail(E_UNSUPPORTED, "obs dim too large");
+  return OK;
+}
+
+int mrl_rollout_reset_rows(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void* stream) {
+  int rc = check_rows(d, b);
+  if (rc) return rc;
+  RollArgs a = make_args(d, b);
+  MRL_DISPATCH_ENV(d->env_id, lrollout_reset_kernel, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a);
+  return hip_check(hipGetLastError(), "mrl_rollout_reset_rows");
+}
+
+int mrl_rollout_obs(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, int32_t t, void* stream) {
+  int rc = check_rows(d, b);
+  if (rc) return rc;
+  if (!b->obs) return fail(E_ARG, "null obs");
+  if (t < 0 || t >= d->horizon) return fail(E_ARG, "t out of range");
+  RollArgs a = make_args(d, b);
+  MRL_DISPATCH_ENV(d->env_id, lrollout_obs_kernel, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a, t);
+  return hip_check(hipGetLastError(), "mrl_rollout_obs");
+}
+
+int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const float* z, const float* logstd,
+                    const mrl_rollout_bufs* b, int32_t t, void* stream) {
+  int rc = check_rows(d, b);
+  if (rc) return rc;
+  if (!b->act || !b->prob || !b->rew || !b->flags || !b->ep_t || !z) return fail(E_ARG, "null trajectory buffer");
+  EnvInfo ei = env_info(d->env_id);
+  const bool gauss = head == MRL_HEAD_GAUSS;
+  if (n_out != ei.act || gauss == (bool)ei.discrete || (!gauss && head != MRL_HEAD_SOFTMAX))
+    return fail(E_ARG, "policy head does not match the env");
+  if (gauss && !logstd) return fail(E_ARG, "DiagGauss needs logstd");
+  if (t < 0 || t >= d->horizon) return fail(E_ARG, "t out of range");
+  RollArgs a = make_args(d, b);
+  MRL_DISPATCH_ENV(d->env_id, lrollout_act_kernel, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a, z, logstd, t);
+  return hip_check(hipGetLastError(), "mrl_rollout_act");
+}
+
 int mrl_rollout_step(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta, const float* image,
                      const mrl_rollout_bufs* b, int32_t t, void* stream) {
   int rc = check_roll(d, b);
   if (rc) return rc;
   if (!pol || !theta || !image) return fail(E_ARG, "null policy");
+  if (d->env_id == MRL_ENV_HUMANOID) return fail(E_UNSUPPORTED, "Humanoid runs on the layered rollout");
   if (!b->obs || !b->act || !b->prob || !b->rew || !b->flags || !b->ep_t) return fail(E_ARG, "null trajectory buffer");
   EnvInfo ei = env_info(d->env_id);
   const bool gauss = pol->head == MRL_HEAD_GAUSS;

@@ -8,6 +8,8 @@ module only describes them with gym-compatible spaces / spec so that
 * ``CartPole-v0`` -- gym's classic-control CartPole equations, TimeLimit 200.
 * ``Hopper-v2``   -- Hopper-v2-SHAPED surrogate (obs 11, act 3, TimeLimit 1000);
   MuJoCo is not available, so its dynamics are a stand-in.
+* ``Humanoid-v2`` -- Humanoid-v2-SHAPED surrogate (obs 376, act 17 in [-0.4, 0.4],
+  TimeLimit 1000); its 376-d obs needs the layered rollout (collector.py).
 """
 import numpy as np
 
@@ -42,6 +44,8 @@ class EnvSpec:
 REGISTRY = {
     "CartPole-v0": dict(kind=_lib.ENV_CARTPOLE, obs=4, act=2, discrete=True, max_steps=200, obs_high=np.inf),
     "Hopper-v2": dict(kind=_lib.ENV_HOPPER, obs=11, act=3, discrete=False, max_steps=1000, obs_high=np.inf),
+    "Humanoid-v2": dict(kind=_lib.ENV_HUMANOID, obs=376, act=17, discrete=False, max_steps=1000, obs_high=np.inf,
+                        act_high=0.4),
 }
 
 
@@ -55,7 +59,8 @@ class DeviceEnv:
         self.kind = r["kind"]
         self.obs_dim = r["obs"]
         self.observation_space = Box(-r["obs_high"], r["obs_high"], (r["obs"],))
-        self.action_space = Discrete(r["act"]) if r["discrete"] else Box(-1.0, 1.0, (r["act"],))
+        ah = r.get("act_high", 1.0)
+        self.action_space = Discrete(r["act"]) if r["discrete"] else Box(-ah, ah, (r["act"],))
         self.discrete = r["discrete"]
         self.act_dim = r["act"]
         self.spec = EnvSpec(env_id, r["max_steps"])

@@ -337,10 +337,15 @@ class LayeredMlpNet:
         for l in reversed(range(L)):
             din, dout = self.dims[l], self.dims[l + 1]
             inp = X if l == 0 else H[l - 1]
-            # [dW; db] = [inp, 1]^T G  (K = rows, split over S slabs)
-            self._gemm(din + 1, dout, n, self._addr(inp), din if l else ldx, self._addr(G), ldg,
-                       self._addr(slab, self.w_off[l]), dout, a_trans=1, epi=_lib.GEMM_SLAB, ones_row=1,
+            # dW = inp^T G (K = rows, split over S slabs).  db rides the GEMM as a ones-row
+            # when that row fits the last 128-row tile, else it is a column-sum pass.
+            ones = din % 128 != 0
+            self._gemm(din + ones, dout, n, self._addr(inp), din if l else ldx, self._addr(G), ldg,
+                       self._addr(slab, self.w_off[l]), dout, a_trans=1, epi=_lib.GEMM_SLAB, ones_row=int(ones),
                        splits=self.SLAB_SPLITS, slab_stride=self.P, skip=skip)
+            if not ones:
+                call("mrl_colsum", self._addr(G), n, dout, ldg, S, self._addr(slab, self.b_off[l]), self.P, ptr(skip),
+                     stream())
             if l > 0:
                 Gn = scr[l % 2]
                 self._gemm(n, din, dout, self._addr(G), ldg, self._addr(theta, self.w_off[l]), dout,
@@ -349,10 +354,16 @@ class LayeredMlpNet:
                 G, ldg = Gn, din
         if self.head == _lib.HEAD_GAUSS:
             A = self.n_out
-            self._gemm(1, A, n, None, 0, self._addr(ghead, A), self.gh, self._addr(slab, self.tls), A, a_trans=1,
-                       epi=_lib.GEMM_SLAB, ones_row=1, splits=self.SLAB_SPLITS, slab_stride=self.P, skip=skip)
+            call("mrl_colsum", self._addr(ghead, A), n, A, self.gh, S, self._addr(slab, self.tls), self.P, ptr(skip),
+                 stream())
         call("mrl_reduce_rows_f32", ptr(slab), S, self.P, ptr(out), ptr(skip), stream())
         return out
+
+    def forward_rows(self, x, n, z, bufs):
+        """Head pre-activations z [n, n_out] of n obs rows into caller-owned buffers
+        (the rollout's per-step forward; bufs: 2 x [n * max(hid)] scratch)."""
+        hb = [bufs[l % 2] for l in range(len(self.hid_sizes))]
+        self._forward(x, self.n_in, int(n), self.theta, hb, z)
 
     def forward(self, x, n, ep_t=None, timestep_limit=1.0, out=None):
         width = 1 if self.head == _lib.HEAD_LINEAR else self.gh

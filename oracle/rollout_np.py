@@ -16,7 +16,7 @@ from . import philox
 from . import trpo_np as T
 
 BLOCK = 128
-CARTPOLE, HOPPER = 0, 1
+CARTPOLE, HOPPER, HUMANOID = 0, 1, 2
 
 
 class FilterState:
@@ -91,19 +91,19 @@ class Envs:
     def __init__(self, kind, E, seed, env_offset=0):
         self.kind, self.E, self.seed = kind, E, seed
         self.gid = np.arange(E, dtype=np.uint64) + np.uint64(env_offset)
-        self.ns = 4 if kind == CARTPOLE else 12
-        self.O = 4 if kind == CARTPOLE else 11
-        self.A = 2 if kind == CARTPOLE else 3
-        self.max_steps = 200 if kind == CARTPOLE else 1000
+        self.ns, self.O, self.A, self.max_steps, self.nu = {
+            CARTPOLE: (4, 4, 2, 200, 4), HOPPER: (12, 11, 3, 1000, 12),
+            HUMANOID: (EV.HM_NS, EV.HM_OBS, EV.HM_ACT, 1000, EV.HM_NU)}[kind]
         self.state = np.zeros((E, self.ns))
         self.ep_t = np.zeros(E, dtype=np.int64)
         self.ep_count = np.zeros(E, dtype=np.int64)
 
     def reset(self, idx):
-        nu = 4 if self.kind == CARTPOLE else 12
-        u = philox.uniforms(self.seed, 1, self.gid[idx], self.ep_count[idx].astype(np.uint64), nu)
+        u = philox.uniforms(self.seed, 1, self.gid[idx], self.ep_count[idx].astype(np.uint64), self.nu)
         if self.kind == CARTPOLE:
             self.state[idx] = EV.cartpole_reset(u)
+        elif self.kind == HUMANOID:
+            self.state[idx] = EV.humanoid_reset(u)
         else:
             q, v = EV.hopper_reset(u)
             self.state[idx] = np.concatenate([q, v], axis=1)
@@ -113,12 +113,16 @@ class Envs:
     def obs(self):
         if self.kind == CARTPOLE:
             return self.state.copy()
+        if self.kind == HUMANOID:
+            return EV.humanoid_obs(self.state)
         return EV.hopper_obs(self.state[:, :6], self.state[:, 6:])
 
     def step(self, act):
         if self.kind == CARTPOLE:
             s2, rew, done = EV.cartpole_step(self.state, act)
             self.state = s2
+        elif self.kind == HUMANOID:
+            self.state, rew, done = EV.humanoid_step(self.state, act)
         else:
             q, v, rew, done = EV.hopper_step(self.state[:, :6], self.state[:, 6:], act)
             self.state = np.concatenate([q, v], axis=1)
