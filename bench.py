@@ -32,18 +32,25 @@ PEAK_FP32_TFLOPS = 157.3     # MI355X dense FP32 (MFMA f32 == VALU rate), MI355X
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec
 
 
-def flops_per_row(O, A):
-    """Algorithmic FLOP per row of the two Fisher-product kernels (tanh MLP O-64-64-A)."""
-    fwd = 2 * (O * 64 + 64 * 64 + 64 * A)
-    jvp = 2 * (O * 64 + 2 * 64 * 64 + 2 * 64 * A)
-    vjp = 2 * (64 * A + 64 * A + 64 * 64 + 64 * 64 + O * 64)   # gh2, gW2, gW1, gh1, gW0
-    return {"fvp_jvp_rows": fwd + jvp, "fvp_vjp": vjp}
+def flops_per_row(net):
+    """Algorithmic FLOP per row of the two timed halves of the Fisher product.
+    Fused 64-wide net: fvp_jvp_rows = forward recompute + JVP, fvp_vjp = backward.
+    Layered net: the forward is the recorded tape, so fvp_jvp_rows = JVP only
+    (layer 0 one product, deeper layers two); fvp_vjp = weight grads of every layer +
+    input grads of layers >= 1."""
+    dims = [net.n_in] + list(net.hid_sizes) + [net.n_out]
+    mm = [dims[i] * dims[i + 1] for i in range(len(dims) - 1)]
+    jvp = 2 * (mm[0] + 2 * sum(mm[1:]))
+    vjp = 2 * (sum(mm) + sum(mm[1:]))
+    if getattr(net, "layered", False):
+        return {"fvp_jvp_rows": jvp, "fvp_vjp": vjp}
+    return {"fvp_jvp_rows": 2 * sum(mm) + jvp, "fvp_vjp": vjp}
 
 
 GAE_BYTES_PER_ROW = 17  # read r 4 + v 4 + flags 1, write adv 4 + ret 4
 
 
-def cpu_baseline(E, Tn, seed=0):
+def cpu_baseline(E, Tn, env_id="Hopper-v2", hid=(64, 64), seed=0):
     """Time the numpy oracle (CPU restatement of the reference) on one full iteration."""
     from oracle import rollout_np as RO
     from oracle import trpo_np as T
@@ -53,28 +60,30 @@ def cpu_baseline(E, Tn, seed=0):
     except Exception:  # pragma: no cover
         threads = os.cpu_count()
     rng = np.random.default_rng(seed)
-    spec = T.Spec(11, [64, 64], 3, "gauss")
-    vspec = T.Spec(12, [64, 64], 1, "linear")
+    kind, O, A = {"Hopper-v2": (RO.HOPPER, 11, 3), "Humanoid-v2": (RO.HUMANOID, 376, 17)}[env_id]
+    spec = T.Spec(O, list(hid), A, "gauss")
+    vspec = T.Spec(O + 1, list(hid), 1, "linear")
     th = T.mlp_init(rng, spec.shapes, True)
     thv = T.mlp_init(rng, vspec.shapes, False)
-    envs = RO.Envs(RO.HOPPER, E, seed)
-    fs = RO.FilterState(12)
+    envs = RO.Envs(kind, E, seed)
+    fs = RO.FilterState(O + 1)
     t0 = time.perf_counter()
     out, fs = RO.collect(envs, fs, spec, th, Tn, 1000, 0)
     N = E * Tn
-    ob = out["obs"].reshape(N, 11).astype(np.float64)
+    ob = out["obs"].reshape(N, O).astype(np.float64)
     X = np.concatenate([ob, (out["ep_t"].reshape(N) / 1000.0)[:, None]], axis=1)
     v = T.mlp_forward(vspec, thv, X, np.float32)[0][:, 0].astype(np.float64).reshape(Tn, E)
     flags = out["flags"]
     adv, ret = T.gae_batched(out["rew"].astype(np.float64), v, (flags & 1) > 0, (flags & 2) > 0, 0.995, 0.97)
     adv = T.standardize(adv).reshape(N)
     T.vf_fit(vspec, thv, X, ret.reshape(N), mixfrac=0.1, maxiter=2, dtype=np.float32)
-    T.trpo_update(spec, th, ob, out["act"].reshape(N, 3).astype(np.float64), adv,
-                  out["prob"].reshape(N, 6).astype(np.float64), cg_damping=0.1, max_kl=0.01, dtype=np.float32)
+    T.trpo_update(spec, th, ob, out["act"].reshape(N, A).astype(np.float64), adv,
+                  out["prob"].reshape(N, 2 * A).astype(np.float64), cg_damping=0.1, max_kl=0.01, dtype=np.float32)
     dt = time.perf_counter() - t0
     return {"value": N / dt, "unit": "env-steps/s", "cores": int(threads), "kind": "port",
-            "sample": f"one full TRPO iteration (rollout+GAE+VF fit+update) of the numpy oracle on Hopper "
-                      f"{E} envs x {Tn} steps = {N} env-steps, float32 update / float64 rollout, {dt:.1f} s"}
+            "sample": f"one full TRPO iteration (rollout+GAE+VF fit+update) of the numpy oracle on {env_id} "
+                      f"{E} envs x {Tn} steps = {N} env-steps, net {O}-{'-'.join(map(str, hid))}-{A}, "
+                      f"float32 update / float64 rollout, {dt:.1f} s"}
 
 
 def main():
@@ -85,8 +94,9 @@ def main():
     ap.add_argument("--env", default="Hopper-v2")
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--horizon", type=int, default=1024)
-    ap.add_argument("--cpu-envs", type=int, default=1024)
-    ap.add_argument("--cpu-horizon", type=int, default=256)
+    ap.add_argument("--hid", default=None, help="hidden sizes, e.g. 512,512,512 (default 64,64; Humanoid 512x3)")
+    ap.add_argument("--cpu-envs", type=int, default=None)
+    ap.add_argument("--cpu-horizon", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -102,8 +112,12 @@ def main():
     rank, world = comm.rank, comm.world
     env = make(args.env)
     E, Tn = args.envs, args.horizon
+    humanoid = args.env == "Humanoid-v2"
+    hid = [int(h) for h in args.hid.split(",")] if args.hid else ([512, 512, 512] if humanoid else [64, 64])
+    cpu_E = args.cpu_envs or (64 if humanoid else 1024)
+    cpu_T = args.cpu_horizon or (64 if humanoid else 256)
     cfg = dict(timestep_limit=env.spec.max_episode_steps, gamma=0.995, lam=0.97, max_kl=0.01, cg_damping=0.1,
-               n_envs=E, horizon=Tn, filter=1, seed=0, hid_sizes=[64, 64], activation="tanh", use_graph=1)
+               n_envs=E, horizon=Tn, filter=1, seed=0, hid_sizes=hid, activation="tanh", use_graph=1)
     agent = TrpoAgent(env.observation_space, env.action_space, cfg, comm=comm)
     collector = agent.make_collector(env, cfg)
 
@@ -157,7 +171,7 @@ def main():
     value = total_steps / elapsed
     if rank != 0:
         return
-    fpr = flops_per_row(env.obs_dim, env.act_dim)
+    fpr = flops_per_row(agent.policy.net)
     kinfo = {}
     for name in ("fvp_jvp_rows", "fvp_vjp"):
         if name in kern:
@@ -166,8 +180,8 @@ def main():
             kinfo[name] = dict(launches=cnt, mean_ms=mean_ms, total_ms=tot_ms, tflops=achieved)
     dom = max(kinfo, key=lambda k: kinfo[k]["total_ms"])
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
-    if os.path.exists(pmc_path):
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")  # measured on the default Hopper config
+    if os.path.exists(pmc_path) and args.env == "Hopper-v2" and not agent.policy.net.layered:
         with open(pmc_path) as f:
             traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
     roofline = {"bound": "mfma", "achieved": round(kinfo[dom]["tflops"], 3), "peak": PEAK_FP32_TFLOPS,
@@ -187,7 +201,9 @@ def main():
         "config": {"workload": f"{args.env} (surrogate dynamics) {E} envs x {Tn} steps per GPU, one TRPO iteration "
                                "per step (rollout+GAE+VF L-BFGS+TRPO CG/linesearch)",
                    "envs_per_gpu": E, "horizon": Tn, "global_batch": E * Tn * world, "parallelism": f"dp{world}",
-                   "policy": f"{env.obs_dim}-64-64-{env.act_dim} tanh DiagGauss", "gamma": 0.995, "lam": 0.97,
+                   "policy": f"{env.obs_dim}-{'-'.join(map(str, hid))}-{env.act_dim} tanh DiagGauss "
+                             f"({'layered GEMM' if agent.policy.net.layered else 'fused'} path)",
+                   "gamma": 0.995, "lam": 0.97,
                    "max_kl": 0.01, "cg_damping": 0.1},
         "trpo_iters_per_sec": round(K / elapsed, 4),
         "rollout_env_steps_per_sec": round(n_local * world * K / (phases["rollout"] * 1e-3), 1),
@@ -197,7 +213,7 @@ def main():
         "roofline_gae": gae,
     }
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_envs, args.cpu_horizon)
+        line["cpu_baseline"] = cpu_baseline(cpu_E, cpu_T, args.env, hid)
     print(json.dumps(line), flush=True)
 
 

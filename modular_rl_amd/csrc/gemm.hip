@@ -8,14 +8,18 @@
 //   epilogue: store | +bias | tanh(. + bias) | . * (1 - H^2) | split-K partial slab
 //
 // Layer forward  Y = tanh(X W + b)        NN, EPI_TANH
-// JVP            dY = (1-Y^2)(dX W + X dW + db)    NN dual + bias, then rows-scale
+// JVP            dY = (1-Y^2)(dX W + X dW + db)    NN dual + bias, EPI_DTANH
 // VJP input grad dX = (G W^T) (1 - X^2)    NT, EPI_DTANH
 // weight grad    dW = X^T G  (K = rows)    TN, EPI_SLAB (split-K over rows, slabs reduced
 //                                          by mrl_reduce_rows_f32 in fixed order)
 //
-// Block 128x128x32, 256 threads = 4 waves, each wave a 64x64 tile = 2x2 MFMA tiles.
-// Global->LDS with coalesced loads; LDS tiles are k-major with an odd row pitch (129)
-// so both the staging writes and the MFMA operand reads are bank-conflict free.
+// Block 128x128x32, 256 threads = 4 waves, each wave a 64x64 tile = 2x2 MFMA tiles
+// (narrow 128x32 variant: 4 waves x 32x32 for head layers and small-M launches).
+// Global -> registers -> LDS, double-buffered so the next tile's loads overlap the
+// MFMAs.  LDS tiles are stored [row c][k] with a 36-float pitch; MFMA k-step (u, v)
+// of lane half h takes tile k = 16h + 4u + v, so a lane's operands for 4 k-steps are
+// one aligned ds_read_b128 and every staging write is a ds_write_b128.  Blocks are
+// dealt to XCDs in contiguous tile runs; interior tiles skip all bounds checks.
 #include <math.h>
 
 #include "../../include/mrl_hip.h"
@@ -24,7 +28,7 @@
 
 namespace mrl {
 
-constexpr int GBM = 128, GBN = 128, GBK = 32, GLD = 129;
+constexpr int GBM = 128, GBN = 128, GBK = 32, LDP = 36;  // LDP: LDS row pitch (floats)
 
 struct GemmArgs {
   int64_t M, N, K;
@@ -45,78 +49,93 @@ struct GemmArgs {
   const int32_t* skip;
 };
 
-// One [GBK x TW] operand tile per K step (TW = 128, or 32 for the narrow head tiles),
-// staged global -> registers -> LDS as dst[k][c] (pitch TW+1: conflict-free);
-// c = tile row (A) or col (B).  CONTIG_C: the source is contiguous along c (lanes along
-// c, coalesced), else along k (each thread reads TW/8 consecutive k of one c, 16 B at
-// a time when aligned).  Rows c >= Creal of an in-range tile read as 1 (the ones-row
-// of the bias gradient).
-template <bool CONTIG_C, int TW>
-__device__ inline void load_tile(float (&r)[TW / 8], const float* __restrict__ src, int64_t ld, int64_t c0,
+// One [TW x GBK] operand tile per K step (TW = 128, or 32 for the narrow tiles),
+// staged global -> registers -> LDS as dst[c][k] (natural k order, pitch LDP = 36);
+// c = tile row (A) or col (B).  Each thread stages TW/8 values as float4 groups of 4
+// consecutive k of one c, so every LDS write is a ds_write_b128.
+//  * K_CONTIG (source contiguous along k, e.g. activations [row][unit] as A): 8 lanes
+//    cover one 128 B row segment -> each wave load instruction reads 8 full lines.
+//  * otherwise (source contiguous along c): lanes along c, 4 coalesced scalar loads
+//    (k .. k+3) per float4.
+// FULL: the whole tile is in range (no per-element checks).  Rows c >= Creal of an
+// in-range tile read as 1 (the ones-row of the bias gradient).
+template <bool K_CONTIG, int TW>
+struct Stage {
+  static constexpr int NV = TW / 32;  // float4 groups per thread
+  // (c, k) of float4 group w for this thread
+  __device__ static inline int c_of(int t, int w) { return K_CONTIG ? (t >> 3) + 32 * w : t % TW; }
+  __device__ static inline int k_of(int t, int w) { return K_CONTIG ? 4 * (t & 7) : (t / TW) * (TW / 8) + 4 * w; }
+};
+
+template <bool K_CONTIG, int TW, bool FULL>
+__device__ inline void load_tile(float4 (&r)[TW / 32], const float* __restrict__ src, int64_t ld, int64_t c0,
                                  int64_t k0, int64_t C, int64_t Kend, int64_t Creal, bool vec) {
-  constexpr int TPC = 256 / TW;  // threads per c (!CONTIG_C) or k rows per pass (CONTIG_C)
-  constexpr int PER = TW / 8;    // values per thread
+  using S = Stage<K_CONTIG, TW>;
   const int t = threadIdx.x;
-  if (CONTIG_C) {
-    const int c = t % TW, kb = t / TW;
-    const int64_t gc = c0 + c;
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int64_t gk = k0 + kb + TPC * q;
-      const bool in = gc < C && gk < Kend;
-      r[q] = (in && gc < Creal) ? src[gk * ld + gc] : (in ? 1.f : 0.f);
-    }
-  } else {
-    const int c = t / TPC, kq = t % TPC;
-    const int64_t gc = c0 + c, gk0 = k0 + kq * PER;
-    if (vec && gc < Creal && gk0 + PER <= Kend) {
-      const float4* p = reinterpret_cast<const float4*>(src + gc * ld + gk0);
+  for (int w = 0; w < S::NV; ++w) {
+    const int64_t gc = c0 + S::c_of(t, w), gk = k0 + S::k_of(t, w);
+    float v[4];
+    if (FULL) {
+      if (K_CONTIG) {
+        const float* p = src + gc * ld + gk;
+        if (vec) {
+          const float4 x = *reinterpret_cast<const float4*>(p);
+          v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+        } else {
 #pragma unroll
-      for (int i = 0; i < PER / 4; ++i) {
-        const float4 v = p[i];
-        r[4 * i] = v.x;
-        r[4 * i + 1] = v.y;
-        r[4 * i + 2] = v.z;
-        r[4 * i + 3] = v.w;
+          for (int q = 0; q < 4; ++q) v[q] = p[q];
+        }
+      } else {
+        const float* p = src + gk * ld + gc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = p[q * ld];
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const int64_t gk = gk0 + q;
-        const bool in = gc < C && gk < Kend;
-        r[q] = (in && gc < Creal) ? src[gc * ld + gk] : (in ? 1.f : 0.f);
+      for (int q = 0; q < 4; ++q) {
+        const bool in = gc < C && gk + q < Kend;
+        const int64_t off = K_CONTIG ? gc * ld + gk + q : (gk + q) * ld + gc;
+        v[q] = (in && gc < Creal) ? src[off] : (in ? 1.f : 0.f);
       }
     }
+    r[w] = make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
-template <bool CONTIG_C, int TW>
-__device__ inline void store_tile(float* dst, const float (&r)[TW / 8]) {
-  constexpr int TPC = 256 / TW, PER = TW / 8, LD = TW + 1;
+template <bool K_CONTIG, int TW>
+__device__ inline void store_tile(float* dst, const float4 (&r)[TW / 32]) {
+  using S = Stage<K_CONTIG, TW>;
   const int t = threadIdx.x;
-  if (CONTIG_C) {
-    const int c = t % TW, kb = t / TW;
 #pragma unroll
-    for (int q = 0; q < PER; ++q) dst[(kb + TPC * q) * LD + c] = r[q];
-  } else {
-    const int c = t / TPC, kq = t % TPC;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) dst[(kq * PER + q) * LD + c] = r[q];
-  }
+  for (int w = 0; w < S::NV; ++w)
+    *reinterpret_cast<float4*>(dst + S::c_of(t, w) * LDP + S::k_of(t, w)) = r[w];
 }
-
-constexpr int GEMM_LDS_FLOATS = 4 * GBK * GLD;  // double-buffered A and B tiles (BN = 128)
 
 // BN = 128: 2x2 waves, each a 64x64 tile (2x2 MFMA tiles).  BN = 32 (narrow heads,
-// n <= 32): 4x1 waves, each a 32x32 tile.
+// small M): 4x1 waves, each a 32x32 tile.
 template <bool AT, bool BT, int BN>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
-  constexpr int MI = BN == 128 ? 2 : 1, NI = BN == 128 ? 2 : 1, BLD = BN + 1;
+  constexpr int MI = BN == 128 ? 2 : 1, NI = BN == 128 ? 2 : 1;
+  constexpr int A_FL = GBM * LDP, B_FL = BN * LDP;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if (g.skip != nullptr && *g.skip != 0) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
   const int wm = BN == 128 ? wave >> 1 : wave, wn = BN == 128 ? wave & 1 : 0;
-  const int64_t m0 = (int64_t)blockIdx.y * GBM, n0 = (int64_t)blockIdx.x * BN;
+  // XCD-aware tile order: the dispatcher deals consecutive block ids round-robin to
+  // the 8 XCDs, so give each XCD a contiguous run of (m, n) tiles -- the N-tiles that
+  // share one A row panel then run on the same XCD and re-read it from its L2.
+  int64_t tm = blockIdx.y, tn = blockIdx.x;
+  {
+    const int64_t nx = gridDim.x, tiles = nx * gridDim.y;
+    const int64_t L = blockIdx.x + nx * (int64_t)blockIdx.y;
+    if (tiles % 8 == 0) {
+      const int64_t T = (L % 8) * (tiles / 8) + L / 8;
+      tm = T / nx;
+      tn = T % nx;
+    }
+  }
+  const int64_t m0 = tm * GBM, n0 = tn * BN;
   int64_t kbeg = 0, kend = g.K;
   if (g.epi == MRL_GEMM_SLAB) {
     kbeg = (int64_t)blockIdx.z * g.k_chunk;
@@ -133,50 +152,84 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
   // 16-byte loads along k need ld % 4 == 0 and 16 B aligned bases
   const bool va = !AT && (g.lda & 3) == 0 && ((reinterpret_cast<uintptr_t>(g.A) | reinterpret_cast<uintptr_t>(g.A2)) & 15) == 0;
   const bool vb = BT && (g.ldb & 3) == 0 && ((reinterpret_cast<uintptr_t>(g.B) | reinterpret_cast<uintptr_t>(g.B2)) & 15) == 0;
-  float ra[16], rb[BN / 8];
+  // interior block: every tile in M/N range (the K tail is checked per tile)
+  const bool interior = m0 + GBM <= g.m_real && n0 + BN <= g.N;
+  float4 ra[GBM / 32], rb[BN / 32];
   auto load = [&](int64_t t) {
     const int p = t >= ntk ? 1 : 0;
     const int64_t k0 = kbeg + (t - p * ntk) * GBK;
-    // A tile: c = row i in [m0, m0+128), contiguous along i iff a_trans
-    load_tile<AT, GBM>(ra, p ? g.A2 : g.A, g.lda, m0, k0, g.M, kend, g.m_real, va);
-    // B tile: c = col j in [n0, n0+BN), contiguous along j iff !b_trans
-    load_tile<!BT, BN>(rb, p ? g.B2 : g.B, g.ldb, n0, k0, g.N, kend, g.N, vb);
+    const float* Ap = p ? g.A2 : g.A;
+    const float* Bp = p ? g.B2 : g.B;
+    if (interior && k0 + GBK <= kend) {
+      load_tile<!AT, GBM, true>(ra, Ap, g.lda, m0, k0, g.M, kend, g.m_real, va);
+      load_tile<BT, BN, true>(rb, Bp, g.ldb, n0, k0, g.N, kend, g.N, vb);
+    } else {
+      load_tile<!AT, GBM, false>(ra, Ap, g.lda, m0, k0, g.M, kend, g.m_real, va);
+      load_tile<BT, BN, false>(rb, Bp, g.ldb, n0, k0, g.N, kend, g.N, vb);
+    }
   };
   if (nt > 0) load(0);
   for (int64_t t = 0; t < nt; ++t) {
-    float* As = smem + (t & 1) * GBK * (GLD + BLD);
-    float* Bs = As + GBK * GLD;
-    store_tile<AT, GBM>(As, ra);
-    store_tile<!BT, BN>(Bs, rb);
+    float* As = smem + (t & 1) * (A_FL + B_FL);
+    float* Bs = As + A_FL;
+    store_tile<!AT, GBM>(As, ra);
+    store_tile<BT, BN>(Bs, rb);
     __syncthreads();
     if (t + 1 < nt) load(t + 1);  // next tile's global loads overlap this tile's MFMAs
+    // MFMA k-step (u, v) of lane half h covers tile k = 16h + 4u + v (any k->step
+    // assignment is valid when A and B agree): one ds_read_b128 per operand per 4 steps
 #pragma unroll
-    for (int s = 0; s < GBK / 2; ++s) {
-      const int k = 2 * s + h;
-      float av[MI], bv[NI];
+    for (int u = 0; u < 4; ++u) {
+      float4 av[MI], bv[NI];
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) av[mi] = As[k * GLD + wm * 32 * MI + 32 * mi + j];
+      for (int mi = 0; mi < MI; ++mi)
+        av[mi] = *reinterpret_cast<const float4*>(As + (wm * 32 * MI + 32 * mi + j) * LDP + h * 16 + 4 * u);
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) bv[ni] = Bs[k * BLD + wn * 32 * NI + 32 * ni + j];
+      for (int ni = 0; ni < NI; ++ni)
+        bv[ni] = *reinterpret_cast<const float4*>(Bs + (wn * 32 * NI + 32 * ni + j) * LDP + h * 16 + 4 * u);
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA32(av[mi], bv[ni], acc[mi][ni]);
+        for (int ni = 0; ni < NI; ++ni) {
+          acc[mi][ni] = MFMA32(av[mi].x, bv[ni].x, acc[mi][ni]);
+          acc[mi][ni] = MFMA32(av[mi].y, bv[ni].y, acc[mi][ni]);
+          acc[mi][ni] = MFMA32(av[mi].z, bv[ni].z, acc[mi][ni]);
+          acc[mi][ni] = MFMA32(av[mi].w, bv[ni].w, acc[mi][ni]);
+        }
     }
   }
   // epilogue: lane holds column j, rows cperm(r, h) of each 32x32 tile
   float* C = g.C;
   if (g.epi == MRL_GEMM_SLAB) C += (int64_t)blockIdx.z * g.slab_stride;
+  const bool full_out = m0 + GBM <= g.M && n0 + BN <= g.N;
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
       const int64_t col = n0 + wn * 32 * NI + ni * 32 + j;
+      const int64_t rbase = m0 + wm * 32 * MI + mi * 32;
+      if (full_out) {
+        // interior tile: no per-element checks, the 16 H loads are issued together
+        const float bv = g.bias != nullptr ? g.bias[col] : 0.f;
+        float hv[16];
+        if (g.epi == MRL_GEMM_DTANH) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) hv[r] = g.H[(rbase + cperm(r, h)) * g.ldh + col];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = acc[mi][ni][r] + bv;
+          if (g.epi == MRL_GEMM_TANH) v = tanh_fast(v);
+          else if (g.epi == MRL_GEMM_DTANH) v *= (1.f - hv[r] * hv[r]);
+          C[(rbase + cperm(r, h)) * g.ldc + col] = v;
+        }
+        continue;
+      }
       if (col >= g.N) continue;
       const float bv = g.bias != nullptr ? g.bias[col] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * 32 * MI + mi * 32 + cperm(r, h);
+        const int64_t row = rbase + cperm(r, h);
         if (row >= g.M) continue;
         float v = acc[mi][ni][r] + bv;
         if (g.epi == MRL_GEMM_TANH) v = tanh_fast(v);
@@ -335,14 +388,14 @@ int mrl_gemm(const mrl_gemm_desc* d, const int32_t* skip, void* stream) {
     // narrow 128x32 tiles: head layers (n_out <= 32) without 128-wide MFMA waste, and
     // small-M launches (the rollout's per-step forward over E rows) with 4x the blocks
     const dim3 grid((unsigned)((g.N + 31) / 32), gm, (unsigned)splits);
-    const size_t shm = 2 * GBK * (GLD + 33) * sizeof(float);
+    const size_t shm = 2 * (GBM + 32) * LDP * sizeof(float);
     if (!d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, false, 32>), grid, dim3(256), shm, s, g);
     else if (!d->a_trans && d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, true, 32>), grid, dim3(256), shm, s, g);
     else if (d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<true, false, 32>), grid, dim3(256), shm, s, g);
     else hipLaunchKernelGGL((gemm_f32_kernel<true, true, 32>), grid, dim3(256), shm, s, g);
   } else {
     const dim3 grid((unsigned)((g.N + GBN - 1) / GBN), gm, (unsigned)splits);
-    const size_t shm = GEMM_LDS_FLOATS * sizeof(float);
+    const size_t shm = 2 * (GBM + GBN) * LDP * sizeof(float);
     if (!d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, false, 128>), grid, dim3(256), shm, s, g);
     else if (!d->a_trans && d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, true, 128>), grid, dim3(256), shm, s, g);
     else if (d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<true, false, 128>), grid, dim3(256), shm, s, g);

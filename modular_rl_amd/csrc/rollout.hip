@@ -442,29 +442,47 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, MlpDims md
 // env step, raw next obs + reward as SoA rows [O+1][E] fp64, block partials).
 constexpr int MAXD_L = 384;  // obs dims + 1 on the layered path
 
-// per-block two-pass partial of the SoA rows raw[k][e0 .. e0+nvalid) for k < D
-__device__ inline void publish_partial_raw(const RollArgs& a, int e0, int nvalid, int D, bool with_rew,
-                                           double* rec_out) {
+// Layered-path kernels are parallel over (env block, 32-column chunk): the 376-d obs
+// makes every per-column loop long, so no block walks all columns.
+constexpr int LCOLS = 32;
+
+// per-(env block, column chunk) two-pass partial of the SoA rows raw[k][e0 .. e0+nvalid):
+// column k = 32*blockIdx.y + (tid & 31); 8 thread groups stride the envs.
+__global__ __launch_bounds__(RB) void lrollout_partials_kernel(RollArgs a, int D, int rec_parity, int with_rew) {
+  __shared__ double red[8][LCOLS];
   const int E = a.d.n_envs;
-  const int g = threadIdx.x >> 4, j = threadIdx.x & 15;
-  double* r = rec_out + (int64_t)blockIdx.x * a.RS;
-  for (int k = g; k < D; k += RB / 16) {
-    const double* col = a.b.raw_obs + (int64_t)k * E + e0;
-    double sm = 0.0;
-    for (int i = j; i < nvalid; i += 16) sm += col[i];
-    const double mean = nvalid > 0 ? sum16(sm) / (double)nvalid : 0.0;
-    double m2 = 0.0;
-    for (int i = j; i < nvalid; i += 16) {
+  const int e0 = blockIdx.x * ENVS_PER_BLOCK;
+  const int nvalid = min(ENVS_PER_BLOCK, E - e0);
+  const int c = threadIdx.x & (LCOLS - 1), g = threadIdx.x >> 5;
+  const int k = blockIdx.y * LCOLS + c;
+  double* r = a.b.records + (int64_t)rec_parity * a.nb * a.RS + (int64_t)blockIdx.x * a.RS;
+  const double* col = a.b.raw_obs + (int64_t)(k < D ? k : 0) * E + e0;
+  double sm = 0.0;
+  if (k < D)
+    for (int i = g; i < nvalid; i += 8) sm += col[i];
+  red[g][c] = sm;
+  __syncthreads();
+  double tot = 0.0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) tot += red[q][c];
+  const double mean = nvalid > 0 ? tot / (double)nvalid : 0.0;
+  __syncthreads();
+  double m2 = 0.0;
+  if (k < D)
+    for (int i = g; i < nvalid; i += 8) {
       const double dv = col[i] - mean;
       m2 += dv * dv;
     }
-    m2 = sum16(m2);
-    if (j == 0) {
-      r[2 + k] = mean;
-      r[2 + D + k] = m2;
-    }
+  red[g][c] = m2;
+  __syncthreads();
+  if (g == 0 && k < D) {
+    double t2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t2 += red[q][c];
+    r[2 + k] = mean;
+    r[2 + D + k] = t2;
   }
-  if (threadIdx.x == 0) {
+  if (blockIdx.y == 0 && threadIdx.x == 0) {
     r[0] = (double)nvalid;
     r[1] = with_rew ? (double)nvalid : 0.0;
   }
@@ -473,11 +491,10 @@ __device__ inline void publish_partial_raw(const RollArgs& a, int e0, int nvalid
 template <int ENV>
 __global__ __launch_bounds__(RB) void lrollout_reset_kernel(RollArgs a) {
   using EC = EnvC<ENV>;
-  constexpr int O = EC::OBS, D = O + 1;
+  constexpr int O = EC::OBS;
   const int E = a.d.n_envs;
-  const int e0 = blockIdx.x * ENVS_PER_BLOCK;
-  const int e = e0 + threadIdx.x;
-  if (threadIdx.x < ENVS_PER_BLOCK && e < E) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < E) {
     double s[EC::NS];
     reset_env<ENV>(a, e, s);
 #pragma unroll
@@ -486,111 +503,120 @@ __global__ __launch_bounds__(RB) void lrollout_reset_kernel(RollArgs a) {
     EC::obs_out(s, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
     raw[(int64_t)O * E + e] = 0.0;
   }
-  __threadfence_block();
-  __syncthreads();
-  publish_partial_raw(a, e0, min(ENVS_PER_BLOCK, E - e0), D, false, a.b.records);
 }
 
+// merge of the batch records (block order, two passes: n, mean = sum n_b m_b / n,
+// M2 = sum M2_b + n_b (m_b - mean)^2 -- oracle/rollout_np.py _batch) into the running
+// stat, then the normalised obs rows of step t for this (env block, column chunk)
 template <int ENV>
 __global__ __launch_bounds__(RB) void lrollout_obs_kernel(RollArgs a, int t) {
   using EC = EnvC<ENV>;
   constexpr int O = EC::OBS, D = O + 1;
-  __shared__ double fmean[MAXD_L], fden[MAXD_L];
-  __shared__ float tile[32 * 129];
+  __shared__ double fmean[LCOLS], fden[LCOLS];
+  __shared__ float tile[LCOLS * 129];
   const int E = a.d.n_envs;
-  // 1. running-stat merge of step t's raw obs (and step t-1's rewards), as the fused kernel
   const double* fs_in = a.b.filter_state + (t & 1) * a.FS;
   double* fs_out = a.b.filter_state + ((t + 1) & 1) * a.FS;
-  const double* rec_in = a.b.records + (int64_t)(t & 1) * a.nb * a.RS;
-  const int g = threadIdx.x >> 4, jj = threadIdx.x & 15;
-  for (int k = g; k < D; k += RB / 16) {
+  const double* rec = a.b.records + (int64_t)(t & 1) * a.nb * a.RS;
+  const int kbase = blockIdx.y * LCOLS;
+  if (threadIdx.x < LCOLS && kbase + (int)threadIdx.x < D) {
+    const int k = kbase + threadIdx.x;
     const bool isr = (k == O);
+    double bn = 0.0, sm = 0.0;
+    for (int b = 0; b < a.nb; ++b) {
+      const double* r = rec + (int64_t)b * a.RS;
+      const double nb_ = r[isr ? 1 : 0];
+      bn += nb_;
+      sm += nb_ * r[2 + k];
+    }
+    double bm = 0.0, bs = 0.0;
+    if (bn > 0.0) {
+      bm = sm / bn;
+      for (int b = 0; b < a.nb; ++b) {
+        const double* r = rec + (int64_t)b * a.RS;
+        const double nb_ = r[isr ? 1 : 0];
+        if (nb_ > 0.0) {
+          const double dm = r[2 + k] - bm;
+          bs += r[2 + D + k] + nb_ * dm * dm;
+        }
+      }
+    }
     double n = fs_in[isr ? 1 : 0], M = fs_in[2 + k], S = fs_in[2 + D + k];
-    double bn, bm, bs;
-    batch_of_records(rec_in, a.nb, a.RS, D, O, k, jj, bn, bm, bs);
     chan_merge(n, M, S, bn, bm, bs);
-    if (jj == 0 && blockIdx.x == 0) {
+    if (blockIdx.x == 0) {
       if (k == 0) fs_out[0] = n;
       if (isr) fs_out[1] = n;
       fs_out[2 + k] = M;
       fs_out[2 + D + k] = S;
     }
-    if (!isr && jj == 0) {
-      const double var = n > 1.0 ? S / (n - 1.0) : M * M;  // running_stat.py:27
-      fmean[k] = M;
-      fden[k] = sqrt(var) + 1e-8;
-    }
+    const double var = n > 1.0 ? S / (n - 1.0) : M * M;  // running_stat.py:27
+    fmean[threadIdx.x] = M;
+    fden[threadIdx.x] = sqrt(var) + 1e-8;
   }
   __syncthreads();
-  // 2. normalised obs rows (core.py:191-192): SoA raw -> LDS tile -> row-major fp32 rows
+  // normalised obs rows (core.py:191-192): SoA raw -> LDS tile -> row-major fp32 rows
   const int e0 = blockIdx.x * ENVS_PER_BLOCK;
   const int nvalid = min(ENVS_PER_BLOCK, E - e0);
   const int64_t row0 = (int64_t)t * E + e0;
-  for (int c0 = 0; c0 < O; c0 += 32) {
-    {
-      const int el = threadIdx.x & 127, kb = threadIdx.x >> 7;
-#pragma unroll 4
+  {
+    const int el = threadIdx.x & 127, kb = threadIdx.x >> 7;
+    double v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = kbase + kb + 2 * q;
+      v[q] = (k < O && el < nvalid) ? a.b.raw_obs[(int64_t)k * E + e0 + el] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int kl = kb + 2 * q;
+      double x = v[q];
+      if (a.d.filter) {
+        x = x - fmean[kl];
+        x = x / fden[kl];
+        x = x < -5.0 ? -5.0 : (x > 5.0 ? 5.0 : x);
+      }
+      tile[kl * 129 + el] = (float)x;
+    }
+  }
+  __syncthreads();
+  {
+    const int el = threadIdx.x >> 1, half = threadIdx.x & 1;
+    if (el < nvalid) {
+      float* dst = a.b.obs + (row0 + el) * O;
+#pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int k = c0 + kb + 2 * q;
-        float vf = 0.f;
-        if (k < O && el < nvalid) {
-          double v = a.b.raw_obs[(int64_t)k * E + e0 + el];
-          if (a.d.filter) {
-            v = v - fmean[k];
-            v = v / fden[k];
-            v = v < -5.0 ? -5.0 : (v > 5.0 ? 5.0 : v);
-          }
-          vf = (float)v;
-        }
-        tile[(kb + 2 * q) * 129 + el] = vf;
+        const int k = kbase + half * 16 + q;
+        if (k < O) dst[k] = tile[(half * 16 + q) * 129 + el];
       }
     }
-    __syncthreads();
-    {
-      const int el = threadIdx.x >> 1, half = threadIdx.x & 1;
-      if (el < nvalid) {
-        float* dst = a.b.obs + (row0 + el) * O;
-#pragma unroll 4
-        for (int q = 0; q < 16; ++q) {
-          const int k = c0 + half * 16 + q;
-          if (k < O) dst[k] = tile[(half * 16 + q) * 129 + el];
-        }
-      }
-    }
-    __syncthreads();
   }
 }
 
+// sample + env step + raw next obs / reward (SoA) for one env per thread
 template <int ENV>
 __global__ __launch_bounds__(RB) void lrollout_act_kernel(RollArgs a, const float* __restrict__ zrows,
                                                           const float* __restrict__ logstd, int t) {
   using EC = EnvC<ENV>;
-  constexpr int O = EC::OBS, D = O + 1, NS = EC::NS, A = EC::ACT;
+  constexpr int O = EC::OBS, NS = EC::NS, A = EC::ACT;
   const int E = a.d.n_envs;
-  const int e0 = blockIdx.x * ENVS_PER_BLOCK;
-  const int e = e0 + threadIdx.x;
-  double* rec_out = a.b.records + (int64_t)((t + 1) & 1) * a.nb * a.RS;
-  if (threadIdx.x < ENVS_PER_BLOCK && e < E) {
-    const int64_t row = (int64_t)t * E + e;
-    double s[NS];
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int64_t row = (int64_t)t * E + e;
+  double s[NS];
 #pragma unroll
-    for (int i = 0; i < NS; ++i) s[i] = a.b.env_state[(int64_t)i * E + e];
-    float z[A];
+  for (int i = 0; i < NS; ++i) s[i] = a.b.env_state[(int64_t)i * E + e];
+  float z[A];
 #pragma unroll
-    for (int q = 0; q < A; ++q) z[q] = zrows[(int64_t)e * A + q];
-    double zn[A + 1];
-    draw_noise<ENV>(a, e, row, t, zn);
-    double rew = 0.0;
-    bool done = false;
-    sample_and_step<ENV>(a, row, z, logstd, zn, s, rew, done);
-    finish_env_step<ENV>(a, e, row, t, s, rew, done);
-    double* raw = a.b.raw_obs;
-    EC::obs_out(s, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
-    raw[(int64_t)O * E + e] = rew;
-  }
-  __threadfence_block();
-  __syncthreads();
-  publish_partial_raw(a, e0, min(ENVS_PER_BLOCK, E - e0), D, true, rec_out);
+  for (int q = 0; q < A; ++q) z[q] = zrows[(int64_t)e * A + q];
+  double zn[A + 1];
+  draw_noise<ENV>(a, e, row, t, zn);
+  double rew = 0.0;
+  bool done = false;
+  sample_and_step<ENV>(a, row, z, logstd, zn, s, rew, done);
+  finish_env_step<ENV>(a, e, row, t, s, rew, done);
+  double* raw = a.b.raw_obs;
+  EC::obs_out(s, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
+  raw[(int64_t)O * E + e] = rew;
 }
 
 __global__ void rollout_finish_kernel(RollArgs a, int O) {
@@ -696,7 +722,11 @@ int mrl_rollout_reset_rows(const mrl_rollout_desc* d, const mrl_rollout_bufs* b,
   int rc = check_rows(d, b);
   if (rc) return rc;
   RollArgs a = make_args(d, b);
-  MRL_DISPATCH_ENV(d->env_id, lrollout_reset_kernel, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a);
+  const int D = env_info(d->env_id).obs + 1;
+  // one wave per block: the per-env step is latency-bound, so spread the waves over CUs
+  const dim3 genv((d->n_envs + 63) / 64), gpart(a.nb, (D + LCOLS - 1) / LCOLS);
+  MRL_DISPATCH_ENV(d->env_id, lrollout_reset_kernel, genv, dim3(64), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(lrollout_partials_kernel, gpart, dim3(RB), 0, (hipStream_t)stream, a, D, 0, 0);
   return hip_check(hipGetLastError(), "mrl_rollout_reset_rows");
 }
 
@@ -706,7 +736,8 @@ int mrl_rollout_obs(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, int32_
   if (!b->obs) return fail(E_ARG, "null obs");
   if (t < 0 || t >= d->horizon) return fail(E_ARG, "t out of range");
   RollArgs a = make_args(d, b);
-  MRL_DISPATCH_ENV(d->env_id, lrollout_obs_kernel, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a, t);
+  const dim3 grid(a.nb, (env_info(d->env_id).obs + 1 + LCOLS - 1) / LCOLS);
+  MRL_DISPATCH_ENV(d->env_id, lrollout_obs_kernel, grid, dim3(RB), 0, (hipStream_t)stream, a, t);
   return hip_check(hipGetLastError(), "mrl_rollout_obs");
 }
 
@@ -722,7 +753,10 @@ int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, cons
   if (gauss && !logstd) return fail(E_ARG, "DiagGauss needs logstd");
   if (t < 0 || t >= d->horizon) return fail(E_ARG, "t out of range");
   RollArgs a = make_args(d, b);
-  MRL_DISPATCH_ENV(d->env_id, lrollout_act_kernel, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a, z, logstd, t);
+  const int D = ei.obs + 1;
+  const dim3 genv((d->n_envs + 63) / 64), gpart(a.nb, (D + LCOLS - 1) / LCOLS);
+  MRL_DISPATCH_ENV(d->env_id, lrollout_act_kernel, genv, dim3(64), 0, (hipStream_t)stream, a, z, logstd, t);
+  hipLaunchKernelGGL(lrollout_partials_kernel, gpart, dim3(RB), 0, (hipStream_t)stream, a, D, (t + 1) & 1, 1);
   return hip_check(hipGetLastError(), "mrl_rollout_act");
 }
 
