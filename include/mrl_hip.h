@@ -62,6 +62,12 @@ int mrl_mlp_pack(const mrl_mlp_desc* d, const float* theta, float* image, int32_
 #define MRL_EPI_SURRGRAD 2  /* LOSSES + ghead <- d surr / d head rows              trpo.py:42-43     */
 #define MRL_EPI_VFLOSS 3    /* partial <- sum (y-yhat)^2; ghead <- 2(yhat-y)/N_glob core.py:611-617  */
 #define MRL_EPI_FVP 4       /* forward + JVP(tangent) + KL metric -> ghead rows      trpo.py:45-58   */
+#define MRL_EPI_PPOGRAD 5   /* LOSSES + ghead <- d(surr + kl_coeff * kl)/d head rows; kl_coeff = the
+                               whole d pensurr / d kl, host-computed            ppo.py:46-52       */
+#define MRL_EPI_PPOSGD 6    /* one launch = one minibatch of n <= MRL_PPO_BLOCK_ROWS rows: block-reduced
+                               kl, c = kl_coeff + 2 cutoff_coeff (kl - cutoff)+, ghead of pensurr
+                               (ppo.py:150-156); partial sums as LOSSES                            */
+#define MRL_PPO_BLOCK_ROWS 128
 
 typedef struct {
   const float* x;          /* [N, n_obs] observations                              */
@@ -76,6 +82,11 @@ typedef struct {
   float* out;              /* EPI_PROB output                                      */
   float* ghead;            /* [N, gh] head-gradient rows (gh = k, 2d or 1)         */
   double* partial;         /* [mrl_partial_rows(n), 4] fp64 per-wave partial sums  */
+  double kl_coeff;         /* PPO epilogues (see MRL_EPI_PPOGRAD / PPOSGD)         */
+  double kl_cutoff;        /* PPOSGD: 2 * kl_target                                */
+  double cutoff_coeff;     /* PPOSGD: kl_cutoff_coeff (1000)                       */
+  int32_t reverse_kl;      /* kl[new, old] instead of kl[old, new] (PpoLbfgs)     */
+  int32_t pad_;
 } mrl_rows_io;
 
 int64_t mrl_partial_rows(int64_t n);  /* rows of `partial` a call over n rows writes */
@@ -168,6 +179,12 @@ int mrl_trpo_step(const float* fvp, const double* x, const float* g, double damp
 /* theta_out = (float)(theta_old + frac * fullstep)   (linesearch, trpo.py:150, core.py:540) */
 int mrl_axpy_cast(const float* theta_old, const double* fullstep, double frac, int64_t n, float* theta_out,
                   void* stream);
+/* Adam in floatX (PpoSgdUpdater's adam_updates, ppo.py:231-258): m, v, theta fp32 [n];
+ * a_t = lr sqrt(1-b2^t)/(1-b1^t) computed by the caller */
+int mrl_adam_step(float* theta, const float* g, float* m, float* v, double a_t, double beta1, double beta2,
+                  double eps, int64_t n, void* stream);
+/* dst row i = src row idx[i] (row_bytes a multiple of 4): PPO minibatch permutation */
+int mrl_gather_rows(const void* src, const int64_t* idx, int64_t n, int64_t row_bytes, void* dst, void* stream);
 /* out (fp64) = scale * (double)in ; in-place-safe */
 int mrl_cast_scale_f32_f64(const float* in, double scale, int64_t n, double* out, void* stream);
 

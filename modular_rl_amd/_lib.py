@@ -13,7 +13,8 @@ LIB_PATH = os.path.join(_HERE, "libmrl_hip.so")
 
 OK = 0
 HEAD_LINEAR, HEAD_SOFTMAX, HEAD_GAUSS = 0, 1, 2
-EPI_PROB, EPI_LOSSES, EPI_SURRGRAD, EPI_VFLOSS, EPI_FVP = 0, 1, 2, 3, 4
+EPI_PROB, EPI_LOSSES, EPI_SURRGRAD, EPI_VFLOSS, EPI_FVP, EPI_PPOGRAD, EPI_PPOSGD = 0, 1, 2, 3, 4, 5, 6
+PPO_BLOCK_ROWS = 128
 ENV_CARTPOLE, ENV_HOPPER, ENV_HUMANOID = 0, 1, 2
 GEMM_STORE, GEMM_TANH, GEMM_DTANH, GEMM_SLAB = 0, 1, 2, 3
 
@@ -34,7 +35,8 @@ class MlpDesc(ctypes.Structure):
 class RowsIO(ctypes.Structure):
     _fields_ = [("x", vp), ("ep_t", vp), ("timestep_limit", f64), ("n", i64), ("inv_n_global", f64),
                 ("act", vp), ("adv", vp), ("oldprob", vp), ("target", vp), ("out", vp), ("ghead", vp),
-                ("partial", vp)]
+                ("partial", vp), ("kl_coeff", f64), ("kl_cutoff", f64), ("cutoff_coeff", f64), ("reverse_kl", i32),
+                ("pad_", i32)]
 
 
 class GemmDesc(ctypes.Structure):
@@ -78,6 +80,8 @@ SIGNATURES = {
     "mrl_trpo_step": (i32, [vp, vp, vp, f64, f64, i64, vp, vp, vp]),
     "mrl_axpy_cast": (i32, [vp, vp, f64, i64, vp, vp]),
     "mrl_cast_scale_f32_f64": (i32, [vp, f64, i64, vp, vp]),
+    "mrl_adam_step": (i32, [vp, vp, vp, vp, f64, f64, f64, f64, i64, vp]),
+    "mrl_gather_rows": (i32, [vp, vp, i64, i64, vp, vp]),
     "mrl_gae": (i32, [vp, vp, vp, i64, i64, f64, f64, vp, vp, vp, vp, vp]),
     "mrl_gae_workspace_bytes": (i64, [i64, i64]),
     "mrl_standardize": (i32, [vp, i64, vp, vp]),

@@ -18,6 +18,7 @@ from .envs import Box, Discrete
 from .filters import DeviceZFilter
 from .misc_utils import IDENTITY, comma_sep_ints, update_default_config
 from .nets import check_hid_sizes, glorot_init, make_net
+from .ppo import PpoLbfgsUpdater, PpoSgdUpdater
 from .trpo import TrpoUpdater
 from .vf import NnVf
 
@@ -85,6 +86,7 @@ class AgentWithPolicy:
 
 class TrpoAgent(AgentWithPolicy):
     options = MLP_OPTIONS + PG_OPTIONS + TrpoUpdater.options + FILTER_OPTIONS
+    updater_cls = TrpoUpdater
 
     def __init__(self, ob_space, ac_space, usercfg, comm=None):
         cfg = update_default_config(self.options, usercfg)
@@ -95,8 +97,9 @@ class TrpoAgent(AgentWithPolicy):
         seed = int((usercfg or {}).get("seed", 0))
         self.seed = seed
         policy, self.baseline = make_mlps(ob_space, ac_space, cfg, comm=self.comm, seed=seed)
-        self.updater = TrpoUpdater(policy, cfg, comm=self.comm)
+        self.updater = self.updater_cls(policy, cfg, comm=self.comm)
         self._collectors = {}
+        self._pending_state = None  # filter / RNG state from load_snapshot, applied to the first collector
         if cfg["filter"]:
             obfilter = DeviceZFilter(self, "obs", clip=5)
             rewfilter = DeviceZFilter(self, "rew", demean=False, clip=10)
@@ -117,6 +120,10 @@ class TrpoAgent(AgentWithPolicy):
             shared = self._filter_owner()
             if shared is not None:  # one running stat per agent
                 col.filter_state = shared.filter_state
+            elif self._pending_state:
+                from .checkpoint import apply_collector_state
+                apply_collector_state(col, self._pending_state)
+                self._pending_state = None
             self._collectors[key] = col
         return self._collectors[key]
 
@@ -127,3 +134,15 @@ class TrpoAgent(AgentWithPolicy):
         for c in self._collectors.values():
             return c
         return None
+
+
+class PpoLbfgsAgent(TrpoAgent):
+    """`agentzoo.py:134-141`: PPO with the L-BFGS penalty updater."""
+    options = MLP_OPTIONS + PG_OPTIONS + PpoLbfgsUpdater.options + FILTER_OPTIONS
+    updater_cls = PpoLbfgsUpdater
+
+
+class PpoSgdAgent(TrpoAgent):
+    """`agentzoo.py:143-150`: PPO with minibatch Adam."""
+    options = MLP_OPTIONS + PG_OPTIONS + PpoSgdUpdater.options + FILTER_OPTIONS
+    updater_cls = PpoSgdUpdater

@@ -1,0 +1,168 @@
+"""Checkpoint / resume and run diagnostics.
+
+The reference snapshots the whole agent as a pickle inside an HDF5 file
+(`run_pg.py:141-142`: ``hdf['/agent_snapshots/%0.4i'] = cPickle.dumps(agent)``) and
+logs per-iteration scalars into ``hdf['diagnostics']`` (`misc_utils.py:111-132`);
+``load_snapshot`` is declared but never read (`misc_utils.py:102`).  Here the agent
+state is a flat set of arrays -- nothing executable is ever stored or loaded:
+
+  policy/theta, vf/theta            fp32 flat parameters (Keras trainable_weights order)
+  filter/state                      ZFilter running stats (n, n_rew, mean[D], M2[D], fp64)
+  rng/iteration, rng/episodes       device Philox step base and per-env episode counters,
+                                    so a resumed run draws exactly the noise the
+                                    uninterrupted run would have drawn
+  meta (JSON)                       cfg, env id, iteration counter
+
+Snapshots are ``.npz`` files (``numpy.load(allow_pickle=False)`` reads them); the run
+log is HDF5 with the reference's layout when ``h5py`` is importable, else an ``.npz``
+with the same keys (``params`` as JSON, ``diagnostics/<stat>`` arrays, ``cmd``).
+"""
+import json
+import os
+import sys
+from collections import defaultdict
+
+import numpy as np
+import torch
+
+SNAPSHOT_VERSION = 1
+
+
+def _jsonable(cfg):
+    out = {}
+    for k, v in (cfg or {}).items():
+        try:
+            json.dumps(v)
+            out[k] = v
+        except TypeError:
+            out[k] = repr(v)
+    return out
+
+
+def agent_state(agent, counter=0, env_id=None):
+    """Arrays (+ JSON meta) that restore ``agent`` to this point of training."""
+    st = {
+        "policy/theta": agent.policy.net.theta.detach().cpu().numpy().copy(),
+        "vf/theta": agent.baseline.net.theta.detach().cpu().numpy().copy(),
+    }
+    col = agent._filter_owner()
+    if col is not None:
+        st["filter/state"] = col.filter_state[:col.FS].detach().cpu().numpy().copy()
+        st["rng/iteration"] = col.iteration.detach().cpu().numpy().copy()
+        st["rng/episodes"] = col.env_int[col.E:].detach().cpu().numpy().copy()
+    meta = dict(version=SNAPSHOT_VERSION, counter=int(counter), env_id=env_id, cfg=_jsonable(agent.cfg))
+    return st, meta
+
+
+def save_snapshot(path, agent, counter=0, env_id=None):
+    st, meta = agent_state(agent, counter, env_id)
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    arrays = {k.replace("/", "__"): v for k, v in st.items()}
+    arrays["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    tmp = path + ".tmp.npz"
+    np.savez(tmp, **arrays)
+    os.replace(tmp, path)
+    return path
+
+
+def load_snapshot(path, agent):
+    """Restore parameters now; filter / RNG state go to the agent's collector (applied
+    immediately if it exists, else when ``make_collector`` creates it)."""
+    with np.load(path, allow_pickle=False) as z:
+        st = {k.replace("__", "/"): z[k] for k in z.files if k != "meta"}
+        meta = json.loads(bytes(z["meta"]).decode())
+    if meta.get("version") != SNAPSHOT_VERSION:
+        raise ValueError(f"{path}: snapshot version {meta.get('version')} != {SNAPSHOT_VERSION}")
+    pol, vf = agent.policy.net, agent.baseline.net
+    if st["policy/theta"].shape != (pol.P,) or st["vf/theta"].shape != (vf.P,):
+        raise ValueError(f"{path}: parameter shapes do not match this agent's nets")
+    pol.set_flat(st["policy/theta"])
+    vf.set_flat(st["vf/theta"])
+    agent._pending_state = {k: v for k, v in st.items() if k.startswith(("filter/", "rng/"))}
+    col = agent._filter_owner()
+    if col is not None:
+        apply_collector_state(col, agent._pending_state)
+        agent._pending_state = None
+    return meta
+
+
+def apply_collector_state(col, st):
+    if not st:
+        return
+    if "filter/state" in st:
+        fs = torch.as_tensor(st["filter/state"], dtype=torch.float64)
+        if fs.numel() != col.FS:
+            raise ValueError("snapshot filter state does not match the env")
+        col.filter_state[:col.FS].copy_(fs.to(col.filter_state.device))
+    if "rng/iteration" in st:
+        col.iteration.copy_(torch.as_tensor(st["rng/iteration"], dtype=torch.int64).to(col.iteration.device))
+    if "rng/episodes" in st:
+        ep = torch.as_tensor(st["rng/episodes"], dtype=torch.int32)
+        if ep.numel() == col.E:
+            col.env_int[col.E:].copy_(ep.to(col.env_int.device))
+
+
+class RunLog:
+    """The reference's ``prepare_h5_file`` (`misc_utils.py:111-132`): params, per-iteration
+    scalar diagnostics, agent snapshots, env id and the command line."""
+
+    def __init__(self, fname, args):
+        self.fname = fname
+        self.params = _jsonable(vars(args) if not isinstance(args, dict) else args)
+        self.diagnostics = defaultdict(list)
+        self.snapshots = {}
+        self.extra = {"cmd": " ".join(sys.argv)}
+        try:
+            import h5py  # noqa: F401
+            self.h5 = True
+        except ImportError:
+            self.h5 = False
+
+    def record(self, stats):
+        for k, v in stats.items():
+            a = np.asarray(v)
+            if a.ndim == 0:
+                self.diagnostics[k].append(float(a))
+            else:
+                self.diagnostics[k].extend(a.ravel().tolist())
+
+    def snapshot(self, counter, agent, env_id=None):
+        st, meta = agent_state(agent, counter, env_id)
+        self.snapshots["%0.4i" % counter] = (st, meta)
+
+    def save(self):
+        d = os.path.dirname(os.path.abspath(self.fname))
+        os.makedirs(d, exist_ok=True)
+        if self.h5:
+            import h5py
+            with h5py.File(self.fname, "w") as f:
+                g = f.create_group("params")
+                for k, v in self.params.items():
+                    try:
+                        g[k] = v
+                    except (TypeError, ValueError):
+                        g[k] = json.dumps(v)
+                dg = f.create_group("diagnostics")
+                for k, v in self.diagnostics.items():
+                    dg[k] = np.asarray(v)
+                for name, (st, meta) in self.snapshots.items():
+                    sg = f.create_group("agent_snapshots/" + name)
+                    for k, v in st.items():
+                        sg[k] = v
+                    sg.attrs["meta"] = json.dumps(meta)
+                for k, v in self.extra.items():
+                    f[k] = v
+            return self.fname
+        arrays = {"params": np.frombuffer(json.dumps(self.params).encode(), dtype=np.uint8)}
+        for k, v in self.diagnostics.items():
+            arrays["diagnostics__" + k] = np.asarray(v, dtype=np.float64)
+        for name, (st, meta) in self.snapshots.items():
+            for k, v in st.items():
+                arrays[f"agent_snapshots__{name}__{k.replace('/', '__')}"] = v
+            arrays[f"agent_snapshots__{name}__meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+        for k, v in self.extra.items():
+            arrays[k] = np.frombuffer(str(v).encode(), dtype=np.uint8)
+        out = self.fname if self.fname.endswith(".npz") else os.path.splitext(self.fname)[0] + ".npz"
+        np.savez(out, **arrays)
+        return out

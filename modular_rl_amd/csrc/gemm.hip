@@ -296,14 +296,36 @@ __global__ __launch_bounds__(256) void head_rows_kernel(RowsArgs a, const float*
     dls[j] = (a.dlogstd != nullptr && j < A) ? a.dlogstd[j] : 0.f;
   }
   double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
-  for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < a.n; row += (int64_t)gridDim.x * 256) {
+  if constexpr (EPI == MRL_EPI_PPOSGD) {
+    // one minibatch (n <= 256) in one block: block-reduced kl sets the penalty slope
+    __shared__ double red[4];
+    const int64_t row = threadIdx.x;
+    const bool valid = row < a.n;
     float z[MA], dz[MA];
 #pragma unroll
     for (int j = 0; j < MA; ++j) {
-      z[j] = j < A ? zr[row * A + j] : 0.f;
-      dz[j] = (EPI == MRL_EPI_FVP && j < A) ? dzr[row * A + j] : 0.f;
+      z[j] = (valid && j < A) ? zr[row * A + j] : 0.f;
+      dz[j] = 0.f;
     }
-    row_epilogue<EPI, MA>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+    if (valid) row_epilogue<MRL_EPI_LOSSES, MA>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+    const double klw = wave_sum(acc1);
+    if (lane == 0) red[wave] = klw;
+    __syncthreads();
+    const double kl = ((red[0] + red[1]) + (red[2] + red[3])) * a.inv_ng;
+    RowsArgs b = a;
+    b.kl_coeff = a.kl_coeff + (kl > a.kl_cutoff ? (float)(2.0 * a.cutoff_coeff * (kl - a.kl_cutoff)) : 0.f);
+    double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+    if (valid) row_epilogue<MRL_EPI_PPOGRAD, MA>(b, row, z, dz, ls, sd, dls, d0, d1, d2);
+  } else {
+    for (int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x; row < a.n; row += (int64_t)gridDim.x * 256) {
+      float z[MA], dz[MA];
+#pragma unroll
+      for (int j = 0; j < MA; ++j) {
+        z[j] = j < A ? zr[row * A + j] : 0.f;
+        dz[j] = (EPI == MRL_EPI_FVP && j < A) ? dzr[row * A + j] : 0.f;
+      }
+      row_epilogue<EPI, MA>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+    }
   }
   if (a.partial != nullptr) {
     acc0 = wave_sum(acc0);
@@ -327,6 +349,8 @@ static void launch_head(int epi, dim3 grid, hipStream_t s, const RowsArgs& a, co
     case MRL_EPI_LOSSES: hipLaunchKernelGGL((head_rows_kernel<MRL_EPI_LOSSES, MA>), grid, dim3(256), 0, s, a, z, dz, skip); break;
     case MRL_EPI_SURRGRAD: hipLaunchKernelGGL((head_rows_kernel<MRL_EPI_SURRGRAD, MA>), grid, dim3(256), 0, s, a, z, dz, skip); break;
     case MRL_EPI_VFLOSS: hipLaunchKernelGGL((head_rows_kernel<MRL_EPI_VFLOSS, MA>), grid, dim3(256), 0, s, a, z, dz, skip); break;
+    case MRL_EPI_PPOGRAD: hipLaunchKernelGGL((head_rows_kernel<MRL_EPI_PPOGRAD, MA>), grid, dim3(256), 0, s, a, z, dz, skip); break;
+    case MRL_EPI_PPOSGD: hipLaunchKernelGGL((head_rows_kernel<MRL_EPI_PPOSGD, MA>), dim3(1), dim3(256), 0, s, a, z, dz, skip); break;
     default: hipLaunchKernelGGL((head_rows_kernel<MRL_EPI_FVP, MA>), grid, dim3(256), 0, s, a, z, dz, skip); break;
   }
 }
@@ -417,9 +441,12 @@ int mrl_head_rows(int32_t head, int32_t n_out, int32_t epi, const float* z, cons
       break;
     case MRL_EPI_LOSSES:
     case MRL_EPI_SURRGRAD:
+    case MRL_EPI_PPOGRAD:
+    case MRL_EPI_PPOSGD:
       if (head == MRL_HEAD_LINEAR) return fail(E_ARG, "policy epilogue on a value net");
       if (!io->act || !io->adv || !io->oldprob || !io->partial) return fail(E_ARG, "losses need act/adv/oldprob/partial");
-      if (epi == MRL_EPI_SURRGRAD && !io->ghead) return fail(E_ARG, "SURRGRAD needs ghead");
+      if (epi != MRL_EPI_LOSSES && !io->ghead) return fail(E_ARG, "gradient epilogues need ghead");
+      if (epi == MRL_EPI_PPOSGD && io->n > MRL_PPO_BLOCK_ROWS) return fail(E_ARG, "PPOSGD minibatch exceeds one block");
       break;
     case MRL_EPI_VFLOSS:
       if (head != MRL_HEAD_LINEAR || !io->target || !io->ghead || !io->partial)
@@ -448,6 +475,10 @@ int mrl_head_rows(int32_t head, int32_t n_out, int32_t epi, const float* z, cons
   a.partial = io->partial;
   a.logstd = head == MRL_HEAD_GAUSS ? logstd : nullptr;
   a.dlogstd = head == MRL_HEAD_GAUSS ? dlogstd : nullptr;
+  a.kl_coeff = (float)io->kl_coeff;
+  a.kl_cutoff = (float)io->kl_cutoff;
+  a.cutoff_coeff = (float)io->cutoff_coeff;
+  a.reverse_kl = io->reverse_kl;
   const dim3 grid((unsigned)(mrl_partial_rows(io->n) / 4));
   if (n_out <= 8) launch_head<8>(epi, grid, (hipStream_t)stream, a, z, dz, skip);
   else launch_head<MRL_LAYERED_MAX_OUT>(epi, grid, (hipStream_t)stream, a, z, dz, skip);

@@ -77,9 +77,24 @@ __global__ __launch_bounds__(ROWS_BLOCK, 2) void mlp_rows_kernel(RowsArgs a, con
     float z[MAX_OUT], dz[MAX_OUT];
     if (EPI == MRL_EPI_FVP) forward_jvp_head_lowreg(lds, ldt, d, xl, lane, z, dz);
     else forward_head_lowreg(lds, d, xl, lane, z);
-    if (!valid || h != 0) continue;
-
-    row_epilogue<EPI, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+    if constexpr (EPI == MRL_EPI_PPOSGD) {
+      // one 128-row minibatch per launch (ppo.py:150-156): block-reduced minibatch KL
+      // sets the penalty slope, then the pensurr head gradient of every row
+      __shared__ double red[4];
+      if (valid && h == 0) row_epilogue<MRL_EPI_LOSSES, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+      const double klw = wave_sum(acc1);
+      if (lane == 0) red[wave] = klw;
+      __syncthreads();
+      const double kl = ((red[0] + red[1]) + (red[2] + red[3])) * a.inv_ng;
+      RowsArgs b = a;
+      b.kl_coeff = a.kl_coeff + (kl > a.kl_cutoff ? (float)(2.0 * a.cutoff_coeff * (kl - a.kl_cutoff)) : 0.f);
+      double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+      if (valid && h == 0) row_epilogue<MRL_EPI_PPOGRAD, MAX_OUT>(b, row, z, dz, ls, sd, dls, d0, d1, d2);
+      continue;
+    } else {
+      if (!valid || h != 0) continue;
+      row_epilogue<EPI, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+    }
   }
   if (a.partial != nullptr) {
     acc0 = wave_sum(acc0);
@@ -463,6 +478,10 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
   a.partial = io->partial;
   a.logstd = (d->head == MRL_HEAD_GAUSS && theta) ? theta + a.d.tls : nullptr;
   a.dlogstd = (d->head == MRL_HEAD_GAUSS && tangent) ? tangent + a.d.tls : nullptr;
+  a.kl_coeff = (float)io->kl_coeff;
+  a.kl_cutoff = (float)io->kl_cutoff;
+  a.cutoff_coeff = (float)io->cutoff_coeff;
+  a.reverse_kl = io->reverse_kl;
   switch (epi) {
     case MRL_EPI_PROB:
       if (!io->out) return fail(E_ARG, "EPI_PROB needs out");
@@ -470,10 +489,13 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
       break;
     case MRL_EPI_LOSSES:
     case MRL_EPI_SURRGRAD:
+    case MRL_EPI_PPOGRAD:
+    case MRL_EPI_PPOSGD:
       if (d->head == MRL_HEAD_LINEAR) return fail(E_ARG, "policy epilogue on a value net");
       if (!io->act || !io->adv || !io->oldprob || !io->partial) return fail(E_ARG, "losses need act/adv/oldprob/partial");
-      if (epi == MRL_EPI_SURRGRAD && !io->ghead) return fail(E_ARG, "SURRGRAD needs ghead");
+      if (epi != MRL_EPI_LOSSES && !io->ghead) return fail(E_ARG, "gradient epilogues need ghead");
       if (d->head == MRL_HEAD_GAUSS && !theta) return fail(E_ARG, "DiagGauss needs theta (logstd)");
+      if (epi == MRL_EPI_PPOSGD && io->n > MRL_PPO_BLOCK_ROWS) return fail(E_ARG, "PPOSGD minibatch exceeds one block");
       break;
     case MRL_EPI_VFLOSS:
       if (d->head != MRL_HEAD_LINEAR || !io->target || !io->ghead || !io->partial)
@@ -505,6 +527,13 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
       break;
     case MRL_EPI_FVP:
       hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_FVP>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t, skip);
+      break;
+    case MRL_EPI_PPOGRAD:
+      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_PPOGRAD>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t,
+                         skip);
+      break;
+    case MRL_EPI_PPOSGD:
+      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_PPOSGD>, dim3(1), dim3(ROWS_BLOCK), shm, s, a, image, image_t, skip);
       break;
   }
   return hip_check(hipGetLastError(), "mrl_mlp_rows");

@@ -25,6 +25,10 @@ struct RowsArgs {
   double* partial;
   const float* logstd;   // theta + tls (DiagGauss) or nullptr
   const float* dlogstd;  // tangent + tls (EPI_FVP, DiagGauss) or nullptr
+  // PPO (ppo.py:3-229): pensurr = surr + c_kl * kl + cutoff_coeff * (kl > cutoff) (kl - cutoff)^2
+  float kl_coeff;        // EPI_PPOGRAD: the full d pensurr / d kl (host-computed); EPI_PPOSGD: kl_coeff
+  float kl_cutoff, cutoff_coeff;
+  int reverse_kl;        // kl[new, old] instead of kl[old, new]
 };
 
 constexpr float LOG2PI_F = 1.8378770664093453f;
@@ -50,8 +54,11 @@ __device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, con
         a.out[row * 2 * A + A + j] = sd[j];
       }
     }
-  } else if (EPI == MRL_EPI_LOSSES || EPI == MRL_EPI_SURRGRAD) {
+  } else if (EPI == MRL_EPI_LOSSES || EPI == MRL_EPI_SURRGRAD || EPI == MRL_EPI_PPOGRAD) {
+    // surrogate term ratio*adv, KL and entropy of the row; SURRGRAD / PPOGRAD also write
+    // the head gradient of surr (+ kl_coeff * kl for PPO)
     const float advr = a.adv[row];
+    const float c = a.kl_coeff * (float)a.inv_ng;
     if (a.head == MRL_HEAD_SOFTMAX) {
       // Categorical: loglik core.py:349-353, kl 355-356, entropy 358-359
       float m = z[0];
@@ -64,16 +71,21 @@ __device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, con
       float pa = 0.f, opa = 0.f, kl = 0.f, ent = 0.f;
       for (int j = 0; j < A; ++j) {
         if (j == act) { pa = p[j]; opa = op[j]; }
-        kl += op[j] * logf(op[j] / p[j]);
+        kl += a.reverse_kl ? p[j] * logf(p[j] / op[j]) : op[j] * logf(op[j] / p[j]);
         ent -= p[j] * logf(p[j]);
       }
       const float ratio = expf(logf(pa) - logf(opa));
       acc0 += (double)(ratio * advr);
       acc1 += (double)kl;
       acc2 += (double)ent;
-      if (EPI == MRL_EPI_SURRGRAD) {
+      if (EPI == MRL_EPI_SURRGRAD || EPI == MRL_EPI_PPOGRAD) {
         const float w = (float)(-a.inv_ng) * ratio * advr;
-        for (int j = 0; j < A; ++j) a.ghead[row * a.gh + j] = w * ((j == act ? 1.f : 0.f) - p[j]);
+        for (int j = 0; j < A; ++j) {
+          float gj = w * ((j == act ? 1.f : 0.f) - p[j]);
+          if (EPI == MRL_EPI_PPOGRAD)
+            gj += c * (a.reverse_kl ? p[j] * (logf(p[j] / op[j]) - kl) : p[j] - op[j]);
+          a.ghead[row * a.gh + j] = gj;
+        }
       }
     } else {
       // DiagGauss: loglik core.py:412-416, kl 421-426, entropy 428-430
@@ -89,7 +101,8 @@ __device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, con
         sls += ls[j];
         sls0 += logf(s0);
         const float dm = m0 - z[j];
-        kl += logf(sd[j] / s0) + (s0 * s0 + dm * dm) / (2.f * sd[j] * sd[j]);
+        kl += a.reverse_kl ? logf(s0 / sd[j]) + (sd[j] * sd[j] + dm * dm) / (2.f * s0 * s0)
+                           : logf(sd[j] / s0) + (s0 * s0 + dm * dm) / (2.f * sd[j] * sd[j]);
       }
       kl -= 0.5f * A;
       const float logp = -0.5f * q - 0.5f * LOG2PI_F * A - sls;
@@ -98,11 +111,23 @@ __device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, con
       acc0 += (double)(ratio * advr);
       acc1 += (double)kl;
       acc2 += (double)(sls + 0.5f * LOG2PIE_F * A);
-      if (EPI == MRL_EPI_SURRGRAD) {
+      if (EPI == MRL_EPI_SURRGRAD || EPI == MRL_EPI_PPOGRAD) {
         const float w = (float)(-a.inv_ng) * ratio * advr;
         for (int j = 0; j < A; ++j) {
-          a.ghead[row * a.gh + j] = w * u[j] / sd[j];
-          a.ghead[row * a.gh + A + j] = w * (u[j] * u[j] - 1.f);
+          float gm = w * u[j] / sd[j];
+          float gs = w * (u[j] * u[j] - 1.f);
+          if (EPI == MRL_EPI_PPOGRAD) {
+            const float m0 = op[j], s0 = op[A + j], dm = z[j] - m0;
+            if (a.reverse_kl) {
+              gm += c * dm / (s0 * s0);
+              gs += c * (sd[j] * sd[j] / (s0 * s0) - 1.f);
+            } else {
+              gm += c * dm / (sd[j] * sd[j]);
+              gs += c * (1.f - (s0 * s0 + dm * dm) / (sd[j] * sd[j]));
+            }
+          }
+          a.ghead[row * a.gh + j] = gm;
+          a.ghead[row * a.gh + A + j] = gs;
         }
       }
     }

@@ -244,6 +244,30 @@ __global__ void axpy_cast_kernel(const float* __restrict__ a, const double* __re
     o[i] = (float)((double)a[i] + frac * b[i]);
 }
 
+// Adam step in floatX (ppo.py:231-258): m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
+// theta -= a_t m / (sqrt(v) + eps), a_t = lr sqrt(1-b2^t)/(1-b1^t) from the host
+__global__ void adam_kernel(float* __restrict__ th, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, float a_t, float b1, float b2, float eps, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * (gi * gi);
+    m[i] = mi;
+    v[i] = vi;
+    th[i] = th[i] - a_t * mi / (sqrtf(vi) + eps);
+  }
+}
+
+// dst row i = src row idx[i] (rows of `words` 32-bit words): minibatch gathers
+__global__ void gather_rows_kernel(const uint32_t* __restrict__ src, const int64_t* __restrict__ idx, int64_t n,
+                                   int64_t words, uint32_t* __restrict__ dst) {
+  const int64_t total = n * words;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / words, c = i - r * words;
+    dst[i] = src[idx[r] * words + c];
+  }
+}
+
 __global__ void cast_scale_kernel(const float* __restrict__ a, double s, int64_t n, double* __restrict__ o) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     o[i] = s * (double)a[i];
@@ -411,6 +435,23 @@ int mrl_axpy_cast(const float* theta_old, const double* fullstep, double frac, i
   hipLaunchKernelGGL(axpy_cast_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, theta_old, fullstep, frac,
                      n, theta_out);
   return hip_check(hipGetLastError(), "mrl_axpy_cast");
+}
+
+int mrl_adam_step(float* theta, const float* g, float* m, float* v, double a_t, double beta1, double beta2,
+                  double eps, int64_t n, void* stream) {
+  if (!theta || !g || !m || !v) return fail(E_ARG, "null pointer");
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, theta, g, m, v, (float)a_t,
+                     (float)beta1, (float)beta2, (float)eps, n);
+  return hip_check(hipGetLastError(), "mrl_adam_step");
+}
+
+int mrl_gather_rows(const void* src, const int64_t* idx, int64_t n, int64_t row_bytes, void* dst, void* stream) {
+  if (!src || !idx || !dst) return fail(E_ARG, "null pointer");
+  if (row_bytes <= 0 || row_bytes % 4 != 0) return fail(E_ARG, "row_bytes must be a positive multiple of 4");
+  if (n <= 0) return OK;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(n * (row_bytes / 4))), dim3(256), 0, (hipStream_t)stream,
+                     (const uint32_t*)src, idx, n, row_bytes / 4, (uint32_t*)dst);
+  return hip_check(hipGetLastError(), "mrl_gather_rows");
 }
 
 int64_t mrl_moments_workspace_bytes(int64_t n) { return grid_for(n, 256, 1024) * 2 * (int64_t)sizeof(double); }

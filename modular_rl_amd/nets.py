@@ -122,9 +122,10 @@ class MlpNet:
     # ---- fused passes
     def rows(self, epi, x, n, ep_t=None, timestep_limit=1.0, inv_n_global=1.0, act=None, adv=None, oldprob=None,
              target=None, out=None, ghead=None, partial=None, theta=None, image=None, tangent=None, image_t=None,
-             skip=None):
+             skip=None, kl_coeff=0.0, kl_cutoff=0.0, cutoff_coeff=0.0, reverse_kl=0):
         io = _lib.RowsIO(ptr(x), ptr(ep_t), float(timestep_limit), int(n), float(inv_n_global), ptr(act), ptr(adv),
-                         ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial))
+                         ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial), float(kl_coeff),
+                         float(kl_cutoff), float(cutoff_coeff), int(reverse_kl))
         theta = self.theta if theta is None else theta
         image = self.image if image is None else image
         call("mrl_mlp_rows", ctypes.byref(self.desc), int(epi), ptr(theta), ptr(image), ptr(tangent), ptr(image_t),
@@ -269,11 +270,12 @@ class LayeredMlpNet:
 
     def rows(self, epi, x, n, ep_t=None, timestep_limit=1.0, inv_n_global=1.0, act=None, adv=None, oldprob=None,
              target=None, out=None, ghead=None, partial=None, theta=None, image=None, tangent=None, image_t=None,
-             skip=None):
+             skip=None, kl_coeff=0.0, kl_cutoff=0.0, cutoff_coeff=0.0, reverse_kl=0):
         n = int(n)
         theta = self.theta if theta is None else theta
         io = _lib.RowsIO(ptr(x), ptr(ep_t), float(timestep_limit), n, float(inv_n_global), ptr(act), ptr(adv),
-                         ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial))
+                         ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial), float(kl_coeff),
+                         float(kl_cutoff), float(cutoff_coeff), int(reverse_kl))
         dz = None
         if epi == _lib.EPI_FVP:
             if tangent is None:
@@ -284,7 +286,7 @@ class LayeredMlpNet:
             _, X, ldx, H, Z, _ = tape
             dz = self.ws.get("tape_dz", n * self.n_out, torch.float32)
             self._jvp(X, ldx, n, theta, tangent, H, dz, skip)
-        elif epi in (_lib.EPI_SURRGRAD, _lib.EPI_VFLOSS):
+        elif epi in (_lib.EPI_SURRGRAD, _lib.EPI_VFLOSS, _lib.EPI_PPOGRAD, _lib.EPI_PPOSGD):
             _, X, ldx, H, Z, _ = self._record(x, n, ep_t, timestep_limit, theta)
         else:
             if n == 0:

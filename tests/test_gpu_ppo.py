@@ -1,0 +1,127 @@
+"""PPO updaters (`ppo.py:3-229`): the device PPOGRAD / PPOSGD epilogues
+against the torch-autograd oracle (oracle/ppo_np.py) at fixed theta, then whole
+PpoLbfgs / PpoSgd updates against the oracle updaters, on both the fused and the
+layered MLP paths."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ppo_np as PO
+from oracle import trpo_np as T
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).cuda()
+
+
+def _case(head, nin, nout, hid, N, seed, layered):
+    from modular_rl_amd import _lib
+    from modular_rl_amd.core import Categorical, DiagGauss, StochPolicyMLP
+    from modular_rl_amd.nets import make_net
+    rng = np.random.default_rng(seed)
+    spec = T.Spec(nin, hid, nout, head)
+    th = T.mlp_init(rng, spec.shapes, head == "gauss") + 0.05 * rng.standard_normal(spec.P)
+    if head == "gauss":
+        th[-nout:] = -0.3 + 0.1 * rng.standard_normal(nout)
+    th = th.astype(np.float32).astype(np.float64)
+    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
+    oldth = th + 0.02 * rng.standard_normal(spec.P)
+    oldprob = T.policy_prob(spec, oldth, ob).astype(np.float32).astype(np.float64)
+    noise = rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N)
+    act = T.sample(spec, oldprob, noise)
+    if head == "gauss":
+        act = act.astype(np.float32).astype(np.float64)
+    adv = T.standardize(rng.standard_normal(N)).astype(np.float32).astype(np.float64)
+    net = make_net(nin, nout, _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX, hid,
+                   impl="layered" if layered else "auto")
+    net.set_flat(th)
+    pol = StochPolicyMLP(net, DiagGauss(nout) if head == "gauss" else Categorical(nout))
+    return spec, th, ob, act, adv, oldprob, pol
+
+
+def _batch(ob, act, adv, prob, head):
+    from modular_rl_amd.collector import Batch
+    b = Batch(ob.shape[0], _dev(ob), _dev(act, torch.int32 if head == "softmax" else torch.float32), _dev(prob))
+    b.adv = _dev(adv)
+    return b
+
+
+@pytest.mark.parametrize("layered", [False, True])
+@pytest.mark.parametrize("head,nin,nout", [("gauss", 11, 3), ("softmax", 4, 2)])
+@pytest.mark.parametrize("reverse", [0, 1])
+@pytest.mark.parametrize("kl_coeff", [1.0, 37.5])
+def test_ppograd_matches_autograd(layered, head, nin, nout, reverse, kl_coeff):
+    from modular_rl_amd import _lib
+    N = 1500
+    spec, th, ob, act, adv, oldprob, pol = _case(head, nin, nout, [64, 64], N, 3, layered)
+    net = pol.net
+    x, a = _dev(ob), _dev(act, torch.int32 if head == "softmax" else torch.float32)
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    ghead = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+    net.rows(_lib.EPI_PPOGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(adv), oldprob=_dev(oldprob), ghead=ghead,
+             partial=partial, kl_coeff=kl_coeff, reverse_kl=reverse)
+    g = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(x, N, ghead, g)
+    sums = torch.zeros(4, dtype=torch.float64, device="cuda")
+    net.reduce_partial(partial, N, sums)
+    s = sums.cpu().numpy()
+    want_l = PO.losses(spec, th, ob, act, adv, oldprob, bool(reverse))
+    np.testing.assert_allclose([-s[0] / N, s[1] / N, s[2] / N], want_l, rtol=1e-4, atol=1e-7)
+    # the kernel's kl_coeff is the whole slope d pensurr / d kl: a cutoff out of reach isolates it
+    _, gw = PO.pensurr_and_grad(spec, th, ob, act, adv, oldprob, kl_coeff, 1e9, reverse_kl=bool(reverse))
+    gd = g.cpu().numpy()
+    assert np.abs(gd - gw).max() <= 1e-4 * np.abs(gw).max()
+
+
+@pytest.mark.parametrize("layered", [False, True])
+def test_ppo_lbfgs_update_matches_oracle(layered):
+    from modular_rl_amd.ppo import PpoLbfgsUpdater
+    N = 3000
+    spec, th, ob, act, adv, oldprob, pol = _case("gauss", 11, 3, [64, 64], N, 5, layered)
+    up = PpoLbfgsUpdater(pol, dict(kl_target=0.01, maxiter=4))
+    info = up.update(_batch(ob, act, adv, oldprob, "gauss"))
+    th_w, info_w, kc_w = PO.lbfgs_update(spec, th, ob, act, adv, oldprob, 1.0, kl_target=0.01, maxiter=4)
+    th1 = pol.get_flat().astype(np.float64)
+    step = np.abs(th_w - th).max()
+    assert np.abs(th1 - th_w).max() <= 2e-3 * step, (np.abs(th1 - th_w).max(), step)
+    for k in ("surr_before", "kl_before", "ent_before"):
+        np.testing.assert_allclose(info[k], info_w[k], rtol=1e-4, atol=1e-7, err_msg=k)
+    for k in ("surr_after", "kl_after", "ent_after"):
+        np.testing.assert_allclose(info[k], info_w[k], rtol=2e-3, atol=1e-6, err_msg=k)
+    assert up.kl_coeff == kc_w
+
+
+@pytest.mark.parametrize("layered", [False, True])
+@pytest.mark.parametrize("head,nin,nout", [("gauss", 11, 3), ("softmax", 4, 3)])
+def test_ppo_sgd_update_matches_oracle(layered, head, nin, nout):
+    from modular_rl_amd.ppo import PpoSgdUpdater
+    N = 600  # 4 full minibatches + one of 88 rows
+    spec, th, ob, act, adv, oldprob, pol = _case(head, nin, nout, [64, 64], N, 7, layered)
+    up = PpoSgdUpdater(pol, dict(kl_target=0.01, epochs=2, stepsize=1e-3))
+    np.random.seed(123)
+    info = up.update(_batch(ob, act, adv, oldprob, head))
+    np.random.seed(123)
+    perms = [np.random.permutation(N) for _ in range(2)]
+    th_w, info_w, kc_w, _ = PO.sgd_update(spec, th, ob, act, adv, perms, 1.0, kl_target=0.01, stepsize=1e-3)
+    th1 = pol.get_flat().astype(np.float64)
+    step = np.abs(th_w - th).max()
+    assert np.abs(th1 - th_w).max() <= 1e-2 * step, (np.abs(th1 - th_w).max(), step)
+    for k in ("surr_before", "kl_before", "ent_before", "surr_after", "kl_after", "ent_after"):
+        np.testing.assert_allclose(info[k], info_w[k], rtol=2e-3, atol=2e-6, err_msg=k)
+    assert up.kl_coeff == kc_w
+
+
+@pytest.mark.parametrize("agent", ["PpoLbfgsAgent", "PpoSgdAgent"])
+def test_ppo_agents_run_iterations(agent):
+    from modular_rl_amd import agentzoo
+    from modular_rl_amd.core import run_policy_gradient_algorithm
+    from modular_rl_amd.envs import make
+    env = make("CartPole-v0")
+    cfg = dict(n_envs=16, horizon=64, timestep_limit=200, n_iter=2, gamma=0.99, lam=0.97, maxiter=5, epochs=2,
+               timesteps_per_batch=16 * 64, use_graph=1)
+    ag = getattr(agentzoo, agent)(env.observation_space, env.action_space, cfg)
+    seen = []
+    run_policy_gradient_algorithm(env, ag, callback=lambda st: seen.append(dict(st)), usercfg=cfg)
+    assert len(seen) == 2 and all(np.isfinite(st["pol_kl_after"]) for st in seen)
