@@ -34,15 +34,16 @@ PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec
 
 def flops_per_row(net):
     """Algorithmic FLOP per row of the two timed halves of the Fisher product.
-    Fused 64-wide net: fvp_jvp_rows = forward recompute + JVP, fvp_vjp = backward.
-    Layered net: the forward is the recorded tape, so fvp_jvp_rows = JVP only
-    (layer 0 one product, deeper layers two); fvp_vjp = weight grads of every layer +
-    input grads of layers >= 1."""
+    The primal forward of the update's theta is cached (fused net: h1/h2 activation
+    cache; layered net: the recorded tape), so fvp_jvp_rows = JVP only (layer 0 one
+    product, deeper layers two) and fvp_vjp = weight grads of every layer + input grads
+    of layers >= 1.  Without the cache the fused JVP kernel also recomputes the forward."""
     dims = [net.n_in] + list(net.hid_sizes) + [net.n_out]
     mm = [dims[i] * dims[i + 1] for i in range(len(dims) - 1)]
     jvp = 2 * (mm[0] + 2 * sum(mm[1:]))
     vjp = 2 * (sum(mm) + sum(mm[1:]))
-    if getattr(net, "layered", False):
+    if getattr(net, "layered", False) or getattr(net, "use_cache", False):
+        # the primal forward comes from the activation cache / recorded tape
         return {"fvp_jvp_rows": jvp, "fvp_vjp": vjp}
     return {"fvp_jvp_rows": 2 * sum(mm) + jvp, "fvp_vjp": vjp}
 

@@ -86,8 +86,20 @@ typedef struct {
   double kl_cutoff;        /* PPOSGD: 2 * kl_target                                */
   double cutoff_coeff;     /* PPOSGD: kl_cutoff_coeff (1000)                       */
   int32_t reverse_kl;      /* kl[new, old] instead of kl[old, new] (PpoLbfgs)     */
-  int32_t pad_;
+  int32_t cache_mode;      /* MRL_CACHE_* (fused path; act_cache NULL = no cache) */
+  float* act_cache;        /* [mrl_act_cache_floats(n)] primal h1/h2 of theta     */
 } mrl_rows_io;
+
+/* Primal activation cache of the fused path: the forward of one theta is shared by
+ * every Fisher product of an update (trpo.py:70 is called 10-11 times at a fixed
+ * theta) and by the VJP that follows a loss pass.  A plain-forward epilogue (PROB,
+ * LOSSES, SURRGRAD, VFLOSS, PPOGRAD) with MRL_CACHE_WRITE stores h1/h2; EPI_FVP with
+ * MRL_CACHE_READ and mrl_mlp_vjp with a non-NULL cache read them instead of
+ * recomputing the forward (bitwise the same activations). */
+#define MRL_CACHE_NONE 0
+#define MRL_CACHE_WRITE 1
+#define MRL_CACHE_READ 2
+int64_t mrl_act_cache_floats(int64_t n);
 
 int64_t mrl_partial_rows(int64_t n);  /* rows of `partial` a call over n rows writes */
 int64_t mrl_slab_rows(int64_t n);     /* rows of the mrl_mlp_vjp slab                */
@@ -101,10 +113,12 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epilogue, const float* theta, co
 
 /* vector-Jacobian product: slab[w, :] <- per-wave partial of sum_n J_n^T ghead_n in
  * flat theta layout (head columns beyond n_out -- DiagGauss logstd -- are summed
- * into the logstd slots).  Replaces flatgrad / the VJP half of the Theano Fvp. */
+ * into the logstd slots).  Replaces flatgrad / the VJP half of the Theano Fvp.
+ * act_cache: the primal activations of the same theta and rows (MRL_CACHE_WRITE of a
+ * preceding pass), or NULL to recompute the forward. */
 int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const int32_t* ep_t,
-                double timestep_limit, const float* ghead, int64_t n, float* slab, const int32_t* skip,
-                void* stream);
+                double timestep_limit, const float* ghead, int64_t n, float* slab, const float* act_cache,
+                const int32_t* skip, void* stream);
 
 /* out[c] = sum_r slab[r, c] in fixed order with fp64 accumulation */
 int mrl_reduce_rows_f32(const float* slab, int64_t rows, int64_t cols, float* out, const int32_t* skip, void* stream);

@@ -13,6 +13,7 @@ LIB_PATH = os.path.join(_HERE, "libmrl_hip.so")
 
 OK = 0
 HEAD_LINEAR, HEAD_SOFTMAX, HEAD_GAUSS = 0, 1, 2
+CACHE_NONE, CACHE_WRITE, CACHE_READ = 0, 1, 2
 EPI_PROB, EPI_LOSSES, EPI_SURRGRAD, EPI_VFLOSS, EPI_FVP, EPI_PPOGRAD, EPI_PPOSGD = 0, 1, 2, 3, 4, 5, 6
 PPO_BLOCK_ROWS = 128
 ENV_CARTPOLE, ENV_HOPPER, ENV_HUMANOID = 0, 1, 2
@@ -36,7 +37,7 @@ class RowsIO(ctypes.Structure):
     _fields_ = [("x", vp), ("ep_t", vp), ("timestep_limit", f64), ("n", i64), ("inv_n_global", f64),
                 ("act", vp), ("adv", vp), ("oldprob", vp), ("target", vp), ("out", vp), ("ghead", vp),
                 ("partial", vp), ("kl_coeff", f64), ("kl_cutoff", f64), ("cutoff_coeff", f64), ("reverse_kl", i32),
-                ("pad_", i32)]
+                ("cache_mode", i32), ("act_cache", vp)]
 
 
 class GemmDesc(ctypes.Structure):
@@ -65,9 +66,10 @@ SIGNATURES = {
     "mrl_mlp_image_floats": (i64, [vp]),
     "mrl_mlp_pack": (i32, [vp, vp, vp, i32, vp, vp]),
     "mrl_partial_rows": (i64, [i64]),
+    "mrl_act_cache_floats": (i64, [i64]),
     "mrl_slab_rows": (i64, [i64]),
     "mrl_mlp_rows": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, vp]),
-    "mrl_mlp_vjp": (i32, [vp, vp, vp, vp, f64, vp, i64, vp, vp, vp]),
+    "mrl_mlp_vjp": (i32, [vp, vp, vp, vp, f64, vp, i64, vp, vp, vp, vp]),
     "mrl_reduce_rows_f32": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_reduce_rows_f64": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_gemm": (i32, [vp, vp, vp]),

@@ -165,9 +165,34 @@ __device__ inline void chain1(const float* lds, int seg, int mo, const f32x16* s
   }
 }
 
-// forward to the head outputs only, layer 2 one M-tile at a time (h2 never fully live)
+// ---- primal activation cache: the forward of one theta is shared by the 11 Fisher
+// products of an update (and by the VJP that follows a loss pass).  Per 32-row tile
+// and lane: h1[2][16], h2[2][16] in register order, as 16 float4 groups interleaved
+// over the 64 lanes (group q of tile t at ((t*16 + q)*64 + lane)*4): every wave load
+// or store instruction moves 1 KB contiguous.
+constexpr int CACHE_TILE_FLOATS = 64 * 64;
+__device__ inline void cache_store(float* tile, int lane, int slot, const f32x16& v) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    reinterpret_cast<float4*>(tile)[(slot * 4 + q) * 64 + lane] =
+        make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+__device__ inline void cache_load(const float* tile, int lane, int slot, f32x16& v) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 x = reinterpret_cast<const float4*>(tile)[(slot * 4 + q) * 64 + lane];
+    v[4 * q] = x.x;
+    v[4 * q + 1] = x.y;
+    v[4 * q + 2] = x.z;
+    v[4 * q + 3] = x.w;
+  }
+}
+
+// forward to the head outputs only, layer 2 one M-tile at a time (h2 never fully live);
+// cache != nullptr: also store h1 / h2 of the tile (slots 0,1 / 2,3)
 template <class XL>
-__device__ inline void forward_head_lowreg(const float* lds, const MlpDims& d, const XL& xl, int lane, float* z) {
+__device__ inline void forward_head_lowreg(const float* lds, const MlpDims& d, const XL& xl, int lane, float* z,
+                                           float* cache = nullptr) {
   const int h = lane >> 5;
   f32x16 h1[2];
   h1[0] = load_bias16(lds, d.fb0, 0, h);
@@ -175,6 +200,10 @@ __device__ inline void forward_head_lowreg(const float* lds, const MlpDims& d, c
   layer0(lds, d, xl, lane, h1);
   tanh16(h1[0]);
   tanh16(h1[1]);
+  if (cache != nullptr) {
+    cache_store(cache, lane, 0, h1[0]);
+    cache_store(cache, lane, 1, h1[1]);
+  }
 #pragma unroll
   for (int o = 0; o < MAX_OUT; ++o) z[o] = 0.f;
 #pragma unroll
@@ -183,10 +212,55 @@ __device__ inline void forward_head_lowreg(const float* lds, const MlpDims& d, c
     chain1(lds, d.fa1, mo, h1, lane, a);
     __builtin_amdgcn_sched_barrier(0);
     tanh16(a);
+    if (cache != nullptr) cache_store(cache, lane, 2 + mo, a);
     head_partial_mt(lds, d, a, mo, h, z);
     __builtin_amdgcn_sched_barrier(0);
   }
   head_finish(lds, d, z);
+}
+
+// JVP to the head from the cached primal activations: no primal chain is recomputed
+// (the head outputs z come from the cached h2 on the VALU)
+template <class XL>
+__device__ inline void jvp_head_cached(const float* lds, const float* ldt, const MlpDims& d, const XL& xl, int lane,
+                                       const float* cache, float* z, float* dz) {
+  const int h = lane >> 5;
+  f32x16 h1[2], dh1[2];
+  cache_load(cache, lane, 0, h1[0]);
+  cache_load(cache, lane, 1, h1[1]);
+  dh1[0] = load_bias16(ldt, d.fb0, 0, h);
+  dh1[1] = load_bias16(ldt, d.fb0, 1, h);
+  layer0(ldt, d, xl, lane, dh1);
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dh1[m][r] *= (1.f - h1[m][r] * h1[m][r]);
+  float dzt[MAX_OUT];
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    z[o] = 0.f;
+    dz[o] = 0.f;
+    dzt[o] = 0.f;
+  }
+#pragma unroll
+  for (int mo = 0; mo < 2; ++mo) {
+    f32x16 a;
+    cache_load(cache, lane, 2 + mo, a);
+    f32x16 da = load_bias16(ldt, d.fb1, mo, h);
+    chain1(lds, d.fa1, mo, dh1, lane, da);
+    __builtin_amdgcn_sched_barrier(0);
+    chain1(ldt, d.fa1, mo, h1, lane, da);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) da[r] *= (1.f - a[r] * a[r]);
+    head_partial_mt(lds, d, a, mo, h, z);
+    head_partial_mt(lds, d, da, mo, h, dz);
+    head_partial_mt(ldt, d, a, mo, h, dzt);
+  }
+  head_finish(lds, d, z);
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) dz[o] += dzt[o];
+  head_finish(ldt, d, dz);
 }
 
 // forward + JVP to the head, layer 2 one M-tile at a time (peak: h1, dh1 + 2 tiles)

@@ -42,11 +42,15 @@ constexpr int SCR_FLOATS = 2 * 64 * IMG_PAD;  // per-wave transpose scratch
 
 static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-template <int EPI>
+constexpr int EPI_FVP_CACHED = 100;  // internal: MRL_EPI_FVP reading the activation cache
+
+template <int EPI_K>
 // 2 waves/SIMD: layer 2 is evaluated one M-tile at a time so the chain fits 256 registers
 __global__ __launch_bounds__(ROWS_BLOCK, 2) void mlp_rows_kernel(RowsArgs a, const float* __restrict__ img,
                                                                const float* __restrict__ imgt,
                                                                const int32_t* __restrict__ skip) {
+  constexpr bool CACHED = EPI_K == EPI_FVP_CACHED;
+  constexpr int EPI = CACHED ? MRL_EPI_FVP : EPI_K;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if (skip != nullptr && *skip != 0) return;
   const MlpDims& d = a.d;
@@ -75,8 +79,10 @@ __global__ __launch_bounds__(ROWS_BLOCK, 2) void mlp_rows_kernel(RowsArgs a, con
     const bool valid = row < a.n;
     XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
     float z[MAX_OUT], dz[MAX_OUT];
-    if (EPI == MRL_EPI_FVP) forward_jvp_head_lowreg(lds, ldt, d, xl, lane, z, dz);
-    else forward_head_lowreg(lds, d, xl, lane, z);
+    float* ctile = a.cache != nullptr ? a.cache + tile * CACHE_TILE_FLOATS : nullptr;
+    if (CACHED) jvp_head_cached(lds, ldt, d, xl, lane, ctile, z, dz);
+    else if (EPI == MRL_EPI_FVP) forward_jvp_head_lowreg(lds, ldt, d, xl, lane, z, dz);
+    else forward_head_lowreg(lds, d, xl, lane, z, a.cache_mode == MRL_CACHE_WRITE ? ctile : nullptr);
     if constexpr (EPI == MRL_EPI_PPOSGD) {
       // one 128-row minibatch per launch (ppo.py:150-156): block-reduced minibatch KL
       // sets the penalty slope, then the pensurr head gradient of every row
@@ -120,6 +126,7 @@ struct VjpArgs {
   int64_t n;
   const float* ghead;
   float* slab;
+  const float* cache;  // primal activation cache (CACHED kernel)
 };
 
 // write a transposed tile (two 32x32 C tiles of 64 units) as img[unit][h'][s'],
@@ -144,21 +151,31 @@ __device__ inline float rowsum32(const float* img, int unit) {
   return s;
 }
 
-// every global operand one tile needs, loaded ahead of use
+// every global operand one tile needs, loaded ahead of use; CACHED: the primal
+// activations come from the cache instead of the layer-0 inputs
+template <bool CACHED>
 struct VjpIn {
-  float x0[16];       // layer-0 B operands x[row][2s+h]
-  float xg[16];       // gW0 A operands x[row0+2s+h][j]
-  float g[4];         // head-gradient rows ghead[row][r+4h]
-  float gs[MAX_OUT];  // summed head columns (DiagGauss logstd), lane half 0 only
+  float x0[CACHED ? 1 : 16];  // layer-0 B operands x[row][2s+h]
+  f32x16 act[CACHED ? 4 : 1]; // cached h1[0], h1[1], h2[0], h2[1]
+  float xg[16];               // gW0 A operands x[row0+2s+h][j]
+  float g[4];                 // head-gradient rows ghead[row][r+4h]
+  float gs[MAX_OUT];          // summed head columns (DiagGauss logstd), lane half 0 only
 };
 
-__device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn& in) {
+template <bool CACHED>
+__device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn<CACHED>& in) {
   const int h = lane >> 5, j = lane & 31;
   const int64_t row0 = tile * 32, row = row0 + j;
   const bool valid = row < a.n;
   XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
+  if constexpr (CACHED) {
+    const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
 #pragma unroll
-  for (int s = 0; s < 16; ++s) in.x0[s] = (s < a.d.KS0p) ? xl(2 * s + h) : 0.f;
+    for (int q = 0; q < 4; ++q) cache_load(ct, lane, q, in.act[q]);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) in.x0[s] = (s < a.d.KS0p) ? xl(2 * s + h) : 0.f;
+  }
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
     const int64_t xr = row0 + 2 * s + h;
@@ -175,6 +192,7 @@ __device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn&
     in.gs[q] = (valid && h == 0 && q < a.n_sum) ? a.ghead[row * a.gh + a.d.A + q] : 0.f;
 }
 
+template <bool CACHED>
 __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __restrict__ img,
                                                        const int32_t* __restrict__ skip) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -204,14 +222,21 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t stride = (int64_t)gridDim.x * 4;
   // software pipeline: every global operand of tile i+1 is in flight while tile i computes
-  VjpIn cur, nxt;
+  VjpIn<CACHED> cur, nxt;
   int64_t tile = (int64_t)blockIdx.x * 4 + wave;
   if (tile < ntiles) vjp_load(a, tile, lane, cur);
   for (; tile < ntiles; tile += stride) {
     if (tile + stride < ntiles) vjp_load(a, tile + stride, lane, nxt);
     const int64_t row0 = tile * 32;
     Fwd f;
-    forward_tile_pre(lds, d, cur.x0, lane, f);
+    if constexpr (CACHED) {
+      f.h1[0] = cur.act[0];
+      f.h1[1] = cur.act[1];
+      f.h2[0] = cur.act[2];
+      f.h2[1] = cur.act[3];
+    } else {
+      forward_tile_pre(lds, d, cur.x0, lane, f);
+    }
 
     // head gradient rows in C layout: register r of half h = out r + 4h
     f32x16 G = zero16();
@@ -438,6 +463,7 @@ int64_t mrl_mlp_image_floats(const mrl_mlp_desc* d) {
   return dims_of(d).total_size;
 }
 int64_t mrl_partial_rows(int64_t n) { return rows_blocks(n) * 4; }
+int64_t mrl_act_cache_floats(int64_t n) { return ceil_div(n, 32) * CACHE_TILE_FLOATS; }
 int64_t mrl_slab_rows(int64_t n) { return vjp_blocks(n) * 4; }
 
 int mrl_mlp_pack(const mrl_mlp_desc* d, const float* theta, float* image, int32_t fwd_only, const int32_t* skip,
@@ -482,6 +508,11 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
   a.kl_cutoff = (float)io->kl_cutoff;
   a.cutoff_coeff = (float)io->cutoff_coeff;
   a.reverse_kl = io->reverse_kl;
+  a.cache = io->act_cache;
+  a.cache_mode = io->act_cache != nullptr ? io->cache_mode : 0;
+  if (a.cache_mode == MRL_CACHE_READ && epi != MRL_EPI_FVP) return fail(E_ARG, "MRL_CACHE_READ is for MRL_EPI_FVP");
+  if (a.cache_mode == MRL_CACHE_WRITE && (epi == MRL_EPI_FVP || epi == MRL_EPI_PPOSGD))
+    return fail(E_ARG, "MRL_CACHE_WRITE is for the plain forward epilogues");
   switch (epi) {
     case MRL_EPI_PROB:
       if (!io->out) return fail(E_ARG, "EPI_PROB needs out");
@@ -526,7 +557,12 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
       hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_VFLOSS>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t, skip);
       break;
     case MRL_EPI_FVP:
-      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_FVP>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t, skip);
+      if (a.cache_mode == MRL_CACHE_READ)
+        hipLaunchKernelGGL(mlp_rows_kernel<EPI_FVP_CACHED>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t,
+                           skip);
+      else
+        hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_FVP>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t,
+                           skip);
       break;
     case MRL_EPI_PPOGRAD:
       hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_PPOGRAD>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t,
@@ -540,7 +576,8 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
 }
 
 int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const int32_t* ep_t, double ts_limit,
-                const float* ghead, int64_t n, float* slab, const int32_t* skip, void* stream) {
+                const float* ghead, int64_t n, float* slab, const float* act_cache, const int32_t* skip,
+                void* stream) {
   int rc = check_desc(d);
   if (rc) return rc;
   if (!image || !x || !ghead || !slab) return fail(E_ARG, "null pointer");
@@ -558,7 +595,11 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
   a.slab = slab;
   const int64_t blocks = vjp_blocks(n);
   size_t shm = ((size_t)a.d.total_size + 4 * (size_t)SCR_FLOATS) * 4;
-  hipLaunchKernelGGL(mlp_vjp_kernel, dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image, skip);
+  a.cache = act_cache;
+  if (act_cache != nullptr)
+    hipLaunchKernelGGL(mlp_vjp_kernel<true>, dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image, skip);
+  else
+    hipLaunchKernelGGL(mlp_vjp_kernel<false>, dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image, skip);
   return hip_check(hipGetLastError(), "mrl_mlp_vjp");
 }
 

@@ -29,6 +29,8 @@ struct RowsArgs {
   float kl_coeff;        // EPI_PPOGRAD: the full d pensurr / d kl (host-computed); EPI_PPOSGD: kl_coeff
   float kl_cutoff, cutoff_coeff;
   int reverse_kl;        // kl[new, old] instead of kl[old, new]
+  float* cache;          // primal activation cache (fused path) or nullptr
+  int cache_mode;        // MRL_CACHE_WRITE: the forward stores h1/h2; MRL_CACHE_READ: FVP reads them
 };
 
 constexpr float LOG2PI_F = 1.8378770664093453f;

@@ -104,6 +104,10 @@ class MlpNet:
         self.gh = 2 * n_out if head == _lib.HEAD_GAUSS else n_out
         self.hid_sizes = [HIDDEN] * N_LAYERS
         self.ws = Workspace(self.device)
+        # primal activation cache (h1/h2 of the last recording pass at self.theta):
+        # the Fisher products of an update and the VJP after a loss pass reuse it
+        self.use_cache = True
+        self._cache_key = None
 
     # ---- flat parameter plumbing (GetFlat / SetFromFlat, core.py:518-557)
     def get_flat(self):
@@ -123,24 +127,45 @@ class MlpNet:
     def rows(self, epi, x, n, ep_t=None, timestep_limit=1.0, inv_n_global=1.0, act=None, adv=None, oldprob=None,
              target=None, out=None, ghead=None, partial=None, theta=None, image=None, tangent=None, image_t=None,
              skip=None, kl_coeff=0.0, kl_cutoff=0.0, cutoff_coeff=0.0, reverse_kl=0):
-        io = _lib.RowsIO(ptr(x), ptr(ep_t), float(timestep_limit), int(n), float(inv_n_global), ptr(act), ptr(adv),
-                         ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial), float(kl_coeff),
-                         float(kl_cutoff), float(cutoff_coeff), int(reverse_kl))
+        own = (theta is None or theta is self.theta) and (image is None or image is self.image)
         theta = self.theta if theta is None else theta
         image = self.image if image is None else image
+        mode, cache = _lib.CACHE_NONE, None
+        if self.use_cache and own:
+            key = self._key(x, n, ep_t, timestep_limit)
+            if epi in (_lib.EPI_SURRGRAD, _lib.EPI_VFLOSS, _lib.EPI_PPOGRAD):
+                mode, cache = _lib.CACHE_WRITE, self._cache(n)
+                self._cache_key = key
+            elif epi == _lib.EPI_FVP and self._cache_key == key:
+                mode, cache = _lib.CACHE_READ, self._cache(n)
+        io = _lib.RowsIO(ptr(x), ptr(ep_t), float(timestep_limit), int(n), float(inv_n_global), ptr(act), ptr(adv),
+                         ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial), float(kl_coeff),
+                         float(kl_cutoff), float(cutoff_coeff), int(reverse_kl), mode, ptr(cache))
         call("mrl_mlp_rows", ctypes.byref(self.desc), int(epi), ptr(theta), ptr(image), ptr(tangent), ptr(image_t),
              ctypes.byref(io), ptr(skip), stream())
+
+    def _key(self, x, n, ep_t, timestep_limit):
+        return (self.theta.data_ptr(), self.theta._version, x.data_ptr(), int(n),
+                None if ep_t is None else ep_t.data_ptr(), float(timestep_limit))
+
+    def _cache(self, n):
+        return self.ws.get("act_cache", int(self.lib.mrl_act_cache_floats(int(n))), torch.float32)
 
     def partial_rows(self, n):
         return int(self.lib.mrl_partial_rows(int(n)))
 
     def vjp_flat(self, x, n, ghead, out, ep_t=None, timestep_limit=1.0, image=None, skip=None):
-        """out[P] (fp32) <- sum_n J_n^T ghead_n (per-wave slab + deterministic reduce)."""
+        """out[P] (fp32) <- sum_n J_n^T ghead_n (per-wave slab + deterministic reduce); the
+        forward comes from the activation cache when the last recording pass was at
+        self.theta on the same rows."""
         rows = int(self.lib.mrl_slab_rows(int(n)))
         slab = self.ws.get("slab", rows * self.P, torch.float32)
+        cache = None
+        if self.use_cache and image is None and self._cache_key == self._key(x, n, ep_t, timestep_limit):
+            cache = self._cache(n)
         image = self.image if image is None else image
         call("mrl_mlp_vjp", ctypes.byref(self.desc), ptr(image), ptr(x), ptr(ep_t), float(timestep_limit),
-             ptr(ghead), int(n), ptr(slab), ptr(skip), stream())
+             ptr(ghead), int(n), ptr(slab), ptr(cache), ptr(skip), stream())
         call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
         return out
 

@@ -129,3 +129,39 @@ def test_value_forward_and_loss_grad_with_time_feature(nin):
     loss, gw, mse, l2 = T.vf_loss_grad(spec, th, X, y.astype(np.float64))
     np.testing.assert_allclose(sums[0].item() / N, mse, rtol=1e-5)
     assert _rel(g.cpu().numpy() + 2e-3 * th, gw) < 1e-4
+
+
+@pytest.mark.parametrize("head,nin,nout", [("gauss", 11, 3), ("softmax", 4, 2)])
+def test_activation_cache_is_bitwise_transparent(head, nin, nout):
+    """SURRGRAD stores h1/h2; the FVP and VJP that follow read them instead of
+    recomputing the forward -- results must equal the uncached kernels bit for bit."""
+    from modular_rl_amd import _lib
+    N = 3000
+    spec, th, ob, act, adv, oldprob = _setup(head, nin, nout, N, seed=9)
+    v = np.random.default_rng(2).standard_normal(spec.P).astype(np.float32)
+    outs = []
+    for use_cache in (False, True):
+        net = _net(head, nin, nout)
+        net.use_cache = use_cache
+        net.set_flat(th)
+        x, vt = _dev(ob), _dev(v)
+        a = _dev(act, torch.int32 if head == "softmax" else torch.float32)
+        partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+        ghead = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+        g = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+        net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(adv), oldprob=_dev(oldprob),
+                 ghead=ghead, partial=partial)
+        net.vjp_flat(x, N, ghead, g)
+        imgt = torch.zeros_like(net.image)
+        net.pack(theta=vt, image=imgt, fwd_only=True)
+        fv = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+        net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=ghead, tangent=vt, image_t=imgt)
+        gh = ghead.clone()
+        net.vjp_flat(x, N, ghead, fv)
+        outs.append((g.cpu(), gh.cpu(), fv.cpu()))
+        if use_cache:
+            assert net._cache_key is not None
+    for u, c in zip(*outs):
+        assert torch.equal(u, c)
+    want = T.fisher_vector_product(spec, th, v.astype(np.float64), ob)
+    assert _rel(outs[1][2].numpy(), want) < 1e-4
