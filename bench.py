@@ -109,7 +109,7 @@ def main():
 
     comm = init_from_env()
     if torch.cuda.is_available() and not comm.enabled:
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
     rank, world = comm.rank, comm.world
     env = make(args.env)
     E, Tn = args.envs, args.horizon

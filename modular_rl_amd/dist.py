@@ -52,12 +52,14 @@ class Comm:
 
 
 def init_from_env(backend=None):
-    """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torchrun) if present."""
+    """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torchrun) if present.
+    ``MRL_DIST_BACKEND=gloo`` rehearses the multi-rank path with several ranks sharing
+    one GPU (each rank uses device LOCAL_RANK mod the visible device count)."""
     if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or dist.is_initialized():
         return Comm()
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-    if backend == "nccl":
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        backend = os.environ.get("MRL_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    if torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
     dist.init_process_group(backend=backend)
     return Comm()
