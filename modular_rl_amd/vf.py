@@ -163,11 +163,22 @@ class NnVf:
         ep_t = torch.arange(n, dtype=torch.int32, device=self.net.device)
         return self.reg.predict(ob, n, ep_t, self.timestep_limit).cpu().numpy().astype(np.float64)
 
+    def features(self, obs, n, ep_t):
+        """X = [obs, t / timestep_limit] materialised once per batch (`core.py:659-660`):
+        every VF pass of the fit then reads plain rows instead of re-deriving the time
+        feature per tile."""
+        n = int(n)
+        X = self.net.ws.get("vf_features", n * self.net.n_in, torch.float32)
+        call("mrl_concat_time", ptr(obs), ptr(ep_t), n, self.net.n_in - 1, float(self.timestep_limit), ptr(X), stream())
+        return X
+
     def predict_batch(self, batch, out=None):
-        return self.reg.predict(batch.obs, batch.n, batch.ep_t, self.timestep_limit, out=out)
+        X = self.features(batch.obs, batch.n, batch.ep_t)
+        return self.reg.predict(X, batch.n, None, 1.0, out=out)
 
     def fit_batch(self, batch):
-        return self.reg.fit(batch.obs, batch.n, batch.ret, batch.ep_t, self.timestep_limit, ypredold=batch.vpred)
+        X = self.features(batch.obs, batch.n, batch.ep_t)
+        return self.reg.fit(X, batch.n, batch.ret, None, 1.0, ypredold=batch.vpred)
 
     def fit(self, paths):
         from .core import Batch

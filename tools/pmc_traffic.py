@@ -1,0 +1,85 @@
+"""HBM traffic per launch of the hot-path kernels from two rocprofv3 counter passes
+(MI355X_MICROARCH.md § HBM: FETCH_SIZE and WRITE_SIZE need separate passes; gfx950's
+FETCH_SIZE counts half the bytes of wide coalesced reads -> x2; both are in KB).
+
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d <fetch_dir> -o run -- python bench.py ...
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d <write_dir> -o run -- python bench.py ...
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> [--out profiles/pmc_r01.json]
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+
+# role -> kernel-name substring (first match wins, most specific first)
+ROLES = [
+    ("fvp_jvp_rows", "mlp_rows_kernel<100>"),
+    ("fvp_vjp", "mlp_vjp_kernel<true>"),
+    ("vjp_uncached", "mlp_vjp_kernel<false>"),
+    ("rows_surrgrad", "mlp_rows_kernel<2>"),
+    ("rows_vfloss", "mlp_rows_kernel<3>"),
+    ("rollout_step", "rollout_step_kernel"),
+    ("gae_summary", "gae_summary_kernel"),
+    ("gae_final", "gae_final_kernel"),
+    ("gemm_nn", "gemm_f32_kernel<false, false, 128>"),
+    ("gemm_nt", "gemm_f32_kernel<false, true, 128>"),
+    ("gemm_tn", "gemm_f32_kernel<true, false, 128>"),
+]
+
+
+def _rows(d):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no *counter_collection.csv under {d}")
+    for f in files:
+        with open(f) as fh:
+            yield from csv.DictReader(fh)
+
+
+def per_role(d, counter):
+    acc = {}
+    for r in _rows(d):
+        if r.get("Counter_Name") != counter:
+            continue
+        name = r.get("Kernel_Name", "")
+        for role, sub in ROLES:
+            if sub in name:
+                a = acc.setdefault(role, [0, 0.0])
+                a[0] += 1
+                a[1] += float(r["Counter_Value"])
+                break
+    return {k: (n, tot / n) for k, (n, tot) in acc.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    fe = per_role(a.fetch_dir, "FETCH_SIZE")
+    wr = per_role(a.write_dir, "WRITE_SIZE")
+    out = {}
+    note = ("FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads, MI355X_MICROARCH.md HBM), KB->bytes x1024; "
+            "separate --pmc passes")
+    for role in sorted(set(fe) | set(wr)):
+        f = fe.get(role)
+        w = wr.get(role)
+        e = {"note": note}
+        if f:
+            e["FETCH_SIZE_KB_mean"], e["launches_FETCH_SIZE"] = f[1], f[0]
+        if w:
+            e["WRITE_SIZE_KB_mean"], e["launches_WRITE_SIZE"] = w[1], w[0]
+        if f and w:
+            e["hbm_bytes_per_launch"] = int(round((2.0 * f[1] + w[1]) * 1024))
+        out[role] = e
+    s = json.dumps(out, indent=1)
+    if a.out:
+        with open(a.out, "w") as fh:
+            fh.write(s + "\n")
+    print(s)
+
+
+if __name__ == "__main__":
+    main()
