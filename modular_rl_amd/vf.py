@@ -84,18 +84,28 @@ class LbfgsOptimizer:
 
     def update(self, data):
         thprev = self.get_params_flat()
+        memo = {}  # float32 theta bytes -> (loss, mse, l2, grad): scipy revisits points
+
+        def evaluate(th32, with_grad):
+            key = th32.tobytes()
+            hit = memo.get(key)
+            if hit is not None and (hit[3] is not None or not with_grad):
+                return hit
+            if not np.array_equal(th32, self.net.theta.detach().cpu().numpy()):
+                self.set_params_flat(th32)
+            self.n_evals += 1
+            r = self._eval(data, with_grad)
+            memo[key] = r
+            return r
 
         def lossandgrad(th):
-            self.set_params_flat(th)
-            self.n_evals += 1
-            l, _, _, g = self._eval(data, True)
+            l, _, _, g = evaluate(th.astype(np.float32), True)
             return l, g.astype("float64")
 
-        self.set_params_flat(thprev)
-        lb, mb, l2b, _ = self._eval(data, False)
+        lb, mb, l2b, _ = evaluate(thprev.astype(np.float32), True)  # scipy's first point is thprev
         theta, _, opt_info = scipy.optimize.fmin_l_bfgs_b(lossandgrad, thprev.astype(np.float64), maxiter=self.maxiter)
+        la, ma, l2a, _ = evaluate(theta.astype(np.float32), False)
         self.set_params_flat(theta)
-        la, ma, l2a, _ = self._eval(data, False)
         info = OrderedDict()
         for name, b, a in (("loss", lb, la), ("mse", mb, ma), ("l2", l2b, l2a)):
             info[name + "_before"] = b
