@@ -257,7 +257,7 @@ typedef struct {
   uint8_t* flags;          /* [T*E] bit0 last-of-episode, bit1 terminated         */
   int32_t* ep_t;           /* [T*E] step index of the row inside its episode      */
   const void* noise;       /* optional injected noise [T*E] u | [T*E, d] z        */
-  int64_t* stamps;         /* optional diagnostic: [T, 8] s_memtime of block 0 phases (NULL in production) */
+  int64_t* stamps;         /* optional diagnostic: [T, 16] s_memrealtime of block 0 phases (NULL in production) */
   double* raw_obs;         /* layered rollout: [obs_dim+1, E] raw next obs + reward (SoA) */
 } mrl_rollout_bufs;
 
@@ -267,9 +267,15 @@ int64_t mrl_record_doubles(int32_t env_id);
 int64_t mrl_rollout_blocks(int32_t n_envs);
 /* reset every env (start of iteration, core.py:186) and publish obs_0 partials */
 int mrl_rollout_reset(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void* stream);
-/* one lock-step env step t (0 <= t < horizon) for all envs */
+/* policy image of the fused step kernel (16 envs per wave on 16x16x4 MFMA tiles,
+ * mlp_layout.h rollout_dims): floats of it, and its packing from flat theta -- once
+ * per iteration, before the steps (theta changes between iterations) */
+int64_t mrl_rollout_image_floats(const mrl_mlp_desc* pol);
+int mrl_rollout_pack(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta, float* rimage,
+                     void* stream);
+/* one lock-step env step t (0 <= t < horizon) for all envs; rimage from mrl_rollout_pack */
 int mrl_rollout_step(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta,
-                     const float* image, const mrl_rollout_bufs* b, int32_t t, void* stream);
+                     const float* rimage, const mrl_rollout_bufs* b, int32_t t, void* stream);
 /* Layered-policy rollout (any policy net; required for Humanoid): step t is
  *   mrl_rollout_obs(t)            filter merge + normalised obs rows of step t -> b->obs
  *   <policy forward over the E rows of step t, e.g. LayeredMlpNet GEMMs> -> z [E, n_out]

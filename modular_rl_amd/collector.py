@@ -7,7 +7,8 @@ policy MLP on MFMA -> sample -> env step -> Welford partials).  With a layered
 policy (wide nets, Humanoid's 376-d obs) a step is mrl_rollout_obs -> the policy's
 GEMM forward over the E rows -> mrl_rollout_act.  The T launches (plus reset/finish) can be captured
 once into a hipGraph and replayed every iteration (``use_graph``): the policy
-weights are read through the persistent ``net.image`` buffer and the RNG step base
+weights are read through persistent buffers (theta / the rollout image repacked at
+the head of every replay) and the RNG step base
 from a device iteration counter, so replays need no re-capture.
 
 Semantics vs the reference: every env is reset at the start of
@@ -159,7 +160,7 @@ class Collector:
         self.flags = torch.zeros(self.N, dtype=torch.uint8, device=self.dev)
         self.ep_t = torch.zeros(self.N, dtype=torch.int32, device=self.dev)
         self.noise = None
-        self.stamps = None  # diagnostic [T, 8] int64 phase stamps (see rollout.hip); None in production
+        self.stamps = None  # diagnostic [T, 16] int64 phase stamps (see rollout.hip); None in production
         net = policy.net
         self.layered = bool(getattr(net, "layered", False))
         if env.kind == _lib.ENV_HUMANOID and not self.layered:
@@ -171,6 +172,10 @@ class Collector:
             self._zrows = torch.zeros(self.E * A, dtype=torch.float32, device=self.dev)
             w = max(net.hid_sizes)
             self._fwd_bufs = [torch.zeros(self.E * w, dtype=torch.float32, device=self.dev) for _ in range(2)]
+        else:
+            # fused step kernel: its own policy image, repacked from theta at every collect
+            n = int(lib.mrl_rollout_image_floats(ctypes.byref(net.desc)))
+            self._rimage = torch.zeros(n, dtype=torch.float32, device=self.dev)
         self.use_graph = use_graph
         self.graph = None
         self._ep_ws = torch.zeros(int(lib.mrl_episode_stats_workspace_bytes(self.E)) // 8 + 1, **f64)
@@ -187,10 +192,12 @@ class Collector:
         net = self.policy.net
         if self.layered:
             return self._launch_all_layered(bufs, net)
+        call("mrl_rollout_pack", ctypes.byref(self.desc), ctypes.byref(net.desc), ptr(net.theta), ptr(self._rimage),
+             stream())
         call("mrl_rollout_reset", ctypes.byref(self.desc), ctypes.byref(bufs), stream())
         for t in range(self.T):
-            call("mrl_rollout_step", ctypes.byref(self.desc), ctypes.byref(net.desc), ptr(net.theta), ptr(net.image),
-                 ctypes.byref(bufs), int(t), stream())
+            call("mrl_rollout_step", ctypes.byref(self.desc), ctypes.byref(net.desc), ptr(net.theta),
+                 ptr(self._rimage), ctypes.byref(bufs), int(t), stream())
         call("mrl_rollout_finish", ctypes.byref(self.desc), ctypes.byref(bufs), stream())
 
     def _launch_all_layered(self, bufs, net):

@@ -66,7 +66,19 @@ __device__ inline void hopper_reset(const double* u, double* s) {
 
 __device__ inline double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-__device__ inline void hopper_substep(double* q, double* v, const double* tau) {
+// the four angle functions of a substep: (s0,c0)=sincos(ar), (s1,c1)=sincos(p1),
+// (s2,c2)=sincos(p2), sa3=sin(a3); one shared range reduction per angle
+struct HopperTrigSerial {
+  __device__ void operator()(double ar, double p1, double p2, double a3, double* sc) const {
+    sincos(ar, &sc[0], &sc[1]);
+    sincos(p1, &sc[2], &sc[3]);
+    sincos(p2, &sc[4], &sc[5]);
+    sc[6] = sin(a3);
+  }
+};
+
+template <class Trig>
+__device__ inline void hopper_substep(double* q, double* v, const double* tau, const Trig& trig) {
   const double HP_I[3] = {4.0, 3.0, 1.5};
   const double HP_K[3] = {30.0, 30.0, 20.0};
   const double HP_C[3] = {8.0, 6.0, 4.0};
@@ -76,17 +88,16 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau) {
   const double p2 = p1 + a2;
   const double w1 = var_ + v1;
   const double w2 = w1 + v2;
-  double s0, c0, s1, c1, s2, c2;  // one shared range reduction per angle
-  sincos(ar, &s0, &c0);
-  sincos(p1, &s1, &c1);
-  sincos(p2, &s2, &c2);
+  double sc[7];
+  trig(ar, p1, p2, a3, sc);
+  const double s0 = sc[0], c0 = sc[1], s1 = sc[2], c1 = sc[3], s2 = sc[4], c2 = sc[5];
   const double fx = x + HP_L_TORSO * s0 + HP_L_THIGH * s1 + HP_L_LEG * s2;
   const double fz = z - HP_L_TORSO * c0 - HP_L_THIGH * c1 - HP_L_LEG * c2;
   const double fvx = vx + HP_L_TORSO * c0 * var_ + HP_L_THIGH * c1 * w1 + HP_L_LEG * c2 * w2;
   const double fvz = vz + HP_L_TORSO * s0 * var_ + HP_L_THIGH * s1 * w1 + HP_L_LEG * s2 * w2;
   const double pen = HP_FOOT_R - fz;
   const double fn = pen > 0.0 ? fmax(HP_KC * pen - HP_CC * fvz, 0.0) : 0.0;
-  const double ft = -HP_MU * fn * tanh(fvx / 0.05) * (1.0 - 0.5 * fabs(sin(a3)));
+  const double ft = -HP_MU * fn * tanh(fvx / 0.05) * (1.0 - 0.5 * fabs(sc[6]));
   const double ax = ft / HP_MASS;
   const double az = fn / HP_MASS - HP_GRAV;
   const double tq_root = (fx - x) * fn - (fz - z) * ft;
@@ -116,7 +127,8 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau) {
   }
 }
 
-__device__ inline void hopper_step(double* s, const float* a, double& rew, bool& done) {
+template <class Trig = HopperTrigSerial>
+__device__ inline void hopper_step(double* s, const float* a, double& rew, bool& done, const Trig& trig = Trig()) {
   double tau[3];
   double asq = 0.0;
   for (int j = 0; j < 3; ++j) {
@@ -127,7 +139,7 @@ __device__ inline void hopper_step(double* s, const float* a, double& rew, bool&
   double* q = s;
   double* v = s + 6;
   const double x_before = q[0];
-  for (int k = 0; k < HP_FRAME_SKIP; ++k) hopper_substep(q, v, tau);
+  for (int k = 0; k < HP_FRAME_SKIP; ++k) hopper_substep(q, v, tau, trig);
   rew = (q[0] - x_before) / (HP_DT * HP_FRAME_SKIP) + 1.0 - 1e-3 * asq;
   bool healthy = true;
   for (int i = 0; i < 12; ++i) healthy = healthy && isfinite(s[i]);

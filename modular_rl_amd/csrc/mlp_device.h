@@ -419,6 +419,34 @@ __device__ inline void forward_jvp_tile(const float* lds, const float* ldt, cons
   head_finish(ldt, d, dz);
 }
 
+// 16-lane-row exchange (v_permlane32_swap + v_permlane16_swap, no LDS): out[q] = v of
+// the lane in row q (lanes 16q .. 16q+15) with this lane's column (lane & 15).  All
+// lanes active.
+__device__ inline void quads_u32(uint32_t x, uint32_t* out) {
+  const auto p = __builtin_amdgcn_permlane32_swap(x, x, false, false);  // [x0 x1 x0 x1], [x2 x3 x2 x3]
+  const auto a = __builtin_amdgcn_permlane16_swap(p[0], p[0], false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(p[1], p[1], false, false);
+  out[0] = a[0];
+  out[1] = a[1];
+  out[2] = b[0];
+  out[3] = b[1];
+}
+__device__ inline void quads(double v, double* out) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  uint32_t lo[4], hi[4];
+  quads_u32((uint32_t)b, lo);
+  quads_u32((uint32_t)(b >> 32), hi);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) out[q] = __longlong_as_double((long long)(((uint64_t)hi[q] << 32) | (uint64_t)lo[q]));
+}
+// (v_row0 + v_row1) + (v_row2 + v_row3) for this lane's column, identical in all rows
+__device__ inline float quad_sum(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float t = __uint_as_float(p[0]) + __uint_as_float(p[1]);  // rows 0,1: v0+v1; rows 2,3: v2+v3
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
 __device__ inline double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

@@ -119,4 +119,56 @@ __host__ __device__ inline float image_value(const MlpDims& d, const float* th, 
   }
 }
 
+// ------------------------------------------------------------------ rollout image
+// The fused rollout step kernel is latency-bound at one wave per SIMD, so it runs 16
+// envs per wave on v_mfma_f32_16x16x4_f32: a 16-row tile halves the per-wave MFMA
+// chain and tanh count of the 32-row layout above.  Activations D[unit][row]: lane l
+// holds row l&15 and units 16*mt + 4*(l>>4) + r (r = 0..3) of 16-unit tile mt, which
+// is directly the B operand of the next layer's k-step (mt, q = r) when the k index
+// of lane group g stands for unit 16*mt + 4*g + q; the weight fragments are permuted
+// to match.  Every lane loads its fragments straight into registers (no LDS copy).
+struct RDims {
+  int KS0, KS0p;  // input-layer k-steps (4 inputs each), padded to a multiple of 4
+  int a0, a1, b0, b1, hv, hb, size;
+};
+
+__host__ __device__ constexpr RDims rollout_dims(int O) {
+  RDims r{};
+  r.KS0 = (O + 3) / 4;
+  r.KS0p = (r.KS0 + 3) & ~3;
+  int o = 0;
+  r.a0 = o; o += 4 * r.KS0p * 64;   // [mo][ks>>2][lane][ks&3] = W0[4ks + (lane>>4)][16mo + (lane&15)]
+  r.a1 = o; o += 4 * 16 * 64;       // [mo][mt][lane][q]       = W1[16mt + 4(lane>>4) + q][16mo + (lane&15)]
+  r.b0 = o; o += 64;                // [g][4mt + r]            = b0[16mt + 4g + r]
+  r.b1 = o; o += 64;                //                           b1
+  r.hv = o; o += 4 * MAX_OUT * 16;  // [g][o][4mt + r]         = W2[16mt + 4g + r][o]
+  r.hb = o; o += 16;                // b2 (padded)
+  r.size = o;
+  return r;
+}
+
+// value of rollout-image element `idx` given flat theta (layout above)
+__host__ __device__ inline float rimage_value(const RDims& r, const MlpDims& d, const float* th, int idx) {
+  if (idx < r.a1) {
+    const int rel = idx - r.a0, q = rel & 3, lane = (rel >> 2) & 63, blk = rel >> 8;
+    const int mo = blk / (r.KS0p / 4), ks = (blk % (r.KS0p / 4)) * 4 + q;
+    const int k = 4 * ks + (lane >> 4), u = 16 * mo + (lane & 15);
+    return k < d.O ? th[d.tW0 + k * HID + u] : 0.f;
+  } else if (idx < r.b0) {
+    const int rel = idx - r.a1, q = rel & 3, lane = (rel >> 2) & 63, blk = rel >> 8;
+    const int mo = blk >> 2, mt = blk & 3;
+    return th[d.tW1 + (16 * mt + 4 * (lane >> 4) + q) * HID + 16 * mo + (lane & 15)];
+  } else if (idx < r.hv) {
+    const bool first = idx < r.b1;
+    const int rel = idx - (first ? r.b0 : r.b1), g = rel >> 4, i = rel & 15;
+    return th[(first ? d.tb0 : d.tb1) + 16 * (i >> 2) + 4 * g + (i & 3)];
+  } else if (idx < r.hb) {
+    const int rel = idx - r.hv, i = rel & 15, o = (rel >> 4) % MAX_OUT, g = rel / (16 * MAX_OUT);
+    return o < d.A ? th[d.tW2 + (16 * (i >> 2) + 4 * g + (i & 3)) * d.A + o] : 0.f;
+  } else {
+    const int o = idx - r.hb;
+    return o < d.A ? th[d.tb2 + o] : 0.f;
+  }
+}
+
 }  // namespace mrl

@@ -6,12 +6,14 @@
 #include <string>
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // v_mfma_f32_32x32x2_f32: exact f32 (a k-ordered fmaf chain), 64 cycles/SIMD.
 // lane l supplies A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31];
 // D[i][j] lives in lane j (+32 for the upper row half), register r holds row
 // i = (r&3) + 8*(r>>2) + 4*(l>>5).
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
+#define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
 
 namespace mrl {
 

@@ -27,8 +27,30 @@
 namespace mrl {
 
 constexpr int RB = 256;  // threads per block
-constexpr int ENVS_PER_BLOCK = 128;
+constexpr int ENVS_PER_BLOCK = 64;  // fused step: 4 waves x 16 envs
 constexpr int MAXD = 16;  // obs dims + 1 (reward)
+
+// Hopper angle functions in the fused step kernel, where the four 16-lane rows of a
+// wave hold the SAME 16 envs: row g evaluates sincos of angle g (ar, p1, p2, a3) and
+// the rows exchange -- one sincos sequence per substep instead of three plus a sin.
+// All lanes must be active.
+struct HopperTrigQuad {
+  int g;
+  __device__ void operator()(double ar, double p1, double p2, double a3, double* sc) const {
+    const double ang = g == 0 ? ar : (g == 1 ? p1 : (g == 2 ? p2 : a3));
+    double sx, cx, sv[4], cv[4];
+    sincos(ang, &sx, &cx);
+    quads(sx, sv);
+    quads(cx, cv);
+    sc[0] = sv[0];
+    sc[1] = cv[0];
+    sc[2] = sv[1];
+    sc[3] = cv[1];
+    sc[4] = sv[2];
+    sc[5] = cv[2];
+    sc[6] = sv[3];
+  }
+};
 
 template <int ENV>
 struct EnvC;
@@ -39,6 +61,7 @@ struct EnvC<MRL_ENV_CARTPOLE> {
   __device__ static void obs(const double* s, double* o) { cartpole_obs(s, o); }
   __device__ static void step_disc(double* s, int a, double& rew, bool& done) { cartpole_step(s, a, rew, done); }
   __device__ static void step_cont(double*, const float*, double&, bool&) {}
+  __device__ static void step_cont_quad(double*, const float*, double&, bool&, int) {}
   template <class Out>
   __device__ static void obs_out(const double* s, Out out) {
     double o[OBS];
@@ -54,6 +77,9 @@ struct EnvC<MRL_ENV_HOPPER> {
   __device__ static void obs(const double* s, double* o) { hopper_obs(s, o); }
   __device__ static void step_disc(double*, int, double&, bool&) {}
   __device__ static void step_cont(double* s, const float* a, double& rew, bool& done) { hopper_step(s, a, rew, done); }
+  __device__ static void step_cont_quad(double* s, const float* a, double& rew, bool& done, int g) {
+    hopper_step(s, a, rew, done, HopperTrigQuad{g});
+  }
   template <class Out>
   __device__ static void obs_out(const double* s, Out out) {
     double o[OBS];
@@ -94,6 +120,104 @@ struct RollArgs {
 };
 
 // reset-noise uniforms for one env: (gid, episode counter) on domain 1
+// ------------------------------------------------------------------ rollout policy forward
+// One wave = 16 envs on v_mfma_f32_16x16x4_f32 (mlp_layout.h, rollout image): the
+// step kernel is a latency chain at one wave per SIMD, and 16-row tiles halve both
+// the MFMA chain and the tanh work of a 32-row tile.  The weight fragments of the
+// wave go straight from global memory (L2-resident rollout image) into registers,
+// loaded at kernel entry so their latency hides under the filter merge.
+template <int O, int A>
+struct RWeights {
+  static constexpr RDims R = rollout_dims(O);
+  float4 a0[4][R.KS0p / 4];
+  float4 a1[4][4];
+  float4 b0[4], b1[4];
+  float4 hv[A][4];
+  float hb[A];
+  __device__ void load(const float* __restrict__ img, int lane) {
+    const int g = lane >> 4;
+    const float4* f = reinterpret_cast<const float4*>(img);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo)
+#pragma unroll
+      for (int s4 = 0; s4 < R.KS0p / 4; ++s4) a0[mo][s4] = f[(R.a0 >> 2) + (mo * (R.KS0p / 4) + s4) * 64 + lane];
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) a1[mo][mt] = f[(R.a1 >> 2) + (mo * 4 + mt) * 64 + lane];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      b0[mt] = f[(R.b0 >> 2) + g * 4 + mt];
+      b1[mt] = f[(R.b1 >> 2) + g * 4 + mt];
+    }
+#pragma unroll
+    for (int o = 0; o < A; ++o)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) hv[o][mt] = f[(R.hv >> 2) + (g * MAX_OUT + o) * 4 + mt];
+#pragma unroll
+    for (int o = 0; o < A; ++o) hb[o] = img[R.hb + o];
+  }
+};
+
+__device__ inline f32x4 as_f32x4(float4 v) {
+  f32x4 r;
+  r[0] = v.x;
+  r[1] = v.y;
+  r[2] = v.z;
+  r[3] = v.w;
+  return r;
+}
+__device__ inline float f4get(const float4& v, int q) { return q == 0 ? v.x : (q == 1 ? v.y : (q == 2 ? v.z : v.w)); }
+
+__device__ inline void tanh4(f32x4& a) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) a[r] = tanh_fast(a[r]);
+}
+
+// head rows z[o] of the wave's 16 envs (every lane of an env's column ends with all A)
+template <int O, int A, class XL>
+__device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane, float* z) {
+  constexpr RDims R = RWeights<O, A>::R;
+  const int g = lane >> 4;
+  float xb[R.KS0p];
+#pragma unroll
+  for (int ks = 0; ks < R.KS0p; ++ks) xb[ks] = ks < R.KS0 ? xl(4 * ks + g) : 0.f;
+  f32x4 h1[4], h2[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    h1[m] = as_f32x4(w.b0[m]);
+    h2[m] = as_f32x4(w.b1[m]);
+  }
+  // layer 0: four independent 16-unit accumulators
+#pragma unroll
+  for (int ks = 0; ks < R.KS0; ++ks)
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) h1[mo] = MFMA16(f4get(w.a0[mo][ks >> 2], ks & 3), xb[ks], h1[mo]);
+  // layer 1: input tile mt needs only tanh(h1[mt]), so later tiles' tanh overlaps the
+  // MFMAs of earlier ones
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    tanh4(h1[mt]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int mo = 0; mo < 4; ++mo) h2[mo] = MFMA16(f4get(w.a1[mo][mt], q), h1[mt][q], h2[mo]);
+  }
+  // head on VALU: 16 units per lane, then the four rows of the column
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) tanh4(h2[mt]);
+#pragma unroll
+  for (int o = 0; o < A; ++o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const float4 hv = w.hv[o][mt];
+      acc += hv.x * h2[mt][0] + hv.y * h2[mt][1] + hv.z * h2[mt][2] + hv.w * h2[mt][3];
+    }
+    z[o] = quad_sum(acc) + w.hb[o];
+  }
+}
+
 template <int ENV>
 __device__ inline void reset_env(const RollArgs& a, int e, double* s) {
   const int E = a.d.n_envs;
@@ -144,22 +268,22 @@ __device__ inline void publish_partial(const RollArgs& a, const double* vals, in
 // combine the per-block records of one column k into a batch (n, mean, M2):
 // mean = sum n_b mean_b / n ; M2 = sum (M2_b + n_b (mean_b - mean)^2).
 // Called by all 16 lanes of thread group k; every lane returns the same values.
-__device__ inline void batch_of_records(const double* rec, int nb, int RS, int D, int O, int k, int j, double& bn,
-                                        double& bm, double& bs) {
-  const bool isr = (k == O);
-  // all record fields in one round of loads (up to RB_MAX records per lane), then combine
-  constexpr int RB_MAX = 4;  // 16 lanes x 4 = 64 blocks (8192 envs) per round
+// Lane j holds records j + 16q of a round (RB_MAX per lane, 128 blocks = 8192 envs).
+constexpr int RB_MAX = 8;
+struct RecRound {
   double rn[RB_MAX], rm[RB_MAX], rs[RB_MAX];
-  double n = 0.0, sm = 0.0, raw = 0.0;
-  for (int b0 = 0; b0 < nb; b0 += 16 * RB_MAX) {
+  __device__ void load(const double* rec, int nb, int RS, int D, int O, int k, int j, int b0) {
+    const bool isr = (k == O);
 #pragma unroll
     for (int q = 0; q < RB_MAX; ++q) {
       const int b = b0 + j + 16 * q;
-      const double* r = rec + (int64_t)b * RS;
+      const double* r = rec + (int64_t)(b < nb ? b : 0) * RS;
       rn[q] = b < nb ? r[isr ? 1 : 0] : 0.0;
       rm[q] = b < nb ? r[2 + k] : 0.0;
       rs[q] = b < nb ? r[2 + D + k] : 0.0;
     }
+  }
+  __device__ void accumulate(double& n, double& sm, double& raw) const {
 #pragma unroll
     for (int q = 0; q < RB_MAX; ++q) {
       n += rn[q];
@@ -167,12 +291,13 @@ __device__ inline void batch_of_records(const double* rec, int nb, int RS, int D
       raw += rs[q] + rn[q] * rm[q] * rm[q];
     }
   }
-  n = sum16(n);
-  sm = sum16(sm);
-  const double mean = n > 0.0 ? sm / n : 0.0;
-  bn = n;
-  bm = mean;
-  if (nb <= 16 * RB_MAX) {  // one round (<= 8192 envs): exact two-pass form from registers
+  // one-round batch (nb <= 16 * RB_MAX): exact two-pass form from registers
+  __device__ void batch(double& bn, double& bm, double& bs) const {
+    double n = 0.0, sm = 0.0, raw = 0.0;
+    accumulate(n, sm, raw);
+    n = sum16(n);
+    sm = sum16(sm);
+    const double mean = n > 0.0 ? sm / n : 0.0;
     double m2 = 0.0;
 #pragma unroll
     for (int q = 0; q < RB_MAX; ++q)
@@ -180,10 +305,32 @@ __device__ inline void batch_of_records(const double* rec, int nb, int RS, int D
         const double dm = rm[q] - mean;
         m2 += rs[q] + rn[q] * dm * dm;
       }
+    bn = n;
+    bm = mean;
     bs = sum16(m2);
-  } else {  // many rounds: sum (M2_b + n_b mean_b^2) - n mean^2
-    bs = sum16(raw) - n * mean * mean;
   }
+};
+
+__device__ inline void batch_of_records(const double* rec, int nb, int RS, int D, int O, int k, int j, double& bn,
+                                        double& bm, double& bs) {
+  RecRound rr;
+  if (nb <= 16 * RB_MAX) {
+    rr.load(rec, nb, RS, D, O, k, j, 0);
+    rr.batch(bn, bm, bs);
+    return;
+  }
+  // many rounds: sum (M2_b + n_b mean_b^2) - n mean^2
+  double n = 0.0, sm = 0.0, raw = 0.0;
+  for (int b0 = 0; b0 < nb; b0 += 16 * RB_MAX) {
+    rr.load(rec, nb, RS, D, O, k, j, b0);
+    rr.accumulate(n, sm, raw);
+  }
+  n = sum16(n);
+  sm = sum16(sm);
+  const double mean = n > 0.0 ? sm / n : 0.0;
+  bn = n;
+  bm = mean;
+  bs = sum16(raw) - n * mean * mean;
 }
 
 // Chan merge of (nb, mb, m2b) into (n, M, S); for nb == 1 this is RunningStat.push
@@ -228,11 +375,56 @@ __device__ inline void draw_noise(const RollArgs& a, int e, int64_t row, int t, 
   }
 }
 
+// draw_noise for the fused step kernel, where the four 16-lane rows of a wave hold
+// the same envs: row g draws the Box-Muller pairs c = 4i + g and the rows exchange
+// (a quarter of the Philox / log / sincos sequences).  All lanes active; `valid`
+// guards the injected-noise loads.  `w` = iteration * horizon + t.
+template <int ENV>
+__device__ inline void draw_noise_quad(const RollArgs& a, int e, int64_t row, uint64_t w, int g, bool valid,
+                                       double* zn) {
+  using EC = EnvC<ENV>;
+  constexpr int A = EC::ACT;
+  if (a.b.noise != nullptr) {
+    if (!valid) return;
+    if constexpr (EC::DISCRETE) zn[0] = reinterpret_cast<const double*>(a.b.noise)[row];
+    else
+#pragma unroll
+      for (int q = 0; q < A; ++q) zn[q] = reinterpret_cast<const double*>(a.b.noise)[row * A + q];
+    return;
+  }
+  const uint32_t gid = (uint32_t)(a.d.env_offset + e);
+  if constexpr (EC::DISCRETE) {
+    double u1;
+    philox_uniform2(a.d.seed, 0, gid, w, 0, zn[0], u1);
+  } else {
+    constexpr int P = (A + 1) / 2;
+#pragma unroll
+    for (int i = 0; i < (P + 3) / 4; ++i) {
+      double u0, u1;
+      philox_uniform2(a.d.seed, 0, gid, w, (uint32_t)(4 * i + g), u0, u1);
+      const double rad = sqrt(-2.0 * log(1.0 - u0));
+      double sn, cn, cq[4], sq[4];
+      sincos(2.0 * 3.141592653589793 * u1, &sn, &cn);
+      quads(rad * cn, cq);
+      quads(rad * sn, sq);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 4 * i + q;
+        if (2 * c < A) zn[2 * c] = cq[q];
+        if (2 * c + 1 < A) zn[2 * c + 1] = sq[q];
+      }
+    }
+  }
+}
+
 // sample the action from the head rows z (core.py:261-267; distributions.py:3-13 /
 // core.py:432-435), write act/prob rows, step the env (fp64)
-template <int ENV>
+// QUAD: the four 16-lane rows of the wave hold this env (fused step kernel); every
+// lane steps it (row h = lane >> 4 of the angle functions), lanes with `store` write
+template <int ENV, bool QUAD = false>
 __device__ inline void sample_and_step(const RollArgs& a, int64_t row, const float* z, const float* logstd,
-                                       const double* zn, double* s, double& rew, bool& done) {
+                                       const double* zn, double* s, double& rew, bool& done, bool store = true,
+                                       int h = 0) {
   using EC = EnvC<ENV>;
   constexpr int A = EC::ACT;
   if constexpr (EC::DISCRETE) {
@@ -259,9 +451,11 @@ __device__ inline void sample_and_step(const RollArgs& a, int64_t row, const flo
         found = true;
       }
     }
-    reinterpret_cast<int32_t*>(a.b.act)[row] = act;
+    if (store) {
+      reinterpret_cast<int32_t*>(a.b.act)[row] = act;
 #pragma unroll
-    for (int q = 0; q < A; ++q) a.b.prob[row * A + q] = p[q];
+      for (int q = 0; q < A; ++q) a.b.prob[row * A + q] = p[q];
+    }
     EC::step_disc(s, act, rew, done);
   } else {
     float av[A];
@@ -269,11 +463,14 @@ __device__ inline void sample_and_step(const RollArgs& a, int64_t row, const flo
     for (int q = 0; q < A; ++q) {
       const float sd = expf(logstd[q]);
       av[q] = __fadd_rn(__fmul_rn((float)zn[q], sd), z[q]);
-      reinterpret_cast<float*>(a.b.act)[row * A + q] = av[q];
-      a.b.prob[row * 2 * A + q] = z[q];
-      a.b.prob[row * 2 * A + A + q] = sd;
+      if (store) {
+        reinterpret_cast<float*>(a.b.act)[row * A + q] = av[q];
+        a.b.prob[row * 2 * A + q] = z[q];
+        a.b.prob[row * 2 * A + A + q] = sd;
+      }
     }
-    EC::step_cont(s, av, rew, done);
+    if constexpr (QUAD) EC::step_cont_quad(s, av, rew, done, h);
+    else EC::step_cont(s, av, rew, done);
   }
 }
 
@@ -318,112 +515,142 @@ __global__ __launch_bounds__(RB) void rollout_reset_kernel(RollArgs a) {
   publish_partial(a, vals, nvalid, D, false, a.b.records);
 }
 
+// rollout image: rimage_value (mlp_layout.h) of every element
+__global__ void rollout_pack_kernel(RDims r, MlpDims d, const float* __restrict__ th, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < r.size) out[i] = rimage_value(r, d, th, i);
+}
+
+// One launch = step t of E envs: 4 waves x 16 envs per block, the four 16-lane rows of
+// a wave share the wave's 16 envs (split angle functions / noise / obs columns, the
+// MFMA tiles of forward16).
 template <int ENV>
-__global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, MlpDims md, const float* __restrict__ theta,
-                                                          const float* __restrict__ img, int t) {
+__global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, const float* __restrict__ logstd,
+                                                          const float* __restrict__ rimg, int t) {
   using EC = EnvC<ENV>;
   constexpr int O = EC::OBS, D = O + 1, NS = EC::NS, A = EC::ACT;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
   __shared__ double vals[ENVS_PER_BLOCK * MAXD];
   __shared__ double fmean[MAXD], fden[MAXD];
-  __shared__ float xt[4][32][MAX_IN];
+  __shared__ float xt[4][16][MAX_IN + 1];  // +1: conflict-free column reads
   // diagnostic phase stamps (100 MHz realtime) of block 0 / thread 0 -- never set in production
 #define STAMP(k)                                                                    \
   do {                                                                              \
     if (a.b.stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0)               \
-      a.b.stamps[(int64_t)t * 8 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); \
+      a.b.stamps[(int64_t)t * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
   STAMP(0);
+  if (a.b.stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0)  // shader clock, for the in-kernel GHz
+    a.b.stamps[(int64_t)t * 16 + 14] = (int64_t)__builtin_amdgcn_s_memtime();
   const int E = a.d.n_envs;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
-  const int le = wave * 32 + j;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  const int le = wave * 16 + j;
   const int e = blockIdx.x * ENVS_PER_BLOCK + le;
   const bool valid = e < E;
   const int64_t row = (int64_t)t * E + e;
 
-  // env state loads first: they overlap the image copy and the filter merge below
-  double s[NS];
-#pragma unroll
-  for (int i = 0; i < NS; ++i) s[i] = valid ? a.b.env_state[(int64_t)i * E + e] : 0.0;
-
-  for (int i = threadIdx.x; i < md.fwd_size / 4; i += RB)
-    reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img)[i];
-  STAMP(1);
-
-  // 1. running-stat merge (filters.py:30-31 push, per step over all envs)
+  // 0. every global load of the step up front, in the order they are consumed (the
+  //    vector-memory counter retires in order): RNG step, filter records, env state,
+  //    policy weights -- their latency hides under the noise draw
+  const uint64_t w = (uint64_t)(*a.b.iteration) * (uint64_t)a.d.horizon + (uint64_t)t;
   const double* fs_in = a.b.filter_state + (t & 1) * a.FS;
   double* fs_out = a.b.filter_state + ((t + 1) & 1) * a.FS;
   const double* rec_in = a.b.records + (int64_t)(t & 1) * a.nb * a.RS;
   double* rec_out = a.b.records + (int64_t)((t + 1) & 1) * a.nb * a.RS;
-  if ((int)(threadIdx.x >> 4) < D) {
-    const int k = threadIdx.x >> 4, jj = threadIdx.x & 15;
-    const bool isr = (k == O);
-    double n = fs_in[isr ? 1 : 0], M = fs_in[2 + k], S = fs_in[2 + D + k];
-    // combine the block partials into one batch, then one Chan merge into the stat
+  const int k = threadIdx.x >> 4, jj = threadIdx.x & 15;
+  const bool kcol = k < D, isr = (k == O), one_round = a.nb <= 16 * RB_MAX;
+  RecRound rr;
+  double fn = 0.0, fM = 0.0, fS = 0.0;
+  if (kcol) {
+    if (one_round) rr.load(rec_in, a.nb, a.RS, D, O, k, jj, 0);
+    fn = fs_in[isr ? 1 : 0];
+    fM = fs_in[2 + k];
+    fS = fs_in[2 + D + k];
+  }
+  double s[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) s[i] = valid ? a.b.env_state[(int64_t)i * E + e] : 0.0;
+  RWeights<O, A> wt;
+  wt.load(rimg, lane);
+  float lsd[A];
+#pragma unroll
+  for (int q = 0; q < A; ++q) lsd[q] = EC::DISCRETE ? 0.f : logstd[q];
+
+  // 1. sampling noise (independent of the policy output)
+  double zn[A + 1] = {};
+  draw_noise_quad<ENV>(a, e, row, w, g, valid, zn);
+  STAMP(1);
+
+  // 2. running-stat merge (filters.py:30-31 push, per step over all envs): the block
+  //    partials -> one batch -> one Chan merge; every block derives the same state
+  if (kcol) {
     double bn, bm, bs;
-    batch_of_records(rec_in, a.nb, a.RS, D, O, k, jj, bn, bm, bs);
-    chan_merge(n, M, S, bn, bm, bs);
+    if (one_round) rr.batch(bn, bm, bs);
+    else batch_of_records(rec_in, a.nb, a.RS, D, O, k, jj, bn, bm, bs);
+    chan_merge(fn, fM, fS, bn, bm, bs);
     if (jj == 0 && blockIdx.x == 0) {
-      if (k == 0) fs_out[0] = n;
-      if (isr) fs_out[1] = n;
-      fs_out[2 + k] = M;
-      fs_out[2 + D + k] = S;
+      if (k == 0) fs_out[0] = fn;
+      if (isr) fs_out[1] = fn;
+      fs_out[2 + k] = fM;
+      fs_out[2 + D + k] = fS;
     }
     if (!isr && jj == 0) {
-      const double var = n > 1.0 ? S / (n - 1.0) : M * M;  // running_stat.py:27
-      fmean[k] = M;
+      const double var = fn > 1.0 ? fS / (fn - 1.0) : fM * fM;  // running_stat.py:27
+      fmean[k] = fM;
       fden[k] = sqrt(var) + 1e-8;
     }
   }
   __syncthreads();
   STAMP(2);
 
-  // 2. filtered observation (core.py:191-192)
+  // 3. filtered observation (core.py:191-192); row g takes columns 4i + g
   {
     double o[O];
     EC::obs(s, o);
 #pragma unroll
-    for (int k = 0; k < O; ++k) {
-      double v = o[k];
+    for (int i = 0; i < (O + 3) / 4; ++i) {
+      const int kc = 4 * i + g;
+      double v = o[4 * i];
+#pragma unroll
+      for (int q = 1; q < 4; ++q)
+        if (4 * i + q < O && g == q) v = o[4 * i + q < O ? 4 * i + q : O - 1];
       if (a.d.filter) {
-        v = v - fmean[k];
-        v = v / fden[k];
+        const int kk = kc < O ? kc : O - 1;
+        v = v - fmean[kk];
+        v = v / fden[kk];
         v = v < -5.0 ? -5.0 : (v > 5.0 ? 5.0 : v);
       }
       const float vf = (float)v;
-      if (valid && h == 0) a.b.obs[row * O + k] = vf;
-      xt[wave][j][k] = vf;
+      if (kc < O) {
+        if (valid) a.b.obs[row * O + kc] = vf;
+        xt[wave][j][kc] = vf;
+      }
     }
   }
   WAVE_LDS_ORDER();
   STAMP(3);
 
-  // 3. policy forward
+  // 4. policy forward (MFMA, 16 envs per wave)
   struct XL {
     const float* p;
     bool valid;
-    __device__ inline float operator()(int k) const { return (valid && k < O) ? p[k] : 0.f; }
+    __device__ inline float operator()(int c) const { return (valid && c < O) ? p[c] : 0.f; }
   } xl{&xt[wave][j][0], valid};
-  // sampling noise does not depend on the policy output: draw it first so its VALU
-  // work overlaps the MFMA chain of the forward
-  double zn[A + 1];
-  if (valid) draw_noise<ENV>(a, e, row, t, zn);
+  float z[A];
+  forward16<O, A>(wt, xl, lane, z);
+  STAMP(4);
 
-  float z[MAX_OUT];
-  forward_head_lowreg(lds, md, xl, lane, z);
-
+  // 5. sample + env step: every row steps the env (split angle functions), row 0 stores
   double rew = 0.0;
-  if (valid && h == 0) {
-    STAMP(4);
-    bool done = false;
-    sample_and_step<ENV>(a, row, z, theta + md.tls, zn, s, rew, done);
-    STAMP(5);
+  bool done = false;
+  sample_and_step<ENV, true>(a, row, z, lsd, zn, s, rew, done, valid && g == 0, g);
+  STAMP(5);
+  if (valid && g == 0) {
     finish_env_step<ENV>(a, e, row, t, s, rew, done);
     // 6. raw next observation + reward into the block partial
     double o[O];
     EC::obs(s, o);
 #pragma unroll
-    for (int k = 0; k < O; ++k) vals[le * D + k] = o[k];
+    for (int c = 0; c < O; ++c) vals[le * D + c] = o[c];
     vals[le * D + O] = rew;
   }
   __syncthreads();
@@ -431,9 +658,10 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, MlpDims md
   const int nvalid = min(ENVS_PER_BLOCK, E - (int)blockIdx.x * ENVS_PER_BLOCK);
   publish_partial(a, vals, nvalid, D, true, rec_out);
   STAMP(7);
+  if (a.b.stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+    a.b.stamps[(int64_t)t * 16 + 15] = (int64_t)__builtin_amdgcn_s_memtime();
 #undef STAMP
 }
-
 
 // ------------------------------------------------------------------ layered-policy rollout
 // For policies the fused step kernel does not cover (wide nets, Humanoid's 376-d obs),
@@ -513,7 +741,9 @@ __global__ __launch_bounds__(RB) void lrollout_obs_kernel(RollArgs a, int t) {
   using EC = EnvC<ENV>;
   constexpr int O = EC::OBS, D = O + 1;
   __shared__ double fmean[LCOLS], fden[LCOLS];
-  __shared__ float tile[LCOLS * 129];
+  constexpr int G = RB / ENVS_PER_BLOCK, CPT = LCOLS / G;  // thread groups over columns, columns per thread
+  static_assert(RB % ENVS_PER_BLOCK == 0 && LCOLS % G == 0, "tile mapping");
+  __shared__ float tile[LCOLS * (ENVS_PER_BLOCK + 1)];
   const int E = a.d.n_envs;
   const double* fs_in = a.b.filter_state + (t & 1) * a.FS;
   double* fs_out = a.b.filter_state + ((t + 1) & 1) * a.FS;
@@ -559,34 +789,34 @@ __global__ __launch_bounds__(RB) void lrollout_obs_kernel(RollArgs a, int t) {
   const int nvalid = min(ENVS_PER_BLOCK, E - e0);
   const int64_t row0 = (int64_t)t * E + e0;
   {
-    const int el = threadIdx.x & 127, kb = threadIdx.x >> 7;
-    double v[16];
+    const int el = threadIdx.x % ENVS_PER_BLOCK, kb = threadIdx.x / ENVS_PER_BLOCK;
+    double v[CPT];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int k = kbase + kb + 2 * q;
+    for (int q = 0; q < CPT; ++q) {
+      const int k = kbase + kb + G * q;
       v[q] = (k < O && el < nvalid) ? a.b.raw_obs[(int64_t)k * E + e0 + el] : 0.0;
     }
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int kl = kb + 2 * q;
+    for (int q = 0; q < CPT; ++q) {
+      const int kl = kb + G * q;
       double x = v[q];
       if (a.d.filter) {
         x = x - fmean[kl];
         x = x / fden[kl];
         x = x < -5.0 ? -5.0 : (x > 5.0 ? 5.0 : x);
       }
-      tile[kl * 129 + el] = (float)x;
+      tile[kl * (ENVS_PER_BLOCK + 1) + el] = (float)x;
     }
   }
   __syncthreads();
   {
-    const int el = threadIdx.x >> 1, half = threadIdx.x & 1;
+    const int el = threadIdx.x / G, part = threadIdx.x % G;
     if (el < nvalid) {
       float* dst = a.b.obs + (row0 + el) * O;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int k = kbase + half * 16 + q;
-        if (k < O) dst[k] = tile[(half * 16 + q) * 129 + el];
+      for (int q = 0; q < CPT; ++q) {
+        const int k = kbase + part * CPT + q;
+        if (k < O) dst[k] = tile[(part * CPT + q) * (ENVS_PER_BLOCK + 1) + el];
       }
     }
   }
@@ -760,28 +990,52 @@ int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, cons
   return hip_check(hipGetLastError(), "mrl_rollout_act");
 }
 
-int mrl_rollout_step(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta, const float* image,
-                     const mrl_rollout_bufs* b, int32_t t, void* stream) {
-  int rc = check_roll(d, b);
-  if (rc) return rc;
-  if (!pol || !theta || !image) return fail(E_ARG, "null policy");
-  if (d->env_id == MRL_ENV_HUMANOID) return fail(E_UNSUPPORTED, "Humanoid runs on the layered rollout");
-  if (!b->obs || !b->act || !b->prob || !b->rew || !b->flags || !b->ep_t) return fail(E_ARG, "null trajectory buffer");
+static int check_fused_policy(const mrl_rollout_desc* d, const mrl_mlp_desc* pol) {
   EnvInfo ei = env_info(d->env_id);
   const bool gauss = pol->head == MRL_HEAD_GAUSS;
   if (pol->n_in != ei.obs || pol->n_out != ei.act || gauss == (bool)ei.discrete || pol->n_hidden != HID ||
       pol->n_layers != 2)
     return fail(E_ARG, "policy shape does not match the env");
+  return OK;
+}
+
+int64_t mrl_rollout_image_floats(const mrl_mlp_desc* pol) {
+  if (!pol || pol->n_in <= 0 || pol->n_in > MAX_IN) return -1;
+  return rollout_dims(pol->n_in).size;
+}
+
+int mrl_rollout_pack(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta, float* rimage,
+                     void* stream) {
+  if (!d || !pol || !theta || !rimage) return fail(E_ARG, "null pointer");
+  if (d->env_id == MRL_ENV_HUMANOID) return fail(E_UNSUPPORTED, "Humanoid runs on the layered rollout");
+  int rc = check_fused_policy(d, pol);
+  if (rc) return rc;
+  const RDims r = rollout_dims(pol->n_in);
+  const MlpDims md = mlp_dims(pol->n_in, pol->n_out, pol->head == MRL_HEAD_GAUSS);
+  hipLaunchKernelGGL(rollout_pack_kernel, dim3((r.size + 255) / 256), dim3(256), 0, (hipStream_t)stream, r, md, theta,
+                     rimage);
+  return hip_check(hipGetLastError(), "mrl_rollout_pack");
+}
+
+int mrl_rollout_step(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta, const float* rimage,
+                     const mrl_rollout_bufs* b, int32_t t, void* stream) {
+  int rc = check_roll(d, b);
+  if (rc) return rc;
+  if (!pol || !theta || !rimage) return fail(E_ARG, "null policy");
+  if (d->env_id == MRL_ENV_HUMANOID) return fail(E_UNSUPPORTED, "Humanoid runs on the layered rollout");
+  if (!b->obs || !b->act || !b->prob || !b->rew || !b->flags || !b->ep_t) return fail(E_ARG, "null trajectory buffer");
+  rc = check_fused_policy(d, pol);
+  if (rc) return rc;
   if (t < 0 || t >= d->horizon) return fail(E_ARG, "t out of range");
   RollArgs a = make_args(d, b);
-  MlpDims md = mlp_dims(pol->n_in, pol->n_out, gauss);
-  size_t shm = (size_t)md.fwd_size * 4;
+  const MlpDims md = mlp_dims(pol->n_in, pol->n_out, pol->head == MRL_HEAD_GAUSS);
+  const float* logstd = pol->head == MRL_HEAD_GAUSS ? theta + md.tls : nullptr;
   if (d->env_id == MRL_ENV_CARTPOLE)
-    hipLaunchKernelGGL(rollout_step_kernel<MRL_ENV_CARTPOLE>, dim3(a.nb), dim3(RB), shm, (hipStream_t)stream, a, md,
-                       theta, image, t);
+    hipLaunchKernelGGL(rollout_step_kernel<MRL_ENV_CARTPOLE>, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a, logstd,
+                       rimage, t);
   else
-    hipLaunchKernelGGL(rollout_step_kernel<MRL_ENV_HOPPER>, dim3(a.nb), dim3(RB), shm, (hipStream_t)stream, a, md,
-                       theta, image, t);
+    hipLaunchKernelGGL(rollout_step_kernel<MRL_ENV_HOPPER>, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a, logstd,
+                       rimage, t);
   return hip_check(hipGetLastError(), "mrl_rollout_step");
 }
 
