@@ -256,7 +256,8 @@ typedef struct {
   float* rew;              /* [T*E] raw rewards (core.py:198)                     */
   uint8_t* flags;          /* [T*E] bit0 last-of-episode, bit1 terminated         */
   int32_t* ep_t;           /* [T*E] step index of the row inside its episode      */
-  const void* noise;       /* optional injected noise [T*E] u | [T*E, d] z        */
+  const void* noise;       /* sampling-noise rows (double) [T*E] u | [T*E, d] z: from
+                              mrl_rollout_noise, or injected (parity tests)       */
   int64_t* stamps;         /* optional diagnostic: [T, 16] s_memrealtime of block 0 phases (NULL in production) */
   double* raw_obs;         /* layered rollout: [obs_dim+1, E] raw next obs + reward (SoA) */
 } mrl_rollout_bufs;
@@ -265,6 +266,11 @@ int64_t mrl_env_state_doubles(int32_t env_id);
 int64_t mrl_filter_doubles(int32_t env_id);
 int64_t mrl_record_doubles(int32_t env_id);
 int64_t mrl_rollout_blocks(int32_t n_envs);
+/* the Philox sampling noise of the CURRENT iteration (device counter b->iteration):
+ * out[T*E] uniforms (Categorical) | out[T*E, d] normals (DiagGauss), row = t*E + e --
+ * drawn once per iteration, before the steps, and passed as b->noise */
+int64_t mrl_rollout_noise_doubles(const mrl_rollout_desc* d);
+int mrl_rollout_noise(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, double* out, void* stream);
 /* reset every env (start of iteration, core.py:186) and publish obs_0 partials */
 int mrl_rollout_reset(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void* stream);
 /* policy image of the fused step kernel (16 envs per wave on 16x16x4 MFMA tiles,

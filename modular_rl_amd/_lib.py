@@ -97,6 +97,8 @@ SIGNATURES = {
     "mrl_record_doubles": (i64, [i32]),
     "mrl_rollout_blocks": (i64, [i32]),
     "mrl_rollout_reset": (i32, [vp, vp, vp]),
+    "mrl_rollout_noise_doubles": (i64, [vp]),
+    "mrl_rollout_noise": (i32, [vp, vp, vp, vp]),
     "mrl_rollout_image_floats": (i64, [vp]),
     "mrl_rollout_pack": (i32, [vp, vp, vp, vp, vp]),
     "mrl_rollout_step": (i32, [vp, vp, vp, vp, vp, i32, vp]),

@@ -159,7 +159,8 @@ class Collector:
         self.rew = torch.zeros(self.N, dtype=torch.float32, device=self.dev)
         self.flags = torch.zeros(self.N, dtype=torch.uint8, device=self.dev)
         self.ep_t = torch.zeros(self.N, dtype=torch.int32, device=self.dev)
-        self.noise = None
+        self.noise = None  # injected noise rows (parity mode); None: Philox rows drawn per iteration
+        self._noise_rows = torch.zeros(int(lib.mrl_rollout_noise_doubles(ctypes.byref(self.desc))), **f64)
         self.stamps = None  # diagnostic [T, 16] int64 phase stamps (see rollout.hip); None in production
         net = policy.net
         self.layered = bool(getattr(net, "layered", False))
@@ -184,12 +185,15 @@ class Collector:
     def _bufs(self):
         return _lib.RolloutBufs(ptr(self.env_state), ptr(self.env_int), ptr(self.filter_state), ptr(self.records),
                                 ptr(self.iteration), ptr(self.obs), ptr(self.act), ptr(self.prob), ptr(self.rew),
-                                ptr(self.flags), ptr(self.ep_t), ptr(self.noise), ptr(self.stamps),
+                                ptr(self.flags), ptr(self.ep_t),
+                                ptr(self.noise if self.noise is not None else self._noise_rows), ptr(self.stamps),
                                 ptr(self.raw_obs))
 
     def _launch_all(self):
         bufs = self._bufs()
         net = self.policy.net
+        if self.noise is None:  # this iteration's sampling noise, one parallel draw
+            call("mrl_rollout_noise", ctypes.byref(self.desc), ctypes.byref(bufs), ptr(self._noise_rows), stream())
         if self.layered:
             return self._launch_all_layered(bufs, net)
         call("mrl_rollout_pack", ctypes.byref(self.desc), ctypes.byref(net.desc), ptr(net.theta), ptr(self._rimage),

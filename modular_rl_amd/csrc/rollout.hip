@@ -176,7 +176,7 @@ __device__ inline void tanh4(f32x4& a) {
 
 // head rows z[o] of the wave's 16 envs (every lane of an env's column ends with all A)
 template <int O, int A, class XL>
-__device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane, float* z) {
+__device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane, float* z, int64_t* st = nullptr) {
   constexpr RDims R = RWeights<O, A>::R;
   const int g = lane >> 4;
   float xb[R.KS0p];
@@ -193,6 +193,7 @@ __device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane
   for (int ks = 0; ks < R.KS0; ++ks)
 #pragma unroll
     for (int mo = 0; mo < 4; ++mo) h1[mo] = MFMA16(f4get(w.a0[mo][ks >> 2], ks & 3), xb[ks], h1[mo]);
+  if (st != nullptr) st[9] = (int64_t)__builtin_amdgcn_s_memrealtime();
   // layer 1: input tile mt needs only tanh(h1[mt]), so later tiles' tanh overlaps the
   // MFMAs of earlier ones
 #pragma unroll
@@ -204,6 +205,7 @@ __device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane
       for (int mo = 0; mo < 4; ++mo) h2[mo] = MFMA16(f4get(w.a1[mo][mt], q), h1[mt][q], h2[mo]);
   }
   // head on VALU: 16 units per lane, then the four rows of the column
+  if (st != nullptr) st[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) tanh4(h2[mt]);
 #pragma unroll
@@ -345,75 +347,43 @@ __device__ inline void chan_merge(double& n, double& M, double& S, double nb, do
   n = nn;
 }
 
-// sampling noise of env e at step t: Philox (gid, iteration*T + t) on domain 0, or the
-// injected noise rows.  zn[0] = uniform (Categorical) | zn[q] = standard normals (Gauss)
+// Sampling noise of env e at step t is Philox (gid, iteration*T + t) on domain 0:
+// Categorical u = first uniform of call 0, Gauss z[2c], z[2c+1] = Box-Muller of call
+// c.  A whole iteration's rows are drawn up front by noise_fill_kernel (one thread per
+// (row, pair): the transcendental work leaves the step kernels' latency chain), or
+// injected by the caller; the step kernels only load zn rows.
 template <int ENV>
-__device__ inline void draw_noise(const RollArgs& a, int e, int64_t row, int t, double* zn) {
+__device__ inline void load_noise(const RollArgs& a, int64_t row, double* zn) {
   using EC = EnvC<ENV>;
-  constexpr int A = EC::ACT;
-  const uint32_t gid = (uint32_t)(a.d.env_offset + e);
-  const uint64_t w = (uint64_t)(*a.b.iteration) * (uint64_t)a.d.horizon + (uint64_t)t;
-  if (a.b.noise != nullptr) {
-    if constexpr (EC::DISCRETE) zn[0] = reinterpret_cast<const double*>(a.b.noise)[row];
-    else
+  const double* nz = reinterpret_cast<const double*>(a.b.noise);
+  if constexpr (EC::DISCRETE) zn[0] = nz[row];
+  else
 #pragma unroll
-      for (int q = 0; q < A; ++q) zn[q] = reinterpret_cast<const double*>(a.b.noise)[row * A + q];
-  } else if constexpr (EC::DISCRETE) {
-    double u1;
-    philox_uniform2(a.d.seed, 0, gid, w, 0, zn[0], u1);
-  } else {
-#pragma unroll
-    for (int c = 0; c < (A + 1) / 2; ++c) {
-      double u0, u1;
-      philox_uniform2(a.d.seed, 0, gid, w, (uint32_t)c, u0, u1);
-      const double rad = sqrt(-2.0 * log(1.0 - u0));
-      double sn, cn;
-      sincos(2.0 * 3.141592653589793 * u1, &sn, &cn);
-      zn[2 * c] = rad * cn;
-      if (2 * c + 1 < A) zn[2 * c + 1] = rad * sn;
-    }
-  }
+    for (int q = 0; q < EC::ACT; ++q) zn[q] = nz[row * EC::ACT + q];
 }
 
-// draw_noise for the fused step kernel, where the four 16-lane rows of a wave hold
-// the same envs: row g draws the Box-Muller pairs c = 4i + g and the rows exchange
-// (a quarter of the Philox / log / sincos sequences).  All lanes active; `valid`
-// guards the injected-noise loads.  `w` = iteration * horizon + t.
 template <int ENV>
-__device__ inline void draw_noise_quad(const RollArgs& a, int e, int64_t row, uint64_t w, int g, bool valid,
-                                       double* zn) {
+__global__ void noise_fill_kernel(RollArgs a, double* __restrict__ out) {
   using EC = EnvC<ENV>;
-  constexpr int A = EC::ACT;
-  if (a.b.noise != nullptr) {
-    if (!valid) return;
-    if constexpr (EC::DISCRETE) zn[0] = reinterpret_cast<const double*>(a.b.noise)[row];
-    else
-#pragma unroll
-      for (int q = 0; q < A; ++q) zn[q] = reinterpret_cast<const double*>(a.b.noise)[row * A + q];
-    return;
-  }
+  constexpr int A = EC::ACT, P = EC::DISCRETE ? 1 : (A + 1) / 2;
+  const int64_t E = a.d.n_envs;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)a.d.horizon * E * P) return;
+  const int c = (int)(i % P);
+  const int64_t row = i / P;
+  const int t = (int)(row / E), e = (int)(row % E);
   const uint32_t gid = (uint32_t)(a.d.env_offset + e);
+  const uint64_t w = (uint64_t)(*a.b.iteration) * (uint64_t)a.d.horizon + (uint64_t)t;
+  double u0, u1;
+  philox_uniform2(a.d.seed, 0, gid, w, (uint32_t)c, u0, u1);
   if constexpr (EC::DISCRETE) {
-    double u1;
-    philox_uniform2(a.d.seed, 0, gid, w, 0, zn[0], u1);
+    out[row] = u0;
   } else {
-    constexpr int P = (A + 1) / 2;
-#pragma unroll
-    for (int i = 0; i < (P + 3) / 4; ++i) {
-      double u0, u1;
-      philox_uniform2(a.d.seed, 0, gid, w, (uint32_t)(4 * i + g), u0, u1);
-      const double rad = sqrt(-2.0 * log(1.0 - u0));
-      double sn, cn, cq[4], sq[4];
-      sincos(2.0 * 3.141592653589793 * u1, &sn, &cn);
-      quads(rad * cn, cq);
-      quads(rad * sn, sq);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = 4 * i + q;
-        if (2 * c < A) zn[2 * c] = cq[q];
-        if (2 * c + 1 < A) zn[2 * c + 1] = sq[q];
-      }
-    }
+    const double rad = sqrt(-2.0 * log(1.0 - u0));
+    double sn, cn;
+    sincos(2.0 * 3.141592653589793 * u1, &sn, &cn);
+    out[row * A + 2 * c] = rad * cn;
+    if (2 * c + 1 < A) out[row * A + 2 * c + 1] = rad * sn;
   }
 }
 
@@ -549,9 +519,8 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, const floa
   const int64_t row = (int64_t)t * E + e;
 
   // 0. every global load of the step up front, in the order they are consumed (the
-  //    vector-memory counter retires in order): RNG step, filter records, env state,
-  //    policy weights -- their latency hides under the noise draw
-  const uint64_t w = (uint64_t)(*a.b.iteration) * (uint64_t)a.d.horizon + (uint64_t)t;
+  //    vector-memory counter retires in order): filter records, env state, noise
+  //    rows, policy weights
   const double* fs_in = a.b.filter_state + (t & 1) * a.FS;
   double* fs_out = a.b.filter_state + ((t + 1) & 1) * a.FS;
   const double* rec_in = a.b.records + (int64_t)(t & 1) * a.nb * a.RS;
@@ -569,15 +538,13 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, const floa
   double s[NS];
 #pragma unroll
   for (int i = 0; i < NS; ++i) s[i] = valid ? a.b.env_state[(int64_t)i * E + e] : 0.0;
+  double zn[A + 1] = {};
+  if (valid) load_noise<ENV>(a, row, zn);
   RWeights<O, A> wt;
   wt.load(rimg, lane);
   float lsd[A];
 #pragma unroll
   for (int q = 0; q < A; ++q) lsd[q] = EC::DISCRETE ? 0.f : logstd[q];
-
-  // 1. sampling noise (independent of the policy output)
-  double zn[A + 1] = {};
-  draw_noise_quad<ENV>(a, e, row, w, g, valid, zn);
   STAMP(1);
 
   // 2. running-stat merge (filters.py:30-31 push, per step over all envs): the block
@@ -636,7 +603,8 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, const floa
     __device__ inline float operator()(int c) const { return (valid && c < O) ? p[c] : 0.f; }
   } xl{&xt[wave][j][0], valid};
   float z[A];
-  forward16<O, A>(wt, xl, lane, z);
+  forward16<O, A>(wt, xl, lane, z,
+                  (a.b.stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0) ? a.b.stamps + t * 16 : nullptr);
   STAMP(4);
 
   // 5. sample + env step: every row steps the env (split angle functions), row 0 stores
@@ -839,7 +807,7 @@ __global__ __launch_bounds__(RB) void lrollout_act_kernel(RollArgs a, const floa
 #pragma unroll
   for (int q = 0; q < A; ++q) z[q] = zrows[(int64_t)e * A + q];
   double zn[A + 1];
-  draw_noise<ENV>(a, e, row, t, zn);
+  load_noise<ENV>(a, row, zn);
   double rew = 0.0;
   bool done = false;
   sample_and_step<ENV>(a, row, z, logstd, zn, s, rew, done);
@@ -914,12 +882,36 @@ static RollArgs make_args(const mrl_rollout_desc* d, const mrl_rollout_bufs* b) 
   return a;
 }
 
+#define MRL_DISPATCH_ENV(id, KERNEL, ...)                                                    \
+  do {                                                                                      \
+    if ((id) == MRL_ENV_CARTPOLE) hipLaunchKernelGGL(KERNEL<MRL_ENV_CARTPOLE>, __VA_ARGS__); \
+    else if ((id) == MRL_ENV_HOPPER) hipLaunchKernelGGL(KERNEL<MRL_ENV_HOPPER>, __VA_ARGS__); \
+    else hipLaunchKernelGGL(KERNEL<MRL_ENV_HUMANOID>, __VA_ARGS__);                         \
+  } while (0)
+
 extern "C" {
 
 int64_t mrl_env_state_doubles(int32_t env_id) { return env_info(env_id).ns; }
 int64_t mrl_filter_doubles(int32_t env_id) { return filt_doubles(env_info(env_id).obs); }
 int64_t mrl_record_doubles(int32_t env_id) { return filt_doubles(env_info(env_id).obs); }
 int64_t mrl_rollout_blocks(int32_t n_envs) { return (n_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK; }
+int64_t mrl_rollout_noise_doubles(const mrl_rollout_desc* d) {
+  if (!d || d->n_envs <= 0 || d->horizon <= 0) return -1;
+  const EnvInfo ei = env_info(d->env_id);
+  return (int64_t)d->horizon * d->n_envs * (ei.discrete ? 1 : ei.act);
+}
+
+int mrl_rollout_noise(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, double* out, void* stream) {
+  int rc = check_roll(d, b);
+  if (rc) return rc;
+  if (!out) return fail(E_ARG, "null noise rows");
+  RollArgs a = make_args(d, b);
+  const EnvInfo ei = env_info(d->env_id);
+  const int64_t n = (int64_t)d->horizon * d->n_envs * (ei.discrete ? 1 : (ei.act + 1) / 2);
+  MRL_DISPATCH_ENV(d->env_id, noise_fill_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                   (hipStream_t)stream, a, out);
+  return hip_check(hipGetLastError(), "mrl_rollout_noise");
+}
 
 int mrl_rollout_reset(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void* stream) {
   int rc = check_roll(d, b);
@@ -933,12 +925,6 @@ int mrl_rollout_reset(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void
   return hip_check(hipGetLastError(), "mrl_rollout_reset");
 }
 
-#define MRL_DISPATCH_ENV(id, KERNEL, ...)                                                    \
-  do {                                                                                      \
-    if ((id) == MRL_ENV_CARTPOLE) hipLaunchKernelGGL(KERNEL<MRL_ENV_CARTPOLE>, __VA_ARGS__); \
-    else if ((id) == MRL_ENV_HOPPER) hipLaunchKernelGGL(KERNEL<MRL_ENV_HOPPER>, __VA_ARGS__); \
-    else hipLaunchKernelGGL(KERNEL<MRL_ENV_HUMANOID>, __VA_ARGS__);                         \
-  } while (0)
 
 static int check_rows(const mrl_rollout_desc* d, const mrl_rollout_bufs* b) {
   int rc = check_roll(d, b);
@@ -976,6 +962,7 @@ int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, cons
   int rc = check_rows(d, b);
   if (rc) return rc;
   if (!b->act || !b->prob || !b->rew || !b->flags || !b->ep_t || !z) return fail(E_ARG, "null trajectory buffer");
+  if (!b->noise) return fail(E_ARG, "bufs.noise: sampling-noise rows (mrl_rollout_noise or injected) required");
   EnvInfo ei = env_info(d->env_id);
   const bool gauss = head == MRL_HEAD_GAUSS;
   if (n_out != ei.act || gauss == (bool)ei.discrete || (!gauss && head != MRL_HEAD_SOFTMAX))
@@ -1024,6 +1011,7 @@ int mrl_rollout_step(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const f
   if (!pol || !theta || !rimage) return fail(E_ARG, "null policy");
   if (d->env_id == MRL_ENV_HUMANOID) return fail(E_UNSUPPORTED, "Humanoid runs on the layered rollout");
   if (!b->obs || !b->act || !b->prob || !b->rew || !b->flags || !b->ep_t) return fail(E_ARG, "null trajectory buffer");
+  if (!b->noise) return fail(E_ARG, "bufs.noise: sampling-noise rows (mrl_rollout_noise or injected) required");
   rc = check_fused_policy(d, pol);
   if (rc) return rc;
   if (t < 0 || t >= d->horizon) return fail(E_ARG, "t out of range");

@@ -1,8 +1,8 @@
 """Diagnostic: per-phase s_memrealtime stamps of one rollout_step launch (block 0).
 
-Phases (rollout.hip STAMP ids in time order): 0 start | 1 loads issued + noise | 2 filter
-merge | 3 filtered obs | 4 forward | 5 sample+env step | 6 finish+obs+sync | 7 publish
-partial.
+Phases (rollout.hip STAMP ids in time order): 0 start | 1 loads issued | 2 filter merge |
+3 filtered obs | 9 forward layer 0 | 10 layer 1 | 4 head | 5 sample+env step |
+6 finish+obs+sync | 7 publish partial.
 """
 import sys
 
@@ -13,8 +13,8 @@ sys.path.insert(0, '.')
 from modular_rl_amd.agentzoo import TrpoAgent  # noqa: E402
 from modular_rl_amd.envs import make  # noqa: E402
 
-ORDER = [0, 1, 2, 3, 4, 5, 6, 7]
-NAMES = ["loads+noise", "filter", "obs", "forward", "step", "finish", "publish"]
+ORDER = [0, 1, 2, 3, 9, 10, 4, 5, 6, 7]
+NAMES = ["issue", "filter", "obs", "fwd-l0", "fwd-l1", "head", "step", "finish", "publish"]
 T = 256
 for env_id in ["Hopper-v2", "CartPole-v0"]:
     env = make(env_id)
