@@ -194,30 +194,40 @@ __device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane
 #pragma unroll
     for (int mo = 0; mo < 4; ++mo) h1[mo] = MFMA16(f4get(w.a0[mo][ks >> 2], ks & 3), xb[ks], h1[mo]);
   if (st != nullptr) st[9] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  // layer 1: input tile mt needs only tanh(h1[mt]), so later tiles' tanh overlaps the
-  // MFMAs of earlier ones
+  // layer 1: input tile mt needs only tanh(h1[mt]): the tanh of tile mt+1 issues
+  // under the MFMAs of tile mt
+  tanh4(h1[0]);
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    tanh4(h1[mt]);
+  for (int mt = 0; mt < 3; ++mt) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int mo = 0; mo < 4; ++mo) h2[mo] = MFMA16(f4get(w.a1[mo][mt], q), h1[mt][q], h2[mo]);
+    tanh4(h1[mt + 1]);
   }
-  // head on VALU: 16 units per lane, then the four rows of the column
   if (st != nullptr) st[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  // last input tile output-tile major: tanh + head of output tile mo issue under the
+  // MFMAs of tile mo+1.  Head on VALU: 16 units per lane, then the column's 4 rows.
+  float acc[A];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) tanh4(h2[mt]);
+  for (int o = 0; o < A; ++o) acc[o] = 0.f;
+  auto head_tile = [&](int mo) {
+    tanh4(h2[mo]);
 #pragma unroll
-  for (int o = 0; o < A; ++o) {
-    float acc = 0.f;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const float4 hv = w.hv[o][mt];
-      acc += hv.x * h2[mt][0] + hv.y * h2[mt][1] + hv.z * h2[mt][2] + hv.w * h2[mt][3];
+    for (int o = 0; o < A; ++o) {
+      const float4 hv = w.hv[o][mo];
+      acc[o] += hv.x * h2[mo][0] + hv.y * h2[mo][1] + hv.z * h2[mo][2] + hv.w * h2[mo][3];
     }
-    z[o] = quad_sum(acc) + w.hb[o];
+  };
+#pragma unroll
+  for (int mo = 0; mo < 4; ++mo) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) h2[mo] = MFMA16(f4get(w.a1[mo][3], q), h1[3][q], h2[mo]);
+    if (mo > 0) head_tile(mo - 1);
   }
+  head_tile(3);
+#pragma unroll
+  for (int o = 0; o < A; ++o) z[o] = quad_sum(acc[o]) + w.hb[o];
 }
 
 template <int ENV>
@@ -233,10 +243,21 @@ __device__ inline void reset_env(const RollArgs& a, int e, double* s) {
   a.b.env_int[e] = 0;
 }
 
-// sum over the 16 lanes of an aligned 16-lane group (fixed butterfly order)
+// sum over the 16 lanes of an aligned 16-lane row by DPP (no LDS round trips): lane
+// pairs i^1, i^2 (quad_perm), then i <-> 7-i (row_half_mirror), i <-> 15-i (row_mirror);
+// every add is commutative in its pair, so all 16 lanes end with the same bits
+template <int CTRL>
+__device__ inline double dpp_d(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 __device__ inline double sum16(double v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);  // row_half_mirror
+  v += dpp_d<0x140>(v);  // row_mirror
   return v;
 }
 
