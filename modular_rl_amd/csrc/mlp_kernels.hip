@@ -162,34 +162,52 @@ struct VjpIn {
   float gs[MAX_OUT];          // summed head columns (DiagGauss logstd), lane half 0 only
 };
 
+// Branch-free prefetch: row indices are clamped to the batch and columns to the row
+// width, so every load is unconditional straight-line code; what must read as zero
+// (head-gradient entries of rows past n, of outputs past A, the logstd sums off lane
+// half 0) is masked when the tile USES the values (a select at load time would force
+// the wait that the prefetch exists to avoid).  The clamped gW0 operands of rows past
+// n multiply head-gradient rows that are exactly zero; those of columns past the
+// input width land in gW0 rows that are never stored.
 template <bool CACHED>
 __device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn<CACHED>& in) {
   const int h = lane >> 5, j = lane & 31;
-  const int64_t row0 = tile * 32, row = row0 + j;
-  const bool valid = row < a.n;
-  XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
+  const int64_t row0 = tile * 32, row = row0 + j, last = a.n - 1;
   if constexpr (CACHED) {
     const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
 #pragma unroll
     for (int q = 0; q < 4; ++q) cache_load(ct, lane, q, in.act[q]);
   } else {
+    XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, row < a.n};
 #pragma unroll
     for (int s = 0; s < 16; ++s) in.x0[s] = (s < a.d.KS0p) ? xl(2 * s + h) : 0.f;
   }
+  if (a.ept == nullptr) {
+    const int jc = j < a.n_obs ? j : a.n_obs - 1;
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int64_t xr = row0 + 2 * s + h;
-    XGlobal xq{a.x, a.ept, a.ts_limit, a.n_obs, xr, xr < a.n};
-    in.xg[s] = (j < a.d.O) ? xq(j) : 0.f;
+    for (int s = 0; s < 16; ++s) {
+      const int64_t xr = row0 + 2 * s + h;
+      in.xg[s] = a.x[(xr < last ? xr : last) * a.n_obs + jc];
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int64_t xr = row0 + 2 * s + h;
+      XGlobal xq{a.x, a.ept, a.ts_limit, a.n_obs, xr, xr < a.n};
+      in.xg[s] = (j < a.d.O) ? xq(j) : 0.f;
+    }
   }
+  const float* gr = a.ghead + (row < last ? row : last) * a.gh;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int o = r + 4 * h;
-    in.g[r] = (valid && o < a.d.A) ? a.ghead[row * a.gh + o] : 0.f;
+    in.g[r] = gr[o < a.gh ? o : a.gh - 1];
   }
 #pragma unroll
-  for (int q = 0; q < MAX_OUT; ++q)
-    in.gs[q] = (valid && h == 0 && q < a.n_sum) ? a.ghead[row * a.gh + a.d.A + q] : 0.f;
+  for (int q = 0; q < MAX_OUT; ++q) {
+    const int c = a.d.A + q;
+    in.gs[q] = gr[c < a.gh ? c : a.gh - 1];
+  }
 }
 
 template <bool CACHED>
@@ -238,13 +256,25 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
       forward_tile_pre(lds, d, cur.x0, lane, f);
     }
 
-    // head gradient rows in C layout: register r of half h = out r + 4h
+    // head gradient rows in C layout: register r of half h = out r + 4h (masked here,
+    // not at load time: see vjp_load)
+    const bool valid = row0 + j < a.n;
     f32x16 G = zero16();
 #pragma unroll
-    for (int r = 0; r < 4; ++r) G[r] = cur.g[r];
+    for (int r = 0; r < 4; ++r) G[r] = (valid && r + 4 * h < A) ? cur.g[r] : 0.f;
 #pragma unroll
-    for (int q = 0; q < MAX_OUT; ++q) gls[q] += cur.gs[q];
-    // gh2 = W2 . G   (K = outs, 4 k-steps)
+    for (int q = 0; q < MAX_OUT; ++q) gls[q] += (valid && h == 0 && q < a.n_sum) ? cur.gs[q] : 0.f;
+    // Phase order keeps the MFMA pipe fed: every LDS transpose is issued while an
+    // independent MFMA chain runs (the wave_lds barriers split scheduling regions, so
+    // the source order is the schedule).  Accumulation orders are unchanged.
+    // (a) transposes that need nothing computed: h2 image, G rows
+    write_img(scrA, f.h2, lane);
+    {
+      const int base = (j & 1) * 16 + (j >> 1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) scrB[(r + 4 * h) * IMG_PAD + base] = G[r];
+    }
+    // (b) gh2 = W2 . G   (K = outs, 4 k-steps) while the transposes land
     f32x16 g2[2];
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) {
@@ -255,14 +285,8 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
       g2[mi] = MFMA32(w.z, G[2], g2[mi]);
       g2[mi] = MFMA32(w.w, G[3], g2[mi]);
     }
-    // gW2 += H2^T G  (row index as K through LDS)
-    write_img(scrA, f.h2, lane);
-    {
-      const int base = (j & 1) * 16 + (j >> 1);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) scrB[(r + 4 * h) * IMG_PAD + base] = G[r];
-    }
     WAVE_LDS_ORDER();
+    // (c) gW2 += H2^T G  (row index as K through LDS)
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       const float4 bq = ld4(scrB + j * IMG_PAD + h * 16 + 4 * s4);
@@ -276,16 +300,22 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
       }
     }
     if (lane < A) gb2 += rowsum32(scrB, lane);
-    // ga2 = gh2 * (1 - h2^2)
+    // (d) ga2 = gh2 * (1 - h2^2)
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int r = 0; r < 16; ++r) g2[m][r] *= (1.f - f.h2[m][r] * f.h2[m][r]);
+    // (e) gh1 = W1 . ga2: registers + the weight image only, so its 64 MFMAs cover the
+    //     h1 / ga2 transposes issued next
+    f32x16 g1[2];
+    g1[0] = zero16();
+    g1[1] = zero16();
+    chain<2>(lds, d.ba1, g2, lane, g1);
     WAVE_LDS_ORDER();
     write_img(scrA, f.h1, lane);
     write_img(scrB, g2, lane);
     WAVE_LDS_ORDER();
-    // gW1 += H1^T GA2
+    // (f) gW1 += H1^T GA2, and ga1 = gh1 * (1 - h1^2) on the VALU under it
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       const float4 a0 = ld4(scrA + j * IMG_PAD + h * 16 + 4 * s4);
@@ -310,11 +340,6 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
       gW1[1][1] = MFMA32(a1.w, b1.w, gW1[1][1]);
     }
     gb1 += rowsum32(scrB, lane);
-    // gh1 = W1 . ga2 ; ga1 = gh1 * (1 - h1^2)
-    f32x16 g1[2];
-    g1[0] = zero16();
-    g1[1] = zero16();
-    chain<2>(lds, d.ba1, g2, lane, g1);
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -322,7 +347,7 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
     WAVE_LDS_ORDER();
     write_img(scrB, g1, lane);
     WAVE_LDS_ORDER();
-    // gW0 += X^T GA1 : A[i = input j][k = row 2s+h] straight from global x
+    // (g) gW0 += X^T GA1 : A[i = input j][k = row 2s+h] straight from global x
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       const float4 b0 = ld4(scrB + j * IMG_PAD + h * 16 + 4 * s4);
