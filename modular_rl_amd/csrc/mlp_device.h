@@ -19,6 +19,7 @@ __device__ inline f32x16 zero16() {
 }
 
 __device__ inline float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ inline float f4get(const float4& v, int q) { return q == 0 ? v.x : (q == 1 ? v.y : (q == 2 ? v.z : v.w)); }
 
 __device__ inline f32x16 load_bias16(const float* lds, int off, int mo, int h) {
   const float* p = lds + off + (mo * 2 + h) * 16;

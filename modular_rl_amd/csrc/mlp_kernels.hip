@@ -153,11 +153,17 @@ __device__ inline float rowsum32(const float* img, int unit) {
 
 // every global operand one tile needs, loaded ahead of use; CACHED: the primal
 // activations come from the cache instead of the layer-0 inputs
-template <bool CACHED>
+// gW2 and gW0 run on v_mfma_f32_16x16x4_f32 (their narrow side -- A <= 8 head
+// outputs, O <= 16 inputs per tile -- pads to 16 instead of 32).  Their K is the 32
+// rows of the tile, read from the transposed LDS images at position p = 8*kk + q
+// (kk = lane >> 4, k-step q), i.e. row r(p) = 16*(kk&1) + 2q + (kk>>1).
+__device__ inline int vjp_row16(int kk, int q) { return 16 * (kk & 1) + 2 * q + (kk >> 1); }
+
+template <bool CACHED, bool WIDE>
 struct VjpIn {
   float x0[CACHED ? 1 : 16];  // layer-0 B operands x[row][2s+h]
   f32x16 act[CACHED ? 4 : 1]; // cached h1[0], h1[1], h2[0], h2[1]
-  float xg[16];               // gW0 A operands x[row0+2s+h][j]
+  float xg[WIDE ? 16 : 8];    // gW0 A operands x[row0 + r(8kk+q)][16mt + (lane&15)] at [8mt + q]
   float g[4];                 // head-gradient rows ghead[row][r+4h]
   float gs[MAX_OUT];          // summed head columns (DiagGauss logstd), lane half 0 only
 };
@@ -169,9 +175,10 @@ struct VjpIn {
 // the wait that the prefetch exists to avoid).  The clamped gW0 operands of rows past
 // n multiply head-gradient rows that are exactly zero; those of columns past the
 // input width land in gW0 rows that are never stored.
-template <bool CACHED>
-__device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn<CACHED>& in) {
-  const int h = lane >> 5, j = lane & 31;
+template <bool CACHED, bool WIDE>
+__device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn<CACHED, WIDE>& in) {
+  const int h = lane >> 5, j = lane & 31, i16 = lane & 15, kk = lane >> 4;
+  constexpr int MT0 = WIDE ? 2 : 1;
   const int64_t row0 = tile * 32, row = row0 + j, last = a.n - 1;
   if constexpr (CACHED) {
     const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
@@ -183,18 +190,25 @@ __device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn<
     for (int s = 0; s < 16; ++s) in.x0[s] = (s < a.d.KS0p) ? xl(2 * s + h) : 0.f;
   }
   if (a.ept == nullptr) {
-    const int jc = j < a.n_obs ? j : a.n_obs - 1;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int64_t xr = row0 + 2 * s + h;
-      in.xg[s] = a.x[(xr < last ? xr : last) * a.n_obs + jc];
+    for (int mt = 0; mt < MT0; ++mt) {
+      const int c = 16 * mt + i16, cc = c < a.n_obs ? c : a.n_obs - 1;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int64_t xr = row0 + vjp_row16(kk, q);
+        in.xg[8 * mt + q] = a.x[(xr < last ? xr : last) * a.n_obs + cc];
+      }
     }
   } else {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int64_t xr = row0 + 2 * s + h;
-      XGlobal xq{a.x, a.ept, a.ts_limit, a.n_obs, xr, xr < a.n};
-      in.xg[s] = (j < a.d.O) ? xq(j) : 0.f;
+    for (int mt = 0; mt < MT0; ++mt) {
+      const int c = 16 * mt + i16;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int64_t xr = row0 + vjp_row16(kk, q);
+        XGlobal xq{a.x, a.ept, a.ts_limit, a.n_obs, xr, xr < a.n};
+        in.xg[8 * mt + q] = (c < a.d.O) ? xq(c) : 0.f;
+      }
     }
   }
   const float* gr = a.ghead + (row < last ? row : last) * a.gh;
@@ -210,9 +224,10 @@ __device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn<
   }
 }
 
-template <bool CACHED>
+template <bool CACHED, bool WIDE>
 __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __restrict__ img,
                                                        const int32_t* __restrict__ skip) {
+  constexpr int MT0 = WIDE ? 2 : 1;  // 16-input tiles of gW0
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if (skip != nullptr && *skip != 0) return;
   const MlpDims& d = a.d;
@@ -224,14 +239,19 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
   float* scrB = scrA + 64 * IMG_PAD;
   const int A = d.A;
 
-  f32x16 gW1[2][2], gW2[2], gW0[2];
+  f32x16 gW1[2][2];
+  f32x4 gW2[4], gW0[MT0][4];  // 16x16 C tiles: gW2 [unit tile], gW0 [input tile][unit tile]
 #pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    gW2[m] = zero16();
-    gW0[m] = zero16();
+  for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int n = 0; n < 2; ++n) gW1[m][n] = zero16();
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    gW2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < MT0; ++m) gW0[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  const int i16 = lane & 15, kk = lane >> 4;
   float gb0 = 0.f, gb1 = 0.f, gb2 = 0.f;
   float gls[MAX_OUT];
 #pragma unroll
@@ -240,7 +260,7 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t stride = (int64_t)gridDim.x * 4;
   // software pipeline: every global operand of tile i+1 is in flight while tile i computes
-  VjpIn<CACHED> cur, nxt;
+  VjpIn<CACHED, WIDE> cur, nxt;
   int64_t tile = (int64_t)blockIdx.x * 4 + wave;
   if (tile < ntiles) vjp_load(a, tile, lane, cur);
   for (; tile < ntiles; tile += stride) {
@@ -286,18 +306,20 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
       g2[mi] = MFMA32(w.w, G[3], g2[mi]);
     }
     WAVE_LDS_ORDER();
-    // (c) gW2 += H2^T G  (row index as K through LDS)
+    // (c) gW2 += H2^T G  (row index as K through LDS; 16x16x4, head outputs as N)
+    {
+      const float4 b0 = ld4(scrB + i16 * IMG_PAD + 8 * kk), b1 = ld4(scrB + i16 * IMG_PAD + 8 * kk + 4);
+      float4 a0[4], a1[4];
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      const float4 bq = ld4(scrB + j * IMG_PAD + h * 16 + 4 * s4);
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi) {
-        const float4 aq = ld4(scrA + (32 * mi + j) * IMG_PAD + h * 16 + 4 * s4);
-        gW2[mi] = MFMA32(aq.x, bq.x, gW2[mi]);
-        gW2[mi] = MFMA32(aq.y, bq.y, gW2[mi]);
-        gW2[mi] = MFMA32(aq.z, bq.z, gW2[mi]);
-        gW2[mi] = MFMA32(aq.w, bq.w, gW2[mi]);
+      for (int mt = 0; mt < 4; ++mt) {
+        a0[mt] = ld4(scrA + (16 * mt + i16) * IMG_PAD + 8 * kk);
+        a1[mt] = ld4(scrA + (16 * mt + i16) * IMG_PAD + 8 * kk + 4);
       }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          gW2[mt] = MFMA16(f4get(q < 4 ? a0[mt] : a1[mt], q & 3), f4get(q < 4 ? b0 : b1, q & 3), gW2[mt]);
     }
     if (lane < A) gb2 += rowsum32(scrB, lane);
     // (d) ga2 = gh2 * (1 - h2^2)
@@ -347,20 +369,21 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
     WAVE_LDS_ORDER();
     write_img(scrB, g1, lane);
     WAVE_LDS_ORDER();
-    // (g) gW0 += X^T GA1 : A[i = input j][k = row 2s+h] straight from global x
+    // (g) gW0 += X^T GA1 : A[i = input][k = row] straight from global x (16x16x4)
+    {
+      float4 b0[4], b1[4];
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      const float4 b0 = ld4(scrB + j * IMG_PAD + h * 16 + 4 * s4);
-      const float4 b1 = ld4(scrB + (32 + j) * IMG_PAD + h * 16 + 4 * s4);
-      const float* av = cur.xg + 4 * s4;
-      gW0[0] = MFMA32(av[0], b0.x, gW0[0]);
-      gW0[1] = MFMA32(av[0], b1.x, gW0[1]);
-      gW0[0] = MFMA32(av[1], b0.y, gW0[0]);
-      gW0[1] = MFMA32(av[1], b1.y, gW0[1]);
-      gW0[0] = MFMA32(av[2], b0.z, gW0[0]);
-      gW0[1] = MFMA32(av[2], b1.z, gW0[1]);
-      gW0[0] = MFMA32(av[3], b0.w, gW0[0]);
-      gW0[1] = MFMA32(av[3], b1.w, gW0[1]);
+      for (int nt = 0; nt < 4; ++nt) {
+        b0[nt] = ld4(scrB + (16 * nt + i16) * IMG_PAD + 8 * kk);
+        b1[nt] = ld4(scrB + (16 * nt + i16) * IMG_PAD + 8 * kk + 4);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int mt = 0; mt < MT0; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            gW0[mt][nt] = MFMA16(cur.xg[8 * mt + q], f4get(q < 4 ? b0[nt] : b1[nt], q & 3), gW0[mt][nt]);
     }
     gb0 += rowsum32(scrB, lane);
     WAVE_LDS_ORDER();
@@ -371,12 +394,14 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
   // per-wave partial gradient in flat theta layout
   float* out = a.slab + ((int64_t)blockIdx.x * 4 + wave) * d.P;
 #pragma unroll
-  for (int mj = 0; mj < 2; ++mj)
+  for (int mt = 0; mt < MT0; ++mt)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = cperm(r, h);
-      if (i < d.O) out[d.tW0 + i * HID + 32 * mj + j] = gW0[mj][r];
-    }
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * mt + 4 * kk + r;
+        if (i < d.O) out[d.tW0 + i * HID + 16 * nt + i16] = gW0[mt][nt][r];
+      }
   out[d.tb0 + lane] = gb0;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -386,10 +411,10 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
       for (int r = 0; r < 16; ++r) out[d.tW1 + (32 * mi + cperm(r, h)) * HID + 32 * mj + j] = gW1[mi][mj][r];
   out[d.tb1 + lane] = gb1;
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      if (j < A) out[d.tW2 + (32 * mi + cperm(r, h)) * A + j] = gW2[mi][r];
+    for (int r = 0; r < 4; ++r)
+      if (i16 < A) out[d.tW2 + (16 * mt + 4 * kk + r) * A + i16] = gW2[mt][r];
   if (lane < A) out[d.tb2 + lane] = gb2;
   for (int q = 0; q < a.n_sum; ++q) {
     const float s = wave_sumf(gls[q]);
@@ -621,10 +646,17 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
   const int64_t blocks = vjp_blocks(n);
   size_t shm = ((size_t)a.d.total_size + 4 * (size_t)SCR_FLOATS) * 4;
   a.cache = act_cache;
-  if (act_cache != nullptr)
-    hipLaunchKernelGGL(mlp_vjp_kernel<true>, dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image, skip);
+  const bool wide = a.d.O > 16;
+  if (act_cache != nullptr && !wide)
+    hipLaunchKernelGGL((mlp_vjp_kernel<true, false>), dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image, skip);
+  else if (act_cache != nullptr)
+    hipLaunchKernelGGL((mlp_vjp_kernel<true, true>), dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image, skip);
+  else if (!wide)
+    hipLaunchKernelGGL((mlp_vjp_kernel<false, false>), dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image,
+                       skip);
   else
-    hipLaunchKernelGGL(mlp_vjp_kernel<false>, dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image, skip);
+    hipLaunchKernelGGL((mlp_vjp_kernel<false, true>), dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image,
+                       skip);
   return hip_check(hipGetLastError(), "mrl_mlp_vjp");
 }
 

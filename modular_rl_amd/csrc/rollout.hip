@@ -167,7 +167,6 @@ __device__ inline f32x4 as_f32x4(float4 v) {
   r[3] = v.w;
   return r;
 }
-__device__ inline float f4get(const float4& v, int q) { return q == 0 ? v.x : (q == 1 ? v.y : (q == 2 ? v.z : v.w)); }
 
 __device__ inline void tanh4(f32x4& a) {
 #pragma unroll
