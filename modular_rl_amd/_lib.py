@@ -9,7 +9,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmrl_hip.so")
+# MRL_LIB_PATH: diagnostic override (ablation builds under tools/); the default is the in-tree build
+LIB_PATH = os.environ.get("MRL_LIB_PATH") or os.path.join(_HERE, "libmrl_hip.so")
 
 OK = 0
 HEAD_LINEAR, HEAD_SOFTMAX, HEAD_GAUSS = 0, 1, 2

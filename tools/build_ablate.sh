@@ -1,0 +1,13 @@
+#!/bin/bash
+# Diagnostic builds of libmrl_hip.so with -D switches (tools/ablate/libmrl_hip_<name>.so);
+# select one at run time with MRL_LIB_PATH.  Usage: tools/build_ablate.sh NAME -DFLAG ...
+set -e
+name=$1; shift
+out=tools/ablate/$name; mkdir -p $out
+for f in mlp_kernels scan rollout gemm; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude "$@" \
+    -c modular_rl_amd/csrc/$f.hip -o $out/$f.o
+done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/ablate/libmrl_hip_$name.so $out/*.o
+rm -rf $out
+echo tools/ablate/libmrl_hip_$name.so
