@@ -179,17 +179,24 @@ int mrl_concat_time(const float* obs, const int32_t* ep_t, int64_t n, int32_t n_
 /* ---------------------------------------------------------------- conjugate gradient
  * Device-resident Demmel CG on flat fp64 vectors (trpo.py:165-200).
  * state (fp64): [0]=rdotr [1]=last pz [2]=iterations run; flag (int32[2]): [0]=converged.
- * init:   x=0, r=p=b, rdotr=r.r, p32=(float)p, flag=0.
- * update: z = fvp + damping*p; v=rdotr/p.z; x+=v p; r-=v z; mu=r.r/rdotr; p=r+mu p;
- *         flag=1 when rdotr<tol; pass `flag` as the `skip` of the next Fvp kernels. */
-int mrl_cg_init(const double* b, int64_t n, double* x, double* r, double* p, float* p32, double* state,
-                int32_t* flag, void* stream);
+ * init:   x=0, r=p=b, rdotr=r.r, p32=(float)p, flag=0, ax=0.
+ * update: z = fvp + damping*p; v=rdotr/p.z; x+=v p; ax+=v z; r-=v z; mu=r.r/rdotr; p=r+mu p;
+ *         flag=1 when rdotr<tol; pass `flag` as the `skip` of the next Fvp kernels.
+ * ax (fp64 [n], optional: NULL skips it) accumulates (F + damping I) x, which the
+ * step scaling needs (trpo.py:119-122) -- A is linear, so A sum v_k p_k = sum v_k z_k
+ * and no Fisher product of the step direction has to be run. */
+int mrl_cg_init(const double* b, int64_t n, double* x, double* r, double* p, float* p32, double* ax,
+                double* state, int32_t* flag, void* stream);
 int mrl_cg_update(const float* fvp, double damping, double residual_tol, int64_t n, double* x, double* r,
-                  double* p, float* p32, double* state, int32_t* flag, void* stream);
+                  double* p, float* p32, double* ax, double* state, int32_t* flag, void* stream);
 /* step scaling (trpo.py:119-124): shs = .5 x.(fvp + damping x), lm = sqrt(shs/max_kl),
  * fullstep = x/lm, out[0]=shs out[1]=lm out[2]=-g.x out[3]=-g.x/lm (expected rate) */
 int mrl_trpo_step(const float* fvp, const double* x, const float* g, double damping, double max_kl,
                   int64_t n, double* fullstep, double* out, void* stream);
+/* the same scaling from ax = (F + damping I) x accumulated by mrl_cg_update:
+ * shs = .5 x.ax (the update path: one Fisher product fewer per TRPO step) */
+int mrl_trpo_step_ax(const double* ax, const double* x, const float* g, double max_kl, int64_t n,
+                     double* fullstep, double* out, void* stream);
 /* theta_out = (float)(theta_old + frac * fullstep)   (linesearch, trpo.py:150, core.py:540) */
 int mrl_axpy_cast(const float* theta_old, const double* fullstep, double frac, int64_t n, float* theta_out,
                   void* stream);

@@ -5,9 +5,8 @@
 // time-major [T, E] rows the per-path reverse recurrences
 //     adv_t = delta_t + gamma*lam*cont_t*adv_{t+1},  ret_t = r_t + gamma*cont_t*ret_{t+1}
 // are linear, so each (chunk of L steps, env) is summarised as an affine map
-// (A, B): adv_in = A + B*adv_out.  Pass 1 writes the summaries; pass 2 folds the
-// summaries of later chunks into a carry and re-scans its chunk (the second read
-// of r/v/flags is served by the 256 MiB Infinity Cache at the benchmark size).
+// (A, B): adv_in = A + B*adv_out, and chunks compose by a parallel scan.
+// One pass: r / v / flags are read once, adv / ret written once (17 B per row).
 // Scans run in fp64 like lfilter; outputs are fp32.
 #include <math.h>
 
@@ -16,89 +15,163 @@
 
 namespace mrl {
 
-constexpr int GAE_CHUNK = 32;
+// One block owns GAE_EB envs over the whole horizon: thread (c, e) holds chunk c
+// (GAE_L consecutive steps) of env e in registers, so every load of the scan is
+// issued up front (a wave instruction covers 4 rows x 64 B) and r / v / flags are
+// read from HBM exactly once.  Each chunk is summarised as the affine map of its
+// recurrence, one wave per env composes the GAE_NC chunk maps with a reverse
+// shuffle scan, and each thread re-runs its chunk from the carried-in value and
+// writes adv / ret.  Horizons longer than GAE_NC * L run as segments from the
+// last to the first, the carry held by the env's scan wave.
+constexpr int GAE_EB = 16;               // envs per block: one 64 B row segment
+constexpr int GAE_NC = 32;               // chunks per segment: one per lane of a half-wave
+constexpr int GAE_THREADS = GAE_EB * GAE_NC;
+constexpr int GAE_LMAX = 32;
+constexpr int GAE_PITCH = GAE_EB + 1;    // LDS row pitch (doubles): 2-way conflicts at most
 
-struct Summ {
-  double A, B, R, C;
-};
-
-__device__ inline double delta_at(const float* rew, const float* v, const uint8_t* flags, int64_t t, int64_t T,
-                                  int64_t E, int64_t e, double gamma, bool& cont) {
-  const int64_t i = t * E + e;
-  const uint8_t fl = flags[i];
-  cont = !(fl & 1) && (t + 1 < T);
-  const double vt = (double)v[i];
-  // bootstrap b1[t+1]: next baseline inside the episode, 0 if terminated, else b[-1] (core.py:73)
-  const double boot = cont ? (double)v[i + E] : ((fl & 2) ? 0.0 : vt);
-  return (double)rew[i] + gamma * boot - vt;
-}
-
-__global__ void gae_summary_kernel(const float* __restrict__ rew, const float* __restrict__ v,
-                                   const uint8_t* __restrict__ flags, int64_t T, int64_t E, double gamma, double lam,
-                                   Summ* __restrict__ summ) {
-  const int64_t C = (T + GAE_CHUNK - 1) / GAE_CHUNK;
-  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= C * E) return;
-  const int64_t c = id / E, e = id % E;
-  const int64_t t0 = c * GAE_CHUNK, t1 = min(T, t0 + GAE_CHUNK);
-  double A = 0.0, B = 1.0, R = 0.0, Cc = 1.0;
+template <int L>
+__global__ __launch_bounds__(GAE_THREADS) void gae_scan_kernel(const float* __restrict__ rew,
+                                                               const float* __restrict__ v,
+                                                               const uint8_t* __restrict__ flags, int64_t T,
+                                                               int64_t E, double gamma, double lam,
+                                                               float* __restrict__ adv, float* __restrict__ ret,
+                                                               double* __restrict__ part) {
+  __shared__ double sA[GAE_NC * GAE_PITCH], sB[GAE_NC * GAE_PITCH], sR[GAE_NC * GAE_PITCH],
+      sC[GAE_NC * GAE_PITCH];
+  __shared__ double red[2][GAE_THREADS / 64];
+  const int tid = threadIdx.x;
+  const int el = tid % GAE_EB, c = tid / GAE_EB;
+  const int64_t e = (int64_t)blockIdx.x * GAE_EB + el;
+  const bool live = e < E;
   const double gl = gamma * lam;
-  for (int64_t t = t1 - 1; t >= t0; --t) {
-    bool cont;
-    const double d = delta_at(rew, v, flags, t, T, E, e, gamma, cont);
-    const double k = cont ? 1.0 : 0.0;
-    A = d + gl * k * A;
-    B = gl * k * B;
-    R = (double)rew[t * E + e] + gamma * k * R;
-    Cc = gamma * k * Cc;
-  }
-  summ[id] = Summ{A, B, R, Cc};
-}
-
-__global__ void gae_final_kernel(const float* __restrict__ rew, const float* __restrict__ v,
-                                 const uint8_t* __restrict__ flags, int64_t T, int64_t E, double gamma, double lam,
-                                 const Summ* __restrict__ summ, float* __restrict__ adv, float* __restrict__ ret,
-                                 double* __restrict__ part) {
-  __shared__ double red[2][256];
-  const int64_t C = (T + GAE_CHUNK - 1) / GAE_CHUNK;
-  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t S = (int64_t)GAE_NC * L;
+  const int64_t nseg = (T + S - 1) / S;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int sc = lane & 31, se = 2 * wave + (lane >> 5);  // scan: half-wave = env slot se, lane = chunk sc
+  double carry_a = 0.0, carry_r = 0.0;                    // held by the half-wave of env slot se
   double s1 = 0.0, s2 = 0.0;
-  if (id < C * E) {
-    const int64_t c = id / E, e = id % E;
-    double a = 0.0, r = 0.0;
-    for (int64_t cc = C - 1; cc > c; --cc) {
-      const Summ s = summ[cc * E + e];
-      a = s.A + s.B * a;
-      r = s.R + s.C * r;
+  for (int64_t seg = nseg - 1; seg >= 0; --seg) {
+    const int64_t t0 = seg * S + (int64_t)c * L;
+    // uniform segment/block base + 32-bit per-lane offsets (S * E < 2^29, checked on the host)
+    const int64_t base = seg * S * E + (int64_t)blockIdx.x * GAE_EB;
+    const float* rb = rew + base;
+    const float* vb = v + base;
+    const uint8_t* fb = flags + base;
+    // branch-free loads: rows past T and envs past E read a clamped valid element
+    // and are masked where they are used
+    const int64_t rows = min(S, T - seg * S);  // rows of this segment
+    const int elc = (int)min((int64_t)el, E - 1 - (int64_t)blockIdx.x * GAE_EB);
+    auto off = [&](int row) -> uint32_t {  // byte offset of (row, env) from the base, float elements
+      const int rc = row < rows ? row : (int)rows - 1;
+      return ((uint32_t)rc * (uint32_t)E + (uint32_t)elc) * 4u;
+    };
+    float rr[L], vv[L];
+    uint8_t ff[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const uint32_t o = off(c * L + j);
+      rr[j] = *(const float*)((const char*)rb + o);
+      vv[j] = *(const float*)((const char*)vb + o);
+      ff[j] = fb[o >> 2];
     }
-    const int64_t t0 = c * GAE_CHUNK, t1 = min(T, t0 + GAE_CHUNK);
-    const double gl = gamma * lam;
-    for (int64_t t = t1 - 1; t >= t0; --t) {
-      bool cont;
-      const double d = delta_at(rew, v, flags, t, T, E, e, gamma, cont);
-      const double k = cont ? 1.0 : 0.0;
-      a = d + gl * k * a;
-      r = (double)rew[t * E + e] + gamma * k * r;
-      const float af = (float)a;
-      adv[t * E + e] = af;
-      ret[t * E + e] = (float)r;
-      s1 += (double)af;
-      s2 += (double)af * (double)af;
+    const int64_t tn = t0 + L;  // first row of the next chunk (may sit in the next segment)
+    const float vnext = (live && tn < T) ? v[tn * E + e] : 0.f;
+    // delta_t and the continuation flag of step j of this chunk
+    auto step = [&](int j, bool& cont) -> double {
+      const int64_t t = t0 + j;
+      cont = !(ff[j] & 1) && (t + 1 < T);
+      const double vt = (double)vv[j];
+      const double vn = (j + 1 < L) ? (double)vv[j + 1 < L ? j + 1 : j] : (double)vnext;
+      // bootstrap b1[t+1]: next baseline inside the episode, 0 if terminated, else b[-1] (core.py:73)
+      const double boot = cont ? vn : ((ff[j] & 2) ? 0.0 : vt);
+      return (double)rr[j] + gamma * boot - vt;
+    };
+    // chunk summary: adv_in = A + B * adv_out, ret_in = R + C * ret_out
+    double A = 0.0, B = 1.0, R = 0.0, Cc = 1.0;
+#pragma unroll
+    for (int j = L - 1; j >= 0; --j) {
+      if (t0 + j < T) {
+        bool cont;
+        const double d = step(j, cont);
+        const double kk = cont ? 1.0 : 0.0;
+        A = d + gl * kk * A;
+        B = gl * kk * B;
+        R = (double)rr[j] + gamma * kk * R;
+        Cc = gamma * kk * Cc;
+      }
     }
-  }
-  red[0][threadIdx.x] = s1;
-  red[1][threadIdx.x] = s2;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + o];
-      red[1][threadIdx.x] += red[1][threadIdx.x + o];
+    sA[c * GAE_PITCH + el] = A;
+    sB[c * GAE_PITCH + el] = B;
+    sR[c * GAE_PITCH + el] = R;
+    sC[c * GAE_PITCH + el] = Cc;
+    __syncthreads();
+    {
+      // reverse inclusive scan of the maps of env slot se over its chunks (lane = chunk)
+      double a = sA[sc * GAE_PITCH + se], b = sB[sc * GAE_PITCH + se];
+      double r = sR[sc * GAE_PITCH + se], cc = sC[sc * GAE_PITCH + se];
+#pragma unroll
+      for (int off = 1; off < 32; off <<= 1) {
+        const double a2 = __shfl_down(a, off), b2 = __shfl_down(b, off);
+        const double r2 = __shfl_down(r, off), c2 = __shfl_down(cc, off);
+        if (sc + off < 32) {
+          a = a + b * a2;
+          b = b * b2;
+          r = r + cc * r2;
+          cc = cc * c2;
+        }
+      }
+      // exclusive: the composite of the later chunks, applied to the segment carry
+      double xa = __shfl_down(a, 1), xb = __shfl_down(b, 1), xr = __shfl_down(r, 1), xc = __shfl_down(cc, 1);
+      if (sc == 31) { xa = 0.0; xb = 1.0; xr = 0.0; xc = 1.0; }
+      const double in_a = xa + xb * carry_a, in_r = xr + xc * carry_r;
+      const int l0 = lane & 32;  // the half-wave's chunk 0
+      const double a0 = __shfl(a, l0), b0 = __shfl(b, l0), r0 = __shfl(r, l0), c0 = __shfl(cc, l0);
+      carry_a = a0 + b0 * carry_a;
+      carry_r = r0 + c0 * carry_r;
+      __syncthreads();  // every summary read before the carries overwrite them
+      sA[sc * GAE_PITCH + se] = in_a;
+      sR[sc * GAE_PITCH + se] = in_r;
     }
     __syncthreads();
+    double a = sA[c * GAE_PITCH + el], r = sR[c * GAE_PITCH + el];
+    float* ab = adv + base;
+    float* tb = ret + base;
+#pragma unroll
+    for (int j = L - 1; j >= 0; --j) {
+      if (live && t0 + j < T) {
+        bool cont;
+        const double dj = step(j, cont);
+        const double kk = cont ? 1.0 : 0.0;
+        a = dj + gl * kk * a;
+        r = (double)rr[j] + gamma * kk * r;
+        const float af = (float)a;
+        const uint32_t o = off(c * L + j);
+        *(float*)((char*)ab + o) = af;
+        *(float*)((char*)tb + o) = (float)r;
+        s1 += (double)af;
+        s2 += (double)af * (double)af;
+      }
+    }
+    __syncthreads();  // LDS reused by the next (earlier) segment
   }
-  if (threadIdx.x == 0) {
-    part[blockIdx.x * 2 + 0] = red[0][0];
-    part[blockIdx.x * 2 + 1] = red[1][0];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_down(s1, off);
+    s2 += __shfl_down(s2, off);
+  }
+  if (lane == 0) {
+    red[0][wave] = s1;
+    red[1][wave] = s2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double t1 = 0.0, t2 = 0.0;
+    for (int w = 0; w < GAE_THREADS / 64; ++w) {
+      t1 += red[0][w];
+      t2 += red[1][w];
+    }
+    part[blockIdx.x * 2 + 0] = t1;
+    part[blockIdx.x * 2 + 1] = t2;
   }
 }
 
@@ -158,12 +231,14 @@ __device__ inline double block_sum(double v, double* red) {
 }
 
 __global__ __launch_bounds__(CG_T) void cg_init_kernel(const double* __restrict__ b, int64_t n, double* x, double* r,
-                                                       double* p, float* p32, double* state, int32_t* flag) {
+                                                       double* p, float* p32, double* ax, double* state,
+                                                       int32_t* flag) {
   __shared__ double red[CG_T];
   double s = 0.0;
   for (int64_t i = threadIdx.x; i < n; i += CG_T) {
     const double bi = b[i];
     x[i] = 0.0;
+    if (ax) ax[i] = 0.0;
     r[i] = bi;
     p[i] = bi;
     p32[i] = (float)bi;
@@ -181,7 +256,7 @@ __global__ __launch_bounds__(CG_T) void cg_init_kernel(const double* __restrict_
 
 __global__ __launch_bounds__(CG_T) void cg_update_kernel(const float* __restrict__ fvp, double damping, double tol,
                                                          int64_t n, double* x, double* r, double* p, float* p32,
-                                                         double* state, int32_t* flag) {
+                                                         double* ax, double* state, int32_t* flag) {
   __shared__ double red[CG_T];
   if (flag[0] != 0) return;
   const double rdotr = state[0];
@@ -197,6 +272,7 @@ __global__ __launch_bounds__(CG_T) void cg_update_kernel(const float* __restrict
     const double pi = p[i];
     const double z = (double)fvp[i] + damping * pi;
     x[i] += v * pi;
+    if (ax) ax[i] += v * z;  // A x = sum_k v_k A p_k: the step scaling needs no extra Fisher product
     const double ri = r[i] - v * z;
     r[i] = ri;
     s += ri * ri;
@@ -228,6 +304,29 @@ __global__ __launch_bounds__(CG_T) void trpo_step_kernel(const float* __restrict
   const double xFx = block_sum(s, red);
   const double gx = block_sum(sg, red);
   const double shs = 0.5 * xFx;
+  const double lm = sqrt(shs / max_kl);
+  for (int64_t i = threadIdx.x; i < n; i += CG_T) fullstep[i] = x[i] / lm;
+  if (threadIdx.x == 0) {
+    out[0] = shs;
+    out[1] = lm;
+    out[2] = -gx;
+    out[3] = -gx / lm;
+  }
+}
+
+// same scaling from A x accumulated by the CG updates (A linear: A sum v_k p_k = sum v_k z_k)
+__global__ __launch_bounds__(CG_T) void trpo_step_ax_kernel(const double* __restrict__ ax, const double* __restrict__ x,
+                                                            const float* __restrict__ g, double max_kl, int64_t n,
+                                                            double* fullstep, double* out) {
+  __shared__ double red[CG_T];
+  double s = 0.0, sg = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += CG_T) {
+    s += x[i] * ax[i];
+    sg += (double)g[i] * x[i];
+  }
+  const double xAx = block_sum(s, red);
+  const double gx = block_sum(sg, red);
+  const double shs = 0.5 * xAx;
   const double lm = sqrt(shs / max_kl);
   for (int64_t i = threadIdx.x; i < n; i += CG_T) fullstep[i] = x[i] / lm;
   if (threadIdx.x == 0) {
@@ -370,24 +469,35 @@ using namespace mrl;
 extern "C" {
 
 int64_t mrl_gae_workspace_bytes(int64_t T, int64_t E) {
-  const int64_t C = (T + GAE_CHUNK - 1) / GAE_CHUNK;
-  const int64_t nb = (C * E + 255) / 256;
-  return C * E * (int64_t)sizeof(Summ) + nb * 2 * (int64_t)sizeof(double) + 64;
+  (void)T;
+  const int64_t nb = (E + GAE_EB - 1) / GAE_EB;
+  return nb * 2 * (int64_t)sizeof(double) + 64;
 }
 
 int mrl_gae(const float* rew, const float* vpred, const uint8_t* flags, int64_t T, int64_t E, double gamma, double lam,
             float* adv, float* ret, double* moments, void* workspace, void* stream) {
   if (!rew || !vpred || !flags || !adv || !ret || !moments || !workspace) return fail(E_ARG, "null pointer");
   if (T <= 0 || E <= 0) return OK;
-  const int64_t C = (T + GAE_CHUNK - 1) / GAE_CHUNK;
-  const int64_t nthreads = C * E;
-  const int64_t nb = (nthreads + 255) / 256;
-  Summ* summ = reinterpret_cast<Summ*>(workspace);
-  double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(workspace) + C * E * sizeof(Summ));
+  const int64_t nb = (E + GAE_EB - 1) / GAE_EB;
+  if ((int64_t)GAE_NC * GAE_LMAX * (E + GAE_EB) >= ((int64_t)1 << 29))
+    return fail(E_UNSUPPORTED, "mrl_gae: E too large for 32-bit segment offsets");
+  double* part = reinterpret_cast<double*>(workspace);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(gae_summary_kernel, dim3(nb), dim3(256), 0, s, rew, vpred, flags, T, E, gamma, lam, summ);
-  hipLaunchKernelGGL(gae_final_kernel, dim3(nb), dim3(256), 0, s, rew, vpred, flags, T, E, gamma, lam, summ, adv, ret,
-                     part);
+  // chunk length: the smallest power of two that covers T in one segment, at most GAE_LMAX
+  int L = 1;
+  while (L < GAE_LMAX && (int64_t)GAE_NC * L < T) L <<= 1;
+#define MRL_GAE_LAUNCH(LL)                                                                                      \
+  hipLaunchKernelGGL(gae_scan_kernel<LL>, dim3(nb), dim3(GAE_THREADS), 0, s, rew, vpred, flags, T, E, gamma, lam, \
+                     adv, ret, part)
+  switch (L) {
+    case 1: MRL_GAE_LAUNCH(1); break;
+    case 2: MRL_GAE_LAUNCH(2); break;
+    case 4: MRL_GAE_LAUNCH(4); break;
+    case 8: MRL_GAE_LAUNCH(8); break;
+    case 16: MRL_GAE_LAUNCH(16); break;
+    default: MRL_GAE_LAUNCH(32); break;
+  }
+#undef MRL_GAE_LAUNCH
   hipLaunchKernelGGL(moments_final_kernel, dim3(1), dim3(256), 0, s, part, nb, (double)(T * E), moments);
   return hip_check(hipGetLastError(), "mrl_gae");
 }
@@ -406,18 +516,18 @@ int mrl_vf_target(const float* ret, const float* vpred, double mixfrac, int64_t 
   return hip_check(hipGetLastError(), "mrl_vf_target");
 }
 
-int mrl_cg_init(const double* b, int64_t n, double* x, double* r, double* p, float* p32, double* state, int32_t* flag,
-                void* stream) {
+int mrl_cg_init(const double* b, int64_t n, double* x, double* r, double* p, float* p32, double* ax, double* state,
+                int32_t* flag, void* stream) {
   if (!b || !x || !r || !p || !p32 || !state || !flag) return fail(E_ARG, "null pointer");
-  hipLaunchKernelGGL(cg_init_kernel, dim3(1), dim3(CG_T), 0, (hipStream_t)stream, b, n, x, r, p, p32, state, flag);
+  hipLaunchKernelGGL(cg_init_kernel, dim3(1), dim3(CG_T), 0, (hipStream_t)stream, b, n, x, r, p, p32, ax, state, flag);
   return hip_check(hipGetLastError(), "mrl_cg_init");
 }
 
 int mrl_cg_update(const float* fvp, double damping, double residual_tol, int64_t n, double* x, double* r, double* p,
-                  float* p32, double* state, int32_t* flag, void* stream) {
+                  float* p32, double* ax, double* state, int32_t* flag, void* stream) {
   if (!fvp || !x || !r || !p || !p32 || !state || !flag) return fail(E_ARG, "null pointer");
   hipLaunchKernelGGL(cg_update_kernel, dim3(1), dim3(CG_T), 0, (hipStream_t)stream, fvp, damping, residual_tol, n, x, r,
-                     p, p32, state, flag);
+                     p, p32, ax, state, flag);
   return hip_check(hipGetLastError(), "mrl_cg_update");
 }
 
@@ -427,6 +537,14 @@ int mrl_trpo_step(const float* fvp, const double* x, const float* g, double damp
   hipLaunchKernelGGL(trpo_step_kernel, dim3(1), dim3(CG_T), 0, (hipStream_t)stream, fvp, x, g, damping, max_kl, n,
                      fullstep, out);
   return hip_check(hipGetLastError(), "mrl_trpo_step");
+}
+
+int mrl_trpo_step_ax(const double* ax, const double* x, const float* g, double max_kl, int64_t n, double* fullstep,
+                     double* out, void* stream) {
+  if (!ax || !x || !g || !fullstep || !out) return fail(E_ARG, "null pointer");
+  hipLaunchKernelGGL(trpo_step_ax_kernel, dim3(1), dim3(CG_T), 0, (hipStream_t)stream, ax, x, g, max_kl, n, fullstep,
+                     out);
+  return hip_check(hipGetLastError(), "mrl_trpo_step_ax");
 }
 
 int mrl_axpy_cast(const float* theta_old, const double* fullstep, double frac, int64_t n, float* theta_out,

@@ -9,8 +9,11 @@ collector.  The numerics run in libmrl_hip:
   cg(F + damping I, -g) device CG vectors (fp64), 10 x [Fvp kernels + cg_update];
                         the residual-tolerance break is a device flag that turns
                         the remaining Fvp launches into no-ops (no host sync)
-  shs / lm / fullstep   one more Fvp + mrl_trpo_step (the duplicate diagnostic
-                        Fvp of trpo.py:111 is dropped)
+  shs / lm / fullstep   mrl_trpo_step_ax: shs = .5 x.(F + damping I)x where
+                        (F + damping I)x = sum_k v_k z_k is accumulated by the CG
+                        updates (z_k = the damped Fisher product of p_k; linearity),
+                        so the Fvp(stepdir) of trpo.py:119-122 costs no pass over the
+                        rows (the duplicate diagnostic Fvp of trpo.py:111 is dropped)
   linesearch            per candidate: theta = theta_old + frac*fullstep (fp64,
                         cast to fp32 like SetFromFlat) + one fused loss pass; the
                         accepted candidate's (surr, kl, ent) are losses_after.
@@ -42,11 +45,10 @@ class HipTrpoOps:
         self.fv = torch.zeros(P, **f32)
         self.b = torch.zeros(P, **f64)
         self.x = torch.zeros(P, **f64)
+        self.ax = torch.zeros(P, **f64)
         self.r = torch.zeros(P, **f64)
         self.p = torch.zeros(P, **f64)
         self.p32 = torch.zeros(P, **f32)
-        self.x32 = torch.zeros(P, **f32)
-        self.zero32 = torch.zeros(P, **f32)
         self.fullstep = torch.zeros(P, **f64)
         self.cand = torch.zeros(P, **f32)
         self.cand_image = torch.zeros_like(net.image)
@@ -96,20 +98,17 @@ class HipTrpoOps:
         return self.b
 
     def cg_init(self, b):
-        call("mrl_cg_init", ptr(b), self.P, ptr(self.x), ptr(self.r), ptr(self.p), ptr(self.p32), ptr(self.state),
-             ptr(self.flag), stream())
+        call("mrl_cg_init", ptr(b), self.P, ptr(self.x), ptr(self.r), ptr(self.p), ptr(self.p32), ptr(self.ax),
+             ptr(self.state), ptr(self.flag), stream())
 
     def cg_update(self, fv, damping, tol):
         call("mrl_cg_update", ptr(fv), float(damping), float(tol), self.P, ptr(self.x), ptr(self.r), ptr(self.p),
-             ptr(self.p32), ptr(self.state), ptr(self.flag), stream())
+             ptr(self.p32), ptr(self.ax), ptr(self.state), ptr(self.flag), stream())
 
-    def stepdir32(self):
-        call("mrl_axpy_cast", ptr(self.zero32), ptr(self.x), 1.0, self.P, ptr(self.x32), stream())
-        return self.x32
-
-    def trpo_step(self, fv, g, damping, max_kl):
-        call("mrl_trpo_step", ptr(fv), ptr(self.x), ptr(g), float(damping), float(max_kl), self.P,
-             ptr(self.fullstep), ptr(self.step_out), stream())
+    def trpo_step(self, g, max_kl):
+        """shs / lm / fullstep from the A x the CG updates accumulated (trpo.py:119-124)."""
+        call("mrl_trpo_step_ax", ptr(self.ax), ptr(self.x), ptr(g), float(max_kl), self.P, ptr(self.fullstep),
+             ptr(self.step_out), stream())
         return self.step_out
 
     def candidate(self, theta_old, frac):
@@ -188,9 +187,7 @@ class TrpoUpdater:
                 fv = ops.fvp(ops.p32, skip=ops.flag)
                 comm.allreduce_(fv)
                 ops.cg_update(fv, damping, self.RESIDUAL_TOL)
-            fv = ops.fvp(ops.stepdir32())
-            comm.allreduce_(fv)
-            out = ops.trpo_step(fv, g, damping, max_kl).cpu().numpy()
+            out = ops.trpo_step(g, max_kl).cpu().numpy()
             shs, lm, neggdotstepdir, rate = (float(v) for v in out)
             fval = losses_before[0]
 

@@ -24,7 +24,7 @@ class OracleOps:
     def __init__(self, spec, net):
         self.spec, self.net, self.P = spec, net, spec.P
         z = lambda: torch.zeros(self.P, dtype=torch.float64)  # noqa: E731
-        self.x, self.r, self.p, self.p32, self.fullstep, self.cand = z(), z(), z(), z(), z(), z()
+        self.x, self.r, self.p, self.p32, self.fullstep, self.cand, self.ax = z(), z(), z(), z(), z(), z(), z()
         self.state = torch.zeros(4, dtype=torch.float64)
         self.flag = torch.zeros(2, dtype=torch.int32)
         self.fv = z()
@@ -57,6 +57,7 @@ class OracleOps:
 
     def cg_init(self, b):
         self.x.zero_()
+        self.ax.zero_()
         self.r.copy_(b)
         self.p.copy_(b)
         self.p32.copy_(b)
@@ -71,6 +72,7 @@ class OracleOps:
         z = fv + damping * self.p
         v = rdotr / float(self.p.dot(z))
         self.x += v * self.p
+        self.ax += v * z
         self.r -= v * z
         newr = float(self.r.dot(self.r))
         self.p.copy_(self.r + (newr / rdotr) * self.p)
@@ -80,11 +82,8 @@ class OracleOps:
         if newr < tol:
             self.flag[0] = 1
 
-    def stepdir32(self):
-        return self.x.clone()
-
-    def trpo_step(self, fv, g, damping, max_kl):
-        shs = 0.5 * float(self.x.dot(fv + damping * self.x))
+    def trpo_step(self, g, max_kl):
+        shs = 0.5 * float(self.x.dot(self.ax))
         lm = np.sqrt(shs / max_kl)
         self.fullstep.copy_(self.x / lm)
         ngx = -float(g.double().dot(self.x))

@@ -18,7 +18,7 @@ def _dev(a, dtype=torch.float32):
     return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).cuda()
 
 
-@pytest.mark.parametrize("Tn,E", [(1, 1), (33, 5), (100, 37), (257, 64)])
+@pytest.mark.parametrize("Tn,E", [(1, 1), (33, 5), (100, 37), (257, 64), (1024, 4096), (2500, 19), (4097, 3)])
 def test_gae_and_standardize(Tn, E):
     from modular_rl_amd import core
     from modular_rl_amd.collector import Batch
