@@ -90,7 +90,7 @@ def cpu_baseline(E, Tn, env_id="Hopper-v2", hid=(64, 64), seed=0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--env", default="Hopper-v2")
     ap.add_argument("--envs", type=int, default=4096)
@@ -99,11 +99,13 @@ def main():
     ap.add_argument("--cpu-envs", type=int, default=None)
     ap.add_argument("--cpu-horizon", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="run the VF fit in the reference order instead of beside the next rollout")
     args = ap.parse_args()
 
     from modular_rl_amd import timing
     from modular_rl_amd.agentzoo import TrpoAgent
-    from modular_rl_amd.core import compute_advantage_batch
+    from modular_rl_amd.core import IterationRunner
     from modular_rl_amd.dist import init_from_env
     from modular_rl_amd.envs import make
 
@@ -121,37 +123,27 @@ def main():
                n_envs=E, horizon=Tn, filter=1, seed=0, hid_sizes=hid, activation="tanh", use_graph=1)
     agent = TrpoAgent(env.observation_space, env.action_space, cfg, comm=comm)
     collector = agent.make_collector(env, cfg)
-
-    def ev():
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        return e
+    runner = IterationRunner(agent, collector, cfg, comm, pipeline=not args.no_pipeline)
 
     phases = {"rollout": 0.0, "advantage": 0.0, "vf_fit": 0.0, "trpo_update": 0.0}
-
-    def iteration(record):
-        e0 = ev()
-        batch = collector.collect()
-        e1 = ev()
-        compute_advantage_batch(agent.baseline, batch, cfg["gamma"], cfg["lam"], comm)
-        e2 = ev()
-        agent.baseline.fit_batch(batch)
-        e3 = ev()
-        agent.updater.update(batch)
-        e4 = ev()
-        collector.episode_stats(batch)
-        if record is not None:
-            record.append((e0, e1, e2, e3, e4))
+    spans = {"rollout": ("rollout0", "rollout1"), "advantage": ("adv0", "adv1"), "vf_fit": ("vf0", "vf1"),
+             "trpo_update": ("upd0", "upd1")}
+    recs = []
 
     for _ in range(args.warmup):
-        iteration(None)
+        runner.step()
+    runner.drain()
     timing.enable(True)
-    rec = []
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    # K whole iterations: K rollouts, advantages, VF fits and policy updates (the last
+    # VF fit drains inside the timed region)
     for _ in range(args.steps):
-        iteration(rec)
+        runner.step()
+        recs.append(runner.last_phase_events)
+    runner.drain()
+    recs.append(runner.last_drain_events if runner.pipeline else {})
     torch.cuda.synchronize()
     comm.barrier()
     elapsed = time.perf_counter() - t0
@@ -161,11 +153,10 @@ def main():
         elapsed = float(t.item())
     kern = timing.summary()
     timing.enable(False)
-    for (e0, e1, e2, e3, e4) in rec:
-        phases["rollout"] += e0.elapsed_time(e1)
-        phases["advantage"] += e1.elapsed_time(e2)
-        phases["vf_fit"] += e2.elapsed_time(e3)
-        phases["trpo_update"] += e3.elapsed_time(e4)
+    for ev in recs:
+        for k, (a, b) in spans.items():
+            if a in ev and b in ev:
+                phases[k] += ev[a].elapsed_time(ev[b])
     K = args.steps
     n_local = E * Tn
     total_steps = n_local * world * K
@@ -205,7 +196,8 @@ def main():
                    "policy": f"{env.obs_dim}-{'-'.join(map(str, hid))}-{env.act_dim} tanh DiagGauss "
                              f"({'layered GEMM' if agent.policy.net.layered else 'fused'} path)",
                    "gamma": 0.995, "lam": 0.97,
-                   "max_kl": 0.01, "cg_damping": 0.1},
+                   "max_kl": 0.01, "cg_damping": 0.1,
+                   "vf_fit_beside_next_rollout": runner.pipeline},
         "trpo_iters_per_sec": round(K / elapsed, 4),
         "rollout_env_steps_per_sec": round(n_local * world * K / (phases["rollout"] * 1e-3), 1),
         "phase_ms_per_iter": {k: round(v / K, 3) for k, v in phases.items()},

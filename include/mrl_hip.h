@@ -302,6 +302,16 @@ int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, cons
  * iteration counter (obs_T is never pushed: the horizon cuts the episode) */
 int mrl_rollout_finish(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void* stream);
 
+/* ---------------------------------------------------------------- streams
+ * CU-masked HIP streams for the iteration pipeline (the rollout of iteration k+1
+ * and the VF fit of iteration k run at once on disjoint CU sets).  No reference
+ * counterpart: the reference runs single-threaded on the CPU (core.py:135-171).
+ * mask: `words` 32-bit words, bit i = CU i (hipExtStreamCreateWithCUMask). */
+int mrl_device_cu_count(int32_t* out);
+int mrl_stream_create_cu_mask(const uint32_t* mask, int32_t words, void** stream_out);
+int mrl_stream_get_cu_mask(void* stream, int32_t words, uint32_t* mask);
+int mrl_stream_destroy(void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -82,6 +82,10 @@ SIGNATURES = {
     "mrl_cg_update": (i32, [vp, f64, f64, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_trpo_step": (i32, [vp, vp, vp, f64, f64, i64, vp, vp, vp]),
     "mrl_trpo_step_ax": (i32, [vp, vp, vp, f64, i64, vp, vp, vp]),
+    "mrl_device_cu_count": (i32, [vp]),
+    "mrl_stream_create_cu_mask": (i32, [vp, i32, vp]),
+    "mrl_stream_get_cu_mask": (i32, [vp, i32, vp]),
+    "mrl_stream_destroy": (i32, [vp]),
     "mrl_axpy_cast": (i32, [vp, vp, f64, i64, vp, vp]),
     "mrl_cast_scale_f32_f64": (i32, [vp, f64, i64, vp, vp]),
     "mrl_adam_step": (i32, [vp, vp, vp, vp, f64, f64, f64, f64, i64, vp]),

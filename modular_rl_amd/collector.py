@@ -79,6 +79,7 @@ class Batch:
         self.obs, self.act, self.prob, self.rew, self.flags, self.ep_t = obs, act, prob, rew, flags, ep_t
         self.T, self.E = T, E
         self.adv = self.ret = self.vpred = None
+        self.vf_x = None  # (VF features tensor, NnVf feature generation) set by NnVf.predict_batch
         self.episode = None
 
     @staticmethod
@@ -222,7 +223,12 @@ class Collector:
         self.graph = None
 
     def collect(self):
-        fs_start = self.filter_state[:self.FS].clone() if self.comm.enabled else None
+        self.launch()
+        return self.finish()
+
+    def launch(self):
+        """Issue one iteration's rollout on the current stream (asynchronous)."""
+        self._fs_start = self.filter_state[:self.FS].clone() if self.comm.enabled else None
         if self.use_graph and self.noise is None:
             if self.graph is None:
                 # captured launches are recorded, not executed: state is untouched by the capture
@@ -232,10 +238,12 @@ class Collector:
             self.graph.replay()
         else:
             self._launch_all()
+
+    def finish(self):
+        """Cross-rank filter merge (waits for the rollout) and the iteration's Batch."""
         if self.comm.enabled:
-            self._merge_filter_across_ranks(fs_start)
-        b = Batch(self.N, self.obs, self.act, self.prob, self.rew, self.flags, self.ep_t, T=self.T, E=self.E)
-        return b
+            self._merge_filter_across_ranks(self._fs_start)
+        return Batch(self.N, self.obs, self.act, self.prob, self.rew, self.flags, self.ep_t, T=self.T, E=self.E)
 
     # ------------------------------------------------------------ filter state
     def _merge_filter_across_ranks(self, fs_start):

@@ -124,6 +124,7 @@ PG_OPTIONS = [
     ("n_envs", int, 1, "envs stepped in lock-step per GPU"),
     ("horizon", int, 0, "steps per env per iteration (0: ceil(timesteps_per_batch / n_envs))"),
     ("use_graph", int, 1, "replay the rollout's per-step launches from one captured hipGraph"),
+    ("pipeline", int, 1, "run the VF fit of iteration k beside the rollout of iteration k+1 on disjoint CUs"),
 ]
 
 
@@ -142,19 +143,140 @@ def run_policy_gradient_algorithm(env, agent, usercfg=None, callback=None):
         raise NotImplementedError("parallel rollouts: launch one process per GPU with torchrun instead")
     comm = agent.comm
     collector = agent.make_collector(env, cfg)
+    runner = IterationRunner(agent, collector, cfg, comm, pipeline=bool(cfg["pipeline"]))
     tstart = time.time()
-    for _ in range(cfg["n_iter"]):
-        batch = collector.collect()
-        compute_advantage_batch(agent.baseline, batch, cfg["gamma"], cfg["lam"], comm)
-        vf_stats = agent.baseline.fit_batch(batch)
-        pol_stats = agent.updater.update(batch)
-        stats = OrderedDict()
-        stats.update(collector.episode_stats(batch))
-        add_prefixed_stats(stats, "vf", vf_stats)
-        add_prefixed_stats(stats, "pol", pol_stats)
+
+    def emit(stats):
         stats["TimeElapsed"] = time.time() - tstart
         if callback:
             callback(stats)
+
+    for _ in range(cfg["n_iter"]):
+        done = runner.step()
+        if done is not None:
+            emit(done)
+    done = runner.drain()
+    if done is not None:
+        emit(done)
+
+
+def rollout_cu_split(n_blocks, n_cus):
+    """(rollout CUs, fit CUs) for the pipelined loop, or None when the rollout needs
+    too many CUs for a split to pay.  The rollout step kernel runs one block per CU
+    (one wave per SIMD: its latency chain wants no co-resident waves); the VF fit
+    gets every other CU."""
+    if n_blocks <= 0 or 2 * n_blocks > n_cus:
+        return None
+    r = list(range(n_blocks))
+    return r, list(range(n_blocks, n_cus))
+
+
+class IterationRunner:
+    """One iteration of `core.py:146-157` per ``step()``: rollout -> compute_advantage
+    -> VF fit -> policy update -> stats.
+
+    ``pipeline``: the VF fit of iteration k is deferred and run on a CU-masked stream
+    while iteration k+1's rollout runs on the disjoint CU set (streams.masked_stream).
+    The dependencies are exactly the sequential ones -- the rollout of k+1 needs the
+    policy after update k (not the VF); compute_advantage of k+1 needs the VF after
+    fit k (so it waits for the fit); fit k reads only iteration k's features, target,
+    returns and V_old, which nothing of iteration k+1 overwrites before it -- so every
+    kernel sees the same inputs as in the reference order and the results are
+    bit-identical to ``pipeline=False``.  ``step()`` returns the stats of the iteration
+    whose VF fit finished during it (pipelined: the previous one) and ``drain()`` the
+    last one."""
+
+    def __init__(self, agent, collector, cfg, comm=None, pipeline=True):
+        self.agent, self.col, self.cfg = agent, collector, cfg
+        self.comm = comm if comm is not None else Comm()
+        self.pending = None
+        self.pipeline = False
+        self.last_phase_events = None
+        self.last_drain_events = {}
+        if pipeline and torch.cuda.is_available() and not collector.layered:
+            from . import streams
+            split = rollout_cu_split(collector.NB, streams.cu_count())
+            if split is not None:
+                self.rollout_stream = streams.masked_stream(split[0])
+                self.fit_stream = streams.masked_stream(split[1])
+                self.pipeline = True
+
+    @staticmethod
+    def _stats(ep, vf_stats, pol_stats):
+        stats = OrderedDict()
+        stats.update(ep)
+        add_prefixed_stats(stats, "vf", vf_stats)
+        add_prefixed_stats(stats, "pol", pol_stats)
+        return stats
+
+    def _event(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def step(self):
+        cfg, agent, col = self.cfg, self.agent, self.col
+        main = torch.cuda.current_stream()
+        ev = {}
+        done = None
+        if self.pipeline:
+            self.rollout_stream.wait_stream(main)
+            with torch.cuda.stream(self.rollout_stream):
+                ev["rollout0"] = self._event()
+                col.launch()
+                ev["rollout1"] = self._event()
+            if self.pending is not None:
+                done = self._fit_pending(self.fit_stream, ev)
+            main.wait_stream(self.rollout_stream)
+        else:
+            ev["rollout0"] = self._event()
+            col.launch()
+            ev["rollout1"] = self._event()
+        batch = col.finish()
+        ev["adv0"] = self._event()
+        compute_advantage_batch(agent.baseline, batch, cfg["gamma"], cfg["lam"], self.comm)
+        ev["adv1"] = self._event()
+        vf_stats = None
+        if not self.pipeline:
+            ev["vf0"] = self._event()
+            vf_stats = agent.baseline.fit_batch(batch)
+            ev["vf1"] = self._event()
+        ev["upd0"] = self._event()
+        pol_stats = agent.updater.update(batch)
+        ev["upd1"] = self._event()
+        ep = col.episode_stats(batch)
+        if self.pipeline:
+            self.pending = (batch, ep, pol_stats)
+        else:
+            done = self._stats(ep, vf_stats, pol_stats)
+        self.last_phase_events = ev
+        return done
+
+    def _fit_pending(self, fit_stream, ev):
+        batch, ep, pol_stats = self.pending
+        self.pending = None
+        main = torch.cuda.current_stream()
+        if fit_stream is None:
+            ev["vf0"] = self._event()
+            vf_stats = self.agent.baseline.fit_batch(batch)
+            ev["vf1"] = self._event()
+        else:
+            fit_stream.wait_stream(main)
+            with torch.cuda.stream(fit_stream):
+                ev["vf0"] = self._event()
+                vf_stats = self.agent.baseline.fit_batch(batch)
+                ev["vf1"] = self._event()
+            main.wait_stream(fit_stream)
+        return self._stats(ep, vf_stats, pol_stats)
+
+    def drain(self):
+        """Fit the deferred VF of the last iteration (on all CUs) and return its stats."""
+        if self.pending is None:
+            return None
+        ev = {}
+        done = self._fit_pending(None, ev)
+        self.last_drain_events = ev
+        return done
 
 
 # ================================================================ per-path API

@@ -23,10 +23,16 @@ namespace mrl {
 // shuffle scan, and each thread re-runs its chunk from the carried-in value and
 // writes adv / ret.  Horizons longer than GAE_NC * L run as segments from the
 // last to the first, the carry held by the env's scan wave.
-constexpr int GAE_EB = 16;               // envs per block: one 64 B row segment
+#ifndef MRL_GAE_EB
+#define MRL_GAE_EB 16
+#endif
+#ifndef MRL_GAE_LMAX
+#define MRL_GAE_LMAX 32
+#endif
+constexpr int GAE_EB = MRL_GAE_EB;       // envs per block: one 64 B row segment
 constexpr int GAE_NC = 32;               // chunks per segment: one per lane of a half-wave
 constexpr int GAE_THREADS = GAE_EB * GAE_NC;
-constexpr int GAE_LMAX = 32;
+constexpr int GAE_LMAX = MRL_GAE_LMAX;
 constexpr int GAE_PITCH = GAE_EB + 1;    // LDS row pitch (doubles): 2-way conflicts at most
 
 template <int L>
@@ -399,49 +405,121 @@ __global__ void moments_kernel(const float* __restrict__ a, const float* __restr
   }
 }
 
-// episode statistics over time-major rows (core.py:31-44): one thread per env scans
-// its rows in time order; part[block][8] = (n_ep, sum R, sum R^2, max R, sum L, max L, sum r, 0)
-__global__ void episode_stats_kernel(const float* __restrict__ rew, const uint8_t* __restrict__ flags, int64_t T,
-                                     int64_t E, double* __restrict__ part) {
-  __shared__ double red[6][256];
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// episode statistics over time-major rows (core.py:31-44), blocked like the GAE scan:
+// thread (c, e) reads chunk c (L steps) of env e once, counts the episodes that start
+// and end inside its chunk and summarises the rest as (head: rows up to its first
+// episode end, tail: rows after its last); one walker thread per env then joins the
+// chunk summaries in time order, carrying the open episode across chunks and
+// segments.  part[block][8] = (n_ep, sum R, sum R^2, max R, sum L, max L, 0, 0)
+constexpr int EPS_EB = 16, EPS_NC = 32, EPS_THREADS = EPS_EB * EPS_NC, EPS_PITCH = EPS_EB + 1;
+
+struct EpAcc {
   double cnt = 0, sr = 0, sr2 = 0, mr = -INFINITY, sl = 0, ml = 0;
-  if (e < E) {
-    double ep = 0.0, len = 0.0;
-    for (int64_t t = 0; t < T; ++t) {
-      ep += (double)rew[t * E + e];
-      len += 1.0;
-      if (flags[t * E + e] & 1) {
-        cnt += 1.0;
-        sr += ep;
-        sr2 += ep * ep;
-        mr = fmax(mr, ep);
-        sl += len;
-        ml = fmax(ml, len);
-        ep = 0.0;
-        len = 0.0;
+  __device__ void add(double r, double len) {
+    cnt += 1.0;
+    sr += r;
+    sr2 += r * r;
+    mr = fmax(mr, r);
+    sl += len;
+    ml = fmax(ml, len);
+  }
+};
+
+template <int L>
+__global__ __launch_bounds__(EPS_THREADS) void episode_stats_kernel(const float* __restrict__ rew,
+                                                                    const uint8_t* __restrict__ flags, int64_t T,
+                                                                    int64_t E, double* __restrict__ part) {
+  __shared__ double sHR[EPS_NC * EPS_PITCH], sTR[EPS_NC * EPS_PITCH];
+  __shared__ int sHL[EPS_NC * EPS_PITCH], sTL[EPS_NC * EPS_PITCH];
+  __shared__ double red[6][EPS_THREADS / 64];
+  const int tid = threadIdx.x;
+  const int el = tid % EPS_EB, c = tid / EPS_EB;
+  const bool live = (int64_t)blockIdx.x * EPS_EB + el < E;
+  const int64_t S = (int64_t)EPS_NC * L;
+  const int64_t nseg = (T + S - 1) / S;
+  const int elc = (int)min((int64_t)el, E - 1 - (int64_t)blockIdx.x * EPS_EB);
+  EpAcc acc;
+  double open_r = 0.0;  // walker (tid < EPS_EB): the episode still open at the segment start
+  int open_len = 0;
+  for (int64_t seg = 0; seg < nseg; ++seg) {
+    const int64_t base = seg * S * E + (int64_t)blockIdx.x * EPS_EB;
+    const int64_t rows = min(S, T - seg * S);
+    float rr[L];
+    uint8_t ff[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int row = c * L + j;
+      const int rc = row < rows ? row : (int)rows - 1;
+      const uint32_t o = (uint32_t)rc * (uint32_t)E + (uint32_t)elc;
+      rr[j] = rew[base + o];
+      ff[j] = flags[base + o];
+    }
+    double cur = 0.0, hr = 0.0;
+    int clen = 0, hl = 0;
+    bool seen = false;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      if (live && c * L + j < rows) {
+        cur += (double)rr[j];
+        clen += 1;
+        if (ff[j] & 1) {
+          if (!seen) {
+            hr = cur;
+            hl = clen;
+            seen = true;
+          } else {
+            acc.add(cur, (double)clen);
+          }
+          cur = 0.0;
+          clen = 0;
+        }
       }
     }
-  }
-  red[0][threadIdx.x] = cnt;
-  red[1][threadIdx.x] = sr;
-  red[2][threadIdx.x] = sr2;
-  red[3][threadIdx.x] = mr;
-  red[4][threadIdx.x] = sl;
-  red[5][threadIdx.x] = ml;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-      for (int q = 0; q < 6; ++q) {
-        if (q == 3 || q == 5) red[q][threadIdx.x] = fmax(red[q][threadIdx.x], red[q][threadIdx.x + o]);
-        else red[q][threadIdx.x] += red[q][threadIdx.x + o];
+    // head = rows through the first end (or the whole chunk: tail length -1 marks "no end")
+    sHR[c * EPS_PITCH + el] = seen ? hr : cur;
+    sHL[c * EPS_PITCH + el] = seen ? hl : clen;
+    sTR[c * EPS_PITCH + el] = cur;
+    sTL[c * EPS_PITCH + el] = seen ? clen : -1;
+    __syncthreads();
+    if (tid < EPS_EB && live) {
+      for (int cc = 0; cc < EPS_NC; ++cc) {
+        const double h = sHR[cc * EPS_PITCH + tid];
+        const int hlen = sHL[cc * EPS_PITCH + tid];
+        const int tl = sTL[cc * EPS_PITCH + tid];
+        if (tl >= 0) {
+          acc.add(open_r + h, (double)(open_len + hlen));
+          open_r = sTR[cc * EPS_PITCH + tid];
+          open_len = tl;
+        } else {
+          open_r += h;
+          open_len += hlen;
+        }
       }
     }
     __syncthreads();
   }
-  if (threadIdx.x < 6) part[blockIdx.x * 8 + threadIdx.x] = red[threadIdx.x][0];
-  if (threadIdx.x == 6) part[blockIdx.x * 8 + 6] = 0.0;
-  if (threadIdx.x == 7) part[blockIdx.x * 8 + 7] = 0.0;
+  // block reduction: sums and maxima
+  double v[6] = {acc.cnt, acc.sr, acc.sr2, acc.mr, acc.sl, acc.ml};
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const double o = __shfl_down(v[q], off);
+      v[q] = (q == 3 || q == 5) ? fmax(v[q], o) : v[q] + o;
+    }
+  }
+  const int lane = tid & 63, wave = tid >> 6;
+  if (lane == 0)
+    for (int q = 0; q < 6; ++q) red[q][wave] = v[q];
+  __syncthreads();
+  if (tid < 8) {
+    double r = 0.0;
+    if (tid < 6) {
+      r = (tid == 3 || tid == 5) ? -INFINITY : 0.0;
+      for (int w = 0; w < EPS_THREADS / 64; ++w) r = (tid == 3 || tid == 5) ? fmax(r, red[tid][w]) : r + red[tid][w];
+    }
+    part[blockIdx.x * 8 + tid] = r;
+  }
 }
 
 __global__ void episode_stats_final_kernel(const double* __restrict__ part, int64_t nb, double* __restrict__ out) {
@@ -584,15 +662,32 @@ int mrl_moments(const float* a, const float* b, int64_t n, double* out, void* wo
   return hip_check(hipGetLastError(), "mrl_moments");
 }
 
-int64_t mrl_episode_stats_workspace_bytes(int64_t E) { return ((E + 255) / 256) * 8 * (int64_t)sizeof(double); }
+int64_t mrl_episode_stats_workspace_bytes(int64_t E) {
+  return ((E + EPS_EB - 1) / EPS_EB) * 8 * (int64_t)sizeof(double);
+}
 
 int mrl_episode_stats(const float* rew, const uint8_t* flags, int64_t T, int64_t E, double* out, void* workspace,
                       void* stream) {
   if (!rew || !flags || !out || !workspace) return fail(E_ARG, "null pointer");
-  const int64_t nb = (E + 255) / 256;
+  if (T <= 0 || E <= 0) return fail(E_ARG, "mrl_episode_stats: empty batch");
+  if ((int64_t)EPS_NC * 32 * (E + EPS_EB) >= ((int64_t)1 << 32))
+    return fail(E_UNSUPPORTED, "mrl_episode_stats: E too large for 32-bit segment offsets");
+  const int64_t nb = (E + EPS_EB - 1) / EPS_EB;
   double* part = reinterpret_cast<double*>(workspace);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(episode_stats_kernel, dim3(nb), dim3(256), 0, s, rew, flags, T, E, part);
+  int L = 1;
+  while (L < 32 && (int64_t)EPS_NC * L < T) L <<= 1;
+#define MRL_EPS_LAUNCH(LL) \
+  hipLaunchKernelGGL(episode_stats_kernel<LL>, dim3(nb), dim3(EPS_THREADS), 0, s, rew, flags, T, E, part)
+  switch (L) {
+    case 1: MRL_EPS_LAUNCH(1); break;
+    case 2: MRL_EPS_LAUNCH(2); break;
+    case 4: MRL_EPS_LAUNCH(4); break;
+    case 8: MRL_EPS_LAUNCH(8); break;
+    case 16: MRL_EPS_LAUNCH(16); break;
+    default: MRL_EPS_LAUNCH(32); break;
+  }
+#undef MRL_EPS_LAUNCH
   hipLaunchKernelGGL(episode_stats_final_kernel, dim3(1), dim3(64), 0, s, part, nb, out);
   return hip_check(hipGetLastError(), "mrl_episode_stats");
 }

@@ -1,0 +1,43 @@
+"""CU-masked HIP streams (mrl_stream_create_cu_mask) wrapped as torch streams.
+
+Used by the pipelined training loop: the rollout of iteration k+1 (a chain of
+latency-bound step launches that occupy one block per CU on E/64 CUs) runs on one
+CU set while the value-function fit of iteration k runs on the complementary set.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import call
+
+
+def cu_count():
+    n = ctypes.c_int32(0)
+    call("mrl_device_cu_count", ctypes.byref(n))
+    return int(n.value)
+
+
+def masked_stream(cus):
+    """A new HIP stream restricted to the CU ids in ``cus`` (torch.cuda.ExternalStream).
+    The stream lives for the rest of the process."""
+    _lib.load(require_gpu=True)
+    n = cu_count()
+    words = (n + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for c in cus:
+        if not 0 <= c < n:
+            raise _lib.MrlError(f"CU id {c} out of range [0, {n})")
+        mask[c // 32] |= 1 << (c % 32)
+    out = ctypes.c_void_p()
+    call("mrl_stream_create_cu_mask", mask, words, ctypes.byref(out))
+    return torch.cuda.ExternalStream(out.value)
+
+
+def stream_cus(s):
+    """The CU ids a stream may use (hipExtStreamGetCUMask)."""
+    n = cu_count()
+    words = (n + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    call("mrl_stream_get_cu_mask", ctypes.c_void_p(s.cuda_stream), words, mask)
+    return [i for i in range(n) if (mask[i // 32] >> (i % 32)) & 1]

@@ -159,6 +159,7 @@ class NnVf:
     def __init__(self, net, timestep_limit, regression_params, comm=None):
         self.reg = NnRegression(net, comm=comm, **regression_params)
         self.timestep_limit = timestep_limit
+        self._feat_gen = 0
 
     @property
     def net(self):
@@ -178,16 +179,23 @@ class NnVf:
         every VF pass of the fit then reads plain rows instead of re-deriving the time
         feature per tile."""
         n = int(n)
+        self._feat_gen += 1
         X = self.net.ws.get("vf_features", n * self.net.n_in, torch.float32)
         call("mrl_concat_time", ptr(obs), ptr(ep_t), n, self.net.n_in - 1, float(self.timestep_limit), ptr(X), stream())
         return X
 
     def predict_batch(self, batch, out=None):
         X = self.features(batch.obs, batch.n, batch.ep_t)
+        # the fit of this batch reuses the features while no other batch's have replaced them
+        batch.vf_x = (X, self._feat_gen)
         return self.reg.predict(X, batch.n, None, 1.0, out=out)
 
     def fit_batch(self, batch):
-        X = self.features(batch.obs, batch.n, batch.ep_t)
+        cached = getattr(batch, "vf_x", None)
+        if cached is not None and cached[1] == self._feat_gen:
+            X = cached[0]
+        else:
+            X = self.features(batch.obs, batch.n, batch.ep_t)
         return self.reg.fit(X, batch.n, batch.ret, None, 1.0, ypredold=batch.vpred)
 
     def fit(self, paths):

@@ -1,0 +1,57 @@
+"""The pipelined iteration loop (VF fit of iteration k on a CU-masked stream beside
+the rollout of iteration k+1) against the reference order: every parameter, filter
+statistic and reported stat is bit-identical."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(env_id, pipeline, n_iter=3, agent_cls="TrpoAgent", **kw):
+    from modular_rl_amd import agentzoo
+    from modular_rl_amd.core import IterationRunner
+    from modular_rl_amd.envs import make
+    env = make(env_id)
+    cfg = dict(timestep_limit=env.spec.max_episode_steps, gamma=0.995, lam=0.97, max_kl=0.01, cg_damping=0.1,
+               n_envs=256, horizon=64, seed=3, use_graph=1)
+    cfg.update(kw)
+    agent = getattr(agentzoo, agent_cls)(env.observation_space, env.action_space, cfg)
+    col = agent.make_collector(env, cfg)
+    runner = IterationRunner(agent, col, cfg, pipeline=pipeline)
+    stats = []
+    for _ in range(n_iter):
+        s = runner.step()
+        if s is not None:
+            stats.append(s)
+    s = runner.drain()
+    if s is not None:
+        stats.append(s)
+    torch.cuda.synchronize()
+    return runner, agent, col, stats
+
+
+@pytest.mark.parametrize("env_id,agent_cls", [("Hopper-v2", "TrpoAgent"), ("CartPole-v0", "TrpoAgent"),
+                                              ("Hopper-v2", "PpoLbfgsAgent")])
+def test_pipelined_loop_is_bit_identical(env_id, agent_cls):
+    r0, a0, c0, s0 = _run(env_id, False, agent_cls=agent_cls)
+    r1, a1, c1, s1 = _run(env_id, True, agent_cls=agent_cls)
+    assert not r0.pipeline and r1.pipeline  # 256 envs = 4 rollout blocks: the CU split applies
+    assert len(s0) == len(s1) == 3
+    np.testing.assert_array_equal(a0.policy.net.get_flat(), a1.policy.net.get_flat())
+    np.testing.assert_array_equal(a0.baseline.net.get_flat(), a1.baseline.net.get_flat())
+    np.testing.assert_array_equal(c0.filter_state.cpu().numpy(), c1.filter_state.cpu().numpy())
+    for x, y in zip(s0, s1):
+        assert list(x) == list(y)
+        for k in x:
+            assert x[k] == y[k] or (np.isnan(x[k]) and np.isnan(y[k])), k
+
+
+def test_masked_streams_are_disjoint():
+    from modular_rl_amd import streams
+    from modular_rl_amd.core import rollout_cu_split
+    n = streams.cu_count()
+    rc, vc = rollout_cu_split(64, n)
+    R, V = streams.masked_stream(rc), streams.masked_stream(vc)
+    assert streams.stream_cus(R) == rc and streams.stream_cus(V) == vc
+    assert rollout_cu_split(n, n) is None

@@ -198,3 +198,35 @@ def test_vf_fit_matches_oracle():
         np.testing.assert_allclose(st[k], st_w[k], rtol=2e-4, atol=1e-6, err_msg=k)
     th1 = net.get_flat().astype(np.float64)
     assert np.abs(th1 - th_w).max() <= 1e-3 * np.abs(th_w - th).max()
+
+
+@pytest.mark.parametrize("Tn,E", [(1, 1), (37, 5), (200, 64), (1024, 4096), (2500, 19)])
+def test_episode_stats_matches_oracle(Tn, E):
+    """mrl_episode_stats (the add_episode_stats scalars, core.py:31-44) vs the oracle on
+    the same rows split into paths; multi-segment horizons included."""
+    from modular_rl_amd import _lib
+    from modular_rl_amd._lib import call, ptr, stream
+    rng = np.random.default_rng(Tn + 7 * E)
+    rew = rng.standard_normal((Tn, E)).astype(np.float32)
+    last = rng.random((Tn, E)) < 0.02
+    last[-1] = True
+    flags = last.astype(np.uint8) | ((last & (rng.random((Tn, E)) < 0.5)).astype(np.uint8) << 1)
+    ws = torch.zeros(int(_lib.load().mrl_episode_stats_workspace_bytes(E)) // 8 + 1, dtype=torch.float64).cuda()
+    out = torch.zeros(8, dtype=torch.float64).cuda()
+    call("mrl_episode_stats", ptr(_dev(rew.reshape(-1))), ptr(_dev(flags.reshape(-1), torch.uint8)), Tn, E, ptr(out),
+         ptr(ws), stream())
+    cnt, sr, sr2, mr, sl, ml = out[:6].cpu().numpy()
+    paths = []
+    for e in range(E):
+        ends = np.nonzero(last[:, e])[0]
+        start = 0
+        for t in ends:
+            paths.append(dict(reward=rew[start:t + 1, e].astype(np.float64)))
+            start = t + 1
+    st = {}
+    T.add_episode_stats(st, paths)
+    assert int(cnt) == st["NumEpBatch"]
+    np.testing.assert_allclose(sr / cnt, st["EpRewMean"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(np.sqrt(max(sr2 / cnt - (sr / cnt) ** 2, 0.0)), st["EpisodeRewards"].std(), rtol=1e-6)
+    np.testing.assert_allclose(mr, st["EpRewMax"], rtol=1e-12)
+    assert sl / cnt == st["EpLenMean"] and ml == st["EpLenMax"] and sl == st["EpisodeLengths"].sum()
