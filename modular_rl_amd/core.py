@@ -160,15 +160,19 @@ def run_policy_gradient_algorithm(env, agent, usercfg=None, callback=None):
         emit(done)
 
 
-def rollout_cu_split(n_blocks, n_cus):
+LAYERED_ROLLOUT_CUS = 64
+
+
+def rollout_cu_split(n_rollout, n_cus):
     """(rollout CUs, fit CUs) for the pipelined loop, or None when the rollout needs
-    too many CUs for a split to pay.  The rollout step kernel runs one block per CU
-    (one wave per SIMD: its latency chain wants no co-resident waves); the VF fit
-    gets every other CU."""
-    if n_blocks <= 0 or 2 * n_blocks > n_cus:
+    too many CUs for a split to pay.  The fused rollout step kernel runs one block per
+    CU (one wave per SIMD: its latency chain wants no co-resident waves), so it gets
+    as many CUs as it has blocks; the layered rollout's per-step GEMMs over E rows use
+    a few dozen tiles and get LAYERED_ROLLOUT_CUS.  The VF fit gets every other CU."""
+    if n_rollout <= 0 or 2 * n_rollout > n_cus:
         return None
-    r = list(range(n_blocks))
-    return r, list(range(n_blocks, n_cus))
+    r = list(range(n_rollout))
+    return r, list(range(n_rollout, n_cus))
 
 
 class IterationRunner:
@@ -193,12 +197,17 @@ class IterationRunner:
         self.pipeline = False
         self.last_phase_events = None
         self.last_drain_events = {}
-        if pipeline and torch.cuda.is_available() and not collector.layered:
+        if pipeline and torch.cuda.is_available():
             from . import streams
-            split = rollout_cu_split(collector.NB, streams.cu_count())
+            need = LAYERED_ROLLOUT_CUS if collector.layered else collector.NB
+            split = rollout_cu_split(need, streams.cu_count())
             if split is not None:
                 self.rollout_stream = streams.masked_stream(split[0])
                 self.fit_stream = streams.masked_stream(split[1])
+                # the iteration's own work runs on a non-blocking stream: an event recorded
+                # on the legacy NULL stream would wait for the rollout stream's work and
+                # serialise the fit behind it
+                self.main_stream = torch.cuda.Stream()
                 self.pipeline = True
 
     @staticmethod
@@ -214,7 +223,20 @@ class IterationRunner:
         e.record()
         return e
 
+    def _on_main(self, fn):
+        if not self.pipeline:
+            return fn()
+        caller = torch.cuda.current_stream()
+        self.main_stream.wait_stream(caller)
+        with torch.cuda.stream(self.main_stream):
+            out = fn()
+        caller.wait_stream(self.main_stream)
+        return out
+
     def step(self):
+        return self._on_main(self._step)
+
+    def _step(self):
         cfg, agent, col = self.cfg, self.agent, self.col
         main = torch.cuda.current_stream()
         ev = {}
@@ -274,7 +296,7 @@ class IterationRunner:
         if self.pending is None:
             return None
         ev = {}
-        done = self._fit_pending(None, ev)
+        done = self._on_main(lambda: self._fit_pending(None, ev))
         self.last_drain_events = ev
         return done
 

@@ -31,12 +31,14 @@ def _run(env_id, pipeline, n_iter=3, agent_cls="TrpoAgent", **kw):
     return runner, agent, col, stats
 
 
-@pytest.mark.parametrize("env_id,agent_cls", [("Hopper-v2", "TrpoAgent"), ("CartPole-v0", "TrpoAgent"),
-                                              ("Hopper-v2", "PpoLbfgsAgent")])
-def test_pipelined_loop_is_bit_identical(env_id, agent_cls):
-    r0, a0, c0, s0 = _run(env_id, False, agent_cls=agent_cls)
-    r1, a1, c1, s1 = _run(env_id, True, agent_cls=agent_cls)
-    assert not r0.pipeline and r1.pipeline  # 256 envs = 4 rollout blocks: the CU split applies
+@pytest.mark.parametrize("env_id,agent_cls,kw", [("Hopper-v2", "TrpoAgent", {}), ("CartPole-v0", "TrpoAgent", {}),
+                                                 ("Hopper-v2", "PpoLbfgsAgent", {}),
+                                                 ("Humanoid-v2", "TrpoAgent", dict(n_envs=128, horizon=16,
+                                                                                   hid_sizes=[128, 96]))])
+def test_pipelined_loop_is_bit_identical(env_id, agent_cls, kw):
+    r0, a0, c0, s0 = _run(env_id, False, agent_cls=agent_cls, **kw)
+    r1, a1, c1, s1 = _run(env_id, True, agent_cls=agent_cls, **kw)
+    assert not r0.pipeline and r1.pipeline  # few rollout blocks: the CU split applies
     assert len(s0) == len(s1) == 3
     np.testing.assert_array_equal(a0.policy.net.get_flat(), a1.policy.net.get_flat())
     np.testing.assert_array_equal(a0.baseline.net.get_flat(), a1.baseline.net.get_flat())

@@ -213,8 +213,8 @@ def test_episode_stats_matches_oracle(Tn, E):
     flags = last.astype(np.uint8) | ((last & (rng.random((Tn, E)) < 0.5)).astype(np.uint8) << 1)
     ws = torch.zeros(int(_lib.load().mrl_episode_stats_workspace_bytes(E)) // 8 + 1, dtype=torch.float64).cuda()
     out = torch.zeros(8, dtype=torch.float64).cuda()
-    call("mrl_episode_stats", ptr(_dev(rew.reshape(-1))), ptr(_dev(flags.reshape(-1), torch.uint8)), Tn, E, ptr(out),
-         ptr(ws), stream())
+    rew_d, flags_d = _dev(rew.reshape(-1)), _dev(flags.reshape(-1), torch.uint8)  # alive until the kernel has run
+    call("mrl_episode_stats", ptr(rew_d), ptr(flags_d), Tn, E, ptr(out), ptr(ws), stream())
     cnt, sr, sr2, mr, sl, ml = out[:6].cpu().numpy()
     paths = []
     for e in range(E):
