@@ -190,11 +190,17 @@ class Collector:
                                 ptr(self.noise if self.noise is not None else self._noise_rows), ptr(self.stamps),
                                 ptr(self.raw_obs))
 
+    def fill_noise(self):
+        """This iteration's sampling noise, one parallel draw over every row (no-op when
+        noise is injected).  Issued outside the captured step graph so the pipelined
+        loop can run it on all CUs while the step chain runs on the rollout's CU set."""
+        if self.noise is None:
+            call("mrl_rollout_noise", ctypes.byref(self.desc), ctypes.byref(self._bufs()), ptr(self._noise_rows),
+                 stream())
+
     def _launch_all(self):
         bufs = self._bufs()
         net = self.policy.net
-        if self.noise is None:  # this iteration's sampling noise, one parallel draw
-            call("mrl_rollout_noise", ctypes.byref(self.desc), ctypes.byref(bufs), ptr(self._noise_rows), stream())
         if self.layered:
             return self._launch_all_layered(bufs, net)
         call("mrl_rollout_pack", ctypes.byref(self.desc), ctypes.byref(net.desc), ptr(net.theta), ptr(self._rimage),
@@ -226,8 +232,11 @@ class Collector:
         self.launch()
         return self.finish()
 
-    def launch(self):
-        """Issue one iteration's rollout on the current stream (asynchronous)."""
+    def launch(self, fill_noise=True):
+        """Issue one iteration's rollout on the current stream (asynchronous);
+        ``fill_noise=False``: the caller already issued fill_noise() in stream order."""
+        if fill_noise:
+            self.fill_noise()
         self._fs_start = self.filter_state[:self.FS].clone() if self.comm.enabled else None
         if self.use_graph and self.noise is None:
             if self.graph is None:

@@ -242,10 +242,11 @@ class IterationRunner:
         ev = {}
         done = None
         if self.pipeline:
+            ev["rollout0"] = self._event()
+            col.fill_noise()  # one wide kernel: on every CU, ahead of the step chain
             self.rollout_stream.wait_stream(main)
             with torch.cuda.stream(self.rollout_stream):
-                ev["rollout0"] = self._event()
-                col.launch()
+                col.launch(fill_noise=False)
                 ev["rollout1"] = self._event()
             if self.pending is not None:
                 done = self._fit_pending(self.fit_stream, ev)

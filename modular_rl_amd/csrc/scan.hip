@@ -523,15 +523,26 @@ __global__ __launch_bounds__(EPS_THREADS) void episode_stats_kernel(const float*
 }
 
 __global__ void episode_stats_final_kernel(const double* __restrict__ part, int64_t nb, double* __restrict__ out) {
-  if (threadIdx.x != 0) return;
+  // one wave: lane-strided partial sums / maxima over the blocks, then a shuffle tree
+  const int lane = threadIdx.x;
   double a[6] = {0, 0, 0, -INFINITY, 0, 0};
-  for (int64_t b = 0; b < nb; ++b) {
+  for (int64_t b = lane; b < nb; b += 64) {
+#pragma unroll
     for (int q = 0; q < 6; ++q) {
       const double v = part[b * 8 + q];
       a[q] = (q == 3 || q == 5) ? fmax(a[q], v) : a[q] + v;
     }
   }
-  for (int q = 0; q < 6; ++q) out[q] = a[q];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const double o = __shfl_down(a[q], off);
+      a[q] = (q == 3 || q == 5) ? fmax(a[q], o) : a[q] + o;
+    }
+  }
+  if (lane == 0)
+    for (int q = 0; q < 6; ++q) out[q] = a[q];
 }
 
 static inline int64_t grid_for(int64_t n, int64_t bs = 256, int64_t cap = 2048) {
