@@ -20,6 +20,19 @@ namespace mrl {
 // accumulator register r of lane half h -> row index inside a 32-row C tile
 __host__ __device__ inline int cperm(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// The dispatcher deals consecutive block ids round-robin to the 8 XCDs (8 L2s).
+// For kernels whose blocks own adjacent column segments of one row-major array,
+// give each XCD a contiguous run of segments so a 128 B line shared by two
+// neighbouring segments is fetched into one L2 only.  Identity unless nb % 8 == 0.
+__device__ inline int64_t xcd_segment(int64_t b, int64_t nb) {
+#ifdef MRL_NO_XCD_SEGMENT  // ablation build (tools/build_ablate.sh)
+  (void)nb;
+  return b;
+#else
+  return (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b;
+#endif
+}
+
 void set_error(const std::string& s);
 int fail(int code, const std::string& s);
 int hip_check(hipError_t e, const char* what);

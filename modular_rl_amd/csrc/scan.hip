@@ -47,7 +47,8 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_scan_kernel(const float* __re
   __shared__ double red[2][GAE_THREADS / 64];
   const int tid = threadIdx.x;
   const int el = tid % GAE_EB, c = tid / GAE_EB;
-  const int64_t e = (int64_t)blockIdx.x * GAE_EB + el;
+  const int64_t blk = xcd_segment(blockIdx.x, gridDim.x);  // env segment of this block
+  const int64_t e = blk * GAE_EB + el;
   const bool live = e < E;
   const double gl = gamma * lam;
   const int64_t S = (int64_t)GAE_NC * L;
@@ -59,14 +60,14 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_scan_kernel(const float* __re
   for (int64_t seg = nseg - 1; seg >= 0; --seg) {
     const int64_t t0 = seg * S + (int64_t)c * L;
     // uniform segment/block base + 32-bit per-lane offsets (S * E < 2^29, checked on the host)
-    const int64_t base = seg * S * E + (int64_t)blockIdx.x * GAE_EB;
+    const int64_t base = seg * S * E + blk * GAE_EB;
     const float* rb = rew + base;
     const float* vb = v + base;
     const uint8_t* fb = flags + base;
     // branch-free loads: rows past T and envs past E read a clamped valid element
     // and are masked where they are used
     const int64_t rows = min(S, T - seg * S);  // rows of this segment
-    const int elc = (int)min((int64_t)el, E - 1 - (int64_t)blockIdx.x * GAE_EB);
+    const int elc = (int)min((int64_t)el, E - 1 - blk * GAE_EB);
     auto off = [&](int row) -> uint32_t {  // byte offset of (row, env) from the base, float elements
       const int rc = row < rows ? row : (int)rows - 1;
       return ((uint32_t)rc * (uint32_t)E + (uint32_t)elc) * 4u;
@@ -176,8 +177,8 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_scan_kernel(const float* __re
       t1 += red[0][w];
       t2 += red[1][w];
     }
-    part[blockIdx.x * 2 + 0] = t1;
-    part[blockIdx.x * 2 + 1] = t2;
+    part[blk * 2 + 0] = t1;
+    part[blk * 2 + 1] = t2;
   }
 }
 
@@ -434,15 +435,16 @@ __global__ __launch_bounds__(EPS_THREADS) void episode_stats_kernel(const float*
   __shared__ double red[6][EPS_THREADS / 64];
   const int tid = threadIdx.x;
   const int el = tid % EPS_EB, c = tid / EPS_EB;
-  const bool live = (int64_t)blockIdx.x * EPS_EB + el < E;
+  const int64_t blk = xcd_segment(blockIdx.x, gridDim.x);  // env segment of this block
+  const bool live = blk * EPS_EB + el < E;
   const int64_t S = (int64_t)EPS_NC * L;
   const int64_t nseg = (T + S - 1) / S;
-  const int elc = (int)min((int64_t)el, E - 1 - (int64_t)blockIdx.x * EPS_EB);
+  const int elc = (int)min((int64_t)el, E - 1 - blk * EPS_EB);
   EpAcc acc;
   double open_r = 0.0;  // walker (tid < EPS_EB): the episode still open at the segment start
   int open_len = 0;
   for (int64_t seg = 0; seg < nseg; ++seg) {
-    const int64_t base = seg * S * E + (int64_t)blockIdx.x * EPS_EB;
+    const int64_t base = seg * S * E + blk * EPS_EB;
     const int64_t rows = min(S, T - seg * S);
     float rr[L];
     uint8_t ff[L];
@@ -518,7 +520,7 @@ __global__ __launch_bounds__(EPS_THREADS) void episode_stats_kernel(const float*
       r = (tid == 3 || tid == 5) ? -INFINITY : 0.0;
       for (int w = 0; w < EPS_THREADS / 64; ++w) r = (tid == 3 || tid == 5) ? fmax(r, red[tid][w]) : r + red[tid][w];
     }
-    part[blockIdx.x * 8 + tid] = r;
+    part[blk * 8 + tid] = r;
   }
 }
 
