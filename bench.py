@@ -48,6 +48,8 @@ def flops_per_row(net):
     return {"fvp_jvp_rows": 2 * sum(mm) + jvp, "fvp_vjp": vjp}
 
 
+DYNAMICS = {"Hopper-v2": "hopper.xml articulated-body dynamics", "Humanoid-v2": "surrogate dynamics",
+            "CartPole-v0": "gym equations"}
 GAE_BYTES_PER_ROW = 17  # read r 4 + v 4 + flags 1, write adv 4 + ret 4
 
 
@@ -190,7 +192,7 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": K,
         "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1000, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-        "config": {"workload": f"{args.env} (surrogate dynamics) {E} envs x {Tn} steps per GPU, one TRPO iteration "
+        "config": {"workload": f"{args.env} ({DYNAMICS[args.env]}) {E} envs x {Tn} steps per GPU, one TRPO iteration "
                                "per step (rollout+GAE+VF L-BFGS+TRPO CG/linesearch)",
                    "envs_per_gpu": E, "horizon": Tn, "global_batch": E * Tn * world, "parallelism": f"dp{world}",
                    "policy": f"{env.obs_dim}-{'-'.join(map(str, hid))}-{env.act_dim} tanh DiagGauss "

@@ -238,7 +238,7 @@ int64_t mrl_episode_stats_workspace_bytes(int64_t E);
  * device for T steps.  Per step the E new observations are merged into the running
  * stat (Chan merge of per-block Welford partials in block order), then normalised. */
 #define MRL_ENV_CARTPOLE 0  /* CartPole-v0 equations (gym), k = 2            */
-#define MRL_ENV_HOPPER 1    /* Hopper-v2-shaped surrogate, obs 11 / act 3     */
+#define MRL_ENV_HOPPER 1    /* Hopper-v2: hopper.xml articulated body, obs 11 / act 3 */
 #define MRL_ENV_HUMANOID 2  /* Humanoid-v2-shaped surrogate, obs 376 / act 17 (layered rollout only) */
 
 typedef struct {

@@ -7,9 +7,9 @@
 //  * Humanoid: a Humanoid-v2-SHAPED surrogate (376-d obs, 17-d action in [-.4, .4],
 //    frame_skip 5 x dt 0.003, 1.25 v + 5 alive - 0.1|a|^2 - impact, 1 < z < 2), a
 //    sagittal two-leg contact model with 17 damped actuated joints (oracle/envs.py).
-//  * Hopper: a Hopper-v2-SHAPED surrogate (11-d obs, 3-d action, gear 200,
-//    frame_skip 4, forward-velocity reward, Hopper-v2 health test).  MuJoCo is not
-//    available, so its planar leg dynamics are a cost-representative stand-in.
+//  * Hopper-v2: gym's hopper.xml as planar articulated rigid-body dynamics with
+//    compliant ground contact (11-d obs, 3-d action, gear 200, frame_skip 4,
+//    forward-velocity reward, Hopper-v2 health test); MuJoCo itself is absent.
 #pragma once
 #include "mrl_common.h"
 
@@ -50,13 +50,37 @@ __device__ inline void cartpole_obs(const double* s, double* o) {
   for (int i = 0; i < 4; ++i) o[i] = s[i];
 }
 
-// ------------------------------------------------------------------ Hopper surrogate
+// ------------------------------------------------------------------ Hopper-v2
+// gym's hopper.xml as planar articulated rigid-body dynamics (oracle/envs.py has
+// the model, its constants and this exact operation order):
+// q = (rootx, rootz, rooty, thigh, leg, foot),  M(q) qdd = tau - h(q, qd) + J_c^T f_c.
+// One dt: pivot kinematics root -> foot; compliant ground contact at the two
+// end-spheres of each capsule; subtree force / moment sums (RNEA: tau_c - h) and
+// composite inertias (CRBA: M) foot -> root; the translational block
+// (M_tt = total mass * I) eliminated by its Schur complement; a 4x4 LDL^T solve;
+// semi-implicit Euler.  frame_skip 4 x dt 0.002.  The fused step kernel splits
+// the contact work and the angle functions over the four 16-lane rows that hold
+// the same envs (HopperQuad, rollout.hip); everything else is evaluated by every
+// row in the same order, so all rows continue with the identical state.
 constexpr int HP_NS = 12, HP_OBS = 11, HP_ACT = 3;
 constexpr double HP_DT = 0.002;
 constexpr int HP_FRAME_SKIP = 4;
-constexpr double HP_GEAR = 200.0, HP_GRAV = 9.81, HP_MASS = 3.5, HP_I_ROOT = 2.0;
-constexpr double HP_L_TORSO = 0.2, HP_L_THIGH = 0.45, HP_L_LEG = 0.5, HP_FOOT_R = 0.1;
-constexpr double HP_KC = 5000.0, HP_CC = 60.0, HP_MU = 0.9, HP_VMAX = 50.0;
+constexpr double HP_GEAR = 200.0, HP_GRAV = 9.81;
+constexpr double HP_KC = 20000.0, HP_CC = 400.0, HP_CF = 1000.0;
+constexpr double HP_DAMP = 1.0, HP_ARM = 1.0, HP_KL = 2000.0, HP_CL = 50.0;
+constexpr double HP_MASS[4] = {3.6651914291880923, 4.057890510886817, 2.7813566959781637, 5.315574769873929};
+constexpr double HP_INERTIA[4] = {0.06924593807287505, 0.0932987568269219, 0.07230254017320971,
+                                  0.10352308059000535};
+constexpr double HP_SEG[3] = {0.2, 0.45, 0.5};
+constexpr double HP_COMX[4] = {0.0, 0.0, 0.0, 0.065}, HP_COMZ[4] = {0.0, -0.225, -0.25, 0.0};
+constexpr double HP_MB3 = HP_MASS[3], HP_MB2 = HP_MASS[2] + HP_MB3, HP_MB1 = HP_MASS[1] + HP_MB2,
+                 HP_MB0 = HP_MASS[0] + HP_MB1;  // subtree masses
+constexpr double HP_MB[4] = {HP_MB0, HP_MB1, HP_MB2, HP_MB3};
+constexpr double HP_IMT = 1.0 / HP_MB0;
+
+__device__ inline double sel4(int k, double a0, double a1, double a2, double a3) {
+  return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
+}
 
 __device__ inline void hopper_reset(const double* u, double* s) {
   for (int i = 0; i < 6; ++i) s[i] = u[i] * 0.01 - 0.005;
@@ -66,80 +90,225 @@ __device__ inline void hopper_reset(const double* u, double* s) {
 
 __device__ inline double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-// the four angle functions of a substep: (s0,c0)=sincos(ar), (s1,c1)=sincos(p1),
-// (s2,c2)=sincos(p2), sa3=sin(a3); one shared range reduction per angle
-struct HopperTrigSerial {
-  __device__ void operator()(double ar, double p1, double p2, double a3, double* sc) const {
-    sincos(ar, &sc[0], &sc[1]);
-    sincos(p1, &sc[2], &sc[3]);
-    sincos(p2, &sc[4], &sc[5]);
-    sc[6] = sin(a3);
+// capsule k's two end-spheres against the floor: contact force sum (x, z) and
+// moment about pivot k (oracle hopper_contacts); k may differ per lane
+__device__ inline void hopper_contacts(int k, double pz, double pvx, double pvz, double om, double sk, double ck,
+                                       double* out) {
+  const double rad = sel4(k, 0.05, 0.05, 0.04, 0.06), mu = sel4(k, 1.0, 1.0, 1.0, 2.0);
+  double fcx = 0.0, fcz = 0.0, ncm = 0.0;
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const double u = n == 0 ? sel4(k, 0.0, 0.0, 0.0, -0.13) : sel4(k, 0.0, 0.0, 0.0, 0.26);
+    const double w = n == 0 ? sel4(k, 0.2, 0.0, 0.0, 0.0) : sel4(k, -0.2, -0.45, -0.5, 0.0);
+    const double ox = u * ck + w * sk;
+    const double oz = (w * ck - u * sk) - rad;
+    const double pen = -(pz + oz);
+    const double vx = pvx + om * oz;
+    const double vz = pvz - om * ox;
+    const double fnr = HP_KC * pen - HP_CC * vz;
+    const double fn = pen > 0.0 ? (fnr > 0.0 ? fnr : 0.0) : 0.0;
+    const double lim = mu * fn;
+    const double fv = HP_CF * vx;
+    const double fl = fv > -lim ? fv : -lim;
+    const double ft = -(fl < lim ? fl : lim);
+    fcx = fcx + ft;
+    fcz = fcz + fn;
+    ncm = ncm + (oz * ft - ox * fn);
+  }
+  out[0] = fcx;
+  out[1] = fcz;
+  out[2] = ncm;
+}
+
+// every lane evaluates the whole env (layered rollout)
+struct HopperSerial {
+  __device__ void sincos4(const double* phi, double* s, double* c) const {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sincos(phi[k], &s[k], &c[k]);
+  }
+  template <class F>
+  __device__ void contacts(F f, double (*ct)[3]) const {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f(k, ct[k]);
   }
 };
 
-template <class Trig>
-__device__ inline void hopper_substep(double* q, double* v, const double* tau, const Trig& trig) {
-  const double HP_I[3] = {4.0, 3.0, 1.5};
-  const double HP_K[3] = {30.0, 30.0, 20.0};
-  const double HP_C[3] = {8.0, 6.0, 4.0};
-  const double x = q[0], z = q[1], ar = q[2], a1 = q[3], a2 = q[4], a3 = q[5];
-  const double vx = v[0], vz = v[1], var_ = v[2], v1 = v[3], v2 = v[4], v3 = v[5];
-  const double p1 = ar + a1;
-  const double p2 = p1 + a2;
-  const double w1 = var_ + v1;
-  const double w2 = w1 + v2;
-  double sc[7];
-  trig(ar, p1, p2, a3, sc);
-  const double s0 = sc[0], c0 = sc[1], s1 = sc[2], c1 = sc[3], s2 = sc[4], c2 = sc[5];
-  const double fx = x + HP_L_TORSO * s0 + HP_L_THIGH * s1 + HP_L_LEG * s2;
-  const double fz = z - HP_L_TORSO * c0 - HP_L_THIGH * c1 - HP_L_LEG * c2;
-  const double fvx = vx + HP_L_TORSO * c0 * var_ + HP_L_THIGH * c1 * w1 + HP_L_LEG * c2 * w2;
-  const double fvz = vz + HP_L_TORSO * s0 * var_ + HP_L_THIGH * s1 * w1 + HP_L_LEG * s2 * w2;
-  const double pen = HP_FOOT_R - fz;
-  const double fn = pen > 0.0 ? fmax(HP_KC * pen - HP_CC * fvz, 0.0) : 0.0;
-  const double ft = -HP_MU * fn * tanh(fvx / 0.05) * (1.0 - 0.5 * fabs(sc[6]));
-  const double ax = ft / HP_MASS;
-  const double az = fn / HP_MASS - HP_GRAV;
-  const double tq_root = (fx - x) * fn - (fz - z) * ft;
-  const double hx = x + HP_L_TORSO * s0;
-  const double hz = z - HP_L_TORSO * c0;
-  const double kx = hx + HP_L_THIGH * s1;
-  const double kz = hz - HP_L_THIGH * c1;
-  const double tq1 = (fx - hx) * fn - (fz - hz) * ft;
-  const double tq2 = (fx - kx) * fn - (fz - kz) * ft;
-  double acc[6];
-  acc[0] = ax;
-  acc[1] = az;
-  acc[2] = (0.05 * tq_root - tau[0] * 0.1 - 1.0 * var_) / HP_I_ROOT;
-  acc[3] = (tau[0] - HP_K[0] * a1 - HP_C[0] * v1 + 0.05 * tq1) / HP_I[0];
-  acc[4] = (tau[1] - HP_K[1] * a2 - HP_C[1] * v2 + 0.05 * tq2) / HP_I[1];
-  acc[5] = (tau[2] - HP_K[2] * a3 - HP_C[2] * v3 - 0.02 * ft) / HP_I[2];
-  for (int i = 0; i < 6; ++i) v[i] = clampd(v[i] + HP_DT * acc[i], -HP_VMAX, HP_VMAX);
-  for (int i = 0; i < 6; ++i) q[i] = q[i] + HP_DT * v[i];
-  const double lo[3] = {-2.61799, -2.61799, -0.785398};
-  const double hi[3] = {0.0, 0.0, 0.785398};
-  for (int jj = 0; jj < 3; ++jj) {
-    const int j = 3 + jj;
-    const bool over = q[j] > hi[jj];
-    const bool under = q[j] < lo[jj];
-    q[j] = over ? hi[jj] : (under ? lo[jj] : q[j]);
-    if (over || under) v[j] = 0.0;
+// LDL^T solve of the 4x4 SPD system K x = r (oracle ldl_solve)
+__device__ inline void ldl_solve4(const double (&K)[4][4], const double* r, double* x) {
+  double L[4][4], D[4], iD[4], y[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double d = K[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) d = d - (L[j][k] * L[j][k]) * D[k];
+    D[j] = d;
+    iD[j] = 1.0 / d;
+#pragma unroll
+    for (int i = j + 1; i < 4; ++i) {
+      double acc = K[i][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) acc = acc - (L[i][k] * L[j][k]) * D[k];
+      L[i][j] = acc * iD[j];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    double acc = r[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) acc = acc - L[i][k] * y[k];
+    y[i] = acc;
+  }
+#pragma unroll
+  for (int i = 3; i >= 0; --i) {
+    double acc = y[i] * iD[i];
+#pragma unroll
+    for (int k = i + 1; k < 4; ++k) acc = acc - L[k][i] * x[k];
+    x[i] = acc;
   }
 }
 
-template <class Trig = HopperTrigSerial>
-__device__ inline void hopper_step(double* s, const float* a, double& rew, bool& done, const Trig& trig = Trig()) {
-  double tau[3];
-  double asq = 0.0;
+template <class Par>
+__device__ inline void hopper_substep(double* q, double* v, const double* tau, const Par& par) {
+  const double HP_LO[3] = {-2.6179938779914944, -2.6179938779914944, -0.7853981633974483};
+  const double HP_HI[3] = {0.0, 0.0, 0.7853981633974483};
+  double phi[4], sg[4], cg[4], om[4];
+  phi[0] = q[2];
+#pragma unroll
+  for (int j = 1; j < 4; ++j) phi[j] = phi[j - 1] - q[2 + j];
+  par.sincos4(phi, sg, cg);
+  om[0] = v[2];
+#pragma unroll
+  for (int j = 1; j < 4; ++j) om[j] = om[j - 1] - v[2 + j];
+  double gx[3], gz[3], rx[4], rz[4];
+#pragma unroll
   for (int j = 0; j < 3; ++j) {
-    const double aj = (double)a[j];
-    tau[j] = HP_GEAR * clampd(aj, -1.0, 1.0);
-    asq += aj * aj;
+    gx[j] = -HP_SEG[j] * sg[j];
+    gz[j] = -HP_SEG[j] * cg[j];
   }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    rx[k] = HP_COMX[k] * cg[k] + HP_COMZ[k] * sg[k];
+    rz[k] = HP_COMZ[k] * cg[k] - HP_COMX[k] * sg[k];
+  }
+  // pivots: height, velocity, bias acceleration (root -> foot)
+  double pz[4], pvx[4], pvz[4], pax[4], paz[4];
+  pz[0] = q[1];
+  pvx[0] = v[0];
+  pvz[0] = v[1];
+  pax[0] = 0.0;
+  paz[0] = 0.0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double w2 = om[j] * om[j];
+    pz[j + 1] = pz[j] + gz[j];
+    pvx[j + 1] = pvx[j] + om[j] * gz[j];
+    pvz[j + 1] = pvz[j] - om[j] * gx[j];
+    pax[j + 1] = pax[j] - w2 * gx[j];
+    paz[j + 1] = paz[j] - w2 * gz[j];
+  }
+  double ct[4][3];
+  par.contacts(
+      [&](int k, double* out) {
+        hopper_contacts(k, sel4(k, pz[0], pz[1], pz[2], pz[3]), sel4(k, pvx[0], pvx[1], pvx[2], pvx[3]),
+                        sel4(k, pvz[0], pvz[1], pvz[2], pvz[3]), sel4(k, om[0], om[1], om[2], om[3]),
+                        sel4(k, sg[0], sg[1], sg[2], sg[3]), sel4(k, cg[0], cg[1], cg[2], cg[3]), out);
+      },
+      ct);
+  // per body: inertial + gravity force minus contact force, moment about its pivot
+  double Fx[4], Fz[4], N[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double w2 = om[k] * om[k];
+    const double mx = HP_MASS[k] * (pax[k] - w2 * rx[k]);
+    const double mz = HP_MASS[k] * ((paz[k] - w2 * rz[k]) + HP_GRAV);
+    Fx[k] = mx - ct[k][0];
+    Fz[k] = mz - ct[k][1];
+    N[k] = (rz[k] * mx - rx[k] * mz) - ct[k][2];
+  }
+  // subtree sums about pivot k (foot -> root)
+  double Fbx[4], Fbz[4], Nb[4], Sx[4], Sz[4], J[4];
+  Fbx[3] = Fx[3];
+  Fbz[3] = Fz[3];
+  Nb[3] = N[3];
+  Sx[3] = HP_MASS[3] * rx[3];
+  Sz[3] = HP_MASS[3] * rz[3];
+  J[3] = HP_INERTIA[3] + HP_MASS[3] * (rx[3] * rx[3] + rz[3] * rz[3]);
+#pragma unroll
+  for (int k = 2; k >= 0; --k) {
+    Nb[k] = (N[k] + Nb[k + 1]) + (gz[k] * Fbx[k + 1] - gx[k] * Fbz[k + 1]);
+    Fbx[k] = Fx[k] + Fbx[k + 1];
+    Fbz[k] = Fz[k] + Fbz[k + 1];
+    J[k] = ((HP_INERTIA[k] + HP_MASS[k] * (rx[k] * rx[k] + rz[k] * rz[k])) + J[k + 1]) +
+           (2.0 * (gx[k] * Sx[k + 1] + gz[k] * Sz[k + 1]) + HP_MB[k + 1] * (HP_SEG[k] * HP_SEG[k]));
+    Sx[k] = (HP_MASS[k] * rx[k] + Sx[k + 1]) + HP_MB[k + 1] * gx[k];
+    Sz[k] = (HP_MASS[k] * rz[k] + Sz[k + 1]) + HP_MB[k + 1] * gz[k];
+  }
+  double rhs[6] = {-Fbx[0], -Fbz[0], -Nb[0], Nb[1], Nb[2], Nb[3]};
+  // rotational block C and coupling rows B0 / B1 of M (oracle hopper_dynamics_terms)
+  double Dx[4][4], Dz[4][4];
+  Dx[0][1] = gx[0];
+  Dz[0][1] = gz[0];
+  Dx[1][2] = gx[1];
+  Dz[1][2] = gz[1];
+  Dx[2][3] = gx[2];
+  Dz[2][3] = gz[2];
+  Dx[0][2] = gx[0] + gx[1];
+  Dz[0][2] = gz[0] + gz[1];
+  Dx[0][3] = Dx[0][2] + gx[2];
+  Dz[0][3] = Dz[0][2] + gz[2];
+  Dx[1][3] = gx[1] + gx[2];
+  Dz[1][3] = gz[1] + gz[2];
+  double C[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    C[a][a] = J[a];
+#pragma unroll
+    for (int b = a + 1; b < 4; ++b) {
+      const double val = (Dx[a][b] * Sx[b] + Dz[a][b] * Sz[b]) + J[b];
+      C[a][b] = a == 0 ? -val : val;
+    }
+  }
+  const double B0[4] = {Sz[0], -Sz[1], -Sz[2], -Sz[3]};
+  const double B1[4] = {-Sx[0], Sx[1], Sx[2], Sx[3]};
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    const int jj = i - 1, j = 2 + i;
+    C[i][i] = C[i][i] + HP_ARM;
+    const double lim = q[j] < HP_LO[jj] ? HP_KL * (HP_LO[jj] - q[j]) - HP_CL * v[j]
+                                        : (q[j] > HP_HI[jj] ? HP_KL * (HP_HI[jj] - q[j]) - HP_CL * v[j] : 0.0);
+    rhs[j] = ((rhs[j] + tau[jj]) - HP_DAMP * v[j]) + lim;
+  }
+  // Schur complement of the translational block, 4x4 LDL^T (oracle hopper_solve)
+  double K[4][4], rr[4], x[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = a; b < 4; ++b) {
+      K[a][b] = C[a][b] - (B0[a] * B0[b] + B1[a] * B1[b]) * HP_IMT;
+      K[b][a] = K[a][b];
+    }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) rr[a] = rhs[2 + a] - (B0[a] * rhs[0] + B1[a] * rhs[1]) * HP_IMT;
+  ldl_solve4(K, rr, x);
+  const double t0 = rhs[0] - (((B0[0] * x[0] + B0[1] * x[1]) + B0[2] * x[2]) + B0[3] * x[3]);
+  const double t1 = rhs[1] - (((B1[0] * x[0] + B1[1] * x[1]) + B1[2] * x[2]) + B1[3] * x[3]);
+  const double qdd[6] = {t0 * HP_IMT, t1 * HP_IMT, x[0], x[1], x[2], x[3]};
+#pragma unroll
+  for (int i = 0; i < 6; ++i) v[i] = v[i] + HP_DT * qdd[i];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) q[i] = q[i] + HP_DT * v[i];
+}
+
+template <class Par = HopperSerial>
+__device__ inline void hopper_step(double* s, const float* a, double& rew, bool& done, const Par& par = Par()) {
+  double tau[3];
+  for (int j = 0; j < 3; ++j) tau[j] = HP_GEAR * clampd((double)a[j], -1.0, 1.0);
+  const double a0 = (double)a[0], a1 = (double)a[1], a2 = (double)a[2];
+  const double asq = ((a0 * a0) + (a1 * a1)) + (a2 * a2);
   double* q = s;
   double* v = s + 6;
   const double x_before = q[0];
-  for (int k = 0; k < HP_FRAME_SKIP; ++k) hopper_substep(q, v, tau, trig);
+  for (int k = 0; k < HP_FRAME_SKIP; ++k) hopper_substep(q, v, tau, par);
   rew = (q[0] - x_before) / (HP_DT * HP_FRAME_SKIP) + 1.0 - 1e-3 * asq;
   bool healthy = true;
   for (int i = 0; i < 12; ++i) healthy = healthy && isfinite(s[i]);

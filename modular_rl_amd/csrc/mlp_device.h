@@ -448,6 +448,20 @@ __device__ inline float quad_sum(float v) {
   return __uint_as_float(q[0]) + __uint_as_float(q[1]);
 }
 
+// the same for a double: both 32-bit halves follow the float pattern
+__device__ inline double quad_sum_d(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const auto plo = __builtin_amdgcn_permlane16_swap((uint32_t)b, (uint32_t)b, false, false);
+  const auto phi = __builtin_amdgcn_permlane16_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+  const double t = __longlong_as_double((long long)(((uint64_t)phi[0] << 32) | plo[0])) +
+                   __longlong_as_double((long long)(((uint64_t)phi[1] << 32) | plo[1]));
+  const uint64_t tb = (uint64_t)__double_as_longlong(t);
+  const auto qlo = __builtin_amdgcn_permlane32_swap((uint32_t)tb, (uint32_t)tb, false, false);
+  const auto qhi = __builtin_amdgcn_permlane32_swap((uint32_t)(tb >> 32), (uint32_t)(tb >> 32), false, false);
+  return __longlong_as_double((long long)(((uint64_t)qhi[0] << 32) | qlo[0])) +
+         __longlong_as_double((long long)(((uint64_t)qhi[1] << 32) | qlo[1]));
+}
+
 __device__ inline double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

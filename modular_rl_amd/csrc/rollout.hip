@@ -30,25 +30,28 @@ constexpr int RB = 256;  // threads per block
 constexpr int ENVS_PER_BLOCK = 64;  // fused step: 4 waves x 16 envs
 constexpr int MAXD = 16;  // obs dims + 1 (reward)
 
-// Hopper angle functions in the fused step kernel, where the four 16-lane rows of a
-// wave hold the SAME 16 envs: row g evaluates sincos of angle g (ar, p1, p2, a3) and
-// the rows exchange -- one sincos sequence per substep instead of three plus a sin.
-// All lanes must be active.
-struct HopperTrigQuad {
+// Hopper-v2 in the fused step kernel, where the four 16-lane rows of a wave hold
+// the SAME 16 envs: row g evaluates sincos of segment angle g and the contacts of
+// capsule g, and the rows exchange the results, so every row continues with the
+// identical state.  All lanes must be active.
+struct HopperQuad {
   int g;
-  __device__ void operator()(double ar, double p1, double p2, double a3, double* sc) const {
-    const double ang = g == 0 ? ar : (g == 1 ? p1 : (g == 2 ? p2 : a3));
-    double sx, cx, sv[4], cv[4];
-    sincos(ang, &sx, &cx);
-    quads(sx, sv);
-    quads(cx, cv);
-    sc[0] = sv[0];
-    sc[1] = cv[0];
-    sc[2] = sv[1];
-    sc[3] = cv[1];
-    sc[4] = sv[2];
-    sc[5] = cv[2];
-    sc[6] = sv[3];
+  __device__ void sincos4(const double* phi, double* s, double* c) const {
+    double sx, cx;
+    sincos(sel4(g, phi[0], phi[1], phi[2], phi[3]), &sx, &cx);
+    quads(sx, s);
+    quads(cx, c);
+  }
+  template <class F>
+  __device__ void contacts(F f, double (*ct)[3]) const {
+    double own[3], x[4];
+    f(g, own);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      quads(own[i], x);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ct[k][i] = x[k];
+    }
   }
 };
 
@@ -78,7 +81,7 @@ struct EnvC<MRL_ENV_HOPPER> {
   __device__ static void step_disc(double*, int, double&, bool&) {}
   __device__ static void step_cont(double* s, const float* a, double& rew, bool& done) { hopper_step(s, a, rew, done); }
   __device__ static void step_cont_quad(double* s, const float* a, double& rew, bool& done, int g) {
-    hopper_step(s, a, rew, done, HopperTrigQuad{g});
+    hopper_step(s, a, rew, done, HopperQuad{g});
   }
   template <class Out>
   __device__ static void obs_out(const double* s, Out out) {

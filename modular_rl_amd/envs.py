@@ -6,7 +6,7 @@ module only describes them with gym-compatible spaces / spec so that
 ``env.spec.max_episode_steps`` (run_pg.py:103-108) work unchanged.
 
 * ``CartPole-v0`` -- gym's classic-control CartPole equations, TimeLimit 200.
-* ``Hopper-v2``   -- Hopper-v2-SHAPED surrogate (obs 11, act 3, TimeLimit 1000);
+* ``Hopper-v2``   -- gym's hopper.xml as articulated rigid-body dynamics (obs 11, act 3, TimeLimit 1000);
   MuJoCo is not available, so its dynamics are a stand-in.
 * ``Humanoid-v2`` -- Humanoid-v2-SHAPED surrogate (obs 376, act 17 in [-0.4, 0.4],
   TimeLimit 1000); its 376-d obs needs the layered rollout (collector.py).

@@ -23,7 +23,8 @@ Pinning (see DESIGN.md "Oracle"):
     double-backward (Theano's own formulation, trpo.py:45-58) in
     ``oracle/torch_ref.py`` -- and the two agree to ~1e-15 in float64.
   * Env dynamics (gym CartPole-v0, MuJoCo Hopper-v2) are absent from the
-    reference: CartPole is restated from the published gym equations and the
-    Hopper/Humanoid-shaped envs are surrogates; env dynamics are
-    "parity unpinned".
+    reference: CartPole is restated from the published gym equations, Hopper-v2
+    as articulated rigid-body dynamics of gym's hopper.xml (compliant contact
+    instead of MuJoCo's solver), and the Humanoid-shaped env is a surrogate;
+    env dynamics are "parity unpinned".
 """

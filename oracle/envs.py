@@ -12,11 +12,14 @@ not vendored and are absent here, so env dynamics are **parity unpinned**:
   - 0.1 |a|^2 - min(5e-7 |cfrc|^2, 10), healthy 1 < z < 2, TimeLimit 1000): a
   sagittal two-leg contact model with 17 damped actuated joints -- shape- and
   cost-representative, not MuJoCo.
-* ``hopper_*`` is a *surrogate* with Hopper-v2's interface (11-d obs =
-  qpos[1:] ++ clip(qvel, -10, 10), 3-d action in [-1, 1] with gear 200,
-  frame_skip 4 x dt 0.002, reward = forward velocity + 1 - 1e-3 |a|^2, the
-  Hopper-v2 health test, TimeLimit 1000).  Its planar leg dynamics are a
-  cost-representative stand-in for MuJoCo, not MuJoCo.
+* ``hopper_*`` restates gym's Hopper-v2 model (hopper.xml: 4 capsule bodies on
+  rootx / rootz / rooty + 3 actuated hinges, gear 200, frame_skip 4 x dt 0.002,
+  11-d obs = qpos[1:] ++ clip(qvel, -10, 10), reward = forward velocity + 1 -
+  1e-3 |a|^2, the Hopper-v2 health test, TimeLimit 1000) as planar articulated
+  rigid-body dynamics (CRBA / RNEA, LDL^T) with compliant ground contact in place
+  of MuJoCo's constraint solver: physical, checked by energy conservation and an
+  independent per-body assembly (tests/test_hopper_physics.py), parity with
+  MuJoCo unpinned.
 
 Every function here is mirrored operation-for-operation by the HIP env kernels
 in ``modular_rl_amd/csrc/envs.h`` (compiled with fp-contract off) so the GPU
@@ -66,26 +69,47 @@ def cartpole_step(s, a):
     return s2, rew, done
 
 
-# ---------------------------------------------------------------- Hopper surrogate
+# ---------------------------------------------------------------- Hopper-v2
+# gym's hopper.xml (MuJoCo, coordinate="global", density 1000, inertiafromgeom):
+#   torso capsule z 1.45..1.05 r .05 on rootx (slide), rootz (slide, ref 1.25),
+#   rooty (hinge +y, at the torso centre); thigh 1.05..0.6 r .05 (thigh_joint,
+#   hinge -y, range -150..0 deg); leg 0.6..0.1 r .04 (leg_joint, -150..0); foot
+#   x -.13..0.26 at z .1, r .06 (foot_joint, -45..45); joint damping 1 and
+#   armature 1 on the three actuated hinges; motors gear 200, ctrl in [-1, 1];
+#   timestep 0.002, frame_skip 4; gravity 9.81.
+# Planar articulated rigid-body dynamics in generalized coordinates
+# q = (rootx, rootz, rooty, thigh, leg, foot): M(q) qdd = tau - h(q, qd) + J_c^T f_c,
+# M and h summed over the 4 capsule bodies, ground contact at the 8 capsule
+# end-spheres (spring-damper normal force, viscous friction clipped to the
+# Coulomb cone, friction max(floor 1, geom)), penalty joint limits, LDL^T solve,
+# semi-implicit Euler.  MuJoCo's soft-constraint solver is replaced by the
+# compliant contact model, so the trajectories are physical but parity with
+# MuJoCo is unpinned.
 HP_DT = 0.002
 HP_FRAME_SKIP = 4
 HP_GEAR = 200.0
 HP_GRAV = 9.81
-HP_MASS = 3.5
-HP_I_ROOT = 2.0
-HP_I = (4.0, 3.0, 1.5)
-HP_K = (30.0, 30.0, 20.0)
-HP_C = (8.0, 6.0, 4.0)
-HP_LO = (-2.61799, -2.61799, -0.785398)
-HP_HI = (0.0, 0.0, 0.785398)
-HP_L_TORSO = 0.2
-HP_L_THIGH = 0.45
-HP_L_LEG = 0.5
-HP_FOOT_R = 0.1
-HP_KC = 5000.0
-HP_CC = 60.0
-HP_MU = 0.9
-HP_VMAX = 50.0
+# per body (torso, thigh, leg, foot): mass, inertia about y at the COM
+HP_MASS = (3.6651914291880923, 4.057890510886817, 2.7813566959781637, 5.315574769873929)
+HP_INERTIA = (0.06924593807287505, 0.0932987568269219, 0.07230254017320971, 0.10352308059000535)
+HP_SEG = (0.2, 0.45, 0.5)                  # pivot-to-next-pivot length of torso, thigh, leg
+HP_COM = ((0.0, 0.0), (0.0, -0.225), (0.0, -0.25), (0.065, 0.0))   # COM in the segment frame
+HP_CAP = (((0.0, 0.2), (0.0, -0.2)), ((0.0, 0.0), (0.0, -0.45)),
+          ((0.0, 0.0), (0.0, -0.5)), ((-0.13, 0.0), (0.26, 0.0)))  # capsule end-sphere centres
+HP_RAD = (0.05, 0.05, 0.04, 0.06)
+HP_MU = (1.0, 1.0, 1.0, 2.0)
+HP_KC = 20000.0      # contact stiffness N/m
+HP_CC = 400.0        # contact damping N s/m
+HP_CF = 1000.0       # viscous friction N s/m (clipped to mu * fn)
+HP_DAMP = 1.0
+HP_ARM = 1.0
+HP_LO = (-2.6179938779914944, -2.6179938779914944, -0.7853981633974483)
+HP_HI = (0.0, 0.0, 0.7853981633974483)
+HP_KL = 2000.0       # joint-limit stiffness N m/rad
+HP_CL = 50.0         # joint-limit damping N m s/rad
+HP_NTERMS = 27       # per-body terms: 21 (upper triangle of M) + 6 (rhs)
+# upper-triangle index order of M (row-major a <= b)
+HP_TRI = tuple((a_, b_) for a_ in range(6) for b_ in range(a_, 6))
 
 
 def hopper_reset(u):
@@ -100,48 +124,262 @@ def hopper_obs(qpos, qvel):
     return np.concatenate([qpos[:, 1:], np.clip(qvel, -10.0, 10.0)], axis=1)
 
 
+def _rot(s, c, u, w):
+    """segment-frame offset (u, w) rotated by the segment angle about +y."""
+    return u * c + w * s, w * c - u * s
+
+
+def _levers(k, gx, gz, ex, ez, om, qd):
+    """A point of body k whose own-segment offset is (ex, ez): the per-segment
+    parts e_j of (point - root) (j < k: pivot-to-pivot vectors, j == k: (ex, ez),
+    j > k: 0), the suffix levers L_i = sum_{j >= i} e_j from pivot i, and the
+    point velocity qd_xz + sum_j om_j perp(e_j), perp(v) = (v_z, -v_x)."""
+    e = [((gx[j], gz[j]) if j < k else ((ex, ez) if j == k else (0.0, 0.0))) for j in range(4)]
+    Lx, Lz = [None] * 4, [None] * 4
+    Lx[3], Lz[3] = e[3]
+    for i in range(2, -1, -1):
+        Lx[i] = e[i][0] + Lx[i + 1]
+        Lz[i] = e[i][1] + Lz[i + 1]
+    vx, vz = qd[0], qd[1]
+    for j in range(4):
+        vx = vx + om[j] * e[j][1]
+        vz = vz - om[j] * e[j][0]
+    return e, Lx, Lz, vx, vz
+
+
+def _gen_force(Lx, Lz, fx, fz):
+    """J^T f of a point force f with suffix levers L: 6 generalized components
+    (columns: x, z, perp(L_0), -perp(L_1..3))."""
+    return [fx, fz, Lz[0] * fx - Lx[0] * fz] + [-(Lz[i] * fx - Lx[i] * fz) for i in range(1, 4)]
+
+
+def hopper_body_terms(k, q, qd, sg, cg):
+    """Body k's contribution: the 21 upper-triangle entries of its
+    m J^T J + I jw^T jw, and the 6 entries of (contact forces of its capsule)
+    - (its bias + gravity force).  Written without branches on k so the device
+    kernel can evaluate one body per lane row (envs.h)."""
+    om = [qd[2]]
+    for j in range(1, 4):
+        om.append(om[j - 1] - qd[2 + j])
+    gx = [-HP_SEG[j] * sg[j] for j in range(3)]
+    gz = [-HP_SEG[j] * cg[j] for j in range(3)]
+    m, I = HP_MASS[k], HP_INERTIA[k]
+    ex, ez = _rot(sg[k], cg[k], *HP_COM[k])
+    e, Lx, Lz, _, _ = _levers(k, gx, gz, ex, ez, om, qd)
+    cx = [1.0, 0.0, Lz[0], -Lz[1], -Lz[2], -Lz[3]]
+    cz = [0.0, 1.0, -Lx[0], Lx[1], Lx[2], Lx[3]]
+    jw = [0.0, 0.0, 1.0] + [(-1.0 if i <= k else 0.0) for i in range(1, 4)]
+    terms = [m * (cx[a_] * cx[b_] + cz[a_] * cz[b_]) + I * (jw[a_] * jw[b_]) for (a_, b_) in HP_TRI]
+    # COM bias acceleration -sum_j om_j^2 e_j, plus gravity, times the mass
+    bx, bz = 0.0, 0.0
+    for j in range(4):
+        w2 = om[j] * om[j]
+        bx = bx - w2 * e[j][0]
+        bz = bz - w2 * e[j][1]
+    h = _gen_force(Lx, Lz, m * bx, m * (bz + HP_GRAV))
+    # ground contact at the two end-spheres of the capsule (lowest point of each)
+    Qc = [0.0] * 6
+    for (u, w) in HP_CAP[k]:
+        px, pz = _rot(sg[k], cg[k], u, w)
+        _, Px, Pz, vx, vz = _levers(k, gx, gz, px, pz - HP_RAD[k], om, qd)
+        pen = -(q[1] + Pz[0])
+        fn = np.where(pen > 0.0, np.maximum(HP_KC * pen - HP_CC * vz, 0.0), 0.0)
+        lim = HP_MU[k] * fn
+        ft = -np.minimum(np.maximum(HP_CF * vx, -lim), lim)
+        g = _gen_force(Px, Pz, ft, fn)
+        Qc = [Qc[i] + g[i] for i in range(6)]
+    return terms + [Qc[i] - h[i] for i in range(6)]
+
+
+def _hopper_substep_per_body(q, v, tau):
+    """Cross-check formulation (tests only): M and tau_c - h summed body by body."""
+    qs = [q[:, i] for i in range(6)]
+    qd = [v[:, i] for i in range(6)]
+    phi = [qs[2]]
+    for j in range(1, 4):
+        phi.append(phi[j - 1] - qs[2 + j])
+    sg = [np.sin(p) for p in phi]
+    cg = [np.cos(p) for p in phi]
+    B = [hopper_body_terms(k, qs, qd, sg, cg) for k in range(4)]
+    tot = [(B[0][t] + B[1][t]) + (B[2][t] + B[3][t]) for t in range(HP_NTERMS)]
+    M = np.zeros((q.shape[0], 6, 6))
+    for n, (a_, b_) in enumerate(HP_TRI):
+        M[:, a_, b_] = tot[n]
+        M[:, b_, a_] = tot[n]
+    rhs = [tot[21 + i] for i in range(6)]
+    for jj in range(3):
+        j = 3 + jj
+        M[:, j, j] = M[:, j, j] + HP_ARM
+        lim = np.where(qs[j] < HP_LO[jj], HP_KL * (HP_LO[jj] - qs[j]) - HP_CL * qd[j],
+                       np.where(qs[j] > HP_HI[jj], HP_KL * (HP_HI[jj] - qs[j]) - HP_CL * qd[j], 0.0))
+        rhs[j] = ((rhs[j] + tau[:, jj]) - HP_DAMP * qd[j]) + lim
+    qdd = ldl_solve6(M, rhs)
+    v2 = np.stack([qd[i] + HP_DT * qdd[i] for i in range(6)], axis=1)
+    q2 = np.stack([qs[i] + HP_DT * v2[:, i] for i in range(6)], axis=1)
+    return q2, v2
+
+
+HP_MB = [None] * 4     # subtree masses sum_{j >= k} m_j
+HP_MB[3] = HP_MASS[3]
+for _k in (2, 1, 0):
+    HP_MB[_k] = HP_MASS[_k] + HP_MB[_k + 1]
+HP_IMT = 1.0 / HP_MB[0]
+
+
 def _hopper_substep(q, v, tau):
-    x, z, ar, a1, a2, a3 = (q[:, i] for i in range(6))
-    vx, vz, var_, v1, v2, v3 = (v[:, i] for i in range(6))
-    p1 = ar + a1
-    p2 = p1 + a2
-    w1 = var_ + v1
-    w2 = w1 + v2
-    s0, c0 = np.sin(ar), np.cos(ar)
-    s1, c1 = np.sin(p1), np.cos(p1)
-    s2, c2 = np.sin(p2), np.cos(p2)
-    # leg tip (contact point) by planar forward kinematics from the root
-    fx = x + HP_L_TORSO * s0 + HP_L_THIGH * s1 + HP_L_LEG * s2
-    fz = z - HP_L_TORSO * c0 - HP_L_THIGH * c1 - HP_L_LEG * c2
-    fvx = vx + HP_L_TORSO * c0 * var_ + HP_L_THIGH * c1 * w1 + HP_L_LEG * c2 * w2
-    fvz = vz + HP_L_TORSO * s0 * var_ + HP_L_THIGH * s1 * w1 + HP_L_LEG * s2 * w2
-    pen = HP_FOOT_R - fz
-    fn = np.where(pen > 0.0, np.maximum(HP_KC * pen - HP_CC * fvz, 0.0), 0.0)
-    ft = -HP_MU * fn * np.tanh(fvx / 0.05) * (1.0 - 0.5 * np.abs(np.sin(a3)))
-    # accelerations
-    ax = ft / HP_MASS
-    az = fn / HP_MASS - HP_GRAV
-    tq_root = (fx - x) * fn - (fz - z) * ft
-    hx = x + HP_L_TORSO * s0
-    hz = z - HP_L_TORSO * c0
-    kx = hx + HP_L_THIGH * s1
-    kz = hz - HP_L_THIGH * c1
-    tq1 = (fx - hx) * fn - (fz - hz) * ft
-    tq2 = (fx - kx) * fn - (fz - kz) * ft
-    aar = (0.05 * tq_root - tau[:, 0] * 0.1 - 1.0 * var_) / HP_I_ROOT
-    aa1 = (tau[:, 0] - HP_K[0] * a1 - HP_C[0] * v1 + 0.05 * tq1) / HP_I[0]
-    aa2 = (tau[:, 1] - HP_K[1] * a2 - HP_C[1] * v2 + 0.05 * tq2) / HP_I[1]
-    aa3 = (tau[:, 2] - HP_K[2] * a3 - HP_C[2] * v3 - 0.02 * ft) / HP_I[2]
-    acc = np.stack([ax, az, aar, aa1, aa2, aa3], axis=1)
-    v = np.clip(v + HP_DT * acc, -HP_VMAX, HP_VMAX)
-    q = q + HP_DT * v
-    # joint limits: clamp position, kill the velocity into the limit
-    for j, lo, hi in zip((3, 4, 5), HP_LO, HP_HI):
-        over = q[:, j] > hi
-        under = q[:, j] < lo
-        q[:, j] = np.where(over, hi, np.where(under, lo, q[:, j]))
-        v[:, j] = np.where(over | under, 0.0, v[:, j])
-    return q, v
+    """One dt of the articulated hopper in recursive form (the device kernel's
+    operation order, envs.h hopper_substep): pivot kinematics root -> foot,
+    contact forces, subtree force / moment / composite-inertia sums foot -> root
+    (RNEA for tau_c - h, CRBA for M), the translational block eliminated
+    (M_tt = total mass * I), a 4x4 LDL^T solve, semi-implicit Euler."""
+    qs = [q[:, i] for i in range(6)]
+    qd = [v[:, i] for i in range(6)]
+    phi = [qs[2]]
+    for j in range(1, 4):
+        phi.append(phi[j - 1] - qs[2 + j])
+    sg = [np.sin(p) for p in phi]
+    cg = [np.cos(p) for p in phi]
+    rhs, C, B0, B1 = hopper_dynamics_terms(qs, qd, sg, cg)
+    for i in range(1, 4):
+        jj = i - 1
+        j = 2 + i
+        C[i][i] = C[i][i] + HP_ARM
+        lim = np.where(qs[j] < HP_LO[jj], HP_KL * (HP_LO[jj] - qs[j]) - HP_CL * qd[j],
+                       np.where(qs[j] > HP_HI[jj], HP_KL * (HP_HI[jj] - qs[j]) - HP_CL * qd[j], 0.0))
+        rhs[j] = ((rhs[j] + tau[:, jj]) - HP_DAMP * qd[j]) + lim
+    qdd = hopper_solve(rhs, C, B0, B1)
+    v2 = np.stack([qd[i] + HP_DT * qdd[i] for i in range(6)], axis=1)
+    q2 = np.stack([qs[i] + HP_DT * v2[:, i] for i in range(6)], axis=1)
+    return q2, v2
+
+
+def hopper_contacts(k, pz, pvx, pvz, om, sk, ck):
+    """Contact force sum (x, z) and moment about pivot k of capsule k's two end-spheres."""
+    fcx, fcz, ncm = 0.0, 0.0, 0.0
+    for (u, w) in HP_CAP[k]:
+        ox = u * ck + w * sk
+        oz = (w * ck - u * sk) - HP_RAD[k]
+        pen = -(pz + oz)
+        vx = pvx + om * oz
+        vz = pvz - om * ox
+        fn = np.where(pen > 0.0, np.maximum(HP_KC * pen - HP_CC * vz, 0.0), 0.0)
+        lim = HP_MU[k] * fn
+        ft = -np.minimum(np.maximum(HP_CF * vx, -lim), lim)
+        fcx = fcx + ft
+        fcz = fcz + fn
+        ncm = ncm + (oz * ft - ox * fn)
+    return fcx, fcz, ncm
+
+
+def hopper_dynamics_terms(qs, qd, sg, cg):
+    """rhs = tau_c - h (6), the rotational block C (4x4, upper triangle, no
+    armature) and the coupling rows B0 / B1 of M."""
+    om = [qd[2]]
+    for j in range(1, 4):
+        om.append(om[j - 1] - qd[2 + j])
+    gx = [-HP_SEG[j] * sg[j] for j in range(3)]
+    gz = [-HP_SEG[j] * cg[j] for j in range(3)]
+    rx = [HP_COM[k][0] * cg[k] + HP_COM[k][1] * sg[k] for k in range(4)]
+    rz = [HP_COM[k][1] * cg[k] - HP_COM[k][0] * sg[k] for k in range(4)]
+    # pivots: height, velocity, bias acceleration (root -> foot)
+    pz, pvx, pvz, pax, paz = [qs[1]], [qd[0]], [qd[1]], [0.0], [0.0]
+    for j in range(3):
+        w2 = om[j] * om[j]
+        pz.append(pz[j] + gz[j])
+        pvx.append(pvx[j] + om[j] * gz[j])
+        pvz.append(pvz[j] - om[j] * gx[j])
+        pax.append(pax[j] - w2 * gx[j])
+        paz.append(paz[j] - w2 * gz[j])
+    ct = [hopper_contacts(k, pz[k], pvx[k], pvz[k], om[k], sg[k], cg[k]) for k in range(4)]
+    # per body: inertial + gravity force minus contact force, moment about its pivot
+    Fx, Fz, N = [None] * 4, [None] * 4, [None] * 4
+    for k in range(4):
+        w2 = om[k] * om[k]
+        mx = HP_MASS[k] * (pax[k] - w2 * rx[k])
+        mz = HP_MASS[k] * ((paz[k] - w2 * rz[k]) + HP_GRAV)
+        Fx[k] = mx - ct[k][0]
+        Fz[k] = mz - ct[k][1]
+        N[k] = (rz[k] * mx - rx[k] * mz) - ct[k][2]
+    # subtree sums about pivot k (foot -> root)
+    Fbx, Fbz, Nb, Sx, Sz, J = [None] * 4, [None] * 4, [None] * 4, [None] * 4, [None] * 4, [None] * 4
+    Fbx[3], Fbz[3], Nb[3] = Fx[3], Fz[3], N[3]
+    Sx[3], Sz[3] = HP_MASS[3] * rx[3], HP_MASS[3] * rz[3]
+    J[3] = HP_INERTIA[3] + HP_MASS[3] * (rx[3] * rx[3] + rz[3] * rz[3])
+    for k in (2, 1, 0):
+        Nb[k] = (N[k] + Nb[k + 1]) + (gz[k] * Fbx[k + 1] - gx[k] * Fbz[k + 1])
+        Fbx[k] = Fx[k] + Fbx[k + 1]
+        Fbz[k] = Fz[k] + Fbz[k + 1]
+        J[k] = ((HP_INERTIA[k] + HP_MASS[k] * (rx[k] * rx[k] + rz[k] * rz[k])) + J[k + 1]) + \
+            (2.0 * (gx[k] * Sx[k + 1] + gz[k] * Sz[k + 1]) + HP_MB[k + 1] * (HP_SEG[k] * HP_SEG[k]))
+        Sx[k] = (HP_MASS[k] * rx[k] + Sx[k + 1]) + HP_MB[k + 1] * gx[k]
+        Sz[k] = (HP_MASS[k] * rz[k] + Sz[k + 1]) + HP_MB[k + 1] * gz[k]
+    rhs = [-Fbx[0], -Fbz[0], -Nb[0], Nb[1], Nb[2], Nb[3]]
+    # M: rotational block C[a][b] = s_a s_b (D_ab . S_b + J_b), s_0 = 1, s_i = -1,
+    # D_ab = pivot b - pivot a; coupling rows M[0][2+b] = s_b Sz_b, M[1][2+b] = -s_b Sx_b
+    Dx = {(0, 1): gx[0], (1, 2): gx[1], (2, 3): gx[2]}
+    Dz = {(0, 1): gz[0], (1, 2): gz[1], (2, 3): gz[2]}
+    Dx[(0, 2)], Dz[(0, 2)] = gx[0] + gx[1], gz[0] + gz[1]
+    Dx[(0, 3)], Dz[(0, 3)] = Dx[(0, 2)] + gx[2], Dz[(0, 2)] + gz[2]
+    Dx[(1, 3)], Dz[(1, 3)] = gx[1] + gx[2], gz[1] + gz[2]
+    C = [[None] * 4 for _ in range(4)]
+    for a in range(4):
+        C[a][a] = J[a]
+        for b in range(a + 1, 4):
+            val = (Dx[(a, b)] * Sx[b] + Dz[(a, b)] * Sz[b]) + J[b]
+            C[a][b] = -val if a == 0 else val
+    B0 = [Sz[0], -Sz[1], -Sz[2], -Sz[3]]
+    B1 = [-Sx[0], Sx[1], Sx[2], Sx[3]]
+    return rhs, C, B0, B1
+
+
+def hopper_solve(rhs, C, B0, B1):
+    """qdd of [[mt I, B], [B^T, C]] qdd = rhs: Schur complement on the rotational
+    block, 4x4 LDL^T, back-substitution of the translational accelerations."""
+    K = [[None] * 4 for _ in range(4)]
+    for a in range(4):
+        for b in range(a, 4):
+            K[a][b] = C[a][b] - (B0[a] * B0[b] + B1[a] * B1[b]) * HP_IMT
+            K[b][a] = K[a][b]
+    rr = [rhs[2 + a] - (B0[a] * rhs[0] + B1[a] * rhs[1]) * HP_IMT for a in range(4)]
+    x = ldl_solve(K, rr, 4)
+    t0 = rhs[0] - (((B0[0] * x[0] + B0[1] * x[1]) + B0[2] * x[2]) + B0[3] * x[3])
+    t1 = rhs[1] - (((B1[0] * x[0] + B1[1] * x[1]) + B1[2] * x[2]) + B1[3] * x[3])
+    return [t0 * HP_IMT, t1 * HP_IMT] + x
+
+
+def ldl_solve(M, rhs, n):
+    """LDL^T solve of an n x n SPD system (nested lists), in the device kernel's
+    operation order."""
+    L = [[None] * n for _ in range(n)]
+    D, iD = [None] * n, [None] * n
+    for j in range(n):
+        d = M[j][j]
+        for k in range(j):
+            d = d - (L[j][k] * L[j][k]) * D[k]
+        D[j] = d
+        iD[j] = 1.0 / d
+        for i in range(j + 1, n):
+            acc = M[i][j]
+            for k in range(j):
+                acc = acc - (L[i][k] * L[j][k]) * D[k]
+            L[i][j] = acc * iD[j]
+    y = [None] * n
+    for i in range(n):
+        acc = rhs[i]
+        for k in range(i):
+            acc = acc - L[i][k] * y[k]
+        y[i] = acc
+    x = [None] * n
+    for i in range(n - 1, -1, -1):
+        acc = y[i] * iD[i]
+        for k in range(i + 1, n):
+            acc = acc - L[k][i] * x[k]
+        x[i] = acc
+    return x
+
+
+def ldl_solve6(M, rhs):
+    return ldl_solve([[M[:, i, j] for j in range(6)] for i in range(6)], rhs, 6)
 
 
 def hopper_step(qpos, qvel, a):
@@ -151,12 +389,15 @@ def hopper_step(qpos, qvel, a):
     tau = HP_GEAR * ac
     x_before = qpos[:, 0].copy()
     q, v = qpos.copy(), qvel.copy()
-    for _ in range(HP_FRAME_SKIP):
-        q, v = _hopper_substep(q, v, tau)
+    with np.errstate(all="ignore"):
+        for _ in range(HP_FRAME_SKIP):
+            q, v = _hopper_substep(q, v, tau)
     x_after = q[:, 0]
-    rew = (x_after - x_before) / (HP_DT * HP_FRAME_SKIP) + 1.0 - 1e-3 * (a * a).sum(axis=1)
+    asq = ((a[:, 0] * a[:, 0]) + (a[:, 1] * a[:, 1])) + (a[:, 2] * a[:, 2])
+    rew = (x_after - x_before) / (HP_DT * HP_FRAME_SKIP) + 1.0 - 1e-3 * asq
     s = np.concatenate([q, v], axis=1)
-    healthy = np.isfinite(s).all(axis=1) & (np.abs(s[:, 2:]) < 100).all(axis=1) & (q[:, 1] > 0.7) & (np.abs(q[:, 2]) < 0.2)
+    with np.errstate(invalid="ignore"):
+        healthy = np.isfinite(s).all(axis=1) & (np.abs(s[:, 2:]) < 100).all(axis=1) & (q[:, 1] > 0.7) & (np.abs(q[:, 2]) < 0.2)
     return q, v, rew, ~healthy
 
 
