@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Benchmark: full TRPO iterations on the Hopper-v2-shaped env, 4096 envs x 1024 steps per GPU.
+"""Benchmark: full TRPO iterations on Hopper-v2 (articulated-body dynamics), 4096 envs x 1024 steps per GPU.
 
 One "step" = one TRPO iteration of run_policy_gradient_algorithm (core.py:135-171):
 lock-step rollout of E x T env steps -> GAE + standardisation -> VF L-BFGS fit ->
@@ -16,6 +16,7 @@ times, the live HIP-event roofline of the dominant kernel (Fisher-vector product
 and of the GAE scan, and the CPU oracle timed on a bounded sample of the workload.
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -164,7 +165,7 @@ def main():
     total_steps = n_local * world * K
     value = total_steps / elapsed
     if rank != 0:
-        return
+        return runner
     fpr = flops_per_row(agent.policy.net)
     kinfo = {}
     for name in ("fvp_jvp_rows", "fvp_vjp"):
@@ -173,11 +174,12 @@ def main():
             achieved = fpr[name] * n_local / (mean_ms * 1e-3) / 1e12
             kinfo[name] = dict(launches=cnt, mean_ms=mean_ms, total_ms=tot_ms, tflops=achieved)
     dom = max(kinfo, key=lambda k: kinfo[k]["total_ms"])
-    traffic = None
+    pmc = {}
     pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")  # measured on the default Hopper config
-    if os.path.exists(pmc_path) and args.env == "Hopper-v2" and not agent.policy.net.layered:
+    if os.path.exists(pmc_path) and args.env == "Hopper-v2" and not agent.policy.net.layered and E == 4096 and Tn == 1024:
         with open(pmc_path) as f:
-            traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+            pmc = json.load(f)
+    traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
     roofline = {"bound": "mfma", "achieved": round(kinfo[dom]["tflops"], 3), "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(kinfo[dom]["tflops"] / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
                 "kernel": dom, "flop_per_row": fpr[dom], "rows_per_launch": n_local,
@@ -187,7 +189,8 @@ def main():
         cnt, mean_ms, _ = kern["gae_scan"]
         gbs = GAE_BYTES_PER_ROW * n_local / (mean_ms * 1e-3) / 1e9
         gae = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-               "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_row": GAE_BYTES_PER_ROW, "mean_launch_ms": round(mean_ms, 4)}
+               "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": pmc.get("gae_scan", {}).get("hbm_bytes_per_launch"),
+               "bytes_per_row": GAE_BYTES_PER_ROW, "mean_launch_ms": round(mean_ms, 4)}
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": K,
         "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1000, 3), "higher_is_better": True,
@@ -210,7 +213,25 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(cpu_E, cpu_T, args.env, hid)
     print(json.dumps(line), flush=True)
+    return runner
+
+
+def _release(runner):
+    """Drop the captured rollout graph, device buffers and the CU-masked streams before
+    interpreter teardown: a stream left to the HIP runtime's own teardown is destroyed
+    after an attached rocprofv3 has finalised, which crashed the process at exit
+    (tools/teardown_probe.py)."""
+    if runner is not None:
+        runner.col.graph = None
+    del runner
+    gc.collect()
+    if torch.cuda.is_available():
+        from modular_rl_amd import streams
+        streams.destroy_all()
+        torch.cuda.empty_cache()
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    _release(main())

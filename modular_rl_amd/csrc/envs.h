@@ -175,7 +175,15 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
   phi[0] = q[2];
 #pragma unroll
   for (int j = 1; j < 4; ++j) phi[j] = phi[j - 1] - q[2 + j];
+#ifdef MRL_HP_ABL_NOSINCOS  // diagnostic timing build only (results are wrong)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    sg[k] = phi[k] - phi[k] * phi[k] * phi[k] * (1.0 / 6.0);
+    cg[k] = 1.0 - phi[k] * phi[k] * 0.5;
+  }
+#else
   par.sincos4(phi, sg, cg);
+#endif
   om[0] = v[2];
 #pragma unroll
   for (int j = 1; j < 4; ++j) om[j] = om[j - 1] - v[2 + j];
@@ -207,6 +215,11 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
     paz[j + 1] = paz[j] - w2 * gz[j];
   }
   double ct[4][3];
+#ifdef MRL_HP_ABL_NOCONTACT  // diagnostic timing build only (results are wrong)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ct[k][0] = ct[k][1] = ct[k][2] = pz[k] * 1e-3;
+  if (false)
+#endif
   par.contacts(
       [&](int k, double* out) {
         hopper_contacts(k, sel4(k, pz[0], pz[1], pz[2], pz[3]), sel4(k, pvx[0], pvx[1], pvx[2], pvx[3]),
@@ -289,7 +302,12 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
     }
 #pragma unroll
   for (int a = 0; a < 4; ++a) rr[a] = rhs[2 + a] - (B0[a] * rhs[0] + B1[a] * rhs[1]) * HP_IMT;
+#ifdef MRL_HP_ABL_NOLDL  // diagnostic timing build only (results are wrong)
+#pragma unroll
+  for (int a = 0; a < 4; ++a) x[a] = rr[a] * K[a][a];
+#else
   ldl_solve4(K, rr, x);
+#endif
   const double t0 = rhs[0] - (((B0[0] * x[0] + B0[1] * x[1]) + B0[2] * x[2]) + B0[3] * x[3]);
   const double t1 = rhs[1] - (((B1[0] * x[0] + B1[1] * x[1]) + B1[2] * x[2]) + B1[3] * x[3]);
   const double qdd[6] = {t0 * HP_IMT, t1 * HP_IMT, x[0], x[1], x[2], x[3]};

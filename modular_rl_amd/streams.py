@@ -4,6 +4,7 @@ Used by the pipelined training loop: the rollout of iteration k+1 (a chain of
 latency-bound step launches that occupy one block per CU on E/64 CUs) runs on one
 CU set while the value-function fit of iteration k runs on the complementary set.
 """
+import atexit
 import ctypes
 
 import torch
@@ -18,9 +19,26 @@ def cu_count():
     return int(n.value)
 
 
+_created = []  # raw handles of the streams made here, destroyed at interpreter exit
+
+
+def destroy_all():
+    """Destroy every CU-masked stream (after draining the device).  Runs at interpreter
+    exit: a stream left to the HIP runtime's own teardown is destroyed after an
+    attached profiler (rocprofv3) has finalised, and that crashed the process."""
+    if not _created:
+        return
+    torch.cuda.synchronize()
+    while _created:
+        call("mrl_stream_destroy", ctypes.c_void_p(_created.pop()))
+
+
+atexit.register(destroy_all)
+
+
 def masked_stream(cus):
     """A new HIP stream restricted to the CU ids in ``cus`` (torch.cuda.ExternalStream).
-    The stream lives for the rest of the process."""
+    The stream lives until destroy_all() (at the latest, interpreter exit)."""
     _lib.load(require_gpu=True)
     n = cu_count()
     words = (n + 31) // 32
@@ -31,6 +49,7 @@ def masked_stream(cus):
         mask[c // 32] |= 1 << (c % 32)
     out = ctypes.c_void_p()
     call("mrl_stream_create_cu_mask", mask, words, ctypes.byref(out))
+    _created.append(out.value)
     return torch.cuda.ExternalStream(out.value)
 
 

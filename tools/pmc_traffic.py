@@ -20,8 +20,8 @@ ROLES = [
     ("rows_surrgrad", "mlp_rows_kernel<2>"),
     ("rows_vfloss", "mlp_rows_kernel<3>"),
     ("rollout_step", "rollout_step_kernel"),
-    ("gae_summary", "gae_summary_kernel"),
-    ("gae_final", "gae_final_kernel"),
+    ("gae_scan", "gae_scan_kernel"),
+    ("episode_stats", "episode_stats_kernel<"),
     ("gemm_nn", "gemm_f32_kernel<false, false, 128>"),
     ("gemm_nt", "gemm_f32_kernel<false, true, 128>"),
     ("gemm_tn", "gemm_f32_kernel<true, false, 128>"),
