@@ -223,8 +223,10 @@ __device__ inline void forward_head_lowreg(const float* lds, const MlpDims& d, c
 // JVP to the head from the cached primal activations: no primal chain is recomputed
 // (the head outputs z come from the cached h2 on the VALU)
 template <class XL>
+// need_z = false (DiagGauss Fisher metric: 1/sigma^2, independent of the mean) skips
+// the primal head, z is left 0
 __device__ inline void jvp_head_cached(const float* lds, const float* ldt, const MlpDims& d, const XL& xl, int lane,
-                                       const float* cache, float* z, float* dz) {
+                                       const float* cache, float* z, float* dz, bool need_z = true) {
   const int h = lane >> 5;
   f32x16 h1[2], dh1[2];
   cache_load(cache, lane, 0, h1[0]);
@@ -254,11 +256,11 @@ __device__ inline void jvp_head_cached(const float* lds, const float* ldt, const
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int r = 0; r < 16; ++r) da[r] *= (1.f - a[r] * a[r]);
-    head_partial_mt(lds, d, a, mo, h, z);
+    if (need_z) head_partial_mt(lds, d, a, mo, h, z);
     head_partial_mt(lds, d, da, mo, h, dz);
     head_partial_mt(ldt, d, a, mo, h, dzt);
   }
-  head_finish(lds, d, z);
+  if (need_z) head_finish(lds, d, z);
 #pragma unroll
   for (int o = 0; o < MAX_OUT; ++o) dz[o] += dzt[o];
   head_finish(ldt, d, dz);

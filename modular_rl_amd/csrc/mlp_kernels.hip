@@ -36,7 +36,10 @@ int hip_check(hipError_t e, const char* what) {
 }
 
 constexpr int ROWS_BLOCK = 256;
-constexpr int ROWS_MAX_BLOCKS = 1024;
+#ifndef MRL_ROWS_MAX_BLOCKS
+#define MRL_ROWS_MAX_BLOCKS 1024
+#endif
+constexpr int ROWS_MAX_BLOCKS = MRL_ROWS_MAX_BLOCKS;
 constexpr int VJP_MAX_BLOCKS = 256;
 constexpr int SCR_FLOATS = 2 * 64 * IMG_PAD;  // per-wave transpose scratch
 
@@ -80,7 +83,7 @@ __global__ __launch_bounds__(ROWS_BLOCK, 2) void mlp_rows_kernel(RowsArgs a, con
     XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
     float z[MAX_OUT], dz[MAX_OUT];
     float* ctile = a.cache != nullptr ? a.cache + tile * CACHE_TILE_FLOATS : nullptr;
-    if (CACHED) jvp_head_cached(lds, ldt, d, xl, lane, ctile, z, dz);
+    if (CACHED) jvp_head_cached(lds, ldt, d, xl, lane, ctile, z, dz, a.head != MRL_HEAD_GAUSS);
     else if (EPI == MRL_EPI_FVP) forward_jvp_head_lowreg(lds, ldt, d, xl, lane, z, dz);
     else forward_head_lowreg(lds, d, xl, lane, z, a.cache_mode == MRL_CACHE_WRITE ? ctile : nullptr);
     if constexpr (EPI == MRL_EPI_PPOSGD) {
