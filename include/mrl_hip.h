@@ -184,7 +184,11 @@ int mrl_concat_time(const float* obs, const int32_t* ep_t, int64_t n, int32_t n_
  *         flag=1 when rdotr<tol; pass `flag` as the `skip` of the next Fvp kernels.
  * ax (fp64 [n], optional: NULL skips it) accumulates (F + damping I) x, which the
  * step scaling needs (trpo.py:119-122) -- A is linear, so A sum v_k p_k = sum v_k z_k
- * and no Fisher product of the step direction has to be run. */
+ * and no Fisher product of the step direction has to be run.
+ * `state` (and the `out` of mrl_trpo_step_ax) must hold mrl_cg_state_doubles(n) doubles:
+ * above 65,536 elements the passes run on 256 blocks and keep their block partials
+ * there (wide nets, e.g. Humanoid P = 727,074). */
+int64_t mrl_cg_state_doubles(int64_t n);
 int mrl_cg_init(const double* b, int64_t n, double* x, double* r, double* p, float* p32, double* ax,
                 double* state, int32_t* flag, void* stream);
 int mrl_cg_update(const float* fvp, double damping, double residual_tol, int64_t n, double* x, double* r,

@@ -344,6 +344,167 @@ __global__ __launch_bounds__(CG_T) void trpo_step_ax_kernel(const double* __rest
   }
 }
 
+// ---- multi-block CG / step scaling for large n (wide nets: Humanoid P = 727,074).
+// The single-block kernels above stream n fp64 elements through one CU (1.6 ms per
+// CG update at P = 727 k); here each of CGB blocks owns one contiguous chunk, block
+// partial sums go to a scratch area of `state` / `out` (mrl_cg_state_doubles), and
+// every block reduces the CGB partials in the same fixed order, so all blocks derive
+// bit-identical scalars.  The scalars and the flag are written by a 1-thread kernel
+// after the last pass, so no block ever reads a value this update is writing.
+constexpr int CGB = 256;                    // blocks of the multi-block passes
+constexpr int CGB_T = 256;                  // threads per block
+constexpr int64_t CG_SMALL_N = 65536;       // n at or below: the single-block kernels
+constexpr int CG_SCALARS = 8;               // state[0..7]; partials from state[8]
+
+__device__ inline void cg_chunk(int64_t n, int64_t& lo, int64_t& hi) {
+  const int64_t chunk = ((n + CGB - 1) / CGB + CGB_T - 1) / CGB_T * CGB_T;
+  lo = (int64_t)blockIdx.x * chunk;
+  hi = min(n, lo + chunk);
+}
+__device__ inline double blk_sum(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = CGB_T / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+// sum of the CGB partials part[0..CGB) in a fixed order (identical in every block)
+__device__ inline double part_sum(const double* part, double* red) {
+  return blk_sum(threadIdx.x < CGB ? part[threadIdx.x] : 0.0, red);
+}
+
+__global__ __launch_bounds__(CGB_T) void cgm_init_kernel(const double* __restrict__ b, int64_t n, double* x, double* r,
+                                                          double* p, float* p32, double* ax, double* part) {
+  __shared__ double red[CGB_T];
+  int64_t lo, hi;
+  cg_chunk(n, lo, hi);
+  double s = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += CGB_T) {
+    const double bi = b[i];
+    x[i] = 0.0;
+    if (ax) ax[i] = 0.0;
+    r[i] = bi;
+    p[i] = bi;
+    p32[i] = (float)bi;
+    s += bi * bi;
+  }
+  s = blk_sum(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+__global__ __launch_bounds__(CGB_T) void cgm_init_final_kernel(double* state, int32_t* flag) {
+  __shared__ double red[CGB_T];
+  const double s = part_sum(state + CG_SCALARS, red);
+  if (threadIdx.x == 0) {
+    state[0] = s;
+    state[1] = 0.0;
+    state[2] = 0.0;
+    flag[0] = 0;
+    flag[1] = 0;
+  }
+}
+// pass 1: p.z partials
+__global__ __launch_bounds__(CGB_T) void cgm_pz_kernel(const float* __restrict__ fvp, double damping, int64_t n,
+                                                        const double* __restrict__ p, double* state,
+                                                        const int32_t* flag) {
+  __shared__ double red[CGB_T];
+  if (flag[0] != 0) return;
+  int64_t lo, hi;
+  cg_chunk(n, lo, hi);
+  double s = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += CGB_T) s += p[i] * ((double)fvp[i] + damping * p[i]);
+  s = blk_sum(s, red);
+  if (threadIdx.x == 0) state[CG_SCALARS + blockIdx.x] = s;
+}
+// pass 2: v = rdotr / p.z; x += v p; ax += v z; r -= v z; r.r partials
+__global__ __launch_bounds__(CGB_T) void cgm_xr_kernel(const float* __restrict__ fvp, double damping, int64_t n,
+                                                        double* x, double* r, const double* __restrict__ p,
+                                                        double* ax, double* state, const int32_t* flag) {
+  __shared__ double red[CGB_T];
+  if (flag[0] != 0) return;
+  const double v = state[0] / part_sum(state + CG_SCALARS, red);
+  int64_t lo, hi;
+  cg_chunk(n, lo, hi);
+  double s = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += CGB_T) {
+    const double pi = p[i];
+    const double z = (double)fvp[i] + damping * pi;
+    x[i] += v * pi;
+    if (ax) ax[i] += v * z;
+    const double ri = r[i] - v * z;
+    r[i] = ri;
+    s += ri * ri;
+  }
+  s = blk_sum(s, red);
+  if (threadIdx.x == 0) state[CG_SCALARS + CGB + blockIdx.x] = s;
+}
+// pass 3: mu = r.r / rdotr; p = r + mu p
+__global__ __launch_bounds__(CGB_T) void cgm_p_kernel(int64_t n, const double* __restrict__ r, double* p, float* p32,
+                                                       const double* state, const int32_t* flag) {
+  __shared__ double red[CGB_T];
+  if (flag[0] != 0) return;
+  const double mu = part_sum(state + CG_SCALARS + CGB, red) / state[0];
+  int64_t lo, hi;
+  cg_chunk(n, lo, hi);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += CGB_T) {
+    const double pi = r[i] + mu * p[i];
+    p[i] = pi;
+    p32[i] = (float)pi;
+  }
+}
+__global__ __launch_bounds__(CGB_T) void cgm_final_kernel(double tol, double* state, int32_t* flag) {
+  __shared__ double red[CGB_T];
+  if (flag[0] != 0) return;
+  const double pz = part_sum(state + CG_SCALARS, red);
+  const double newr = part_sum(state + CG_SCALARS + CGB, red);
+  if (threadIdx.x == 0) {
+    state[0] = newr;
+    state[1] = pz;
+    state[2] += 1.0;
+    if (newr < tol) flag[0] = 1;
+  }
+}
+// step scaling: x.ax and g.x partials, then every block derives shs / lm and writes its
+// chunk of fullstep = x / lm (block 0 the scalars)
+__global__ __launch_bounds__(CGB_T) void cgm_step_part_kernel(const double* __restrict__ ax,
+                                                               const double* __restrict__ x, const float* __restrict__ g,
+                                                               int64_t n, double* out) {
+  __shared__ double red[CGB_T];
+  int64_t lo, hi;
+  cg_chunk(n, lo, hi);
+  double s = 0.0, sg = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += CGB_T) {
+    s += x[i] * ax[i];
+    sg += (double)g[i] * x[i];
+  }
+  s = blk_sum(s, red);
+  sg = blk_sum(sg, red);
+  if (threadIdx.x == 0) {
+    out[CG_SCALARS + blockIdx.x] = s;
+    out[CG_SCALARS + CGB + blockIdx.x] = sg;
+  }
+}
+__global__ __launch_bounds__(CGB_T) void cgm_step_kernel(const double* __restrict__ x, double max_kl, int64_t n,
+                                                          double* fullstep, double* out) {
+  __shared__ double red[CGB_T];
+  const double xAx = part_sum(out + CG_SCALARS, red);
+  const double gx = part_sum(out + CG_SCALARS + CGB, red);
+  const double shs = 0.5 * xAx;
+  const double lm = sqrt(shs / max_kl);
+  int64_t lo, hi;
+  cg_chunk(n, lo, hi);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += CGB_T) fullstep[i] = x[i] / lm;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    out[0] = shs;
+    out[1] = lm;
+    out[2] = -gx;
+    out[3] = -gx / lm;
+  }
+}
+
 __global__ void axpy_cast_kernel(const float* __restrict__ a, const double* __restrict__ b, double frac, int64_t n,
                                  float* __restrict__ o) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -607,18 +768,34 @@ int mrl_vf_target(const float* ret, const float* vpred, double mixfrac, int64_t 
   return hip_check(hipGetLastError(), "mrl_vf_target");
 }
 
+int64_t mrl_cg_state_doubles(int64_t n) { return n > CG_SMALL_N ? CG_SCALARS + 2 * CGB : 4; }
+
 int mrl_cg_init(const double* b, int64_t n, double* x, double* r, double* p, float* p32, double* ax, double* state,
                 int32_t* flag, void* stream) {
   if (!b || !x || !r || !p || !p32 || !state || !flag) return fail(E_ARG, "null pointer");
-  hipLaunchKernelGGL(cg_init_kernel, dim3(1), dim3(CG_T), 0, (hipStream_t)stream, b, n, x, r, p, p32, ax, state, flag);
+  hipStream_t s = (hipStream_t)stream;
+  if (n > CG_SMALL_N) {
+    hipLaunchKernelGGL(cgm_init_kernel, dim3(CGB), dim3(CGB_T), 0, s, b, n, x, r, p, p32, ax, state + CG_SCALARS);
+    hipLaunchKernelGGL(cgm_init_final_kernel, dim3(1), dim3(CGB_T), 0, s, state, flag);
+  } else {
+    hipLaunchKernelGGL(cg_init_kernel, dim3(1), dim3(CG_T), 0, s, b, n, x, r, p, p32, ax, state, flag);
+  }
   return hip_check(hipGetLastError(), "mrl_cg_init");
 }
 
 int mrl_cg_update(const float* fvp, double damping, double residual_tol, int64_t n, double* x, double* r, double* p,
                   float* p32, double* ax, double* state, int32_t* flag, void* stream) {
   if (!fvp || !x || !r || !p || !p32 || !state || !flag) return fail(E_ARG, "null pointer");
-  hipLaunchKernelGGL(cg_update_kernel, dim3(1), dim3(CG_T), 0, (hipStream_t)stream, fvp, damping, residual_tol, n, x, r,
-                     p, p32, ax, state, flag);
+  hipStream_t s = (hipStream_t)stream;
+  if (n > CG_SMALL_N) {
+    hipLaunchKernelGGL(cgm_pz_kernel, dim3(CGB), dim3(CGB_T), 0, s, fvp, damping, n, p, state, flag);
+    hipLaunchKernelGGL(cgm_xr_kernel, dim3(CGB), dim3(CGB_T), 0, s, fvp, damping, n, x, r, p, ax, state, flag);
+    hipLaunchKernelGGL(cgm_p_kernel, dim3(CGB), dim3(CGB_T), 0, s, n, r, p, p32, state, flag);
+    hipLaunchKernelGGL(cgm_final_kernel, dim3(1), dim3(CGB_T), 0, s, residual_tol, state, flag);
+  } else {
+    hipLaunchKernelGGL(cg_update_kernel, dim3(1), dim3(CG_T), 0, s, fvp, damping, residual_tol, n, x, r, p, p32, ax,
+                       state, flag);
+  }
   return hip_check(hipGetLastError(), "mrl_cg_update");
 }
 
@@ -633,8 +810,13 @@ int mrl_trpo_step(const float* fvp, const double* x, const float* g, double damp
 int mrl_trpo_step_ax(const double* ax, const double* x, const float* g, double max_kl, int64_t n, double* fullstep,
                      double* out, void* stream) {
   if (!ax || !x || !g || !fullstep || !out) return fail(E_ARG, "null pointer");
-  hipLaunchKernelGGL(trpo_step_ax_kernel, dim3(1), dim3(CG_T), 0, (hipStream_t)stream, ax, x, g, max_kl, n, fullstep,
-                     out);
+  hipStream_t s = (hipStream_t)stream;
+  if (n > CG_SMALL_N) {
+    hipLaunchKernelGGL(cgm_step_part_kernel, dim3(CGB), dim3(CGB_T), 0, s, ax, x, g, n, out);
+    hipLaunchKernelGGL(cgm_step_kernel, dim3(CGB), dim3(CGB_T), 0, s, x, max_kl, n, fullstep, out);
+  } else {
+    hipLaunchKernelGGL(trpo_step_ax_kernel, dim3(1), dim3(CG_T), 0, s, ax, x, g, max_kl, n, fullstep, out);
+  }
   return hip_check(hipGetLastError(), "mrl_trpo_step_ax");
 }
 

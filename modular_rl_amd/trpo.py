@@ -53,9 +53,10 @@ class HipTrpoOps:
         self.cand = torch.zeros(P, **f32)
         self.cand_image = torch.zeros_like(net.image)
         self.tan_image = torch.zeros_like(net.image)
-        self.state = torch.zeros(4, **f64)
+        ns = int(_lib.load().mrl_cg_state_doubles(self.P))  # scalars + block partials (wide nets)
+        self.state = torch.zeros(ns, **f64)
         self.flag = torch.zeros(2, dtype=torch.int32, device=dev)
-        self.step_out = torch.zeros(4, **f64)
+        self.step_out = torch.zeros(ns, **f64)
         self.sums = torch.zeros(4, **f64)
         self.batch = None
 
@@ -187,7 +188,7 @@ class TrpoUpdater:
                 fv = ops.fvp(ops.p32, skip=ops.flag)
                 comm.allreduce_(fv)
                 ops.cg_update(fv, damping, self.RESIDUAL_TOL)
-            out = ops.trpo_step(g, max_kl).cpu().numpy()
+            out = ops.trpo_step(g, max_kl)[:4].cpu().numpy()
             shs, lm, neggdotstepdir, rate = (float(v) for v in out)
             fval = losses_before[0]
 
