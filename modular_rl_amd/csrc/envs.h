@@ -453,9 +453,29 @@ __device__ inline void humanoid_step(double* s, const float* a, double& rew, boo
   done = !healthy;
 }
 
-// 376-d observation, written through out(k, value) (SoA global rows on the layered path)
+constexpr int HM_OBS_SLOTS = 16;
+// body b's features from its joint angle phi = q[6+b], joint velocity vb = v[6+b],
+// root angular velocity v3 = v[3 + b%3] and root linear velocities v0, v2
 template <class Out>
-__device__ inline void humanoid_obs(const double* s, Out out) {
+__device__ inline void humanoid_body_features(int b, double phi, double vb, double v3, double v0, double v2,
+                                              Out out) {
+  const double m = hm_body_mass(b);
+  const int base = 45 + 10 * b;
+  for (int k = 0; k < 5; ++k) out(base + k, m * cos((double)k * phi));
+  for (int k = 1; k < 6; ++k) out(base + 4 + k, m * sin((double)k * phi));
+  double sph, cph;
+  sincos(phi, &sph, &cph);
+  const int cb = 185 + 6 * b;
+  out(cb + 0, vb);
+  out(cb + 1, v3);
+  out(cb + 2, v0 * cph);
+  out(cb + 3, v2 * sph);
+  out(cb + 4, vb * cph);
+  out(cb + 5, vb * sph);
+}
+// slot 14: qpos[2:], cos(pitch), qvel, zeros, actuator torques
+template <class Out>
+__device__ inline void humanoid_obs_misc(const double* s, Out out) {
   const double* q = s;
   const double* v = s + HM_NQ;
   const double* tau = s + HM_NQ + HM_NV;
@@ -464,26 +484,15 @@ __device__ inline void humanoid_obs(const double* s, Out out) {
   out(21, cos(q[4]));
 #pragma unroll
   for (int i = 0; i < HM_NV; ++i) out(22 + i, v[i]);
-#pragma unroll
-  for (int b = 0; b < 14; ++b) {
-    const double phi = q[6 + b];
-    const double m = hm_body_mass(b);
-    const int base = 45 + 10 * b;
-    for (int k = 0; k < 5; ++k) out(base + k, m * cos((double)k * phi));
-    for (int k = 1; k < 6; ++k) out(base + 4 + k, m * sin((double)k * phi));
-    double sph, cph;
-    sincos(phi, &sph, &cph);
-    const int cb = 185 + 6 * b;
-    out(cb + 0, v[6 + b]);
-    out(cb + 1, v[3 + b % 3]);
-    out(cb + 2, v[0] * cph);
-    out(cb + 3, v[2] * sph);
-    out(cb + 4, v[6 + b] * cph);
-    out(cb + 5, v[6 + b] * sph);
-  }
   for (int i = 0; i < 6; ++i) out(269 + i, 0.0);
 #pragma unroll
   for (int i = 0; i < HM_ACT; ++i) out(275 + i, tau[i]);
+}
+// slot 15: external contact forces of the two feet
+template <class Out>
+__device__ inline void humanoid_obs_contacts(const double* s, Out out) {
+  const double* q = s;
+  const double* v = s + HM_NQ;
   double fxr, fzr, fnr, ftr, fxl, fzl, fnl, ftl;
   hm_leg(q, v, 5, 6, fxr, fzr, fnr, ftr);
   hm_leg(q, v, 9, 10, fxl, fzl, fnl, ftl);
@@ -495,6 +504,20 @@ __device__ inline void humanoid_obs(const double* s, Out out) {
     else if (i == 55) val = ftl;
     out(292 + i, val);
   }
+}
+
+// 376-d observation, written through out(k, value) (SoA global rows on the layered
+// path), in 16 independent slots so a kernel can spread one env over 16 threads:
+// slot b < 14 = body b's 10 harmonic + 6 velocity features, 14 = qpos / cos / qvel /
+// zeros / torques, 15 = contact features
+template <class Out>
+__device__ inline void humanoid_obs(const double* s, Out out) {
+  const double* q = s;
+  const double* v = s + HM_NQ;
+#pragma unroll
+  for (int b = 0; b < 14; ++b) humanoid_body_features(b, q[6 + b], v[6 + b], v[3 + b % 3], v[0], v[2], out);
+  humanoid_obs_misc(s, out);
+  humanoid_obs_contacts(s, out);
 }
 
 }  // namespace mrl

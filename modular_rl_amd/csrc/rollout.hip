@@ -59,7 +59,7 @@ template <int ENV>
 struct EnvC;
 template <>
 struct EnvC<MRL_ENV_CARTPOLE> {
-  static constexpr int NS = CP_NS, OBS = CP_OBS, ACT = 2, DISCRETE = 1, MAX_STEPS = 200, NU = 4;
+  static constexpr int NS = CP_NS, OBS = CP_OBS, ACT = 2, DISCRETE = 1, MAX_STEPS = 200, NU = 4, OBS_SLOTS = 0;
   __device__ static void reset(const double* u, double* s) { cartpole_reset(u, s); }
   __device__ static void obs(const double* s, double* o) { cartpole_obs(s, o); }
   __device__ static void step_disc(double* s, int a, double& rew, bool& done) { cartpole_step(s, a, rew, done); }
@@ -75,7 +75,8 @@ struct EnvC<MRL_ENV_CARTPOLE> {
 };
 template <>
 struct EnvC<MRL_ENV_HOPPER> {
-  static constexpr int NS = HP_NS, OBS = HP_OBS, ACT = HP_ACT, DISCRETE = 0, MAX_STEPS = 1000, NU = 12;
+  static constexpr int NS = HP_NS, OBS = HP_OBS, ACT = HP_ACT, DISCRETE = 0, MAX_STEPS = 1000, NU = 12,
+                       OBS_SLOTS = 0;
   __device__ static void reset(const double* u, double* s) { hopper_reset(u, s); }
   __device__ static void obs(const double* s, double* o) { hopper_obs(s, o); }
   __device__ static void step_disc(double*, int, double&, bool&) {}
@@ -93,7 +94,8 @@ struct EnvC<MRL_ENV_HOPPER> {
 };
 template <>
 struct EnvC<MRL_ENV_HUMANOID> {
-  static constexpr int NS = HM_NS, OBS = HM_OBS, ACT = HM_ACT, DISCRETE = 0, MAX_STEPS = 1000, NU = HM_NU;
+  static constexpr int NS = HM_NS, OBS = HM_OBS, ACT = HM_ACT, DISCRETE = 0, MAX_STEPS = 1000, NU = HM_NU,
+                       OBS_SLOTS = HM_OBS_SLOTS;  // obs features by lrollout_feat_kernel
   __device__ static void reset(const double* u, double* s) { humanoid_reset(u, s); }
   __device__ static void step_disc(double*, int, double&, bool&) {}
   __device__ static void step_cont(double* s, const float* a, double& rew, bool& done) {
@@ -103,6 +105,7 @@ struct EnvC<MRL_ENV_HUMANOID> {
   __device__ static void obs_out(const double* s, Out out) {
     humanoid_obs(s, out);
   }
+
 };
 
 struct EnvInfo {
@@ -836,8 +839,36 @@ __global__ __launch_bounds__(RB) void lrollout_act_kernel(RollArgs a, const floa
   sample_and_step<ENV>(a, row, z, logstd, zn, s, rew, done);
   finish_env_step<ENV>(a, e, row, t, s, rew, done);
   double* raw = a.b.raw_obs;
-  EC::obs_out(s, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
+  if constexpr (EC::OBS_SLOTS == 0) EC::obs_out(s, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
   raw[(int64_t)O * E + e] = rew;
+}
+
+// raw next observation of envs whose features split into OBS_SLOTS independent slots
+// (Humanoid: 376 features, ~160 angle functions per env): thread (slot, env) of a
+// 16-env block evaluates one slot from the stepped state, instead of one thread per
+// env evaluating all of them serially inside lrollout_act_kernel.
+template <int ENV>
+__global__ __launch_bounds__(RB) void lrollout_feat_kernel(RollArgs a) {
+  using EC = EnvC<ENV>;
+  constexpr int NS = EC::NS, EB = RB / EC::OBS_SLOTS;
+  const int E = a.d.n_envs;
+  const int slot = threadIdx.x / EB, e = blockIdx.x * EB + threadIdx.x % EB;
+  if (e >= E) return;
+  const double* st = a.b.env_state + e;
+  double* raw = a.b.raw_obs;
+  auto out = [&](int k, double v) { raw[(int64_t)k * E + e] = v; };
+  static_assert(ENV == MRL_ENV_HUMANOID, "feature slots: Humanoid only");
+  if (slot < 14) {
+    humanoid_body_features(slot, st[(int64_t)(6 + slot) * E], st[(int64_t)(HM_NQ + 6 + slot) * E],
+                           st[(int64_t)(HM_NQ + 3 + slot % 3) * E], st[(int64_t)HM_NQ * E],
+                           st[(int64_t)(HM_NQ + 2) * E], out);
+  } else {
+    double s[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) s[i] = st[(int64_t)i * E];
+    if (slot == 14) humanoid_obs_misc(s, out);
+    else humanoid_obs_contacts(s, out);
+  }
 }
 
 __global__ void rollout_finish_kernel(RollArgs a, int O) {
@@ -996,6 +1027,11 @@ int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, cons
   const int D = ei.obs + 1;
   const dim3 genv((d->n_envs + 63) / 64), gpart(a.nb, (D + LCOLS - 1) / LCOLS);
   MRL_DISPATCH_ENV(d->env_id, lrollout_act_kernel, genv, dim3(64), 0, (hipStream_t)stream, a, z, logstd, t);
+  if (d->env_id == MRL_ENV_HUMANOID) {
+    constexpr int EB = RB / EnvC<MRL_ENV_HUMANOID>::OBS_SLOTS;
+    hipLaunchKernelGGL(lrollout_feat_kernel<MRL_ENV_HUMANOID>, dim3((d->n_envs + EB - 1) / EB), dim3(RB), 0,
+                       (hipStream_t)stream, a);
+  }
   hipLaunchKernelGGL(lrollout_partials_kernel, gpart, dim3(RB), 0, (hipStream_t)stream, a, D, (t + 1) & 1, 1);
   return hip_check(hipGetLastError(), "mrl_rollout_act");
 }
