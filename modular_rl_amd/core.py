@@ -67,7 +67,7 @@ class _GaeWorkspace:
     def get(self, T, E, device):
         nbytes = int(_lib.load().mrl_gae_workspace_bytes(int(T), int(E)))
         if self.ws is None or self.ws.numel() < nbytes or self.ws.device != device:
-            self.ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            self.ws = torch.zeros(nbytes, dtype=torch.uint8, device=device)  # zeroed arrival counter
             self.moments = torch.zeros(3, dtype=torch.float64, device=device)
         return self.ws, self.moments
 
