@@ -220,8 +220,6 @@ int mrl_cast_scale_f32_f64(const float* in, double scale, int64_t n, double* out
  * moments (fp64 [3]) <- (sum adv, sum adv^2, count)  (for core.py:100-105). */
 int mrl_gae(const float* rew, const float* vpred, const uint8_t* flags, int64_t T, int64_t E, double gamma,
             double lam, float* adv, float* ret, double* moments, void* workspace, void* stream);
-/* the workspace must be zero-filled before its first use (the kernel leaves its
- * arrival counter at 0 for the next call) */
 int64_t mrl_gae_workspace_bytes(int64_t T, int64_t E);
 /* adv <- (adv - mean)/std from global moments (sum, sumsq, n): numpy std, ddof=0, no eps */
 int mrl_standardize(float* adv, int64_t n, const double* moments, void* stream);

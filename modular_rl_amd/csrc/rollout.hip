@@ -392,24 +392,27 @@ template <int ENV>
 __global__ void noise_fill_kernel(RollArgs a, double* __restrict__ out) {
   using EC = EnvC<ENV>;
   constexpr int A = EC::ACT, P = EC::DISCRETE ? 1 : (A + 1) / 2;
-  const int64_t E = a.d.n_envs;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)a.d.horizon * E * P) return;
-  const int c = (int)(i % P);
-  const int64_t row = i / P;
-  const int t = (int)(row / E), e = (int)(row % E);
-  const uint32_t gid = (uint32_t)(a.d.env_offset + e);
-  const uint64_t w = (uint64_t)(*a.b.iteration) * (uint64_t)a.d.horizon + (uint64_t)t;
-  double u0, u1;
-  philox_uniform2(a.d.seed, 0, gid, w, (uint32_t)c, u0, u1);
-  if constexpr (EC::DISCRETE) {
-    out[row] = u0;
-  } else {
-    const double rad = sqrt(-2.0 * log(1.0 - u0));
-    double sn, cn;
-    sincos(2.0 * 3.141592653589793 * u1, &sn, &cn);
-    out[row * A + 2 * c] = rad * cn;
-    if (2 * c + 1 < A) out[row * A + 2 * c + 1] = rad * sn;
+  // grid (ceil(E * P / 256), min(T, 65535)): steps t = blockIdx.y + k * gridDim.y, no runtime
+  // 64-bit division
+  const int E = a.d.n_envs;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E * P) return;
+  const int c = i % P, e = i / P;
+  for (int t = blockIdx.y; t < a.d.horizon; t += gridDim.y) {
+    const int64_t row = (int64_t)t * E + e;
+    const uint32_t gid = (uint32_t)(a.d.env_offset + e);
+    const uint64_t w = (uint64_t)(*a.b.iteration) * (uint64_t)a.d.horizon + (uint64_t)t;
+    double u0, u1;
+    philox_uniform2(a.d.seed, 0, gid, w, (uint32_t)c, u0, u1);
+    if constexpr (EC::DISCRETE) {
+      out[row] = u0;
+    } else {
+      const double rad = sqrt(-2.0 * log(1.0 - u0));
+      double sn, cn;
+      sincos(2.0 * 3.141592653589793 * u1, &sn, &cn);
+      out[row * A + 2 * c] = rad * cn;
+      if (2 * c + 1 < A) out[row * A + 2 * c + 1] = rad * sn;
+    }
   }
 }
 
@@ -961,9 +964,9 @@ int mrl_rollout_noise(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, doub
   if (!out) return fail(E_ARG, "null noise rows");
   RollArgs a = make_args(d, b);
   const EnvInfo ei = env_info(d->env_id);
-  const int64_t n = (int64_t)d->horizon * d->n_envs * (ei.discrete ? 1 : (ei.act + 1) / 2);
-  MRL_DISPATCH_ENV(d->env_id, noise_fill_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                   (hipStream_t)stream, a, out);
+  const int64_t per_step = (int64_t)d->n_envs * (ei.discrete ? 1 : (ei.act + 1) / 2);
+  MRL_DISPATCH_ENV(d->env_id, noise_fill_kernel, dim3((unsigned)((per_step + 255) / 256), (unsigned)(d->horizon < 65535 ? d->horizon : 65535)),
+                   dim3(256), 0, (hipStream_t)stream, a, out);
   return hip_check(hipGetLastError(), "mrl_rollout_noise");
 }
 

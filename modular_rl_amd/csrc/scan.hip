@@ -41,8 +41,7 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_scan_kernel(const float* __re
                                                                const uint8_t* __restrict__ flags, int64_t T,
                                                                int64_t E, double gamma, double lam,
                                                                float* __restrict__ adv, float* __restrict__ ret,
-                                                               double* __restrict__ part, unsigned* counter,
-                                                               double* __restrict__ moments) {
+                                                               double* __restrict__ part) {
   __shared__ double sA[GAE_NC * GAE_PITCH], sB[GAE_NC * GAE_PITCH], sR[GAE_NC * GAE_PITCH],
       sC[GAE_NC * GAE_PITCH];
   __shared__ double red[2][GAE_THREADS / 64];
@@ -172,48 +171,14 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_scan_kernel(const float* __re
     red[1][wave] = s2;
   }
   __syncthreads();
-  __shared__ int last;
   if (tid == 0) {
     double t1 = 0.0, t2 = 0.0;
     for (int w = 0; w < GAE_THREADS / 64; ++w) {
       t1 += red[0][w];
       t2 += red[1][w];
     }
-    // the block whose arrival comes last reduces the moments (no second launch).  The
-    // partials are handed over without fences (a release fence would write back the
-    // L2, i.e. the 33 MB of adv / ret this kernel just stored): agent-scope (sc1)
-    // stores drained before the relaxed arrival, and sc1 loads by the last arriver
-    // (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms)
-    __hip_atomic_store(&part[blk * 2 + 0], t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&part[blk * 2 + 1], t2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  // fixed-order reduction of the block partials (== the former moments_final_kernel)
-  __shared__ double fin[2][GAE_THREADS];
-  double s1f = 0.0, s2f = 0.0;
-  for (int64_t i = tid; i < (int64_t)gridDim.x; i += GAE_THREADS) {
-    s1f += __hip_atomic_load(&part[i * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s2f += __hip_atomic_load(&part[i * 2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  fin[0][tid] = s1f;
-  fin[1][tid] = s2f;
-  __syncthreads();
-  for (int o = GAE_THREADS / 2; o > 0; o >>= 1) {
-    if (tid < o) {
-      fin[0][tid] += fin[0][tid + o];
-      fin[1][tid] += fin[1][tid + o];
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    moments[0] = fin[0][0];
-    moments[1] = fin[1][0];
-    moments[2] = (double)T * (double)E;
-    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+    part[blk * 2 + 0] = t1;
+    part[blk * 2 + 1] = t2;
   }
 }
 
@@ -768,17 +733,14 @@ int mrl_gae(const float* rew, const float* vpred, const uint8_t* flags, int64_t 
   const int64_t nb = (E + GAE_EB - 1) / GAE_EB;
   if ((int64_t)GAE_NC * GAE_LMAX * (E + GAE_EB) >= ((int64_t)1 << 29))
     return fail(E_UNSUPPORTED, "mrl_gae: E too large for 32-bit segment offsets");
-  // [0, 64): the arrival counter (zeroed by the caller once, left at 0 by every launch, at a
-  // fixed offset so a workspace reused for another T x E still holds 0 there); then partials
-  unsigned* counter = reinterpret_cast<unsigned*>(workspace);
-  double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(workspace) + 64);
+  double* part = reinterpret_cast<double*>(workspace);
   hipStream_t s = (hipStream_t)stream;
   // chunk length: the smallest power of two that covers T in one segment, at most GAE_LMAX
   int L = 1;
   while (L < GAE_LMAX && (int64_t)GAE_NC * L < T) L <<= 1;
 #define MRL_GAE_LAUNCH(LL)                                                                                      \
   hipLaunchKernelGGL(gae_scan_kernel<LL>, dim3(nb), dim3(GAE_THREADS), 0, s, rew, vpred, flags, T, E, gamma, lam, \
-                     adv, ret, part, counter, moments)
+                     adv, ret, part)
   switch (L) {
     case 1: MRL_GAE_LAUNCH(1); break;
     case 2: MRL_GAE_LAUNCH(2); break;
@@ -788,6 +750,7 @@ int mrl_gae(const float* rew, const float* vpred, const uint8_t* flags, int64_t 
     default: MRL_GAE_LAUNCH(32); break;
   }
 #undef MRL_GAE_LAUNCH
+  hipLaunchKernelGGL(moments_final_kernel, dim3(1), dim3(256), 0, s, part, nb, (double)(T * E), moments);
   return hip_check(hipGetLastError(), "mrl_gae");
 }
 
