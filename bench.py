@@ -64,25 +64,28 @@ def cpu_baseline(E, Tn, env_id="Hopper-v2", hid=(64, 64), seed=0):
     except Exception:  # pragma: no cover
         threads = os.cpu_count()
     rng = np.random.default_rng(seed)
-    kind, O, A = {"Hopper-v2": (RO.HOPPER, 11, 3), "Humanoid-v2": (RO.HUMANOID, 376, 17)}[env_id]
-    spec = T.Spec(O, list(hid), A, "gauss")
+    kind, O, A, limit = {"Hopper-v2": (RO.HOPPER, 11, 3, 1000), "Humanoid-v2": (RO.HUMANOID, 376, 17, 1000),
+                         "CartPole-v0": (RO.CARTPOLE, 4, 2, 200)}[env_id]
+    head = "softmax" if env_id == "CartPole-v0" else "gauss"
+    spec = T.Spec(O, list(hid), A, head)
     vspec = T.Spec(O + 1, list(hid), 1, "linear")
-    th = T.mlp_init(rng, spec.shapes, True)
+    th = T.mlp_init(rng, spec.shapes, head == "gauss")
     thv = T.mlp_init(rng, vspec.shapes, False)
     envs = RO.Envs(kind, E, seed)
     fs = RO.FilterState(O + 1)
     t0 = time.perf_counter()
-    out, fs = RO.collect(envs, fs, spec, th, Tn, 1000, 0)
+    out, fs = RO.collect(envs, fs, spec, th, Tn, limit, 0)
     N = E * Tn
     ob = out["obs"].reshape(N, O).astype(np.float64)
-    X = np.concatenate([ob, (out["ep_t"].reshape(N) / 1000.0)[:, None]], axis=1)
+    X = np.concatenate([ob, (out["ep_t"].reshape(N) / float(limit))[:, None]], axis=1)
     v = T.mlp_forward(vspec, thv, X, np.float32)[0][:, 0].astype(np.float64).reshape(Tn, E)
     flags = out["flags"]
     adv, ret = T.gae_batched(out["rew"].astype(np.float64), v, (flags & 1) > 0, (flags & 2) > 0, 0.995, 0.97)
     adv = T.standardize(adv).reshape(N)
     T.vf_fit(vspec, thv, X, ret.reshape(N), mixfrac=0.1, maxiter=2, dtype=np.float32)
-    T.trpo_update(spec, th, ob, out["act"].reshape(N, A).astype(np.float64), adv,
-                  out["prob"].reshape(N, 2 * A).astype(np.float64), cg_damping=0.1, max_kl=0.01, dtype=np.float32)
+    act = out["act"].reshape(N, -1).astype(np.float64)
+    T.trpo_update(spec, th, ob, act[:, 0] if head == "softmax" else act, adv,
+                  out["prob"].reshape(N, -1).astype(np.float64), cg_damping=0.1, max_kl=0.01, dtype=np.float32)
     dt = time.perf_counter() - t0
     return {"value": N / dt, "unit": "env-steps/s", "cores": int(threads), "kind": "port",
             "sample": f"one full TRPO iteration (rollout+GAE+VF fit+update) of the numpy oracle on {env_id} "
@@ -198,7 +201,8 @@ def main():
         "config": {"workload": f"{args.env} ({DYNAMICS[args.env]}) {E} envs x {Tn} steps per GPU, one TRPO iteration "
                                "per step (rollout+GAE+VF L-BFGS+TRPO CG/linesearch)",
                    "envs_per_gpu": E, "horizon": Tn, "global_batch": E * Tn * world, "parallelism": f"dp{world}",
-                   "policy": f"{env.obs_dim}-{'-'.join(map(str, hid))}-{env.act_dim} tanh DiagGauss "
+                   "policy": f"{env.obs_dim}-{'-'.join(map(str, hid))}-{env.act_dim} tanh "
+                             f"{'Categorical' if args.env == 'CartPole-v0' else 'DiagGauss'} "
                              f"({'layered GEMM' if agent.policy.net.layered else 'fused'} path)",
                    "gamma": 0.995, "lam": 0.97,
                    "max_kl": 0.01, "cg_damping": 0.1,

@@ -28,11 +28,15 @@ def timed(fn, reps=5):
 
 
 def main():
-    nin, nout = 11, 3
-    net = MlpNet(nin, nout, _lib.HEAD_GAUSS)
-    net.set_flat(glorot_init(rng, nin, nout, _lib.HEAD_GAUSS))
+    # MRL_PROBE_NET=nin,nout,head (head gauss | softmax), default the Hopper policy 11,3,gauss
+    nin, nout, hname = (os.environ.get("MRL_PROBE_NET") or "11,3,gauss").split(",")
+    nin, nout = int(nin), int(nout)
+    head = _lib.HEAD_GAUSS if hname == "gauss" else _lib.HEAD_SOFTMAX
+    net = MlpNet(nin, nout, head)
+    net.set_flat(glorot_init(rng, nin, nout, head))
     x = torch.randn(N, nin, device='cuda')
-    act = torch.randn(N, nout, device='cuda')
+    act = (torch.randn(N, nout, device='cuda') if head == _lib.HEAD_GAUSS
+           else torch.randint(0, nout, (N,), device='cuda', dtype=torch.int32))
     adv = torch.randn(N, device='cuda')
     prob = net.forward(x, N).clone()
     gh = torch.zeros(N * net.gh, device='cuda')
@@ -57,7 +61,7 @@ def main():
 
     lib = os.environ.get("MRL_LIB_PATH", "default")
     surrgrad()
-    print(f"[{os.path.basename(lib)}] surrgrad {timed(surrgrad):.3f} ms  fvp_jvp_rows {timed(jvp):.3f} ms  "
+    print(f"[{os.path.basename(lib)} {nin},{nout},{hname}] surrgrad {timed(surrgrad):.3f} ms  fvp_jvp_rows {timed(jvp):.3f} ms  "
           f"vjp {timed(vjp):.3f} ms  prob {timed(prob_pass):.3f} ms", flush=True)
 
 
