@@ -19,6 +19,10 @@ def enable(on=True):
     _events.clear()
 
 
+def enabled():
+    return _ENABLED
+
+
 def start(name):
     if _ENABLED:
         e = torch.cuda.Event(enable_timing=True)
@@ -31,6 +35,13 @@ def stop(name):
         e = torch.cuda.Event(enable_timing=True)
         e.record()
         _events[name].append((_open.pop(name), e))
+
+
+def drop_last(name, k):
+    """Forget the last k timed regions of `name` (launches a device flag made skip, e.g.
+    Fisher products after CG converged, so averages cover launches that did the work)."""
+    if _ENABLED and k > 0 and name in _events:
+        del _events[name][-k:]
 
 
 def summary():

@@ -190,6 +190,10 @@ class TrpoUpdater:
                 ops.cg_update(fv, damping, self.RESIDUAL_TOL)
             out = ops.trpo_step(g, max_kl)[:4].cpu().numpy()
             shs, lm, neggdotstepdir, rate = (float(v) for v in out)
+            if timing.enabled():
+                skipped = self.CG_ITERS - int(ops.state[2].item())  # Fisher products after convergence
+                timing.drop_last("fvp_jvp_rows", skipped)
+                timing.drop_last("fvp_vjp", skipped)
             fval = losses_before[0]
 
             def f(stepfrac):
