@@ -17,6 +17,8 @@ import time
 from collections import OrderedDict
 from importlib import import_module
 
+import os
+
 import numpy as np
 import torch
 
@@ -160,7 +162,7 @@ def run_policy_gradient_algorithm(env, agent, usercfg=None, callback=None):
         emit(done)
 
 
-LAYERED_ROLLOUT_CUS = 64
+LAYERED_ROLLOUT_CUS = int(os.environ.get("MRL_LAYERED_ROLLOUT_CUS", "64"))
 
 
 def rollout_cu_split(n_rollout, n_cus):
