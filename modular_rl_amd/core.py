@@ -13,11 +13,10 @@ The per-path API (``rollout``, ``do_rollouts_serial``, ``compute_advantage(vf,
 paths, ...)``, ``agent.updater(paths)``) is kept for compatibility and runs the
 same kernels on E = 1.
 """
+import os
 import time
 from collections import OrderedDict
 from importlib import import_module
-
-import os
 
 import numpy as np
 import torch
