@@ -29,8 +29,12 @@ namespace mrl {
 #ifndef MRL_GAE_LMAX
 #define MRL_GAE_LMAX 32
 #endif
+#ifndef MRL_GAE_NC
+#define MRL_GAE_NC 32
+#endif
 constexpr int GAE_EB = MRL_GAE_EB;       // envs per block: one 64 B row segment
-constexpr int GAE_NC = 32;               // chunks per segment: one per lane of a half-wave
+constexpr int GAE_NC = MRL_GAE_NC;       // chunks per segment: one per lane of a half-wave (32) or wave (64)
+static_assert(GAE_NC == 32 || GAE_NC == 64, "scan groups are half-waves or waves");
 constexpr int GAE_THREADS = GAE_EB * GAE_NC;
 constexpr int GAE_LMAX = MRL_GAE_LMAX;
 constexpr int GAE_PITCH = GAE_EB + 1;    // LDS row pitch (doubles): 2-way conflicts at most
@@ -54,7 +58,7 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_scan_kernel(const float* __re
   const int64_t S = (int64_t)GAE_NC * L;
   const int64_t nseg = (T + S - 1) / S;
   const int lane = tid & 63, wave = tid >> 6;
-  const int sc = lane & 31, se = 2 * wave + (lane >> 5);  // scan: half-wave = env slot se, lane = chunk sc
+  const int sc = tid % GAE_NC, se = tid / GAE_NC;  // scan: a group of GAE_NC lanes = env slot se, lane = chunk sc
   double carry_a = 0.0, carry_r = 0.0;                    // held by the half-wave of env slot se
   double s1 = 0.0, s2 = 0.0;
   for (int64_t seg = nseg - 1; seg >= 0; --seg) {
@@ -117,10 +121,10 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_scan_kernel(const float* __re
       double a = sA[sc * GAE_PITCH + se], b = sB[sc * GAE_PITCH + se];
       double r = sR[sc * GAE_PITCH + se], cc = sC[sc * GAE_PITCH + se];
 #pragma unroll
-      for (int off = 1; off < 32; off <<= 1) {
+      for (int off = 1; off < GAE_NC; off <<= 1) {
         const double a2 = __shfl_down(a, off), b2 = __shfl_down(b, off);
         const double r2 = __shfl_down(r, off), c2 = __shfl_down(cc, off);
-        if (sc + off < 32) {
+        if (sc + off < GAE_NC) {
           a = a + b * a2;
           b = b * b2;
           r = r + cc * r2;
@@ -129,9 +133,9 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_scan_kernel(const float* __re
       }
       // exclusive: the composite of the later chunks, applied to the segment carry
       double xa = __shfl_down(a, 1), xb = __shfl_down(b, 1), xr = __shfl_down(r, 1), xc = __shfl_down(cc, 1);
-      if (sc == 31) { xa = 0.0; xb = 1.0; xr = 0.0; xc = 1.0; }
+      if (sc == GAE_NC - 1) { xa = 0.0; xb = 1.0; xr = 0.0; xc = 1.0; }
       const double in_a = xa + xb * carry_a, in_r = xr + xc * carry_r;
-      const int l0 = lane & 32;  // the half-wave's chunk 0
+      const int l0 = lane & (64 - GAE_NC);  // the group's chunk 0 (lane 32 or 0 of a half-wave, 0 of a wave)
       const double a0 = __shfl(a, l0), b0 = __shfl(b, l0), r0 = __shfl(r, l0), c0 = __shfl(cc, l0);
       carry_a = a0 + b0 * carry_a;
       carry_r = r0 + c0 * carry_r;
