@@ -274,6 +274,11 @@ class Collector:
     # ------------------------------------------------------------ episode stats
     def episode_stats(self, batch):
         """add_episode_stats scalars (core.py:31-44), reduced on device and over ranks."""
+        return self.episode_stats_finish(self.episode_stats_launch(batch))
+
+    def episode_stats_launch(self, batch):
+        """The device half: per-episode sums / maxima reduced on device and over ranks,
+        returned as a device tensor (no host sync; the pipelined loop reads it later)."""
         call("mrl_episode_stats", ptr(batch.rew), ptr(batch.flags), batch.T, batch.E, ptr(self._ep_out),
              ptr(self._ep_ws), stream())
         v = self._ep_out[:6].clone()
@@ -283,6 +288,10 @@ class Collector:
             if self.comm.world > 1:
                 torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
                 v[3], v[5] = mx[0], mx[1]
+        return v
+
+    @staticmethod
+    def episode_stats_finish(v):
         cnt, sr, sr2, mr, sl, ml = (float(x) for x in v.cpu().numpy())
         mean = sr / cnt
         return dict(NumEpBatch=int(cnt), EpRewMean=mean,

@@ -268,16 +268,16 @@ class IterationRunner:
         ev["upd0"] = self._event()
         pol_stats = agent.updater.update(batch)
         ev["upd1"] = self._event()
-        ep = col.episode_stats(batch)
         if self.pipeline:
-            self.pending = (batch, ep, pol_stats)
+            # read back with the deferred VF fit's stats (no host sync here)
+            self.pending = (batch, col.episode_stats_launch(batch), pol_stats)
         else:
-            done = self._stats(ep, vf_stats, pol_stats)
+            done = self._stats(col.episode_stats(batch), vf_stats, pol_stats)
         self.last_phase_events = ev
         return done
 
     def _fit_pending(self, fit_stream, ev):
-        batch, ep, pol_stats = self.pending
+        batch, ep_dev, pol_stats = self.pending
         self.pending = None
         main = torch.cuda.current_stream()
         if fit_stream is None:
@@ -291,7 +291,7 @@ class IterationRunner:
                 vf_stats = self.agent.baseline.fit_batch(batch)
                 ev["vf1"] = self._event()
             main.wait_stream(fit_stream)
-        return self._stats(ep, vf_stats, pol_stats)
+        return self._stats(self.col.episode_stats_finish(ep_dev), vf_stats, pol_stats)
 
     def drain(self):
         """Fit the deferred VF of the last iteration (on all CUs) and return its stats."""

@@ -118,7 +118,7 @@ class HipTrpoOps:
 
 
 def _losses(sums, n_glob):
-    s = sums.detach().double().cpu().numpy()
+    s = sums.detach().double().cpu().numpy() if torch.is_tensor(sums) else np.asarray(sums, dtype=np.float64)
     return np.array([-s[0] / n_glob, s[1] / n_glob, s[2] / n_glob])
 
 
@@ -174,24 +174,28 @@ class TrpoUpdater:
         g, sums = ops.surrgrad()
         comm.allreduce_(g)
         comm.allreduce_(sums)
-        losses_before = _losses(sums, n_glob)
         diag = {"n_global": n_glob}
+        # The conjugate gradient is issued before the host looks at g: losses_before,
+        # the zero-gradient test (np.allclose(g, 0) == max|g| <= 1e-8) and the step
+        # scaling come back in ONE device-to-host copy after CG, instead of a pipeline
+        # drain ahead of it.  A zero gradient discards the CG result (theta untouched).
+        damping, max_kl = float(cfg["cg_damping"]), float(cfg["max_kl"])
+        ops.cg_init(ops.neg_g64(g))
+        for _ in range(self.CG_ITERS):
+            fv = ops.fvp(ops.p32, skip=ops.flag)
+            comm.allreduce_(fv)
+            ops.cg_update(fv, damping, self.RESIDUAL_TOL)
+        step = ops.trpo_step(g, max_kl)[:4]
+        host = torch.cat([step, sums.double()[:3], g.abs().max().double().reshape(1), ops.state[:3]]).cpu().numpy()
+        losses_before = _losses(host[4:7], n_glob)
         losses_after = losses_before
-        g_host = g.detach().double().cpu().numpy()
-        if np.allclose(g_host, 0):
+        if host[7] <= 1e-8:
             print("got zero gradient. not updating")
             diag["skipped"] = True
         else:
-            damping, max_kl = float(cfg["cg_damping"]), float(cfg["max_kl"])
-            ops.cg_init(ops.neg_g64(g))
-            for _ in range(self.CG_ITERS):
-                fv = ops.fvp(ops.p32, skip=ops.flag)
-                comm.allreduce_(fv)
-                ops.cg_update(fv, damping, self.RESIDUAL_TOL)
-            out = ops.trpo_step(g, max_kl)[:4].cpu().numpy()
-            shs, lm, neggdotstepdir, rate = (float(v) for v in out)
+            shs, lm, neggdotstepdir, rate = (float(v) for v in host[:4])
             if timing.enabled():
-                skipped = self.CG_ITERS - int(ops.state[2].item())  # Fisher products after convergence
+                skipped = self.CG_ITERS - int(host[10])  # Fisher products after convergence
                 timing.drop_last("fvp_jvp_rows", skipped)
                 timing.drop_last("fvp_vjp", skipped)
             fval = losses_before[0]
@@ -207,9 +211,8 @@ class TrpoUpdater:
             else:
                 net.theta.copy_(thprev)
             net.pack()
-            st = ops.state.cpu().numpy()
             diag.update(skipped=False, shs=shs, lm=lm, neggdotstepdir=neggdotstepdir, expected_rate=rate,
-                        success=success, k=k, stepfrac=frac, cg_iters=int(st[2]), rdotr=float(st[0]))
+                        success=success, k=k, stepfrac=frac, cg_iters=int(host[10]), rdotr=float(host[8]))
         self.last_diag = diag
         out = OrderedDict()
         for (lname, lbefore, lafter) in zip(self.loss_names, losses_before, losses_after):
