@@ -61,7 +61,8 @@ def _policy(head, nin, nout, seed):
 
 @pytest.mark.parametrize("env_id,E,Tn,limit,inject", [
     ("CartPole-v0", 200, 48, 200, False), ("CartPole-v0", 7, 30, 12, True),
-    ("Hopper-v2", 150, 24, 1000, False), ("Hopper-v2", 130, 16, 9, True), ("CartPole-v0", 1, 40, 200, False)])
+    ("Hopper-v2", 150, 24, 1000, False), ("Hopper-v2", 130, 16, 9, True), ("CartPole-v0", 1, 40, 200, False),
+    ("Hopper-v2", 64, 200, 1000, False)])  # long horizon: episodes end and auto-reset through contact
 def test_rollout_matches_oracle(env_id, E, Tn, limit, inject):
     from modular_rl_amd.collector import Collector
     from modular_rl_amd.envs import make
