@@ -51,10 +51,9 @@ def merge_filter_deltas(s0, s1, comm):
             delta[2 + k] = md
             delta[2 + D + k] = S1 - S0 - (md - M0) ** 2 * n0 * nd / n1
     dev = "cuda" if comm.enabled and torch.distributed.get_backend() == "nccl" else "cpu"
-    all_d = comm.allgather(torch.as_tensor(delta).to(dev))
+    all_d = torch.stack(comm.allgather(torch.as_tensor(delta).to(dev))).cpu().numpy()  # one copy for all ranks
     out = np.array(s0, dtype=np.float64).copy()
     for d in all_d:
-        d = d.cpu().numpy()
         for which, cols in ((0, range(D - 1)), (1, [D - 1])):
             nb = d[which]
             if nb <= 0:
