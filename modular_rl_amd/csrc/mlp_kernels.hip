@@ -165,33 +165,25 @@ __device__ inline int vjp_row16(int kk, int q) { return 16 * (kk & 1) + 2 * q + 
 template <bool CACHED, bool WIDE>
 struct VjpIn {
   float x0[CACHED ? 1 : 16];  // layer-0 B operands x[row][2s+h]
-  f32x16 act[CACHED ? 4 : 1]; // cached h1[0], h1[1], h2[0], h2[1]
+  f32x16 act[CACHED ? 2 : 1]; // cached h2[0], h2[1] (h1 is loaded by the tile itself)
   float xg[WIDE ? 16 : 8];    // gW0 A operands x[row0 + r(8kk+q)][16mt + (lane&15)] at [8mt + q]
   float g[4];                 // head-gradient rows ghead[row][r+4h]
   float gs[MAX_OUT];          // summed head columns (DiagGauss logstd), lane half 0 only
 };
 
-// Branch-free prefetch: row indices are clamped to the batch and columns to the row
+// Branch-free loads: row indices are clamped to the batch and columns to the row
 // width, so every load is unconditional straight-line code; what must read as zero
 // (head-gradient entries of rows past n, of outputs past A, the logstd sums off lane
 // half 0) is masked when the tile USES the values (a select at load time would force
-// the wait that the prefetch exists to avoid).  The clamped gW0 operands of rows past
+// a wait right after the loads are issued).  The clamped gW0 operands of rows past
 // n multiply head-gradient rows that are exactly zero; those of columns past the
 // input width land in gW0 rows that are never stored.
-template <bool CACHED, bool WIDE>
-__device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn<CACHED, WIDE>& in) {
-  const int h = lane >> 5, j = lane & 31, i16 = lane & 15, kk = lane >> 4;
+// gW0 A operands of one tile (used last: issued after the operands of the first phases)
+template <bool WIDE>
+__device__ inline void vjp_load_xg(const VjpArgs& a, int64_t tile, int lane, float* xg) {
+  const int i16 = lane & 15, kk = lane >> 4;
   constexpr int MT0 = WIDE ? 2 : 1;
-  const int64_t row0 = tile * 32, row = row0 + j, last = a.n - 1;
-  if constexpr (CACHED) {
-    const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) cache_load(ct, lane, q, in.act[q]);
-  } else {
-    XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, row < a.n};
-#pragma unroll
-    for (int s = 0; s < 16; ++s) in.x0[s] = (s < a.d.KS0p) ? xl(2 * s + h) : 0.f;
-  }
+  const int64_t row0 = tile * 32, last = a.n - 1;
   if (a.ept == nullptr) {
 #pragma unroll
     for (int mt = 0; mt < MT0; ++mt) {
@@ -199,7 +191,7 @@ __device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn<
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int64_t xr = row0 + vjp_row16(kk, q);
-        in.xg[8 * mt + q] = a.x[(xr < last ? xr : last) * a.n_obs + cc];
+        xg[8 * mt + q] = a.x[(xr < last ? xr : last) * a.n_obs + cc];
       }
     }
   } else {
@@ -210,9 +202,24 @@ __device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn<
       for (int q = 0; q < 8; ++q) {
         const int64_t xr = row0 + vjp_row16(kk, q);
         XGlobal xq{a.x, a.ept, a.ts_limit, a.n_obs, xr, xr < a.n};
-        in.xg[8 * mt + q] = (c < a.d.O) ? xq(c) : 0.f;
+        xg[8 * mt + q] = (c < a.d.O) ? xq(c) : 0.f;
       }
     }
+  }
+}
+
+template <bool CACHED, bool WIDE>
+__device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn<CACHED, WIDE>& in) {
+  const int h = lane >> 5, j = lane & 31;
+  const int64_t row0 = tile * 32, row = row0 + j, last = a.n - 1;
+  if constexpr (CACHED) {
+    const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) cache_load(ct, lane, 2 + q, in.act[q]);
+  } else {
+    XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, row < a.n};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) in.x0[s] = (s < a.d.KS0p) ? xl(2 * s + h) : 0.f;
   }
   const float* gr = a.ghead + (row < last ? row : last) * a.gh;
 #pragma unroll
@@ -262,22 +269,28 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
 
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t stride = (int64_t)gridDim.x * 4;
-  // software pipeline: every global operand of tile i+1 is in flight while tile i computes
-  VjpIn<CACHED, WIDE> cur, nxt;
+  // Every global operand of a tile is issued at the tile's start (h2 and the head rows
+  // first, h1 and the gW0 operands, used later, after them).  A register prefetch of
+  // the next tile (double buffering) measured slower: its 84 registers went to AGPRs
+  // and were copied back every tile (1.11 ms vs 1.00 ms per launch at 4.19 M rows).
+  VjpIn<CACHED, WIDE> cur;
   int64_t tile = (int64_t)blockIdx.x * 4 + wave;
-  if (tile < ntiles) vjp_load(a, tile, lane, cur);
   for (; tile < ntiles; tile += stride) {
-    if (tile + stride < ntiles) vjp_load(a, tile + stride, lane, nxt);
+    vjp_load(a, tile, lane, cur);
     const int64_t row0 = tile * 32;
     Fwd f;
     if constexpr (CACHED) {
-      f.h1[0] = cur.act[0];
-      f.h1[1] = cur.act[1];
-      f.h2[0] = cur.act[2];
-      f.h2[1] = cur.act[3];
+      // h1 is first used after the gh1 chain: its loads are issued after the ones the
+      // first phases wait for
+      const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
+      cache_load(ct, lane, 0, f.h1[0]);
+      cache_load(ct, lane, 1, f.h1[1]);
+      f.h2[0] = cur.act[0];
+      f.h2[1] = cur.act[1];
     } else {
       forward_tile_pre(lds, d, cur.x0, lane, f);
     }
+    vjp_load_xg<WIDE>(a, tile, lane, cur.xg);  // used last
 
     // head gradient rows in C layout: register r of half h = out r + 4h (masked here,
     // not at load time: see vjp_load)
@@ -391,7 +404,6 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
     gb0 += rowsum32(scrB, lane);
     WAVE_LDS_ORDER();
     (void)row0;
-    cur = nxt;
   }
 
   // per-wave partial gradient in flat theta layout
