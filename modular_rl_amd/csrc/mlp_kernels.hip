@@ -42,6 +42,11 @@ constexpr int ROWS_BLOCK = 256;
 constexpr int ROWS_MAX_BLOCKS = MRL_ROWS_MAX_BLOCKS;
 constexpr int VJP_MAX_BLOCKS = 256;
 constexpr int SCR_FLOATS = 2 * 64 * IMG_PAD;  // per-wave transpose scratch
+#ifdef MRL_VJP_ABL_NOGW1  // diagnostic builds (tools/build_ablate.sh): drop one MFMA phase
+#define VJP_ABL_S4 0
+#else
+#define VJP_ABL_S4 4
+#endif
 
 static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -142,6 +147,10 @@ __device__ inline void write_img(float* img, const f32x16* t, int lane) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) img[(32 * mt + cperm(r, h)) * IMG_PAD + base] = t[mt][r];
 }
+
+// tanh' from the activation as one explicit fma, so its rounding never depends on the
+// compiler's contraction choice (the cached and uncached instantiations agree bit for bit)
+__device__ inline float dtanh(float h) { return fmaf(-h, h, 1.f); }
 
 __device__ inline float rowsum32(const float* img, int unit) {
   const float* p = img + unit * IMG_PAD;
@@ -335,27 +344,33 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
       for (int q = 0; q < 8; ++q)
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
+#ifndef MRL_VJP_ABL_NOGW2
           gW2[mt] = MFMA16(f4get(q < 4 ? a0[mt] : a1[mt], q & 3), f4get(q < 4 ? b0 : b1, q & 3), gW2[mt]);
+#else
+          ;
+#endif
     }
     if (lane < A) gb2 += rowsum32(scrB, lane);
     // (d) ga2 = gh2 * (1 - h2^2)
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) g2[m][r] *= (1.f - f.h2[m][r] * f.h2[m][r]);
+      for (int r = 0; r < 16; ++r) g2[m][r] *= dtanh(f.h2[m][r]);
     // (e) gh1 = W1 . ga2: registers + the weight image only, so its 64 MFMAs cover the
     //     h1 / ga2 transposes issued next
     f32x16 g1[2];
     g1[0] = zero16();
     g1[1] = zero16();
+#ifndef MRL_VJP_ABL_NOCHAIN
     chain<2>(lds, d.ba1, g2, lane, g1);
+#endif
     WAVE_LDS_ORDER();
     write_img(scrA, f.h1, lane);
     write_img(scrB, g2, lane);
     WAVE_LDS_ORDER();
     // (f) gW1 += H1^T GA2, and ga1 = gh1 * (1 - h1^2) on the VALU under it
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
+    for (int s4 = 0; s4 < VJP_ABL_S4; ++s4) {
       const float4 a0 = ld4(scrA + j * IMG_PAD + h * 16 + 4 * s4);
       const float4 a1 = ld4(scrA + (32 + j) * IMG_PAD + h * 16 + 4 * s4);
       const float4 b0 = ld4(scrB + j * IMG_PAD + h * 16 + 4 * s4);
@@ -381,7 +396,7 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) g1[m][r] *= (1.f - f.h1[m][r] * f.h1[m][r]);
+      for (int r = 0; r < 16; ++r) g1[m][r] *= dtanh(f.h1[m][r]);
     WAVE_LDS_ORDER();
     write_img(scrB, g1, lane);
     WAVE_LDS_ORDER();
@@ -399,7 +414,11 @@ __global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __
         for (int mt = 0; mt < MT0; ++mt)
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt)
+#ifndef MRL_VJP_ABL_NOGW0
             gW0[mt][nt] = MFMA16(cur.xg[8 * mt + q], f4get(q < 4 ? b0[nt] : b1[nt], q & 3), gW0[mt][nt]);
+#else
+          ;
+#endif
     }
     gb0 += rowsum32(scrB, lane);
     WAVE_LDS_ORDER();
