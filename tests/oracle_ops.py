@@ -92,3 +92,41 @@ class OracleOps:
     def candidate(self, theta_old, frac):
         self.cand.copy_(theta_old + frac * self.fullstep)
         return self.cand
+
+
+class OracleVfNet:
+    """Oracle-backed stand-in for the value-function MlpNet under vf.LbfgsOptimizer --
+    TEST ONLY.  rows(EPI_VFLOSS) returns this rank's squared-error sum and the head
+    gradient rows 2 (v - y) / N_global like the kernel; vjp_flat backpropagates them
+    through the float64 oracle.  theta holds float32 values, as on the device."""
+
+    def __init__(self, spec, theta):
+        self.spec, self.P, self.device = spec, spec.P, torch.device("cpu")
+        self.theta = torch.tensor(np.asarray(theta, np.float32), dtype=torch.float64)
+        self.ws = types.SimpleNamespace(get=lambda name, n, dtype: torch.zeros(n, dtype=torch.float64))
+        self._acts = None
+
+    def get_flat(self):
+        return self.theta.numpy().astype(np.float32)
+
+    def set_flat(self, th):
+        self.theta.copy_(torch.as_tensor(np.asarray(th, np.float32), dtype=torch.float64))
+
+    def partial_rows(self, n):
+        return 1
+
+    def rows(self, epi, x, n, ep_t=None, timestep_limit=1.0, inv_n_global=1.0, target=None, ghead=None,
+             partial=None):
+        z, self._acts = T.mlp_forward(self.spec, self.theta.numpy(), x)
+        err = z[:, 0] - target.numpy()
+        partial.zero_()
+        partial[0] = float(np.sum(err * err))
+        ghead.copy_(torch.as_tensor(2.0 * err * inv_n_global))
+
+    def reduce_partial(self, partial, n, sums):
+        sums.copy_(partial[:4])
+        return sums
+
+    def vjp_flat(self, x, n, ghead, g, ep_t=None, timestep_limit=1.0):
+        gz = ghead.numpy().reshape(-1, 1)
+        g.copy_(torch.as_tensor(T.flatten(T.mlp_vjp(self.spec, self.theta.numpy(), self._acts, gz))))

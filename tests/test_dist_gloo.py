@@ -5,12 +5,17 @@
   scaled correctly: g, every CG Fvp, loss sums, line-search losses).
 * merge_filter_deltas: 2 ranks pushing different observations from a common start
   end with the running stat of one process pushing all of them (rank order).
+* vf.LbfgsOptimizer (the VF fit, `core.py:663-697`) with the rows split over 2 ranks
+  (loss sums and gradients all-reduced per L-BFGS evaluation, scaled by 1/N_global)
+  ends where one rank holding all rows does, and where scipy L-BFGS-B on the float64
+  oracle loss does.
 """
 import os
 import types
 
 import numpy as np
 import pytest
+import scipy.optimize
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -41,6 +46,27 @@ def _update(rank_rows, comm):
     return pol.net.theta.numpy().copy(), stats, up.last_diag
 
 
+def _vf_data(N=600):
+    rng = np.random.default_rng(7)
+    spec = T.Spec(6, [64, 64], 1, "linear")
+    th = (T.mlp_init(rng, spec.shapes, False) + 0.05 * rng.standard_normal(spec.P)).astype(np.float32)
+    X = rng.standard_normal((N, 6)).astype(np.float32).astype(np.float64)
+    y = (np.sin(X[:, 0]) + 0.5 * X[:, 1] * X[:, 2] + 0.1 * rng.standard_normal(N)).astype(np.float32)
+    return spec, th, X, y
+
+
+def _vf_fit(rank_rows, comm):
+    from modular_rl_amd.vf import LbfgsOptimizer
+    from tests.oracle_ops import OracleVfNet
+    spec, th, X, y = _vf_data()
+    net = OracleVfNet(spec, th)
+    opt = LbfgsOptimizer(net, maxiter=2, comm=comm)
+    x, t = X[rank_rows], torch.as_tensor(y[rank_rows], dtype=torch.float64)
+    n_glob = comm.allreduce_int(len(x))
+    info = opt.update((x, None, 1.0, len(x), t, n_glob))
+    return net.get_flat().astype(np.float64), info
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -65,8 +91,9 @@ def _worker(rank, world, port, q):
         rr.push(r)
     s1 = np.concatenate([[rs.n, rr.n], np.append(rs.M, rr.M), np.append(rs.S, rr.S)])
     merged = merge_filter_deltas(s0, s1, comm)
+    th_vf, info_vf = _vf_fit(rows, comm)
     if rank == 0:
-        q.put((th, dict(stats), diag["k"], merged))
+        q.put((th, dict(stats), diag["k"], merged, th_vf, dict(info_vf)))
     dist.destroy_process_group()
 
 
@@ -78,7 +105,7 @@ def test_two_rank_update_equals_single_rank_and_oracle():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    th2, stats2, k2, merged = q.get(timeout=300)
+    th2, stats2, k2, merged, thv2, infov2 = q.get(timeout=300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -106,3 +133,19 @@ def test_two_rank_update_equals_single_rank_and_oracle():
             rr.push(rw)
     want = np.concatenate([[rs.n, rr.n], np.append(rs.M, rr.M), np.append(rs.S, rr.S)])
     np.testing.assert_allclose(merged, want, rtol=1e-10, atol=1e-10)
+    # VF fit: 2 ranks == 1 rank (float32 gradients summed per rank) == scipy on the oracle
+    thv1, infov1 = _vf_fit(slice(0, 600), Comm())
+    spec, thv, X, y = _vf_data()
+
+    def lossandgrad(t):
+        l, g, _, _ = T.vf_loss_grad(spec, t.astype(np.float32).astype(np.float64), X, y.astype(np.float64))
+        return float(l), g
+
+    thw, _, _ = scipy.optimize.fmin_l_bfgs_b(lossandgrad, thv.astype(np.float64), maxiter=2)
+    move = np.abs(thw - thv).max()
+    assert move > 1e-3
+    assert np.abs(thv2 - thv1).max() <= 1e-4 * move
+    assert np.abs(thv1 - thw.astype(np.float32)).max() <= 1e-5 * move
+    for k in ("loss_before", "loss_after", "mse_before", "mse_after"):
+        np.testing.assert_allclose(infov2[k], infov1[k], rtol=1e-6)
+    assert infov1["loss_after"] < infov1["loss_before"]
