@@ -43,15 +43,61 @@ def flops_per_row(net):
     mm = [dims[i] * dims[i + 1] for i in range(len(dims) - 1)]
     jvp = 2 * (mm[0] + 2 * sum(mm[1:]))
     vjp = 2 * (sum(mm) + sum(mm[1:]))
+    fwd = 2 * sum(mm)
     if getattr(net, "layered", False) or getattr(net, "use_cache", False):
         # the primal forward comes from the activation cache / recorded tape
-        return {"fvp_jvp_rows": jvp, "fvp_vjp": vjp}
-    return {"fvp_jvp_rows": 2 * sum(mm) + jvp, "fvp_vjp": vjp}
+        return {"fvp_jvp_rows": jvp, "fvp_vjp": vjp, "policy_forward": fwd}
+    return {"fvp_jvp_rows": fwd + jvp, "fvp_vjp": vjp, "policy_forward": fwd}
 
 
 DYNAMICS = {"Hopper-v2": "hopper.xml articulated-body dynamics", "Humanoid-v2": "surrogate dynamics",
             "CartPole-v0": "gym equations"}
 GAE_BYTES_PER_ROW = 17  # read r 4 + v 4 + flags 1, write adv 4 + ret 4
+PMC_FILE = "pmc_r01.json"
+
+
+def cpu_serial_c1(seconds=8.0, seed=0):
+    """the reference's serial loop restated -- ONE
+    CartPole env, a single-row (M = 1) policy forward per step (core.py:182-221,
+    StochPolicy.act core.py:261-267), then GAE, the VF fit and the TRPO update on the
+    batch (timesteps_per_batch 200, whole episodes: core.py:210-221).  Iterations
+    repeat until ``seconds`` have passed; one core (numpy per-row work)."""
+    from oracle import rollout_np as RO
+    from oracle import trpo_np as T
+    rng = np.random.default_rng(seed)
+    spec = T.Spec(4, [64, 64], 2, "softmax")
+    vspec = T.Spec(5, [64, 64], 1, "linear")
+    th = T.mlp_init(rng, spec.shapes, False)
+    thv = T.mlp_init(rng, vspec.shapes, False)
+    fs = RO.FilterState(5)
+    steps = iters = 0
+    from threadpoolctl import threadpool_limits
+    limit = threadpool_limits(1)  # one core, like the reference's single process
+    torch_threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        envs = RO.Envs(RO.CARTPOLE, 1, seed + iters)
+        out, fs = RO.collect(envs, fs, spec, th, 200, 200, iters)  # E = 1: one row per step
+        N = 200
+        ob = out["obs"].reshape(N, 4).astype(np.float64)
+        X = np.concatenate([ob, (out["ep_t"].reshape(N) / 200.0)[:, None]], axis=1)
+        v = T.mlp_forward(vspec, thv, X, np.float32)[0][:, 0].astype(np.float64).reshape(200, 1)
+        flags = out["flags"]
+        adv, ret = T.gae_batched(out["rew"].astype(np.float64), v, (flags & 1) > 0, (flags & 2) > 0, 0.995, 0.97)
+        adv = T.standardize(adv).reshape(N)
+        thv, _, _, _ = T.vf_fit(vspec, thv, X, ret.reshape(N), mixfrac=0.1, maxiter=2, dtype=np.float32)
+        act = out["act"].reshape(N, -1).astype(np.float64)[:, 0]
+        th, _, _ = T.trpo_update(spec, th, ob, act, adv, out["prob"].reshape(N, -1).astype(np.float64),
+                                 cg_damping=0.1, max_kl=0.01, dtype=np.float32)
+        steps += N
+        iters += 1
+    dt = time.perf_counter() - t0
+    limit.unregister()
+    torch.set_num_threads(torch_threads)
+    return {"value": steps / dt, "unit": "env-steps/s", "trpo_iters_per_sec": iters / dt, "cores": 1, "kind": "port",
+            "sample": f"C1: {iters} serial TRPO iterations of ONE CartPole-v0 env x 200 steps, one-row policy forward "
+                      f"per step, numpy oracle, {dt:.1f} s"}
 
 
 def cpu_baseline(E, Tn, env_id="Hopper-v2", hid=(64, 64), seed=0):
@@ -170,23 +216,43 @@ def main():
     if rank != 0:
         return runner
     fpr = flops_per_row(agent.policy.net)
+    pmc = {}
+    pmc_path = os.path.join(ROOT, "profiles", PMC_FILE)  # measured on the default Hopper config
+    if os.path.exists(pmc_path) and args.env == "Hopper-v2" and not agent.policy.net.layered and E == 4096 and Tn == 1024:
+        with open(pmc_path) as f:
+            pmc = json.load(f)
     kinfo = {}
     for name in ("fvp_jvp_rows", "fvp_vjp"):
         if name in kern:
             cnt, mean_ms, tot_ms = kern[name]
-            achieved = fpr[name] * n_local / (mean_ms * 1e-3) / 1e12
-            kinfo[name] = dict(launches=cnt, mean_ms=mean_ms, total_ms=tot_ms, tflops=achieved)
+            kinfo[name] = dict(launches=cnt, mean_ms=mean_ms, total_ms=tot_ms, rows_per_launch=n_local,
+                               flop_per_row=fpr[name])
+    if "rollout_steps" in kern:
+        # one timed region per iteration around the T step launches (graph replay on the
+        # rollout stream): the step-to-step mean, so it carries the inter-launch gap
+        cnt, mean_ms, tot_ms = kern["rollout_steps"]
+        kinfo["rollout_step"] = dict(launches=cnt * Tn, mean_ms=mean_ms / Tn, total_ms=tot_ms, rows_per_launch=E,
+                                     flop_per_row=fpr["policy_forward"], step_to_step=True)
+    for name, ki in kinfo.items():
+        ki["tflops"] = ki["flop_per_row"] * ki["rows_per_launch"] / (ki["mean_ms"] * 1e-3) / 1e12
+        ki["frac_fp32_mfma"] = ki["tflops"] / PEAK_FP32_TFLOPS
+        if pmc.get(name, {}).get("hbm_bytes_per_launch"):
+            ki["hbm_gbs_pmc"] = pmc[name]["hbm_bytes_per_launch"] / (ki["mean_ms"] * 1e-3) / 1e9
+    # the dominant kernel = the largest device time per iteration
     dom = max(kinfo, key=lambda k: kinfo[k]["total_ms"])
-    pmc = {}
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")  # measured on the default Hopper config
-    if os.path.exists(pmc_path) and args.env == "Hopper-v2" and not agent.policy.net.layered and E == 4096 and Tn == 1024:
-        with open(pmc_path) as f:
-            pmc = json.load(f)
     traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
     roofline = {"bound": "mfma", "achieved": round(kinfo[dom]["tflops"], 3), "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(kinfo[dom]["tflops"] / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-                "kernel": dom, "flop_per_row": fpr[dom], "rows_per_launch": n_local,
-                "mean_launch_ms": round(kinfo[dom]["mean_ms"], 4), "launches_timed": kinfo[dom]["launches"]}
+                "traffic_source": f"profiles/{PMC_FILE} (PMC FETCH_SIZE x2 + WRITE_SIZE, separate passes; "
+                                  "not measured in this run)" if traffic else None,
+                "kernel": dom, "flop_per_row": kinfo[dom]["flop_per_row"],
+                "rows_per_launch": kinfo[dom]["rows_per_launch"],
+                "mean_launch_ms": round(kinfo[dom]["mean_ms"], 5), "launches_timed": kinfo[dom]["launches"],
+                "ms_per_iter": round(kinfo[dom]["total_ms"] / K, 3)}
+    if dom == "rollout_step":
+        roofline["note"] = ("latency-bound: T dependent step launches, each a filter merge over all envs + the "
+                            "policy forward (the FLOPs counted) + fp64 env substeps, on E/64 CUs; mean is "
+                            "step-to-step (launch gap included)")
     gae = None
     if "gae_scan" in kern:
         cnt, mean_ms, _ = kern["gae_scan"]
@@ -210,12 +276,13 @@ def main():
         "trpo_iters_per_sec": round(K / elapsed, 4),
         "rollout_env_steps_per_sec": round(n_local * world * K / (phases["rollout"] * 1e-3), 1),
         "phase_ms_per_iter": {k: round(v / K, 3) for k, v in phases.items()},
-        "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()} for k, v in kinfo.items()},
+        "kernels": {k: {kk: (round(vv, 5) if isinstance(vv, float) else vv) for kk, vv in v.items()} for k, v in kinfo.items()},
         "roofline": roofline,
         "roofline_gae": gae,
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(cpu_E, cpu_T, args.env, hid)
+        line["cpu_baseline"]["serial_c1"] = cpu_serial_c1()
     print(json.dumps(line), flush=True)
     return runner
 

@@ -213,6 +213,15 @@ int mrl_gather_rows(const void* src, const int64_t* idx, int64_t n, int64_t row_
 /* out (fp64) = scale * (double)in ; in-place-safe */
 int mrl_cast_scale_f32_f64(const float* in, double scale, int64_t n, double* out, void* stream);
 
+/* Per-row probtype values on probability rows (the reference's Categorical /
+ * DiagGauss loglik, kl, entropy: core.py:349-359, 412-430), computed by the same fp32
+ * device helpers as the MLP row epilogues.  head MRL_HEAD_SOFTMAX: prob [n, k], x
+ * int32 [n]; MRL_HEAD_GAUSS: prob [n, 2k] = [mean | std], x fp32 [n, k].
+ * loglik[r] = log p(x_r), kl[r] = KL(prob_r || prob2_r), ent[r] = entropy(prob_r); any
+ * output may be NULL.  The reference checks them with validate_probtype (core.py:457-483). */
+int mrl_probtype_rows(int32_t head, int32_t k, int64_t n, const float* prob, const float* prob2, const void* x,
+                      float* loglik, float* kl, float* ent, void* stream);
+
 /* ---------------------------------------------------------------- advantage
  * GAE + discounted return over time-major [T, E] rows (core.py:63-75 with
  * misc_utils.py:9-27 discount): flags bit0 = episode ends at this row, bit1 = the
@@ -221,13 +230,21 @@ int mrl_cast_scale_f32_f64(const float* in, double scale, int64_t n, double* out
 int mrl_gae(const float* rew, const float* vpred, const uint8_t* flags, int64_t T, int64_t E, double gamma,
             double lam, float* adv, float* ret, double* moments, void* workspace, void* stream);
 int64_t mrl_gae_workspace_bytes(int64_t T, int64_t E);
-/* adv <- (adv - mean)/std from global moments (sum, sumsq, n): numpy std, ddof=0, no eps */
-int mrl_standardize(float* adv, int64_t n, const double* moments, void* stream);
+/* adv <- (adv - mean)/std, numpy std (ddof=0, no eps) as its two passes (core.py:100-105):
+ * moments = (sum, sumsq, n) of the first pass (mrl_gae), cmoments = (sum, sumsq, n) of
+ * (adv - moments[0]/moments[2]) from mrl_moments_centered (both summed over ranks).
+ * cmoments may be NULL: single-pass E[x^2]-mean^2 (cancels when |mean| >> std). */
+int mrl_standardize(float* adv, int64_t n, const double* moments, const double* cmoments, void* stream);
 /* y = mixfrac * ret + (1 - mixfrac) * vpred  (NnRegression.fit target, core.py:622-624) */
 int mrl_vf_target(const float* ret, const float* vpred, double mixfrac, int64_t n, float* y, void* stream);
 /* out (fp64 [3]) <- (sum (a-b), sum (a-b)^2, n); b may be NULL.  For the VF stats
  * (PredStdev / TargStdev / explained variance, core.py:629-636, misc_utils.py:29-49) */
 int mrl_moments(const float* a, const float* b, int64_t n, double* out, void* workspace, void* stream);
+/* out (fp64 [3]) <- (sum d, sum d^2, n) of d = a - b - center[0]/center[2] (center: a
+ * device fp64 [3] from a previous mrl_moments / mrl_gae pass): the second pass of a
+ * two-pass variance, var = out[1]/n - (out[0]/n)^2, with no cancellation */
+int mrl_moments_centered(const float* a, const float* b, int64_t n, const double* center, double* out,
+                         void* workspace, void* stream);
 int64_t mrl_moments_workspace_bytes(int64_t n);
 /* episode statistics of the batch (add_episode_stats, core.py:31-44): out (fp64 [6]) <-
  * (n_episodes, sum R, sum R^2, max R, sum len, max len); an episode = a row run ending

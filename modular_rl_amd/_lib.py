@@ -93,9 +93,11 @@ SIGNATURES = {
     "mrl_gather_rows": (i32, [vp, vp, i64, i64, vp, vp]),
     "mrl_gae": (i32, [vp, vp, vp, i64, i64, f64, f64, vp, vp, vp, vp, vp]),
     "mrl_gae_workspace_bytes": (i64, [i64, i64]),
-    "mrl_standardize": (i32, [vp, i64, vp, vp]),
+    "mrl_standardize": (i32, [vp, i64, vp, vp, vp]),
     "mrl_vf_target": (i32, [vp, vp, f64, i64, vp, vp]),
     "mrl_moments": (i32, [vp, vp, i64, vp, vp, vp]),
+    "mrl_moments_centered": (i32, [vp, vp, i64, vp, vp, vp, vp]),
+    "mrl_probtype_rows": (i32, [i32, i32, i64, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_moments_workspace_bytes": (i64, [i64]),
     "mrl_episode_stats": (i32, [vp, vp, i64, i64, vp, vp, vp]),
     "mrl_episode_stats_workspace_bytes": (i64, [i64]),

@@ -11,7 +11,15 @@ state is a flat set of arrays -- nothing executable is ever stored or loaded:
   rng/iteration, rng/episodes       device Philox step base and per-env episode counters,
                                     so a resumed run draws exactly the noise the
                                     uninterrupted run would have drawn
+  updater/*                         the policy updater's own state (PPO: kl_coeff, the
+                                    Adam moments and step count) -- the reference keeps
+                                    it by pickling the whole agent
   meta (JSON)                       cfg, env id, iteration counter
+
+In the pipelined loop (core.IterationRunner) the callback for iteration k fires
+after iteration k+1 has already been issued; the runner therefore captures the state
+at the end of iteration k on the device (``agent._snapshot_capture``) and snapshots
+taken in that callback read the capture, not the live tensors.
 
 Snapshots are ``.npz`` files (``numpy.load(allow_pickle=False)`` reads them); the run
 log is HDF5 with the reference's layout when ``h5py`` is importable, else an ``.npz``
@@ -39,17 +47,33 @@ def _jsonable(cfg):
     return out
 
 
-def agent_state(agent, counter=0, env_id=None):
-    """Arrays (+ JSON meta) that restore ``agent`` to this point of training."""
-    st = {
-        "policy/theta": agent.policy.net.theta.detach().cpu().numpy().copy(),
-        "vf/theta": agent.baseline.net.theta.detach().cpu().numpy().copy(),
-    }
+def _host(v):
+    return v.detach().cpu().numpy().copy() if torch.is_tensor(v) else np.array(v, copy=True)
+
+
+def capture_state(agent, with_vf=True):
+    """Device-side copies (stream-ordered, no host sync) of everything agent_state
+    saves; the pipelined runner takes one at the end of each iteration."""
+    cap = {"policy/theta": agent.policy.net.theta.detach().clone()}
+    if with_vf:
+        cap["vf/theta"] = agent.baseline.net.theta.detach().clone()
     col = agent._filter_owner()
     if col is not None:
-        st["filter/state"] = col.filter_state[:col.FS].detach().cpu().numpy().copy()
-        st["rng/iteration"] = col.iteration.detach().cpu().numpy().copy()
-        st["rng/episodes"] = col.env_int[col.E:].detach().cpu().numpy().copy()
+        cap["filter/state"] = col.filter_state[:col.FS].detach().clone()
+        cap["rng/iteration"] = col.iteration.detach().clone()
+        cap["rng/episodes"] = col.env_int[col.E:].detach().clone()
+    upd = getattr(agent, "updater", None)
+    if upd is not None and hasattr(upd, "state_arrays"):
+        for k, v in upd.state_arrays().items():
+            cap["updater/" + k] = v.detach().clone() if torch.is_tensor(v) else np.array(v, copy=True)
+    return cap
+
+
+def agent_state(agent, counter=0, env_id=None):
+    """Arrays (+ JSON meta) that restore ``agent`` to this point of training: the
+    pipelined runner's capture of the iteration last reported, else the live state."""
+    cap = getattr(agent, "_snapshot_capture", None) or capture_state(agent)
+    st = {k: _host(v) for k, v in cap.items()}
     meta = dict(version=SNAPSHOT_VERSION, counter=int(counter), env_id=env_id, cfg=_jsonable(agent.cfg))
     return st, meta
 
@@ -79,6 +103,13 @@ def load_snapshot(path, agent):
         raise ValueError(f"{path}: parameter shapes do not match this agent's nets")
     pol.set_flat(st["policy/theta"])
     vf.set_flat(st["vf/theta"])
+    upd_state = {k[len("updater/"):]: v for k, v in st.items() if k.startswith("updater/")}
+    upd = getattr(agent, "updater", None)
+    if upd_state:
+        if upd is None or not hasattr(upd, "load_state_arrays"):
+            raise ValueError(f"{path}: snapshot holds updater state this agent's updater cannot take")
+        upd.load_state_arrays(upd_state)
+    agent._snapshot_capture = None
     agent._pending_state = {k: v for k, v in st.items() if k.startswith(("filter/", "rng/"))}
     col = agent._filter_owner()
     if col is not None:
@@ -99,8 +130,9 @@ def apply_collector_state(col, st):
         col.iteration.copy_(torch.as_tensor(st["rng/iteration"], dtype=torch.int64).to(col.iteration.device))
     if "rng/episodes" in st:
         ep = torch.as_tensor(st["rng/episodes"], dtype=torch.int32)
-        if ep.numel() == col.E:
-            col.env_int[col.E:].copy_(ep.to(col.env_int.device))
+        if ep.numel() != col.E:
+            raise ValueError(f"snapshot has episode counters for {ep.numel()} envs, this collector steps {col.E}")
+        col.env_int[col.E:].copy_(ep.to(col.env_int.device))
 
 
 class RunLog:

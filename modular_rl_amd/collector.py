@@ -25,7 +25,7 @@ import ctypes
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, timing
 from ._lib import call, ptr, stream
 from .dist import Comm
 
@@ -243,9 +243,13 @@ class Collector:
                 self.graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.graph):
                     self._launch_all()
+            timing.start("rollout_steps")
             self.graph.replay()
+            timing.stop("rollout_steps")
         else:
+            timing.start("rollout_steps")
             self._launch_all()
+            timing.stop("rollout_steps")
 
     def finish(self):
         """Cross-rank filter merge (waits for the rollout) and the iteration's Batch."""

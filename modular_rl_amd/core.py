@@ -25,6 +25,7 @@ from . import _lib, timing
 from ._lib import call, ptr, stream
 from .collector import Batch, Collector
 from .dist import Comm
+from .checkpoint import capture_state
 from .misc_utils import update_default_config
 from .vf import LbfgsOptimizer, NnRegression, NnVf  # noqa: F401  (reference names live in core)
 
@@ -66,10 +67,11 @@ class _GaeWorkspace:
         self.moments = None
 
     def get(self, T, E, device):
-        nbytes = int(_lib.load().mrl_gae_workspace_bytes(int(T), int(E)))
+        lib = _lib.load()
+        nbytes = max(int(lib.mrl_gae_workspace_bytes(int(T), int(E))), int(lib.mrl_moments_workspace_bytes(int(T * E))))
         if self.ws is None or self.ws.numel() < nbytes or self.ws.device != device:
-            self.ws = torch.zeros(nbytes, dtype=torch.uint8, device=device)  # zeroed arrival counter
-            self.moments = torch.zeros(3, dtype=torch.float64, device=device)
+            self.ws = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+            self.moments = torch.zeros(2, 3, dtype=torch.float64, device=device)  # first pass, centred pass
         return self.ws, self.moments
 
 
@@ -93,8 +95,11 @@ def compute_advantage_batch(vf, batch, gamma, lam, comm=None):
     call("mrl_gae", ptr(batch.rew), ptr(batch.vpred), ptr(batch.flags), int(batch.T), int(batch.E), float(gamma),
          float(lam), ptr(batch.adv), ptr(batch.ret), ptr(moments), ptr(ws), stream())
     timing.stop("gae_scan")
-    comm.allreduce_(moments)
-    call("mrl_standardize", ptr(batch.adv), int(n), ptr(moments), stream())
+    # numpy's two-pass std (core.py:100-105): global mean first, then the centred sums
+    comm.allreduce_(moments[0])
+    call("mrl_moments_centered", ptr(batch.adv), None, int(n), ptr(moments[0]), ptr(moments[1]), ptr(ws), stream())
+    comm.allreduce_(moments[1])
+    call("mrl_standardize", ptr(batch.adv), int(n), ptr(moments[0]), ptr(moments[1]), stream())
     return batch
 
 
@@ -269,28 +274,36 @@ class IterationRunner:
         pol_stats = agent.updater.update(batch)
         ev["upd1"] = self._event()
         if self.pipeline:
-            # read back with the deferred VF fit's stats (no host sync here)
-            self.pending = (batch, col.episode_stats_launch(batch), pol_stats)
+            # read back with the deferred VF fit's stats (no host sync here); the state at
+            # the end of this iteration (the VF after its fit is added then) is captured
+            # for snapshots taken in the callback that reports it
+            cap = capture_state(agent, with_vf=False)
+            self.pending = (batch, col.episode_stats_launch(batch), pol_stats, cap)
         else:
+            agent._snapshot_capture = None
             done = self._stats(col.episode_stats(batch), vf_stats, pol_stats)
         self.last_phase_events = ev
         return done
 
     def _fit_pending(self, fit_stream, ev):
-        batch, ep_dev, pol_stats = self.pending
+        batch, ep_dev, pol_stats, cap = self.pending
         self.pending = None
         main = torch.cuda.current_stream()
+        vf_net = self.agent.baseline.net
         if fit_stream is None:
             ev["vf0"] = self._event()
             vf_stats = self.agent.baseline.fit_batch(batch)
             ev["vf1"] = self._event()
+            cap["vf/theta"] = vf_net.theta.detach().clone()
         else:
             fit_stream.wait_stream(main)
             with torch.cuda.stream(fit_stream):
                 ev["vf0"] = self._event()
                 vf_stats = self.agent.baseline.fit_batch(batch)
                 ev["vf1"] = self._event()
+                cap["vf/theta"] = vf_net.theta.detach().clone()
             main.wait_stream(fit_stream)
+        self.agent._snapshot_capture = cap
         return self._stats(self.col.episode_stats_finish(ep_dev), vf_stats, pol_stats)
 
     def drain(self):

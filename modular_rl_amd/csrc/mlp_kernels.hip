@@ -507,6 +507,50 @@ __global__ void reduce_rows_narrow_kernel(const T* __restrict__ slab, int64_t ro
   if (threadIdx.x == 0) out[col] = (O)red[0];
 }
 
+// per-row probtype values on probability rows (mrl_probtype_rows): the helpers the
+// row epilogues use, one thread per row
+__global__ void probtype_rows_kernel(int head, int A, int64_t n, const float* __restrict__ prob,
+                                     const float* __restrict__ prob2, const void* __restrict__ x,
+                                     float* __restrict__ loglik, float* __restrict__ kl, float* __restrict__ ent) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    if (head == MRL_HEAD_SOFTMAX) {
+      const float* p = prob + r * A;
+      if (loglik) loglik[r] = logf(p[reinterpret_cast<const int32_t*>(x)[r]]);
+      if (kl) {
+        const float* q = prob2 + r * A;
+        float k = 0.f;
+        for (int j = 0; j < A; ++j) k += cat_kl_term(p[j], q[j]);
+        kl[r] = k;
+      }
+      if (ent) {
+        float h = 0.f;
+        for (int j = 0; j < A; ++j) h += cat_ent_term(p[j]);
+        ent[r] = h;
+      }
+    } else {
+      const float* p = prob + r * 2 * A;
+      float sumlog = 0.f;
+      for (int j = 0; j < A; ++j) sumlog += logf(p[A + j]);
+      if (loglik) {
+        const float* xv = reinterpret_cast<const float*>(x) + r * A;
+        float q = 0.f;
+        for (int j = 0; j < A; ++j) {
+          const float u = (xv[j] - p[j]) / p[A + j];
+          q += u * u;
+        }
+        loglik[r] = gauss_loglik(q, sumlog, A);
+      }
+      if (kl) {
+        const float* p2 = prob2 + r * 2 * A;
+        float k = 0.f;
+        for (int j = 0; j < A; ++j) k += gauss_kl_term(p[j], p[A + j], p2[j], p2[A + j]);
+        kl[r] = k - 0.5f * A;
+      }
+      if (ent) ent[r] = gauss_entropy(sumlog, A);
+    }
+  }
+}
+
 }  // namespace mrl
 
 using namespace mrl;
@@ -695,6 +739,17 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
     hipLaunchKernelGGL((mlp_vjp_kernel<false, true>), dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image,
                        skip);
   return hip_check(hipGetLastError(), "mrl_mlp_vjp");
+}
+
+int mrl_probtype_rows(int32_t head, int32_t k, int64_t n, const float* prob, const float* prob2, const void* x,
+                      float* loglik, float* kl, float* ent, void* stream) {
+  if (head != MRL_HEAD_SOFTMAX && head != MRL_HEAD_GAUSS) return fail(E_ARG, "mrl_probtype_rows: bad head kind");
+  if (k < 1) return fail(E_ARG, "mrl_probtype_rows: k < 1");
+  if (!prob || (loglik && !x) || (kl && !prob2)) return fail(E_ARG, "null pointer");
+  if (n <= 0) return OK;
+  hipLaunchKernelGGL(probtype_rows_kernel, dim3(std::min<int64_t>(ceil_div(n, 256), 2048)), dim3(256), 0, (hipStream_t)stream, (int)head, (int)k, n,
+                     prob, prob2, x, loglik, kl, ent);
+  return hip_check(hipGetLastError(), "mrl_probtype_rows");
 }
 
 int mrl_reduce_rows_f32(const float* slab, int64_t rows, int64_t cols, float* out, const int32_t* skip, void* stream) {

@@ -36,6 +36,23 @@ struct RowsArgs {
 constexpr float LOG2PI_F = 1.8378770664093453f;
 constexpr float LOG2PIE_F = 2.8378770664093453f;
 
+// Probtype math of one row, fp32 (the reference's floatX): the fused / layered row
+// epilogues below and mrl_probtype_rows (the per-row loglik / kl / entropy the
+// reference's validate_probtype checks, core.py:457-483) share these.
+// Categorical on probability rows: loglik core.py:349-353, kl 355-356, entropy 358-359
+__device__ __forceinline__ float cat_kl_term(float p0, float p1) { return p0 * logf(p0 / p1); }
+__device__ __forceinline__ float cat_ent_term(float p) { return -(p * logf(p)); }
+// DiagGauss on (mean, std[, log std]): loglik core.py:412-416, kl 421-426, entropy 428-430
+__device__ __forceinline__ float gauss_kl_term(float m0, float s0, float m1, float s1) {
+  const float dm = m0 - m1;
+  return logf(s1 / s0) + (s0 * s0 + dm * dm) / (2.f * s1 * s1);
+}
+// -0.5 sum u^2 - 0.5 d log 2pi - sum log std, from sum u^2 and sum log std
+__device__ __forceinline__ float gauss_loglik(float q, float sumlog, int A) {
+  return -0.5f * q - 0.5f * LOG2PI_F * A - sumlog;
+}
+__device__ __forceinline__ float gauss_entropy(float sumlog, int A) { return sumlog + 0.5f * LOG2PIE_F * A; }
+
 template <int EPI, int MA>
 __device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, const float (&z)[MA],
                                              const float (&dz)[MA], const float (&ls)[MA], const float (&sd)[MA],
@@ -73,8 +90,8 @@ __device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, con
       float pa = 0.f, opa = 0.f, kl = 0.f, ent = 0.f;
       for (int j = 0; j < A; ++j) {
         if (j == act) { pa = p[j]; opa = op[j]; }
-        kl += a.reverse_kl ? p[j] * logf(p[j] / op[j]) : op[j] * logf(op[j] / p[j]);
-        ent -= p[j] * logf(p[j]);
+        kl += a.reverse_kl ? cat_kl_term(p[j], op[j]) : cat_kl_term(op[j], p[j]);
+        ent += cat_ent_term(p[j]);
       }
       const float ratio = expf(logf(pa) - logf(opa));
       acc0 += (double)(ratio * advr);
@@ -102,17 +119,15 @@ __device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, con
         q0 += u0 * u0;
         sls += ls[j];
         sls0 += logf(s0);
-        const float dm = m0 - z[j];
-        kl += a.reverse_kl ? logf(s0 / sd[j]) + (sd[j] * sd[j] + dm * dm) / (2.f * s0 * s0)
-                           : logf(sd[j] / s0) + (s0 * s0 + dm * dm) / (2.f * sd[j] * sd[j]);
+        kl += a.reverse_kl ? gauss_kl_term(z[j], sd[j], m0, s0) : gauss_kl_term(m0, s0, z[j], sd[j]);
       }
       kl -= 0.5f * A;
-      const float logp = -0.5f * q - 0.5f * LOG2PI_F * A - sls;
-      const float oldlogp = -0.5f * q0 - 0.5f * LOG2PI_F * A - sls0;
+      const float logp = gauss_loglik(q, sls, A);
+      const float oldlogp = gauss_loglik(q0, sls0, A);
       const float ratio = expf(logp - oldlogp);
       acc0 += (double)(ratio * advr);
       acc1 += (double)kl;
-      acc2 += (double)(sls + 0.5f * LOG2PIE_F * A);
+      acc2 += (double)gauss_entropy(sls, A);
       if (EPI == MRL_EPI_SURRGRAD || EPI == MRL_EPI_PPOGRAD) {
         const float w = (float)(-a.inv_ng) * ratio * advr;
         for (int j = 0; j < A; ++j) {

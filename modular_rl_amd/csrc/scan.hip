@@ -211,10 +211,21 @@ __global__ void moments_final_kernel(const double* __restrict__ part, int64_t nb
   }
 }
 
-__global__ void standardize_kernel(float* __restrict__ adv, int64_t n, const double* __restrict__ mom) {
-  const double cnt = mom[2];
-  const double mean = mom[0] / cnt;
-  const double var = fmax(mom[1] / cnt - mean * mean, 0.0);
+// mom = (sum, sumsq, n) of the first pass; cmom = (sum, sumsq, n) of (adv - mom[0]/mom[2]),
+// the second pass of numpy's two-pass std (core.py:100-105): the centred sums do not
+// cancel when |mean| >> std.  Without cmom the single-pass form is used.
+__global__ void standardize_kernel(float* __restrict__ adv, int64_t n, const double* __restrict__ mom,
+                                   const double* __restrict__ cmom) {
+  const double mean0 = mom[0] / mom[2];
+  double mean, var;
+  if (cmom) {
+    const double d = cmom[0] / cmom[2];  // residual of the shift (rounding of mean0)
+    mean = mean0 + d;
+    var = fmax(cmom[1] / cmom[2] - d * d, 0.0);
+  } else {
+    mean = mean0;
+    var = fmax(mom[1] / mom[2] - mean * mean, 0.0);
+  }
   const double stdv = sqrt(var);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     adv[i] = (float)(((double)adv[i] - mean) / stdv);
@@ -545,13 +556,15 @@ __global__ void cast_scale_kernel(const float* __restrict__ a, double s, int64_t
 }
 
 // ------------------------------------------------------------------ moments / episode stats
-// per-block fp64 (sum, sumsq) of (a - b) -> part[block][2]
+// per-block fp64 (sum, sumsq) of (a - b - shift) -> part[block][2]; shift = center[0] /
+// center[2] (a previous pass's mean) or 0
 __global__ void moments_kernel(const float* __restrict__ a, const float* __restrict__ b, int64_t n,
-                               double* __restrict__ part) {
+                               const double* __restrict__ center, double* __restrict__ part) {
   __shared__ double red[2][256];
+  const double shift = center ? center[0] / center[2] : 0.0;
   double s1 = 0.0, s2 = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const double v = (double)a[i] - (b ? (double)b[i] : 0.0);
+    const double v = (double)a[i] - (b ? (double)b[i] : 0.0) - shift;
     s1 += v;
     s2 += v * v;
   }
@@ -758,10 +771,11 @@ int mrl_gae(const float* rew, const float* vpred, const uint8_t* flags, int64_t 
   return hip_check(hipGetLastError(), "mrl_gae");
 }
 
-int mrl_standardize(float* adv, int64_t n, const double* moments, void* stream) {
+int mrl_standardize(float* adv, int64_t n, const double* moments, const double* cmoments, void* stream) {
   if (!adv || !moments) return fail(E_ARG, "null pointer");
   if (n <= 0) return OK;
-  hipLaunchKernelGGL(standardize_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, adv, n, moments);
+  hipLaunchKernelGGL(standardize_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, adv, n, moments,
+                     cmoments);
   return hip_check(hipGetLastError(), "mrl_standardize");
 }
 
@@ -851,14 +865,20 @@ int mrl_gather_rows(const void* src, const int64_t* idx, int64_t n, int64_t row_
 
 int64_t mrl_moments_workspace_bytes(int64_t n) { return grid_for(n, 256, 1024) * 2 * (int64_t)sizeof(double); }
 
-int mrl_moments(const float* a, const float* b, int64_t n, double* out, void* workspace, void* stream) {
+int mrl_moments_centered(const float* a, const float* b, int64_t n, const double* center, double* out,
+                         void* workspace, void* stream) {
   if (!a || !out || !workspace) return fail(E_ARG, "null pointer");
+  if (n <= 0) return fail(E_ARG, "mrl_moments: empty input");
   const int64_t g = grid_for(n, 256, 1024);
   double* part = reinterpret_cast<double*>(workspace);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(moments_kernel, dim3(g), dim3(256), 0, s, a, b, n, part);
+  hipLaunchKernelGGL(moments_kernel, dim3(g), dim3(256), 0, s, a, b, n, center, part);
   hipLaunchKernelGGL(moments_final_kernel, dim3(1), dim3(256), 0, s, part, g, (double)n, out);
   return hip_check(hipGetLastError(), "mrl_moments");
+}
+
+int mrl_moments(const float* a, const float* b, int64_t n, double* out, void* workspace, void* stream) {
+  return mrl_moments_centered(a, b, n, nullptr, out, workspace, stream);
 }
 
 int64_t mrl_episode_stats_workspace_bytes(int64_t E) {

@@ -1,56 +1,64 @@
-"""Config / CLI plumbing and small utilities with the reference's names and meaning
-(`misc_utils.py:51-104,134-189`).  Host-side Python by nature (argparse), not
-compute."""
-from collections import defaultdict  # noqa: F401  (re-exported like the reference)
+"""Option-tuple config and CLI plumbing behind the reference's agent API.
 
-import numpy as np
-
-
-class dict2(dict):
-    """dictionary-like object that exposes its keys as attributes (`misc_utils.py:139-143`)."""
-
-    def __init__(self, **kwargs):
-        dict.__init__(self, kwargs)
-        self.__dict__ = self
+The reference configures everything through ``(name, type, default, help)`` tuples
+(``misc_utils.py:56-104``): agents merge user settings over the defaults and
+``run_pg.py`` turns the same tuples into ``--name`` flags.  Only the pieces the
+product imports live here: ``update_default_config``, ``update_argument_parser``,
+``comma_sep_ints``, ``IDENTITY`` and ``GENERAL_OPTIONS``.
+"""
 
 
-def update_default_config(tuples, usercfg):
-    """Defaults from (name, type, default, desc) tuples, overridden by usercfg (`misc_utils.py:56-74`)."""
-    out = dict2()
-    for (name, _, defval, _) in tuples:
-        out[name] = defval
-    if usercfg:
-        for (k, v) in usercfg.items():
-            if k in out:
-                out[k] = v
-    return out
+class Config(dict):
+    """A dict whose keys read as attributes too (``cfg["gamma"]`` == ``cfg.gamma``),
+    the behaviour of the reference's ``dict2`` (``misc_utils.py:139-143``)."""
+
+    def __getattr__(self, key):
+        try:
+            return self[key]
+        except KeyError as exc:
+            raise AttributeError(key) from exc
+
+    def __setattr__(self, key, value):
+        self[key] = value
 
 
-def update_argument_parser(parser, options, **kwargs):
-    """Add --name flags for option tuples (`misc_utils.py:76-85`)."""
-    kwargs = kwargs.copy()
-    for (name, typ, default, desc) in options:
-        flag = "--" + name
-        if flag in parser._option_string_actions.keys():  # pylint: disable=W0212
-            print("warning: already have option %s. skipping" % name)
-        else:
-            parser.add_argument(flag, type=typ, default=kwargs.pop(name, default), help=desc or " ")
-    if kwargs:
-        raise ValueError("options %s ignored" % kwargs)
+def update_default_config(option_tuples, usercfg):
+    """Defaults of ``option_tuples`` overridden by the user's values for KNOWN names;
+    unknown user keys are dropped (``misc_utils.py:56-74``)."""
+    cfg = Config((opt[0], opt[2]) for opt in option_tuples)
+    for key, value in (usercfg or {}).items():
+        if key in cfg:
+            cfg[key] = value
+    return cfg
 
 
-def comma_sep_ints(s):
-    """'64,64' -> [64, 64].  The reference returns a one-shot ``map`` under py3
-    (`misc_utils.py:87-91`); a list is the intended behaviour."""
-    if s:
-        return [int(v) for v in s.split(",")]
-    return []
+def update_argument_parser(parser, option_tuples, **overrides):
+    """Register ``--name`` for every option tuple; a flag already registered by an
+    earlier group is skipped with a warning, and an override naming no tuple is an
+    error (``misc_utils.py:76-85``)."""
+    pending = dict(overrides)
+    for name, typ, default, helptext in option_tuples:
+        flag = f"--{name}"
+        if flag in parser._option_string_actions:  # pylint: disable=protected-access
+            print(f"warning: already have option {name}. skipping")
+            continue
+        parser.add_argument(flag, type=typ, default=pending.pop(name, default), help=helptext or " ")
+    if pending:
+        raise ValueError(f"options {pending} ignored")
 
 
-def IDENTITY(x):
+def comma_sep_ints(text):
+    """``"64,64"`` -> ``[64, 64]``.  The reference returns a one-shot ``map`` under
+    py3 (``misc_utils.py:87-91``), which would leave the VF net
+    with no hidden layers; a list is the intended behaviour."""
+    return [int(tok) for tok in text.split(",")] if text else []
+
+
+def IDENTITY(x):  # noqa: N802  (the reference's name: agentzoo filters default to it)
     return x
 
 
+# run_pg.py's general flags (misc_utils.py:96-104)
 GENERAL_OPTIONS = [
     ("seed", int, 0, "random seed"),
     ("metadata", str, "", "metadata about experiment"),
@@ -60,53 +68,3 @@ GENERAL_OPTIONS = [
     ("load_snapshot", str, "", "path to snapshot"),
     ("video", int, 1, "whether to record video"),
 ]
-
-
-def zipsame(*seqs):
-    L = len(seqs[0])
-    assert all(len(seq) == L for seq in seqs[1:])
-    return zip(*seqs)
-
-
-def flatten(arrs):
-    return np.concatenate([np.asarray(arr).ravel() for arr in arrs])
-
-
-def unflatten(vec, shapes):
-    i = 0
-    arrs = []
-    for shape in shapes:
-        size = int(np.prod(shape))
-        arrs.append(vec[i:i + size].reshape(shape))
-        i += size
-    return arrs
-
-
-class EzPickle:
-    """Objects pickled via their constructor arguments (`misc_utils.py:163-189`)."""
-
-    def __init__(self, *args, **kwargs):
-        self._ezpickle_args = args
-        self._ezpickle_kwargs = kwargs
-
-    def __getstate__(self):
-        return {"_ezpickle_args": self._ezpickle_args, "_ezpickle_kwargs": self._ezpickle_kwargs}
-
-    def __setstate__(self, d):
-        out = type(self)(*d["_ezpickle_args"], **d["_ezpickle_kwargs"])
-        self.__dict__.update(out.__dict__)
-
-
-def fmt_row(width, row, header=False):
-    out = " | ".join(fmt_item(x, width) for x in row)
-    if header:
-        out = out + "\n" + "-" * len(out)
-    return out
-
-
-def fmt_item(x, l):
-    if isinstance(x, np.ndarray):
-        assert x.ndim == 0
-        x = x.item()
-    rep = "%g" % x if isinstance(x, float) else str(x)
-    return " " * (l - len(rep)) + rep

@@ -121,6 +121,10 @@ class MlpNet:
     def pack(self, theta=None, image=None, fwd_only=False, skip=None):
         theta = self.theta if theta is None else theta
         image = self.image if image is None else image
+        if image is self.image:
+            # the net's own weights change: a cached forward of the old ones is stale (raw
+            # device writes to theta, e.g. mrl_adam_step, do not bump theta._version)
+            self._cache_key = None
         call("mrl_mlp_pack", ctypes.byref(self.desc), ptr(theta), ptr(image), int(fwd_only), ptr(skip), stream())
 
     # ---- fused passes

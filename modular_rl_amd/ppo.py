@@ -84,6 +84,13 @@ class _PpoBase:
     def set_params_flat(self, th):
         self.stochpol.set_from_flat(th)
 
+    # updater state for checkpoints (the reference pickles the whole agent)
+    def state_arrays(self):
+        return {"kl_coeff": np.array([self.kl_coeff], dtype=np.float64)}
+
+    def load_state_arrays(self, st):
+        self.kl_coeff = float(np.asarray(st["kl_coeff"]).reshape(-1)[0])
+
     def __call__(self, paths):
         from .core import Batch
         batch = Batch.from_paths(paths, self.stochpol, device=self.stochpol.net.device)
@@ -179,6 +186,20 @@ class PpoSgdUpdater(_PpoBase):
         self.m = torch.zeros(net.P, dtype=torch.float32, device=net.device)
         self.v = torch.zeros(net.P, dtype=torch.float32, device=net.device)
         self.t = 0
+
+    def state_arrays(self):
+        st = super().state_arrays()
+        st.update(adam_m=self.m, adam_v=self.v, adam_t=np.array([self.t], dtype=np.int64))
+        return st
+
+    def load_state_arrays(self, st):
+        super().load_state_arrays(st)
+        for name, dst in (("adam_m", self.m), ("adam_v", self.v)):
+            src = torch.as_tensor(np.asarray(st[name]), dtype=torch.float32)
+            if src.numel() != dst.numel():
+                raise ValueError(f"snapshot {name} has {src.numel()} entries, the policy has {dst.numel()}")
+            dst.copy_(src.to(dst.device))
+        self.t = int(np.asarray(st["adam_t"]).reshape(-1)[0])
 
     def _a_t(self):
         """a_t = lr sqrt(1 - b2^t) / (1 - b1^t) in floatX (`ppo.py:240`)."""

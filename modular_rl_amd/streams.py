@@ -29,6 +29,7 @@ def destroy_all():
     if not _created:
         return
     torch.cuda.synchronize()
+    _by_cus.clear()
     while _created:
         call("mrl_stream_destroy", ctypes.c_void_p(_created.pop()))
 
@@ -36,9 +37,17 @@ def destroy_all():
 atexit.register(destroy_all)
 
 
+_by_cus = {}  # (device, CU ids) -> stream: one hardware-queue-backed stream per CU set per process
+
+
 def masked_stream(cus):
-    """A new HIP stream restricted to the CU ids in ``cus`` (torch.cuda.ExternalStream).
-    The stream lives until destroy_all() (at the latest, interpreter exit)."""
+    """The HIP stream restricted to the CU ids in ``cus`` (torch.cuda.ExternalStream),
+    created once per (device, CU set) and reused: every IterationRunner asks for the
+    same two sets, and the box gives a process few hardware queues.  The stream lives
+    until destroy_all() (at the latest, interpreter exit)."""
+    key = (torch.cuda.current_device(), tuple(sorted(cus)))
+    if key in _by_cus:
+        return _by_cus[key]
     _lib.load(require_gpu=True)
     n = cu_count()
     words = (n + 31) // 32
@@ -50,7 +59,8 @@ def masked_stream(cus):
     out = ctypes.c_void_p()
     call("mrl_stream_create_cu_mask", mask, words, ctypes.byref(out))
     _created.append(out.value)
-    return torch.cuda.ExternalStream(out.value)
+    _by_cus[key] = torch.cuda.ExternalStream(out.value)
+    return _by_cus[key]
 
 
 def stream_cus(s):

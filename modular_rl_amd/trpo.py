@@ -122,16 +122,19 @@ def _losses(sums, n_glob):
     return np.array([-s[0] / n_glob, s[1] / n_glob, s[2] / n_glob])
 
 
-def linesearch(f, fval, expected_improve_rate, max_backtracks=10, accept_ratio=.1):
+def linesearch(f, fval, expected_improve_rate, max_backtracks=10, accept_ratio=.1, trace=None):
     """Backtracking line search on the surrogate only (`trpo.py:143-159`).
     ``fval`` is the surrogate at x (the reference's ``f(x)``); ``f(stepfrac) ->
     (newfval, aux)`` evaluates the candidate x + stepfrac*fullstep on device.
+    ``trace`` (a list) receives (stepfrac, actual, expected, ratio) per backtrack.
     Returns (success, stepfrac or None, k, aux)."""
     for k, stepfrac in enumerate(.5 ** np.arange(max_backtracks)):
         newfval, aux = f(stepfrac)
         actual_improve = fval - newfval
         expected_improve = expected_improve_rate * stepfrac
         ratio = actual_improve / expected_improve
+        if trace is not None:
+            trace.append((stepfrac, actual_improve, expected_improve, ratio))
         if ratio > accept_ratio and actual_improve > 0:
             return True, stepfrac, k, aux
     return False, None, -1, None
@@ -204,7 +207,8 @@ class TrpoUpdater:
                 l = _losses(self._candidate_losses(thprev, stepfrac), n_glob)
                 return l[0], l
 
-            success, frac, k, laux = linesearch(f, fval, rate)
+            trace = []
+            success, frac, k, laux = linesearch(f, fval, rate, trace=trace)
             if success:
                 net.theta.copy_(ops.cand)  # the accepted (last evaluated) candidate
                 losses_after = laux
@@ -212,7 +216,8 @@ class TrpoUpdater:
                 net.theta.copy_(thprev)
             net.pack()
             diag.update(skipped=False, shs=shs, lm=lm, neggdotstepdir=neggdotstepdir, expected_rate=rate,
-                        success=success, k=k, stepfrac=frac, cg_iters=int(host[10]), rdotr=float(host[8]))
+                        success=success, k=k, stepfrac=frac, cg_iters=int(host[10]), rdotr=float(host[8]),
+                        ls=np.array(trace, dtype=np.float64))
         self.last_diag = diag
         out = OrderedDict()
         for (lname, lbefore, lafter) in zip(self.loss_names, losses_before, losses_after):

@@ -23,26 +23,26 @@ L2_COEF = 1e-3
 
 
 class DeviceMoments:
-    """(sum, sumsq, n) of (a - b) over rows, summed over ranks."""
+    """numpy std of (a - b) over all rows of all ranks, as numpy computes it: two
+    passes (the global mean, then the sums of the centred values), one host read."""
 
     def __init__(self, device, comm):
         self.device, self.comm = device, comm
-        self.out = torch.zeros(3, dtype=torch.float64, device=device)
+        self.out = torch.zeros(2, 3, dtype=torch.float64, device=device)
         self.ws = None
 
-    def __call__(self, a, b, n):
+    def std(self, a, b, n):
         nbytes = int(_lib.load().mrl_moments_workspace_bytes(int(n)))
         if self.ws is None or self.ws.numel() * 8 < nbytes:
             self.ws = torch.empty(nbytes // 8 + 1, dtype=torch.float64, device=self.device)
-        call("mrl_moments", ptr(a), ptr(b), int(n), ptr(self.out), ptr(self.ws), stream())
-        self.comm.allreduce_(self.out)
-        s, s2, c = (float(v) for v in self.out.cpu().numpy())
-        return s, s2, c
-
-    def std(self, a, b, n):
-        s, s2, c = self(a, b, n)
-        m = s / c
-        return float(np.sqrt(max(s2 / c - m * m, 0.0)))
+        call("mrl_moments", ptr(a), ptr(b), int(n), ptr(self.out[0]), ptr(self.ws), stream())
+        self.comm.allreduce_(self.out[0])
+        call("mrl_moments_centered", ptr(a), ptr(b), int(n), ptr(self.out[0]), ptr(self.out[1]), ptr(self.ws),
+             stream())
+        self.comm.allreduce_(self.out[1])
+        s, s2, c = (float(v) for v in self.out[1].cpu().numpy())
+        d = s / c
+        return float(np.sqrt(max(s2 / c - d * d, 0.0)))
 
 
 class LbfgsOptimizer:

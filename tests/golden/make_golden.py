@@ -51,8 +51,13 @@ def ref_pkg():
     return mods
 
 
-def extract(path, names, drop_lines=(), extra_ns=None):
-    """AST-extract top-level defs (or Class.method via 'Class.method') from a reference file."""
+def extract(path, names, drop_lines=(), extra_ns=None, record_after=None):
+    """AST-extract top-level defs (or Class.method via 'Class.method') from a reference file.
+
+    ``record_after`` maps a reference line number to a recorder statement (source
+    text of this script, not of the reference) appended after that statement, so a
+    fixture can keep the reference's own intermediate locals (e.g. shs / lm)."""
+    record_after = dict(record_after or {})
     src = open(path).read()
     tree = ast.parse(src)
 
@@ -65,6 +70,8 @@ def extract(path, names, drop_lines=(), extra_ns=None):
                         continue
                     strip(st)
                     kept.append(st)
+                    if st.lineno in record_after:
+                        kept.extend(ast.parse(record_after[st.lineno]).body)
                 if not kept and field == "body":
                     kept = [ast.Pass()]
                 setattr(node, field, kept)
@@ -159,23 +166,39 @@ def main():
     np.savez(os.path.join(HERE, "cg_linesearch.npz"), **out)
 
     # ---------------- TrpoUpdater.__call__ (trpo.py:72-140) on small policy batches
+    # Every input is fp32-representable (obs, actions, advantages, oldprob, theta0), so
+    # the fp32 device pipeline and the float64 reference see identical inputs.  The
+    # reference's own locals are recorded: after trpo.py:124 (g, stepdir, shs, lm,
+    # fullstep, the expected improve rate) and after trpo.py:154 in linesearch (each
+    # backtrack's actual / expected improvement and ratio), so the fixture pins the
+    # chosen step size and the accepted backtrack k.
     out = {}
+    rec = {}
     ns_tr = extract(tr, ["cg", "linesearch", "TrpoUpdater.__call__"],
                     drop_lines={82, 84, 98, 100, 131, 132},
                     extra_ns={"np": np, "OrderedDict": OrderedDict, "concat": np.concatenate,
-                              "zipsame": mu.zipsame})
+                              "zipsame": mu.zipsame, "_rec": rec},
+                    record_after={124: "_rec.update(g=g, stepdir=stepdir, shs=shs, lm=lm, fullstep=fullstep, "
+                                       "rate=neggdotstepdir / lm)",
+                                  154: "_rec.setdefault('ls', []).append((stepfrac, actual_improve, "
+                                       "expected_improve, ratio))"})
     call = ns_tr["__call__"]
+    f32 = (lambda a: np.asarray(a, dtype=np.float32).astype(np.float64))
     for tag, (nin, nout, head, N) in {"gauss": (11, 3, "gauss", 512), "cat": (4, 2, "softmax", 400)}.items():
         spec = trpo_np.Spec(nin, [64, 64], nout, head)
         th0 = trpo_np.mlp_init(rng, spec.shapes, head == "gauss")
-        th0 = th0 + 0.02 * rng.standard_normal(th0.shape)
-        ob = rng.standard_normal((N, nin))
+        th0 = f32(th0 + 0.02 * rng.standard_normal(th0.shape))
+        ob = f32(rng.standard_normal((N, nin)))
         oldth = th0 + 0.01 * rng.standard_normal(th0.shape)
-        oldprob = trpo_np.policy_prob(spec, oldth, ob)
+        oldprob = f32(trpo_np.policy_prob(spec, oldth, ob))
         noise = rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N)
         act = trpo_np.sample(spec, oldprob, noise)
-        adv = trpo_np.standardize(rng.standard_normal(N) + 0.3 * ob[:, 0])
-        for cfg_i, cfg in enumerate([dict(cg_damping=1e-3, max_kl=1e-2), dict(cg_damping=0.1, max_kl=0.01)]):
+        act = f32(act) if head == "gauss" else act
+        adv = f32(trpo_np.standardize(rng.standard_normal(N) + 0.3 * ob[:, 0]))
+        # cfg 0: the reference default (rank-deficient for cat: P=4,610 > N=400 rows);
+        # cfg 1: the battery settings; cfg 2: a trust region so large the line search backtracks
+        for cfg_i, cfg in enumerate([dict(cg_damping=1e-3, max_kl=1e-2), dict(cg_damping=0.1, max_kl=0.01),
+                                     dict(cg_damping=0.1, max_kl=100.0)]):
             state = {"th": th0.copy()}
             self = types.SimpleNamespace(
                 cfg=cfg, loss_names=["surr", "kl", "ent"],
@@ -187,12 +210,21 @@ def main():
             )
             paths = [dict(prob=oldprob[:N // 2], observation=ob[:N // 2], action=act[:N // 2], advantage=adv[:N // 2]),
                      dict(prob=oldprob[N // 2:], observation=ob[N // 2:], action=act[N // 2:], advantage=adv[N // 2:])]
+            rec.clear()
             stats = quiet(call, self, paths)
             k = f"{tag}{cfg_i}"
             out[f"{k}_theta0"], out[f"{k}_theta1"] = th0, state["th"]
             out[f"{k}_ob"], out[f"{k}_act"], out[f"{k}_adv"], out[f"{k}_oldprob"] = ob, act, adv, oldprob
             out[f"{k}_cfg"] = np.array([cfg["cg_damping"], cfg["max_kl"]])
             out[f"{k}_stats"] = np.array([stats[n] for n in ("surr_before", "surr_after", "kl_before", "kl_after", "ent_before", "ent_after")])
+            ls = np.array(rec["ls"], dtype=np.float64)  # rows: (stepfrac, actual, expected, ratio)
+            accepted = [i for i, (_, act_i, _, r) in enumerate(ls) if r > 0.1 and act_i > 0]
+            out[f"{k}_g"], out[f"{k}_stepdir"], out[f"{k}_fullstep"] = rec["g"], rec["stepdir"], rec["fullstep"]
+            out[f"{k}_shs"], out[f"{k}_lm"], out[f"{k}_rate"] = np.float64(rec["shs"]), np.float64(rec["lm"]), np.float64(rec["rate"])
+            out[f"{k}_ls"] = ls
+            out[f"{k}_k"] = np.int64(accepted[0] if accepted else -1)
+            # distance of the accept test from its threshold at the accepted backtrack
+            out[f"{k}_margin"] = np.float64(ls[accepted[0], 3] - 0.1 if accepted else np.nan)
     np.savez(os.path.join(HERE, "trpo_update.npz"), **out)
 
     # ---------------- compute_advantage (core.py:63-105, TF check 79-96 dropped)
@@ -200,21 +232,30 @@ def main():
     cr = os.path.join(REF, "core.py")
     ns_c = extract(cr, ["compute_advantage", "add_episode_stats", "pathlength"],
                    drop_lines=set(range(79, 97)), extra_ns={"np": np, "discount": mu.discount})
+    # set p: five paths (terminated and not) at gamma 0.995, lam 0.97;
+    # set q: the same lengths with |mean adv| >> std (rewards around 300, lam 0 so the
+    # advantage is the TD residual): an untrained value function's regime, where a
+    # single-pass E[x^2]-mean^2 standardisation would cancel (core.py:100-105 is numpy's
+    # two-pass std).  Rewards and baselines are fp32-representable.
+    f32 = (lambda a: np.asarray(a, dtype=np.float32).astype(np.float64))
     lens = [5, 17, 1, 30, 12]
-    paths = []
-    for i, L in enumerate(lens):
-        paths.append(dict(reward=rng.standard_normal(L) + 1, action=np.zeros(L), terminated=(i % 2 == 0),
-                          _b=rng.standard_normal(L)))
-    vf = types.SimpleNamespace(predict=lambda path: path["_b"])
-    quiet(ns_c["compute_advantage"], vf, paths, 0.995, 0.97)
-    for i, p in enumerate(paths):
-        out[f"p{i}_reward"], out[f"p{i}_b"], out[f"p{i}_term"] = p["reward"], p["_b"], np.bool_(p["terminated"])
-        out[f"p{i}_adv"], out[f"p{i}_ret"] = p["advantage"], p["return"]
-    stats = OrderedDict()
-    ns_c["add_episode_stats"](stats, paths)
-    out["stats_keys"] = np.array(list(k for k, v in stats.items() if np.ndim(v) == 0))
-    out["stats_vals"] = np.array([v for v in stats.values() if np.ndim(v) == 0], dtype=np.float64)
-    out["n_paths"] = len(paths)
+    for pre, (gam, lam, r0, rs) in {"p": (0.995, 0.97, 1.0, 1.0), "q": (0.995, 0.0, 300.0, 1.0)}.items():
+        paths = []
+        for i, L in enumerate(lens):
+            paths.append(dict(reward=f32(rng.standard_normal(L) * rs + r0), action=np.zeros(L), terminated=(i % 2 == 0),
+                              _b=f32(rng.standard_normal(L))))
+        vf = types.SimpleNamespace(predict=lambda path: path["_b"])
+        quiet(ns_c["compute_advantage"], vf, paths, gam, lam)
+        out[f"{pre}_gamma_lam"] = np.array([gam, lam])
+        for i, p in enumerate(paths):
+            out[f"{pre}{i}_reward"], out[f"{pre}{i}_b"], out[f"{pre}{i}_term"] = p["reward"], p["_b"], np.bool_(p["terminated"])
+            out[f"{pre}{i}_adv"], out[f"{pre}{i}_ret"] = p["advantage"], p["return"]
+        if pre == "p":
+            stats = OrderedDict()
+            ns_c["add_episode_stats"](stats, paths)
+            out["stats_keys"] = np.array(list(k for k, v in stats.items() if np.ndim(v) == 0))
+            out["stats_vals"] = np.array([v for v in stats.values() if np.ndim(v) == 0], dtype=np.float64)
+    out["n_paths"] = len(lens)
     np.savez(os.path.join(HERE, "compute_advantage.npz"), **out)
     print("golden fixtures written to", HERE)
 

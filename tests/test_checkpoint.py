@@ -88,30 +88,80 @@ def test_run_log_npz_layout(tmp_path):
 
 
 @pytest.mark.gpu
-def test_resume_continues_bit_identically(tmp_path):
-    from modular_rl_amd.agentzoo import TrpoAgent
+@pytest.mark.parametrize("agent_name,pipeline", [("TrpoAgent", 1), ("TrpoAgent", 0), ("PpoLbfgsAgent", 1),
+                                                 ("PpoSgdAgent", 1)])
+def test_resume_continues_bit_identically(tmp_path, agent_name, pipeline):
+    """A snapshot taken INSIDE the iteration-2 callback (as run_pg.py takes them) and
+    resumed for one iteration ends bit-identical to the uninterrupted 3-iteration run:
+    parameters, VF, the updater's state (PPO kl_coeff / Adam moments) and the stats.
+    With pipeline=1 the callback fires after iteration 3 is already issued, so this
+    checks the runner's end-of-iteration capture."""
+    from modular_rl_amd import agentzoo
     from modular_rl_amd.core import run_policy_gradient_algorithm
     from modular_rl_amd.envs import make
     env = make("Hopper-v2")
     cfg = dict(n_envs=64, horizon=64, timestep_limit=1000, gamma=0.995, lam=0.97, max_kl=0.01, cg_damping=0.1,
-               timesteps_per_batch=64 * 64, use_graph=1, seed=3)
+               timesteps_per_batch=64 * 64, use_graph=1, seed=3, pipeline=pipeline, epochs=2, kl_target=0.003)
+    Agent = getattr(agentzoo, agent_name)
+    path = str(tmp_path / "snap.npz")
 
-    def run(agent, n):
+    def run(agent, n, snap_at=None):
         seen = []
-        c = dict(cfg, n_iter=n)
-        run_policy_gradient_algorithm(env, agent, callback=lambda st: seen.append(dict(st)), usercfg=c)
+
+        def cb(st):
+            seen.append(dict(st))
+            if len(seen) == snap_at:
+                save_snapshot(path, agent, counter=snap_at, env_id="Hopper-v2")
+        run_policy_gradient_algorithm(env, agent, callback=cb, usercfg=dict(cfg, n_iter=n))
         return seen
 
-    full = TrpoAgent(env.observation_space, env.action_space, cfg)
-    st_full = run(full, 3)
-    first = TrpoAgent(env.observation_space, env.action_space, cfg)
-    run(first, 2)
-    path = save_snapshot(str(tmp_path / "snap.npz"), first, counter=2, env_id="Hopper-v2")
-    resumed = TrpoAgent(env.observation_space, env.action_space, cfg)
-    load_snapshot(path, resumed)
+    full = Agent(env.observation_space, env.action_space, cfg)
+    st_full = run(full, 3, snap_at=2)
+    resumed = Agent(env.observation_space, env.action_space, cfg)
+    meta = load_snapshot(path, resumed)
+    assert meta["counter"] == 2
     st_res = run(resumed, 1)
     assert np.array_equal(resumed.policy.get_flat(), full.policy.get_flat())
     assert np.array_equal(resumed.baseline.net.get_flat(), full.baseline.net.get_flat())
+    if hasattr(full.updater, "state_arrays"):
+        for k, v in full.updater.state_arrays().items():
+            w = resumed.updater.state_arrays()[k]
+            a = v.cpu().numpy() if torch.is_tensor(v) else v
+            b = w.cpu().numpy() if torch.is_tensor(w) else w
+            assert np.array_equal(a, b), k
     for k in ("EpRewMean", "pol_surr_after", "pol_kl_after", "vf_EVBefore"):
         if k in st_full[-1]:
             assert st_res[0][k] == st_full[-1][k], k
+
+
+def test_updater_state_roundtrip(tmp_path):
+    """PPO updater state (kl_coeff, Adam m / v / t) is saved and restored as arrays."""
+    class _Upd:
+        def __init__(self, seed):
+            rng = np.random.default_rng(seed)
+            self.kl_coeff = float(rng.random())
+            self.m = torch.as_tensor(rng.standard_normal(37), dtype=torch.float32)
+            self.t = int(rng.integers(1, 100))
+
+        def state_arrays(self):
+            return {"kl_coeff": np.array([self.kl_coeff]), "adam_m": self.m, "adam_t": np.array([self.t])}
+
+        def load_state_arrays(self, st):
+            self.kl_coeff = float(st["kl_coeff"][0])
+            self.m.copy_(torch.as_tensor(st["adam_m"]))
+            self.t = int(st["adam_t"][0])
+
+    a, b = _Agent(11), _Agent(12)
+    a.updater, b.updater = _Upd(1), _Upd(2)
+    load_snapshot(save_snapshot(str(tmp_path / "u.npz"), a), b)
+    assert b.updater.kl_coeff == a.updater.kl_coeff and b.updater.t == a.updater.t
+    assert torch.equal(b.updater.m, a.updater.m)
+
+
+def test_episode_counters_of_another_env_count_are_refused(tmp_path):
+    a = _Agent(13)
+    path = save_snapshot(str(tmp_path / "e.npz"), a)
+    b = _Agent(14, with_col=False)
+    load_snapshot(path, b)
+    with pytest.raises(ValueError):
+        apply_collector_state(_Col(16, 14, 0), b._pending_state)

@@ -113,10 +113,25 @@ def test_rollout_graph_replay_equals_eager():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("tag", ["gauss1", "cat1", "gauss0"])
+STAT_KEYS = ("surr_before", "surr_after", "kl_before", "kl_after", "ent_before", "ent_after")
+
+
+@pytest.mark.parametrize("tag", ["gauss0", "gauss1", "gauss2", "cat0", "cat1", "cat2"])
 def test_trpo_update_matches_reference_golden(tag):
-    """Device TrpoUpdater on the batch of tests/golden/trpo_update.npz (produced by the
-    reference's own TrpoUpdater.__call__ control flow)."""
+    """Device TrpoUpdater on the batch of tests/golden/trpo_update.npz, produced by the
+    reference's own TrpoUpdater.__call__ / cg / linesearch (trpo.py:72-200, float64) on
+    fp32-representable inputs, so both sides see identical inputs.  Held to north_star's
+    1e-4 relative: theta (relative to the step), the six loss stats, shs, lm, the expected
+    improve rate and every backtrack's ratio; the accepted backtrack k exactly (every
+    fixture's accept test clears its 0.1 threshold by >= 0.05, gauss2 / cat2 backtrack).
+
+    cat0 (the reference default cg_damping 1e-3 on 400 CartPole rows, P = 4,610) is
+    rank-deficient: cond(F + 1e-3 I) ~ 1e3 and CG stops after 10 of thousands of
+    needed iterations, so fp32 rounding moves the unconverged step direction far more
+    than 1e-4 (the float32 oracle lands 4.4e-2 of the step away from the float64
+    reference).  For cat0 only the step-independent stats are held to 1e-4; k must
+    still agree (margin 0.22 > 1e-3) and the step-dependent values are
+    checked to 1e-1."""
     from modular_rl_amd.collector import Batch
     from modular_rl_amd.trpo import TrpoUpdater
     d = np.load(os.path.join(G, "trpo_update.npz"))
@@ -124,6 +139,7 @@ def test_trpo_update_matches_reference_golden(tag):
     nin, nout = (11, 3) if head == "gauss" else (4, 2)
     _, _, pol = _policy(head, nin, nout, seed=0)
     th0 = d[f"{tag}_theta0"]
+    assert np.array_equal(th0.astype(np.float32).astype(np.float64), th0)  # fp32-representable input
     pol.net.set_flat(th0)
     damping, max_kl = d[f"{tag}_cfg"]
     up = TrpoUpdater(pol, dict(cg_damping=damping, max_kl=max_kl))
@@ -133,15 +149,58 @@ def test_trpo_update_matches_reference_golden(tag):
               _dev(d[f"{tag}_oldprob"]))
     b.adv = _dev(d[f"{tag}_adv"])
     stats = up.update(b)
+    dg = up.last_diag
+    tol = 1e-1 if tag == "cat0" else 1e-4
+    assert dg["success"] and dg["k"] == int(d[f"{tag}_k"]), (dg["k"], int(d[f"{tag}_k"]))
     th1 = pol.get_flat().astype(np.float64)
     want = d[f"{tag}_theta1"]
     step = np.abs(want - th0).max()
-    # fp32 device pipeline vs float64 reference: relative to the step it took
-    assert np.abs(th1 - want).max() <= 2e-3 * step, (np.abs(th1 - want).max(), step)
-    got = np.array([stats[k] for k in ("surr_before", "surr_after", "kl_before", "kl_after", "ent_before", "ent_after")])
+    assert np.abs(th1 - want).max() <= tol * step, (np.abs(th1 - want).max() / step)
+    np.testing.assert_allclose([dg["shs"], dg["lm"], dg["expected_rate"]],
+                               [d[f"{tag}_shs"], d[f"{tag}_lm"], d[f"{tag}_rate"]], rtol=tol)
+    ls = d[f"{tag}_ls"]
+    assert dg["ls"].shape == ls.shape
+    # ratio = actual / expected improvement: actual is a difference of two surrogate
+    # values, so its error is relative to |surr| ~ the expected improvement scale
+    np.testing.assert_allclose(dg["ls"][:, 3], ls[:, 3], rtol=tol, atol=tol * np.abs(ls[:, 3]).max())
+    got = np.array([stats[k] for k in STAT_KEYS])
     ref = d[f"{tag}_stats"]
-    np.testing.assert_allclose(got, ref, rtol=2e-3, atol=1e-6)
-    assert up.last_diag["success"]
+    before = [0, 2, 4]
+    np.testing.assert_allclose(got[before], ref[before], rtol=1e-4, atol=1e-9)
+    np.testing.assert_allclose(got, ref, rtol=tol, atol=1e-9)
+
+
+@pytest.mark.parametrize("pre", ["p", "q"])
+def test_compute_advantage_matches_reference_golden(pre):
+    """compute_advantage (core.py:63-105) on the reference-generated paths of
+    tests/golden/compute_advantage.npz, laid out as one env's rows (the paths back to
+    back, ends flagged): returns and standardised advantages within 1e-4.  Set q has
+    |mean adv| ~ 230 std (two-pass std on the device, like numpy's); the fp32 storage of
+    the unstandardised advantage bounds that error at 2^-24 * |mean| / std ~ 2e-5."""
+    from modular_rl_amd import core
+    from modular_rl_amd.collector import Batch
+    d = np.load(os.path.join(G, "compute_advantage.npz"))
+    n = int(d["n_paths"])
+    gam, lam = (float(x) for x in d[f"{pre}_gamma_lam"])
+    rew = np.concatenate([d[f"{pre}{i}_reward"] for i in range(n)])
+    base = np.concatenate([d[f"{pre}{i}_b"] for i in range(n)])
+    flags = np.concatenate([np.r_[np.zeros(len(d[f"{pre}{i}_reward"]) - 1, np.uint8),
+                                  np.uint8(1 | (2 * bool(d[f"{pre}{i}_term"])))] for i in range(n)])
+    want_adv = np.concatenate([d[f"{pre}{i}_adv"] for i in range(n)])
+    want_ret = np.concatenate([d[f"{pre}{i}_ret"] for i in range(n)])
+    if pre == "q":  # the regime the case exists for: raw TD residuals with |mean| >> std
+        raw = rew - base
+        assert abs(raw.mean()) > 100 * raw.std()
+    Tn = len(rew)
+
+    class VF:  # the fixture's baseline predictions
+        def predict_batch(self, batch, out=None):
+            return _dev(base)
+
+    b = Batch(Tn, _dev(np.zeros((Tn, 1))), None, None, _dev(rew), _dev(flags, torch.uint8), None, T=Tn, E=1)
+    core.compute_advantage_batch(VF(), b, gam, lam)
+    np.testing.assert_allclose(b.ret.cpu().numpy(), want_ret, rtol=1e-4, atol=1e-4 * np.abs(want_ret).max())
+    np.testing.assert_allclose(b.adv.cpu().numpy(), want_adv, rtol=1e-4, atol=1e-4)
 
 
 def test_trpo_update_matches_oracle_fp32_tolerance():
