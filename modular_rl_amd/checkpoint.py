@@ -11,6 +11,8 @@ state is a flat set of arrays -- nothing executable is ever stored or loaded:
   rng/iteration, rng/episodes       device Philox step base and per-env episode counters,
                                     so a resumed run draws exactly the noise the
                                     uninterrupted run would have drawn
+  rng/np_mt19937, rng/np_pos_gauss  numpy's global MT19937 state (PpoSgd's minibatch
+                                    permutations)
   updater/*                         the policy updater's own state (PPO: kl_coeff, the
                                     Adam moments and step count) -- the reference keeps
                                     it by pickling the whole agent
@@ -62,6 +64,11 @@ def capture_state(agent, with_vf=True):
         cap["filter/state"] = col.filter_state[:col.FS].detach().clone()
         cap["rng/iteration"] = col.iteration.detach().clone()
         cap["rng/episodes"] = col.env_int[col.E:].detach().clone()
+    # numpy's global MT19937 (PpoSgd draws its minibatch permutations from it, as the
+    # reference does): saved as arrays so a resumed run permutes identically
+    name, keys, pos, has_gauss, gauss = np.random.get_state()
+    cap["rng/np_mt19937"] = np.array(keys, dtype=np.uint32)
+    cap["rng/np_pos_gauss"] = np.array([pos, has_gauss, gauss], dtype=np.float64)
     upd = getattr(agent, "updater", None)
     if upd is not None and hasattr(upd, "state_arrays"):
         for k, v in upd.state_arrays().items():
@@ -109,8 +116,12 @@ def load_snapshot(path, agent):
         if upd is None or not hasattr(upd, "load_state_arrays"):
             raise ValueError(f"{path}: snapshot holds updater state this agent's updater cannot take")
         upd.load_state_arrays(upd_state)
+    if "rng/np_mt19937" in st:
+        pos, has_gauss, gauss = st["rng/np_pos_gauss"]
+        np.random.set_state(("MT19937", st["rng/np_mt19937"].astype(np.uint32), int(pos), int(has_gauss), float(gauss)))
     agent._snapshot_capture = None
-    agent._pending_state = {k: v for k, v in st.items() if k.startswith(("filter/", "rng/"))}
+    agent._pending_state = {k: v for k, v in st.items() if k.startswith(("filter/", "rng/"))
+                            and not k.startswith("rng/np_")}
     col = agent._filter_owner()
     if col is not None:
         apply_collector_state(col, agent._pending_state)
