@@ -310,6 +310,17 @@ int mrl_rollout_pack(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const f
 /* one lock-step env step t (0 <= t < horizon) for all envs; rimage from mrl_rollout_pack */
 int mrl_rollout_step(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta,
                      const float* rimage, const mrl_rollout_bufs* b, int32_t t, void* stream);
+/* The whole horizon of the fused path in one call: reset + steps 0..T-1 (then
+ * mrl_rollout_finish).  persistent != 0: ONE cooperative launch whose blocks stay
+ * resident and loop over the steps, handing the per-step running-stat partials to each
+ * other as step-tagged granules in sync (device workspace of mrl_rollout_sync_bytes(d)
+ * bytes, zeroed by this call; the u32 sync[32] != 0 afterwards means the grid could not
+ * run resident and gave up).  Falls back to mrl_rollout_reset + T x mrl_rollout_step
+ * (identical results) when persistent == 0, sync is NULL, or the stream's CUs are fewer
+ * than the blocks. */
+int64_t mrl_rollout_sync_bytes(const mrl_rollout_desc* d);
+int mrl_rollout_run(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta, const float* rimage,
+                    const mrl_rollout_bufs* b, uint32_t* sync, int32_t persistent, void* stream);
 /* Layered-policy rollout (any policy net; required for Humanoid): step t is
  *   mrl_rollout_obs(t)            filter merge + normalised obs rows of step t -> b->obs
  *   <policy forward over the E rows of step t, e.g. LayeredMlpNet GEMMs> -> z [E, n_out]

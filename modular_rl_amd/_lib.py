@@ -111,6 +111,8 @@ SIGNATURES = {
     "mrl_rollout_image_floats": (i64, [vp]),
     "mrl_rollout_pack": (i32, [vp, vp, vp, vp, vp]),
     "mrl_rollout_step": (i32, [vp, vp, vp, vp, vp, i32, vp]),
+    "mrl_rollout_sync_bytes": (i64, [vp]),
+    "mrl_rollout_run": (i32, [vp, vp, vp, vp, vp, vp, i32, vp]),
     "mrl_rollout_finish": (i32, [vp, vp, vp]),
     "mrl_rollout_reset_rows": (i32, [vp, vp, vp]),
     "mrl_rollout_obs": (i32, [vp, vp, i32, vp]),

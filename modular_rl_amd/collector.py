@@ -21,6 +21,7 @@ iteration (rank order), so ranks normalise with identical statistics at every
 iteration start.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -177,6 +178,10 @@ class Collector:
             # fused step kernel: its own policy image, repacked from theta at every collect
             n = int(lib.mrl_rollout_image_floats(ctypes.byref(net.desc)))
             self._rimage = torch.zeros(n, dtype=torch.float32, device=self.dev)
+            nsync = int(lib.mrl_rollout_sync_bytes(ctypes.byref(self.desc)))
+            self._sync = torch.zeros((nsync + 3) // 4, dtype=torch.int32, device=self.dev)
+        # the whole horizon as one persistent launch (MRL_ROLLOUT_PERSISTENT=0: step launches)
+        self.persistent = os.environ.get("MRL_ROLLOUT_PERSISTENT", "1") != "0"
         self.use_graph = use_graph
         self.graph = None
         self._ep_ws = torch.zeros(int(lib.mrl_episode_stats_workspace_bytes(self.E)) // 8 + 1, **f64)
@@ -204,10 +209,10 @@ class Collector:
             return self._launch_all_layered(bufs, net)
         call("mrl_rollout_pack", ctypes.byref(self.desc), ctypes.byref(net.desc), ptr(net.theta), ptr(self._rimage),
              stream())
-        call("mrl_rollout_reset", ctypes.byref(self.desc), ctypes.byref(bufs), stream())
-        for t in range(self.T):
-            call("mrl_rollout_step", ctypes.byref(self.desc), ctypes.byref(net.desc), ptr(net.theta),
-                 ptr(self._rimage), ctypes.byref(bufs), int(t), stream())
+        # reset + T steps: one persistent cooperative launch (or T step launches when
+        # persistent is off / the stream has too few CUs; identical results)
+        call("mrl_rollout_run", ctypes.byref(self.desc), ctypes.byref(net.desc), ptr(net.theta), ptr(self._rimage),
+             ctypes.byref(bufs), ptr(self._sync), int(self.persistent), stream())
         call("mrl_rollout_finish", ctypes.byref(self.desc), ctypes.byref(bufs), stream())
 
     def _launch_all_layered(self, bufs, net):
@@ -250,6 +255,13 @@ class Collector:
             timing.start("rollout_steps")
             self._launch_all()
             timing.stop("rollout_steps")
+
+    def check(self):
+        """Raise if a persistent rollout launch gave up waiting for its blocks (the grid
+        was not resident at once); synchronises on the rollout."""
+        if not self.layered and int(self._sync[32].item()) != 0:
+            raise _lib.MrlError("persistent rollout: blocks never all arrived (grid not resident); "
+                                "run with MRL_ROLLOUT_PERSISTENT=0")
 
     def finish(self):
         """Cross-rank filter merge (waits for the rollout) and the iteration's Batch."""

@@ -660,6 +660,289 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, const floa
 #undef STAMP
 }
 
+// ------------------------------------------------------------------ persistent rollout
+// The whole horizon in ONE launch (mrl_rollout_run): the nb blocks of the step kernel
+// stay resident (cooperative launch) and loop over t.  Weights, env state, episode
+// counters and the running stat live in registers for all T steps; the only cross-block
+// dependency of a step -- the Welford partials of the E raw observations (and rewards)
+// that every block merges into its copy of the running stat -- is handed off in memory
+// as data-tagged granules: each (block, column) partial is two 16-B {fp64 value, u64
+// step tag} records written by single write-through (sc1) stores; a consumer polls the
+// granules themselves with sc1 loads until every tag carries the step it waits for, so
+// one memory round trip both signals and delivers (MI355X_MICROARCH.md, hand-offs:
+// untorn 16-B sc1 granules).  Counts are not sent: every block knows each block's
+// number of envs.  Two parities as between step launches: block b can only overwrite a
+// parity-p granule at step t+2 after every block's step-t+1 granules arrived, i.e.
+// after every block has read parity p at step t.  Bit-identical to the step kernels.
+constexpr int SYNC_ABORT = 32;             // u32 word: a block gave up waiting (own 128-B line)
+constexpr int64_t SYNC_HEAD_BYTES = 256;   // then the granules: [2 parities][D][nb][2] x 16 B
+constexpr uint32_t SPIN_LIMIT = 1u << 22;  // polls (~seconds): a non-resident grid exits
+
+typedef uint32_t gran_t __attribute__((ext_vector_type(4)));  // one 16-B granule
+
+struct Granules {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int nb, D;
+  __device__ Granules(uint32_t* sync, int nb_, int D_) : nb(nb_), D(D_) {
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(sync) + SYNC_HEAD_BYTES, 0,
+                                             2 * D_ * nb_ * 32, 0x00020000);
+  }
+  __device__ uint32_t off(int parity, int k, int b, int which) const {
+    return (uint32_t)((((parity * D + k) * nb + b) * 2 + which) * 16);
+  }
+  __device__ void put(int parity, int k, int b, int which, double v, uint64_t tag) const {
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);
+    gran_t g = {(uint32_t)bits, (uint32_t)(bits >> 32), (uint32_t)tag, (uint32_t)(tag >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(g, rsrc, off(parity, k, b, which), 0, 16);  // aux 16 = sc1
+  }
+  __device__ gran_t get(int parity, int k, int b, int which) const {
+    return __builtin_amdgcn_raw_buffer_load_b128(rsrc, off(parity, k, b, which), 0, 16);
+  }
+};
+__device__ inline double g_val(gran_t g) { return __longlong_as_double((long long)(((uint64_t)g.y << 32) | g.x)); }
+__device__ inline bool g_tag_is(gran_t g, uint64_t tag) { return g.z == (uint32_t)tag && g.w == (uint32_t)(tag >> 32); }
+
+// the block's (mean, M2) partial of vals[nvalid][D] (publish_partial's arithmetic) as
+// granules tagged `tag`; lane 0 / 1 of column group k write mean / M2
+__device__ inline void publish_granules(const Granules& gr, const double* vals, int nvalid, int parity, uint64_t tag) {
+  const int k = threadIdx.x >> 4, j = threadIdx.x & 15;
+  double s = 0.0;
+  if (k < gr.D)
+    for (int i = j; i < nvalid; i += 16) s += vals[i * gr.D + k];
+  const double mean = nvalid > 0 ? sum16(s) / (double)nvalid : 0.0;
+  double m2 = 0.0;
+  if (k < gr.D)
+    for (int i = j; i < nvalid; i += 16) {
+      const double dv = vals[i * gr.D + k] - mean;
+      m2 += dv * dv;
+    }
+  m2 = sum16(m2);
+  if (k < gr.D && j < 2) gr.put(parity, k, blockIdx.x, j, j == 0 ? mean : m2, tag);
+}
+
+// column k's records of blocks b0 + jj + 16q as RecRound registers, polled until every
+// granule carries `tag`; n_b is known (envs of block b; 0 for the reward column of the
+// reset partial).  false: the grid gave up (some block never published).
+__device__ inline bool gather_granules(const Granules& gr, RecRound& rr, int parity, int k, int jj, int b0, int E,
+                                       bool rew_counted, uint64_t tag, uint32_t* sync) {
+  const bool isr = (k == gr.D - 1);
+#pragma unroll
+  for (int q = 0; q < RB_MAX; ++q) {
+    const int b = b0 + jj + 16 * q;
+    rr.rn[q] = (b < gr.nb && (!isr || rew_counted)) ? (double)min(ENVS_PER_BLOCK, E - b * ENVS_PER_BLOCK) : 0.0;
+  }
+  uint32_t it = 0;
+  while (true) {
+    bool ready = true;
+#pragma unroll
+    for (int q = 0; q < RB_MAX; ++q) {
+      const int b = b0 + jj + 16 * q;
+      if (b < gr.nb) {
+        const gran_t gm = gr.get(parity, k, b, 0), gs = gr.get(parity, k, b, 1);
+        ready = ready && g_tag_is(gm, tag) && g_tag_is(gs, tag);
+        rr.rm[q] = g_val(gm);
+        rr.rs[q] = g_val(gs);
+      } else {
+        rr.rm[q] = 0.0;
+        rr.rs[q] = 0.0;
+      }
+    }
+    if (ready) return true;
+    __builtin_amdgcn_s_sleep(1);
+    if ((++it & 255) == 0 &&
+        (it > SPIN_LIMIT || __hip_atomic_load(sync + SYNC_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+      __hip_atomic_store(sync + SYNC_ABORT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+}
+
+template <int ENV>
+__device__ inline void reset_env_reg(const RollArgs& a, int e, double* s, uint32_t& epc, int& ept) {
+  const uint32_t gid = (uint32_t)(a.d.env_offset + e);
+  double u[EnvC<ENV>::NU];
+#pragma unroll
+  for (int c = 0; c < EnvC<ENV>::NU / 2; ++c)
+    philox_uniform2(a.d.seed, 1, gid, (uint64_t)epc, (uint32_t)c, u[2 * c], u[2 * c + 1]);
+  EnvC<ENV>::reset(u, s);
+  epc += 1u;
+  ept = 0;
+}
+
+template <int ENV>
+__global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, const float* __restrict__ logstd,
+                                                                const float* __restrict__ rimg,
+                                                                uint32_t* __restrict__ sync) {
+  using EC = EnvC<ENV>;
+  constexpr int O = EC::OBS, D = O + 1, NS = EC::NS, A = EC::ACT;
+  __shared__ double vals[ENVS_PER_BLOCK * MAXD];
+  __shared__ double fmean[MAXD], fden[MAXD];
+  __shared__ float xt[4][16][MAX_IN + 1];  // +1: conflict-free column reads
+  __shared__ int s_fail;
+  const int E = a.d.n_envs, T = a.d.horizon, nb = a.nb;
+  // diagnostic phase stamps (100 MHz realtime) of block 0 -- never set in production
+#define PSTAMP(tt, k)                                                                  \
+  do {                                                                                 \
+    if (a.b.stamps != nullptr && threadIdx.x == 0 && blockIdx.x == 0)                  \
+      a.b.stamps[(int64_t)(tt) * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  const int le = wave * 16 + j;
+  const int e = blockIdx.x * ENVS_PER_BLOCK + le;
+  const bool valid = e < E;
+  const int ec = valid ? e : E - 1;  // invalid lanes shadow a valid env, store nothing
+  const int k = threadIdx.x >> 4, jj = threadIdx.x & 15;
+  const bool kcol = k < D, isr = (k == O);
+  const int nvalid = min(ENVS_PER_BLOCK, E - (int)blockIdx.x * ENVS_PER_BLOCK);
+  const Granules gr(sync, nb, D);
+  if (threadIdx.x == 0) s_fail = 0;
+
+  RWeights<O, A> wt;
+  wt.load(rimg, lane);
+  float lsd[A];
+#pragma unroll
+  for (int q = 0; q < A; ++q) lsd[q] = EC::DISCRETE ? 0.f : logstd[q];
+  // the running stat at the start of the iteration (every block keeps the same copy)
+  double fn = 0.0, fM = 0.0, fS = 0.0;
+  if (kcol) {
+    fn = a.b.filter_state[isr ? 1 : 0];
+    fM = a.b.filter_state[2 + k];
+    fS = a.b.filter_state[2 + D + k];
+  }
+  // reset every env (core.py:186); all four rows of a wave hold the same env
+  double s[NS];
+  uint32_t epc = (uint32_t)a.b.env_int[E + ec];
+  int ept = 0;
+  reset_env_reg<ENV>(a, ec, s, epc, ept);
+  if (valid && g == 0) {
+    double o[O];
+    EC::obs(s, o);
+#pragma unroll
+    for (int c = 0; c < O; ++c) vals[le * D + c] = o[c];
+    vals[le * D + O] = 0.0;
+  }
+  __syncthreads();
+  publish_granules(gr, vals, nvalid, 0, 1);  // step 0's partials: parity 0, tag 1
+
+  for (int t = 0; t < T; ++t) {
+    const int64_t row = (int64_t)t * E + e;
+    PSTAMP(t, 0);
+    double zn[A + 1] = {};
+    load_noise<ENV>(a, (int64_t)t * E + ec, zn);  // independent of the hand-off: issued first
+    // running-stat merge of step t's batch (filters.py:30-31), identical in every block
+    if (kcol) {
+      double bn, bm, bs;
+      RecRound rr;
+      bool ok = true;
+      if (nb <= 16 * RB_MAX) {
+        ok = gather_granules(gr, rr, t & 1, k, jj, 0, E, t > 0, (uint64_t)t + 1, sync);
+        rr.batch(bn, bm, bs);
+      } else {
+        double n = 0.0, sm = 0.0, raw = 0.0;
+        for (int b0 = 0; b0 < nb && ok; b0 += 16 * RB_MAX) {
+          ok = gather_granules(gr, rr, t & 1, k, jj, b0, E, t > 0, (uint64_t)t + 1, sync);
+          rr.accumulate(n, sm, raw);
+        }
+        n = sum16(n);
+        sm = sum16(sm);
+        bm = n > 0.0 ? sm / n : 0.0;
+        bn = n;
+        bs = sum16(raw) - n * bm * bm;
+      }
+      if (!ok) s_fail = 1;
+      chan_merge(fn, fM, fS, bn, bm, bs);
+      if (!isr && jj == 0) {
+        const double var = fn > 1.0 ? fS / (fn - 1.0) : fM * fM;  // running_stat.py:27
+        fmean[k] = fM;
+        fden[k] = sqrt(var) + 1e-8;
+      }
+    }
+    __syncthreads();
+    if (s_fail) break;  // uniform: a block that gave up leaves the loop whole
+    PSTAMP(t, 1);
+    // filtered observation (core.py:191-192); row g takes columns 4i + g
+    {
+      double o[O];
+      EC::obs(s, o);
+#pragma unroll
+      for (int i = 0; i < (O + 3) / 4; ++i) {
+        const int kc = 4 * i + g;
+        double v = o[4 * i];
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+          if (4 * i + q < O && g == q) v = o[4 * i + q < O ? 4 * i + q : O - 1];
+        if (a.d.filter) {
+          const int kk = kc < O ? kc : O - 1;
+          v = v - fmean[kk];
+          v = v / fden[kk];
+          v = v < -5.0 ? -5.0 : (v > 5.0 ? 5.0 : v);
+        }
+        const float vf = (float)v;
+        if (kc < O) {
+          if (valid) a.b.obs[row * O + kc] = vf;
+          xt[wave][j][kc] = vf;
+        }
+      }
+    }
+    WAVE_LDS_ORDER();
+    PSTAMP(t, 2);
+    struct XL {
+      const float* p;
+      bool valid;
+      __device__ inline float operator()(int c) const { return (valid && c < O) ? p[c] : 0.f; }
+    } xl{&xt[wave][j][0], valid};
+    float z[A];
+    forward16<O, A>(wt, xl, lane, z);
+    PSTAMP(t, 3);
+    // sample + env step on every row (split angle functions); row 0 stores
+    double rew = 0.0;
+    bool done = false;
+    sample_and_step<ENV, true>(a, row, z, lsd, zn, s, rew, done, valid && g == 0, g);
+    PSTAMP(t, 4);
+    // episode bookkeeping on every row, so the rows keep identical env state
+    // (finish_env_step: gym TimeLimit => terminated; limit / horizon cut => not)
+    {
+      const bool term = done || (ept + 1 >= EC::MAX_STEPS);
+      const bool last = term || (ept + 1 >= a.d.timestep_limit) || (t == T - 1);
+      if (valid && g == 0) {
+        a.b.ep_t[row] = ept;
+        a.b.rew[row] = (float)rew;
+        a.b.flags[row] = (uint8_t)((last ? 1 : 0) | (term ? 2 : 0));
+      }
+      if (last && t < T - 1) reset_env_reg<ENV>(a, ec, s, epc, ept);
+      else ept += 1;
+    }
+    if (valid && g == 0) {
+      double o[O];
+      EC::obs(s, o);
+#pragma unroll
+      for (int c = 0; c < O; ++c) vals[le * D + c] = o[c];
+      vals[le * D + O] = rew;
+    }
+    __syncthreads();
+    PSTAMP(t, 5);
+    if (t + 1 < T) publish_granules(gr, vals, nvalid, (t + 1) & 1, (uint64_t)t + 2);
+    else publish_partial(a, vals, nvalid, D, true, a.b.records + (int64_t)(T & 1) * nb * a.RS);  // for finish
+    PSTAMP(t, 6);
+  }
+#undef PSTAMP
+  // state for the next iteration and the finish kernel: env state / counters, and the
+  // running stat where the step kernels leave it (parity T)
+  if (valid && g == 0) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) a.b.env_state[(int64_t)i * E + e] = s[i];
+    a.b.env_int[e] = ept;
+    a.b.env_int[E + e] = (int32_t)epc;
+  }
+  if (blockIdx.x == 0 && kcol && jj == 0) {
+    double* fs_out = a.b.filter_state + (T & 1) * a.FS;
+    if (k == 0) fs_out[0] = fn;
+    if (isr) fs_out[1] = fn;
+    fs_out[2 + k] = fM;
+    fs_out[2 + D + k] = fS;
+  }
+}
+
 // ------------------------------------------------------------------ layered-policy rollout
 // For policies the fused step kernel does not cover (wide nets, Humanoid's 376-d obs),
 // step t is three launches: lrollout_obs (filter merge + normalised obs rows) ->
@@ -1064,6 +1347,58 @@ int mrl_rollout_pack(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const f
   hipLaunchKernelGGL(rollout_pack_kernel, dim3((r.size + 255) / 256), dim3(256), 0, (hipStream_t)stream, r, md, theta,
                      rimage);
   return hip_check(hipGetLastError(), "mrl_rollout_pack");
+}
+
+int64_t mrl_rollout_sync_bytes(const mrl_rollout_desc* d) {
+  if (!d || d->n_envs <= 0) return -1;
+  const int64_t nb = (d->n_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
+  return SYNC_HEAD_BYTES + 2 * (int64_t)(env_info(d->env_id).obs + 1) * nb * 32;
+}
+
+// The nb blocks fit one per CU of the launch stream (its CU mask) at this kernel's
+// register use: the persistent launch may run (cooperative: HIP refuses a grid that
+// cannot be resident at once).
+static bool persistent_fits(int nb, hipStream_t s) {
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return false;
+  int cus = ncu;
+  if (s != nullptr) {
+    uint32_t mask[16] = {};
+    const int words = (ncu + 31) / 32;
+    if (words <= 16 && hipExtStreamGetCUMask(s, (uint32_t)words, mask) == hipSuccess) {
+      cus = 0;
+      for (int w = 0; w < words; ++w) cus += __builtin_popcount(mask[w]);
+    }
+  }
+  return nb <= cus;
+}
+
+int mrl_rollout_run(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta, const float* rimage,
+                    const mrl_rollout_bufs* b, uint32_t* sync, int32_t persistent, void* stream) {
+  int rc = check_roll(d, b);
+  if (rc) return rc;
+  if (!pol || !theta || !rimage) return fail(E_ARG, "null policy");
+  if (d->env_id == MRL_ENV_HUMANOID) return fail(E_UNSUPPORTED, "Humanoid runs on the layered rollout");
+  if (!b->obs || !b->act || !b->prob || !b->rew || !b->flags || !b->ep_t) return fail(E_ARG, "null trajectory buffer");
+  if (!b->noise) return fail(E_ARG, "bufs.noise: sampling-noise rows (mrl_rollout_noise or injected) required");
+  rc = check_fused_policy(d, pol);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  RollArgs a = make_args(d, b);
+  if (!persistent || !sync || !persistent_fits(a.nb, s)) {
+    rc = mrl_rollout_reset(d, b, stream);
+    for (int32_t t = 0; t < d->horizon && rc == OK; ++t) rc = mrl_rollout_step(d, pol, theta, rimage, b, t, stream);
+    return rc;
+  }
+  const MlpDims md = mlp_dims(pol->n_in, pol->n_out, pol->head == MRL_HEAD_GAUSS);
+  const float* logstd = pol->head == MRL_HEAD_GAUSS ? theta + md.tls : nullptr;
+  rc = hip_check(hipMemsetAsync(sync, 0, (size_t)mrl_rollout_sync_bytes(d), s), "mrl_rollout_run");
+  if (rc) return rc;
+  void* args[] = {&a, &logstd, &rimage, &sync};
+  const void* fn = d->env_id == MRL_ENV_CARTPOLE ? (const void*)rollout_persistent_kernel<MRL_ENV_CARTPOLE>
+                                                 : (const void*)rollout_persistent_kernel<MRL_ENV_HOPPER>;
+  return hip_check(hipLaunchCooperativeKernel(fn, dim3(a.nb), dim3(RB), args, 0, s), "mrl_rollout_run");
 }
 
 int mrl_rollout_step(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta, const float* rimage,

@@ -98,6 +98,35 @@ def test_rollout_matches_oracle(env_id, E, Tn, limit, inject):
         np.testing.assert_allclose(mr, fs.M[-1], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("env_id,E,Tn,graph", [("Hopper-v2", 4096, 64, True), ("Hopper-v2", 100, 300, False),
+                                               ("CartPole-v0", 1, 250, False), ("CartPole-v0", 8256, 12, False),
+                                               ("Hopper-v2", 8256, 8, True)])
+def test_persistent_rollout_equals_step_launches(env_id, E, Tn, graph):
+    """mrl_rollout_run as ONE persistent launch (blocks resident, per-step running-stat
+    hand-off through memory) vs T step launches: every trajectory row, the filter
+    state, env state and counters bit-identical over two iterations.  E = 8256 takes
+    the multi-round record merge (129 blocks > 128)."""
+    from modular_rl_amd.collector import Collector
+    from modular_rl_amd.envs import make
+    env = make(env_id)
+    head = "softmax" if env.discrete else "gauss"
+    _, _, pol = _policy(head, env.obs_dim, env.act_dim, seed=17)
+    outs = []
+    for persistent in (False, True):
+        col = Collector(env, pol, E, Tn, 1000 if not env.discrete else 200, seed=31, use_graph=graph)
+        col.persistent = persistent
+        got = []
+        for _ in range(2):
+            b = col.collect()
+            if persistent:
+                col.check()
+            got += [t.clone() for t in (b.obs, b.act, b.prob, b.rew, b.flags, b.ep_t)]
+        got += [col.filter_state[:col.FS].clone(), col.env_state.clone(), col.env_int.clone(), col.iteration.clone()]
+        outs.append(got)
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), i
+
+
 def test_rollout_graph_replay_equals_eager():
     from modular_rl_amd.collector import Collector
     from modular_rl_amd.envs import make
