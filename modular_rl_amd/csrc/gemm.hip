@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
         for (int r = 0; r < 16; ++r) {
           float v = acc[mi][ni][r] + bv;
           if (g.epi == MRL_GEMM_TANH) v = tanh_fast(v);
-          else if (g.epi == MRL_GEMM_DTANH) v *= (1.f - hv[r] * hv[r]);
+          else if (g.epi == MRL_GEMM_DTANH) v *= dtanh(hv[r]);
           C[(rbase + cperm(r, h)) * g.ldc + col] = v;
         }
         continue;
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
         if (g.epi == MRL_GEMM_TANH) v = tanh_fast(v);
         else if (g.epi == MRL_GEMM_DTANH) {
           const float hv = g.H[row * g.ldh + col];
-          v *= (1.f - hv * hv);
+          v *= dtanh(hv);
         }
         C[row * g.ldc + col] = v;
       }

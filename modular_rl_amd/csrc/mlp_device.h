@@ -45,11 +45,13 @@ struct XGlobal {
   int n_obs;
   int64_t row;
   bool valid;
+  // branch-free: rows past the batch read row 0 and are zeroed at the end
   __device__ inline float operator()(int k) const {
-    if (!valid) return 0.f;
-    if (k < n_obs) return x[row * n_obs + k];
-    if (ept != nullptr && k == n_obs) return (float)((double)ept[row] / ts_limit);
-    return 0.f;
+    const int64_t r = valid ? row : 0;
+    float v = 0.f;
+    if (k < n_obs) v = x[r * n_obs + k];
+    else if (ept != nullptr && k == n_obs) v = (float)((double)ept[r] / ts_limit);
+    return valid ? v : 0.f;
   }
 };
 
@@ -93,15 +95,24 @@ __device__ inline void chain(const float* lds, int seg, const f32x16* src, int l
 // critical path): odd Taylor polynomial for |x| < 0.125 (rel. err < 1e-9), else
 // 1 - 2/(exp(2|x|)+1) with v_exp_f32 / v_rcp_f32 (abs. err ~1e-7); saturates to
 // +-1, propagates NaN.
+// Every multiply-add is an explicit fmaf, so the rounding never depends on the
+// compiler's contraction choice: each kernel instantiation that evaluates the same
+// activation gets the same bits (the activation cache is bitwise transparent).
 __device__ inline float tanh_fast(float x) {
   const float ax = fabsf(x);
   const float x2 = x * x;
-  const float p = x * (1.f + x2 * (-0.333333343f + x2 * (0.133333340f + x2 * -0.0539682545f)));
+  float q = fmaf(x2, -0.0539682545f, 0.133333340f);
+  q = fmaf(x2, q, -0.333333343f);
+  q = fmaf(x2, q, 1.f);
+  const float p = x * q;
   const float e = __expf(2.f * ax);
-  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+  const float t = fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
   const float r = copysignf(t, x);
   return ax < 0.125f ? p : r;
 }
+
+// tanh' from the activation, 1 - h^2, as one explicit fma (see tanh_fast)
+__device__ inline float dtanh(float h) { return fmaf(-h, h, 1.f); }
 
 __device__ inline void tanh16(f32x16& a) {
 #pragma unroll
@@ -122,7 +133,10 @@ __device__ inline void head_partial(const float* lds, const MlpDims& d, const f3
       for (int q = 0; q < 8; ++q) {
         const float4 wv = ld4(w + o * 32 + 4 * q);
         const int mt = q >> 2, r0 = 4 * (q & 3);
-        acc += wv.x * src[mt][r0] + wv.y * src[mt][r0 + 1] + wv.z * src[mt][r0 + 2] + wv.w * src[mt][r0 + 3];
+        acc = fmaf(wv.x, src[mt][r0], acc);
+        acc = fmaf(wv.y, src[mt][r0 + 1], acc);
+        acc = fmaf(wv.z, src[mt][r0 + 2], acc);
+        acc = fmaf(wv.w, src[mt][r0 + 3], acc);
       }
       z[o] += acc;
     }
@@ -146,7 +160,10 @@ __device__ inline void head_partial_mt(const float* lds, const MlpDims& d, const
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 wv = ld4(w + o * 32 + 4 * q);
-        acc += wv.x * src[4 * q] + wv.y * src[4 * q + 1] + wv.z * src[4 * q + 2] + wv.w * src[4 * q + 3];
+        acc = fmaf(wv.x, src[4 * q], acc);
+        acc = fmaf(wv.y, src[4 * q + 1], acc);
+        acc = fmaf(wv.z, src[4 * q + 2], acc);
+        acc = fmaf(wv.w, src[4 * q + 3], acc);
       }
       z[o] += acc;
     }
@@ -237,7 +254,7 @@ __device__ inline void jvp_head_cached(const float* lds, const float* ldt, const
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dh1[m][r] *= (1.f - h1[m][r] * h1[m][r]);
+    for (int r = 0; r < 16; ++r) dh1[m][r] *= dtanh(h1[m][r]);
   float dzt[MAX_OUT];
 #pragma unroll
   for (int o = 0; o < MAX_OUT; ++o) {
@@ -255,7 +272,7 @@ __device__ inline void jvp_head_cached(const float* lds, const float* ldt, const
     chain1(ldt, d.fa1, mo, h1, lane, da);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) da[r] *= (1.f - a[r] * a[r]);
+    for (int r = 0; r < 16; ++r) da[r] *= dtanh(a[r]);
     if (need_z) head_partial_mt(lds, d, a, mo, h, z);
     head_partial_mt(lds, d, da, mo, h, dz);
     head_partial_mt(ldt, d, a, mo, h, dzt);
@@ -283,7 +300,7 @@ __device__ inline void forward_jvp_head_lowreg(const float* lds, const float* ld
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dh1[m][r] *= (1.f - h1[m][r] * h1[m][r]);
+    for (int r = 0; r < 16; ++r) dh1[m][r] *= dtanh(h1[m][r]);
 #pragma unroll
   for (int o = 0; o < MAX_OUT; ++o) {
     z[o] = 0.f;
@@ -305,7 +322,7 @@ __device__ inline void forward_jvp_head_lowreg(const float* lds, const float* ld
     __builtin_amdgcn_sched_barrier(0);
     tanh16(a);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) da[r] *= (1.f - a[r] * a[r]);
+    for (int r = 0; r < 16; ++r) da[r] *= dtanh(a[r]);
     head_partial_mt(lds, d, a, mo, h, z);
     head_partial_mt(lds, d, da, mo, h, dz);
     head_partial_mt(ldt, d, a, mo, h, dzt);
@@ -395,7 +412,7 @@ __device__ inline void forward_jvp_tile(const float* lds, const float* ldt, cons
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dh[m][r] *= (1.f - f.h1[m][r] * f.h1[m][r]);
+    for (int r = 0; r < 16; ++r) dh[m][r] *= dtanh(f.h1[m][r]);
   f32x16 da[2];
   f.h2[0] = load_bias16(lds, d.fb1, 0, h);
   f.h2[1] = load_bias16(lds, d.fb1, 1, h);
@@ -409,7 +426,7 @@ __device__ inline void forward_jvp_tile(const float* lds, const float* ldt, cons
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) da[m][r] *= (1.f - f.h2[m][r] * f.h2[m][r]);
+    for (int r = 0; r < 16; ++r) da[m][r] *= dtanh(f.h2[m][r]);
 #pragma unroll
   for (int o = 0; o < MAX_OUT; ++o) {
     f.z[o] = 0.f;

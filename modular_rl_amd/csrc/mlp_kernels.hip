@@ -55,11 +55,29 @@ static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 constexpr int EPI_FVP_CACHED = 100;  // internal: MRL_EPI_FVP reading the activation cache
 
-template <int EPI_K>
+// the kernel arguments with a static shape's dimensions substituted (compile-time
+// constants after inlining); SH == 0 leaves the run-time shape
+template <int SH>
+__device__ inline RowsArgs rows_shape(const RowsArgs& in) {
+  RowsArgs a = in;
+  if constexpr (SH != 0) {
+    constexpr StaticShape S = STATIC_SHAPES[SH];
+    a.d = static_dims(SH);
+    a.A = S.A;
+    a.head = S.head;
+    a.n_obs = S.O;
+    a.gh = S.head == MRL_HEAD_GAUSS ? 2 * S.A : S.A;
+    a.ept = nullptr;
+  }
+  return a;
+}
+
+template <int EPI_K, int SH>
 // 2 waves/SIMD: layer 2 is evaluated one M-tile at a time so the chain fits 256 registers
-__global__ __launch_bounds__(ROWS_BLOCK, 2) void mlp_rows_kernel(RowsArgs a, const float* __restrict__ img,
+__global__ __launch_bounds__(ROWS_BLOCK, 2) void mlp_rows_kernel(RowsArgs a_in, const float* __restrict__ img,
                                                                const float* __restrict__ imgt,
                                                                const int32_t* __restrict__ skip) {
+  const RowsArgs a = rows_shape<SH>(a_in);
   constexpr bool CACHED = EPI_K == EPI_FVP_CACHED;
   constexpr int EPI = CACHED ? MRL_EPI_FVP : EPI_K;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -151,9 +169,6 @@ __device__ inline void write_img(float* img, const f32x16* t, int lane) {
     for (int r = 0; r < 16; ++r) img[(32 * mt + cperm(r, h)) * IMG_PAD + base] = t[mt][r];
 }
 
-// tanh' from the activation as one explicit fma, so its rounding never depends on the
-// compiler's contraction choice (the cached and uncached instantiations agree bit for bit)
-__device__ inline float dtanh(float h) { return fmaf(-h, h, 1.f); }
 
 __device__ inline float rowsum32(const float* img, int unit) {
   const float* p = img + unit * IMG_PAD;
@@ -246,9 +261,27 @@ __device__ inline void vjp_load(const VjpArgs& a, int64_t tile, int lane, VjpIn<
   }
 }
 
-template <bool CACHED, bool WIDE>
-__global__ __launch_bounds__(256) void mlp_vjp_kernel(VjpArgs a, const float* __restrict__ img,
+template <int SH>
+__device__ inline VjpArgs vjp_shape(const VjpArgs& in) {
+  VjpArgs a = in;
+  if constexpr (SH != 0) {
+    constexpr StaticShape S = STATIC_SHAPES[SH];
+    a.d = static_dims(SH);
+    a.n_obs = S.O;
+    a.n_sum = S.head == MRL_HEAD_GAUSS ? S.A : 0;
+    a.gh = S.A + a.n_sum;
+    a.ept = nullptr;
+  }
+  return a;
+}
+
+#ifndef MRL_VJP_MINW  // minimum waves per SIMD the VJP's registers must allow (build switch)
+#define MRL_VJP_MINW 1
+#endif
+template <bool CACHED, bool WIDE, int SH>
+__global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in, const float* __restrict__ img,
                                                        const int32_t* __restrict__ skip) {
+  const VjpArgs a = vjp_shape<SH>(a_in);
   constexpr int MT0 = WIDE ? 2 : 1;  // 16-input tiles of gW0
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if (skip != nullptr && *skip != 0) return;
@@ -569,6 +602,21 @@ static int check_desc(const mrl_mlp_desc* d) {
 
 static MlpDims dims_of(const mrl_mlp_desc* d) { return mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS); }
 
+// the static shape (mlp_layout.h) a launch matches, or 0: plain rows only (a time
+// feature column built from ep_t takes the generic kernels)
+static int static_shape_of(const mrl_mlp_desc* d, bool has_ept) {
+#ifdef MRL_NO_STATIC_SHAPES
+  (void)d;
+  (void)has_ept;
+  return 0;
+#else
+  if (has_ept) return 0;
+  for (int i = 1; i < N_STATIC_SHAPES; ++i)
+    if (STATIC_SHAPES[i].O == d->n_in && STATIC_SHAPES[i].A == d->n_out && STATIC_SHAPES[i].head == d->head) return i;
+  return 0;
+#endif
+}
+
 static int64_t rows_blocks(int64_t n) {
   int64_t b = ceil_div(ceil_div(n, 32), 4);
   if (b < 1) b = 1;
@@ -673,36 +721,30 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
   const int64_t blocks = rows_blocks(io->n);
   size_t shm = (size_t)a.d.fwd_size * 4 * (epi == MRL_EPI_FVP ? 2 : 1);
   hipStream_t s = (hipStream_t)stream;
+  const int sh = static_shape_of(d, io->ep_t != nullptr);
+  const bool pol = sh == 1 || sh == 2, vf = sh == 3 || sh == 4;
+  const dim3 grid(epi == MRL_EPI_PPOSGD ? 1 : blocks), blk(ROWS_BLOCK);
+#define MRL_ROWS_LAUNCH(EK, OK)                                                                                     \
+  do {                                                                                                              \
+    if ((OK) && sh == 1) hipLaunchKernelGGL((mlp_rows_kernel<EK, 1>), grid, blk, shm, s, a, image, image_t, skip); \
+    else if ((OK) && sh == 2) hipLaunchKernelGGL((mlp_rows_kernel<EK, 2>), grid, blk, shm, s, a, image, image_t, skip); \
+    else if ((OK) && sh == 3) hipLaunchKernelGGL((mlp_rows_kernel<EK, 3>), grid, blk, shm, s, a, image, image_t, skip); \
+    else if ((OK) && sh == 4) hipLaunchKernelGGL((mlp_rows_kernel<EK, 4>), grid, blk, shm, s, a, image, image_t, skip); \
+    else hipLaunchKernelGGL((mlp_rows_kernel<EK, 0>), grid, blk, shm, s, a, image, image_t, skip);                  \
+  } while (0)
   switch (epi) {
-    case MRL_EPI_PROB:
-      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_PROB>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t, skip);
-      break;
-    case MRL_EPI_LOSSES:
-      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_LOSSES>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t, skip);
-      break;
-    case MRL_EPI_SURRGRAD:
-      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_SURRGRAD>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t,
-                         skip);
-      break;
-    case MRL_EPI_VFLOSS:
-      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_VFLOSS>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t, skip);
-      break;
+    case MRL_EPI_PROB: MRL_ROWS_LAUNCH(MRL_EPI_PROB, true); break;
+    case MRL_EPI_LOSSES: MRL_ROWS_LAUNCH(MRL_EPI_LOSSES, pol); break;
+    case MRL_EPI_SURRGRAD: MRL_ROWS_LAUNCH(MRL_EPI_SURRGRAD, pol); break;
+    case MRL_EPI_VFLOSS: MRL_ROWS_LAUNCH(MRL_EPI_VFLOSS, vf); break;
     case MRL_EPI_FVP:
-      if (a.cache_mode == MRL_CACHE_READ)
-        hipLaunchKernelGGL(mlp_rows_kernel<EPI_FVP_CACHED>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t,
-                           skip);
-      else
-        hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_FVP>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t,
-                           skip);
+      if (a.cache_mode == MRL_CACHE_READ) MRL_ROWS_LAUNCH(EPI_FVP_CACHED, pol);
+      else MRL_ROWS_LAUNCH(MRL_EPI_FVP, pol);
       break;
-    case MRL_EPI_PPOGRAD:
-      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_PPOGRAD>, dim3(blocks), dim3(ROWS_BLOCK), shm, s, a, image, image_t,
-                         skip);
-      break;
-    case MRL_EPI_PPOSGD:
-      hipLaunchKernelGGL(mlp_rows_kernel<MRL_EPI_PPOSGD>, dim3(1), dim3(ROWS_BLOCK), shm, s, a, image, image_t, skip);
-      break;
+    case MRL_EPI_PPOGRAD: MRL_ROWS_LAUNCH(MRL_EPI_PPOGRAD, pol); break;
+    case MRL_EPI_PPOSGD: MRL_ROWS_LAUNCH(MRL_EPI_PPOSGD, pol); break;
   }
+#undef MRL_ROWS_LAUNCH
   return hip_check(hipGetLastError(), "mrl_mlp_rows");
 }
 
@@ -728,16 +770,24 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
   size_t shm = ((size_t)a.d.total_size + 4 * (size_t)SCR_FLOATS) * 4;
   a.cache = act_cache;
   const bool wide = a.d.O > 16;
-  if (act_cache != nullptr && !wide)
-    hipLaunchKernelGGL((mlp_vjp_kernel<true, false>), dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image, skip);
-  else if (act_cache != nullptr)
-    hipLaunchKernelGGL((mlp_vjp_kernel<true, true>), dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image, skip);
-  else if (!wide)
-    hipLaunchKernelGGL((mlp_vjp_kernel<false, false>), dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image,
-                       skip);
-  else
-    hipLaunchKernelGGL((mlp_vjp_kernel<false, true>), dim3(blocks), dim3(256), shm, (hipStream_t)stream, a, image,
-                       skip);
+  // the run-time-shape VJP measured faster than its static-shape instantiations (Hopper
+  // policy at 4.19 M rows: 1.02 vs 1.07 ms; the register allocation differs), so the
+  // static shapes are used by the rows kernels only
+  const int sh = 0;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(blocks), blk(256);
+#define MRL_VJP_LAUNCH(C)                                                                                   \
+  do {                                                                                                      \
+    if (sh == 1) hipLaunchKernelGGL((mlp_vjp_kernel<C, false, 1>), grid, blk, shm, s, a, image, skip);     \
+    else if (sh == 2) hipLaunchKernelGGL((mlp_vjp_kernel<C, false, 2>), grid, blk, shm, s, a, image, skip); \
+    else if (sh == 3) hipLaunchKernelGGL((mlp_vjp_kernel<C, false, 3>), grid, blk, shm, s, a, image, skip); \
+    else if (sh == 4) hipLaunchKernelGGL((mlp_vjp_kernel<C, false, 4>), grid, blk, shm, s, a, image, skip); \
+    else if (!wide) hipLaunchKernelGGL((mlp_vjp_kernel<C, false, 0>), grid, blk, shm, s, a, image, skip);   \
+    else hipLaunchKernelGGL((mlp_vjp_kernel<C, true, 0>), grid, blk, shm, s, a, image, skip);               \
+  } while (0)
+  if (act_cache != nullptr) MRL_VJP_LAUNCH(true);
+  else MRL_VJP_LAUNCH(false);
+#undef MRL_VJP_LAUNCH
   return hip_check(hipGetLastError(), "mrl_mlp_vjp");
 }
 

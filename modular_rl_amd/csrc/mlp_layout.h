@@ -14,6 +14,7 @@
 // half h supplying unit 32*(s>>4) + cperm(s&15, h)), so layers chain with no data
 // movement; the weight fragments below are permuted to match.
 #pragma once
+#include "../../include/mrl_hip.h"
 #include "mrl_common.h"
 
 namespace mrl {
@@ -32,8 +33,8 @@ struct MlpDims {
   int tW0, tb0, tW1, tb1, tW2, tb2, tls, P;
 };
 
-__host__ __device__ inline MlpDims mlp_dims(int O, int A, int gauss) {
-  MlpDims d;
+__host__ __device__ constexpr MlpDims mlp_dims(int O, int A, int gauss) {
+  MlpDims d{};
   d.O = O;
   d.A = A;
   int ks0 = (O + 1) / 2;
@@ -58,6 +59,25 @@ __host__ __device__ inline MlpDims mlp_dims(int O, int A, int gauss) {
   d.tls = d.tb2 + A;
   d.P = d.tls + (gauss ? A : 0);
   return d;
+}
+
+// Shapes the benchmark configs run, compiled as their own kernel instantiations so
+// every dimension (inputs, outputs, head, k-steps) is a compile-time constant: no
+// runtime branches on the net shape inside the tile loops.  Shape 0 = any shape,
+// dimensions read at run time.  Inputs are plain rows (no time-feature column).
+struct StaticShape {
+  int O, A, head;
+};
+constexpr int N_STATIC_SHAPES = 5;
+constexpr StaticShape STATIC_SHAPES[N_STATIC_SHAPES] = {
+    {0, 0, 0},
+    {11, 3, MRL_HEAD_GAUSS},   // Hopper-v2 policy
+    {4, 2, MRL_HEAD_SOFTMAX},  // CartPole-v0 policy
+    {12, 1, MRL_HEAD_LINEAR},  // Hopper-v2 value net ([obs, t / limit])
+    {5, 1, MRL_HEAD_LINEAR},   // CartPole-v0 value net
+};
+__host__ __device__ constexpr MlpDims static_dims(int sh) {
+  return mlp_dims(STATIC_SHAPES[sh].O, STATIC_SHAPES[sh].A, STATIC_SHAPES[sh].head == MRL_HEAD_GAUSS);
 }
 
 // fragment slot (mo, s) of a segment with KSp k-steps -> float offset of lane 0

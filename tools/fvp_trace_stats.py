@@ -1,6 +1,6 @@
 """Per-role kernel durations from a rocprofv3 --kernel-trace CSV, with the Fisher-product
 VJP told apart from the other launches of the same template: it is the mlp_vjp_kernel
-dispatch that follows an mlp_rows_kernel<100> (FVP rows) dispatch on the same stream.
+dispatch that follows an mlp_rows_kernel<100 (FVP rows) dispatch on the same stream.
 bench.py's live HIP-event averages (``kernels``, ``roofline``) are over exactly these.
 
     python tools/fvp_trace_stats.py <run_kernel_trace.csv>    (all launches, warmup included)
@@ -21,7 +21,7 @@ def main():
     for r in rows:
         n, s = r["Kernel_Name"], r["Stream_Id"]
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6  # ms
-        if "mlp_rows_kernel<100>" in n:
+        if "mlp_rows_kernel<100" in n:
             dur["fvp_jvp_rows"].append(d)
             last_rows100[s] = True
         elif "mlp_vjp_kernel<true" in n:

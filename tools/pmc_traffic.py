@@ -14,11 +14,11 @@ import os
 
 # role -> kernel-name substring (first match wins, most specific first)
 ROLES = [
-    ("fvp_jvp_rows", "mlp_rows_kernel<100>"),
+    ("fvp_jvp_rows", "mlp_rows_kernel<100"),
     ("fvp_vjp", "mlp_vjp_kernel<true"),
     ("vjp_uncached", "mlp_vjp_kernel<false"),
-    ("rows_surrgrad", "mlp_rows_kernel<2>"),
-    ("rows_vfloss", "mlp_rows_kernel<3>"),
+    ("rows_surrgrad", "mlp_rows_kernel<2,"),
+    ("rows_vfloss", "mlp_rows_kernel<3,"),
     ("rollout_step", "rollout_step_kernel"),
     ("gae_scan", "gae_scan_kernel"),
     ("episode_stats", "episode_stats_kernel<"),
