@@ -4,9 +4,8 @@
 //
 //  * CartPole-v0: gym's classic-control equations (Euler, tau 0.02, reward 1,
 //    12-degree / 2.4 limits), reached through `env.step` at core.py:197.
-//  * Humanoid: a Humanoid-v2-SHAPED surrogate (376-d obs, 17-d action in [-.4, .4],
-//    frame_skip 5 x dt 0.003, 1.25 v + 5 alive - 0.1|a|^2 - impact, 1 < z < 2), a
-//    sagittal two-leg contact model with 17 damped actuated joints (oracle/envs.py).
+//  * Humanoid-v2: gym's humanoid.xml as 3-D articulated rigid-body dynamics
+//    (humanoid.h, twin of oracle/humanoid.py).
 //  * Hopper-v2: gym's hopper.xml as planar articulated rigid-body dynamics with
 //    compliant ground contact (11-d obs, 3-d action, gear 200, frame_skip 4,
 //    forward-velocity reward, Hopper-v2 health test); MuJoCo itself is absent.
@@ -340,184 +339,6 @@ __device__ inline void hopper_obs(const double* s, double* o) {
   for (int i = 0; i < 6; ++i) o[5 + i] = clampd(s[6 + i], -10.0, 10.0);
 }
 
-// ------------------------------------------------------------------ Humanoid surrogate
-// state: q[23] (x, y, z, roll, pitch, yaw, 17 joints) ++ v[23] ++ last torques[17]
-constexpr int HM_NQ = 23, HM_NV = 23, HM_ACT = 17, HM_NS = 63, HM_OBS = 376, HM_NU = 46;
-constexpr double HM_DT = 0.003;
-constexpr int HM_FRAME_SKIP = 5;
-constexpr double HM_GEAR = 100.0, HM_ACT_LIM = 0.4, HM_MASS = 40.0, HM_GRAV = 9.81;
-constexpr double HM_L_THIGH = 0.42, HM_L_SHIN = 0.42, HM_HIP_DROP = 0.5, HM_FOOT_R = 0.05;
-constexpr double HM_KC = 20000.0, HM_CC = 800.0, HM_MU = 0.9, HM_VMAX = 50.0;
-constexpr double HM_I_ROOT0 = 8.0, HM_I_ROOT1 = 6.0, HM_I_ROOT2 = 6.0;
-constexpr double HM_K_ROOT0 = 20.0, HM_K_ROOT1 = 5.0, HM_TOPPLE = 120.0;
-constexpr double HM_C_ROOT0 = 30.0, HM_C_ROOT1 = 30.0, HM_C_ROOT2 = 10.0;
-constexpr double HM_I_J = 1.0, HM_K_J = 100.0, HM_C_J = 10.0, HM_Z0 = 1.4;
-
-__device__ inline double hm_body_mass(int b) {
-  constexpr double m[14] = {8.0, 2.0, 6.0, 4.5, 2.6, 1.2, 4.5, 2.6, 1.2, 1.6, 1.2, 1.6, 1.2, 2.0};
-  return m[b];
-}
-__device__ inline void hm_limits(int j, double& lo, double& hi) {
-  if (j == 6 || j == 10) { lo = -2.5; hi = 0.0; }
-  else if (j == 13 || j == 16) { lo = -2.0; hi = 0.5; }
-  else { lo = -1.0; hi = 1.0; }
-}
-
-__device__ inline void humanoid_reset(const double* u, double* s) {
-  for (int i = 0; i < HM_NQ; ++i) s[i] = u[i] * 0.02 - 0.01;
-  s[2] = s[2] + HM_Z0;
-  for (int i = 0; i < HM_NV; ++i) s[HM_NQ + i] = u[HM_NQ + i] * 0.02 - 0.01;
-  for (int i = 0; i < HM_ACT; ++i) s[HM_NQ + HM_NV + i] = 0.0;
-}
-
-// foot of one leg (hip_y joint hy, knee kn): position x/z, normal and friction force
-__device__ inline void hm_leg(const double* q, const double* v, int hy, int kn, double& fx, double& fz, double& fn,
-                              double& ft) {
-  const double a1 = q[4] + q[6 + hy];
-  const double a2 = a1 + q[6 + kn];
-  const double w1 = v[4] + v[6 + hy];
-  const double w2 = w1 + v[6 + kn];
-  double s1, c1, s2, c2;
-  sincos(a1, &s1, &c1);
-  sincos(a2, &s2, &c2);
-  fx = (q[0] + HM_L_THIGH * s1) + HM_L_SHIN * s2;
-  fz = ((q[2] - HM_HIP_DROP) - HM_L_THIGH * c1) - HM_L_SHIN * c2;
-  const double fvx = (v[0] + (HM_L_THIGH * c1) * w1) + (HM_L_SHIN * c2) * w2;
-  const double fvz = (v[2] + (HM_L_THIGH * s1) * w1) + (HM_L_SHIN * s2) * w2;
-  const double pen = HM_FOOT_R - fz;
-  fn = pen > 0.0 ? fmax(HM_KC * pen - HM_CC * fvz, 0.0) : 0.0;
-  ft = (-HM_MU * fn) * tanh(fvx / 0.05);
-}
-
-__device__ inline void humanoid_substep(double* q, double* v, const double* tau) {
-  double fxr, fzr, fnr, ftr, fxl, fzl, fnl, ftl;
-  hm_leg(q, v, 5, 6, fxr, fzr, fnr, ftr);
-  hm_leg(q, v, 9, 10, fxl, fzl, fnl, ftl);
-  const double x = q[0], z = q[2];
-  double acc[HM_NV];
-  acc[0] = (ftr + ftl) / HM_MASS;
-  acc[1] = -0.5 * v[1];
-  acc[2] = (fnr + fnl) / HM_MASS - HM_GRAV;
-  const double tq_p = ((fxr - x) * fnr - (fzr - z) * ftr) + ((fxl - x) * fnl - (fzl - z) * ftl);
-  acc[3] = ((((HM_TOPPLE * sin(q[3]) - HM_K_ROOT0 * q[3]) - HM_C_ROOT0 * v[3]) + 0.02 * (tau[3] - tau[7])) +
-            0.01 * (fnr - fnl)) / HM_I_ROOT0;
-  acc[4] = ((((HM_TOPPLE * sin(q[4]) + 0.02 * tq_p) - HM_K_ROOT1 * q[4]) - HM_C_ROOT1 * v[4]) -
-            0.05 * (tau[5] + tau[9])) / HM_I_ROOT1;
-  acc[5] = (0.02 * (tau[4] + tau[8]) - HM_C_ROOT2 * v[5]) / HM_I_ROOT2;
-#pragma unroll
-  for (int j = 0; j < HM_ACT; ++j) {
-    const double qj = q[6 + j], vj = v[6 + j];
-    double a = (tau[j] - HM_K_J * qj) - HM_C_J * vj;
-    if (j >= 3 && j <= 6) a = a + (0.03 * fnr) * sin(qj);
-    else if (j >= 7 && j <= 10) a = a + (0.03 * fnl) * sin(qj);
-    acc[6 + j] = a / HM_I_J;
-  }
-#pragma unroll
-  for (int i = 0; i < HM_NV; ++i) v[i] = clampd(v[i] + HM_DT * acc[i], -HM_VMAX, HM_VMAX);
-#pragma unroll
-  for (int i = 0; i < HM_NQ; ++i) q[i] = q[i] + HM_DT * v[i];
-#pragma unroll
-  for (int j = 0; j < HM_ACT; ++j) {
-    double lo, hi;
-    hm_limits(j, lo, hi);
-    const bool over = q[6 + j] > hi;
-    const bool under = q[6 + j] < lo;
-    q[6 + j] = over ? hi : (under ? lo : q[6 + j]);
-    if (over || under) v[6 + j] = 0.0;
-  }
-}
-
-__device__ inline void humanoid_step(double* s, const float* a, double& rew, bool& done) {
-  double* q = s;
-  double* v = s + HM_NQ;
-  double* tau = s + HM_NQ + HM_NV;
-  double asq = 0.0;
-#pragma unroll
-  for (int j = 0; j < HM_ACT; ++j) {
-    const double aj = (double)a[j];
-    tau[j] = HM_GEAR * clampd(aj, -HM_ACT_LIM, HM_ACT_LIM);
-    asq = asq + aj * aj;
-  }
-  const double x_before = q[0];
-  for (int k = 0; k < HM_FRAME_SKIP; ++k) humanoid_substep(q, v, tau);
-  double fxr, fzr, fnr, ftr, fxl, fzl, fnl, ftl;
-  hm_leg(q, v, 5, 6, fxr, fzr, fnr, ftr);
-  hm_leg(q, v, 9, 10, fxl, fzl, fnl, ftl);
-  const double cfrc = ((fnr * fnr + ftr * ftr) + fnl * fnl) + ftl * ftl;
-  const double impact = fmin(5e-7 * cfrc, 10.0);
-  rew = ((1.25 * (q[0] - x_before) / (HM_DT * HM_FRAME_SKIP) + 5.0) - 0.1 * asq) - impact;
-  bool healthy = true;
-#pragma unroll
-  for (int i = 0; i < HM_NS; ++i) healthy = healthy && isfinite(s[i]);
-  healthy = healthy && (q[2] > 1.0) && (q[2] < 2.0);
-  done = !healthy;
-}
-
-constexpr int HM_OBS_SLOTS = 16;
-// body b's features from its joint angle phi = q[6+b], joint velocity vb = v[6+b],
-// root angular velocity v3 = v[3 + b%3] and root linear velocities v0, v2
-template <class Out>
-__device__ inline void humanoid_body_features(int b, double phi, double vb, double v3, double v0, double v2,
-                                              Out out) {
-  const double m = hm_body_mass(b);
-  const int base = 45 + 10 * b;
-  for (int k = 0; k < 5; ++k) out(base + k, m * cos((double)k * phi));
-  for (int k = 1; k < 6; ++k) out(base + 4 + k, m * sin((double)k * phi));
-  double sph, cph;
-  sincos(phi, &sph, &cph);
-  const int cb = 185 + 6 * b;
-  out(cb + 0, vb);
-  out(cb + 1, v3);
-  out(cb + 2, v0 * cph);
-  out(cb + 3, v2 * sph);
-  out(cb + 4, vb * cph);
-  out(cb + 5, vb * sph);
-}
-// slot 14: qpos[2:], cos(pitch), qvel, zeros, actuator torques
-template <class Out>
-__device__ inline void humanoid_obs_misc(const double* s, Out out) {
-  const double* q = s;
-  const double* v = s + HM_NQ;
-  const double* tau = s + HM_NQ + HM_NV;
-#pragma unroll
-  for (int i = 0; i < 21; ++i) out(i, q[2 + i]);
-  out(21, cos(q[4]));
-#pragma unroll
-  for (int i = 0; i < HM_NV; ++i) out(22 + i, v[i]);
-  for (int i = 0; i < 6; ++i) out(269 + i, 0.0);
-#pragma unroll
-  for (int i = 0; i < HM_ACT; ++i) out(275 + i, tau[i]);
-}
-// slot 15: external contact forces of the two feet
-template <class Out>
-__device__ inline void humanoid_obs_contacts(const double* s, Out out) {
-  const double* q = s;
-  const double* v = s + HM_NQ;
-  double fxr, fzr, fnr, ftr, fxl, fzl, fnl, ftl;
-  hm_leg(q, v, 5, 6, fxr, fzr, fnr, ftr);
-  hm_leg(q, v, 9, 10, fxl, fzl, fnl, ftl);
-  for (int i = 0; i < 84; ++i) {
-    double val = 0.0;
-    if (i == 36) val = fnr;
-    else if (i == 37) val = ftr;
-    else if (i == 54) val = fnl;
-    else if (i == 55) val = ftl;
-    out(292 + i, val);
-  }
-}
-
-// 376-d observation, written through out(k, value) (SoA global rows on the layered
-// path), in 16 independent slots so a kernel can spread one env over 16 threads:
-// slot b < 14 = body b's 10 harmonic + 6 velocity features, 14 = qpos / cos / qvel /
-// zeros / torques, 15 = contact features
-template <class Out>
-__device__ inline void humanoid_obs(const double* s, Out out) {
-  const double* q = s;
-  const double* v = s + HM_NQ;
-#pragma unroll
-  for (int b = 0; b < 14; ++b) humanoid_body_features(b, q[6 + b], v[6 + b], v[3 + b % 3], v[0], v[2], out);
-  humanoid_obs_misc(s, out);
-  humanoid_obs_contacts(s, out);
-}
-
 }  // namespace mrl
+
+#include "humanoid.h"

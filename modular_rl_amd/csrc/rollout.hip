@@ -93,19 +93,14 @@ struct EnvC<MRL_ENV_HOPPER> {
   }
 };
 template <>
-struct EnvC<MRL_ENV_HUMANOID> {
+struct EnvC<MRL_ENV_HUMANOID> {  // stepped by the wave-per-env kernels (hm_*_kernel), not per thread
   static constexpr int NS = HM_NS, OBS = HM_OBS, ACT = HM_ACT, DISCRETE = 0, MAX_STEPS = 1000, NU = HM_NU,
-                       OBS_SLOTS = HM_OBS_SLOTS;  // obs features by lrollout_feat_kernel
-  __device__ static void reset(const double* u, double* s) { humanoid_reset(u, s); }
+                       OBS_SLOTS = 0;
+  __device__ static void reset(const double*, double*) {}
   __device__ static void step_disc(double*, int, double&, bool&) {}
-  __device__ static void step_cont(double* s, const float* a, double& rew, bool& done) {
-    humanoid_step(s, a, rew, done);
-  }
+  __device__ static void step_cont(double*, const float*, double&, bool&) {}
   template <class Out>
-  __device__ static void obs_out(const double* s, Out out) {
-    humanoid_obs(s, out);
-  }
-
+  __device__ static void obs_out(const double*, Out) {}
 };
 
 struct EnvInfo {
@@ -1125,36 +1120,81 @@ __global__ __launch_bounds__(RB) void lrollout_act_kernel(RollArgs a, const floa
   sample_and_step<ENV>(a, row, z, logstd, zn, s, rew, done);
   finish_env_step<ENV>(a, e, row, t, s, rew, done);
   double* raw = a.b.raw_obs;
-  if constexpr (EC::OBS_SLOTS == 0) EC::obs_out(s, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
+  EC::obs_out(s, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
   raw[(int64_t)O * E + e] = rew;
 }
 
-// raw next observation of envs whose features split into OBS_SLOTS independent slots
-// (Humanoid: 376 features, ~160 angle functions per env): thread (slot, env) of a
-// 16-env block evaluates one slot from the stepped state, instead of one thread per
-// env evaluating all of them serially inside lrollout_act_kernel.
-template <int ENV>
-__global__ __launch_bounds__(RB) void lrollout_feat_kernel(RollArgs a) {
-  using EC = EnvC<ENV>;
-  constexpr int NS = EC::NS, EB = RB / EC::OBS_SLOTS;
-  const int E = a.d.n_envs;
-  const int slot = threadIdx.x / EB, e = blockIdx.x * EB + threadIdx.x % EB;
-  if (e >= E) return;
-  const double* st = a.b.env_state + e;
+// Humanoid-v2 on the layered rollout: one wave per env (humanoid.h), its state in LDS.
+// hm_reset_kernel = lrollout_reset_kernel, hm_act_kernel = lrollout_act_kernel.
+__global__ __launch_bounds__(64) void hm_reset_kernel(RollArgs a) {
+  __shared__ hm::Wave W;
+  const int E = a.d.n_envs, e = blockIdx.x, lane = threadIdx.x;
+  const uint32_t w = (uint32_t)a.b.env_int[E + e];
+  hm::reset(W, lane, a.d.seed, (uint32_t)(a.d.env_offset + e), (uint64_t)w);
+  hm::forward(W, lane);
   double* raw = a.b.raw_obs;
-  auto out = [&](int k, double v) { raw[(int64_t)k * E + e] = v; };
-  static_assert(ENV == MRL_ENV_HUMANOID, "feature slots: Humanoid only");
-  if (slot < 14) {
-    humanoid_body_features(slot, st[(int64_t)(6 + slot) * E], st[(int64_t)(HM_NQ + 6 + slot) * E],
-                           st[(int64_t)(HM_NQ + 3 + slot % 3) * E], st[(int64_t)HM_NQ * E],
-                           st[(int64_t)(HM_NQ + 2) * E], out);
-  } else {
-    double s[NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) s[i] = st[(int64_t)i * E];
-    if (slot == 14) humanoid_obs_misc(s, out);
-    else humanoid_obs_contacts(s, out);
+  hm::observation(W, lane, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
+  if (lane < HM_NS) a.b.env_state[(int64_t)lane * E + e] = W.s[lane];
+  if (lane == 0) {
+    raw[(int64_t)HM_OBS * E + e] = 0.0;
+    a.b.env_int[E + e] = (int32_t)(w + 1);
+    a.b.env_int[e] = 0;
   }
+}
+
+__global__ __launch_bounds__(64) void hm_act_kernel(RollArgs a, const float* __restrict__ zrows,
+                                                    const float* __restrict__ logstd, int t) {
+  __shared__ hm::Wave W;
+  constexpr int A = HM_ACT;
+  const int E = a.d.n_envs, e = blockIdx.x, lane = threadIdx.x;
+  const int64_t row = (int64_t)t * E + e;
+  if (lane < HM_NS) W.s[lane] = a.b.env_state[(int64_t)lane * E + e];
+  WAVE_SYNC();
+  // sample (DiagGauss, core.py:432-435): a = z + sd * noise in fp32; the action is the ctrl
+  if (lane < A) {
+    const float z = zrows[(int64_t)e * A + lane];
+    const float sd = expf(logstd[lane]);
+    const double zn = reinterpret_cast<const double*>(a.b.noise)[row * A + lane];
+    const float av = __fadd_rn(__fmul_rn((float)zn, sd), z);
+    reinterpret_cast<float*>(a.b.act)[row * A + lane] = av;
+    a.b.prob[row * 2 * A + lane] = z;
+    a.b.prob[row * 2 * A + A + lane] = sd;
+    W.s[HM_NQ + HM_NV + lane] = (double)av;
+  }
+  WAVE_SYNC();
+  double x_before = 0.0;
+  for (int k = 0; k < hm::FRAME_SKIP; ++k) {
+    const double x0 = hm::substep(W, lane);
+    if (k == 0) x_before = x0;
+  }
+  hm::forward(W, lane);
+  double rew;
+  bool done;
+  hm::reward_done(W, lane, x_before, rew, done);
+  // episode bookkeeping (finish_env_step): TimeLimit => terminated, limit / horizon cut => not
+  const int ept = a.b.env_int[e];
+  const bool term = done || (ept + 1 >= EnvC<MRL_ENV_HUMANOID>::MAX_STEPS);
+  const bool last = term || (ept + 1 >= a.d.timestep_limit) || (t == a.d.horizon - 1);
+  if (lane == 0) {
+    a.b.ep_t[row] = ept;
+    a.b.rew[row] = (float)rew;
+    a.b.flags[row] = (uint8_t)((last ? 1 : 0) | (term ? 2 : 0));
+  }
+  if (last && t < a.d.horizon - 1) {
+    const uint32_t w = (uint32_t)a.b.env_int[E + e];
+    hm::reset(W, lane, a.d.seed, (uint32_t)(a.d.env_offset + e), (uint64_t)w);
+    hm::forward(W, lane);
+    if (lane == 0) {
+      a.b.env_int[E + e] = (int32_t)(w + 1);
+      a.b.env_int[e] = 0;
+    }
+  } else if (lane == 0) {
+    a.b.env_int[e] = ept + 1;
+  }
+  if (lane < HM_NS) a.b.env_state[(int64_t)lane * E + e] = W.s[lane];
+  double* raw = a.b.raw_obs;
+  hm::observation(W, lane, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
+  if (lane == 0) raw[(int64_t)HM_OBS * E + e] = rew;
 }
 
 __global__ void rollout_finish_kernel(RollArgs a, int O) {
@@ -1281,7 +1321,12 @@ int mrl_rollout_reset_rows(const mrl_rollout_desc* d, const mrl_rollout_bufs* b,
   const int D = env_info(d->env_id).obs + 1;
   // one wave per block: the per-env step is latency-bound, so spread the waves over CUs
   const dim3 genv((d->n_envs + 63) / 64), gpart(a.nb, (D + LCOLS - 1) / LCOLS);
-  MRL_DISPATCH_ENV(d->env_id, lrollout_reset_kernel, genv, dim3(64), 0, (hipStream_t)stream, a);
+  if (d->env_id == MRL_ENV_HUMANOID)
+    hipLaunchKernelGGL(hm_reset_kernel, dim3(d->n_envs), dim3(64), 0, (hipStream_t)stream, a);
+  else if (d->env_id == MRL_ENV_CARTPOLE)
+    hipLaunchKernelGGL(lrollout_reset_kernel<MRL_ENV_CARTPOLE>, genv, dim3(64), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(lrollout_reset_kernel<MRL_ENV_HOPPER>, genv, dim3(64), 0, (hipStream_t)stream, a);
   hipLaunchKernelGGL(lrollout_partials_kernel, gpart, dim3(RB), 0, (hipStream_t)stream, a, D, 0, 0);
   return hip_check(hipGetLastError(), "mrl_rollout_reset_rows");
 }
@@ -1312,12 +1357,12 @@ int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, cons
   RollArgs a = make_args(d, b);
   const int D = ei.obs + 1;
   const dim3 genv((d->n_envs + 63) / 64), gpart(a.nb, (D + LCOLS - 1) / LCOLS);
-  MRL_DISPATCH_ENV(d->env_id, lrollout_act_kernel, genv, dim3(64), 0, (hipStream_t)stream, a, z, logstd, t);
-  if (d->env_id == MRL_ENV_HUMANOID) {
-    constexpr int EB = RB / EnvC<MRL_ENV_HUMANOID>::OBS_SLOTS;
-    hipLaunchKernelGGL(lrollout_feat_kernel<MRL_ENV_HUMANOID>, dim3((d->n_envs + EB - 1) / EB), dim3(RB), 0,
-                       (hipStream_t)stream, a);
-  }
+  if (d->env_id == MRL_ENV_HUMANOID)
+    hipLaunchKernelGGL(hm_act_kernel, dim3(d->n_envs), dim3(64), 0, (hipStream_t)stream, a, z, logstd, t);
+  else if (d->env_id == MRL_ENV_CARTPOLE)
+    hipLaunchKernelGGL(lrollout_act_kernel<MRL_ENV_CARTPOLE>, genv, dim3(64), 0, (hipStream_t)stream, a, z, logstd, t);
+  else
+    hipLaunchKernelGGL(lrollout_act_kernel<MRL_ENV_HOPPER>, genv, dim3(64), 0, (hipStream_t)stream, a, z, logstd, t);
   hipLaunchKernelGGL(lrollout_partials_kernel, gpart, dim3(RB), 0, (hipStream_t)stream, a, D, (t + 1) & 1, 1);
   return hip_check(hipGetLastError(), "mrl_rollout_act");
 }

@@ -6,12 +6,12 @@ not vendored and are absent here, so env dynamics are **parity unpinned**:
 
 * ``cartpole_*`` restates gym's CartPole-v0 equations (Euler, tau=0.02,
   force 10, 12-degree / 2.4 thresholds, reward 1 per step, TimeLimit 200).
-* ``humanoid_*`` is a *surrogate* with Humanoid-v2's interface (376-d obs laid out
-  as qpos[2:] / qvel / cinert / cvel / qfrc_actuator / cfrc_ext, 17-d action in
-  [-0.4, 0.4], frame_skip 5 x dt 0.003, reward 1.25 forward velocity + 5 alive
-  - 0.1 |a|^2 - min(5e-7 |cfrc|^2, 10), healthy 1 < z < 2, TimeLimit 1000): a
-  sagittal two-leg contact model with 17 damped actuated joints -- shape- and
-  cost-representative, not MuJoCo.
+* ``humanoid_*`` (oracle/humanoid.py) restates gym's Humanoid-v2 (humanoid.xml: 13
+  bodies on a free joint + 17 hinges, 17 motors, frame_skip 5 x dt 0.003, the 376-d
+  qpos[2:] / qvel / cinert / cvel / qfrc_actuator / cfrc_ext observation, reward
+  0.25 dx_com / 0.003 + 5 - 0.1 |ctrl|^2 - min(0.5e-6 |cfrc_ext|^2, 10), healthy
+  1 <= z <= 2) as 3-D articulated rigid-body dynamics (com-based RNEA / CRBA,
+  tree-sparse L^T D L) with compliant ground contact; parity with MuJoCo unpinned.
 * ``hopper_*`` restates gym's Hopper-v2 model (hopper.xml: 4 capsule bodies on
   rootx / rootz / rooty + 3 actuated hinges, gear 200, frame_skip 4 x dt 0.002,
   11-d obs = qpos[1:] ++ clip(qvel, -10, 10), reward = forward velocity + 1 -
@@ -401,170 +401,11 @@ def hopper_step(qpos, qvel, a):
     return q, v, rew, ~healthy
 
 
-# ---------------------------------------------------------------- Humanoid surrogate
-# q: x, y, z, roll, pitch, yaw, 17 joints (Humanoid-v2 actuator order: abdomen y/z/x,
-# right hip x/z/y, right knee, left hip x/z/y, left knee, right shoulder 1/2, right
-# elbow, left shoulder 1/2, left elbow); state = q[23] ++ v[23] ++ last torques[17].
-HM_NQ, HM_NV, HM_ACT = 23, 23, 17
-HM_NS = HM_NQ + HM_NV + HM_ACT
-HM_OBS = 376
-HM_NU = 46
-HM_DT = 0.003
-HM_FRAME_SKIP = 5
-HM_GEAR = 100.0
-HM_ACT_LIM = 0.4
-HM_MASS = 40.0
-HM_GRAV = 9.81
-HM_L_THIGH = 0.42
-HM_L_SHIN = 0.42
-HM_HIP_DROP = 0.5
-HM_FOOT_R = 0.05
-HM_KC = 20000.0
-HM_CC = 800.0
-HM_MU = 0.9
-HM_VMAX = 50.0
-HM_I_ROOT = (8.0, 6.0, 6.0)
-HM_K_ROOT = (20.0, 5.0)
-HM_TOPPLE = 120.0  # m g h of the torso: upright is an unstable equilibrium
-HM_C_ROOT = (30.0, 30.0, 10.0)
-HM_I_J = 1.0
-HM_K_J = 100.0
-HM_C_J = 10.0
-HM_Z0 = 1.4
-HM_BODY_MASS = (8.0, 2.0, 6.0, 4.5, 2.6, 1.2, 4.5, 2.6, 1.2, 1.6, 1.2, 1.6, 1.2, 2.0)
-HM_RIGHT = (5, 6)  # hip_y, knee joint indices
-HM_LEFT = (9, 10)
-
-
-def hm_joint_limits(j):
-    if j in (6, 10):
-        return -2.5, 0.0
-    if j in (13, 16):
-        return -2.0, 0.5
-    return -1.0, 1.0
-
-
-def humanoid_reset(u):
-    """u: [E, 46] uniforms -> state [E, 63] (q0 + U(-.01,.01), v U(-.01,.01), torques 0)."""
-    E = u.shape[0]
-    s = np.zeros((E, HM_NS))
-    for i in range(HM_NQ):
-        s[:, i] = u[:, i] * 0.02 - 0.01
-    s[:, 2] = s[:, 2] + HM_Z0
-    for i in range(HM_NV):
-        s[:, HM_NQ + i] = u[:, HM_NQ + i] * 0.02 - 0.01
-    return s
-
-
-def _hm_leg(q, v, hy, kn):
-    """Foot of one leg: position, velocity, normal and friction force."""
-    pitch, vp = q[:, 4], v[:, 4]
-    a1 = pitch + q[:, 6 + hy]
-    a2 = a1 + q[:, 6 + kn]
-    w1 = vp + v[:, 6 + hy]
-    w2 = w1 + v[:, 6 + kn]
-    s1, c1 = np.sin(a1), np.cos(a1)
-    s2, c2 = np.sin(a2), np.cos(a2)
-    fx = (q[:, 0] + HM_L_THIGH * s1) + HM_L_SHIN * s2
-    fz = ((q[:, 2] - HM_HIP_DROP) - HM_L_THIGH * c1) - HM_L_SHIN * c2
-    fvx = (v[:, 0] + (HM_L_THIGH * c1) * w1) + (HM_L_SHIN * c2) * w2
-    fvz = (v[:, 2] + (HM_L_THIGH * s1) * w1) + (HM_L_SHIN * s2) * w2
-    pen = HM_FOOT_R - fz
-    fn = np.where(pen > 0.0, np.maximum(HM_KC * pen - HM_CC * fvz, 0.0), 0.0)
-    ft = (-HM_MU * fn) * np.tanh(fvx / 0.05)
-    return fx, fz, fn, ft
-
-
-def _hm_substep(q, v, tau):
-    fxr, fzr, fnr, ftr = _hm_leg(q, v, *HM_RIGHT)
-    fxl, fzl, fnl, ftl = _hm_leg(q, v, *HM_LEFT)
-    x, z = q[:, 0], q[:, 2]
-    acc = np.zeros_like(v)
-    acc[:, 0] = (ftr + ftl) / HM_MASS
-    acc[:, 1] = -0.5 * v[:, 1]
-    acc[:, 2] = (fnr + fnl) / HM_MASS - HM_GRAV
-    tq_p = ((fxr - x) * fnr - (fzr - z) * ftr) + ((fxl - x) * fnl - (fzl - z) * ftl)
-    acc[:, 3] = ((((HM_TOPPLE * np.sin(q[:, 3]) - HM_K_ROOT[0] * q[:, 3]) - HM_C_ROOT[0] * v[:, 3])
-                  + 0.02 * (tau[:, 3] - tau[:, 7])) + 0.01 * (fnr - fnl)) / HM_I_ROOT[0]
-    acc[:, 4] = ((((HM_TOPPLE * np.sin(q[:, 4]) + 0.02 * tq_p) - HM_K_ROOT[1] * q[:, 4]) - HM_C_ROOT[1] * v[:, 4])
-                 - 0.05 * (tau[:, 5] + tau[:, 9])) / HM_I_ROOT[1]
-    acc[:, 5] = (0.02 * (tau[:, 4] + tau[:, 8]) - HM_C_ROOT[2] * v[:, 5]) / HM_I_ROOT[2]
-    for j in range(HM_ACT):
-        qj, vj = q[:, 6 + j], v[:, 6 + j]
-        a = (tau[:, j] - HM_K_J * qj) - HM_C_J * vj
-        if 3 <= j <= 6:
-            a = a + (0.03 * fnr) * np.sin(qj)
-        elif 7 <= j <= 10:
-            a = a + (0.03 * fnl) * np.sin(qj)
-        acc[:, 6 + j] = a / HM_I_J
-    v = np.clip(v + HM_DT * acc, -HM_VMAX, HM_VMAX)
-    q = q + HM_DT * v
-    for j in range(HM_ACT):
-        lo, hi = hm_joint_limits(j)
-        over = q[:, 6 + j] > hi
-        under = q[:, 6 + j] < lo
-        q[:, 6 + j] = np.where(over, hi, np.where(under, lo, q[:, 6 + j]))
-        v[:, 6 + j] = np.where(over | under, 0.0, v[:, 6 + j])
-    return q, v
-
-
-def humanoid_step(s, a):
-    """s: [E, 63]; a: [E, 17] -> (s', reward, done)."""
-    a = np.asarray(a, dtype=np.float64)
-    tau = HM_GEAR * np.clip(a, -HM_ACT_LIM, HM_ACT_LIM)
-    asq = np.zeros(a.shape[0])
-    for j in range(HM_ACT):
-        asq = asq + a[:, j] * a[:, j]
-    q = s[:, :HM_NQ].copy()
-    v = s[:, HM_NQ:HM_NQ + HM_NV].copy()
-    x_before = q[:, 0].copy()
-    for _ in range(HM_FRAME_SKIP):
-        q, v = _hm_substep(q, v, tau)
-    _, _, fnr, ftr = _hm_leg(q, v, *HM_RIGHT)
-    _, _, fnl, ftl = _hm_leg(q, v, *HM_LEFT)
-    cfrc = ((fnr * fnr + ftr * ftr) + fnl * fnl) + ftl * ftl
-    impact = np.minimum(5e-7 * cfrc, 10.0)
-    rew = ((1.25 * (q[:, 0] - x_before) / (HM_DT * HM_FRAME_SKIP) + 5.0) - 0.1 * asq) - impact
-    s2 = np.concatenate([q, v, tau], axis=1)
-    healthy = np.isfinite(s2).all(axis=1) & (q[:, 2] > 1.0) & (q[:, 2] < 2.0)
-    return s2, rew, ~healthy
-
-
-def humanoid_obs(s):
-    """[E, 376] = qpos[2:] (21) ++ cos(pitch) | qvel (23) | cinert (14 x 10) | cvel (14 x 6)
-    | qfrc_actuator (6 zeros ++ 17 torques) | cfrc_ext (14 x 6, feet only)."""
-    q = s[:, :HM_NQ]
-    v = s[:, HM_NQ:HM_NQ + HM_NV]
-    tau = s[:, HM_NQ + HM_NV:]
-    E = s.shape[0]
-    o = np.zeros((E, HM_OBS))
-    o[:, 0:21] = q[:, 2:23]
-    o[:, 21] = np.cos(q[:, 4])
-    o[:, 22:45] = v
-    for b in range(14):
-        phi = q[:, 6 + b]
-        m = HM_BODY_MASS[b]
-        base = 45 + 10 * b
-        for k in range(5):
-            o[:, base + k] = m * np.cos(float(k) * phi)
-        for k in range(1, 6):
-            o[:, base + 4 + k] = m * np.sin(float(k) * phi)
-        cph, sph = np.cos(phi), np.sin(phi)
-        cb = 185 + 6 * b
-        o[:, cb + 0] = v[:, 6 + b]
-        o[:, cb + 1] = v[:, 3 + b % 3]
-        o[:, cb + 2] = v[:, 0] * cph
-        o[:, cb + 3] = v[:, 2] * sph
-        o[:, cb + 4] = v[:, 6 + b] * cph
-        o[:, cb + 5] = v[:, 6 + b] * sph
-    o[:, 275:292] = tau
-    _, _, fnr, ftr = _hm_leg(q, v, *HM_RIGHT)
-    _, _, fnl, ftl = _hm_leg(q, v, *HM_LEFT)
-    o[:, 292 + 6 * 6 + 0] = fnr
-    o[:, 292 + 6 * 6 + 1] = ftr
-    o[:, 292 + 9 * 6 + 0] = fnl
-    o[:, 292 + 9 * 6 + 1] = ftl
-    return o
+# ---------------------------------------------------------------- Humanoid-v2
+# 3-D articulated dynamics of gym's humanoid.xml: oracle/humanoid.py
+from oracle.humanoid import NS as HM_NS, NU as HM_NU, OBS as HM_OBS  # noqa: E402
+from oracle.humanoid import humanoid_obs, humanoid_reset, humanoid_step  # noqa: E402,F401
+HM_ACT = 17
 
 
 ENV_SPECS = {

@@ -39,6 +39,9 @@ KINDS = {"CartPole-v0": RO.CARTPOLE, "Hopper-v2": RO.HOPPER, "Humanoid-v2": RO.H
     ("CartPole-v0", [32], 7, 30, 12, True),
     ("Humanoid-v2", [512, 512, 512], 40, 12, 1000, False),
     ("Humanoid-v2", [128, 64], 130, 10, 6, True),
+    # articulated Humanoid-v2: ~22-step episodes under this policy end (healthy-z
+    # test) and auto-reset inside the horizon
+    ("Humanoid-v2", [64, 64], 64, 60, 1000, False),
 ])
 def test_layered_rollout_matches_oracle(env_id, hid, E, Tn, limit, inject):
     from modular_rl_amd.collector import Collector
@@ -59,6 +62,8 @@ def test_layered_rollout_matches_oracle(env_id, hid, E, Tn, limit, inject):
             col.set_noise(noise.reshape(Tn * E, -1) if not env.discrete else noise.reshape(-1))
         b = col.collect()
         want, fs = RO.collect(envs, fs, spec, th, Tn, limit, it, filt=True, noise=noise)
+        if env_id == "Humanoid-v2" and Tn >= 60:
+            assert (want["flags"] & 2).any()  # terminations happened (and were reset)
         np.testing.assert_array_equal(b.flags.cpu().numpy().reshape(Tn, E), want["flags"])
         np.testing.assert_array_equal(b.ep_t.cpu().numpy().reshape(Tn, E), want["ep_t"])
         np.testing.assert_allclose(b.obs.cpu().numpy().reshape(Tn, E, -1), want["obs"], rtol=1e-4, atol=1e-4)
