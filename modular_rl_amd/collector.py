@@ -21,6 +21,7 @@ iteration (rank order), so ranks normalise with identical statistics at every
 iteration start.
 """
 import ctypes
+import gc
 import os
 
 import numpy as np
@@ -165,6 +166,8 @@ class Collector:
         self.stamps = None  # diagnostic [T, 16] int64 phase stamps (see rollout.hip); None in production
         net = policy.net
         self.layered = bool(getattr(net, "layered", False))
+        # Humanoid steps one env per wave (humanoid.h): its chain wants one wave per SIMD
+        self.wave_per_env = env.kind == _lib.ENV_HUMANOID
         if env.kind == _lib.ENV_HUMANOID and not self.layered:
             raise _lib.MrlError("Humanoid-v2 needs a layered policy net (its 376-d obs exceeds the fused kernel)")
         self.raw_obs = None
@@ -244,10 +247,20 @@ class Collector:
         self._fs_start = self.filter_state[:self.FS].clone() if self.comm.enabled else None
         if self.use_graph and self.noise is None:
             if self.graph is None:
-                # captured launches are recorded, not executed: state is untouched by the capture
+                # captured launches are recorded, not executed: state is untouched by the
+                # capture.  No garbage collection inside the capture: collecting a dead
+                # object that owns HIP state (an earlier collector's graph) while the
+                # stream captures fails in its destructor and aborts the process.
+                gc.collect()
                 self.graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.graph):
-                    self._launch_all()
+                gc_was = gc.isenabled()
+                gc.disable()
+                try:
+                    with torch.cuda.graph(self.graph):
+                        self._launch_all()
+                finally:
+                    if gc_was:
+                        gc.enable()
             timing.start("rollout_steps")
             self.graph.replay()
             timing.stop("rollout_steps")

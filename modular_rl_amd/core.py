@@ -169,6 +169,15 @@ def run_policy_gradient_algorithm(env, agent, usercfg=None, callback=None):
 LAYERED_ROLLOUT_CUS = int(os.environ.get("MRL_LAYERED_ROLLOUT_CUS", "64"))
 
 
+def rollout_cus_needed(collector):
+    """CUs the rollout's step chain wants to itself: the fused step kernel one block per
+    CU (NB); Humanoid's wave-per-env step one wave per SIMD (E / 4 CUs); other layered
+    rollouts LAYERED_ROLLOUT_CUS for their GEMM tiles."""
+    if getattr(collector, "wave_per_env", False):
+        return -(-collector.E // 4)
+    return LAYERED_ROLLOUT_CUS if collector.layered else collector.NB
+
+
 def rollout_cu_split(n_rollout, n_cus):
     """(rollout CUs, fit CUs) for the pipelined loop, or None when the rollout needs
     too many CUs for a split to pay.  The fused rollout step kernel runs one block per
@@ -205,7 +214,7 @@ class IterationRunner:
         self.last_drain_events = {}
         if pipeline and torch.cuda.is_available():
             from . import streams
-            need = LAYERED_ROLLOUT_CUS if collector.layered else collector.NB
+            need = rollout_cus_needed(collector)
             split = rollout_cu_split(need, streams.cu_count())
             if split is not None:
                 self.rollout_stream = streams.masked_stream(split[0])

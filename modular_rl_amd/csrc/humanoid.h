@@ -29,6 +29,7 @@ constexpr int FRAME_SKIP = 5;
 constexpr double KC = 20000.0, CC = 400.0, CF = 1000.0, MU = 1.0, KL = 2000.0, CL = 5.0;
 constexpr double CTRL_LIMIT = 0.4, INIT_Z = 1.4;
 constexpr int NS = NQ + NV + NACT, OBS = 376, NU = 48;
+constexpr int NHINGE = NV - 6;  // the hinge dofs follow the free joint's 6
 
 __device__ inline void cross3(const double* a, const double* b, double* r) {
   r[0] = a[1] * b[2] - a[2] * b[1];
@@ -100,51 +101,232 @@ __device__ inline double dot6(const double* a, const double* b) {
 }
 
 #define WAVE_SYNC() asm volatile("" ::: "memory")
+#define HM_INLINE __device__ __attribute__((always_inline)) inline
+// diagnostic phase stamps (shader clock) into st[k] when st is set -- never in production
+#define HM_STAMP(k)                                                                     \
+  do {                                                                                  \
+    if (st != nullptr && lane == 0) st[k] = (int64_t)__builtin_amdgcn_s_memtime();      \
+  } while (0)
+
+// The model's index tables and constants, built at compile time (SHARED) and copied
+// into each block's LDS (Shared) at launch: a phase reads its table word or constant
+// with a ds_read issued ahead of its data instead of a lane-indexed global load (a
+// round trip of ~1k cycles each), and the sequential walks stay rolled loops -- the
+// step's loop body must fit the instruction cache (fully unrolled it did not: 4.5 ms
+// per step instead of 0.9).  Index tables are packed bytes, NONE = no entry.
+constexpr uint32_t NONE = 0xff;
+HM_INLINE uint32_t byte_of(uint32_t w, int s) { return (w >> (8 * s)) & 0xffu; }
+
+constexpr int N_ENT = NV + 170;               // mass-matrix entries (i, j in {i} + ancestors(i)); bound checked below
+constexpr int W_SUB = 0;                      // [NLEVEL] level lv's body at this lane | its children << 8, 16, 24
+constexpr int W_PATH = W_SUB + NLEVEL;        // [2] body `lane`'s path below the root, root side first (bytes)
+constexpr int W_OWN = W_PATH + 2;             // body `lane`: hinge0 | nhinge << 8 | sph0 << 16 | nsph << 24
+constexpr int W_MISC = W_OWN + 1;             // dof `lane`'s body | sphere `lane`'s body << 8 | hinge `lane - 32`'s parent body << 16
+constexpr int W_PAIR = W_MISC + 1;            // [NV] pivot k's (i, j) pairs at this lane: i0 | j0 << 8 | i1 << 16 | j1 << 24
+constexpr int W_KANC = W_PAIR + NV;           // [(NV+3)/4] pivot k's lane-th strict ancestor: byte k % 4 of word k / 4
+constexpr int W_ENT = W_KANC + (NV + 3) / 4;  // [ceil(N_ENT/128)] mass-matrix entries r, r+64: i | j << 8 (, << 16, 24)
+constexpr int N_ENT_WORDS = (N_ENT + 127) / 128;
+constexpr int TOPO_WORDS = W_ENT + N_ENT_WORDS;
+constexpr int PATH_LEN = NLEVEL - 1;
+
+struct Shared {
+  uint32_t w[TOPO_WORDS][64];
+  double quat[NB][4], pos[NB][3], ipos[NB][3], inertia[NB][6], mass[NB];
+  double hax[NHINGE][3], hpos[NHINGE][3], lo[NHINGE], hi[NHINGE], stiff[NHINGE], damp[NHINGE], arm[NHINGE];
+  double sph_pos[NSPH][3], sph_r[NSPH], gear[NACT];
+  uint8_t hinge0[NB], nhinge[NB], act_of_dof[NV];  // act_of_dof: NONE for the root dofs
+};
+
+// strict-ancestor / strict-descendant bit masks of each dof
+constexpr uint32_t anc_mask(int i) {
+  uint32_t m = 0;
+  for (int j = DOF_PARENT[i]; j >= 0; j = DOF_PARENT[j]) m |= 1u << j;
+  return m;
+}
+constexpr uint32_t desc_mask(int j) {
+  uint32_t m = 0;
+  for (int i = 0; i < NV; ++i)
+    if ((anc_mask(i) >> j) & 1u) m |= 1u << i;
+  return m;
+}
+constexpr int n_entries() {
+  int n = 0;
+  for (int i = 0; i < NV; ++i) {
+    ++n;
+    for (int j = DOF_PARENT[i]; j >= 0; j = DOF_PARENT[j]) ++n;
+  }
+  return n;
+}
+constexpr int body_depth(int b) {
+  int d = 0;
+  for (int a = BODY_PARENT[b]; a >= 0; a = BODY_PARENT[a]) ++d;
+  return d;
+}
+constexpr bool topo_fits() {
+  for (int b = 0; b < NB; ++b) {
+    if (CHILD_START[b + 1] - CHILD_START[b] > 3 || BODY_NHINGE[b] > 3 || body_depth(b) > PATH_LEN || body_depth(b) > 8) return false;
+    if (BODY_PARENT[b] >= b) return false;  // parents first
+  }
+  for (int k = 0; k < NV; ++k)
+    if (LDL_START[k + 1] - LDL_START[k] > 128) return false;
+  for (int lv = 0; lv < NLEVEL; ++lv)
+    if (LEVEL_START[lv + 1] - LEVEL_START[lv] > 64) return false;
+  return NV <= 32 && NB <= 32 && NSPH <= 64 && NACT <= 64 && NHINGE <= 32 && n_entries() <= N_ENT;
+}
+static_assert(topo_fits(), "humanoid tree exceeds the wave layout");
+
+struct MaskTable {
+  uint32_t anc[NV], desc[NV];
+};
+constexpr MaskTable make_masks() {
+  MaskTable m{};
+  for (int i = 0; i < NV; ++i) {
+    m.anc[i] = anc_mask(i);
+    m.desc[i] = desc_mask(i);
+  }
+  return m;
+}
+__device__ constexpr MaskTable MASKS = make_masks();
+
+constexpr uint32_t bytes4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return a | b << 8 | c << 16 | d << 24; }
+constexpr uint32_t nb(int v) { return v < 0 ? NONE : (uint32_t)v; }
+constexpr int hinge_body(int j) {
+  for (int b = 0; b < NB; ++b)
+    if (j >= BODY_HINGE0[b] && j < BODY_HINGE0[b] + BODY_NHINGE[b]) return b;
+  return -1;
+}
+constexpr Shared make_shared() {
+  Shared t{};
+  for (int lane = 0; lane < 64; ++lane) {
+    for (int lv = 0; lv < NLEVEL; ++lv) {
+      const int n = LEVEL_START[lv + 1] - LEVEL_START[lv];
+      uint32_t u = bytes4(NONE, NONE, NONE, NONE);
+      if (lane < n) {
+        const int b = LEVEL_BODIES[LEVEL_START[lv] + lane];
+        u = (uint32_t)b;
+        for (int c = 0; c < 3; ++c)
+          u |= (CHILD_START[b] + c < CHILD_START[b + 1] ? (uint32_t)CHILDREN[CHILD_START[b] + c] : NONE) << (8 * (c + 1));
+      }
+      t.w[W_SUB + lv][lane] = u;
+    }
+    uint32_t path[8] = {NONE, NONE, NONE, NONE, NONE, NONE, NONE, NONE};
+    if (lane < NB) {
+      const int d = body_depth(lane);
+      int a = lane;
+      for (int s = d - 1; s >= 0; --s, a = BODY_PARENT[a]) path[s] = (uint32_t)a;
+    }
+    t.w[W_PATH][lane] = bytes4(path[0], path[1], path[2], path[3]);
+    t.w[W_PATH + 1][lane] = bytes4(path[4], path[5], path[6], path[7]);
+    t.w[W_OWN][lane] = lane < NB ? bytes4((uint32_t)BODY_HINGE0[lane], (uint32_t)BODY_NHINGE[lane], (uint32_t)BODY_SPH0[lane],
+                                          (uint32_t)BODY_NSPH[lane])
+                                 : 0u;
+    t.w[W_MISC][lane] = (lane < NV ? (uint32_t)DOF_BODY[lane] : 0u) | (lane < NSPH ? (uint32_t)SPHERE_BODY[lane] : 0u) << 8 |
+                        (lane >= 32 && lane < 32 + NHINGE ? nb(BODY_PARENT[hinge_body(lane - 32)]) : 0u) << 16;
+    for (int k = 0; k < NV; ++k) {
+      uint32_t v = 0;
+      for (int h = 0; h < 2; ++h) {
+        const int pp = LDL_START[k] + lane + 64 * h;
+        const uint32_t ij = pp < LDL_START[k + 1] ? ((uint32_t)LDL_I[pp] | (uint32_t)LDL_J[pp] << 8) : (NONE | NONE << 8);
+        v |= ij << (16 * h);
+      }
+      t.w[W_PAIR + k][lane] = v;
+    }
+    for (int q = 0; q < (NV + 3) / 4; ++q) {
+      uint32_t v = 0;
+      for (int c = 0; c < 4 && 4 * q + c < NV; ++c) v |= nb(lane < 16 ? ANC[16 * (4 * q + c) + lane] : -1) << (8 * c);
+      t.w[W_KANC + q][lane] = v;
+    }
+  }
+  // mass-matrix entries, row by row (diagonal first, then the ancestors nearest first)
+  uint32_t ent[N_ENT_WORDS * 128] = {};
+  for (int r = 0; r < N_ENT_WORDS * 128; ++r) ent[r] = NONE | NONE << 8;
+  int r = 0;
+  for (int i = 0; i < NV; ++i) {
+    ent[r++] = (uint32_t)i | (uint32_t)i << 8;
+    for (int j = DOF_PARENT[i]; j >= 0; j = DOF_PARENT[j]) ent[r++] = (uint32_t)i | (uint32_t)j << 8;
+  }
+  for (int q = 0; q < N_ENT_WORDS; ++q)
+    for (int lane = 0; lane < 64; ++lane) t.w[W_ENT + q][lane] = ent[128 * q + lane] | ent[128 * q + 64 + lane] << 16;
+  for (int b = 0; b < NB; ++b) {
+    for (int i = 0; i < 4; ++i) t.quat[b][i] = BODY_QUAT[4 * b + i];
+    for (int i = 0; i < 3; ++i) {
+      t.pos[b][i] = BODY_POS[3 * b + i];
+      t.ipos[b][i] = BODY_IPOS[3 * b + i];
+    }
+    for (int i = 0; i < 6; ++i) t.inertia[b][i] = BODY_INERTIA[6 * b + i];
+    t.mass[b] = BODY_MASS[b];
+    t.hinge0[b] = (uint8_t)BODY_HINGE0[b];
+    t.nhinge[b] = (uint8_t)BODY_NHINGE[b];
+  }
+  for (int j = 0; j < NHINGE; ++j) {
+    for (int i = 0; i < 3; ++i) {
+      t.hax[j][i] = HINGE_AXIS[3 * j + i];
+      t.hpos[j][i] = HINGE_POS[3 * j + i];
+    }
+    t.lo[j] = HINGE_LO[j];
+    t.hi[j] = HINGE_HI[j];
+    t.stiff[j] = HINGE_STIFF[j];
+    t.damp[j] = HINGE_DAMP[j];
+    t.arm[j] = HINGE_ARM[j];
+  }
+  for (int s = 0; s < NSPH; ++s) {
+    for (int i = 0; i < 3; ++i) t.sph_pos[s][i] = SPHERE_POS[3 * s + i];
+    t.sph_r[s] = SPHERE_R[s];
+  }
+  for (int i = 0; i < NV; ++i) t.act_of_dof[i] = (uint8_t)NONE;
+  for (int k = 0; k < NACT; ++k) {
+    t.gear[k] = ACT_GEAR[k];
+    t.act_of_dof[ACT_DOF[k]] = (uint8_t)k;
+  }
+  return t;
+}
+__device__ constexpr Shared SHARED = make_shared();
+
+// the block's copy of SHARED (one wave per block)
+HM_INLINE void load_shared(Shared& S, int lane) {
+  static_assert(sizeof(Shared) % 8 == 0, "Shared copies as doubles");
+  const double* src = reinterpret_cast<const double*>(&SHARED);
+  double* dst = reinterpret_cast<double*>(&S);
+#pragma unroll 8
+  for (int i = lane; i < (int)(sizeof(Shared) / 8); i += 64) dst[i] = src[i];
+  WAVE_SYNC();
+}
+
+// a double broadcast from lane l (uniform) of the wave
+HM_INLINE double read_lane(double v, int l) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 
 // one env's working state (LDS, one wave)
 struct Wave {
   double s[NQ + NV + NACT];  // qpos ++ qvel ++ ctrl
-  double Qloc[NB][9], oloc[NB][3], lax[17][3], lanc[17][3];
-  double R[NB][9], xpos[NB][3], xipos[NB][3], haxis[17][3], hanchor[17][3], com[3];
+  double rot[NHINGE][9], Qloc[NB][9], oloc[NB][3], lax[NHINGE][3], lanc[NHINGE][3];
+  double R[NB][9], xpos[NB][3], xipos[NB][3], haxis[NHINGE][3], hanchor[NHINGE][3], com[3];
   double cinert[NB][10], cdof[NV][6], cdof_dot[NV][6], cvel[NB][6];
-  double fsph[NSPH][6], cfrc[NB][6], cacc[NB][6], fb[NB][6], crb[NB][10];
-  double L[NV][NV], x[NV];
+  double fsph[NSPH][6], cfrc[NB][6], fb[NB][6], crb[NB][10];
+  double F[NV][6];
+  double L[NV][NV], junk[64], x[NV];  // junk: the target of lanes with no entry (branch-free stores)
   double red[2];
 };
 
-// kinematics, com-based inertias / axes / velocities and contact forces of W.s
-__device__ inline void forward(Wave& W, int lane) {
+HM_INLINE int path_body(uint32_t p0, uint32_t p1, int s) { return (int)byte_of(s < 4 ? p0 : p1, s & 3); }
+
+// kinematics, com-based inertias / axes / velocities and contact forces of W.s.  The
+// chains down the tree (world poses, velocities) run per body along its own path from
+// the root -- every lane repeats its ancestors' arithmetic exactly, so no level needs
+// a round trip through LDS.
+HM_INLINE void forward(Wave& W, const Shared& S, int lane, int64_t* st = nullptr) {
   const double* q = W.s;
   const double* qd = W.s + NQ;
-  // each body's pose in its parent's frame (after its hinges), all bodies at once
-  if (lane >= 1 && lane < NB) {
-    const int b = lane;
-    double Q[9], o[3];
-    quat_mat(BODY_QUAT[4 * b], BODY_QUAT[4 * b + 1], BODY_QUAT[4 * b + 2], BODY_QUAT[4 * b + 3], Q);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) o[i] = BODY_POS[3 * b + i];
-    for (int j = BODY_HINGE0[b]; j < BODY_HINGE0[b] + BODY_NHINGE[b]; ++j) {
-      const double* ax = &HINGE_AXIS[3 * j];
-      const double* jp = &HINGE_POS[3 * j];
-      double ra[3], rot[9], Qn[9], rb[3];
-      mv3(Q, jp, ra);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) W.lanc[j][i] = o[i] + ra[i];
-      mv3(Q, ax, W.lax[j]);
-      double sn, cs;
-      sincos(q[7 + j], &sn, &cs);
-      axis_rot(ax, sn, cs, rot);
-      mm3(Q, rot, Qn);
-#pragma unroll
-      for (int i = 0; i < 9; ++i) Q[i] = Qn[i];
-      mv3(Q, jp, rb);
-#pragma unroll
-      for (int i = 0; i < 3; ++i) o[i] = W.lanc[j][i] - rb[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 9; ++i) W.Qloc[b][i] = Q[i];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) W.oloc[b][i] = o[i];
+  // hinge rotations (all hinges at once) and the root's orientation
+  if (lane >= 32 && lane < 32 + NHINGE) {
+    const int j = lane - 32;
+    double sn, cs;
+    sincos(q[7 + j], &sn, &cs);
+    axis_rot(S.hax[j], sn, cs, W.rot[j]);
   } else if (lane == 0) {
     const double qn = sqrt(((q[3] * q[3] + q[4] * q[4]) + q[5] * q[5]) + q[6] * q[6]);
     quat_mat(q[3] / qn, q[4] / qn, q[5] / qn, q[6] / qn, W.R[0]);
@@ -153,43 +335,91 @@ __device__ inline void forward(Wave& W, int lane) {
     W.xpos[0][2] = q[2];
   }
   WAVE_SYNC();
-  // world poses, root -> leaves (one tree level at a time)
-  for (int lv = 1; lv < NLEVEL; ++lv) {
-    const int n = LEVEL_START[lv + 1] - LEVEL_START[lv];
-    if (lane < n) {
-      const int b = LEVEL_BODIES[LEVEL_START[lv] + lane];
-      const int p = BODY_PARENT[b];
-      double off[3];
-      mm3(W.R[p], W.Qloc[b], W.R[b]);
-      mv3(W.R[p], W.oloc[b], off);
+  // each body's pose in its parent's frame (after its hinges), all bodies at once
+  if (lane >= 1 && lane < NB) {
+    const int b = lane;
+    double Q[9], o[3];
+    quat_mat(S.quat[b][0], S.quat[b][1], S.quat[b][2], S.quat[b][3], Q);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) W.xpos[b][i] = W.xpos[p][i] + off[i];
-      for (int j = BODY_HINGE0[b]; j < BODY_HINGE0[b] + BODY_NHINGE[b]; ++j) {
-        double ra[3];
-        mv3(W.R[p], W.lax[j], W.haxis[j]);
-        mv3(W.R[p], W.lanc[j], ra);
+    for (int i = 0; i < 3; ++i) o[i] = S.pos[b][i];
+    const int h0 = S.hinge0[b], nh = S.nhinge[b];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) W.hanchor[j][i] = W.xpos[p][i] + ra[i];
+    for (int c = 0; c < 3; ++c) {
+      if (c < nh) {
+        const int j = h0 + c;
+        double ra[3], Qn[9], rb[3];
+        mv3(Q, S.hpos[j], ra);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) W.lanc[j][i] = o[i] + ra[i];
+        mv3(Q, S.hax[j], W.lax[j]);
+        mm3(Q, W.rot[j], Qn);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Q[i] = Qn[i];
+        mv3(Q, S.hpos[j], rb);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) o[i] = W.lanc[j][i] - rb[i];
       }
     }
-    WAVE_SYNC();
+#pragma unroll
+    for (int i = 0; i < 9; ++i) W.Qloc[b][i] = Q[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) W.oloc[b][i] = o[i];
   }
+  WAVE_SYNC();
+  HM_STAMP(1);
+  // world poses: body `lane` composes its path from the root
+  if (lane >= 1 && lane < NB) {
+    const uint32_t p0 = S.w[W_PATH][lane], p1 = S.w[W_PATH + 1][lane];
+    double R[9], x[3];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = W.R[0][i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x[i] = W.xpos[0][i];
+#pragma unroll
+    for (int s = 0; s < PATH_LEN; ++s) {
+      const int a = path_body(p0, p1, s);
+      const bool has = a != (int)NONE;
+      const int ac = has ? a : 0;
+      double Rn[9], off[3];
+      mm3(R, W.Qloc[ac], Rn);
+      mv3(R, W.oloc[ac], off);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) x[i] = has ? x[i] + off[i] : x[i];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) R[i] = has ? Rn[i] : R[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) W.R[lane][i] = R[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) W.xpos[lane][i] = x[i];
+  }
+  WAVE_SYNC();
+  HM_STAMP(2);
+  // inertia centres (bodies) and hinge axes / anchors in the world (hinges)
   if (lane < NB) {
     double ri[3];
-    mv3(W.R[lane], &BODY_IPOS[3 * lane], ri);
+    mv3(W.R[lane], S.ipos[lane], ri);
 #pragma unroll
     for (int i = 0; i < 3; ++i) W.xipos[lane][i] = W.xpos[lane][i] + ri[i];
+  } else if (lane >= 32 && lane < 32 + NHINGE) {
+    const int j = lane - 32;
+    const int p = (int)byte_of(S.w[W_MISC][lane], 2);
+    double ra[3];
+    mv3(W.R[p], W.lax[j], W.haxis[j]);
+    mv3(W.R[p], W.lanc[j], ra);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) W.hanchor[j][i] = W.xpos[p][i] + ra[i];
   }
   WAVE_SYNC();
   if (lane < 3) {
     double acc = 0.0;
-    for (int b = 0; b < NB; ++b) acc = acc + BODY_MASS[b] * W.xipos[b][lane];
+    for (int b = 0; b < NB; ++b) acc = acc + S.mass[b] * W.xipos[b][lane];
     W.com[lane] = acc / TOTAL_MASS;
   }
   WAVE_SYNC();
   if (lane < NB) {  // cinert
     const int b = lane;
-    const double* I6 = &BODY_INERTIA[6 * b];
+    const double* I6 = S.inertia[b];
     const double Ib[9] = {I6[0], I6[3], I6[4], I6[3], I6[1], I6[5], I6[4], I6[5], I6[2]};
     double Rt[9], T[9], Iw[9], d[3];
 #pragma unroll
@@ -198,7 +428,7 @@ __device__ inline void forward(Wave& W, int lane) {
       for (int j = 0; j < 3; ++j) Rt[3 * i + j] = W.R[b][3 * j + i];
     mm3(W.R[b], Ib, T);
     mm3(T, Rt, Iw);
-    const double m = BODY_MASS[b];
+    const double m = S.mass[b];
 #pragma unroll
     for (int i = 0; i < 3; ++i) d[i] = W.xipos[b][i] - W.com[i];
     double* ci = W.cinert[b];
@@ -237,45 +467,55 @@ __device__ inline void forward(Wave& W, int lane) {
     }
   }
   WAVE_SYNC();
-  // cvel and cdof_dot (MuJoCo mj_comVel order), root -> leaves
-  if (lane == 0) {
+  HM_STAMP(3);
+  // cvel and cdof_dot (MuJoCo mj_comVel order): body `lane` accumulates its path
+  if (lane < NB) {
     double cv[6];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      W.cdof_dot[0][i] = W.cdof_dot[1][i] = W.cdof_dot[2][i] = 0.0;
-      cv[i] = 0.0 + ((W.cdof[0][i] * qd[0] + W.cdof[1][i] * qd[1]) + W.cdof[2][i] * qd[2]);
+    for (int i = 0; i < 6; ++i) cv[i] = 0.0 + ((W.cdof[0][i] * qd[0] + W.cdof[1][i] * qd[1]) + W.cdof[2][i] * qd[2]);
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) W.cdof_dot[0][i] = W.cdof_dot[1][i] = W.cdof_dot[2][i] = 0.0;
+#pragma unroll
+      for (int k = 3; k < 6; ++k) cross_motion(cv, W.cdof[k], W.cdof_dot[k]);
     }
 #pragma unroll
-    for (int k = 3; k < 6; ++k) cross_motion(cv, W.cdof[k], W.cdof_dot[k]);
+    for (int i = 0; i < 6; ++i) cv[i] = cv[i] + ((W.cdof[3][i] * qd[3] + W.cdof[4][i] * qd[4]) + W.cdof[5][i] * qd[5]);
+    const uint32_t p0 = S.w[W_PATH][lane], p1 = S.w[W_PATH + 1][lane];
 #pragma unroll
-    for (int i = 0; i < 6; ++i)
-      W.cvel[0][i] = cv[i] + ((W.cdof[3][i] * qd[3] + W.cdof[4][i] * qd[4]) + W.cdof[5][i] * qd[5]);
+    for (int s = 0; s < PATH_LEN; ++s) {
+      const int a = path_body(p0, p1, s);
+      const int ac = a == (int)NONE ? 0 : a;
+      const int h0 = S.hinge0[ac], nh = a == (int)NONE ? 0 : S.nhinge[ac];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const bool has = c < nh;
+        const int d = 6 + (has ? h0 + c : 0);
+        double cd[6], cdd[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) cd[i] = W.cdof[d][i];
+        const double qdd = qd[d];
+        cross_motion(cv, cd, cdd);
+        if (has && a == lane) {
+#pragma unroll
+          for (int i = 0; i < 6; ++i) W.cdof_dot[d][i] = cdd[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) cv[i] = has ? cv[i] + cd[i] * qdd : cv[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) W.cvel[lane][i] = cv[i];
   }
   WAVE_SYNC();
-  for (int lv = 1; lv < NLEVEL; ++lv) {
-    const int n = LEVEL_START[lv + 1] - LEVEL_START[lv];
-    if (lane < n) {
-      const int b = LEVEL_BODIES[LEVEL_START[lv] + lane];
-      double cv[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) cv[i] = W.cvel[BODY_PARENT[b]][i];
-      for (int d = 6 + BODY_HINGE0[b]; d < 6 + BODY_HINGE0[b] + BODY_NHINGE[b]; ++d) {
-        cross_motion(cv, W.cdof[d], W.cdof_dot[d]);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) cv[i] = cv[i] + W.cdof[d][i] * qd[d];
-      }
-#pragma unroll
-      for (int i = 0; i < 6; ++i) W.cvel[b][i] = cv[i];
-    }
-    WAVE_SYNC();
-  }
+  HM_STAMP(4);
   // ground contact: sphere s of body b against z = 0, at the sphere's lowest point
   if (lane < NSPH) {
     const int s = lane;
-    const int b = SPHERE_BODY[s];
-    const double r = SPHERE_R[s];
+    const int b = (int)byte_of(S.w[W_MISC][lane], 1);
+    const double r = S.sph_r[s];
     double cs[3], c[3], rel[3], wr[3], v[3], fv[3];
-    mv3(W.R[b], &SPHERE_POS[3 * s], cs);
+    mv3(W.R[b], S.sph_pos[s], cs);
 #pragma unroll
     for (int i = 0; i < 3; ++i) c[i] = W.xpos[b][i] + cs[i];
     const double pen = r - c[2];
@@ -303,59 +543,56 @@ __device__ inline void forward(Wave& W, int lane) {
   if (lane < NB) {  // per body, its spheres in order
     const int b = lane;
     double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int s = BODY_SPH0[b]; s < BODY_SPH0[b] + BODY_NSPH[b]; ++s)
+    const uint32_t own = S.w[W_OWN][lane];
+    const int s0 = (int)byte_of(own, 2), ns = (int)byte_of(own, 3);
+    for (int s = s0; s < s0 + ns; ++s)
 #pragma unroll
       for (int i = 0; i < 6; ++i) acc[i] = acc[i] + W.fsph[s][i];
 #pragma unroll
     for (int i = 0; i < 6; ++i) W.cfrc[b][i] = acc[i];
   }
   WAVE_SYNC();
+  HM_STAMP(5);
 }
 
 __device__ inline double clamp_ctrl(double c) { return c < -CTRL_LIMIT ? -CTRL_LIMIT : (c > CTRL_LIMIT ? CTRL_LIMIT : c); }
 
 // gear * clip(ctrl) at dof i (0 for the unactuated root dofs)
-__device__ inline double actuator_force(const double* ctrl, int i) {
-  double f = 0.0;
-  for (int k = 0; k < NACT; ++k)
-    if (ACT_DOF[k] == i) f = ACT_GEAR[k] * clamp_ctrl(ctrl[k]);
-  return f;
+HM_INLINE double actuator_force(const Shared& S, const double* ctrl, int i) {
+  const int k = S.act_of_dof[i];
+  return k == (int)NONE ? 0.0 : S.gear[k] * clamp_ctrl(ctrl[k]);
 }
 
 // W.x <- qdd of M qdd = qfrc_actuator + passive + limits - (bias - contact); needs forward(W)
-__device__ inline void accelerations(Wave& W, int lane) {
+HM_INLINE void accelerations(Wave& W, const Shared& S, int lane, int64_t* st = nullptr) {
   const double* q = W.s;
   const double* qd = W.s + NQ;
   const double* ctrl = W.s + NQ + NV;
-  if (lane == 0) {
+  // cacc along body `lane`'s path, then its bias force (RNEA forward pass)
+  if (lane < NB) {
+    const int b = lane;
     double ca[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0 + GRAV};
 #pragma unroll
     for (int k = 3; k < 6; ++k)
 #pragma unroll
       for (int i = 0; i < 6; ++i) ca[i] = ca[i] + W.cdof_dot[k][i] * qd[k];
+    const uint32_t p0 = S.w[W_PATH][lane], p1 = S.w[W_PATH + 1][lane];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) W.cacc[0][i] = ca[i];
-  }
-  WAVE_SYNC();
-  for (int lv = 1; lv < NLEVEL; ++lv) {
-    const int n = LEVEL_START[lv + 1] - LEVEL_START[lv];
-    if (lane < n) {
-      const int b = LEVEL_BODIES[LEVEL_START[lv] + lane];
-      double ca[6];
+    for (int s = 0; s < PATH_LEN; ++s) {
+      const int a = path_body(p0, p1, s);
+      const int ac = a == (int)NONE ? 0 : a;
+      const int h0 = S.hinge0[ac], nh = a == (int)NONE ? 0 : S.nhinge[ac];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) ca[i] = W.cacc[BODY_PARENT[b]][i];
-      for (int d = 6 + BODY_HINGE0[b]; d < 6 + BODY_HINGE0[b] + BODY_NHINGE[b]; ++d)
+      for (int c = 0; c < 3; ++c) {
+        const bool has = c < nh;
+        const int d = 6 + (has ? h0 + c : 0);
+        const double qdd = qd[d];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) ca[i] = ca[i] + W.cdof_dot[d][i] * qd[d];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) W.cacc[b][i] = ca[i];
+        for (int i = 0; i < 6; ++i) ca[i] = has ? ca[i] + W.cdof_dot[d][i] * qdd : ca[i];
+      }
     }
-    WAVE_SYNC();
-  }
-  if (lane < NB) {
-    const int b = lane;
     double Ia[6], Iv[6], cf[6];
-    mul_inert(W.cinert[b], W.cacc[b], Ia);
+    mul_inert(W.cinert[b], ca, Ia);
     mul_inert(W.cinert[b], W.cvel[b], Iv);
     cross_force(W.cvel[b], Iv, cf);
 #pragma unroll
@@ -364,79 +601,135 @@ __device__ inline void accelerations(Wave& W, int lane) {
     for (int i = 0; i < 10; ++i) W.crb[b][i] = W.cinert[b][i];
   }
   WAVE_SYNC();
+  HM_STAMP(6);
   // subtree sums, leaves -> root: a parent adds its children in descending index
+#pragma unroll 1
   for (int lv = NLEVEL - 2; lv >= 0; --lv) {
-    const int n = LEVEL_START[lv + 1] - LEVEL_START[lv];
-    if (lane < n) {
-      const int p = LEVEL_BODIES[LEVEL_START[lv] + lane];
-      for (int c = CHILD_START[p]; c < CHILD_START[p + 1]; ++c) {
-        const int ch = CHILDREN[c];
+    const uint32_t ts = S.w[W_SUB + lv][lane];
+    const int p = (int)byte_of(ts, 0);
+    if (p != (int)NONE) {
+      double f[6], c[10];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) W.fb[p][i] = W.fb[p][i] + W.fb[ch][i];
+      for (int i = 0; i < 6; ++i) f[i] = W.fb[p][i];
 #pragma unroll
-        for (int i = 0; i < 10; ++i) W.crb[p][i] = W.crb[p][i] + W.crb[ch][i];
+      for (int i = 0; i < 10; ++i) c[i] = W.crb[p][i];
+      // every child slot loads (a missing child reads the parent) so the loads batch;
+      // only existing children add
+      double fc[3][6], cc[3][10];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int ch = (int)byte_of(ts, k + 1);
+        const int chc = ch == (int)NONE ? p : ch;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) fc[k][i] = W.fb[chc][i];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) cc[k][i] = W.crb[chc][i];
       }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const bool has = byte_of(ts, k + 1) != NONE;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) f[i] = has ? f[i] + fc[k][i] : f[i];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) c[i] = has ? c[i] + cc[k][i] : c[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) W.fb[p][i] = f[i];
+#pragma unroll
+      for (int i = 0; i < 10; ++i) W.crb[p][i] = c[i];
     }
     WAVE_SYNC();
   }
-  // mass-matrix row i over its ancestors, and the generalised force
+  HM_STAMP(7);
+  // per dof i: F_i = crb(body(i)) cdof_i and the generalised force
   if (lane < NV) {
     const int i = lane;
-    double F[6];
-    mul_inert(W.crb[DOF_BODY[i]], W.cdof[i], F);
-    for (int j = i; j >= 0; j = DOF_PARENT[j]) W.L[i][j] = dot6(W.cdof[j], F);
-    if (i >= 6) W.L[i][i] = W.L[i][i] + HINGE_ARM[i - 6];
-    const double bias = dot6(W.cdof[i], W.fb[DOF_BODY[i]]);
-    double t = actuator_force(ctrl, i) - bias;
+    const int bi = (int)byte_of(S.w[W_MISC][lane], 0);
+    mul_inert(W.crb[bi], W.cdof[i], W.F[i]);
+    const double bias = dot6(W.cdof[i], W.fb[bi]);
+    double t = actuator_force(S, ctrl, i) - bias;
     if (i >= 6) {
       const int j = i - 6;
       const double qj = q[7 + j], vj = qd[i];
-      const double lo = HINGE_LO[j], hi = HINGE_HI[j];
+      const double lo = S.lo[j], hi = S.hi[j];
       const double lim = qj < lo ? KL * (lo - qj) - CL * vj : (qj > hi ? KL * (hi - qj) - CL * vj : 0.0);
-      const double passive = (-(HINGE_STIFF[j] * qj) - HINGE_DAMP[j] * vj) + lim;
+      const double passive = (-(S.stiff[j] * qj) - S.damp[j] * vj) + lim;
       t = t + passive;
     }
     W.x[i] = t;
   }
   WAVE_SYNC();
-  // L^T D L, leaves first: pivot k updates every (ancestor i, ancestor-or-self j of i)
-  // pair from its still unscaled row, then scales its row
-  for (int k = NV - 1; k >= 0; --k) {
-    const double invd = 1.0 / W.L[k][k];
-    for (int pp = LDL_START[k] + lane; pp < LDL_START[k + 1]; pp += 64) {
-      const int i = LDL_I[pp], j = LDL_J[pp];
-      W.L[i][j] = W.L[i][j] - W.L[k][i] * (W.L[k][j] * invd);
-    }
-    WAVE_SYNC();
-    int i = DOF_PARENT[k];
-    for (int a = 0; a < lane && i >= 0; ++a) i = DOF_PARENT[i];  // the lane-th ancestor
-    if (i >= 0) W.L[k][i] = W.L[k][i] * invd;
-    WAVE_SYNC();
+  HM_STAMP(8);
+  // mass-matrix entries M_ij = cdof_j . F_i (j = i or an ancestor), all lanes at once
+  double* Lf = &W.L[0][0];
+  const int junk = NV * NV + lane;  // W.junk[lane]
+#pragma unroll
+  for (int r = 0; r < 2 * N_ENT_WORDS; ++r) {
+    const uint32_t e = (S.w[W_ENT + (r >> 1)][lane] >> (16 * (r & 1))) & 0xffffu;
+    const int i = (int)(e & 0xff), j = (int)((e >> 8) & 0xff);
+    const int ic = i == (int)NONE ? 0 : i, jc = j == (int)NONE ? 0 : j;
+    const double v = dot6(W.cdof[jc], W.F[ic]);
+    Lf[i == (int)NONE ? junk : ic * NV + jc] = v;
   }
-  // L^T y = x (leaves first), D z = y, L x = z (column by column)
-  for (int i = NV - 1; i >= 0; --i) {
-    int j = DOF_PARENT[i];
-    for (int a = 0; a < lane && j >= 0; ++a) j = DOF_PARENT[j];
-    if (j >= 0) W.x[j] = W.x[j] - W.L[i][j] * W.x[i];
-    WAVE_SYNC();
-  }
-  if (lane < NV) W.x[lane] = W.x[lane] / W.L[lane][lane];
   WAVE_SYNC();
-  for (int j = 0; j < NV; ++j) {
-    const int pp = DESC_START[j] + lane;
-    if (pp < DESC_START[j + 1]) {
-      const int i = DESC[pp];
-      W.x[i] = W.x[i] - W.L[i][j] * W.x[j];
-    }
+  if (lane >= 6 && lane < NV) W.L[lane][lane] = W.L[lane][lane] + S.arm[lane - 6];
+  WAVE_SYNC();
+  HM_STAMP(9);
+  // L^T D L, leaves first: pivot k updates every (ancestor i, ancestor-or-self j of i)
+  // pair from its still unscaled row, then scales its row (reads before writes: one
+  // phase per pivot)
+  // the next pivot's table words are loaded a pivot ahead (constants: no ordering)
+  uint32_t pr = S.w[W_PAIR + NV - 1][lane];
+  uint32_t ka = S.w[W_KANC + ((NV - 1) >> 2)][lane];
+#pragma unroll 1
+  for (int k = NV - 1; k >= 0; --k) {
+    const int a = (int)byte_of(ka, k & 3);
+    const int i0 = (int)byte_of(pr, 0), j0 = (int)byte_of(pr, 1), i1 = (int)byte_of(pr, 2), j1 = (int)byte_of(pr, 3);
+    // no-entry lanes read harmless in-range elements and write their junk slot
+    const int r0 = i0 == (int)NONE ? 0 : i0, c0 = j0 == (int)NONE ? 0 : j0;
+    const int r1 = i1 == (int)NONE ? 0 : i1, c1 = j1 == (int)NONE ? 0 : j1;
+    const int ca = a == (int)NONE ? 0 : a;
+    const double lkk = W.L[k][k];
+    const double l00 = Lf[r0 * NV + c0], lk0 = Lf[k * NV + r0], lkc0 = Lf[k * NV + c0];
+    const double l11 = Lf[r1 * NV + c1], lk1 = Lf[k * NV + r1], lkc1 = Lf[k * NV + c1];
+    const double lka = Lf[k * NV + ca];
+    const int kn = k > 0 ? k - 1 : 0;
+    pr = S.w[W_PAIR + kn][lane];
+    ka = S.w[W_KANC + (kn >> 2)][lane];
+    const double invd = 1.0 / lkk;
+    const double u0 = l00 - lk0 * (lkc0 * invd);
+    const double u1 = l11 - lk1 * (lkc1 * invd);
+    const double sc = lka * invd;
+    Lf[i0 == (int)NONE ? junk : r0 * NV + c0] = u0;
+    Lf[i1 == (int)NONE ? junk : r1 * NV + c1] = u1;
+    Lf[a == (int)NONE ? junk : k * NV + ca] = sc;
     WAVE_SYNC();
   }
+  HM_STAMP(10);
+  // the solves with x in registers (lane j holds x_j), the pivot broadcast by readlane:
+  // L^T y = x (leaves first), D z = y, L x = z (column by column)
+  double x = lane < NV ? W.x[lane] : 0.0;
+  const int lr = lane < NV ? lane : 0;
+#pragma unroll 4
+  for (int i = NV - 1; i >= 0; --i) {
+    const double xi = read_lane(x, i);
+    const double y = x - W.L[i][lr] * xi;
+    x = ((MASKS.anc[i] >> lane) & 1u) ? y : x;
+  }
+  if (lane < NV) x = x / W.L[lane][lane];
+#pragma unroll 4
+  for (int j = 0; j < NV; ++j) {
+    const double xj = read_lane(x, j);
+    const double y = x - W.L[lr][j] * xj;
+    x = ((MASKS.desc[j] >> lane) & 1u) ? y : x;
+  }
+  if (lane < NV) W.x[lane] = x;
+  WAVE_SYNC();
+  HM_STAMP(11);
 }
 
-// one dt in place on W.s; returns the COM x of the state it started from
-__device__ inline double substep(Wave& W, int lane) {
-  forward(W, lane);
-  const double com_x = W.com[0];
-  accelerations(W, lane);
+// semi-implicit Euler over dt in place on W.s from the accelerations in W.x
+HM_INLINE void integrate(Wave& W, int lane) {
   double* q = W.s;
   double* qd = W.s + NQ;
   if (lane < NV) qd[lane] = qd[lane] + DT * W.x[lane];
@@ -465,12 +758,20 @@ __device__ inline double substep(Wave& W, int lane) {
     q[7 + j] = q[7 + j] + DT * qd[6 + j];
   }
   WAVE_SYNC();
+}
+
+// one dt in place on W.s; returns the COM x of the state it started from
+HM_INLINE double substep(Wave& W, const Shared& S, int lane) {
+  forward(W, S, lane);
+  const double com_x = W.com[0];
+  accelerations(W, S, lane);
+  integrate(W, lane);
   return com_x;
 }
 
 // reward and done of a step that started at COM x x_before; needs forward(W) of the
 // new state.  reward = 0.25 dx_com / dt + 5 - 0.1 |ctrl|^2 - min(0.5e-6 |cfrc_ext|^2, 10)
-__device__ inline void reward_done(Wave& W, int lane, double x_before, double& rew, bool& done) {
+HM_INLINE void reward_done(Wave& W, int lane, double x_before, double& rew, bool& done) {
   const double* ctrl = W.s + NQ + NV;
   if (lane == 0) {
     double asq = 0.0;
@@ -511,7 +812,7 @@ __device__ inline void reset(Wave& W, int lane, uint64_t seed, uint32_t gid, uin
 // the 376-d observation through out(k, value), lanes splitting the entries; needs
 // forward(W): qpos[2:] | qvel | cinert | cvel | qfrc_actuator | cfrc_ext (world: 0)
 template <class Out>
-__device__ inline void observation(const Wave& W, int lane, Out out) {
+__device__ inline void observation(const Wave& W, const Shared& S, int lane, Out out) {
   for (int k = lane; k < OBS; k += 64) {
     double v;
     if (k < 22) {
@@ -525,7 +826,7 @@ __device__ inline void observation(const Wave& W, int lane, Out out) {
       const int b = (k - 185) / 6 - 1, c = (k - 185) % 6;
       v = b < 0 ? 0.0 : W.cvel[b][c];
     } else if (k < 292) {
-      v = actuator_force(W.s + NQ + NV, k - 269);
+      v = actuator_force(S, W.s + NQ + NV, k - 269);
     } else {
       const int b = (k - 292) / 6 - 1, c = (k - 292) % 6;
       v = b < 0 ? 0.0 : W.cfrc[b][c];

@@ -1129,11 +1129,13 @@ __global__ __launch_bounds__(RB) void lrollout_act_kernel(RollArgs a, const floa
 __global__ __launch_bounds__(64) void hm_reset_kernel(RollArgs a) {
   __shared__ hm::Wave W;
   const int E = a.d.n_envs, e = blockIdx.x, lane = threadIdx.x;
+  __shared__ hm::Shared S;
+  hm::load_shared(S, lane);
   const uint32_t w = (uint32_t)a.b.env_int[E + e];
   hm::reset(W, lane, a.d.seed, (uint32_t)(a.d.env_offset + e), (uint64_t)w);
-  hm::forward(W, lane);
+  hm::forward(W, S, lane);
   double* raw = a.b.raw_obs;
-  hm::observation(W, lane, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
+  hm::observation(W, S, lane, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
   if (lane < HM_NS) a.b.env_state[(int64_t)lane * E + e] = W.s[lane];
   if (lane == 0) {
     raw[(int64_t)HM_OBS * E + e] = 0.0;
@@ -1148,6 +1150,8 @@ __global__ __launch_bounds__(64) void hm_act_kernel(RollArgs a, const float* __r
   constexpr int A = HM_ACT;
   const int E = a.d.n_envs, e = blockIdx.x, lane = threadIdx.x;
   const int64_t row = (int64_t)t * E + e;
+  __shared__ hm::Shared S;
+  hm::load_shared(S, lane);
   if (lane < HM_NS) W.s[lane] = a.b.env_state[(int64_t)lane * E + e];
   WAVE_SYNC();
   // sample (DiagGauss, core.py:432-435): a = z + sd * noise in fp32; the action is the ctrl
@@ -1162,39 +1166,75 @@ __global__ __launch_bounds__(64) void hm_act_kernel(RollArgs a, const float* __r
     W.s[HM_NQ + HM_NV + lane] = (double)av;
   }
   WAVE_SYNC();
-  double x_before = 0.0;
-  for (int k = 0; k < hm::FRAME_SKIP; ++k) {
-    const double x0 = hm::substep(W, lane);
-    if (k == 0) x_before = x0;
+  // one forward site (the kernel's code must fit the instruction cache): passes
+  // 0..FRAME_SKIP-1 are the substeps, pass FRAME_SKIP observes the new state, pass
+  // FRAME_SKIP + 1 the reset one
+  double x_before = 0.0, rew = 0.0;
+  // diagnostic stamps of block 0 (cols 0-11: phases of pass 1, 12/15 realtime and
+  // 13/14 shader clock at kernel start / end) -- never set in production
+  int64_t* st = (a.b.stamps != nullptr && blockIdx.x == 0) ? a.b.stamps + (int64_t)t * 16 : nullptr;
+  if (st != nullptr && lane == 0) {
+    st[12] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    st[13] = (int64_t)__builtin_amdgcn_s_memtime();
   }
-  hm::forward(W, lane);
-  double rew;
-  bool done;
-  hm::reward_done(W, lane, x_before, rew, done);
-  // episode bookkeeping (finish_env_step): TimeLimit => terminated, limit / horizon cut => not
-  const int ept = a.b.env_int[e];
-  const bool term = done || (ept + 1 >= EnvC<MRL_ENV_HUMANOID>::MAX_STEPS);
-  const bool last = term || (ept + 1 >= a.d.timestep_limit) || (t == a.d.horizon - 1);
-  if (lane == 0) {
-    a.b.ep_t[row] = ept;
-    a.b.rew[row] = (float)rew;
-    a.b.flags[row] = (uint8_t)((last ? 1 : 0) | (term ? 2 : 0));
-  }
-  if (last && t < a.d.horizon - 1) {
+  for (int pass = 0;; ++pass) {
+    int64_t* sp = pass == 1 ? st : nullptr;
+    if (sp != nullptr && lane == 0) sp[0] = (int64_t)__builtin_amdgcn_s_memtime();
+    hm::forward(W, S, lane, sp);
+    if (pass < hm::FRAME_SKIP) {
+      if (pass == 0) x_before = W.com[0];
+      hm::accelerations(W, S, lane, sp);
+      hm::integrate(W, lane);
+      continue;
+    }
+    if (pass > hm::FRAME_SKIP) break;
+    bool done;
+    hm::reward_done(W, lane, x_before, rew, done);
+    // episode bookkeeping (finish_env_step): TimeLimit => terminated, limit / horizon cut => not
+    const int ept = a.b.env_int[e];
+    const bool term = done || (ept + 1 >= EnvC<MRL_ENV_HUMANOID>::MAX_STEPS);
+    const bool last = term || (ept + 1 >= a.d.timestep_limit) || (t == a.d.horizon - 1);
+    if (lane == 0) {
+      a.b.ep_t[row] = ept;
+      a.b.rew[row] = (float)rew;
+      a.b.flags[row] = (uint8_t)((last ? 1 : 0) | (term ? 2 : 0));
+    }
+    if (!(last && t < a.d.horizon - 1)) {
+      if (lane == 0) a.b.env_int[e] = ept + 1;
+      break;
+    }
     const uint32_t w = (uint32_t)a.b.env_int[E + e];
     hm::reset(W, lane, a.d.seed, (uint32_t)(a.d.env_offset + e), (uint64_t)w);
-    hm::forward(W, lane);
     if (lane == 0) {
       a.b.env_int[E + e] = (int32_t)(w + 1);
       a.b.env_int[e] = 0;
     }
-  } else if (lane == 0) {
-    a.b.env_int[e] = ept + 1;
   }
   if (lane < HM_NS) a.b.env_state[(int64_t)lane * E + e] = W.s[lane];
   double* raw = a.b.raw_obs;
-  hm::observation(W, lane, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
+  hm::observation(W, S, lane, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
   if (lane == 0) raw[(int64_t)HM_OBS * E + e] = rew;
+  if (st != nullptr && lane == 0) {
+    st[14] = (int64_t)__builtin_amdgcn_s_memtime();
+    st[15] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  }
+}
+
+// Dynamic LDS padding for the wave-per-env Humanoid step: while the envs fit one wave
+// per SIMD, at most 4 blocks (waves) may share a CU, so the dispatcher cannot stack two
+// latency chains on one SIMD and leave another idle.
+static size_t hm_lds_pad(int n_envs) {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      ncu = n;
+    else
+      ncu = -1;
+  }
+  if (ncu <= 0 || n_envs > 4 * ncu) return 0;
+  constexpr size_t LDS_CU = 160 * 1024, used = sizeof(hm::Wave) + sizeof(hm::Shared), want = LDS_CU / 5 + 1024;
+  return used < want ? want - used : 0;
 }
 
 __global__ void rollout_finish_kernel(RollArgs a, int O) {
@@ -1358,7 +1398,7 @@ int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, cons
   const int D = ei.obs + 1;
   const dim3 genv((d->n_envs + 63) / 64), gpart(a.nb, (D + LCOLS - 1) / LCOLS);
   if (d->env_id == MRL_ENV_HUMANOID)
-    hipLaunchKernelGGL(hm_act_kernel, dim3(d->n_envs), dim3(64), 0, (hipStream_t)stream, a, z, logstd, t);
+    hipLaunchKernelGGL(hm_act_kernel, dim3(d->n_envs), dim3(64), hm_lds_pad(d->n_envs), (hipStream_t)stream, a, z, logstd, t);
   else if (d->env_id == MRL_ENV_CARTPOLE)
     hipLaunchKernelGGL(lrollout_act_kernel<MRL_ENV_CARTPOLE>, genv, dim3(64), 0, (hipStream_t)stream, a, z, logstd, t);
   else
