@@ -50,10 +50,10 @@ def flops_per_row(net):
     return {"fvp_jvp_rows": fwd + jvp, "fvp_vjp": vjp, "policy_forward": fwd}
 
 
-DYNAMICS = {"Hopper-v2": "hopper.xml articulated-body dynamics", "Humanoid-v2": "surrogate dynamics",
+DYNAMICS = {"Hopper-v2": "hopper.xml articulated-body dynamics", "Humanoid-v2": "humanoid.xml articulated-body dynamics",
             "CartPole-v0": "gym equations"}
 GAE_BYTES_PER_ROW = 17  # read r 4 + v 4 + flags 1, write adv 4 + ret 4
-PMC_FILE = "pmc_r01.json"
+PMC_FILE = "pmc_r02.json"
 
 
 def cpu_serial_c1(seconds=8.0, seed=0):

@@ -657,7 +657,7 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, const floa
 
 // ------------------------------------------------------------------ persistent rollout
 // The whole horizon in ONE launch (mrl_rollout_run): the nb blocks of the step kernel
-// stay resident (cooperative launch) and loop over t.  Weights, env state, episode
+// stay resident (one block per CU of the launch stream's CU set) and loop over t.  Weights, env state, episode
 // counters and the running stat live in registers for all T steps; the only cross-block
 // dependency of a step -- the Welford partials of the E raw observations (and rewards)
 // that every block merges into its copy of the running stat -- is handed off in memory
@@ -1441,8 +1441,8 @@ int64_t mrl_rollout_sync_bytes(const mrl_rollout_desc* d) {
 }
 
 // The nb blocks fit one per CU of the launch stream (its CU mask) at this kernel's
-// register use: the persistent launch may run (cooperative: HIP refuses a grid that
-// cannot be resident at once).
+// register use: the persistent launch may run (its blocks wait on each other, so the
+// whole grid must be resident at once).
 static bool persistent_fits(int nb, hipStream_t s) {
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -1480,10 +1480,16 @@ int mrl_rollout_run(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const fl
   const float* logstd = pol->head == MRL_HEAD_GAUSS ? theta + md.tls : nullptr;
   rc = hip_check(hipMemsetAsync(sync, 0, (size_t)mrl_rollout_sync_bytes(d), s), "mrl_rollout_run");
   if (rc) return rc;
-  void* args[] = {&a, &logstd, &rimage, &sync};
-  const void* fn = d->env_id == MRL_ENV_CARTPOLE ? (const void*)rollout_persistent_kernel<MRL_ENV_CARTPOLE>
-                                                 : (const void*)rollout_persistent_kernel<MRL_ENV_HOPPER>;
-  return hip_check(hipLaunchCooperativeKernel(fn, dim3(a.nb), dim3(RB), args, 0, s), "mrl_rollout_run");
+  // A plain launch: persistent_fits() guarantees one block per CU of the stream's CU
+  // set, so every block becomes resident (kernels of other streams on those CUs finish
+  // on their own), and the step hand-off polls are bounded (SPIN_LIMIT).  A cooperative
+  // launch made HIP keep a runtime-owned queue that its teardown destroyed after an
+  // attached rocprofv3 had finalised: the profiled process crashed at exit.
+  if (d->env_id == MRL_ENV_CARTPOLE)
+    hipLaunchKernelGGL(rollout_persistent_kernel<MRL_ENV_CARTPOLE>, dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync);
+  else
+    hipLaunchKernelGGL(rollout_persistent_kernel<MRL_ENV_HOPPER>, dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync);
+  return hip_check(hipGetLastError(), "mrl_rollout_run");
 }
 
 int mrl_rollout_step(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const float* theta, const float* rimage,

@@ -19,6 +19,7 @@ ROLES = [
     ("vjp_uncached", "mlp_vjp_kernel<false"),
     ("rows_surrgrad", "mlp_rows_kernel<2,"),
     ("rows_vfloss", "mlp_rows_kernel<3,"),
+    ("rollout_persistent", "rollout_persistent_kernel"),
     ("rollout_step", "rollout_step_kernel"),
     ("gae_scan", "gae_scan_kernel"),
     ("episode_stats", "episode_stats_kernel<"),
@@ -57,6 +58,8 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--horizon", type=int, default=1024,
+                    help="steps per persistent rollout launch: its bytes / horizon = the per-step rollout_step figure")
     a = ap.parse_args()
     fe = per_role(a.fetch_dir, "FETCH_SIZE")
     wr = per_role(a.write_dir, "WRITE_SIZE")
@@ -74,6 +77,10 @@ def main():
         if f and w:
             e["hbm_bytes_per_launch"] = int(round((2.0 * f[1] + w[1]) * 1024))
         out[role] = e
+    if "rollout_persistent" in out and "hbm_bytes_per_launch" in out["rollout_persistent"]:
+        out["rollout_step"] = {"note": f"rollout_persistent bytes / {a.horizon} steps (one launch runs the horizon)",
+                               "hbm_bytes_per_launch": int(round(out["rollout_persistent"]["hbm_bytes_per_launch"]
+                                                                 / a.horizon))}
     s = json.dumps(out, indent=1)
     if a.out:
         with open(a.out, "w") as fh:
