@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "env-steps/sec + TRPO-iters/sec, 4096 envs×1024 steps, 1/2/4/8 MI355X"
 PEAK_FP32_TFLOPS = 157.3     # MI355X dense FP32 (MFMA f32 == VALU rate), MI355X_MICROARCH.md
+PEAK_BF16_TFLOPS = 2500.0    # MI355X dense BF16 MFMA (no 2:1 sparsity), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec
 
 
@@ -151,6 +152,8 @@ def main():
     ap.add_argument("--cpu-envs", type=int, default=None)
     ap.add_argument("--cpu-horizon", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="MFMA operand precision of every MLP pass (fp32: the parity dtype; bf16: throughput mode)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run the VF fit in the reference order instead of beside the next rollout")
     args = ap.parse_args()
@@ -172,7 +175,8 @@ def main():
     cpu_E = args.cpu_envs or (64 if humanoid else 1024)
     cpu_T = args.cpu_horizon or (64 if humanoid else 256)
     cfg = dict(timestep_limit=env.spec.max_episode_steps, gamma=0.995, lam=0.97, max_kl=0.01, cg_damping=0.1,
-               n_envs=E, horizon=Tn, filter=1, seed=0, hid_sizes=hid, activation="tanh", use_graph=1)
+               n_envs=E, horizon=Tn, filter=1, seed=0, hid_sizes=hid, activation="tanh", use_graph=1,
+               mlp_dtype=args.dtype)
     agent = TrpoAgent(env.observation_space, env.action_space, cfg, comm=comm)
     collector = agent.make_collector(env, cfg)
     runner = IterationRunner(agent, collector, cfg, comm, pipeline=not args.no_pipeline)
@@ -216,9 +220,16 @@ def main():
     if rank != 0:
         return runner
     fpr = flops_per_row(agent.policy.net)
+    peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_FP32_TFLOPS
+    net = agent.policy.net
+    # algorithmic HBM bytes per row of the fused Fisher-product kernels: the primal
+    # activation cache (h1 + h2: 512 B fp32, 256 B bf16), the obs row, the head rows
+    cache_b = 0 if net.layered else (256 if args.dtype == "bf16" else 512)
+    row_b = cache_b + 4 * net.n_in + 4 * net.gh
     pmc = {}
     pmc_path = os.path.join(ROOT, "profiles", PMC_FILE)  # measured on the default Hopper config
-    if os.path.exists(pmc_path) and args.env == "Hopper-v2" and not agent.policy.net.layered and E == 4096 and Tn == 1024:
+    if (os.path.exists(pmc_path) and args.env == "Hopper-v2" and not agent.policy.net.layered and E == 4096
+            and Tn == 1024 and args.dtype == "fp32"):
         with open(pmc_path) as f:
             pmc = json.load(f)
     kinfo = {}
@@ -227,6 +238,9 @@ def main():
             cnt, mean_ms, tot_ms = kern[name]
             kinfo[name] = dict(launches=cnt, mean_ms=mean_ms, total_ms=tot_ms, rows_per_launch=n_local,
                                flop_per_row=fpr[name])
+            if not net.layered:
+                kinfo[name]["bytes_per_row"] = row_b
+                kinfo[name]["hbm_gbs_alg"] = row_b * n_local / (mean_ms * 1e-3) / 1e9
     if "rollout_steps" in kern:
         # one timed region per iteration around the T step launches (graph replay on the
         # rollout stream): the step-to-step mean, so it carries the inter-launch gap
@@ -235,14 +249,14 @@ def main():
                                      flop_per_row=fpr["policy_forward"], step_to_step=True)
     for name, ki in kinfo.items():
         ki["tflops"] = ki["flop_per_row"] * ki["rows_per_launch"] / (ki["mean_ms"] * 1e-3) / 1e12
-        ki["frac_fp32_mfma"] = ki["tflops"] / PEAK_FP32_TFLOPS
+        ki["frac_mfma"] = ki["tflops"] / peak
         if pmc.get(name, {}).get("hbm_bytes_per_launch"):
             ki["hbm_gbs_pmc"] = pmc[name]["hbm_bytes_per_launch"] / (ki["mean_ms"] * 1e-3) / 1e9
     # the dominant kernel = the largest device time per iteration
     dom = max(kinfo, key=lambda k: kinfo[k]["total_ms"])
     traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
-    roofline = {"bound": "mfma", "achieved": round(kinfo[dom]["tflops"], 3), "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(kinfo[dom]["tflops"] / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+    roofline = {"bound": "mfma", "achieved": round(kinfo[dom]["tflops"], 3), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(kinfo[dom]["tflops"] / peak, 4), "traffic": traffic,
                 "traffic_source": f"profiles/{PMC_FILE} (PMC FETCH_SIZE x2 + WRITE_SIZE, separate passes; "
                                   "not measured in this run)" if traffic else None,
                 "kernel": dom, "flop_per_row": kinfo[dom]["flop_per_row"],
@@ -263,14 +277,14 @@ def main():
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": K,
         "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1000, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
         "config": {"workload": f"{args.env} ({DYNAMICS[args.env]}) {E} envs x {Tn} steps per GPU, one TRPO iteration "
                                "per step (rollout+GAE+VF L-BFGS+TRPO CG/linesearch)",
                    "envs_per_gpu": E, "horizon": Tn, "global_batch": E * Tn * world, "parallelism": f"dp{world}",
                    "policy": f"{env.obs_dim}-{'-'.join(map(str, hid))}-{env.act_dim} tanh "
                              f"{'Categorical' if args.env == 'CartPole-v0' else 'DiagGauss'} "
                              f"({'layered GEMM' if agent.policy.net.layered else 'fused'} path)",
-                   "gamma": 0.995, "lam": 0.97,
+                   "mlp_dtype": args.dtype, "gamma": 0.995, "lam": 0.97,
                    "max_kl": 0.01, "cg_damping": 0.1,
                    "vf_fit_beside_next_rollout": runner.pipeline},
         "trpo_iters_per_sec": round(K / elapsed, 4),

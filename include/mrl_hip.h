@@ -121,6 +121,26 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
                 const int32_t* skip, void* stream);
 
 /* out[c] = sum_r slab[r, c] in fixed order with fp64 accumulation */
+/* bf16 throughput mode of the three fused passes above (MRL_COMPUTE_BF16,
+ * csrc/mlp_bf16.hip): same arguments and semantics, bf16 MFMA operands (weights, layer
+ * inputs, backpropagated rows) with f32 accumulation; f32 biases / tanh / head /
+ * epilogues.  `image` is the bf16 image (mrl_mlp_pack_bf16, mrl_mlp_image_words_bf16
+ * 4-byte words), `act_cache` the bf16 activation cache (mrl_act_cache_words_bf16);
+ * partial / slab buffers are sized by the _bf16 row counts.  fp32 stays the parity
+ * dtype (north_star 1e-4); bf16 is checked at a bf16 bound. */
+int64_t mrl_mlp_image_words_bf16(const mrl_mlp_desc* d);
+int64_t mrl_act_cache_words_bf16(int64_t n);
+int64_t mrl_partial_rows_bf16(int64_t n);
+int64_t mrl_slab_rows_bf16(int64_t n);
+int mrl_mlp_pack_bf16(const mrl_mlp_desc* d, const float* theta, float* image, int32_t fwd_only,
+                      const int32_t* skip, void* stream);
+int mrl_mlp_rows_bf16(const mrl_mlp_desc* d, int32_t epi, const float* theta, const float* image,
+                      const float* tangent, const float* image_t, const mrl_rows_io* io, const int32_t* skip,
+                      void* stream);
+int mrl_mlp_vjp_bf16(const mrl_mlp_desc* d, const float* image, const float* x, const int32_t* ep_t, double ts_limit,
+                     const float* ghead, int64_t n, float* slab, const float* act_cache, const int32_t* skip,
+                     void* stream);
+
 int mrl_reduce_rows_f32(const float* slab, int64_t rows, int64_t cols, float* out, const int32_t* skip, void* stream);
 int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* out, const int32_t* skip, void* stream);
 
@@ -135,6 +155,10 @@ int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* 
 #define MRL_GEMM_STORE 0  /* C = AB (+ bias)                                         */
 #define MRL_GEMM_TANH 1   /* C = tanh(AB + bias)                  Dense + tanh forward */
 #define MRL_GEMM_DTANH 2  /* C = (AB + bias) * (1 - H^2)          JVP / input-grad    */
+/* operand precision of the MFMA passes (fp32 is the parity dtype, north_star 1e-4;
+ * bf16 is the throughput mode: operands rounded to bf16 RNE, f32 accumulation) */
+#define MRL_COMPUTE_F32 0
+#define MRL_COMPUTE_BF16 1
 #define MRL_GEMM_SLAB 3   /* c + z*slab_stride = sum over K-split z of AB  (weight grads) */
 
 typedef struct {
@@ -155,7 +179,7 @@ typedef struct {
   const float* h;       /* MRL_GEMM_DTANH: [m, ldh] activations                          */
   int64_t ldh;
   int32_t splits;       /* MRL_GEMM_SLAB: requested K splits (see mrl_gemm_slab_splits)  */
-  int32_t pad_;
+  int32_t compute;      /* MRL_COMPUTE_F32 (exact f32 MFMA) | MRL_COMPUTE_BF16 (bf16 operands, f32 accumulate) */
   int64_t slab_stride;  /* MRL_GEMM_SLAB: floats between consecutive split slabs         */
 } mrl_gemm_desc;
 
@@ -270,6 +294,10 @@ typedef struct {
   int32_t filter;          /* 1: ZFilter obs (clip 5) + reward RunningStat       */
   int32_t env_offset;      /* rank * E: global env id for the RNG streams         */
   uint64_t seed;           /* Philox key                                         */
+  int32_t compute;         /* MRL_COMPUTE_*: the policy net's dtype; BF16 rounds the
+                              fused forward's W0, W1, x, h1, h2 to bf16 like
+                              mrl_mlp_rows_bf16, so rollout prob rows = update's    */
+  int32_t pad_;
 } mrl_rollout_desc;
 
 typedef struct {

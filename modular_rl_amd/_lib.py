@@ -19,6 +19,8 @@ EPI_PROB, EPI_LOSSES, EPI_SURRGRAD, EPI_VFLOSS, EPI_FVP, EPI_PPOGRAD, EPI_PPOSGD
 PPO_BLOCK_ROWS = 128
 ENV_CARTPOLE, ENV_HOPPER, ENV_HUMANOID = 0, 1, 2
 GEMM_STORE, GEMM_TANH, GEMM_DTANH, GEMM_SLAB = 0, 1, 2, 3
+COMPUTE_F32, COMPUTE_BF16 = 0, 1
+COMPUTE = {"fp32": COMPUTE_F32, "bf16": COMPUTE_BF16}
 
 vp = ctypes.c_void_p
 i32 = ctypes.c_int32
@@ -44,13 +46,13 @@ class RowsIO(ctypes.Structure):
 class GemmDesc(ctypes.Structure):
     _fields_ = [("m", i64), ("n", i64), ("k", i64), ("a", vp), ("lda", i64), ("a_trans", i32), ("ones_row", i32),
                 ("b", vp), ("ldb", i64), ("b_trans", i32), ("epilogue", i32), ("a2", vp), ("b2", vp), ("c", vp),
-                ("ldc", i64), ("bias", vp), ("h", vp), ("ldh", i64), ("splits", i32), ("pad_", i32),
+                ("ldc", i64), ("bias", vp), ("h", vp), ("ldh", i64), ("splits", i32), ("compute", i32),
                 ("slab_stride", i64)]
 
 
 class RolloutDesc(ctypes.Structure):
     _fields_ = [("env_id", i32), ("n_envs", i32), ("horizon", i32), ("timestep_limit", i32), ("filter", i32),
-                ("env_offset", i32), ("seed", ctypes.c_uint64)]
+                ("env_offset", i32), ("seed", ctypes.c_uint64), ("compute", i32), ("pad_", i32)]
 
 
 class RolloutBufs(ctypes.Structure):
@@ -71,6 +73,13 @@ SIGNATURES = {
     "mrl_slab_rows": (i64, [i64]),
     "mrl_mlp_rows": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_mlp_vjp": (i32, [vp, vp, vp, vp, f64, vp, i64, vp, vp, vp, vp]),
+    "mrl_mlp_image_words_bf16": (i64, [vp]),
+    "mrl_act_cache_words_bf16": (i64, [i64]),
+    "mrl_partial_rows_bf16": (i64, [i64]),
+    "mrl_slab_rows_bf16": (i64, [i64]),
+    "mrl_mlp_pack_bf16": (i32, [vp, vp, vp, i32, vp, vp]),
+    "mrl_mlp_rows_bf16": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, vp]),
+    "mrl_mlp_vjp_bf16": (i32, [vp, vp, vp, vp, f64, vp, i64, vp, vp, vp, vp]),
     "mrl_reduce_rows_f32": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_reduce_rows_f64": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_gemm": (i32, [vp, vp, vp]),

@@ -26,6 +26,8 @@ MLP_OPTIONS = [
     ("hid_sizes", comma_sep_ints, [64, 64], "Sizes of hidden layers of MLP"),
     ("activation", str, "tanh", "nonlinearity"),
     ("mlp_impl", str, "auto", "HIP MLP path: auto (fused 64-wide kernels when the shape allows), fused, layered"),
+    ("mlp_dtype", str, "fp32", "MFMA operand precision of every MLP pass: fp32 (exact, the parity dtype) or "
+                               "bf16 (bf16 operands, f32 accumulation: throughput mode)"),
 ]
 
 FILTER_OPTIONS = [
@@ -41,16 +43,17 @@ def make_mlps(ob_space, ac_space, cfg, comm=None, seed=0):
         raise _lib.MrlError("only activation=tanh is implemented on the HIP path")
     hid = check_hid_sizes(cfg["hid_sizes"])
     impl = cfg.get("mlp_impl", "auto")
+    dtype = cfg.get("mlp_dtype", "fp32")
     rng = np.random.default_rng(seed)
     if isinstance(ac_space, Box):
         outdim, head, probtype = ac_space.shape[0], _lib.HEAD_GAUSS, DiagGauss(ac_space.shape[0])
     else:
         outdim, head, probtype = ac_space.n, _lib.HEAD_SOFTMAX, Categorical(ac_space.n)
     nin = ob_space.shape[0]
-    net = make_net(nin, outdim, head, hid, impl=impl)
+    net = make_net(nin, outdim, head, hid, impl=impl, dtype=dtype)
     net.set_flat(glorot_init(rng, nin, outdim, head, hid))
     policy = StochPolicyMLP(net, probtype)
-    vfnet = make_net(nin + 1, 1, _lib.HEAD_LINEAR, hid, impl=impl)
+    vfnet = make_net(nin + 1, 1, _lib.HEAD_LINEAR, hid, impl=impl, dtype=dtype)
     vfnet.set_flat(glorot_init(rng, nin + 1, 1, _lib.HEAD_LINEAR, hid))
     baseline = NnVf(vfnet, cfg["timestep_limit"], dict(mixfrac=0.1), comm=comm)
     return policy, baseline

@@ -139,7 +139,8 @@ class Collector:
         self.N = self.E * self.T
         self.dev = torch.device(device)
         self.desc = _lib.RolloutDesc(env.kind, self.E, self.T, int(timestep_limit), int(filter),
-                                     self.comm.rank * self.E, int(seed) & 0xFFFFFFFFFFFFFFFF)
+                                     self.comm.rank * self.E, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                     _lib.COMPUTE[getattr(policy.net, "dtype", "fp32")], 0)
         ns = lib.mrl_env_state_doubles(env.kind)
         self.FS = int(lib.mrl_filter_doubles(env.kind))
         self.RS = int(lib.mrl_record_doubles(env.kind))

@@ -29,6 +29,10 @@
 namespace mrl {
 
 constexpr int GBM = 128, GBN = 128, GBK = 32, LDP = 36;  // LDP: LDS row pitch (floats)
+// bf16 compute (MRL_COMPUTE_BF16): the same tiles staged as bf16 (converted, RNE, on the
+// way into LDS; global operands stay fp32), pitch 40 bf16 = 80 B: the 16 rows a
+// ds_read_b128 16-lane group touches land on distinct 4-bank groups.
+constexpr int LDPB = 40;
 
 struct GemmArgs {
   int64_t M, N, K;
@@ -112,12 +116,29 @@ __device__ inline void store_tile(float* dst, const float4 (&r)[TW / 32]) {
     *reinterpret_cast<float4*>(dst + S::c_of(t, w) * LDP + S::k_of(t, w)) = r[w];
 }
 
+template <bool K_CONTIG, int TW>
+__device__ inline void store_tile_bf16(__bf16* dst, const float4 (&r)[TW / 32]) {
+  using S = Stage<K_CONTIG, TW>;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int w = 0; w < S::NV; ++w) {
+    bf16x4 v;
+    v[0] = (__bf16)r[w].x;
+    v[1] = (__bf16)r[w].y;
+    v[2] = (__bf16)r[w].z;
+    v[3] = (__bf16)r[w].w;
+    *reinterpret_cast<bf16x4*>(dst + S::c_of(t, w) * LDPB + S::k_of(t, w)) = v;
+  }
+}
+
 // BN = 128: 2x2 waves, each a 64x64 tile (2x2 MFMA tiles).  BN = 32 (narrow heads,
-// small M): 4x1 waves, each a 32x32 tile.
-template <bool AT, bool BT, int BN>
+// small M): 4x1 waves, each a 32x32 tile.  BF: bf16 operands (v_mfma_f32_32x32x16_bf16,
+// two k-steps per 32-deep tile), f32 accumulation and epilogue.
+template <bool AT, bool BT, int BN, bool BF>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
   constexpr int MI = BN == 128 ? 2 : 1, NI = BN == 128 ? 2 : 1;
-  constexpr int A_FL = GBM * LDP, B_FL = BN * LDP;
+  // tile sizes in floats (fp32) or in 4-byte words holding two bf16 (BF)
+  constexpr int A_FL = BF ? GBM * LDPB / 2 : GBM * LDP, B_FL = BF ? BN * LDPB / 2 : BN * LDP;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if (g.skip != nullptr && *g.skip != 0) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
@@ -172,10 +193,35 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
   for (int64_t t = 0; t < nt; ++t) {
     float* As = smem + (t & 1) * (A_FL + B_FL);
     float* Bs = As + A_FL;
-    store_tile<!AT, GBM>(As, ra);
-    store_tile<BT, BN>(Bs, rb);
+    if constexpr (BF) {
+      store_tile_bf16<!AT, GBM>(reinterpret_cast<__bf16*>(As), ra);
+      store_tile_bf16<BT, BN>(reinterpret_cast<__bf16*>(Bs), rb);
+    } else {
+      store_tile<!AT, GBM>(As, ra);
+      store_tile<BT, BN>(Bs, rb);
+    }
     __syncthreads();
     if (t + 1 < nt) load(t + 1);  // next tile's global loads overlap this tile's MFMAs
+    if constexpr (BF) {
+      // k-step s of lane half h: tile k = 16s + 8h + j (A and B agree, any order is valid)
+      const __bf16* Ab = reinterpret_cast<const __bf16*>(As);
+      const __bf16* Bb = reinterpret_cast<const __bf16*>(Bs);
+#pragma unroll
+      for (int ks = 0; ks < GBK / 16; ++ks) {
+        bf16x8 av[MI], bv[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+          av[mi] = *reinterpret_cast<const bf16x8*>(Ab + (wm * 32 * MI + 32 * mi + j) * LDPB + 16 * ks + 8 * h);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          bv[ni] = *reinterpret_cast<const bf16x8*>(Bb + (wn * 32 * NI + 32 * ni + j) * LDPB + 16 * ks + 8 * h);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA32B(av[mi], bv[ni], acc[mi][ni]);
+      }
+      continue;
+    }
     // MFMA k-step (u, v) of lane half h covers tile k = 16h + 4u + v (any k->step
     // assignment is valid when A and B agree): one ds_read_b128 per operand per 4 steps
 #pragma unroll
@@ -378,6 +424,7 @@ int mrl_gemm(const mrl_gemm_desc* d, const int32_t* skip, void* stream) {
   if ((d->a2 == nullptr) != (d->b2 == nullptr)) return fail(E_ARG, "mrl_gemm: a2/b2 must be both set or both null");
   if (d->epilogue < MRL_GEMM_STORE || d->epilogue > MRL_GEMM_SLAB) return fail(E_ARG, "mrl_gemm: bad epilogue");
   if (d->epilogue == MRL_GEMM_DTANH && !d->h) return fail(E_ARG, "mrl_gemm: DTANH needs h");
+  if (d->compute != MRL_COMPUTE_F32 && d->compute != MRL_COMPUTE_BF16) return fail(E_ARG, "mrl_gemm: bad compute");
   if (d->m <= 0 || d->n <= 0) return OK;
   GemmArgs g;
   g.M = d->m;
@@ -408,23 +455,34 @@ int mrl_gemm(const mrl_gemm_desc* d, const int32_t* skip, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const unsigned gm = (unsigned)((g.M + GBM - 1) / GBM);
   const int64_t wide_blocks = (g.N + GBN - 1) / GBN * (int64_t)gm * splits;
+  const bool bf = d->compute == MRL_COMPUTE_BF16;
+#define MRL_GEMM_LAUNCH(BNW, SHM)                                                                                   \
+  do {                                                                                                              \
+    const dim3 grid((unsigned)((g.N + BNW - 1) / BNW), gm, (unsigned)splits);                                       \
+    if (!d->a_trans && !d->b_trans) {                                                                               \
+      if (bf) hipLaunchKernelGGL((gemm_f32_kernel<false, false, BNW, true>), grid, dim3(256), SHM, s, g);           \
+      else hipLaunchKernelGGL((gemm_f32_kernel<false, false, BNW, false>), grid, dim3(256), SHM, s, g);             \
+    } else if (!d->a_trans && d->b_trans) {                                                                         \
+      if (bf) hipLaunchKernelGGL((gemm_f32_kernel<false, true, BNW, true>), grid, dim3(256), SHM, s, g);            \
+      else hipLaunchKernelGGL((gemm_f32_kernel<false, true, BNW, false>), grid, dim3(256), SHM, s, g);              \
+    } else if (d->a_trans && !d->b_trans) {                                                                         \
+      if (bf) hipLaunchKernelGGL((gemm_f32_kernel<true, false, BNW, true>), grid, dim3(256), SHM, s, g);            \
+      else hipLaunchKernelGGL((gemm_f32_kernel<true, false, BNW, false>), grid, dim3(256), SHM, s, g);              \
+    } else {                                                                                                        \
+      if (bf) hipLaunchKernelGGL((gemm_f32_kernel<true, true, BNW, true>), grid, dim3(256), SHM, s, g);             \
+      else hipLaunchKernelGGL((gemm_f32_kernel<true, true, BNW, false>), grid, dim3(256), SHM, s, g);               \
+    }                                                                                                               \
+  } while (0)
   if (g.N <= 32 || wide_blocks < 160) {
     // narrow 128x32 tiles: head layers (n_out <= 32) without 128-wide MFMA waste, and
     // small-M launches (the rollout's per-step forward over E rows) with 4x the blocks
-    const dim3 grid((unsigned)((g.N + 31) / 32), gm, (unsigned)splits);
-    const size_t shm = 2 * (GBM + 32) * LDP * sizeof(float);
-    if (!d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, false, 32>), grid, dim3(256), shm, s, g);
-    else if (!d->a_trans && d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, true, 32>), grid, dim3(256), shm, s, g);
-    else if (d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<true, false, 32>), grid, dim3(256), shm, s, g);
-    else hipLaunchKernelGGL((gemm_f32_kernel<true, true, 32>), grid, dim3(256), shm, s, g);
+    const size_t shm = bf ? 2 * (GBM + 32) * LDPB * sizeof(__bf16) : 2 * (GBM + 32) * LDP * sizeof(float);
+    MRL_GEMM_LAUNCH(32, shm);
   } else {
-    const dim3 grid((unsigned)((g.N + GBN - 1) / GBN), gm, (unsigned)splits);
-    const size_t shm = 2 * (GBM + GBN) * LDP * sizeof(float);
-    if (!d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, false, 128>), grid, dim3(256), shm, s, g);
-    else if (!d->a_trans && d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<false, true, 128>), grid, dim3(256), shm, s, g);
-    else if (d->a_trans && !d->b_trans) hipLaunchKernelGGL((gemm_f32_kernel<true, false, 128>), grid, dim3(256), shm, s, g);
-    else hipLaunchKernelGGL((gemm_f32_kernel<true, true, 128>), grid, dim3(256), shm, s, g);
+    const size_t shm = bf ? 2 * (GBM + GBN) * LDPB * sizeof(__bf16) : 2 * (GBM + GBN) * LDP * sizeof(float);
+    MRL_GEMM_LAUNCH(128, shm);
   }
+#undef MRL_GEMM_LAUNCH
   return hip_check(hipGetLastError(), "mrl_gemm");
 }
 

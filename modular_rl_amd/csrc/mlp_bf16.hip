@@ -1,0 +1,716 @@
+// bf16 throughput mode of the fused 64-wide MLP kernels (MRL_COMPUTE_BF16): the same
+// passes as mlp_kernels.hip (forward + row epilogues, Fisher-product JVP, VJP) on
+// v_mfma_f32_32x32x16_bf16 -- 16x the f32 MFMA rate -- with f32 accumulation.
+//
+// Rounding points (bf16 RNE): the weights W0, W1 (and the tangent's dW0, dW1), the
+// layer inputs x, h1, h2 and the backpropagated head rows / layer-2 gradients that
+// enter an MFMA.  Biases, tanh, tanh', the head layer (n_out <= 8, f32 VALU on the
+// bf16-rounded h2) and every row epilogue stay f32.  fp32 (mlp_kernels.hip) is the
+// parity dtype; this mode is checked against the fp64 oracle at a bf16 bound
+// (tests/test_gpu_bf16.py).
+//
+// Layouts.  A 32-row tile keeps activations transposed in the accumulators exactly as
+// the f32 kernels do ("F layout", D[unit][row]: row on the lane, 16 units in the
+// registers, unit = 32*mt + cperm(r, h)); the C/D layout of the bf16 MFMA is the f32
+// one.  Registers 8s'..8s'+7 of a tile, converted to bf16, are the B fragment of a
+// k-step whose k index j of lane half h is unit cperm(8s' + j, h): layers chain with
+// no data movement, the weight fragments of the image are permuted to match.
+// The weight gradients sum over rows (the lane index of an F tile), so the VJP turns
+// F tiles into "T layout" tiles D[row][unit] (unit on the lane, rows in the
+// registers) with an identity MFMA (X^T . I: exact, the values are bf16 already) and
+// feeds T tiles as both operands of X^T . Y -- no LDS transposes at all.
+//
+// Replaces the same reference functions as mlp_kernels.hip (core.py:269-270,
+// trpo.py:68-70, core.py:608, 670-671) in reduced precision.
+#include <math.h>
+
+#include "../../include/mrl_hip.h"
+#include "mlp_device.h"
+#include "rows_epilogue.h"
+
+namespace mrl {
+
+// ------------------------------------------------------------------ image layout
+// In 4-byte words.  f32 section: fb0, fb1 [mo][h][r], hv [h][o][mt*16 + r], hb -- the
+// f32 image's biases and VALU head, same order.  bf16 section: fragments of 8 bf16
+// (16 B) per lane, [frag][lane]:
+//   fa0 [mo][s0]  A[i = 32mo + l%32][k = 16 s0 + 8h + j]   = W0[k][i]          (k < O)
+//   fa1 [mo][s]   A[i = 32mo + l%32][k ~ u(s, h, j)]       = W1[u][i]
+//   bw2 [mo]      A[i = 32mo + l%32][k = 8h + j]           = W2[i][o = k]      (o < A)
+//   bt1 [no][s]   B[k ~ u(s, h, j)][col = 32no + l%32]     = W1[col][u]
+// with u(s, h, j) = 32 (s >> 1) + cperm(8 (s & 1) + j, h).
+struct BDims {
+  int O, A, KS0B;
+  int fb0, fb1, hv, hb, fa0, fa1, fwd_words, bw2, bt1, total_words;
+};
+
+__host__ __device__ constexpr BDims bf16_dims(int O, int A) {
+  BDims b{};
+  b.O = O;
+  b.A = A;
+  b.KS0B = (O + 15) / 16;
+  int o = 0;
+  b.fb0 = o; o += 64;
+  b.fb1 = o; o += 64;
+  b.hv = o; o += 2 * MAX_OUT * 32;
+  b.hb = o; o += 16;
+  b.fa0 = o; o += 2 * b.KS0B * 64 * 4;
+  b.fa1 = o; o += 2 * 4 * 64 * 4;
+  b.fwd_words = o;
+  b.bw2 = o; o += 2 * 64 * 4;
+  b.bt1 = o; o += 2 * 4 * 64 * 4;
+  b.total_words = o;
+  return b;
+}
+
+// the f32 kernels' VALU head helpers read d.hv / d.hb: point them at this image's copies
+__host__ __device__ inline MlpDims head_dims(MlpDims d, const BDims& b) {
+  d.hv = b.hv;
+  d.hb = b.hb;
+  return d;
+}
+
+__host__ __device__ inline int chain_u(int s, int h, int j) { return 32 * (s >> 1) + cperm(8 * (s & 1) + j, h); }
+
+// bf16-section element j of fragment `frag` (lane-major within the segment)
+__device__ inline float bimage_elem(const MlpDims& d, const BDims& b, const float* th, int seg, int frag, int j) {
+  const int lane = frag & 63, blk = frag >> 6, i = lane & 31, h = lane >> 5;
+  if (seg == 0) {  // fa0
+    const int mo = blk / b.KS0B, s0 = blk % b.KS0B, k = 16 * s0 + 8 * h + j;
+    return k < d.O ? th[d.tW0 + k * HID + 32 * mo + i] : 0.f;
+  } else if (seg == 1) {  // fa1
+    const int mo = blk >> 2, s = blk & 3;
+    return th[d.tW1 + chain_u(s, h, j) * HID + 32 * mo + i];
+  } else if (seg == 2) {  // bw2
+    const int o = 8 * h + j;
+    return o < d.A ? th[d.tW2 + (32 * blk + i) * d.A + o] : 0.f;
+  } else {  // bt1
+    const int no = blk >> 2, s = blk & 3;
+    return th[d.tW1 + (32 * no + i) * HID + chain_u(s, h, j)];
+  }
+}
+
+__global__ void mlp_pack_bf16_kernel(MlpDims d, BDims b, const float* __restrict__ th, float* __restrict__ image,
+                                     int words, const int32_t* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= words) return;
+  if (w < b.fa0) {
+    // f32 section: the f32 image's element at the same segment-relative position
+    int idx;
+    if (w < b.fb1) idx = d.fb0 + (w - b.fb0);
+    else if (w < b.hv) idx = d.fb1 + (w - b.fb1);
+    else if (w < b.hb) idx = d.hv + (w - b.hv);
+    else idx = d.hb + (w - b.hb);
+    image[w] = image_value(d, th, idx);
+    return;
+  }
+  int seg, rel;
+  if (w < b.fa1) { seg = 0; rel = w - b.fa0; }
+  else if (w < b.bw2) { seg = 1; rel = w - b.fa1; }
+  else if (w < b.bt1) { seg = 2; rel = w - b.bw2; }
+  else { seg = 3; rel = w - b.bt1; }
+  const int frag = rel >> 2, q = rel & 3;
+  const __bf16 lo = (__bf16)bimage_elem(d, b, th, seg, frag, 2 * q);
+  const __bf16 hi = (__bf16)bimage_elem(d, b, th, seg, frag, 2 * q + 1);
+  const uint32_t v = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+  image[w] = __uint_as_float(v);
+}
+
+// ------------------------------------------------------------------ device helpers
+__device__ inline bf16x8 frag_at(const float* img, int seg, int f, int lane) {
+  return reinterpret_cast<const bf16x8*>(img + seg)[f * 64 + lane];
+}
+
+// registers 8s'..8s'+7 of an F (or T) tile as a bf16 fragment
+__device__ inline bf16x8 pack8(const f32x16& t, int sp) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)t[8 * sp + j];
+  return r;
+}
+
+// the f32 value of every register of tile mt from its two fragments (4-fragment set)
+__device__ inline f32x16 unpack16(const bf16x8* fr, int mt) {
+  f32x16 t;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    t[j] = (float)fr[2 * mt][j];
+    t[8 + j] = (float)fr[2 * mt + 1][j];
+  }
+  return t;
+}
+
+// Identity B fragments.  Permuted (k ~ unit cperm(8s' + j, h) of an F tile): Xᵀ . I_perm
+// turns F tile X into its T tile.  Natural (k = koff + 8h + j): turns the row operand
+// A[row][k] of a k-step into the T tile D[row][k - koff ... ].
+__device__ inline bf16x8 ident_perm(int sp, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)(cperm(8 * sp + j, h) == c ? 1.f : 0.f);
+  return r;
+}
+__device__ inline bf16x8 ident_nat(int koff, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)(koff + 8 * h + j == c ? 1.f : 0.f);
+  return r;
+}
+
+// row operand of input k-step s0: x[row][16 s0 + 8h + j] (time feature via XGlobal)
+template <class XL>
+__device__ inline bf16x8 x_frag(const XL& xl, int s0, int h) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)xl(16 * s0 + 8 * h + j);
+  return r;
+}
+
+constexpr int MAX_KS0B = 2;  // n_in <= 32
+
+// acc[mo] += W0-type product over the input k-steps (fa0 segment of `img`)
+__device__ inline void layer0_b(const float* img, const BDims& b, const bf16x8* xb, int lane, f32x16* acc) {
+#pragma unroll
+  for (int s0 = 0; s0 < MAX_KS0B; ++s0) {
+    if (s0 < b.KS0B) {
+      acc[0] = MFMA32B(frag_at(img, b.fa0, 0 * b.KS0B + s0, lane), xb[s0], acc[0]);
+      acc[1] = MFMA32B(frag_at(img, b.fa0, 1 * b.KS0B + s0, lane), xb[s0], acc[1]);
+    }
+  }
+}
+
+// acc += sum_s fa1[mo][s] . src[s]  (src: 4 fragments of a 64-unit F activation)
+__device__ inline void chain_b(const float* img, const BDims& b, int mo, const bf16x8* src, int lane, f32x16& acc) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = MFMA32B(frag_at(img, b.fa1, mo * 4 + s, lane), src[s], acc);
+}
+
+// ---- primal activation cache, bf16: per 32-row tile [layer 2][s 4][lane 64] x 16 B
+// (8 KB per tile): every wave load / store instruction moves 1 KB contiguous.
+constexpr int BCACHE_TILE_WORDS = 2 * 4 * 64 * 4;
+__device__ inline void bcache_store(float* tile, int layer, int lane, const bf16x8* fr) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) reinterpret_cast<bf16x8*>(tile)[(layer * 4 + s) * 64 + lane] = fr[s];
+}
+__device__ inline void bcache_load(const float* tile, int layer, int lane, bf16x8* fr) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) fr[s] = reinterpret_cast<const bf16x8*>(tile)[(layer * 4 + s) * 64 + lane];
+}
+
+// head partials from a 32-unit tile of bf16-valued h2 (f32 VALU, the f32 kernels' head)
+// forward: h1 / h2 fragments (bf16) and, with the f32 head, z
+template <class XL>
+__device__ inline void forward_b(const float* img, const MlpDims& d, const BDims& b, const XL& xl, int lane,
+                                 bf16x8* h1b, bf16x8* h2b, float* z) {
+  const int h = lane >> 5;
+  bf16x8 xb[MAX_KS0B];
+#pragma unroll
+  for (int s0 = 0; s0 < MAX_KS0B; ++s0) xb[s0] = s0 < b.KS0B ? x_frag(xl, s0, h) : bf16x8{};
+  f32x16 a1[2];
+  a1[0] = load_bias16(img, b.fb0, 0, h);
+  a1[1] = load_bias16(img, b.fb0, 1, h);
+  layer0_b(img, b, xb, lane, a1);
+  tanh16(a1[0]);
+  tanh16(a1[1]);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) h1b[s] = pack8(a1[s >> 1], s & 1);
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) z[o] = 0.f;
+#pragma unroll
+  for (int mo = 0; mo < 2; ++mo) {
+    f32x16 a = load_bias16(img, b.fb1, mo, h);
+    chain_b(img, b, mo, h1b, lane, a);
+    tanh16(a);
+    h2b[2 * mo] = pack8(a, 0);
+    h2b[2 * mo + 1] = pack8(a, 1);
+    const f32x16 ar = unpack16(h2b, mo);
+    head_partial_mt(img, d, ar, mo, h, z);  // d = head_dims(...)
+  }
+  head_finish(img, d, z);
+}
+
+// JVP to the head from cached bf16 h1 / h2 fragments (need_z: also the primal head)
+template <class XL>
+__device__ inline void jvp_b(const float* img, const float* imt, const MlpDims& d, const BDims& b, const XL& xl,
+                             int lane, const bf16x8* h1b, const bf16x8* h2b, float* z, float* dz, bool need_z) {
+  const int h = lane >> 5;
+  bf16x8 xb[MAX_KS0B];
+#pragma unroll
+  for (int s0 = 0; s0 < MAX_KS0B; ++s0) xb[s0] = s0 < b.KS0B ? x_frag(xl, s0, h) : bf16x8{};
+  f32x16 dh[2];
+  dh[0] = load_bias16(imt, b.fb0, 0, h);
+  dh[1] = load_bias16(imt, b.fb0, 1, h);
+  layer0_b(imt, b, xb, lane, dh);
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const f32x16 h1 = unpack16(h1b, m);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dh[m][r] *= dtanh(h1[r]);
+  }
+  bf16x8 dhb[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) dhb[s] = pack8(dh[s >> 1], s & 1);
+  float dzt[MAX_OUT];
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    if (need_z) z[o] = 0.f;
+    dz[o] = 0.f;
+    dzt[o] = 0.f;
+  }
+#pragma unroll
+  for (int mo = 0; mo < 2; ++mo) {
+    f32x16 da = load_bias16(imt, b.fb1, mo, h);
+    chain_b(img, b, mo, dhb, lane, da);
+    chain_b(imt, b, mo, h1b, lane, da);
+    const f32x16 a = unpack16(h2b, mo);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) da[r] *= dtanh(a[r]);
+    if (need_z) head_partial_mt(img, d, a, mo, h, z);
+    head_partial_mt(img, d, da, mo, h, dz);
+    head_partial_mt(imt, d, a, mo, h, dzt);
+  }
+  if (need_z) head_finish(img, d, z);
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) dz[o] += dzt[o];
+  head_finish(imt, d, dz);
+}
+
+constexpr int ROWS_BLOCK_B = 256;
+constexpr int ROWS_MAX_BLOCKS_B = 2048;
+constexpr int EPI_FVP_CACHED_B = 100;
+
+template <int EPI_K>
+__global__ __launch_bounds__(ROWS_BLOCK_B, 2) void mlp_rows_bf16_kernel(RowsArgs a, BDims b,
+                                                                       const float* __restrict__ img_g,
+                                                                       const float* __restrict__ imt_g,
+                                                                       const int32_t* __restrict__ skip) {
+  constexpr bool CACHED = EPI_K == EPI_FVP_CACHED_B;
+  constexpr int EPI = CACHED ? MRL_EPI_FVP : EPI_K;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (skip != nullptr && *skip != 0) return;
+  const int fw = b.fwd_words;
+  for (int i = threadIdx.x; i < fw / 4; i += ROWS_BLOCK_B)
+    reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img_g)[i];
+  if (EPI == MRL_EPI_FVP)
+    for (int i = threadIdx.x; i < fw / 4; i += ROWS_BLOCK_B)
+      reinterpret_cast<float4*>(lds + fw)[i] = reinterpret_cast<const float4*>(imt_g)[i];
+  __syncthreads();
+  const float* img = lds;
+  const float* imt = lds + fw;
+  const MlpDims dd = head_dims(a.d, b);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int A = a.A;
+  float ls[MAX_OUT], sd[MAX_OUT], dls[MAX_OUT];
+#pragma unroll
+  for (int j = 0; j < MAX_OUT; ++j) {
+    ls[j] = (a.logstd != nullptr && j < A) ? a.logstd[j] : 0.f;
+    sd[j] = expf(ls[j]);
+    dls[j] = (a.dlogstd != nullptr && j < A) ? a.dlogstd[j] : 0.f;
+  }
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+  const int64_t ntiles = (a.n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t row = tile * 32 + (lane & 31);
+    const bool valid = row < a.n;
+    XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
+    float z[MAX_OUT], dz[MAX_OUT];
+    float* ctile = a.cache != nullptr ? a.cache + tile * BCACHE_TILE_WORDS : nullptr;
+    bf16x8 h1b[4], h2b[4];
+    if constexpr (EPI == MRL_EPI_FVP) {
+      if (CACHED) {
+        bcache_load(ctile, 0, lane, h1b);
+        bcache_load(ctile, 1, lane, h2b);
+      } else {
+        forward_b(img, dd, b, xl, lane, h1b, h2b, z);
+      }
+      jvp_b(img, imt, dd, b, xl, lane, h1b, h2b, z, dz, CACHED && a.head != MRL_HEAD_GAUSS);
+    } else {
+      forward_b(img, dd, b, xl, lane, h1b, h2b, z);
+      if (a.cache_mode == MRL_CACHE_WRITE && ctile != nullptr) {
+        bcache_store(ctile, 0, lane, h1b);
+        bcache_store(ctile, 1, lane, h2b);
+      }
+#pragma unroll
+      for (int o = 0; o < MAX_OUT; ++o) dz[o] = 0.f;
+    }
+    if constexpr (EPI == MRL_EPI_PPOSGD) {
+      __shared__ double red[4];
+      if (valid && h == 0) row_epilogue<MRL_EPI_LOSSES, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+      const double klw = wave_sum(acc1);
+      if (lane == 0) red[wave] = klw;
+      __syncthreads();
+      const double kl = ((red[0] + red[1]) + (red[2] + red[3])) * a.inv_ng;
+      RowsArgs c = a;
+      c.kl_coeff = a.kl_coeff + (kl > a.kl_cutoff ? (float)(2.0 * a.cutoff_coeff * (kl - a.kl_cutoff)) : 0.f);
+      double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+      if (valid && h == 0) row_epilogue<MRL_EPI_PPOGRAD, MAX_OUT>(c, row, z, dz, ls, sd, dls, d0, d1, d2);
+      continue;
+    } else {
+      if (!valid || h != 0) continue;
+      row_epilogue<EPI, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+    }
+  }
+  if (a.partial != nullptr) {
+    acc0 = wave_sum(acc0);
+    acc1 = wave_sum(acc1);
+    acc2 = wave_sum(acc2);
+    if (lane == 0) {
+      double* p = a.partial + ((int64_t)blockIdx.x * 4 + wave) * 4;
+      p[0] = acc0;
+      p[1] = acc1;
+      p[2] = acc2;
+      p[3] = 0.0;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ VJP
+struct VjpArgsB {
+  MlpDims d;
+  BDims b;
+  int n_obs, gh, n_sum;
+  const float* x;
+  const int32_t* ept;
+  double ts_limit;
+  int64_t n;
+  const float* ghead;
+  float* slab;
+  const float* cache;
+};
+
+// T tile of F tile mt from its fragments: D[row][unit] = sum over the two k-steps
+__device__ inline f32x16 transpose_f(const bf16x8* fr, int mt, const bf16x8* ip) {
+  f32x16 t = zero16();
+  t = MFMA32B(fr[2 * mt], ip[0], t);
+  t = MFMA32B(fr[2 * mt + 1], ip[1], t);
+  return t;
+}
+
+constexpr int VJP_MAX_BLOCKS_B = 512;
+
+// One 32-row tile per wave iteration; weight-gradient accumulators per wave, written
+// as one slab row per wave (reduced in fixed order by mrl_reduce_rows_f32).
+template <bool CACHED>
+__global__ __launch_bounds__(256, 1) void mlp_vjp_bf16_kernel(VjpArgsB a, const float* __restrict__ img_g,
+                                                             const int32_t* __restrict__ skip) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (skip != nullptr && *skip != 0) return;
+  const MlpDims& d = a.d;
+  const BDims& b = a.b;
+  for (int i = threadIdx.x; i < b.total_words / 4; i += 256)
+    reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img_g)[i];
+  __syncthreads();
+  const float* img = lds;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j32 = lane & 31;
+  const int A = d.A;
+  const bf16x8 ip[2] = {ident_perm(0, lane), ident_perm(1, lane)};
+  const bf16x8 in0 = ident_nat(0, lane), in1 = ident_nat(16, lane);
+
+  f32x16 gW2[2], gW1[2][2], gW0[2];  // T-tile products: [u2][o], [u1][u2], [in][u1]
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    gW2[m] = zero16();
+    gW0[m] = zero16();
+#pragma unroll
+    for (int n = 0; n < 2; ++n) gW1[m][n] = zero16();
+  }
+  float gb0[2] = {0.f, 0.f}, gb1[2] = {0.f, 0.f};  // per lane = unit, this half's rows
+  float gb2[MAX_OUT], gls[MAX_OUT];
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    gb2[o] = 0.f;
+    gls[o] = 0.f;
+  }
+
+  const int64_t ntiles = (a.n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t row = tile * 32 + j32;
+    const bool valid = row < a.n;
+    XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
+    bf16x8 h1b[4], h2b[4];
+    if constexpr (CACHED) {
+      const float* ct = a.cache + tile * BCACHE_TILE_WORDS;
+      bcache_load(ct, 1, lane, h2b);
+      bcache_load(ct, 0, lane, h1b);
+    } else {
+      float zz[MAX_OUT];
+      forward_b(img, head_dims(d, b), b, xl, lane, h1b, h2b, zz);
+    }
+    // head-gradient row (f32) and its bf16 operand: o = 8h + j (h = 1: zero, A <= 8)
+    const float* gr = a.ghead + (valid ? row : 0) * a.gh;
+    float g[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) g[o] = (valid && h == 0 && o < A) ? gr[o] : 0.f;
+#pragma unroll
+    for (int q = 0; q < MAX_OUT; ++q) gls[q] += (valid && h == 0 && q < a.n_sum) ? gr[A + q] : 0.f;
+    bf16x8 gB;
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+      gb2[o] += g[o];
+      gB[o] = (__bf16)g[o];
+    }
+    // gh2 = W2 . G (F layout), ga2 = gh2 (1 - h2^2)
+    bf16x8 ga2b[4];
+    f32x16 ga2T[2];
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo) {
+      f32x16 g2 = zero16();
+      g2 = MFMA32B(frag_at(img, b.bw2, mo, lane), gB, g2);
+      const f32x16 h2 = unpack16(h2b, mo);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) g2[r] *= dtanh(h2[r]);
+      ga2b[2 * mo] = pack8(g2, 0);
+      ga2b[2 * mo + 1] = pack8(g2, 1);
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      ga2T[m] = transpose_f(ga2b, m, ip);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gb1[m] += ga2T[m][r];
+    }
+    // gh1 (T layout) = ga2^T . W1^T, ga1 = gh1 (1 - h1^2)
+    f32x16 ga1T[2], h1T[2];
+#pragma unroll
+    for (int no = 0; no < 2; ++no) {
+      f32x16 t = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t = MFMA32B(ga2b[s], frag_at(img, b.bt1, no * 4 + s, lane), t);
+      h1T[no] = transpose_f(h1b, no, ip);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        t[r] *= dtanh(h1T[no][r]);
+        gb0[no] += t[r];
+      }
+      ga1T[no] = t;
+    }
+    // gW1 += H1^T GA2 (K = rows: T tiles of both)
+#pragma unroll
+    for (int m1 = 0; m1 < 2; ++m1)
+#pragma unroll
+      for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) gW1[m1][m2] = MFMA32B(pack8(h1T[m1], sp), pack8(ga2T[m2], sp), gW1[m1][m2]);
+    // gW2 += H2^T G
+    {
+      f32x16 gT = zero16();
+      gT = MFMA32B(gB, in0, gT);  // D[row][o]
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const f32x16 h2T = transpose_f(h2b, m, ip);
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) gW2[m] = MFMA32B(pack8(h2T, sp), pack8(gT, sp), gW2[m]);
+      }
+    }
+    // gW0 += X^T GA1 (x rows -> T tile D[row][in])
+    {
+      f32x16 xT = zero16();
+#pragma unroll
+      for (int s0 = 0; s0 < MAX_KS0B; ++s0)
+        if (s0 < b.KS0B) xT = MFMA32B(x_frag(xl, s0, h), s0 == 0 ? in0 : in1, xT);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) gW0[m] = MFMA32B(pack8(xT, sp), pack8(ga1T[m], sp), gW0[m]);
+    }
+  }
+
+  // per-wave partial gradient in flat theta layout; accumulator tiles are D[i][j] with
+  // j = lane & 31 and i = cperm(r, h)
+  float* out = a.slab + ((int64_t)blockIdx.x * 4 + wave) * d.P;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = cperm(r, h);
+      if (i < d.O) out[d.tW0 + i * HID + 32 * m + j32] = gW0[m][r];
+      if (j32 < A) out[d.tW2 + (32 * m + i) * A + j32] = gW2[m][r];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) out[d.tW1 + (32 * m + i) * HID + 32 * n + j32] = gW1[m][n][r];
+    }
+  // bias sums: this half's rows, then the other half's (lanes l, l ^ 32 hold one unit)
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const float s0 = gb0[m] + __shfl_xor(gb0[m], 32);
+    const float s1 = gb1[m] + __shfl_xor(gb1[m], 32);
+    if (h == 0) {
+      out[d.tb0 + 32 * m + j32] = s0;
+      out[d.tb1 + 32 * m + j32] = s1;
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    const float s = wave_sumf(gb2[o]);
+    if (lane == 0 && o < A) out[d.tb2 + o] = s;
+  }
+  for (int q = 0; q < a.n_sum; ++q) {
+    const float s = wave_sumf(gls[q]);
+    if (lane == 0) out[d.tls + q] = s;
+  }
+}
+
+}  // namespace mrl
+
+using namespace mrl;
+
+static int check_desc_b(const mrl_mlp_desc* d) {
+  if (d == nullptr) return fail(E_ARG, "null mlp desc");
+  if (d->n_hidden != HID || d->n_layers != 2)
+    return fail(E_UNSUPPORTED, "only hid_sizes=[64,64] is implemented on the fused HIP path");
+  if (d->n_in < 1 || d->n_in > MAX_IN) return fail(E_UNSUPPORTED, "n_in must be in [1, 32]");
+  if (d->n_out < 1 || d->n_out > MAX_OUT) return fail(E_UNSUPPORTED, "n_out must be in [1, 8]");
+  if (d->head < 0 || d->head > 2) return fail(E_ARG, "bad head kind");
+  if (d->head == MRL_HEAD_LINEAR && d->n_out != 1) return fail(E_ARG, "linear head needs n_out=1");
+  return OK;
+}
+
+static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+static int64_t rows_blocks_b(int64_t n) {
+  int64_t g = cdiv(cdiv(n, 32), 4);
+  if (g < 1) g = 1;
+  return g > ROWS_MAX_BLOCKS_B ? ROWS_MAX_BLOCKS_B : g;
+}
+static int64_t vjp_blocks_b(int64_t n) {
+  int64_t g = cdiv(cdiv(n, 32), 4);
+  if (g < 1) g = 1;
+  return g > VJP_MAX_BLOCKS_B ? VJP_MAX_BLOCKS_B : g;
+}
+
+extern "C" {
+
+int64_t mrl_mlp_image_words_bf16(const mrl_mlp_desc* d) {
+  if (check_desc_b(d) != OK) return -1;
+  return bf16_dims(d->n_in, d->n_out).total_words;
+}
+int64_t mrl_act_cache_words_bf16(int64_t n) { return cdiv(n, 32) * BCACHE_TILE_WORDS; }
+int64_t mrl_partial_rows_bf16(int64_t n) { return rows_blocks_b(n) * 4; }
+int64_t mrl_slab_rows_bf16(int64_t n) { return vjp_blocks_b(n) * 4; }
+
+int mrl_mlp_pack_bf16(const mrl_mlp_desc* d, const float* theta, float* image, int32_t fwd_only,
+                      const int32_t* skip, void* stream) {
+  int rc = check_desc_b(d);
+  if (rc) return rc;
+  if (!theta || !image) return fail(E_ARG, "null pointer");
+  const MlpDims m = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
+  const BDims b = bf16_dims(d->n_in, d->n_out);
+  const int words = fwd_only ? b.fwd_words : b.total_words;
+  hipLaunchKernelGGL(mlp_pack_bf16_kernel, dim3((words + 255) / 256), dim3(256), 0, (hipStream_t)stream, m, b, theta,
+                     image, words, skip);
+  return hip_check(hipGetLastError(), "mrl_mlp_pack_bf16");
+}
+
+int mrl_mlp_rows_bf16(const mrl_mlp_desc* d, int32_t epi, const float* theta, const float* image,
+                      const float* tangent, const float* image_t, const mrl_rows_io* io, const int32_t* skip,
+                      void* stream) {
+  int rc = check_desc_b(d);
+  if (rc) return rc;
+  if (!io || !image || !io->x) return fail(E_ARG, "null pointer");
+  if (io->n <= 0) return OK;
+  RowsArgs a{};
+  a.d = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
+  a.head = d->head;
+  a.n_obs = d->n_in - (io->ep_t ? 1 : 0);
+  a.gh = d->head == MRL_HEAD_GAUSS ? 2 * d->n_out : d->n_out;
+  a.A = d->n_out;
+  a.x = io->x;
+  a.ept = io->ep_t;
+  a.ts_limit = io->timestep_limit;
+  a.n = io->n;
+  a.inv_ng = io->inv_n_global;
+  a.act = io->act;
+  a.adv = io->adv;
+  a.oldprob = io->oldprob;
+  a.target = io->target;
+  a.out = io->out;
+  a.ghead = io->ghead;
+  a.partial = io->partial;
+  a.logstd = (d->head == MRL_HEAD_GAUSS && theta) ? theta + a.d.tls : nullptr;
+  a.dlogstd = (d->head == MRL_HEAD_GAUSS && tangent) ? tangent + a.d.tls : nullptr;
+  a.kl_coeff = (float)io->kl_coeff;
+  a.kl_cutoff = (float)io->kl_cutoff;
+  a.cutoff_coeff = (float)io->cutoff_coeff;
+  a.reverse_kl = io->reverse_kl;
+  a.cache = io->act_cache;
+  a.cache_mode = io->act_cache != nullptr ? io->cache_mode : 0;
+  if (a.cache_mode == MRL_CACHE_READ && epi != MRL_EPI_FVP) return fail(E_ARG, "MRL_CACHE_READ is for MRL_EPI_FVP");
+  if (a.cache_mode == MRL_CACHE_WRITE && (epi == MRL_EPI_FVP || epi == MRL_EPI_PPOSGD))
+    return fail(E_ARG, "MRL_CACHE_WRITE is for the plain forward epilogues");
+  switch (epi) {
+    case MRL_EPI_PROB:
+      if (!io->out) return fail(E_ARG, "EPI_PROB needs out");
+      if (d->head == MRL_HEAD_GAUSS && !theta) return fail(E_ARG, "DiagGauss needs theta (logstd)");
+      break;
+    case MRL_EPI_LOSSES:
+    case MRL_EPI_SURRGRAD:
+    case MRL_EPI_PPOGRAD:
+    case MRL_EPI_PPOSGD:
+      if (d->head == MRL_HEAD_LINEAR) return fail(E_ARG, "policy epilogue on a value net");
+      if (!io->act || !io->adv || !io->oldprob || !io->partial) return fail(E_ARG, "losses need act/adv/oldprob/partial");
+      if (epi != MRL_EPI_LOSSES && !io->ghead) return fail(E_ARG, "gradient epilogues need ghead");
+      if (d->head == MRL_HEAD_GAUSS && !theta) return fail(E_ARG, "DiagGauss needs theta (logstd)");
+      if (epi == MRL_EPI_PPOSGD && io->n > MRL_PPO_BLOCK_ROWS) return fail(E_ARG, "PPOSGD minibatch exceeds one block");
+      break;
+    case MRL_EPI_VFLOSS:
+      if (d->head != MRL_HEAD_LINEAR || !io->target || !io->ghead || !io->partial)
+        return fail(E_ARG, "VFLOSS needs a linear head, target, ghead, partial");
+      break;
+    case MRL_EPI_FVP:
+      if (!tangent || !image_t || !io->ghead) return fail(E_ARG, "FVP needs tangent, image_t, ghead");
+      if (d->head == MRL_HEAD_GAUSS && !theta) return fail(E_ARG, "DiagGauss needs theta (logstd)");
+      break;
+    default:
+      return fail(E_ARG, "unknown epilogue");
+  }
+  const BDims b = bf16_dims(d->n_in, d->n_out);
+  const size_t shm = (size_t)b.fwd_words * 4 * (epi == MRL_EPI_FVP ? 2 : 1);
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid(epi == MRL_EPI_PPOSGD ? 1 : rows_blocks_b(io->n)), blk(ROWS_BLOCK_B);
+  switch (epi) {
+    case MRL_EPI_PROB: hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_PROB>, grid, blk, shm, s, a, b, image, image_t, skip); break;
+    case MRL_EPI_LOSSES: hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_LOSSES>, grid, blk, shm, s, a, b, image, image_t, skip); break;
+    case MRL_EPI_SURRGRAD: hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_SURRGRAD>, grid, blk, shm, s, a, b, image, image_t, skip); break;
+    case MRL_EPI_VFLOSS: hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_VFLOSS>, grid, blk, shm, s, a, b, image, image_t, skip); break;
+    case MRL_EPI_FVP:
+      if (a.cache_mode == MRL_CACHE_READ)
+        hipLaunchKernelGGL(mlp_rows_bf16_kernel<EPI_FVP_CACHED_B>, grid, blk, shm, s, a, b, image, image_t, skip);
+      else
+        hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_FVP>, grid, blk, shm, s, a, b, image, image_t, skip);
+      break;
+    case MRL_EPI_PPOGRAD: hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_PPOGRAD>, grid, blk, shm, s, a, b, image, image_t, skip); break;
+    case MRL_EPI_PPOSGD: hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_PPOSGD>, grid, blk, shm, s, a, b, image, image_t, skip); break;
+  }
+  return hip_check(hipGetLastError(), "mrl_mlp_rows_bf16");
+}
+
+int mrl_mlp_vjp_bf16(const mrl_mlp_desc* d, const float* image, const float* x, const int32_t* ep_t, double ts_limit,
+                     const float* ghead, int64_t n, float* slab, const float* act_cache, const int32_t* skip,
+                     void* stream) {
+  int rc = check_desc_b(d);
+  if (rc) return rc;
+  if (!image || !x || !ghead || !slab) return fail(E_ARG, "null pointer");
+  if (n <= 0) return OK;
+  VjpArgsB a{};
+  a.d = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
+  a.b = bf16_dims(d->n_in, d->n_out);
+  a.n_obs = d->n_in - (ep_t ? 1 : 0);
+  a.n_sum = d->head == MRL_HEAD_GAUSS ? d->n_out : 0;
+  a.gh = d->n_out + a.n_sum;
+  a.x = x;
+  a.ept = ep_t;
+  a.ts_limit = ts_limit;
+  a.n = n;
+  a.ghead = ghead;
+  a.slab = slab;
+  a.cache = act_cache;
+  const size_t shm = (size_t)a.b.total_words * 4;
+  const dim3 grid(vjp_blocks_b(n)), blk(256);
+  if (act_cache != nullptr)
+    hipLaunchKernelGGL(mlp_vjp_bf16_kernel<true>, grid, blk, shm, (hipStream_t)stream, a, image, skip);
+  else
+    hipLaunchKernelGGL(mlp_vjp_bf16_kernel<false>, grid, blk, shm, (hipStream_t)stream, a, image, skip);
+  return hip_check(hipGetLastError(), "mrl_mlp_vjp_bf16");
+}
+
+}  // extern "C"

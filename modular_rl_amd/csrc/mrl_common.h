@@ -7,6 +7,8 @@
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 // v_mfma_f32_32x32x2_f32: exact f32 (a k-ordered fmaf chain), 64 cycles/SIMD.
 // lane l supplies A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31];
@@ -14,6 +16,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // i = (r&3) + 8*(r>>2) + 4*(l>>5).
 #define MFMA32(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
+// v_mfma_f32_32x32x16_bf16 (bf16 operands, f32 accumulate; 32 cycles/SIMD, 16x the f32
+// rate): lane l supplies A[i = l&31][k = 8(l>>5) + j] and B[k = 8(l>>5) + j][col l&31]
+// in element j; the C/D layout is the f32 form's (cperm below).
+#define MFMA32B(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
 namespace mrl {
 

@@ -174,14 +174,25 @@ __device__ inline void tanh4(f32x4& a) {
   for (int r = 0; r < 4; ++r) a[r] = tanh_fast(a[r]);
 }
 
-// head rows z[o] of the wave's 16 envs (every lane of an env's column ends with all A)
-template <int O, int A, class XL>
+// bf16 RNE round trip (the bf16 compute mode's operand rounding on the f32-input MFMA)
+__device__ inline float bf16r(float x) { return (float)(__bf16)x; }
+template <bool BF>
+__device__ inline void tanh4r(f32x4& a) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) a[r] = BF ? bf16r(tanh_fast(a[r])) : tanh_fast(a[r]);
+}
+
+// head rows z[o] of the wave's 16 envs (every lane of an env's column ends with all A).
+// BF (MRL_COMPUTE_BF16): x, h1, h2 rounded to bf16 (W0, W1 are rounded in the image),
+// the operands mlp_rows_bf16 multiplies -- the products and sums stay f32, so the prob
+// rows equal the update's bf16 forward up to f32 summation order.
+template <int O, int A, bool BF, class XL>
 __device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane, float* z, int64_t* st = nullptr) {
   constexpr RDims R = RWeights<O, A>::R;
   const int g = lane >> 4;
   float xb[R.KS0p];
 #pragma unroll
-  for (int ks = 0; ks < R.KS0p; ++ks) xb[ks] = ks < R.KS0 ? xl(4 * ks + g) : 0.f;
+  for (int ks = 0; ks < R.KS0p; ++ks) xb[ks] = ks < R.KS0 ? (BF ? bf16r(xl(4 * ks + g)) : xl(4 * ks + g)) : 0.f;
   f32x4 h1[4], h2[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
@@ -196,14 +207,14 @@ __device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane
   if (st != nullptr) st[9] = (int64_t)__builtin_amdgcn_s_memrealtime();
   // layer 1: input tile mt needs only tanh(h1[mt]): the tanh of tile mt+1 issues
   // under the MFMAs of tile mt
-  tanh4(h1[0]);
+  tanh4r<BF>(h1[0]);
 #pragma unroll
   for (int mt = 0; mt < 3; ++mt) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int mo = 0; mo < 4; ++mo) h2[mo] = MFMA16(f4get(w.a1[mo][mt], q), h1[mt][q], h2[mo]);
-    tanh4(h1[mt + 1]);
+    tanh4r<BF>(h1[mt + 1]);
   }
   if (st != nullptr) st[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
   // last input tile output-tile major: tanh + head of output tile mo issue under the
@@ -212,7 +223,7 @@ __device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane
 #pragma unroll
   for (int o = 0; o < A; ++o) acc[o] = 0.f;
   auto head_tile = [&](int mo) {
-    tanh4(h2[mo]);
+    tanh4r<BF>(h2[mo]);
 #pragma unroll
     for (int o = 0; o < A; ++o) {
       const float4 hv = w.hv[o][mo];
@@ -510,15 +521,19 @@ __global__ __launch_bounds__(RB) void rollout_reset_kernel(RollArgs a) {
 }
 
 // rollout image: rimage_value (mlp_layout.h) of every element
-__global__ void rollout_pack_kernel(RDims r, MlpDims d, const float* __restrict__ th, float* __restrict__ out) {
+__global__ void rollout_pack_kernel(RDims r, MlpDims d, const float* __restrict__ th, float* __restrict__ out,
+                                    int bf) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < r.size) out[i] = rimage_value(r, d, th, i);
+  if (i < r.size) {
+    const float v = rimage_value(r, d, th, i);
+    out[i] = (bf && i < r.b0) ? bf16r(v) : v;  // bf16 mode: the MFMA weights W0, W1
+  }
 }
 
 // One launch = step t of E envs: 4 waves x 16 envs per block, the four 16-lane rows of
 // a wave share the wave's 16 envs (split angle functions / noise / obs columns, the
 // MFMA tiles of forward16).
-template <int ENV>
+template <int ENV, bool BF>
 __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, const float* __restrict__ logstd,
                                                           const float* __restrict__ rimg, int t) {
   using EC = EnvC<ENV>;
@@ -627,7 +642,7 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, const floa
     __device__ inline float operator()(int c) const { return (valid && c < O) ? p[c] : 0.f; }
   } xl{&xt[wave][j][0], valid};
   float z[A];
-  forward16<O, A>(wt, xl, lane, z,
+  forward16<O, A, BF>(wt, xl, lane, z,
                   (a.b.stamps != nullptr && blockIdx.x == 0 && threadIdx.x == 0) ? a.b.stamps + t * 16 : nullptr);
   STAMP(4);
 
@@ -764,7 +779,7 @@ __device__ inline void reset_env_reg(const RollArgs& a, int e, double* s, uint32
   ept = 0;
 }
 
-template <int ENV>
+template <int ENV, bool BF>
 __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, const float* __restrict__ logstd,
                                                                 const float* __restrict__ rimg,
                                                                 uint32_t* __restrict__ sync) {
@@ -887,7 +902,7 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
       __device__ inline float operator()(int c) const { return (valid && c < O) ? p[c] : 0.f; }
     } xl{&xt[wave][j][0], valid};
     float z[A];
-    forward16<O, A>(wt, xl, lane, z);
+    forward16<O, A, BF>(wt, xl, lane, z);
     PSTAMP(t, 3);
     // sample + env step on every row (split angle functions); row 0 stores
     double rew = 0.0;
@@ -1288,6 +1303,7 @@ static int check_roll(const mrl_rollout_desc* d, const mrl_rollout_bufs* b) {
   if (d->env_id != MRL_ENV_CARTPOLE && d->env_id != MRL_ENV_HOPPER && d->env_id != MRL_ENV_HUMANOID)
     return fail(E_UNSUPPORTED, "unknown env_id");
   if (d->n_envs <= 0 || d->horizon <= 0 || d->timestep_limit <= 0) return fail(E_ARG, "bad sizes");
+  if (d->compute != MRL_COMPUTE_F32 && d->compute != MRL_COMPUTE_BF16) return fail(E_ARG, "bad compute");
   if (!b->env_state || !b->env_int || !b->filter_state || !b->records || !b->iteration) return fail(E_ARG, "null state");
   return OK;
 }
@@ -1430,7 +1446,7 @@ int mrl_rollout_pack(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const f
   const RDims r = rollout_dims(pol->n_in);
   const MlpDims md = mlp_dims(pol->n_in, pol->n_out, pol->head == MRL_HEAD_GAUSS);
   hipLaunchKernelGGL(rollout_pack_kernel, dim3((r.size + 255) / 256), dim3(256), 0, (hipStream_t)stream, r, md, theta,
-                     rimage);
+                     rimage, (int)(d->compute == MRL_COMPUTE_BF16));
   return hip_check(hipGetLastError(), "mrl_rollout_pack");
 }
 
@@ -1485,10 +1501,14 @@ int mrl_rollout_run(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const fl
   // on their own), and the step hand-off polls are bounded (SPIN_LIMIT).  A cooperative
   // launch made HIP keep a runtime-owned queue that its teardown destroyed after an
   // attached rocprofv3 had finalised: the profiled process crashed at exit.
-  if (d->env_id == MRL_ENV_CARTPOLE)
-    hipLaunchKernelGGL(rollout_persistent_kernel<MRL_ENV_CARTPOLE>, dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync);
-  else
-    hipLaunchKernelGGL(rollout_persistent_kernel<MRL_ENV_HOPPER>, dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync);
+  const bool bf = d->compute == MRL_COMPUTE_BF16;
+  if (d->env_id == MRL_ENV_CARTPOLE) {
+    if (bf) hipLaunchKernelGGL((rollout_persistent_kernel<MRL_ENV_CARTPOLE, true>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync);
+    else hipLaunchKernelGGL((rollout_persistent_kernel<MRL_ENV_CARTPOLE, false>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync);
+  } else {
+    if (bf) hipLaunchKernelGGL((rollout_persistent_kernel<MRL_ENV_HOPPER, true>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync);
+    else hipLaunchKernelGGL((rollout_persistent_kernel<MRL_ENV_HOPPER, false>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync);
+  }
   return hip_check(hipGetLastError(), "mrl_rollout_run");
 }
 
@@ -1506,12 +1526,15 @@ int mrl_rollout_step(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const f
   RollArgs a = make_args(d, b);
   const MlpDims md = mlp_dims(pol->n_in, pol->n_out, pol->head == MRL_HEAD_GAUSS);
   const float* logstd = pol->head == MRL_HEAD_GAUSS ? theta + md.tls : nullptr;
-  if (d->env_id == MRL_ENV_CARTPOLE)
-    hipLaunchKernelGGL(rollout_step_kernel<MRL_ENV_CARTPOLE>, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a, logstd,
-                       rimage, t);
-  else
-    hipLaunchKernelGGL(rollout_step_kernel<MRL_ENV_HOPPER>, dim3(a.nb), dim3(RB), 0, (hipStream_t)stream, a, logstd,
-                       rimage, t);
+  const bool bf = d->compute == MRL_COMPUTE_BF16;
+  hipStream_t s = (hipStream_t)stream;
+  if (d->env_id == MRL_ENV_CARTPOLE) {
+    if (bf) hipLaunchKernelGGL((rollout_step_kernel<MRL_ENV_CARTPOLE, true>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, t);
+    else hipLaunchKernelGGL((rollout_step_kernel<MRL_ENV_CARTPOLE, false>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, t);
+  } else {
+    if (bf) hipLaunchKernelGGL((rollout_step_kernel<MRL_ENV_HOPPER, true>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, t);
+    else hipLaunchKernelGGL((rollout_step_kernel<MRL_ENV_HOPPER, false>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, t);
+  }
   return hip_check(hipGetLastError(), "mrl_rollout_step");
 }
 

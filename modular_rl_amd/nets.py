@@ -42,16 +42,25 @@ def fused_ok(n_in, n_out, hid_sizes):
     return list(hid_sizes) == [HIDDEN] * N_LAYERS and n_in <= FUSED_MAX_IN and n_out <= FUSED_MAX_OUT
 
 
-def make_net(n_in, n_out, head, hid_sizes=(HIDDEN,) * N_LAYERS, impl="auto", device="cuda"):
-    """Fused 64-wide net when the shape allows it (impl="auto"), else the layered net."""
+def check_dtype(dtype):
+    if dtype not in _lib.COMPUTE:
+        raise MrlError(f"mlp dtype {dtype!r}: expected one of {sorted(_lib.COMPUTE)}")
+    return dtype
+
+
+def make_net(n_in, n_out, head, hid_sizes=(HIDDEN,) * N_LAYERS, impl="auto", device="cuda", dtype="fp32"):
+    """Fused 64-wide net when the shape allows it (impl="auto"), else the layered net.
+    dtype: MFMA operand precision of every pass -- "fp32" (exact f32 MFMA, the parity
+    dtype) or "bf16" (operands rounded to bf16, f32 accumulation: the throughput mode)."""
     hid = check_hid_sizes(hid_sizes)
+    check_dtype(dtype)
     if impl not in ("auto", "fused", "layered"):
         raise MrlError(f"mlp impl {impl!r}: expected auto, fused or layered")
     if impl == "fused" or (impl == "auto" and fused_ok(n_in, n_out, hid)):
         if not fused_ok(n_in, n_out, hid):
             raise MrlError(f"fused MLP path needs hid_sizes=[64, 64], n_in<=32, n_out<=8 (got {hid}, {n_in}, {n_out})")
-        return MlpNet(n_in, n_out, head, device=device)
-    return LayeredMlpNet(n_in, n_out, head, hid, device=device)
+        return MlpNet(n_in, n_out, head, device=device, dtype=dtype)
+    return LayeredMlpNet(n_in, n_out, head, hid, device=device, dtype=dtype)
 
 
 def glorot_init(rng, n_in, n_out, head, hid_sizes=(HIDDEN,) * N_LAYERS):
@@ -89,15 +98,20 @@ class MlpNet:
 
     layered = False
 
-    def __init__(self, n_in, n_out, head, device="cuda"):
+    def __init__(self, n_in, n_out, head, device="cuda", dtype="fp32"):
         self.lib = _lib.load(require_gpu=True)
+        self.dtype = check_dtype(dtype)
+        self.bf16 = dtype == "bf16"
+        # bf16: the _bf16 entry points (csrc/mlp_bf16.hip) with their own image / cache
+        self._sfx = "_bf16" if self.bf16 else ""
         self.desc = _lib.MlpDesc(n_in, n_out, head, HIDDEN, N_LAYERS)
         self.n_in, self.n_out, self.head = n_in, n_out, head
         P = self.lib.mrl_mlp_num_params(ctypes.byref(self.desc))
         if P < 0:
             raise MrlError(self.lib.mrl_last_error().decode())
         self.P = int(P)
-        self.image_floats = int(self.lib.mrl_mlp_image_floats(ctypes.byref(self.desc)))
+        self.image_floats = int((self.lib.mrl_mlp_image_words_bf16 if self.bf16 else self.lib.mrl_mlp_image_floats)(
+            ctypes.byref(self.desc)))
         self.device = torch.device(device)
         self.theta = torch.zeros(self.P, dtype=torch.float32, device=self.device)
         self.image = torch.zeros(self.image_floats, dtype=torch.float32, device=self.device)
@@ -125,7 +139,8 @@ class MlpNet:
             # the net's own weights change: a cached forward of the old ones is stale (raw
             # device writes to theta, e.g. mrl_adam_step, do not bump theta._version)
             self._cache_key = None
-        call("mrl_mlp_pack", ctypes.byref(self.desc), ptr(theta), ptr(image), int(fwd_only), ptr(skip), stream())
+        call("mrl_mlp_pack" + self._sfx, ctypes.byref(self.desc), ptr(theta), ptr(image), int(fwd_only), ptr(skip),
+             stream())
 
     # ---- fused passes
     def rows(self, epi, x, n, ep_t=None, timestep_limit=1.0, inv_n_global=1.0, act=None, adv=None, oldprob=None,
@@ -145,31 +160,32 @@ class MlpNet:
         io = _lib.RowsIO(ptr(x), ptr(ep_t), float(timestep_limit), int(n), float(inv_n_global), ptr(act), ptr(adv),
                          ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial), float(kl_coeff),
                          float(kl_cutoff), float(cutoff_coeff), int(reverse_kl), mode, ptr(cache))
-        call("mrl_mlp_rows", ctypes.byref(self.desc), int(epi), ptr(theta), ptr(image), ptr(tangent), ptr(image_t),
-             ctypes.byref(io), ptr(skip), stream())
+        call("mrl_mlp_rows" + self._sfx, ctypes.byref(self.desc), int(epi), ptr(theta), ptr(image), ptr(tangent),
+             ptr(image_t), ctypes.byref(io), ptr(skip), stream())
 
     def _key(self, x, n, ep_t, timestep_limit):
         return (self.theta.data_ptr(), self.theta._version, x.data_ptr(), int(n),
                 None if ep_t is None else ep_t.data_ptr(), float(timestep_limit))
 
     def _cache(self, n):
-        return self.ws.get("act_cache", int(self.lib.mrl_act_cache_floats(int(n))), torch.float32)
+        words = (self.lib.mrl_act_cache_words_bf16 if self.bf16 else self.lib.mrl_act_cache_floats)(int(n))
+        return self.ws.get("act_cache", int(words), torch.float32)
 
     def partial_rows(self, n):
-        return int(self.lib.mrl_partial_rows(int(n)))
+        return int((self.lib.mrl_partial_rows_bf16 if self.bf16 else self.lib.mrl_partial_rows)(int(n)))
 
     def vjp_flat(self, x, n, ghead, out, ep_t=None, timestep_limit=1.0, image=None, skip=None):
         """out[P] (fp32) <- sum_n J_n^T ghead_n (per-wave slab + deterministic reduce); the
         forward comes from the activation cache when the last recording pass was at
         self.theta on the same rows."""
-        rows = int(self.lib.mrl_slab_rows(int(n)))
+        rows = int((self.lib.mrl_slab_rows_bf16 if self.bf16 else self.lib.mrl_slab_rows)(int(n)))
         slab = self.ws.get("slab", rows * self.P, torch.float32)
         cache = None
         if self.use_cache and image is None and self._cache_key == self._key(x, n, ep_t, timestep_limit):
             cache = self._cache(n)
         image = self.image if image is None else image
-        call("mrl_mlp_vjp", ctypes.byref(self.desc), ptr(image), ptr(x), ptr(ep_t), float(timestep_limit),
-             ptr(ghead), int(n), ptr(slab), ptr(cache), ptr(skip), stream())
+        call("mrl_mlp_vjp" + self._sfx, ctypes.byref(self.desc), ptr(image), ptr(x), ptr(ep_t),
+             float(timestep_limit), ptr(ghead), int(n), ptr(slab), ptr(cache), ptr(skip), stream())
         call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
         return out
 
@@ -210,8 +226,10 @@ class LayeredMlpNet:
     layered = True
     SLAB_SPLITS = 64
 
-    def __init__(self, n_in, n_out, head, hid_sizes, device="cuda"):
+    def __init__(self, n_in, n_out, head, hid_sizes, device="cuda", dtype="fp32"):
         self.lib = _lib.load(require_gpu=True)
+        self.dtype = check_dtype(dtype)
+        self.compute = _lib.COMPUTE[dtype]
         if not 1 <= n_out <= MAX_OUT_LAYERED:
             raise MrlError(f"n_out={n_out}: the layered head supports 1..{MAX_OUT_LAYERED} outputs")
         if head == _lib.HEAD_LINEAR and n_out != 1:
@@ -256,7 +274,7 @@ class LayeredMlpNet:
               h=None, ldh=0, ones_row=0, splits=1, slab_stride=0, skip=None):
         g = _lib.GemmDesc(m=m, n=n, k=k, a=a, lda=lda, a_trans=a_trans, ones_row=ones_row, b=b, ldb=ldb,
                           b_trans=b_trans, epilogue=epi, a2=a2, b2=b2, c=c, ldc=ldc, bias=bias, h=h, ldh=ldh,
-                          splits=splits, slab_stride=slab_stride)
+                          splits=splits, slab_stride=slab_stride, compute=self.compute)
         call("mrl_gemm", ctypes.byref(g), ptr(skip), stream())
 
     def _input(self, x, n, ep_t, timestep_limit, name="x_time"):

@@ -1,0 +1,312 @@
+"""GPU checks of the bf16 throughput mode (MRL_COMPUTE_BF16) through the C ABI.
+
+fp32 is the parity dtype (north_star: 1e-4 relative); bf16 rounds the MFMA operands
+(weights, layer inputs, backpropagated rows) to bf16 and accumulates in f32.  Two
+bounds per pass:
+  * against a float64 numpy emulation of the SAME rounding points (bfr() below):
+    only f32 accumulation order, the tanh approximation and the rare bf16 rounding
+    flip those cause differ -> rel 3e-3 on sums over rows;
+  * against the unrounded float64 oracle: the bf16 bound, rel 3e-2 (8 significant
+    bits per operand, errors averaging over K and over rows).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import trpo_np as T
+
+pytestmark = pytest.mark.gpu
+
+BF16_EMU_RTOL = 3e-3
+BF16_ORACLE_RTOL = 3e-2
+
+
+def bfr(a):
+    """Round to bf16 (RNE) through float32, returned as float64."""
+    u = np.ascontiguousarray(np.asarray(a, dtype=np.float32)).view(np.uint32).astype(np.uint64)
+    u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return u.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+def _rel(a, b):
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+# ---- float64 emulation of csrc/mlp_bf16.hip's rounding points (fused 64-wide net)
+def emu_forward(spec, th, x):
+    (W0, W1, W2), (b0, b1, b2), _ = spec.split(th)
+    xb = bfr(x)
+    h1 = bfr(np.tanh(xb @ bfr(W0) + b0))
+    h2 = bfr(np.tanh(h1 @ bfr(W1) + b1))
+    z = h2 @ W2 + b2  # f32 VALU head on the rounded h2
+    return z, (xb, h1, h2)
+
+
+def emu_vjp(spec, th, acts, G, gls=None):
+    (W0, W1, W2), _, _ = spec.split(th)
+    xb, h1, h2 = acts
+    Gb = bfr(G)
+    ga2 = bfr((Gb @ bfr(W2).T) * (1 - h2 ** 2))
+    ga1 = (ga2 @ bfr(W1).T) * (1 - h1 ** 2)
+    out = [xb.T @ bfr(ga1), ga1.sum(0), h1.T @ ga2, ga2.sum(0), h2.T @ Gb, G.sum(0)]
+    if gls is not None:
+        out.append(gls)
+    return T.flatten(out)
+
+
+def emu_jvp(spec, th, v, acts):
+    (W0, W1, W2), _, _ = spec.split(th)
+    (dW0, dW1, dW2), (db0, db1, db2), _ = spec.split(v)
+    xb, h1, h2 = acts
+    dh1 = bfr((xb @ bfr(dW0) + db0) * (1 - h1 ** 2))
+    da2 = (dh1 @ bfr(W1) + h1 @ bfr(dW1) + db1) * (1 - h2 ** 2)
+    return da2 @ W2 + h2 @ dW2 + db2
+
+
+def _setup(head, nin, nout, N, seed):
+    rng = np.random.default_rng(seed)
+    spec = T.Spec(nin, [64, 64], nout, head)
+    th = T.mlp_init(rng, spec.shapes, head == "gauss") + 0.05 * rng.standard_normal(spec.P)
+    if head == "gauss":
+        th[-nout:] = 0.3 * rng.standard_normal(nout)
+    th = th.astype(np.float32).astype(np.float64)
+    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
+    return rng, spec, th, ob
+
+
+def _net(head, nin, nout, impl="fused"):
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import make_net
+    h = {"gauss": _lib.HEAD_GAUSS, "softmax": _lib.HEAD_SOFTMAX, "linear": _lib.HEAD_LINEAR}[head]
+    return make_net(nin, nout, h, [64, 64], impl=impl, dtype="bf16")
+
+
+def _dev(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).cuda()
+
+
+CASES = [("gauss", 11, 3), ("softmax", 4, 2), ("gauss", 17, 6), ("softmax", 20, 5)]
+
+
+@pytest.mark.parametrize("head,nin,nout", CASES)
+def test_bf16_forward_prob(head, nin, nout):
+    N = 3001
+    _, spec, th, ob = _setup(head, nin, nout, N, 0)
+    net = _net(head, nin, nout)
+    net.set_flat(th)
+    got = net.forward(_dev(ob), N).cpu().numpy().astype(np.float64)
+    z, _ = emu_forward(spec, th, ob)
+    emu = T.head_prob(spec, th, z)
+    want = T.policy_prob(spec, th, ob)
+    np.testing.assert_allclose(got, emu, rtol=BF16_EMU_RTOL, atol=1e-3)
+    assert _rel(got, want) < BF16_ORACLE_RTOL
+
+
+@pytest.mark.parametrize("head,nin,nout", CASES)
+def test_bf16_fisher_vector_product(head, nin, nout):
+    from modular_rl_amd import _lib
+    N = 4000
+    rng, spec, th, ob = _setup(head, nin, nout, N, 2)
+    v = rng.standard_normal(spec.P).astype(np.float32).astype(np.float64)
+    net = _net(head, nin, nout)
+    net.set_flat(th)
+    x, vt = _dev(ob), _dev(v)
+    imgt = torch.zeros_like(net.image)
+    net.pack(theta=vt, image=imgt, fwd_only=True)
+    ghead = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+    got = {}
+    for cached in (False, True):
+        if cached:  # a recording pass at theta writes the bf16 activation cache
+            part = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+            adv = _dev(rng.standard_normal(N))
+            prob = _dev(T.policy_prob(spec, th, ob))
+            act = _dev(rng.integers(0, nout, N), torch.int32) if head == "softmax" else _dev(ob[:, :nout] * 0.1)
+            gtmp = torch.zeros_like(ghead)
+            net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=act, adv=adv, oldprob=prob, ghead=gtmp,
+                     partial=part)
+        else:
+            net.use_cache = False
+        net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=ghead, tangent=vt, image_t=imgt)
+        fv = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+        net.vjp_flat(x, N, ghead, fv)
+        got[cached] = fv.cpu().numpy().astype(np.float64)
+        net.use_cache = True
+    # emulation: the metric rows from the emulated JVP, then the emulated VJP
+    z, acts = emu_forward(spec, th, ob)
+    dz = emu_jvp(spec, th, v, acts)
+    if head == "softmax":
+        p = T.softmax(z)
+        G = p * (dz - (p * dz).sum(1, keepdims=True)) / N
+        emu = emu_vjp(spec, th, acts, G)
+    else:
+        _, _, ls = spec.split(th)
+        _, _, dls = spec.split(v)
+        emu = emu_vjp(spec, th, acts, dz / np.exp(2 * ls)[None, :] / N, 2.0 * dls)
+    want = T.fisher_vector_product(spec, th, v, ob)
+    for cached, fv in got.items():
+        assert _rel(fv, emu) < BF16_EMU_RTOL, (cached, _rel(fv, emu))
+        assert _rel(fv, want) < BF16_ORACLE_RTOL, (cached, _rel(fv, want))
+    # the cached pass reads exactly the activations the uncached one recomputes
+    assert _rel(got[True], got[False]) < 1e-6
+
+
+@pytest.mark.parametrize("head,nin,nout", CASES[:2])
+def test_bf16_losses_and_policy_gradient(head, nin, nout):
+    from modular_rl_amd import _lib
+    N = 5000
+    rng, spec, th, ob = _setup(head, nin, nout, N, 1)
+    oldth = th + 0.01 * rng.standard_normal(spec.P)
+    oldprob = T.policy_prob(spec, oldth, ob).astype(np.float32).astype(np.float64)
+    noise = rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N)
+    act = T.sample(spec, oldprob, noise)
+    if head == "gauss":
+        act = act.astype(np.float32).astype(np.float64)
+    adv = rng.standard_normal(N).astype(np.float32).astype(np.float64)
+    net = _net(head, nin, nout)
+    net.set_flat(th)
+    x = _dev(ob)
+    a = _dev(act, torch.int32 if head == "softmax" else torch.float32)
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    ghead = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(adv), oldprob=_dev(oldprob),
+             ghead=ghead, partial=partial)
+    sums = torch.zeros(4, dtype=torch.float64, device="cuda")
+    net.reduce_partial(partial, N, sums)
+    g = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(x, N, ghead, g)
+    s = sums.cpu().numpy()
+    losses = np.array([-s[0] / N, s[1] / N, s[2] / N])
+    want = T.surr_kl_ent(spec, th, ob, act, adv, oldprob)
+    np.testing.assert_allclose(losses, want, rtol=BF16_ORACLE_RTOL, atol=2e-3)
+    # gradient: the emulated VJP of the kernel's own head rows, and the oracle
+    z, acts = emu_forward(spec, th, ob)
+    gh = ghead.cpu().numpy().astype(np.float64).reshape(N, -1)
+    if head == "softmax":
+        emu = emu_vjp(spec, th, acts, gh)
+    else:
+        emu = emu_vjp(spec, th, acts, gh[:, :nout], gh[:, nout:].sum(0))
+    assert _rel(g.cpu().numpy(), emu) < BF16_EMU_RTOL
+    assert _rel(g.cpu().numpy(), T.policy_gradient(spec, th, ob, act, adv, oldprob)) < 5e-2
+
+
+def test_bf16_value_loss_grad_with_time_feature():
+    from modular_rl_amd import _lib
+    N, nin, limit = 3000, 12, 200.0
+    rng = np.random.default_rng(3)
+    spec = T.Spec(nin, [64, 64], 1, "linear")
+    th = (T.mlp_init(rng, spec.shapes, False) + 0.05 * rng.standard_normal(spec.P)).astype(np.float32)
+    th = th.astype(np.float64)
+    ob = rng.standard_normal((N, nin - 1)).astype(np.float32).astype(np.float64)
+    ept = rng.integers(0, 200, N)
+    X = np.concatenate([ob, (ept / limit)[:, None]], axis=1)
+    y = rng.standard_normal(N).astype(np.float32).astype(np.float64)
+    net = _net("linear", nin, 1)
+    net.set_flat(th)
+    x, et = _dev(ob), _dev(ept, torch.int32)
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    ghead = torch.zeros(N, dtype=torch.float32, device="cuda")
+    net.rows(_lib.EPI_VFLOSS, x, N, ep_t=et, timestep_limit=limit, inv_n_global=1.0 / N, target=_dev(y),
+             ghead=ghead, partial=partial)
+    g = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(x, N, ghead, g, ep_t=et, timestep_limit=limit)
+    z, acts = emu_forward(spec, th, X)
+    emu = emu_vjp(spec, th, acts, 2.0 * (z - y[:, None]) / N)
+    _, want_g, _, _ = T.vf_loss_grad(spec, th, X, y)
+    want_g = want_g - 2.0 * T.VF_L2 * th  # the kernel's part: the MSE gradient (L2 is added on the host)
+    assert _rel(g.cpu().numpy(), emu) < BF16_EMU_RTOL
+    assert _rel(g.cpu().numpy(), want_g) < BF16_ORACLE_RTOL
+
+
+def test_bf16_gemm_exact_on_rounded_operands():
+    """mrl_gemm with MRL_COMPUTE_BF16 == the float64 product of the bf16-rounded
+    operands up to f32 accumulation (all four orientations, K tail, both tile widths)."""
+    import ctypes
+
+    from modular_rl_amd import _lib
+    from modular_rl_amd._lib import call, stream
+    rng = np.random.default_rng(7)
+    for (M, N, K) in [(300, 200, 77), (1000, 24, 512), (64, 512, 130)]:
+        for at in (0, 1):
+            for bt in (0, 1):
+                A = rng.standard_normal((K, M) if at else (M, K)).astype(np.float32)
+                B = rng.standard_normal((N, K) if bt else (K, N)).astype(np.float32)
+                C = torch.zeros(M * N, dtype=torch.float32, device="cuda")
+                dA, dB = _dev(A), _dev(B)
+                g = _lib.GemmDesc(m=M, n=N, k=K, a=ctypes.c_void_p(dA.data_ptr()), lda=A.shape[1], a_trans=at,
+                                  b=ctypes.c_void_p(dB.data_ptr()), ldb=B.shape[1], b_trans=bt,
+                                  epilogue=_lib.GEMM_STORE, c=ctypes.c_void_p(C.data_ptr()), ldc=N,
+                                  compute=_lib.COMPUTE_BF16)
+                call("mrl_gemm", ctypes.byref(g), None, stream())
+                opA = bfr(A.T if at else A)
+                opB = bfr(B.T if bt else B)
+                want = opA @ opB
+                got = C.cpu().numpy().reshape(M, N).astype(np.float64)
+                err = np.abs(got - want).max() / np.abs(want).max()
+                assert err < 1e-5, (M, N, K, at, bt, err)
+
+
+@pytest.mark.parametrize("head,nin,nout", [("gauss", 40, 9), ("softmax", 30, 4)])
+def test_bf16_layered_fvp_and_gradient(head, nin, nout):
+    """Layered GEMM path (hid 96,80) in bf16: Fisher product and gradient at the bf16 bound."""
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import make_net
+    N = 3000
+    rng = np.random.default_rng(11)
+    hid = [96, 80]
+    spec = T.Spec(nin, hid, nout, head)
+    th = (T.mlp_init(rng, spec.shapes, head == "gauss") + 0.05 * rng.standard_normal(spec.P)).astype(np.float32)
+    th = th.astype(np.float64)
+    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
+    h = _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX
+    net = make_net(nin, nout, h, hid, impl="layered", dtype="bf16")
+    net.set_flat(th)
+    v = rng.standard_normal(spec.P).astype(np.float32).astype(np.float64)
+    x, vt = _dev(ob), _dev(v)
+    ghead = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+    net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=ghead, tangent=vt)
+    fv = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(x, N, ghead, fv)
+    want = T.fisher_vector_product(spec, th, v, ob)
+    assert _rel(fv.cpu().numpy(), want) < BF16_ORACLE_RTOL
+
+
+@pytest.mark.parametrize("env_id", ["CartPole-v0", "Hopper-v2"])
+def test_bf16_rollout_prob_rows_equal_update_forward(env_id):
+    """bf16 mode: the rollout's fused forward rounds W0, W1, x, h1, h2 like
+    mrl_mlp_rows_bf16, so the prob rows it stores (the update's oldprob) equal the
+    update's own bf16 forward on the stored observations up to f32 summation order."""
+    from modular_rl_amd.agentzoo import TrpoAgent
+    from modular_rl_amd.envs import make
+    env = make(env_id)
+    cfg = dict(timestep_limit=env.spec.max_episode_steps, n_envs=256, horizon=32, seed=5, mlp_dtype="bf16")
+    agent = TrpoAgent(env.observation_space, env.action_space, cfg)
+    net = agent.policy.net
+    assert net.dtype == "bf16"
+    col = agent.make_collector(env, cfg)
+    b = col.collect()
+    got = b.prob.reshape(b.n, -1)
+    fwd = net.forward(b.obs, b.n).reshape(b.n, -1)
+    err = (got - fwd).abs().max().item() / fwd.abs().max().item()
+    assert err < 2e-5, err
+    # and the fp32 policy's rows differ from them at bf16 scale (the rounding is real)
+    net32 = agent.baseline.net.__class__(net.n_in, net.n_out, net.head)
+    net32.set_flat(net.get_flat())
+    d32 = (net32.forward(b.obs, b.n).reshape(b.n, -1) - fwd).abs().max().item() / fwd.abs().max().item()
+    assert d32 > 1e-4, d32
+
+
+def test_bf16_trpo_learns_cartpole():
+    """C2's throughput mode end to end: TRPO with every MLP pass in bf16 still learns."""
+    from modular_rl_amd.agentzoo import TrpoAgent
+    from modular_rl_amd.core import run_policy_gradient_algorithm
+    from modular_rl_amd.envs import make
+    env = make("CartPole-v0")
+    cfg = dict(timestep_limit=env.spec.max_episode_steps, gamma=0.99, lam=0.97, max_kl=0.01, cg_damping=0.1,
+               n_envs=128, horizon=200, seed=1, n_iter=12, mlp_dtype="bf16")
+    agent = TrpoAgent(env.observation_space, env.action_space, cfg)
+    assert agent.policy.net.dtype == "bf16" and agent.baseline.net.dtype == "bf16"
+    seen = []
+    run_policy_gradient_algorithm(env, agent, usercfg=cfg, callback=seen.append)
+    assert len(seen) == 12
+    assert all(s["pol_kl_after"] <= 2.0 * 0.01 for s in seen)
+    assert seen[-1]["EpRewMean"] > 1.5 * seen[0]["EpRewMean"], (seen[0]["EpRewMean"], seen[-1]["EpRewMean"])
