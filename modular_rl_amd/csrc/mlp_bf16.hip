@@ -388,15 +388,32 @@ __device__ inline f32x16 transpose_f(const bf16x8* fr, int mt, const bf16x8* ip)
   return t;
 }
 
-constexpr int VJP_MAX_BLOCKS_B = 512;
+constexpr int VJP_MAX_BLOCKS_B = 256;  // one block (4 waves) per CU at one wave per SIMD
 
-// One 32-row tile per wave iteration; weight-gradient accumulators per wave, written
-// as one slab row per wave (reduced in fixed order by mrl_reduce_rows_f32).
-template <bool CACHED>
-__global__ __launch_bounds__(256, 1) void mlp_vjp_bf16_kernel(VjpArgsB a, const float* __restrict__ img_g,
+// SH != 0: a static shape of mlp_layout.h (plain rows), every dimension a constant
+template <int SH>
+__device__ inline VjpArgsB vjp_shape_b(const VjpArgsB& in) {
+  VjpArgsB a = in;
+  if constexpr (SH != 0) {
+    constexpr StaticShape S = STATIC_SHAPES[SH];
+    a.d = static_dims(SH);
+    a.b = bf16_dims(S.O, S.A);
+    a.n_obs = S.O;
+    a.n_sum = S.head == MRL_HEAD_GAUSS ? S.A : 0;
+    a.gh = S.A + a.n_sum;
+    a.ept = nullptr;
+  }
+  return a;
+}
+
+// Weight-gradient accumulators per wave (128 registers, in AGPRs: one wave per SIMD),
+// written as one slab row per wave (reduced in fixed order by mrl_reduce_rows_f32).
+template <bool CACHED, int SH>
+__global__ __launch_bounds__(256, 1) void mlp_vjp_bf16_kernel(VjpArgsB a_in, const float* __restrict__ img_g,
                                                              const int32_t* __restrict__ skip) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if (skip != nullptr && *skip != 0) return;
+  const VjpArgsB a = vjp_shape_b<SH>(a_in);
   const MlpDims& d = a.d;
   const BDims& b = a.b;
   for (int i = threadIdx.x; i < b.total_words / 4; i += 256)
@@ -406,7 +423,6 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_bf16_kernel(VjpArgsB a, const 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j32 = lane & 31;
   const int A = d.A;
   const bf16x8 ip[2] = {ident_perm(0, lane), ident_perm(1, lane)};
-  const bf16x8 in0 = ident_nat(0, lane), in1 = ident_nat(16, lane);
 
   f32x16 gW2[2], gW1[2][2], gW0[2];  // T-tile products: [u2][o], [u1][u2], [in][u1]
 #pragma unroll
@@ -424,96 +440,139 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_bf16_kernel(VjpArgsB a, const 
     gls[o] = 0.f;
   }
 
+  // Two tiles per iteration, phase by phase: the MFMA -> VALU -> MFMA dependency chain of
+  // one tile (gh2 -> tanh' -> transpose -> weight-gradient products) issues between the
+  // steps of the other's, so one wave per SIMD still overlaps MFMA latency.  A second tile
+  // past the batch is a clamped copy of the last one with every head row masked to zero:
+  // all its contributions vanish.
   const int64_t ntiles = (a.n + 31) / 32;
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
-    const int64_t row = tile * 32 + j32;
-    const bool valid = row < a.n;
-    XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
-    bf16x8 h1b[4], h2b[4];
-    if constexpr (CACHED) {
-      const float* ct = a.cache + tile * BCACHE_TILE_WORDS;
-      bcache_load(ct, 1, lane, h2b);
-      bcache_load(ct, 0, lane, h1b);
-    } else {
-      float zz[MAX_OUT];
-      forward_b(img, head_dims(d, b), b, xl, lane, h1b, h2b, zz);
-    }
-    // head-gradient row (f32) and its bf16 operand: o = 8h + j (h = 1: zero, A <= 8)
-    const float* gr = a.ghead + (valid ? row : 0) * a.gh;
-    float g[8];
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += 2 * stride) {
+    bf16x8 h1b[2][4], h2b[2][4], gB[2], xb[2][MAX_KS0B];
+    bool live[2];
 #pragma unroll
-    for (int o = 0; o < 8; ++o) g[o] = (valid && h == 0 && o < A) ? gr[o] : 0.f;
+    for (int u = 0; u < 2; ++u) {
+      const int64_t tu = tile + u * stride;
+      live[u] = tu < ntiles;
+      const int64_t tc = live[u] ? tu : ntiles - 1;
+      const int64_t row = tc * 32 + j32;
+      const bool valid = live[u] && row < a.n;
+      XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, row < a.n};
+      if constexpr (CACHED) {
+        bcache_load(a.cache + tc * BCACHE_TILE_WORDS, 1, lane, h2b[u]);
+        bcache_load(a.cache + tc * BCACHE_TILE_WORDS, 0, lane, h1b[u]);
+      } else {
+        float zz[MAX_OUT];
+        forward_b(img, head_dims(d, b), b, xl, lane, h1b[u], h2b[u], zz);
+      }
 #pragma unroll
-    for (int q = 0; q < MAX_OUT; ++q) gls[q] += (valid && h == 0 && q < a.n_sum) ? gr[A + q] : 0.f;
-    bf16x8 gB;
+      for (int s0 = 0; s0 < MAX_KS0B; ++s0) xb[u][s0] = s0 < b.KS0B ? x_frag(xl, s0, h) : bf16x8{};
+      // head-gradient row (f32) and its bf16 operand: o = 8h + j (h = 1: zero, A <= 8)
+      const float* gr = a.ghead + (row < a.n ? row : 0) * a.gh;
 #pragma unroll
-    for (int o = 0; o < 8; ++o) {
-      gb2[o] += g[o];
-      gB[o] = (__bf16)g[o];
+      for (int o = 0; o < 8; ++o) {
+        const float g = (valid && h == 0 && o < A) ? gr[o] : 0.f;
+        gb2[o] += g;
+        gB[u][o] = (__bf16)g;
+      }
+#pragma unroll
+      for (int q = 0; q < MAX_OUT; ++q) gls[q] += (valid && h == 0 && q < a.n_sum) ? gr[A + q] : 0.f;
     }
     // gh2 = W2 . G (F layout), ga2 = gh2 (1 - h2^2)
-    bf16x8 ga2b[4];
-    f32x16 ga2T[2];
+    bf16x8 ga2b[2][4];
 #pragma unroll
     for (int mo = 0; mo < 2; ++mo) {
-      f32x16 g2 = zero16();
-      g2 = MFMA32B(frag_at(img, b.bw2, mo, lane), gB, g2);
-      const f32x16 h2 = unpack16(h2b, mo);
+      f32x16 g2[2];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) g2[r] *= dtanh(h2[r]);
-      ga2b[2 * mo] = pack8(g2, 0);
-      ga2b[2 * mo + 1] = pack8(g2, 1);
-    }
+      for (int u = 0; u < 2; ++u) g2[u] = MFMA32B(frag_at(img, b.bw2, mo, lane), gB[u], zero16());
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      ga2T[m] = transpose_f(ga2b, m, ip);
+      for (int u = 0; u < 2; ++u) {
+        const f32x16 h2 = unpack16(h2b[u], mo);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) gb1[m] += ga2T[m][r];
-    }
-    // gh1 (T layout) = ga2^T . W1^T, ga1 = gh1 (1 - h1^2)
-    f32x16 ga1T[2], h1T[2];
-#pragma unroll
-    for (int no = 0; no < 2; ++no) {
-      f32x16 t = zero16();
-#pragma unroll
-      for (int s = 0; s < 4; ++s) t = MFMA32B(ga2b[s], frag_at(img, b.bt1, no * 4 + s, lane), t);
-      h1T[no] = transpose_f(h1b, no, ip);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        t[r] *= dtanh(h1T[no][r]);
-        gb0[no] += t[r];
+        for (int r = 0; r < 16; ++r) g2[u][r] *= dtanh(h2[r]);
+        ga2b[u][2 * mo] = pack8(g2[u], 0);
+        ga2b[u][2 * mo + 1] = pack8(g2[u], 1);
       }
-      ga1T[no] = t;
     }
-    // gW1 += H1^T GA2 (K = rows: T tiles of both)
-#pragma unroll
-    for (int m1 = 0; m1 < 2; ++m1)
-#pragma unroll
-      for (int m2 = 0; m2 < 2; ++m2)
-#pragma unroll
-        for (int sp = 0; sp < 2; ++sp) gW1[m1][m2] = MFMA32B(pack8(h1T[m1], sp), pack8(ga2T[m2], sp), gW1[m1][m2]);
     // gW2 += H2^T G
     {
-      f32x16 gT = zero16();
-      gT = MFMA32B(gB, in0, gT);  // D[row][o]
+      f32x16 gT[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) gT[u] = MFMA32B(gB[u], ident_nat(0, lane), zero16());  // D[row][o]
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
-        const f32x16 h2T = transpose_f(h2b, m, ip);
+        f32x16 h2T[2];
 #pragma unroll
-        for (int sp = 0; sp < 2; ++sp) gW2[m] = MFMA32B(pack8(h2T, sp), pack8(gT, sp), gW2[m]);
+        for (int u = 0; u < 2; ++u) h2T[u] = transpose_f(h2b[u], m, ip);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          gW2[m] = MFMA32B(pack8(h2T[u], 0), pack8(gT[u], 0), gW2[m]);
+          gW2[m] = MFMA32B(pack8(h2T[u], 1), pack8(gT[u], 1), gW2[m]);
+        }
       }
     }
-    // gW0 += X^T GA1 (x rows -> T tile D[row][in])
-    {
-      f32x16 xT = zero16();
+    // ga2 and the inputs in T layout
+    bf16x8 ga2T[2][2][2], xT[2][2];
 #pragma unroll
-      for (int s0 = 0; s0 < MAX_KS0B; ++s0)
-        if (s0 < b.KS0B) xT = MFMA32B(x_frag(xl, s0, h), s0 == 0 ? in0 : in1, xT);
+    for (int m = 0; m < 2; ++m) {
+      f32x16 t[2];
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+      for (int u = 0; u < 2; ++u) t[u] = transpose_f(ga2b[u], m, ip);
 #pragma unroll
-        for (int sp = 0; sp < 2; ++sp) gW0[m] = MFMA32B(pack8(xT, sp), pack8(ga1T[m], sp), gW0[m]);
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) gb1[m] += t[u][r];
+        ga2T[u][m][0] = pack8(t[u], 0);
+        ga2T[u][m][1] = pack8(t[u], 1);
+      }
     }
+    {
+      f32x16 t[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        t[u] = zero16();
+#pragma unroll
+        for (int s0 = 0; s0 < MAX_KS0B; ++s0)
+          if (s0 < b.KS0B) t[u] = MFMA32B(xb[u][s0], ident_nat(16 * s0, lane), t[u]);  // D[row][in]
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        xT[u][0] = pack8(t[u], 0);
+        xT[u][1] = pack8(t[u], 1);
+      }
+    }
+    // per u1 tile: gh1 (T layout) = ga2^T . W1^T, ga1 = gh1 (1 - h1^2), then
+    // gW1 += H1^T GA2 and gW0 += X^T GA1
+#pragma unroll
+    for (int no = 0; no < 2; ++no) {
+      f32x16 ga1[2], h1T[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) ga1[u] = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) ga1[u] = MFMA32B(ga2b[u][s], frag_at(img, b.bt1, no * 4 + s, lane), ga1[u]);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) h1T[u] = transpose_f(h1b[u], no, ip);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          ga1[u][r] *= dtanh(h1T[u][r]);
+          gb0[no] += ga1[u][r];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+          const bf16x8 h1p = pack8(h1T[u], sp);
+          gW1[no][0] = MFMA32B(h1p, ga2T[u][0][sp], gW1[no][0]);
+          gW1[no][1] = MFMA32B(h1p, ga2T[u][1][sp], gW1[no][1]);
+          gW0[no] = MFMA32B(xT[u][sp], pack8(ga1[u], sp), gW0[no]);
+        }
+    }
+    (void)live;
   }
 
   // per-wave partial gradient in flat theta layout; accumulator tiles are D[i][j] with
@@ -541,12 +600,12 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_bf16_kernel(VjpArgsB a, const 
   }
 #pragma unroll
   for (int o = 0; o < MAX_OUT; ++o) {
-    const float s = wave_sumf(gb2[o]);
-    if (lane == 0 && o < A) out[d.tb2 + o] = s;
+    const float sum = wave_sumf(gb2[o]);
+    if (lane == 0 && o < A) out[d.tb2 + o] = sum;
   }
   for (int q = 0; q < a.n_sum; ++q) {
-    const float s = wave_sumf(gls[q]);
-    if (lane == 0) out[d.tls + q] = s;
+    const float sum = wave_sumf(gls[q]);
+    if (lane == 0) out[d.tls + q] = sum;
   }
 }
 
@@ -706,10 +765,22 @@ int mrl_mlp_vjp_bf16(const mrl_mlp_desc* d, const float* image, const float* x, 
   a.cache = act_cache;
   const size_t shm = (size_t)a.b.total_words * 4;
   const dim3 grid(vjp_blocks_b(n)), blk(256);
-  if (act_cache != nullptr)
-    hipLaunchKernelGGL(mlp_vjp_bf16_kernel<true>, grid, blk, shm, (hipStream_t)stream, a, image, skip);
-  else
-    hipLaunchKernelGGL(mlp_vjp_bf16_kernel<false>, grid, blk, shm, (hipStream_t)stream, a, image, skip);
+  hipStream_t s = (hipStream_t)stream;
+  // the benchmark policies as static shapes (plain rows only; the VF's time feature
+  // column takes the generic kernel)
+  int sh = 0;
+  if (!ep_t)
+    for (int i = 1; i < N_STATIC_SHAPES; ++i)
+      if (STATIC_SHAPES[i].O == d->n_in && STATIC_SHAPES[i].A == d->n_out && STATIC_SHAPES[i].head == d->head) sh = i;
+#define MRL_VJPB(C)                                                                                              \
+  do {                                                                                                           \
+    if (sh == 1) hipLaunchKernelGGL((mlp_vjp_bf16_kernel<C, 1>), grid, blk, shm, s, a, image, skip);              \
+    else if (sh == 2) hipLaunchKernelGGL((mlp_vjp_bf16_kernel<C, 2>), grid, blk, shm, s, a, image, skip);         \
+    else hipLaunchKernelGGL((mlp_vjp_bf16_kernel<C, 0>), grid, blk, shm, s, a, image, skip);                      \
+  } while (0)
+  if (act_cache != nullptr) MRL_VJPB(true);
+  else MRL_VJPB(false);
+#undef MRL_VJPB
   return hip_check(hipGetLastError(), "mrl_mlp_vjp_bf16");
 }
 

@@ -149,7 +149,8 @@ __host__ __device__ inline float image_value(const MlpDims& d, const float* th, 
 // to match.  Every lane loads its fragments straight into registers (no LDS copy).
 struct RDims {
   int KS0, KS0p;  // input-layer k-steps (4 inputs each), padded to a multiple of 4
-  int a0, a1, b0, b1, hv, hb, size;
+  int a0, a1, b0, b1, hv, hb, f32_size;
+  int ba0, ba1, size;  // bf16 fragments (v_mfma_f32_16x16x32_bf16) of the bf16 compute mode
 };
 
 __host__ __device__ constexpr RDims rollout_dims(int O) {
@@ -163,8 +164,28 @@ __host__ __device__ constexpr RDims rollout_dims(int O) {
   r.b1 = o; o += 64;                //                           b1
   r.hv = o; o += 4 * MAX_OUT * 16;  // [g][o][4mt + r]         = W2[16mt + 4g + r][o]
   r.hb = o; o += 16;                // b2 (padded)
+  r.f32_size = o;
+  // bf16 mode: 8 bf16 (4 words) per lane and fragment, A[i = 16mo + (l&15)][k = 8g + j]
+  // (g = l >> 4): ba0 [mo][lane] = W0[k][i] (one k-step covers n_in <= 32); ba1
+  // [mo][p][lane] = W1[u][i], k ~ unit u = 32p + 16(j>>2) + 4g + (j&3) -- the units lane
+  // group g holds in registers r of the 16-unit activation tiles 2p, 2p+1.
+  r.ba0 = o; o += 4 * 64 * 4;
+  r.ba1 = o; o += 4 * 2 * 64 * 4;
   r.size = o;
   return r;
+}
+
+__host__ __device__ inline int rb_unit(int p, int g, int j) { return 32 * p + 16 * (j >> 2) + 4 * g + (j & 3); }
+
+// element j of bf16 fragment `frag` (ba0: frag = mo*64 + lane; ba1: (mo*2 + p)*64 + lane)
+__host__ __device__ inline float rimage_bf16_elem(const MlpDims& d, const float* th, bool l1, int frag, int j) {
+  const int lane = frag & 63, blk = frag >> 6, g = lane >> 4, i = lane & 15;
+  if (!l1) {
+    const int k = 8 * g + j;
+    return k < d.O ? th[d.tW0 + k * HID + 16 * blk + i] : 0.f;
+  }
+  const int mo = blk >> 1, p = blk & 1;
+  return th[d.tW1 + rb_unit(p, g, j) * HID + 16 * mo + i];
 }
 
 // value of rollout-image element `idx` given flat theta (layout above)

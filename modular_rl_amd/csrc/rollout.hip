@@ -20,6 +20,8 @@
 // (registers, no scratch).
 #include <math.h>
 
+#include <type_traits>
+
 #include "../../include/mrl_hip.h"
 #include "envs.h"
 #include "mlp_device.h"
@@ -160,6 +162,44 @@ struct RWeights {
   }
 };
 
+// bf16 compute mode: layer-0 / layer-1 fragments of v_mfma_f32_16x16x32_bf16 (image
+// segments ba0 / ba1), biases and the VALU head as in RWeights
+template <int O, int A>
+struct RWeightsB {
+  static constexpr RDims R = rollout_dims(O);
+  bf16x8 a0[4];
+  bf16x8 a1[4][2];
+  float4 b0[4], b1[4];
+  float4 hv[A][4];
+  float hb[A];
+  __device__ void load(const float* __restrict__ img, int lane) {
+    const int g = lane >> 4;
+    const bf16x8* f0 = reinterpret_cast<const bf16x8*>(img + R.ba0);
+    const bf16x8* f1 = reinterpret_cast<const bf16x8*>(img + R.ba1);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) {
+      a0[mo] = f0[mo * 64 + lane];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) a1[mo][p] = f1[(mo * 2 + p) * 64 + lane];
+    }
+    const float4* f = reinterpret_cast<const float4*>(img);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      b0[mt] = f[(R.b0 >> 2) + g * 4 + mt];
+      b1[mt] = f[(R.b1 >> 2) + g * 4 + mt];
+    }
+#pragma unroll
+    for (int o = 0; o < A; ++o)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) hv[o][mt] = f[(R.hv >> 2) + (g * MAX_OUT + o) * 4 + mt];
+#pragma unroll
+    for (int o = 0; o < A; ++o) hb[o] = img[R.hb + o];
+  }
+};
+
+template <int O, int A, bool BF>
+using RollWeights = typename std::conditional<BF, RWeightsB<O, A>, RWeights<O, A>>::type;
+
 __device__ inline f32x4 as_f32x4(float4 v) {
   f32x4 r;
   r[0] = v.x;
@@ -237,6 +277,54 @@ __device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane
     if (mo > 0) head_tile(mo - 1);
   }
   head_tile(3);
+#pragma unroll
+  for (int o = 0; o < A; ++o) z[o] = quad_sum(acc[o]) + w.hb[o];
+}
+
+// bf16 compute mode on v_mfma_f32_16x16x32_bf16: one k-step covers the inputs, two
+// the 64 hidden units (8 MFMAs for layer 1 instead of 64 f32 16x16x4), same rounding
+// points as forward16<BF = true> and mlp_rows_bf16.
+template <int O, int A, bool BF, class XL>
+__device__ inline void forward16(const RWeightsB<O, A>& w, const XL& xl, int lane, float* z, int64_t* st = nullptr) {
+  const int g = lane >> 4;
+  bf16x8 xb;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) xb[jj] = (__bf16)xl(8 * g + jj);
+  f32x4 h1[4], h2[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    h1[m] = as_f32x4(w.b0[m]);
+    h2[m] = as_f32x4(w.b1[m]);
+  }
+#pragma unroll
+  for (int mo = 0; mo < 4; ++mo) h1[mo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.a0[mo], xb, h1[mo], 0, 0, 0);
+  if (st != nullptr) st[9] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  // B fragment of k-step p: tanh(h1) of tiles 2p (elements 0..3) and 2p+1 (4..7)
+  bf16x8 hb[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      hb[p][r] = (__bf16)tanh_fast(h1[2 * p][r]);
+      hb[p][4 + r] = (__bf16)tanh_fast(h1[2 * p + 1][r]);
+    }
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) h2[mo] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.a1[mo][p], hb[p], h2[mo], 0, 0, 0);
+  if (st != nullptr) st[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  float acc[A];
+#pragma unroll
+  for (int o = 0; o < A; ++o) acc[o] = 0.f;
+#pragma unroll
+  for (int mo = 0; mo < 4; ++mo) {
+    tanh4r<true>(h2[mo]);
+#pragma unroll
+    for (int o = 0; o < A; ++o) {
+      const float4 hv = w.hv[o][mo];
+      acc[o] += hv.x * h2[mo][0] + hv.y * h2[mo][1] + hv.z * h2[mo][2] + hv.w * h2[mo][3];
+    }
+  }
 #pragma unroll
   for (int o = 0; o < A; ++o) z[o] = quad_sum(acc[o]) + w.hb[o];
 }
@@ -524,9 +612,17 @@ __global__ __launch_bounds__(RB) void rollout_reset_kernel(RollArgs a) {
 __global__ void rollout_pack_kernel(RDims r, MlpDims d, const float* __restrict__ th, float* __restrict__ out,
                                     int bf) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < r.size) {
+  if (i < r.f32_size) {
     const float v = rimage_value(r, d, th, i);
     out[i] = (bf && i < r.b0) ? bf16r(v) : v;  // bf16 mode: the MFMA weights W0, W1
+  } else if (i < r.size) {
+    // bf16 fragments: two bf16 per word
+    const bool l1 = i >= r.ba1;
+    const int rel = i - (l1 ? r.ba1 : r.ba0), frag = rel >> 2, q = rel & 3;
+    const __bf16 lo = (__bf16)rimage_bf16_elem(d, th, l1, frag, 2 * q);
+    const __bf16 hi = (__bf16)rimage_bf16_elem(d, th, l1, frag, 2 * q + 1);
+    out[i] = __uint_as_float((uint32_t)__builtin_bit_cast(uint16_t, lo) |
+                             ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16));
   }
 }
 
@@ -579,7 +675,7 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, const floa
   for (int i = 0; i < NS; ++i) s[i] = valid ? a.b.env_state[(int64_t)i * E + e] : 0.0;
   double zn[A + 1] = {};
   if (valid) load_noise<ENV>(a, row, zn);
-  RWeights<O, A> wt;
+  RollWeights<O, A, BF> wt;
   wt.load(rimg, lane);
   float lsd[A];
 #pragma unroll
@@ -807,7 +903,7 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
   const Granules gr(sync, nb, D);
   if (threadIdx.x == 0) s_fail = 0;
 
-  RWeights<O, A> wt;
+  RollWeights<O, A, BF> wt;
   wt.load(rimg, lane);
   float lsd[A];
 #pragma unroll

@@ -32,7 +32,7 @@ def main():
     nin, nout, hname = (os.environ.get("MRL_PROBE_NET") or "11,3,gauss").split(",")
     nin, nout = int(nin), int(nout)
     head = _lib.HEAD_GAUSS if hname == "gauss" else _lib.HEAD_SOFTMAX
-    net = MlpNet(nin, nout, head)
+    net = MlpNet(nin, nout, head, dtype=os.environ.get("MRL_PROBE_DTYPE", "fp32"))
     net.set_flat(glorot_init(rng, nin, nout, head))
     x = torch.randn(N, nin, device='cuda')
     act = (torch.randn(N, nout, device='cuda') if head == _lib.HEAD_GAUSS

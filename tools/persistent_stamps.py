@@ -16,10 +16,13 @@ from modular_rl_amd.envs import make  # noqa: E402
 
 NAMES = ["gather+merge", "obs", "forward", "step", "finish", "publish"]
 T = 256
-for env_id in sys.argv[1:] or ["Hopper-v2", "CartPole-v0"]:
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+dtype = "bf16" if "--bf16" in sys.argv else "fp32"
+for env_id in args or ["Hopper-v2", "CartPole-v0"]:
     env = make(env_id)
     for E in [4096, 1024]:
-        cfg = dict(timestep_limit=env.spec.max_episode_steps, n_envs=E, horizon=T, seed=0, use_graph=0)
+        cfg = dict(timestep_limit=env.spec.max_episode_steps, n_envs=E, horizon=T, seed=0, use_graph=0,
+                   mlp_dtype=dtype)
         ag = TrpoAgent(env.observation_space, env.action_space, cfg)
         col = ag.make_collector(env, cfg)
         col.collect()
