@@ -12,6 +12,11 @@ timeout -k 10 600 python bench.py --env Humanoid-v2 --envs 1024 --hid 512,512,51
 cat gpurun_out/${tag}_bench_humanoid.json
 timeout -k 10 400 python bench.py --env CartPole-v0 --steps 5 > gpurun_out/${tag}_bench_cartpole.json 2> gpurun_out/${tag}_bench_cartpole.err || exit 1
 cat gpurun_out/${tag}_bench_cartpole.json
+for c in "Hopper-v2 --steps 10" "CartPole-v0 --steps 5" "Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 3 --warmup 1"; do
+n=$(echo $c | cut -d' ' -f1 | cut -d- -f1 | tr A-Z a-z)
+timeout -k 10 600 python bench.py --env $c --dtype bf16 --no-cpu-baseline > gpurun_out/${tag}_bench_${n}_bf16.json 2> gpurun_out/${tag}_bench_${n}_bf16.err || exit 1
+cat gpurun_out/${tag}_bench_${n}_bf16.json
+done
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 1 --no-cpu-baseline > gpurun_out/${tag}_prof.log 2>&1 || exit 1
 if [ "$2" = "pmc" ]; then
