@@ -23,6 +23,7 @@
 // Replaces the same reference functions as mlp_kernels.hip (core.py:269-270,
 // trpo.py:68-70, core.py:608, 670-671) in reduced precision.
 #include <math.h>
+#include <stdlib.h>
 
 #include "../../include/mrl_hip.h"
 #include "mlp_device.h"
@@ -222,11 +223,15 @@ __device__ inline void forward_b(const float* img, const MlpDims& d, const BDims
   for (int mo = 0; mo < 2; ++mo) {
     f32x16 a = load_bias16(img, b.fb1, mo, h);
     chain_b(img, b, mo, h1b, lane, a);
+    __builtin_amdgcn_sched_barrier(0);
     tanh16(a);
     h2b[2 * mo] = pack8(a, 0);
     h2b[2 * mo + 1] = pack8(a, 1);
     const f32x16 ar = unpack16(h2b, mo);
     head_partial_mt(img, d, ar, mo, h, z);  // d = head_dims(...)
+    // scheduling fences keep the head's weight reads and the next tile's fragment
+    // prefetch from all being hoisted (the static-shape builds otherwise spill)
+    __builtin_amdgcn_sched_barrier(0);
   }
   head_finish(img, d, z);
 }
@@ -270,6 +275,7 @@ __device__ inline void jvp_b(const float* img, const float* imt, const MlpDims& 
     if (need_z) head_partial_mt(img, d, a, mo, h, z);
     head_partial_mt(img, d, da, mo, h, dz);
     head_partial_mt(imt, d, a, mo, h, dzt);
+    __builtin_amdgcn_sched_barrier(0);
   }
   if (need_z) head_finish(img, d, z);
 #pragma unroll
@@ -278,14 +284,30 @@ __device__ inline void jvp_b(const float* img, const float* imt, const MlpDims& 
 }
 
 constexpr int ROWS_BLOCK_B = 256;
-constexpr int ROWS_MAX_BLOCKS_B = 2048;
+constexpr int ROWS_MAX_BLOCKS_B = 3072;
 constexpr int EPI_FVP_CACHED_B = 100;
 
-template <int EPI_K>
+// the kernel arguments with a static shape's dimensions substituted (SH == 0: run time)
+template <int SH>
+__device__ inline void rows_shape_b(RowsArgs& a, BDims& b) {
+  if constexpr (SH != 0) {
+    constexpr StaticShape S = STATIC_SHAPES[SH];
+    a.d = static_dims(SH);
+    a.A = S.A;
+    a.head = S.head;
+    a.n_obs = S.O;
+    a.gh = S.head == MRL_HEAD_GAUSS ? 2 * S.A : S.A;
+    a.ept = nullptr;
+    b = bf16_dims(S.O, S.A);
+  }
+}
+
+template <int EPI_K, int SH>
 __global__ __launch_bounds__(ROWS_BLOCK_B, 2) void mlp_rows_bf16_kernel(RowsArgs a, BDims b,
                                                                        const float* __restrict__ img_g,
                                                                        const float* __restrict__ imt_g,
                                                                        const int32_t* __restrict__ skip) {
+  rows_shape_b<SH>(a, b);
   constexpr bool CACHED = EPI_K == EPI_FVP_CACHED_B;
   constexpr int EPI = CACHED ? MRL_EPI_FVP : EPI_K;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -626,10 +648,21 @@ static int check_desc_b(const mrl_mlp_desc* d) {
 
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-static int64_t rows_blocks_b(int64_t n) {
+// Grid caps, swept with tools/fvp_probe.py at 4.19 M rows (MRL_ROWS_BF16_BLOCKS
+// overrides both): the Fisher-product JVP (154 VGPRs: 3 blocks per CU) is fastest at
+// exactly one resident round (768: 0.347 ms; 1024: 0.47, 1536: 0.356, 2048: 0.395);
+// the forward passes (≤ 128 VGPRs) at three rounds and more (3072: surrgrad 0.526,
+// prob 0.299 ms; 2048: 0.538 / 0.303).
+constexpr int ROWS_FVP_BLOCKS_B = 768;
+static int64_t rows_blocks_b(int64_t n, bool fvp = false) {
+  static const int64_t env_cap = [] {
+    const char* e = getenv("MRL_ROWS_BF16_BLOCKS");
+    return (int64_t)(e ? atoi(e) : 0);
+  }();
+  const int64_t cap = env_cap > 0 ? env_cap : (fvp ? ROWS_FVP_BLOCKS_B : ROWS_MAX_BLOCKS_B);
   int64_t g = cdiv(cdiv(n, 32), 4);
   if (g < 1) g = 1;
-  return g > ROWS_MAX_BLOCKS_B ? ROWS_MAX_BLOCKS_B : g;
+  return g > cap ? cap : g;
 }
 static int64_t vjp_blocks_b(int64_t n) {
   int64_t g = cdiv(cdiv(n, 32), 4);
@@ -725,21 +758,35 @@ int mrl_mlp_rows_bf16(const mrl_mlp_desc* d, int32_t epi, const float* theta, co
   const BDims b = bf16_dims(d->n_in, d->n_out);
   const size_t shm = (size_t)b.fwd_words * 4 * (epi == MRL_EPI_FVP ? 2 : 1);
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(epi == MRL_EPI_PPOSGD ? 1 : rows_blocks_b(io->n)), blk(ROWS_BLOCK_B);
+  const dim3 grid(epi == MRL_EPI_PPOSGD ? 1 : rows_blocks_b(io->n, epi == MRL_EPI_FVP)), blk(ROWS_BLOCK_B);
+  // the benchmark nets as static shapes (plain rows; a time-feature column built from
+  // ep_t takes the generic kernel); policy epilogues only for the policy shapes
+  int sh = 0;
+  if (!io->ep_t)
+    for (int i = 1; i < N_STATIC_SHAPES; ++i)
+      if (STATIC_SHAPES[i].O == d->n_in && STATIC_SHAPES[i].A == d->n_out && STATIC_SHAPES[i].head == d->head) sh = i;
+  const bool pol = sh == 1 || sh == 2, vf = sh == 3 || sh == 4;
+#define MRL_ROWSB(EK, OK)                                                                                          \
+  do {                                                                                                             \
+    if ((OK) && sh == 1) hipLaunchKernelGGL((mlp_rows_bf16_kernel<EK, 1>), grid, blk, shm, s, a, b, image, image_t, skip); \
+    else if ((OK) && sh == 2) hipLaunchKernelGGL((mlp_rows_bf16_kernel<EK, 2>), grid, blk, shm, s, a, b, image, image_t, skip); \
+    else if ((OK) && sh == 3) hipLaunchKernelGGL((mlp_rows_bf16_kernel<EK, 3>), grid, blk, shm, s, a, b, image, image_t, skip); \
+    else if ((OK) && sh == 4) hipLaunchKernelGGL((mlp_rows_bf16_kernel<EK, 4>), grid, blk, shm, s, a, b, image, image_t, skip); \
+    else hipLaunchKernelGGL((mlp_rows_bf16_kernel<EK, 0>), grid, blk, shm, s, a, b, image, image_t, skip);               \
+  } while (0)
   switch (epi) {
-    case MRL_EPI_PROB: hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_PROB>, grid, blk, shm, s, a, b, image, image_t, skip); break;
-    case MRL_EPI_LOSSES: hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_LOSSES>, grid, blk, shm, s, a, b, image, image_t, skip); break;
-    case MRL_EPI_SURRGRAD: hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_SURRGRAD>, grid, blk, shm, s, a, b, image, image_t, skip); break;
-    case MRL_EPI_VFLOSS: hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_VFLOSS>, grid, blk, shm, s, a, b, image, image_t, skip); break;
+    case MRL_EPI_PROB: MRL_ROWSB(MRL_EPI_PROB, true); break;
+    case MRL_EPI_LOSSES: MRL_ROWSB(MRL_EPI_LOSSES, pol); break;
+    case MRL_EPI_SURRGRAD: MRL_ROWSB(MRL_EPI_SURRGRAD, pol); break;
+    case MRL_EPI_VFLOSS: MRL_ROWSB(MRL_EPI_VFLOSS, vf); break;
     case MRL_EPI_FVP:
-      if (a.cache_mode == MRL_CACHE_READ)
-        hipLaunchKernelGGL(mlp_rows_bf16_kernel<EPI_FVP_CACHED_B>, grid, blk, shm, s, a, b, image, image_t, skip);
-      else
-        hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_FVP>, grid, blk, shm, s, a, b, image, image_t, skip);
+      if (a.cache_mode == MRL_CACHE_READ) MRL_ROWSB(EPI_FVP_CACHED_B, pol);
+      else MRL_ROWSB(MRL_EPI_FVP, pol);
       break;
-    case MRL_EPI_PPOGRAD: hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_PPOGRAD>, grid, blk, shm, s, a, b, image, image_t, skip); break;
-    case MRL_EPI_PPOSGD: hipLaunchKernelGGL(mlp_rows_bf16_kernel<MRL_EPI_PPOSGD>, grid, blk, shm, s, a, b, image, image_t, skip); break;
+    case MRL_EPI_PPOGRAD: MRL_ROWSB(MRL_EPI_PPOGRAD, pol); break;
+    case MRL_EPI_PPOSGD: MRL_ROWSB(MRL_EPI_PPOSGD, pol); break;
   }
+#undef MRL_ROWSB
   return hip_check(hipGetLastError(), "mrl_mlp_rows_bf16");
 }
 
