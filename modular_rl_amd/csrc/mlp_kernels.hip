@@ -324,23 +324,27 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
     vjp_load(a, tile, lane, cur);
     const int64_t row0 = tile * 32;
     Fwd f;
+    const float* ct = CACHED ? a.cache + tile * CACHE_TILE_FLOATS : nullptr;
     if constexpr (CACHED) {
+#if MRL_VJP_MINW == 1
       // h1 is first used after the gh1 chain: its loads are issued after the ones the
       // first phases wait for
-      const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
       cache_load(ct, lane, 0, f.h1[0]);
       cache_load(ct, lane, 1, f.h1[1]);
+#endif
       f.h2[0] = cur.act[0];
       f.h2[1] = cur.act[1];
     } else {
       forward_tile_pre(lds, d, cur.x0, lane, f);
     }
+#if MRL_VJP_MINW == 1
     vjp_load_xg<WIDE>(a, tile, lane, cur.xg);  // used last
+#endif
 
     // head gradient rows in C layout: register r of half h = out r + 4h (masked here,
     // not at load time: see vjp_load)
     const bool valid = row0 + j < a.n;
-    f32x16 G = zero16();
+    float G[4];  // head-gradient rows: register r of half h = output r + 4h
 #pragma unroll
     for (int r = 0; r < 4; ++r) G[r] = (valid && r + 4 * h < A) ? cur.g[r] : 0.f;
 #pragma unroll
@@ -368,22 +372,25 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
     }
     WAVE_LDS_ORDER();
     // (c) gW2 += H2^T G  (row index as K through LDS; 16x16x4, head outputs as N)
-    {
-      const float4 b0 = ld4(scrB + i16 * IMG_PAD + 8 * kk), b1 = ld4(scrB + i16 * IMG_PAD + 8 * kk + 4);
-      float4 a0[4], a1[4];
+    // k-steps 0-3 then 4-7, each half's operands read just before it (the same MFMA
+    // order as one pass; half the live operand registers)
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        a0[mt] = ld4(scrA + (16 * mt + i16) * IMG_PAD + 8 * kk);
-        a1[mt] = ld4(scrA + (16 * mt + i16) * IMG_PAD + 8 * kk + 4);
-      }
+    for (int hq = 0; hq < 2; ++hq) {
+      const float4 bq = ld4(scrB + i16 * IMG_PAD + 8 * kk + 4 * hq);
+      float4 aq[4];
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
+      for (int mt = 0; mt < 4; ++mt) aq[mt] = ld4(scrA + (16 * mt + i16) * IMG_PAD + 8 * kk + 4 * hq);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
 #ifndef MRL_VJP_ABL_NOGW2
-          gW2[mt] = MFMA16(f4get(q < 4 ? a0[mt] : a1[mt], q & 3), f4get(q < 4 ? b0 : b1, q & 3), gW2[mt]);
+          gW2[mt] = MFMA16(f4get(aq[mt], q), f4get(bq, q), gW2[mt]);
 #else
           ;
+#endif
+#if MRL_VJP_MINW > 1
+      __builtin_amdgcn_sched_barrier(0);
 #endif
     }
     if (lane < A) gb2 += rowsum32(scrB, lane);
@@ -392,18 +399,48 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int r = 0; r < 16; ++r) g2[m][r] *= dtanh(f.h2[m][r]);
+#if MRL_VJP_MINW > 1
+    // two waves per SIMD: h1 is loaded once h2 is dead (the other wave covers the
+    // latency), keeping the tile's live registers within 256
+    if constexpr (CACHED) {
+      __builtin_amdgcn_sched_barrier(0);
+      cache_load(ct, lane, 0, f.h1[0]);
+      cache_load(ct, lane, 1, f.h1[1]);
+    }
+#endif
     // (e) gh1 = W1 . ga2: registers + the weight image only, so its 64 MFMAs cover the
     //     h1 / ga2 transposes issued next
     f32x16 g1[2];
     g1[0] = zero16();
     g1[1] = zero16();
 #ifndef MRL_VJP_ABL_NOCHAIN
+#if MRL_VJP_MINW > 1
+    // one k-group's weight fragments live at a time (the fence stops the scheduler
+    // from hoisting all sixteen ds_read_b128 of the chain)
+#pragma unroll
+    for (int s4 = 0; s4 < 8; ++s4) {
+#pragma unroll
+      for (int mo = 0; mo < 2; ++mo) {
+        const float4 w = frag4(lds, d.ba1, 32, mo, s4, lane);
+        const int s = 4 * s4;
+        g1[mo] = MFMA32(w.x, g2[(s + 0) >> 4][(s + 0) & 15], g1[mo]);
+        g1[mo] = MFMA32(w.y, g2[(s + 1) >> 4][(s + 1) & 15], g1[mo]);
+        g1[mo] = MFMA32(w.z, g2[(s + 2) >> 4][(s + 2) & 15], g1[mo]);
+        g1[mo] = MFMA32(w.w, g2[(s + 3) >> 4][(s + 3) & 15], g1[mo]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#else
     chain<2>(lds, d.ba1, g2, lane, g1);
+#endif
 #endif
     WAVE_LDS_ORDER();
     write_img(scrA, f.h1, lane);
     write_img(scrB, g2, lane);
     WAVE_LDS_ORDER();
+#if MRL_VJP_MINW > 1
+    vjp_load_xg<WIDE>(a, tile, lane, cur.xg);  // used by (g), under gW1's MFMAs
+#endif
     // (f) gW1 += H1^T GA2, and ga1 = gh1 * (1 - h1^2) on the VALU under it
 #pragma unroll
     for (int s4 = 0; s4 < VJP_ABL_S4; ++s4) {
@@ -427,6 +464,9 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
       gW1[0][1] = MFMA32(a0.w, b1.w, gW1[0][1]);
       gW1[1][0] = MFMA32(a1.w, b0.w, gW1[1][0]);
       gW1[1][1] = MFMA32(a1.w, b1.w, gW1[1][1]);
+#if MRL_VJP_MINW > 1
+      __builtin_amdgcn_sched_barrier(0);  // one k-group's operands live at a time
+#endif
     }
     gb1 += rowsum32(scrB, lane);
 #pragma unroll
@@ -437,23 +477,24 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
     write_img(scrB, g1, lane);
     WAVE_LDS_ORDER();
     // (g) gW0 += X^T GA1 : A[i = input][k = row] straight from global x (16x16x4)
-    {
-      float4 b0[4], b1[4];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        b0[nt] = ld4(scrB + (16 * nt + i16) * IMG_PAD + 8 * kk);
-        b1[nt] = ld4(scrB + (16 * nt + i16) * IMG_PAD + 8 * kk + 4);
-      }
+    for (int hq = 0; hq < 2; ++hq) {
+      float4 bq[4];
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
+      for (int nt = 0; nt < 4; ++nt) bq[nt] = ld4(scrB + (16 * nt + i16) * IMG_PAD + 8 * kk + 4 * hq);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
 #pragma unroll
         for (int mt = 0; mt < MT0; ++mt)
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt)
 #ifndef MRL_VJP_ABL_NOGW0
-            gW0[mt][nt] = MFMA16(cur.xg[8 * mt + q], f4get(q < 4 ? b0[nt] : b1[nt], q & 3), gW0[mt][nt]);
+            gW0[mt][nt] = MFMA16(cur.xg[8 * mt + 4 * hq + q4], f4get(bq[nt], q4), gW0[mt][nt]);
 #else
           ;
+#endif
+#if MRL_VJP_MINW > 1
+      __builtin_amdgcn_sched_barrier(0);
 #endif
     }
     gb0 += rowsum32(scrB, lane);
@@ -773,7 +814,7 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
   // the run-time-shape VJP measured faster than its static-shape instantiations (Hopper
   // policy at 4.19 M rows: 1.02 vs 1.07 ms; the register allocation differs), so the
   // static shapes are used by the rows kernels only
-  const int sh = 0;
+  const int sh = MRL_VJP_MINW > 1 ? static_shape_of(d, ep_t != nullptr) : 0;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(blocks), blk(256);
 #define MRL_VJP_LAUNCH(C)                                                                                   \
