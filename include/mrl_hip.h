@@ -358,6 +358,13 @@ int mrl_rollout_reset_rows(const mrl_rollout_desc* d, const mrl_rollout_bufs* b,
 int mrl_rollout_obs(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, int32_t t, void* stream);
 int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const float* z, const float* logstd,
                     const mrl_rollout_bufs* b, int32_t t, void* stream);
+/* Humanoid: the same step with the policy head fused in -- the caller's forward stops at
+ * the last hidden layer (hidden [E, n_hidden]) and the step computes z = hidden . w_head
+ * + b_head per env (w_head [n_hidden, n_out] Keras layout; MRL_COMPUTE_BF16 in the desc
+ * rounds hidden and w_head to bf16 like the layered bf16 GEMM) */
+int mrl_rollout_act_head(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const float* hidden,
+                         int32_t n_hidden, const float* w_head, const float* b_head, const float* logstd,
+                         const mrl_rollout_bufs* b, int32_t t, void* stream);
 /* after step T-1: fold the last reward partials into the reward stat, advance the
  * iteration counter (obs_T is never pushed: the horizon cuts the episode) */
 int mrl_rollout_finish(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void* stream);

@@ -126,6 +126,7 @@ SIGNATURES = {
     "mrl_rollout_reset_rows": (i32, [vp, vp, vp]),
     "mrl_rollout_obs": (i32, [vp, vp, i32, vp]),
     "mrl_rollout_act": (i32, [vp, i32, i32, vp, vp, vp, i32, vp]),
+    "mrl_rollout_act_head": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
 }
 
 _lib = None

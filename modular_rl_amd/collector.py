@@ -224,11 +224,20 @@ class Collector:
         d = ctypes.byref(self.desc)
         logstd = net._addr(net.theta, net.tls) if net.head == _lib.HEAD_GAUSS else None
         call("mrl_rollout_reset_rows", d, ctypes.byref(bufs), stream())
+        L = len(net.dims) - 1
         for t in range(self.T):
             call("mrl_rollout_obs", d, ctypes.byref(bufs), int(t), stream())
-            net.forward_rows(self.obs[t * E:(t + 1) * E], E, self._zrows, self._fwd_bufs)
-            call("mrl_rollout_act", d, int(net.head), int(net.n_out), ptr(self._zrows), logstd, ctypes.byref(bufs),
-                 int(t), stream())
+            x = self.obs[t * E:(t + 1) * E]
+            if self.wave_per_env:
+                # Humanoid: the head (1024 x 512 x 17, a thin GEMM) runs inside the step
+                hid = net.forward_hidden_rows(x, E, self._fwd_bufs)
+                call("mrl_rollout_act_head", d, int(net.head), int(net.n_out), ptr(hid), int(net.dims[L - 1]),
+                     net._addr(net.theta, net.w_off[L - 1]), net._addr(net.theta, net.b_off[L - 1]), logstd,
+                     ctypes.byref(bufs), int(t), stream())
+            else:
+                net.forward_rows(x, E, self._zrows, self._fwd_bufs)
+                call("mrl_rollout_act", d, int(net.head), int(net.n_out), ptr(self._zrows), logstd,
+                     ctypes.byref(bufs), int(t), stream())
         call("mrl_rollout_finish", d, ctypes.byref(bufs), stream())
 
     def set_noise(self, noise):

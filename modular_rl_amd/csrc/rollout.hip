@@ -1255,7 +1255,40 @@ __global__ __launch_bounds__(64) void hm_reset_kernel(RollArgs a) {
   }
 }
 
-__global__ __launch_bounds__(64) void hm_act_kernel(RollArgs a, const float* __restrict__ zrows,
+// The policy head fused into the step (HeadRows.hid != nullptr): z = hid[e] . W + b for
+// the env's row of the last hidden layer, lane-strided over the hidden units (17
+// accumulators per lane) and reduced across the wave in a fixed order -- one launch of
+// a 1024 x 512 x 17 GEMM with 8 blocks (33 us per step) removed.  bf: the operands
+// rounded to bf16 like the layered bf16 GEMM's (products and sums stay f32).
+struct HeadRows {
+  const float* hid;  // [E, nh] rows of the last hidden layer, or nullptr: z rows given
+  const float* w;    // [nh, A] head kernel (Keras layout)
+  const float* b;    // [A]
+  int nh, bf;
+};
+
+__device__ inline float head_z(const HeadRows& hr, int e, int lane) {
+  constexpr int A = HM_ACT;
+  float acc[A];
+#pragma unroll
+  for (int o = 0; o < A; ++o) acc[o] = 0.f;
+  const float* hrow = hr.hid + (int64_t)e * hr.nh;
+  for (int k = lane; k < hr.nh; k += 64) {
+    const float hv = hr.bf ? bf16r(hrow[k]) : hrow[k];
+    const float* wr = hr.w + (int64_t)k * A;
+#pragma unroll
+    for (int o = 0; o < A; ++o) acc[o] = fmaf(hv, hr.bf ? bf16r(wr[o]) : wr[o], acc[o]);
+  }
+  float z = 0.f;
+#pragma unroll
+  for (int o = 0; o < A; ++o) {
+    const float sum = wave_sumf(acc[o]);
+    if (lane == o) z = sum + hr.b[o];
+  }
+  return z;
+}
+
+__global__ __launch_bounds__(64) void hm_act_kernel(RollArgs a, const float* __restrict__ zrows, HeadRows hr,
                                                     const float* __restrict__ logstd, int t) {
   __shared__ hm::Wave W;
   constexpr int A = HM_ACT;
@@ -1264,10 +1297,11 @@ __global__ __launch_bounds__(64) void hm_act_kernel(RollArgs a, const float* __r
   __shared__ hm::Shared S;
   hm::load_shared(S, lane);
   if (lane < HM_NS) W.s[lane] = a.b.env_state[(int64_t)lane * E + e];
+  const float zh = hr.hid != nullptr ? head_z(hr, e, lane) : 0.f;
   WAVE_SYNC();
   // sample (DiagGauss, core.py:432-435): a = z + sd * noise in fp32; the action is the ctrl
   if (lane < A) {
-    const float z = zrows[(int64_t)e * A + lane];
+    const float z = hr.hid != nullptr ? zh : zrows[(int64_t)e * A + lane];
     const float sd = expf(logstd[lane]);
     const double zn = reinterpret_cast<const double*>(a.b.noise)[row * A + lane];
     const float av = __fadd_rn(__fmul_rn((float)zn, sd), z);
@@ -1494,11 +1528,13 @@ int mrl_rollout_obs(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, int32_
   return hip_check(hipGetLastError(), "mrl_rollout_obs");
 }
 
-int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const float* z, const float* logstd,
-                    const mrl_rollout_bufs* b, int32_t t, void* stream) {
+static int rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const float* z, const HeadRows& hr,
+                       const float* logstd, const mrl_rollout_bufs* b, int32_t t, void* stream) {
   int rc = check_rows(d, b);
   if (rc) return rc;
-  if (!b->act || !b->prob || !b->rew || !b->flags || !b->ep_t || !z) return fail(E_ARG, "null trajectory buffer");
+  if (!b->act || !b->prob || !b->rew || !b->flags || !b->ep_t || (!z && !hr.hid))
+    return fail(E_ARG, "null trajectory buffer");
+  if (hr.hid && d->env_id != MRL_ENV_HUMANOID) return fail(E_UNSUPPORTED, "the fused head is the Humanoid step's");
   if (!b->noise) return fail(E_ARG, "bufs.noise: sampling-noise rows (mrl_rollout_noise or injected) required");
   EnvInfo ei = env_info(d->env_id);
   const bool gauss = head == MRL_HEAD_GAUSS;
@@ -1510,13 +1546,31 @@ int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, cons
   const int D = ei.obs + 1;
   const dim3 genv((d->n_envs + 63) / 64), gpart(a.nb, (D + LCOLS - 1) / LCOLS);
   if (d->env_id == MRL_ENV_HUMANOID)
-    hipLaunchKernelGGL(hm_act_kernel, dim3(d->n_envs), dim3(64), hm_lds_pad(d->n_envs), (hipStream_t)stream, a, z, logstd, t);
+    hipLaunchKernelGGL(hm_act_kernel, dim3(d->n_envs), dim3(64), hm_lds_pad(d->n_envs), (hipStream_t)stream, a, z, hr,
+                       logstd, t);
   else if (d->env_id == MRL_ENV_CARTPOLE)
     hipLaunchKernelGGL(lrollout_act_kernel<MRL_ENV_CARTPOLE>, genv, dim3(64), 0, (hipStream_t)stream, a, z, logstd, t);
   else
     hipLaunchKernelGGL(lrollout_act_kernel<MRL_ENV_HOPPER>, genv, dim3(64), 0, (hipStream_t)stream, a, z, logstd, t);
   hipLaunchKernelGGL(lrollout_partials_kernel, gpart, dim3(RB), 0, (hipStream_t)stream, a, D, (t + 1) & 1, 1);
   return hip_check(hipGetLastError(), "mrl_rollout_act");
+}
+
+int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const float* z, const float* logstd,
+                    const mrl_rollout_bufs* b, int32_t t, void* stream) {
+  if (!z) return fail(E_ARG, "null z rows");
+  return rollout_act(d, head, n_out, z, HeadRows{nullptr, nullptr, nullptr, 0, 0}, logstd, b, t, stream);
+}
+
+int mrl_rollout_act_head(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const float* hidden,
+                         int32_t n_hidden, const float* w_head, const float* b_head, const float* logstd,
+                         const mrl_rollout_bufs* b, int32_t t, void* stream) {
+  if (!d || !hidden || !w_head || !b_head || n_hidden <= 0) return fail(E_ARG, "mrl_rollout_act_head: bad arguments");
+  if (d->env_id != MRL_ENV_HUMANOID || n_out != HM_ACT)
+    return fail(E_UNSUPPORTED, "mrl_rollout_act_head: the fused head is the Humanoid step's (17 outputs)");
+  return rollout_act(d, head, n_out, nullptr,
+                     HeadRows{hidden, w_head, b_head, n_hidden, (int)(d->compute == MRL_COMPUTE_BF16)}, logstd, b, t,
+                     stream);
 }
 
 static int check_fused_policy(const mrl_rollout_desc* d, const mrl_mlp_desc* pol) {

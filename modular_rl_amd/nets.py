@@ -408,6 +408,20 @@ class LayeredMlpNet:
         call("mrl_reduce_rows_f32", ptr(slab), S, self.P, ptr(out), ptr(skip), stream())
         return out
 
+    def forward_hidden_rows(self, x, n, bufs):
+        """The hidden layers only, for a step kernel that applies the head itself; returns
+        the buffer holding the last hidden layer's rows [n, hid_sizes[-1]]."""
+        L = len(self.dims) - 1
+        a, lda = self._addr(x), self.n_in
+        out = None
+        for l in range(L - 1):
+            din, dout = self.dims[l], self.dims[l + 1]
+            out = bufs[l % 2]
+            self._gemm(int(n), dout, din, a, lda, self._addr(self.theta, self.w_off[l]), dout, self._addr(out), dout,
+                       epi=_lib.GEMM_TANH, bias=self._addr(self.theta, self.b_off[l]))
+            a, lda = self._addr(out), dout
+        return out
+
     def forward_rows(self, x, n, z, bufs):
         """Head pre-activations z [n, n_out] of n obs rows into caller-owned buffers
         (the rollout's per-step forward; bufs: 2 x [n * max(hid)] scratch)."""
