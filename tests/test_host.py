@@ -61,3 +61,33 @@ def test_paths_batch_roundtrip_flags():
     assert b.flags.tolist() == [0, 0, 3, 0, 1]
     assert b.ep_t.tolist() == [0, 1, 2, 0, 1]
     assert b.T == 5 and b.E == 1
+
+
+def test_mlp_dtype_option_and_validation():
+    """mlp_dtype (the bf16 throughput mode) is an MLP option defaulting to fp32, the
+    parity dtype; an unknown dtype is rejected before any device work."""
+    import pytest
+
+    from modular_rl_amd import _lib
+    from modular_rl_amd.agentzoo import MLP_OPTIONS, TrpoAgent
+    from modular_rl_amd.nets import check_dtype
+    assert ("mlp_dtype" in [o[0] for o in MLP_OPTIONS])
+    d = MU.update_default_config(TrpoAgent.options, {})
+    assert d.mlp_dtype == "fp32"
+    assert check_dtype("bf16") == "bf16" and check_dtype("fp32") == "fp32"
+    with pytest.raises(_lib.MrlError):
+        check_dtype("fp16")
+    assert _lib.COMPUTE == {"fp32": _lib.COMPUTE_F32, "bf16": _lib.COMPUTE_BF16}
+
+
+def test_bench_flop_and_byte_accounting():
+    """bench.py's algorithmic work per row of the Fisher-product kernels (the roofline
+    numerators): fused 11-64-64-3 net, JVP and VJP 18,560 FLOP each with the cache."""
+    import types
+
+    import bench
+    net = types.SimpleNamespace(n_in=11, n_out=3, hid_sizes=[64, 64], layered=False, use_cache=True)
+    f = bench.flops_per_row(net)
+    assert f["fvp_jvp_rows"] == 18560 and f["fvp_vjp"] == 18560 and f["policy_forward"] == 2 * (11 * 64 + 64 * 64 + 64 * 3)
+    hum = types.SimpleNamespace(n_in=376, n_out=17, hid_sizes=[512, 512, 512], layered=True)
+    assert bench.flops_per_row(hum)["fvp_vjp"] == 2516992
