@@ -98,6 +98,67 @@ def test_rollout_matches_oracle(env_id, E, Tn, limit, inject):
         np.testing.assert_allclose(mr, fs.M[-1], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("env_id", ["Hopper-v2", "CartPole-v0"])
+def test_rollout_full_width_matches_oracle(env_id):
+    """The C2 / C3 env count (4096 envs = 64 blocks: the full cross-block filter merge of
+    the persistent launch) against the oracle row by row, over a short horizon."""
+    from modular_rl_amd.collector import Collector
+    from modular_rl_amd.envs import make
+    env = make(env_id)
+    head = "softmax" if env.discrete else "gauss"
+    E, Tn = 4096, 6
+    spec, th, pol = _policy(head, env.obs_dim, env.act_dim, seed=11)
+    col = Collector(env, pol, E, Tn, 1000 if not env.discrete else 200, filter=1, seed=99, use_graph=True)
+    kind = RO.CARTPOLE if env.discrete else RO.HOPPER
+    envs = RO.Envs(kind, E, 99)
+    fs = RO.FilterState(env.obs_dim + 1)
+    for it in range(2):
+        b = col.collect()
+        want, fs = RO.collect(envs, fs, spec, th, Tn, 1000 if not env.discrete else 200, it)
+        np.testing.assert_array_equal(b.flags.cpu().numpy().reshape(Tn, E), want["flags"])
+        np.testing.assert_array_equal(b.ep_t.cpu().numpy().reshape(Tn, E), want["ep_t"])
+        np.testing.assert_allclose(b.obs.cpu().numpy().reshape(Tn, E, -1), want["obs"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(b.prob.cpu().numpy().reshape(Tn, E, -1), want["prob"], rtol=1e-4, atol=1e-5)
+        (n, m, _), (nr, mr, _) = col.filter_stats()
+        assert n == fs.n and nr == fs.nr
+        np.testing.assert_allclose(m, fs.M[:-1], rtol=1e-5, atol=1e-6)
+
+
+def test_full_size_rollout_invariants():
+    """C3 at full size (4096 envs x 1024 steps, persistent launch, graph replay): the
+    size-independent properties of a lock-step batch -- episode counters advance by one
+    and restart after every episode end, terminations are episode ends, observations
+    stay inside the ZFilter clip, the running stat counts every pushed row once, and
+    each env's episode lengths add up to the horizon."""
+    from modular_rl_amd.collector import Collector
+    from modular_rl_amd.envs import make
+    env = make("Hopper-v2")
+    E, Tn = 4096, 1024
+    _, _, pol = _policy("gauss", 11, 3, seed=5)
+    col = Collector(env, pol, E, Tn, 1000, filter=1, seed=7, use_graph=True)
+    b = col.collect()
+    col.check()
+    flags = b.flags.cpu().numpy().reshape(Tn, E)
+    ep_t = b.ep_t.cpu().numpy().reshape(Tn, E).astype(np.int64)
+    last, term = (flags & 1) > 0, (flags & 2) > 0
+    assert not (term & ~last).any()
+    assert (ep_t[0] == 0).all() and last[-1].all()
+    nxt = np.where(last[:-1], 0, ep_t[:-1] + 1)
+    np.testing.assert_array_equal(ep_t[1:], nxt)
+    assert (ep_t < 1000).all()
+    lens = np.where(last, ep_t + 1, 0).sum(0)
+    np.testing.assert_array_equal(lens, np.full(E, Tn))
+    obs = b.obs.cpu().numpy()
+    assert np.isfinite(obs).all() and np.abs(obs).max() <= 5.0
+    (n, _, var), (nr, _, _) = col.filter_stats()
+    assert n == E * Tn and nr == E * Tn
+    assert np.isfinite(var).all() and (var > 0).all()
+    rew = b.rew.cpu().numpy()
+    assert np.isfinite(rew).all()
+    prob = b.prob.cpu().numpy().reshape(Tn * E, -1)
+    np.testing.assert_array_equal(prob[:, 3:], np.broadcast_to(prob[:1, 3:], prob[:, 3:].shape))  # std = exp(logstd)
+
+
 @pytest.mark.parametrize("env_id,E,Tn,graph", [("Hopper-v2", 4096, 64, True), ("Hopper-v2", 100, 300, False),
                                                ("CartPole-v0", 1, 250, False), ("CartPole-v0", 8256, 12, False),
                                                ("Hopper-v2", 8256, 8, True)])

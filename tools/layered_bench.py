@@ -25,11 +25,12 @@ def main():
     ap.add_argument("--obs", type=int, default=376)
     ap.add_argument("--act", type=int, default=17)
     ap.add_argument("--hid", type=str, default="512,512,512")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     args = ap.parse_args()
     hid = [int(h) for h in args.hid.split(",")]
     N, O, A = args.rows, args.obs, args.act
     rng = np.random.default_rng(0)
-    net = LayeredMlpNet(O, A, _lib.HEAD_GAUSS, hid)
+    net = LayeredMlpNet(O, A, _lib.HEAD_GAUSS, hid, dtype=args.dtype)
     net.set_flat(glorot_init(rng, O, A, _lib.HEAD_GAUSS, hid))
     dev = "cuda"
     x = torch.randn(N, O, device=dev)
