@@ -16,6 +16,8 @@ import os
 ROLES = [
     ("fvp_jvp_rows", "mlp_rows_kernel<100"),
     ("fvp_vjp", "mlp_vjp_kernel<true"),
+    ("fvp_jvp_rows_bf16", "mlp_rows_bf16_kernel<100"),
+    ("fvp_vjp_bf16", "mlp_vjp_bf16_kernel<true"),
     ("vjp_uncached", "mlp_vjp_kernel<false"),
     ("rows_surrgrad", "mlp_rows_kernel<2,"),
     ("rows_vfloss", "mlp_rows_kernel<3,"),
