@@ -772,45 +772,53 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, const floa
 // counters and the running stat live in registers for all T steps; the only cross-block
 // dependency of a step -- the Welford partials of the E raw observations (and rewards)
 // that every block merges into its copy of the running stat -- is handed off in memory
-// as data-tagged granules: each (block, column) partial is two 16-B {fp64 value, u64
-// step tag} records written by single write-through (sc1) stores; a consumer polls the
-// granules themselves with sc1 loads until every tag carries the step it waits for, so
-// one memory round trip both signals and delivers (MI355X_MICROARCH.md, hand-offs:
-// untorn 16-B sc1 granules).  Counts are not sent: every block knows each block's
-// number of envs.  Two parities as between step launches: block b can only overwrite a
-// parity-p granule at step t+2 after every block's step-t+1 granules arrived, i.e.
-// after every block has read parity p at step t.  Bit-identical to the step kernels.
+// as data-tagged granules: each (block, column) partial is ONE 16-B granule {fp64 mean,
+// fp64 M2} written by a single write-through (sc1) store, the step tag riding in M2's
+// sign bit (M2 >= 0); a consumer polls the granules themselves with sc1 loads until
+// every tag carries the step it waits for, so one memory round trip both signals and
+// delivers (MI355X_MICROARCH.md, hand-offs: untorn 16-B sc1 granules).  Counts are not
+// sent: every block knows each block's number of envs.  Two parities as between step
+// launches: block b can only overwrite the parity-p granule of gather step s at step
+// s+2 after every block's step-s+1 granules arrived, i.e. after every block has read
+// step s; so a slot only ever holds step s or s-2 (or the launch's memset zeros), and
+// one tag bit that alternates between consecutive writes of a slot -- tag(s) =
+// ((s >> 1) & 1) ^ 1, never the memset's 0 for s = 0, 1 -- tells them apart.
+// Bit-identical to the step kernels.
 constexpr int SYNC_ABORT = 32;             // u32 word: a block gave up waiting (own 128-B line)
-constexpr int64_t SYNC_HEAD_BYTES = 256;   // then the granules: [2 parities][D][nb][2] x 16 B
+constexpr int64_t SYNC_HEAD_BYTES = 256;   // then the granules: [2 parities][D][nb] x 16 B
 constexpr uint32_t SPIN_LIMIT = 1u << 22;  // polls (~seconds): a non-resident grid exits
 
 typedef uint32_t gran_t __attribute__((ext_vector_type(4)));  // one 16-B granule
+
+__device__ inline uint32_t step_tag(int s) { return (((uint32_t)s >> 1) & 1u) ^ 1u; }
 
 struct Granules {
   __amdgpu_buffer_rsrc_t rsrc;
   int nb, D;
   __device__ Granules(uint32_t* sync, int nb_, int D_) : nb(nb_), D(D_) {
     rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(sync) + SYNC_HEAD_BYTES, 0,
-                                             2 * D_ * nb_ * 32, 0x00020000);
+                                             2 * D_ * nb_ * 16, 0x00020000);
   }
-  __device__ uint32_t off(int parity, int k, int b, int which) const {
-    return (uint32_t)((((parity * D + k) * nb + b) * 2 + which) * 16);
+  __device__ uint32_t off(int parity, int k, int b) const { return (uint32_t)(((parity * D + k) * nb + b) * 16); }
+  __device__ void put(int step, int k, int b, double mean, double m2) const {
+    const uint64_t mb = (uint64_t)__double_as_longlong(mean);
+    const uint64_t sb = ((uint64_t)__double_as_longlong(m2) & ~(1ull << 63)) | ((uint64_t)step_tag(step) << 63);
+    gran_t g = {(uint32_t)mb, (uint32_t)(mb >> 32), (uint32_t)sb, (uint32_t)(sb >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(g, rsrc, off(step & 1, k, b), 0, 16);  // aux 16 = sc1
   }
-  __device__ void put(int parity, int k, int b, int which, double v, uint64_t tag) const {
-    const uint64_t bits = (uint64_t)__double_as_longlong(v);
-    gran_t g = {(uint32_t)bits, (uint32_t)(bits >> 32), (uint32_t)tag, (uint32_t)(tag >> 32)};
-    __builtin_amdgcn_raw_buffer_store_b128(g, rsrc, off(parity, k, b, which), 0, 16);  // aux 16 = sc1
-  }
-  __device__ gran_t get(int parity, int k, int b, int which) const {
-    return __builtin_amdgcn_raw_buffer_load_b128(rsrc, off(parity, k, b, which), 0, 16);
+  __device__ gran_t get(int step, int k, int b) const {
+    return __builtin_amdgcn_raw_buffer_load_b128(rsrc, off(step & 1, k, b), 0, 16);
   }
 };
-__device__ inline double g_val(gran_t g) { return __longlong_as_double((long long)(((uint64_t)g.y << 32) | g.x)); }
-__device__ inline bool g_tag_is(gran_t g, uint64_t tag) { return g.z == (uint32_t)tag && g.w == (uint32_t)(tag >> 32); }
+__device__ inline double g_mean(gran_t g) { return __longlong_as_double((long long)(((uint64_t)g.y << 32) | g.x)); }
+__device__ inline double g_m2(gran_t g) {
+  return __longlong_as_double((long long)((((uint64_t)(g.w & 0x7fffffffu)) << 32) | g.z));
+}
+__device__ inline bool g_tag_is(gran_t g, int step) { return (g.w >> 31) == step_tag(step); }
 
 // the block's (mean, M2) partial of vals[nvalid][D] (publish_partial's arithmetic) as
-// granules tagged `tag`; lane 0 / 1 of column group k write mean / M2
-__device__ inline void publish_granules(const Granules& gr, const double* vals, int nvalid, int parity, uint64_t tag) {
+// the granules of gather step `step`; lane 0 of column group k writes column k's
+__device__ inline void publish_granules(const Granules& gr, const double* vals, int nvalid, int step) {
   const int k = threadIdx.x >> 4, j = threadIdx.x & 15;
   double s = 0.0;
   if (k < gr.D)
@@ -823,14 +831,15 @@ __device__ inline void publish_granules(const Granules& gr, const double* vals, 
       m2 += dv * dv;
     }
   m2 = sum16(m2);
-  if (k < gr.D && j < 2) gr.put(parity, k, blockIdx.x, j, j == 0 ? mean : m2, tag);
+  if (k < gr.D && j == 0) gr.put(step, k, blockIdx.x, mean, m2);
 }
 
 // column k's records of blocks b0 + jj + 16q as RecRound registers, polled until every
-// granule carries `tag`; n_b is known (envs of block b; 0 for the reward column of the
-// reset partial).  false: the grid gave up (some block never published).
-__device__ inline bool gather_granules(const Granules& gr, RecRound& rr, int parity, int k, int jj, int b0, int E,
-                                       bool rew_counted, uint64_t tag, uint32_t* sync) {
+// granule carries gather step `step`'s tag; n_b is known (envs of block b; 0 for the
+// reward column of the reset partial).  false: the grid gave up (some block never
+// published).
+__device__ inline bool gather_granules(const Granules& gr, RecRound& rr, int step, int k, int jj, int b0, int E,
+                                       bool rew_counted, uint32_t* sync) {
   const bool isr = (k == gr.D - 1);
 #pragma unroll
   for (int q = 0; q < RB_MAX; ++q) {
@@ -844,10 +853,10 @@ __device__ inline bool gather_granules(const Granules& gr, RecRound& rr, int par
     for (int q = 0; q < RB_MAX; ++q) {
       const int b = b0 + jj + 16 * q;
       if (b < gr.nb) {
-        const gran_t gm = gr.get(parity, k, b, 0), gs = gr.get(parity, k, b, 1);
-        ready = ready && g_tag_is(gm, tag) && g_tag_is(gs, tag);
-        rr.rm[q] = g_val(gm);
-        rr.rs[q] = g_val(gs);
+        const gran_t g = gr.get(step, k, b);
+        ready = ready && g_tag_is(g, step);
+        rr.rm[q] = g_mean(g);
+        rr.rs[q] = g_m2(g);
       } else {
         rr.rm[q] = 0.0;
         rr.rs[q] = 0.0;
@@ -863,19 +872,21 @@ __device__ inline bool gather_granules(const Granules& gr, RecRound& rr, int par
   }
 }
 
+// initial state of env e's episode number epc (reset_env's Philox draw, domain 1)
 template <int ENV>
-__device__ inline void reset_env_reg(const RollArgs& a, int e, double* s, uint32_t& epc, int& ept) {
+__device__ inline void episode_start_state(const RollArgs& a, int e, uint32_t epc, double* s) {
   const uint32_t gid = (uint32_t)(a.d.env_offset + e);
   double u[EnvC<ENV>::NU];
 #pragma unroll
   for (int c = 0; c < EnvC<ENV>::NU / 2; ++c)
     philox_uniform2(a.d.seed, 1, gid, (uint64_t)epc, (uint32_t)c, u[2 * c], u[2 * c + 1]);
   EnvC<ENV>::reset(u, s);
-  epc += 1u;
-  ept = 0;
 }
 
-template <int ENV, bool BF>
+// ST: the diagnostic build with phase stamps (launched only when bufs.stamps is set);
+// production launches carry no stamp code, whose uniform pointers / offsets cost SGPRs
+// that the compiler then spilled to VGPR lanes (a v_readlane per reload, every step).
+template <int ENV, bool BF, bool ST>
 __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, const float* __restrict__ logstd,
                                                                 const float* __restrict__ rimg,
                                                                 uint32_t* __restrict__ sync) {
@@ -889,7 +900,7 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
   // diagnostic phase stamps (100 MHz realtime) of block 0 -- never set in production
 #define PSTAMP(tt, k)                                                                  \
   do {                                                                                 \
-    if (a.b.stamps != nullptr && threadIdx.x == 0 && blockIdx.x == 0)                  \
+    if (ST && threadIdx.x == 0 && blockIdx.x == 0)                                     \
       a.b.stamps[(int64_t)(tt) * 16 + (k)] = (int64_t)__builtin_amdgcn_s_memrealtime(); \
   } while (0)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
@@ -915,11 +926,16 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
     fM = a.b.filter_state[2 + k];
     fS = a.b.filter_state[2 + D + k];
   }
-  // reset every env (core.py:186); all four rows of a wave hold the same env
-  double s[NS];
+  // reset every env (core.py:186); all four rows of a wave hold the same env.  sn is
+  // the start state of the env's NEXT episode, drawn ahead so an auto-reset is a copy:
+  // its Philox draw runs behind the step's publish, under the hand-off latency.
+  double s[NS], sn[NS];
   uint32_t epc = (uint32_t)a.b.env_int[E + ec];
   int ept = 0;
-  reset_env_reg<ENV>(a, ec, s, epc, ept);
+  episode_start_state<ENV>(a, ec, epc, s);
+  epc += 1u;
+  episode_start_state<ENV>(a, ec, epc, sn);
+  bool refill = false;
   if (valid && g == 0) {
     double o[O];
     EC::obs(s, o);
@@ -928,7 +944,7 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
     vals[le * D + O] = 0.0;
   }
   __syncthreads();
-  publish_granules(gr, vals, nvalid, 0, 1);  // step 0's partials: parity 0, tag 1
+  publish_granules(gr, vals, nvalid, 0);  // gather step 0's partials
 
   for (int t = 0; t < T; ++t) {
     const int64_t row = (int64_t)t * E + e;
@@ -941,12 +957,13 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
       RecRound rr;
       bool ok = true;
       if (nb <= 16 * RB_MAX) {
-        ok = gather_granules(gr, rr, t & 1, k, jj, 0, E, t > 0, (uint64_t)t + 1, sync);
+        ok = gather_granules(gr, rr, t, k, jj, 0, E, t > 0, sync);
+        PSTAMP(t, 7);
         rr.batch(bn, bm, bs);
       } else {
         double n = 0.0, sm = 0.0, raw = 0.0;
         for (int b0 = 0; b0 < nb && ok; b0 += 16 * RB_MAX) {
-          ok = gather_granules(gr, rr, t & 1, k, jj, b0, E, t > 0, (uint64_t)t + 1, sync);
+          ok = gather_granules(gr, rr, t, k, jj, b0, E, t > 0, sync);
           rr.accumulate(n, sm, raw);
         }
         n = sum16(n);
@@ -1015,8 +1032,15 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
         a.b.rew[row] = (float)rew;
         a.b.flags[row] = (uint8_t)((last ? 1 : 0) | (term ? 2 : 0));
       }
-      if (last && t < T - 1) reset_env_reg<ENV>(a, ec, s, epc, ept);
-      else ept += 1;
+      if (last && t < T - 1) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) s[i] = sn[i];
+        epc += 1u;
+        ept = 0;
+        refill = true;
+      } else {
+        ept += 1;
+      }
     }
     if (valid && g == 0) {
       double o[O];
@@ -1027,9 +1051,13 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
     }
     __syncthreads();
     PSTAMP(t, 5);
-    if (t + 1 < T) publish_granules(gr, vals, nvalid, (t + 1) & 1, (uint64_t)t + 2);
+    if (t + 1 < T) publish_granules(gr, vals, nvalid, t + 1);
     else publish_partial(a, vals, nvalid, D, true, a.b.records + (int64_t)(T & 1) * nb * a.RS);  // for finish
     PSTAMP(t, 6);
+    if (refill) {  // the next episode's start state, off the step's critical path
+      episode_start_state<ENV>(a, ec, epc, sn);
+      refill = false;
+    }
   }
 #undef PSTAMP
   // state for the next iteration and the finish kernel: env state / counters, and the
@@ -1603,7 +1631,7 @@ int mrl_rollout_pack(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const f
 int64_t mrl_rollout_sync_bytes(const mrl_rollout_desc* d) {
   if (!d || d->n_envs <= 0) return -1;
   const int64_t nb = (d->n_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK;
-  return SYNC_HEAD_BYTES + 2 * (int64_t)(env_info(d->env_id).obs + 1) * nb * 32;
+  return SYNC_HEAD_BYTES + 2 * (int64_t)(env_info(d->env_id).obs + 1) * nb * 16;
 }
 
 // The nb blocks fit one per CU of the launch stream (its CU mask) at this kernel's
@@ -1651,14 +1679,21 @@ int mrl_rollout_run(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const fl
   // on their own), and the step hand-off polls are bounded (SPIN_LIMIT).  A cooperative
   // launch made HIP keep a runtime-owned queue that its teardown destroyed after an
   // attached rocprofv3 had finalised: the profiled process crashed at exit.
-  const bool bf = d->compute == MRL_COMPUTE_BF16;
+  const bool bf = d->compute == MRL_COMPUTE_BF16, st = b->stamps != nullptr;
+#define MRL_PERSIST(ENV, BF, ST) \
+  hipLaunchKernelGGL((rollout_persistent_kernel<ENV, BF, ST>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync)
   if (d->env_id == MRL_ENV_CARTPOLE) {
-    if (bf) hipLaunchKernelGGL((rollout_persistent_kernel<MRL_ENV_CARTPOLE, true>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync);
-    else hipLaunchKernelGGL((rollout_persistent_kernel<MRL_ENV_CARTPOLE, false>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync);
+    if (st && bf) MRL_PERSIST(MRL_ENV_CARTPOLE, true, true);
+    else if (st) MRL_PERSIST(MRL_ENV_CARTPOLE, false, true);
+    else if (bf) MRL_PERSIST(MRL_ENV_CARTPOLE, true, false);
+    else MRL_PERSIST(MRL_ENV_CARTPOLE, false, false);
   } else {
-    if (bf) hipLaunchKernelGGL((rollout_persistent_kernel<MRL_ENV_HOPPER, true>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync);
-    else hipLaunchKernelGGL((rollout_persistent_kernel<MRL_ENV_HOPPER, false>), dim3(a.nb), dim3(RB), 0, s, a, logstd, rimage, sync);
+    if (st && bf) MRL_PERSIST(MRL_ENV_HOPPER, true, true);
+    else if (st) MRL_PERSIST(MRL_ENV_HOPPER, false, true);
+    else if (bf) MRL_PERSIST(MRL_ENV_HOPPER, true, false);
+    else MRL_PERSIST(MRL_ENV_HOPPER, false, false);
   }
+#undef MRL_PERSIST
   return hip_check(hipGetLastError(), "mrl_rollout_run");
 }
 

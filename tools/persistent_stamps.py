@@ -1,7 +1,7 @@
 """Diagnostic: per-phase s_memrealtime stamps of the persistent rollout launch.
 
-Block 0 stamps columns 0-6 of every step.  Phases: 0 step start | 1 every block's
-step-t partials gathered (the tagged-granule hand-off) and merged | 2 filtered obs |
+Block 0 stamps columns 0-7 of every step.  Phases: 0 step start | 1 every block's
+step-t partials gathered (the tagged-granule hand-off; 7: the last granule arrived) and merged | 2 filtered obs |
 3 forward | 4 sample + env step | 5 finish + raw obs in LDS | 6 partial published.
 Prints the mean duration of each phase (ns) over steps 16..T-1.
 """
@@ -26,6 +26,16 @@ for env_id in args or ["Hopper-v2", "CartPole-v0"]:
         ag = TrpoAgent(env.observation_space, env.action_space, cfg)
         col = ag.make_collector(env, cfg)
         col.collect()
+        # production kernel (no stamp code): mean of 3 collects
+        torch.cuda.synchronize()
+        p0 = torch.cuda.Event(enable_timing=True)
+        p1 = torch.cuda.Event(enable_timing=True)
+        p0.record()
+        for _ in range(3):
+            col.collect()
+        p1.record()
+        torch.cuda.synchronize()
+        prod_ms = p0.elapsed_time(p1) / 3
         st = torch.zeros(T * 16, dtype=torch.int64, device="cuda")
         col.stamps = st
         torch.cuda.synchronize()
@@ -40,5 +50,8 @@ for env_id in args or ["Hopper-v2", "CartPole-v0"]:
         s = raw[16:, :7]
         d = np.diff(s, axis=1).mean(0)
         tot = (raw[17:, 0] - raw[16:-1, 0]).mean()
-        print(env_id, E, "ms/collect %.3f" % e0.elapsed_time(e1), "step-to-step ns %.0f" % tot,
-              " ".join("%s %.0f" % (n, v) for n, v in zip(NAMES, d)), flush=True)
+        # column 7: the gather's last granule arrived (before the merge arithmetic)
+        arr = (raw[16:, 7] - raw[16:, 0]).mean()
+        print(env_id, E, "prod ms/collect %.3f (%.0f ns/step)" % (prod_ms, prod_ms * 1e6 / T),
+              "stamped ms/collect %.3f" % e0.elapsed_time(e1), "step-to-step ns %.0f" % tot,
+              " ".join("%s %.0f" % (n, v) for n, v in zip(NAMES, d)), "(arrival %.0f)" % arr, flush=True)
