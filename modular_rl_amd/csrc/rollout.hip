@@ -392,12 +392,13 @@ __device__ inline void publish_partial(const RollArgs& a, const double* vals, in
 // Called by all 16 lanes of thread group k; every lane returns the same values.
 // Lane j holds records j + 16q of a round (RB_MAX per lane, 128 blocks = 8192 envs).
 constexpr int RB_MAX = 8;
-struct RecRound {
-  double rn[RB_MAX], rm[RB_MAX], rs[RB_MAX];
+template <int R>
+struct RecRoundT {
+  double rn[R], rm[R], rs[R];
   __device__ void load(const double* rec, int nb, int RS, int D, int O, int k, int j, int b0) {
     const bool isr = (k == O);
 #pragma unroll
-    for (int q = 0; q < RB_MAX; ++q) {
+    for (int q = 0; q < R; ++q) {
       const int b = b0 + j + 16 * q;
       const double* r = rec + (int64_t)(b < nb ? b : 0) * RS;
       rn[q] = b < nb ? r[isr ? 1 : 0] : 0.0;
@@ -407,13 +408,13 @@ struct RecRound {
   }
   __device__ void accumulate(double& n, double& sm, double& raw) const {
 #pragma unroll
-    for (int q = 0; q < RB_MAX; ++q) {
+    for (int q = 0; q < R; ++q) {
       n += rn[q];
       sm += rn[q] * rm[q];
       raw += rs[q] + rn[q] * rm[q] * rm[q];
     }
   }
-  // one-round batch (nb <= 16 * RB_MAX): exact two-pass form from registers
+  // one-round batch (nb <= 16 * R): exact two-pass form from registers
   __device__ void batch(double& bn, double& bm, double& bs) const {
     double n = 0.0, sm = 0.0, raw = 0.0;
     accumulate(n, sm, raw);
@@ -422,7 +423,7 @@ struct RecRound {
     const double mean = n > 0.0 ? sm / n : 0.0;
     double m2 = 0.0;
 #pragma unroll
-    for (int q = 0; q < RB_MAX; ++q)
+    for (int q = 0; q < R; ++q)
       if (rn[q] > 0.0) {
         const double dm = rm[q] - mean;
         m2 += rs[q] + rn[q] * dm * dm;
@@ -432,6 +433,10 @@ struct RecRound {
     bs = sum16(m2);
   }
 };
+
+using RecRound = RecRoundT<RB_MAX>;
+// persistent rollout: 16 * RB_SMALL blocks (<= 4096 envs) gather in half the registers
+constexpr int RB_SMALL = 4;
 
 __device__ inline void batch_of_records(const double* rec, int nb, int RS, int D, int O, int k, int j, double& bn,
                                         double& bm, double& bs) {
@@ -838,29 +843,31 @@ __device__ inline void publish_granules(const Granules& gr, const double* vals, 
 // granule carries gather step `step`'s tag; n_b is known (envs of block b; 0 for the
 // reward column of the reset partial).  false: the grid gave up (some block never
 // published).
-__device__ inline bool gather_granules(const Granules& gr, RecRound& rr, int step, int k, int jj, int b0, int E,
-                                       bool rew_counted, uint32_t* sync) {
+template <int R, class Under>
+__device__ inline bool gather_granules(const Granules& gr, RecRoundT<R>& rr, int step, int k, int jj, int b0, int E,
+                                       bool rew_counted, uint32_t* sync, Under&& under) {
   const bool isr = (k == gr.D - 1);
 #pragma unroll
-  for (int q = 0; q < RB_MAX; ++q) {
+  for (int q = 0; q < R; ++q) {
     const int b = b0 + jj + 16 * q;
     rr.rn[q] = (b < gr.nb && (!isr || rew_counted)) ? (double)min(ENVS_PER_BLOCK, E - b * ENVS_PER_BLOCK) : 0.0;
   }
   uint32_t it = 0;
   while (true) {
+    gran_t gq[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int b = b0 + jj + 16 * q;
+      gq[q] = gr.get(step, k, b < gr.nb ? b : 0);
+    }
+    if (it == 0) under();  // independent work while the first poll's loads are in flight
     bool ready = true;
 #pragma unroll
-    for (int q = 0; q < RB_MAX; ++q) {
-      const int b = b0 + jj + 16 * q;
-      if (b < gr.nb) {
-        const gran_t g = gr.get(step, k, b);
-        ready = ready && g_tag_is(g, step);
-        rr.rm[q] = g_mean(g);
-        rr.rs[q] = g_m2(g);
-      } else {
-        rr.rm[q] = 0.0;
-        rr.rs[q] = 0.0;
-      }
+    for (int q = 0; q < R; ++q) {
+      const bool in = b0 + jj + 16 * q < gr.nb;
+      ready = ready && (!in || g_tag_is(gq[q], step));
+      rr.rm[q] = in ? g_mean(gq[q]) : 0.0;
+      rr.rs[q] = in ? g_m2(gq[q]) : 0.0;
     }
     if (ready) return true;
     __builtin_amdgcn_s_sleep(1);
@@ -951,19 +958,33 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
     PSTAMP(t, 0);
     double zn[A + 1] = {};
     load_noise<ENV>(a, (int64_t)t * E + ec, zn);  // independent of the hand-off: issued first
+    // the next episode's start state of envs that auto-reset at step t-1: off the step's
+    // critical path, under the first poll of the hand-off (or beside it, non-polling waves)
+    auto refill_next = [&]() {
+      if (refill) {
+        episode_start_state<ENV>(a, ec, epc, sn);
+        refill = false;
+      }
+    };
     // running-stat merge of step t's batch (filters.py:30-31), identical in every block
+    if (!kcol) refill_next();  // kcol is wave-uniform: waves that do not poll
     if (kcol) {
       double bn, bm, bs;
       RecRound rr;
       bool ok = true;
-      if (nb <= 16 * RB_MAX) {
-        ok = gather_granules(gr, rr, t, k, jj, 0, E, t > 0, sync);
+      if (nb <= 16 * RB_SMALL) {
+        RecRoundT<RB_SMALL> r4;
+        ok = gather_granules(gr, r4, t, k, jj, 0, E, t > 0, sync, refill_next);
+        PSTAMP(t, 7);
+        r4.batch(bn, bm, bs);
+      } else if (nb <= 16 * RB_MAX) {
+        ok = gather_granules(gr, rr, t, k, jj, 0, E, t > 0, sync, refill_next);
         PSTAMP(t, 7);
         rr.batch(bn, bm, bs);
       } else {
         double n = 0.0, sm = 0.0, raw = 0.0;
         for (int b0 = 0; b0 < nb && ok; b0 += 16 * RB_MAX) {
-          ok = gather_granules(gr, rr, t, k, jj, b0, E, t > 0, sync);
+          ok = gather_granules(gr, rr, t, k, jj, b0, E, t > 0, sync, refill_next);
           rr.accumulate(n, sm, raw);
         }
         n = sum16(n);
@@ -980,6 +1001,7 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
         fden[k] = sqrt(var) + 1e-8;
       }
     }
+    PSTAMP(t, 8);
     __syncthreads();
     if (s_fail) break;  // uniform: a block that gave up leaves the loop whole
     PSTAMP(t, 1);
@@ -1054,10 +1076,6 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
     if (t + 1 < T) publish_granules(gr, vals, nvalid, t + 1);
     else publish_partial(a, vals, nvalid, D, true, a.b.records + (int64_t)(T & 1) * nb * a.RS);  // for finish
     PSTAMP(t, 6);
-    if (refill) {  // the next episode's start state, off the step's critical path
-      episode_start_state<ENV>(a, ec, epc, sn);
-      refill = false;
-    }
   }
 #undef PSTAMP
   // state for the next iteration and the finish kernel: env state / counters, and the

@@ -52,6 +52,7 @@ for env_id in args or ["Hopper-v2", "CartPole-v0"]:
         tot = (raw[17:, 0] - raw[16:-1, 0]).mean()
         # column 7: the gather's last granule arrived (before the merge arithmetic)
         arr = (raw[16:, 7] - raw[16:, 0]).mean()
+        mrg = (raw[16:, 8] - raw[16:, 7]).mean()  # column 8: block 0 wave 0's merge done (before the barrier)
         print(env_id, E, "prod ms/collect %.3f (%.0f ns/step)" % (prod_ms, prod_ms * 1e6 / T),
               "stamped ms/collect %.3f" % e0.elapsed_time(e1), "step-to-step ns %.0f" % tot,
-              " ".join("%s %.0f" % (n, v) for n, v in zip(NAMES, d)), "(arrival %.0f)" % arr, flush=True)
+              " ".join("%s %.0f" % (n, v) for n, v in zip(NAMES, d)), "(arrival %.0f, merge %.0f)" % (arr, mrg), flush=True)
