@@ -103,6 +103,7 @@ def cpu_serial_c1(seconds=8.0, seed=0):
 
 def cpu_baseline(E, Tn, env_id="Hopper-v2", hid=(64, 64), seed=0):
     """Time the numpy oracle (CPU restatement of the reference) on one full iteration."""
+    from oracle import fma
     from oracle import rollout_np as RO
     from oracle import trpo_np as T
     try:
@@ -121,7 +122,8 @@ def cpu_baseline(E, Tn, env_id="Hopper-v2", hid=(64, 64), seed=0):
     envs = RO.Envs(kind, E, seed)
     fs = RO.FilterState(O + 1)
     t0 = time.perf_counter()
-    out, fs = RO.collect(envs, fs, spec, th, Tn, limit, 0)
+    with fma.plain():  # multiply-adds as a*b + c: the exact fma emulation is for parity only
+        out, fs = RO.collect(envs, fs, spec, th, Tn, limit, 0)
     N = E * Tn
     ob = out["obs"].reshape(N, O).astype(np.float64)
     X = np.concatenate([ob, (out["ep_t"].reshape(N) / float(limit))[:, None]], axis=1)
@@ -137,7 +139,7 @@ def cpu_baseline(E, Tn, env_id="Hopper-v2", hid=(64, 64), seed=0):
     return {"value": N / dt, "unit": "env-steps/s", "cores": int(threads), "kind": "port",
             "sample": f"one full TRPO iteration (rollout+GAE+VF fit+update) of the numpy oracle on {env_id} "
                       f"{E} envs x {Tn} steps = {N} env-steps, net {O}-{'-'.join(map(str, hid))}-{A}, "
-                      f"float32 update / float64 rollout, {dt:.1f} s"}
+                      f"float32 update / float64 rollout (multiply-adds unfused), {dt:.1f} s"}
 
 
 def main():

@@ -1,6 +1,8 @@
 // Batched env dynamics on device (fp64, struct-of-arrays state), operation-for-
 // operation twins of oracle/envs.py.  FMA contraction is disabled so the results
-// follow the same rounding sequence as the numpy oracle.
+// follow the same rounding sequence as the numpy oracle; the Hopper step fuses
+// multiply-adds only at explicit fmad() calls, which the oracle mirrors exactly
+// (oracle/fma.py).
 //
 //  * CartPole-v0: gym's classic-control equations (Euler, tau 0.02, reward 1,
 //    12-degree / 2.4 limits), reached through `env.step` at core.py:197.
@@ -89,6 +91,11 @@ __device__ inline void hopper_reset(const double* u, double* s) {
 
 __device__ inline double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// a * b + c with one rounding (v_fma_f64).  FMA contraction stays off in this file, so
+// only these explicit calls fuse, at the places the oracle fuses with its exact
+// emulation (oracle/fma.py) -- the GPU and numpy dynamics stay bit-identical.
+__device__ inline double fmad(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
 // capsule k's two end-spheres against the floor: contact force sum (x, z) and
 // moment about pivot k (oracle hopper_contacts); k may differ per lane
 __device__ inline void hopper_contacts(int k, double pz, double pvx, double pvz, double om, double sk, double ck,
@@ -99,12 +106,12 @@ __device__ inline void hopper_contacts(int k, double pz, double pvx, double pvz,
   for (int n = 0; n < 2; ++n) {
     const double u = n == 0 ? sel4(k, 0.0, 0.0, 0.0, -0.13) : sel4(k, 0.0, 0.0, 0.0, 0.26);
     const double w = n == 0 ? sel4(k, 0.2, 0.0, 0.0, 0.0) : sel4(k, -0.2, -0.45, -0.5, 0.0);
-    const double ox = u * ck + w * sk;
-    const double oz = (w * ck - u * sk) - rad;
+    const double ox = fmad(u, ck, w * sk);
+    const double oz = fmad(w, ck, -(u * sk)) - rad;
     const double pen = -(pz + oz);
-    const double vx = pvx + om * oz;
-    const double vz = pvz - om * ox;
-    const double fnr = HP_KC * pen - HP_CC * vz;
+    const double vx = fmad(om, oz, pvx);
+    const double vz = fmad(-om, ox, pvz);
+    const double fnr = fmad(HP_KC, pen, -(HP_CC * vz));
     const double fn = pen > 0.0 ? (fnr > 0.0 ? fnr : 0.0) : 0.0;
     const double lim = mu * fn;
     const double fv = HP_CF * vx;
@@ -112,7 +119,7 @@ __device__ inline void hopper_contacts(int k, double pz, double pvx, double pvz,
     const double ft = -(fl < lim ? fl : lim);
     fcx = fcx + ft;
     fcz = fcz + fn;
-    ncm = ncm + (oz * ft - ox * fn);
+    ncm = ncm + fmad(oz, ft, -(ox * fn));
   }
   out[0] = fcx;
   out[1] = fcz;
@@ -132,21 +139,21 @@ struct HopperSerial {
   }
 };
 
-// LDL^T solve of the 4x4 SPD system K x = r (oracle ldl_solve)
+// LDL^T solve of the 4x4 SPD system K x = r (oracle hopper_ldl4)
 __device__ inline void ldl_solve4(const double (&K)[4][4], const double* r, double* x) {
   double L[4][4], D[4], iD[4], y[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     double d = K[j][j];
 #pragma unroll
-    for (int k = 0; k < j; ++k) d = d - (L[j][k] * L[j][k]) * D[k];
+    for (int k = 0; k < j; ++k) d = fmad(-(L[j][k] * L[j][k]), D[k], d);
     D[j] = d;
     iD[j] = 1.0 / d;
 #pragma unroll
     for (int i = j + 1; i < 4; ++i) {
       double acc = K[i][j];
 #pragma unroll
-      for (int k = 0; k < j; ++k) acc = acc - (L[i][k] * L[j][k]) * D[k];
+      for (int k = 0; k < j; ++k) acc = fmad(-(L[i][k] * L[j][k]), D[k], acc);
       L[i][j] = acc * iD[j];
     }
   }
@@ -154,14 +161,14 @@ __device__ inline void ldl_solve4(const double (&K)[4][4], const double* r, doub
   for (int i = 0; i < 4; ++i) {
     double acc = r[i];
 #pragma unroll
-    for (int k = 0; k < i; ++k) acc = acc - L[i][k] * y[k];
+    for (int k = 0; k < i; ++k) acc = fmad(-L[i][k], y[k], acc);
     y[i] = acc;
   }
 #pragma unroll
   for (int i = 3; i >= 0; --i) {
     double acc = y[i] * iD[i];
 #pragma unroll
-    for (int k = i + 1; k < 4; ++k) acc = acc - L[k][i] * x[k];
+    for (int k = i + 1; k < 4; ++k) acc = fmad(-L[k][i], x[k], acc);
     x[i] = acc;
   }
 }
@@ -192,11 +199,14 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
     gx[j] = -HP_SEG[j] * sg[j];
     gz[j] = -HP_SEG[j] * cg[j];
   }
+  // COM offsets: (0, COMZ) on the torso / thigh / leg, (COMX, 0) on the foot
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    rx[k] = HP_COMX[k] * cg[k] + HP_COMZ[k] * sg[k];
-    rz[k] = HP_COMZ[k] * cg[k] - HP_COMX[k] * sg[k];
+  for (int k = 0; k < 3; ++k) {
+    rx[k] = HP_COMZ[k] * sg[k];
+    rz[k] = HP_COMZ[k] * cg[k];
   }
+  rx[3] = HP_COMX[3] * cg[3];
+  rz[3] = -(HP_COMX[3] * sg[3]);
   // pivots: height, velocity, bias acceleration (root -> foot)
   double pz[4], pvx[4], pvz[4], pax[4], paz[4];
   pz[0] = q[1];
@@ -208,10 +218,10 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
   for (int j = 0; j < 3; ++j) {
     const double w2 = om[j] * om[j];
     pz[j + 1] = pz[j] + gz[j];
-    pvx[j + 1] = pvx[j] + om[j] * gz[j];
-    pvz[j + 1] = pvz[j] - om[j] * gx[j];
-    pax[j + 1] = pax[j] - w2 * gx[j];
-    paz[j + 1] = paz[j] - w2 * gz[j];
+    pvx[j + 1] = fmad(om[j], gz[j], pvx[j]);
+    pvz[j + 1] = fmad(-om[j], gx[j], pvz[j]);
+    pax[j + 1] = fmad(-w2, gx[j], pax[j]);
+    paz[j + 1] = fmad(-w2, gz[j], paz[j]);
   }
   double ct[4][3];
 #ifdef MRL_HP_ABL_NOCONTACT  // diagnostic timing build only (results are wrong)
@@ -231,11 +241,11 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const double w2 = om[k] * om[k];
-    const double mx = HP_MASS[k] * (pax[k] - w2 * rx[k]);
-    const double mz = HP_MASS[k] * ((paz[k] - w2 * rz[k]) + HP_GRAV);
+    const double mx = HP_MASS[k] * fmad(-w2, rx[k], pax[k]);
+    const double mz = HP_MASS[k] * (fmad(-w2, rz[k], paz[k]) + HP_GRAV);
     Fx[k] = mx - ct[k][0];
     Fz[k] = mz - ct[k][1];
-    N[k] = (rz[k] * mx - rx[k] * mz) - ct[k][2];
+    N[k] = fmad(rz[k], mx, -(rx[k] * mz)) - ct[k][2];
   }
   // subtree sums about pivot k (foot -> root)
   double Fbx[4], Fbz[4], Nb[4], Sx[4], Sz[4], J[4];
@@ -244,16 +254,16 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
   Nb[3] = N[3];
   Sx[3] = HP_MASS[3] * rx[3];
   Sz[3] = HP_MASS[3] * rz[3];
-  J[3] = HP_INERTIA[3] + HP_MASS[3] * (rx[3] * rx[3] + rz[3] * rz[3]);
+  J[3] = fmad(HP_MASS[3], fmad(rx[3], rx[3], rz[3] * rz[3]), HP_INERTIA[3]);
 #pragma unroll
   for (int k = 2; k >= 0; --k) {
-    Nb[k] = (N[k] + Nb[k + 1]) + (gz[k] * Fbx[k + 1] - gx[k] * Fbz[k + 1]);
+    Nb[k] = (N[k] + Nb[k + 1]) + fmad(gz[k], Fbx[k + 1], -(gx[k] * Fbz[k + 1]));
     Fbx[k] = Fx[k] + Fbx[k + 1];
     Fbz[k] = Fz[k] + Fbz[k + 1];
-    J[k] = ((HP_INERTIA[k] + HP_MASS[k] * (rx[k] * rx[k] + rz[k] * rz[k])) + J[k + 1]) +
-           (2.0 * (gx[k] * Sx[k + 1] + gz[k] * Sz[k + 1]) + HP_MB[k + 1] * (HP_SEG[k] * HP_SEG[k]));
-    Sx[k] = (HP_MASS[k] * rx[k] + Sx[k + 1]) + HP_MB[k + 1] * gx[k];
-    Sz[k] = (HP_MASS[k] * rz[k] + Sz[k + 1]) + HP_MB[k + 1] * gz[k];
+    J[k] = (fmad(HP_MASS[k], fmad(rx[k], rx[k], rz[k] * rz[k]), HP_INERTIA[k]) + J[k + 1]) +
+           fmad(2.0, fmad(gx[k], Sx[k + 1], gz[k] * Sz[k + 1]), HP_MB[k + 1] * (HP_SEG[k] * HP_SEG[k]));
+    Sx[k] = fmad(HP_MB[k + 1], gx[k], fmad(HP_MASS[k], rx[k], Sx[k + 1]));
+    Sz[k] = fmad(HP_MB[k + 1], gz[k], fmad(HP_MASS[k], rz[k], Sz[k + 1]));
   }
   double rhs[6] = {-Fbx[0], -Fbz[0], -Nb[0], Nb[1], Nb[2], Nb[3]};
   // rotational block C and coupling rows B0 / B1 of M (oracle hopper_dynamics_terms)
@@ -276,7 +286,7 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
     C[a][a] = J[a];
 #pragma unroll
     for (int b = a + 1; b < 4; ++b) {
-      const double val = (Dx[a][b] * Sx[b] + Dz[a][b] * Sz[b]) + J[b];
+      const double val = fmad(Dx[a][b], Sx[b], fmad(Dz[a][b], Sz[b], J[b]));
       C[a][b] = a == 0 ? -val : val;
     }
   }
@@ -286,9 +296,9 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
   for (int i = 1; i < 4; ++i) {
     const int jj = i - 1, j = 2 + i;
     C[i][i] = C[i][i] + HP_ARM;
-    const double lim = q[j] < HP_LO[jj] ? HP_KL * (HP_LO[jj] - q[j]) - HP_CL * v[j]
-                                        : (q[j] > HP_HI[jj] ? HP_KL * (HP_HI[jj] - q[j]) - HP_CL * v[j] : 0.0);
-    rhs[j] = ((rhs[j] + tau[jj]) - HP_DAMP * v[j]) + lim;
+    const double lim = q[j] < HP_LO[jj] ? fmad(HP_KL, HP_LO[jj] - q[j], -(HP_CL * v[j]))
+                                        : (q[j] > HP_HI[jj] ? fmad(HP_KL, HP_HI[jj] - q[j], -(HP_CL * v[j])) : 0.0);
+    rhs[j] = fmad(-HP_DAMP, v[j], rhs[j] + tau[jj]) + lim;
   }
   // Schur complement of the translational block, 4x4 LDL^T (oracle hopper_solve)
   double K[4][4], rr[4], x[4];
@@ -296,24 +306,24 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = a; b < 4; ++b) {
-      K[a][b] = C[a][b] - (B0[a] * B0[b] + B1[a] * B1[b]) * HP_IMT;
+      K[a][b] = fmad(-fmad(B0[a], B0[b], B1[a] * B1[b]), HP_IMT, C[a][b]);
       K[b][a] = K[a][b];
     }
 #pragma unroll
-  for (int a = 0; a < 4; ++a) rr[a] = rhs[2 + a] - (B0[a] * rhs[0] + B1[a] * rhs[1]) * HP_IMT;
+  for (int a = 0; a < 4; ++a) rr[a] = fmad(-fmad(B0[a], rhs[0], B1[a] * rhs[1]), HP_IMT, rhs[2 + a]);
 #ifdef MRL_HP_ABL_NOLDL  // diagnostic timing build only (results are wrong)
 #pragma unroll
   for (int a = 0; a < 4; ++a) x[a] = rr[a] * K[a][a];
 #else
   ldl_solve4(K, rr, x);
 #endif
-  const double t0 = rhs[0] - (((B0[0] * x[0] + B0[1] * x[1]) + B0[2] * x[2]) + B0[3] * x[3]);
-  const double t1 = rhs[1] - (((B1[0] * x[0] + B1[1] * x[1]) + B1[2] * x[2]) + B1[3] * x[3]);
+  const double t0 = rhs[0] - fmad(B0[3], x[3], fmad(B0[2], x[2], fmad(B0[1], x[1], B0[0] * x[0])));
+  const double t1 = rhs[1] - fmad(B1[3], x[3], fmad(B1[2], x[2], fmad(B1[1], x[1], B1[0] * x[0])));
   const double qdd[6] = {t0 * HP_IMT, t1 * HP_IMT, x[0], x[1], x[2], x[3]};
 #pragma unroll
-  for (int i = 0; i < 6; ++i) v[i] = v[i] + HP_DT * qdd[i];
+  for (int i = 0; i < 6; ++i) v[i] = fmad(HP_DT, qdd[i], v[i]);
 #pragma unroll
-  for (int i = 0; i < 6; ++i) q[i] = q[i] + HP_DT * v[i];
+  for (int i = 0; i < 6; ++i) q[i] = fmad(HP_DT, v[i], q[i]);
 }
 
 template <class Par = HopperSerial>

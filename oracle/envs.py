@@ -23,9 +23,13 @@ not vendored and are absent here, so env dynamics are **parity unpinned**:
 
 Every function here is mirrored operation-for-operation by the HIP env kernels
 in ``modular_rl_amd/csrc/envs.h`` (compiled with fp-contract off) so the GPU
-collector can be checked against it in float64.
+collector can be checked against it in float64.  The Hopper step fuses
+multiply-adds at the kernel's explicit ``fmad`` calls; ``fma`` (oracle/fma.py) is
+their exact single-rounding emulation.
 """
 import numpy as np
+
+from oracle.fma import fma
 
 # ---------------------------------------------------------------- CartPole-v0
 CP_GRAVITY = 9.8
@@ -244,12 +248,12 @@ def _hopper_substep(q, v, tau):
         jj = i - 1
         j = 2 + i
         C[i][i] = C[i][i] + HP_ARM
-        lim = np.where(qs[j] < HP_LO[jj], HP_KL * (HP_LO[jj] - qs[j]) - HP_CL * qd[j],
-                       np.where(qs[j] > HP_HI[jj], HP_KL * (HP_HI[jj] - qs[j]) - HP_CL * qd[j], 0.0))
-        rhs[j] = ((rhs[j] + tau[:, jj]) - HP_DAMP * qd[j]) + lim
+        lim = np.where(qs[j] < HP_LO[jj], fma(HP_KL, HP_LO[jj] - qs[j], -(HP_CL * qd[j])),
+                       np.where(qs[j] > HP_HI[jj], fma(HP_KL, HP_HI[jj] - qs[j], -(HP_CL * qd[j])), 0.0))
+        rhs[j] = fma(-HP_DAMP, qd[j], rhs[j] + tau[:, jj]) + lim
     qdd = hopper_solve(rhs, C, B0, B1)
-    v2 = np.stack([qd[i] + HP_DT * qdd[i] for i in range(6)], axis=1)
-    q2 = np.stack([qs[i] + HP_DT * v2[:, i] for i in range(6)], axis=1)
+    v2 = np.stack([fma(HP_DT, qdd[i], qd[i]) for i in range(6)], axis=1)
+    q2 = np.stack([fma(HP_DT, v2[:, i], qs[i]) for i in range(6)], axis=1)
     return q2, v2
 
 
@@ -257,17 +261,17 @@ def hopper_contacts(k, pz, pvx, pvz, om, sk, ck):
     """Contact force sum (x, z) and moment about pivot k of capsule k's two end-spheres."""
     fcx, fcz, ncm = 0.0, 0.0, 0.0
     for (u, w) in HP_CAP[k]:
-        ox = u * ck + w * sk
-        oz = (w * ck - u * sk) - HP_RAD[k]
+        ox = fma(u, ck, w * sk)
+        oz = fma(w, ck, -(u * sk)) - HP_RAD[k]
         pen = -(pz + oz)
-        vx = pvx + om * oz
-        vz = pvz - om * ox
-        fn = np.where(pen > 0.0, np.maximum(HP_KC * pen - HP_CC * vz, 0.0), 0.0)
+        vx = fma(om, oz, pvx)
+        vz = fma(-om, ox, pvz)
+        fn = np.where(pen > 0.0, np.maximum(fma(HP_KC, pen, -(HP_CC * vz)), 0.0), 0.0)
         lim = HP_MU[k] * fn
         ft = -np.minimum(np.maximum(HP_CF * vx, -lim), lim)
         fcx = fcx + ft
         fcz = fcz + fn
-        ncm = ncm + (oz * ft - ox * fn)
+        ncm = ncm + fma(oz, ft, -(ox * fn))
     return fcx, fcz, ncm
 
 
@@ -279,40 +283,41 @@ def hopper_dynamics_terms(qs, qd, sg, cg):
         om.append(om[j - 1] - qd[2 + j])
     gx = [-HP_SEG[j] * sg[j] for j in range(3)]
     gz = [-HP_SEG[j] * cg[j] for j in range(3)]
-    rx = [HP_COM[k][0] * cg[k] + HP_COM[k][1] * sg[k] for k in range(4)]
-    rz = [HP_COM[k][1] * cg[k] - HP_COM[k][0] * sg[k] for k in range(4)]
+    # COM offsets: (0, COMZ) on the torso / thigh / leg, (COMX, 0) on the foot
+    rx = [HP_COM[k][1] * sg[k] for k in range(3)] + [HP_COM[3][0] * cg[3]]
+    rz = [HP_COM[k][1] * cg[k] for k in range(3)] + [-(HP_COM[3][0] * sg[3])]
     # pivots: height, velocity, bias acceleration (root -> foot)
     pz, pvx, pvz, pax, paz = [qs[1]], [qd[0]], [qd[1]], [0.0], [0.0]
     for j in range(3):
         w2 = om[j] * om[j]
         pz.append(pz[j] + gz[j])
-        pvx.append(pvx[j] + om[j] * gz[j])
-        pvz.append(pvz[j] - om[j] * gx[j])
-        pax.append(pax[j] - w2 * gx[j])
-        paz.append(paz[j] - w2 * gz[j])
+        pvx.append(fma(om[j], gz[j], pvx[j]))
+        pvz.append(fma(-om[j], gx[j], pvz[j]))
+        pax.append(fma(-w2, gx[j], pax[j]))
+        paz.append(fma(-w2, gz[j], paz[j]))
     ct = [hopper_contacts(k, pz[k], pvx[k], pvz[k], om[k], sg[k], cg[k]) for k in range(4)]
     # per body: inertial + gravity force minus contact force, moment about its pivot
     Fx, Fz, N = [None] * 4, [None] * 4, [None] * 4
     for k in range(4):
         w2 = om[k] * om[k]
-        mx = HP_MASS[k] * (pax[k] - w2 * rx[k])
-        mz = HP_MASS[k] * ((paz[k] - w2 * rz[k]) + HP_GRAV)
+        mx = HP_MASS[k] * fma(-w2, rx[k], pax[k])
+        mz = HP_MASS[k] * (fma(-w2, rz[k], paz[k]) + HP_GRAV)
         Fx[k] = mx - ct[k][0]
         Fz[k] = mz - ct[k][1]
-        N[k] = (rz[k] * mx - rx[k] * mz) - ct[k][2]
+        N[k] = fma(rz[k], mx, -(rx[k] * mz)) - ct[k][2]
     # subtree sums about pivot k (foot -> root)
     Fbx, Fbz, Nb, Sx, Sz, J = [None] * 4, [None] * 4, [None] * 4, [None] * 4, [None] * 4, [None] * 4
     Fbx[3], Fbz[3], Nb[3] = Fx[3], Fz[3], N[3]
     Sx[3], Sz[3] = HP_MASS[3] * rx[3], HP_MASS[3] * rz[3]
-    J[3] = HP_INERTIA[3] + HP_MASS[3] * (rx[3] * rx[3] + rz[3] * rz[3])
+    J[3] = fma(HP_MASS[3], fma(rx[3], rx[3], rz[3] * rz[3]), HP_INERTIA[3])
     for k in (2, 1, 0):
-        Nb[k] = (N[k] + Nb[k + 1]) + (gz[k] * Fbx[k + 1] - gx[k] * Fbz[k + 1])
+        Nb[k] = (N[k] + Nb[k + 1]) + fma(gz[k], Fbx[k + 1], -(gx[k] * Fbz[k + 1]))
         Fbx[k] = Fx[k] + Fbx[k + 1]
         Fbz[k] = Fz[k] + Fbz[k + 1]
-        J[k] = ((HP_INERTIA[k] + HP_MASS[k] * (rx[k] * rx[k] + rz[k] * rz[k])) + J[k + 1]) + \
-            (2.0 * (gx[k] * Sx[k + 1] + gz[k] * Sz[k + 1]) + HP_MB[k + 1] * (HP_SEG[k] * HP_SEG[k]))
-        Sx[k] = (HP_MASS[k] * rx[k] + Sx[k + 1]) + HP_MB[k + 1] * gx[k]
-        Sz[k] = (HP_MASS[k] * rz[k] + Sz[k + 1]) + HP_MB[k + 1] * gz[k]
+        J[k] = (fma(HP_MASS[k], fma(rx[k], rx[k], rz[k] * rz[k]), HP_INERTIA[k]) + J[k + 1]) + \
+            fma(2.0, fma(gx[k], Sx[k + 1], gz[k] * Sz[k + 1]), HP_MB[k + 1] * (HP_SEG[k] * HP_SEG[k]))
+        Sx[k] = fma(HP_MB[k + 1], gx[k], fma(HP_MASS[k], rx[k], Sx[k + 1]))
+        Sz[k] = fma(HP_MB[k + 1], gz[k], fma(HP_MASS[k], rz[k], Sz[k + 1]))
     rhs = [-Fbx[0], -Fbz[0], -Nb[0], Nb[1], Nb[2], Nb[3]]
     # M: rotational block C[a][b] = s_a s_b (D_ab . S_b + J_b), s_0 = 1, s_i = -1,
     # D_ab = pivot b - pivot a; coupling rows M[0][2+b] = s_b Sz_b, M[1][2+b] = -s_b Sx_b
@@ -325,7 +330,7 @@ def hopper_dynamics_terms(qs, qd, sg, cg):
     for a in range(4):
         C[a][a] = J[a]
         for b in range(a + 1, 4):
-            val = (Dx[(a, b)] * Sx[b] + Dz[(a, b)] * Sz[b]) + J[b]
+            val = fma(Dx[(a, b)], Sx[b], fma(Dz[(a, b)], Sz[b], J[b]))
             C[a][b] = -val if a == 0 else val
     B0 = [Sz[0], -Sz[1], -Sz[2], -Sz[3]]
     B1 = [-Sx[0], Sx[1], Sx[2], Sx[3]]
@@ -338,13 +343,45 @@ def hopper_solve(rhs, C, B0, B1):
     K = [[None] * 4 for _ in range(4)]
     for a in range(4):
         for b in range(a, 4):
-            K[a][b] = C[a][b] - (B0[a] * B0[b] + B1[a] * B1[b]) * HP_IMT
+            K[a][b] = fma(-fma(B0[a], B0[b], B1[a] * B1[b]), HP_IMT, C[a][b])
             K[b][a] = K[a][b]
-    rr = [rhs[2 + a] - (B0[a] * rhs[0] + B1[a] * rhs[1]) * HP_IMT for a in range(4)]
-    x = ldl_solve(K, rr, 4)
-    t0 = rhs[0] - (((B0[0] * x[0] + B0[1] * x[1]) + B0[2] * x[2]) + B0[3] * x[3])
-    t1 = rhs[1] - (((B1[0] * x[0] + B1[1] * x[1]) + B1[2] * x[2]) + B1[3] * x[3])
+    rr = [fma(-fma(B0[a], rhs[0], B1[a] * rhs[1]), HP_IMT, rhs[2 + a]) for a in range(4)]
+    x = hopper_ldl4(K, rr)
+    t0 = rhs[0] - fma(B0[3], x[3], fma(B0[2], x[2], fma(B0[1], x[1], B0[0] * x[0])))
+    t1 = rhs[1] - fma(B1[3], x[3], fma(B1[2], x[2], fma(B1[1], x[1], B1[0] * x[0])))
     return [t0 * HP_IMT, t1 * HP_IMT] + x
+
+
+def hopper_ldl4(M, rhs):
+    """LDL^T solve of the 4x4 SPD Schur block in the device kernel's operation order
+    (envs.h ldl_solve4, multiply-adds fused)."""
+    n = 4
+    L = [[None] * n for _ in range(n)]
+    D, iD = [None] * n, [None] * n
+    for j in range(n):
+        d = M[j][j]
+        for k in range(j):
+            d = fma(-(L[j][k] * L[j][k]), D[k], d)
+        D[j] = d
+        iD[j] = 1.0 / d
+        for i in range(j + 1, n):
+            acc = M[i][j]
+            for k in range(j):
+                acc = fma(-(L[i][k] * L[j][k]), D[k], acc)
+            L[i][j] = acc * iD[j]
+    y = [None] * n
+    for i in range(n):
+        acc = rhs[i]
+        for k in range(i):
+            acc = fma(-L[i][k], y[k], acc)
+        y[i] = acc
+    x = [None] * n
+    for i in range(n - 1, -1, -1):
+        acc = y[i] * iD[i]
+        for k in range(i + 1, n):
+            acc = fma(-L[k][i], x[k], acc)
+        x[i] = acc
+    return x
 
 
 def ldl_solve(M, rhs, n):
