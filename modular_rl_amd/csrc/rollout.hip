@@ -218,6 +218,9 @@ __device__ inline void tanh4(f32x4& a) {
 __device__ inline float bf16r(float x) { return (float)(__bf16)x; }
 template <bool BF>
 __device__ inline void tanh4r(f32x4& a) {
+#ifdef MRL_ABL_NOTANH  // diagnostic timing build only (results are wrong)
+  return;
+#endif
 #pragma unroll
   for (int r = 0; r < 4; ++r) a[r] = BF ? bf16r(tanh_fast(a[r])) : tanh_fast(a[r]);
 }
@@ -253,7 +256,13 @@ __device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int mo = 0; mo < 4; ++mo) h2[mo] = MFMA16(f4get(w.a1[mo][mt], q), h1[mt][q], h2[mo]);
+      for (int mo = 0; mo < 4; ++mo) {
+#ifdef MRL_ABL_NOL1  // diagnostic timing build only (results are wrong)
+        if (q == 0) h2[mo][mt] += h1[mt][q];
+        continue;
+#endif
+        h2[mo] = MFMA16(f4get(w.a1[mo][mt], q), h1[mt][q], h2[mo]);
+      }
     tanh4r<BF>(h1[mt + 1]);
   }
   if (st != nullptr) st[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
@@ -956,6 +965,8 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
   for (int t = 0; t < T; ++t) {
     const int64_t row = (int64_t)t * E + e;
     PSTAMP(t, 0);
+    if (ST && threadIdx.x == 0 && blockIdx.x == 0)  // shader clock beside the 100 MHz one (in-kernel GHz)
+      a.b.stamps[(int64_t)t * 16 + 9] = (int64_t)__builtin_amdgcn_s_memtime();
     double zn[A + 1] = {};
     load_noise<ENV>(a, (int64_t)t * E + ec, zn);  // independent of the hand-off: issued first
     // the next episode's start state of envs that auto-reset at step t-1: off the step's

@@ -53,6 +53,8 @@ for env_id in args or ["Hopper-v2", "CartPole-v0"]:
         # column 7: the gather's last granule arrived (before the merge arithmetic)
         arr = (raw[16:, 7] - raw[16:, 0]).mean()
         mrg = (raw[16:, 8] - raw[16:, 7]).mean()  # column 8: block 0 wave 0's merge done (before the barrier)
+        clk = st.view(T, 16).cpu().numpy()[:, 9].astype(np.float64)  # shader clock at step start
+        ghz = (clk[-1] - clk[16]) / (raw[-1, 0] - raw[16, 0])
         print(env_id, E, "prod ms/collect %.3f (%.0f ns/step)" % (prod_ms, prod_ms * 1e6 / T),
               "stamped ms/collect %.3f" % e0.elapsed_time(e1), "step-to-step ns %.0f" % tot,
-              " ".join("%s %.0f" % (n, v) for n, v in zip(NAMES, d)), "(arrival %.0f, merge %.0f)" % (arr, mrg), flush=True)
+              " ".join("%s %.0f" % (n, v) for n, v in zip(NAMES, d)), "(arrival %.0f, merge %.0f) clock %.2f GHz" % (arr, mrg, ghz), flush=True)
