@@ -184,6 +184,52 @@ typedef struct {
 } mrl_gemm_desc;
 
 int mrl_gemm(const mrl_gemm_desc* g, const int32_t* skip, void* stream);
+
+/* bf16-operand GEMMs of the layered path's bf16 mode (csrc/gemm_bf16.hip): operands in
+ * HBM as bf16 (a bf16 tape and packed bf16 weight images), f32 accumulation.  The
+ * reference interface they serve is the same as mrl_gemm's (Keras Dense layers,
+ * agentzoo.py:34-48, and their Theano gradients, trpo.py:40-47). */
+typedef struct {
+  int64_t m, n, k;
+  const uint16_t* a;    /* bf16 [m, lda] row-major, k contiguous; columns k..lda-1 zero   */
+  int64_t lda;          /* multiple of 8                                                  */
+  const uint16_t* bt;   /* B transposed: bf16 [n, ldb] (k contiguous), zero padding       */
+  int64_t ldb;          /* multiple of 8                                                  */
+  const uint16_t* a2;   /* optional second product a2 . bt2^T (same k / lda / ldb)         */
+  const uint16_t* bt2;
+  void* c;              /* [m, ldc] f32, or bf16 when c_bf16                              */
+  int64_t ldc;
+  int32_t c_bf16;
+  int32_t epilogue;     /* MRL_GEMM_STORE | MRL_GEMM_TANH | MRL_GEMM_DTANH                */
+  const float* bias;    /* [n] or NULL                                                    */
+  const uint16_t* h;    /* DTANH: bf16 [m, ldh] activations                               */
+  int64_t ldh;
+} mrl_gemm_bf16_desc;
+int mrl_gemm_bf16(const mrl_gemm_bf16_desc* g, const int32_t* skip, void* stream);
+
+/* weight gradients: slab[z*slab_stride + i*ldc + j] = sum over row split z of
+ * a[r, i] * b[r, j] (both bf16 row-major over the k rows); ones_row: row m-1 of the
+ * result is the column sums of b (the bias gradient: a's column m-1 reads as 1).
+ * Splits as mrl_gemm_slab_splits(k, splits). */
+typedef struct {
+  int64_t m, n, k;
+  const uint16_t* a;
+  int64_t lda;
+  const uint16_t* b;
+  int64_t ldb;
+  int32_t ones_row;
+  int32_t splits;
+  float* slab;
+  int64_t slab_stride, ldc;
+} mrl_gemm_bf16_tn_desc;
+int mrl_gemm_bf16_tn(const mrl_gemm_bf16_tn_desc* g, const int32_t* skip, void* stream);
+/* y[r, c] = bf16(x[r, c]) (RNE) for c < cols, 0 for cols <= c < ldy */
+int mrl_cast_rows_bf16(const float* x, int64_t rows, int64_t cols, int64_t ldx, uint16_t* y, int64_t ldy,
+                       void* stream);
+/* bf16 image of a Dense kernel W [din, dout] (f32): transpose 0 -> [din, ld] = W,
+ * transpose 1 -> [dout, ld] = W^T; zero padding columns */
+int mrl_pack_w_bf16(const float* w, int64_t din, int64_t dout, int32_t transpose, uint16_t* out, int64_t ld,
+                    void* stream);
 /* slabs a MRL_GEMM_SLAB call over k rows with `max_splits` requested actually writes */
 int64_t mrl_gemm_slab_splits(int64_t k, int32_t max_splits);
 /* bias / logstd gradients: slab[z*slab_stride + c] = sum of g[r, c] (ld ldg) over the

@@ -50,6 +50,17 @@ class GemmDesc(ctypes.Structure):
                 ("slab_stride", i64)]
 
 
+class GemmBf16Desc(ctypes.Structure):
+    _fields_ = [("m", i64), ("n", i64), ("k", i64), ("a", vp), ("lda", i64), ("bt", vp), ("ldb", i64), ("a2", vp),
+                ("bt2", vp), ("c", vp), ("ldc", i64), ("c_bf16", i32), ("epilogue", i32), ("bias", vp), ("h", vp),
+                ("ldh", i64)]
+
+
+class GemmBf16TnDesc(ctypes.Structure):
+    _fields_ = [("m", i64), ("n", i64), ("k", i64), ("a", vp), ("lda", i64), ("b", vp), ("ldb", i64),
+                ("ones_row", i32), ("splits", i32), ("slab", vp), ("slab_stride", i64), ("ldc", i64)]
+
+
 class RolloutDesc(ctypes.Structure):
     _fields_ = [("env_id", i32), ("n_envs", i32), ("horizon", i32), ("timestep_limit", i32), ("filter", i32),
                 ("env_offset", i32), ("seed", ctypes.c_uint64), ("compute", i32), ("pad_", i32)]
@@ -84,6 +95,10 @@ SIGNATURES = {
     "mrl_reduce_rows_f64": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_gemm": (i32, [vp, vp, vp]),
     "mrl_gemm_slab_splits": (i64, [i64, i32]),
+    "mrl_gemm_bf16": (i32, [vp, vp, vp]),
+    "mrl_gemm_bf16_tn": (i32, [vp, vp, vp]),
+    "mrl_cast_rows_bf16": (i32, [vp, i64, i64, i64, vp, i64, vp]),
+    "mrl_pack_w_bf16": (i32, [vp, i64, i64, i32, vp, i64, vp]),
     "mrl_colsum": (i32, [vp, i64, i64, i64, i32, vp, i64, vp, vp]),
     "mrl_head_rows": (i32, [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_concat_time": (i32, [vp, vp, i64, i32, f64, vp, vp]),

@@ -1,0 +1,442 @@
+// bf16-operand GEMMs of the layered MLP path's throughput mode (MRL_COMPUTE_BF16 with
+// a bf16 tape): the operands live in HBM as bf16 (half the bytes of gemm.hip's
+// fp32-staged tiles), accumulation stays f32 on v_mfma_f32_32x32x16_bf16.
+//
+//  mrl_gemm_bf16      C[M,N] = A[M,K] . B[K,N]  (+ A2 . B2)  + bias, epilogue store |
+//                     tanh | * (1 - H^2); A row-major (K contiguous), B given as its
+//                     transpose Bt[N,K] (K contiguous: the packed weight images), so
+//                     both tiles stage global -> LDS as whole 16-B rows segments and
+//                     every MFMA operand is one ds_read_b128.  Output f32 or bf16.
+//                     Layer forward (tanh), JVP (dual product, * (1 - H^2)), VJP
+//                     input grad (Bt = W itself, * (1 - H^2)).
+//  mrl_gemm_bf16_tn   weight gradients C[M,N] = sum_r A[r,M] B[r,N] over the rows r
+//                     (K = rows, split-K into f32 slabs); A and B are row-major
+//                     activations / gradients, staged row-major and read as MFMA
+//                     operands with the gfx950 transposing LDS read ds_read_b64_tr_b16.
+//                     The bias gradient rides as a ones-column of A.
+//
+// Block 128 x BN (BN = 128: 2x2 waves of 64x64; BN = 32: 4 waves of 32x32, for the
+// heads), global -> registers -> LDS double-buffered (the next K step's loads are in
+// flight under this step's MFMAs), blocks dealt to the XCDs in contiguous tile runs.
+#include <math.h>
+
+#include "../../include/mrl_hip.h"
+#include "mlp_device.h"
+
+namespace mrl {
+
+typedef uint16_t bfr_t;  // raw bf16 bits in memory
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+__device__ inline float bf2f(bfr_t v) { return __uint_as_float((uint32_t)v << 16); }
+__device__ inline bfr_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }  // RNE
+
+// ------------------------------------------------------------------ NN / NT (Bt) GEMM
+constexpr int QBM = 128;
+
+struct GemmB16Args {
+  int64_t M, N, K;
+  const bfr_t* A;
+  const bfr_t* Bt;
+  const bfr_t* A2;
+  const bfr_t* Bt2;
+  int64_t lda, ldb;
+  void* C;
+  int64_t ldc;
+  const float* bias;
+  const bfr_t* H;
+  int64_t ldh;
+  int epi;
+  const int32_t* skip;
+};
+
+// one 16-B chunk (8 bf16 along k) of row r, k offset kc of a row-major [rows][ld]
+// operand; chunks at or past K read as zero (K's padding columns are zero in memory)
+__device__ inline u32x4v load_chunk(const bfr_t* __restrict__ p, int64_t r, int64_t rows, int64_t ld, int64_t kc,
+                                    int64_t K) {
+  if (r < rows && kc < K) return *reinterpret_cast<const u32x4v*>(p + r * ld + kc);
+  return u32x4v{0u, 0u, 0u, 0u};
+}
+
+// QBK: K per LDS stage; row pitch QBK + 8 bf16 (144 B for 64, 80 B for 32): the 16
+// rows a ds_read_b128 16-lane group touches start on distinct 4-bank groups
+template <int BN, bool OUTBF, int QBK>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmB16Args g) {
+  constexpr int QLD = QBK + 8;
+  constexpr int MI = BN == 128 ? 2 : 1, NI = MI;
+  constexpr int NA = QBM * (QBK / 8) / 256, NB = (BN * (QBK / 8) + 255) / 256;  // 16-B chunks per thread
+  constexpr int STAGE = (QBM + BN) * QLD;                               // bf16 per LDS stage
+  __shared__ __attribute__((aligned(16))) bfr_t smem[2 * STAGE];
+  if (g.skip != nullptr && *g.skip != 0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
+  const int wm = BN == 128 ? wave >> 1 : wave, wn = BN == 128 ? wave & 1 : 0;
+  int64_t tm = blockIdx.y, tn = blockIdx.x;
+  {
+    const int64_t nx = gridDim.x, tiles = nx * gridDim.y;
+    const int64_t L = blockIdx.x + nx * (int64_t)blockIdx.y;
+    if (tiles % 8 == 0) {
+      const int64_t T = (L % 8) * (tiles / 8) + L / 8;
+      tm = T / nx;
+      tn = T % nx;
+    }
+  }
+  const int64_t m0 = tm * QBM, n0 = tn * BN;
+  const int64_t ntk = (g.K + QBK - 1) / QBK;
+  const int64_t nt = (g.A2 != nullptr ? 2 : 1) * ntk;
+  // thread t stages chunk c (k = 8c) of rows r (+ RS i)
+  constexpr int CPR = QBK / 8, RS = 256 / CPR;  // chunks per row, rows per pass
+  const int sc = threadIdx.x % CPR, sr = threadIdx.x / CPR;
+  u32x4v ra[NA], rb[NB];
+  auto load = [&](int64_t t) {
+    const bool p2 = t >= ntk;
+    const int64_t k0 = (t - (p2 ? ntk : 0)) * QBK + 8 * sc;
+    const bfr_t* A = p2 ? g.A2 : g.A;
+    const bfr_t* B = p2 ? g.Bt2 : g.Bt;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) ra[i] = load_chunk(A, m0 + sr + RS * i, g.M, g.lda, k0, g.K);
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      rb[i] = sr + RS * i < BN ? load_chunk(B, n0 + sr + RS * i, g.N, g.ldb, k0, g.K) : u32x4v{0u, 0u, 0u, 0u};
+  };
+  auto store = [&](bfr_t* st) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) *reinterpret_cast<u32x4v*>(st + (sr + RS * i) * QLD + 8 * sc) = ra[i];
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if (sr + RS * i < BN) *reinterpret_cast<u32x4v*>(st + (QBM + sr + RS * i) * QLD + 8 * sc) = rb[i];
+  };
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int a = 0; a < MI; ++a)
+#pragma unroll
+    for (int b = 0; b < NI; ++b) acc[a][b] = zero16();
+  if (nt > 0) {
+    load(0);
+    store(smem);
+  }
+  for (int64_t t = 0; t < nt; ++t) {
+    __syncthreads();
+    const bfr_t* As = smem + (t & 1) * STAGE;
+    const bfr_t* Bs = As + QBM * QLD;
+    if (t + 1 < nt) load(t + 1);
+#pragma unroll
+    for (int ks = 0; ks < QBK / 16; ++ks) {
+      bf16x8 av[MI], bv[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+        av[mi] = *reinterpret_cast<const bf16x8*>(As + (wm * 32 * MI + 32 * mi + j) * QLD + 16 * ks + 8 * h);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+        bv[ni] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 32 * NI + 32 * ni + j) * QLD + 16 * ks + 8 * h);
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA32B(av[mi], bv[ni], acc[mi][ni]);
+    }
+    if (t + 1 < nt) store(smem + ((t + 1) & 1) * STAGE);
+  }
+  // epilogue: lane holds column j, rows cperm(r, h) of each 32x32 tile
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int64_t col = n0 + wn * 32 * NI + ni * 32 + j;
+      if (col >= g.N) continue;
+      const int64_t rbase = m0 + wm * 32 * MI + mi * 32;
+      const float bv = g.bias != nullptr ? g.bias[col] : 0.f;
+      if (rbase + 32 <= g.M) {
+        // full row range: the 16 H loads issue together, then the stores
+        float hv[16];
+        if (g.epi == MRL_GEMM_DTANH) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) hv[r] = bf2f(g.H[(rbase + cperm(r, h)) * g.ldh + col]);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t row = rbase + cperm(r, h);
+          float v = acc[mi][ni][r] + bv;
+          if (g.epi == MRL_GEMM_TANH) v = tanh_fast(v);
+          else if (g.epi == MRL_GEMM_DTANH) v *= dtanh(hv[r]);
+          if (OUTBF) reinterpret_cast<bfr_t*>(g.C)[row * g.ldc + col] = f2bf(v);
+          else reinterpret_cast<float*>(g.C)[row * g.ldc + col] = v;
+        }
+        continue;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = rbase + cperm(r, h);
+        if (row >= g.M) continue;
+        float v = acc[mi][ni][r] + bv;
+        if (g.epi == MRL_GEMM_TANH) v = tanh_fast(v);
+        else if (g.epi == MRL_GEMM_DTANH) v *= dtanh(bf2f(g.H[row * g.ldh + col]));
+        if (OUTBF) reinterpret_cast<bfr_t*>(g.C)[row * g.ldc + col] = f2bf(v);
+        else reinterpret_cast<float*>(g.C)[row * g.ldc + col] = v;
+      }
+    }
+}
+
+// ------------------------------------------------------------------ TN (weight grads)
+// K step: 32 rows; LDS images [32 rows][BM or BN columns], pitch 160 bf16 (320 B): a
+// 32-lane half's transposed read (rows q = 0..3, 8 B at columns 16G + 4p) covers all
+// 64 banks once.
+constexpr int TBK = 32, TLD = 160;
+
+struct GemmTnArgs {
+  int64_t M, N, K;  // C[M][N] over K rows
+  const bfr_t* A;   // [K][lda]: columns 0..m_real-1 (column m_real = 1 if ones)
+  const bfr_t* B;   // [K][ldb]
+  int64_t lda, ldb;
+  int64_t m_real;
+  int64_t k_chunk;  // rows per split
+  float* slab;
+  int64_t slab_stride, ldc;
+  const int32_t* skip;
+};
+
+// the 8 columns c0 .. c0+7 of row r as a 16-B chunk; column m_real reads as 1 (the
+// ones-column of the bias gradient), columns past it as 0
+__device__ inline u32x4v load_row_chunk(const bfr_t* __restrict__ p, int64_t r, int64_t r_end, int64_t ld,
+                                        int64_t c0, int64_t creal, int64_t cmax, bool ones) {
+  if (r >= r_end) return u32x4v{0u, 0u, 0u, 0u};
+  if (c0 + 8 <= creal) return *reinterpret_cast<const u32x4v*>(p + r * ld + c0);
+  uint16_t v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int64_t c = c0 + q;
+    v[q] = c < creal ? p[r * ld + c] : ((ones && c == creal && c < cmax) ? (uint16_t)0x3F80 : (uint16_t)0);
+  }
+  return u32x4v{(uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
+                (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16)};
+}
+
+// 8 consecutive k (rows 8kg .. 8kg+7 of the 16-row k step `ks`) of column
+// c0 + (lane & 31) from a [rows][TLD] image: two transposing reads of 4 rows each
+__device__ inline bf16x8 tr_operand(const bfr_t* img, int c0, int ks, int lane) {
+  const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;  // lane 4q + p: row q, columns 4p .. 4p+3
+  const int kg = G >> 1, col = c0 + 16 * (G & 1) + 4 * p;
+  typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+  const bfr_t* r0 = img + (16 * ks + 8 * kg + q) * TLD + col;
+  // (the v4bf16 form and one shuffle: element-wise bit casts of the i16 form were
+  // lowered to permutes that duplicated elements)
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(r0));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(r0 + 4 * TLD));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int BN>
+__global__ __launch_bounds__(256) void gemm_bf16_tn_kernel(GemmTnArgs g) {
+  constexpr int MI = BN == 128 ? 2 : 1, NI = MI;
+  constexpr int NA = TBK * (QBM / 8) / 256, NB = TBK * (BN / 8) / 256 > 0 ? TBK * (BN / 8) / 256 : 1;
+  constexpr int STAGE = 2 * TBK * TLD;  // A image then B image
+  __shared__ __attribute__((aligned(16))) bfr_t smem[2 * STAGE];
+  if (g.skip != nullptr && *g.skip != 0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
+  const int wm = BN == 128 ? wave >> 1 : wave, wn = BN == 128 ? wave & 1 : 0;
+  const int64_t m0 = (int64_t)blockIdx.y * QBM, n0 = (int64_t)blockIdx.x * BN;
+  const int64_t kbeg = (int64_t)blockIdx.z * g.k_chunk, kend = min(g.K, kbeg + g.k_chunk);
+  const int64_t nt = kend > kbeg ? (kend - kbeg + TBK - 1) / TBK : 0;
+  // A rows: thread t stages 16-B chunk t & 15 (columns 8c) of rows t >> 4 (+ 16 i);
+  // B (BN = 128) the same; B (BN = 32): chunk t & 3 of row t >> 2 (threads < 128)
+  const int ac = threadIdx.x & 15, ar = threadIdx.x >> 4;
+  const int bcw = BN / 8, bc = threadIdx.x % bcw, br = threadIdx.x / bcw;
+  const bool b_active = threadIdx.x < TBK * bcw;
+  u32x4v ra[NA], rb[NB];
+  auto load = [&](int64_t t) {
+    const int64_t k0 = kbeg + t * TBK;
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      ra[i] = load_row_chunk(g.A, k0 + ar + 16 * i, kend, g.lda, m0 + 8 * ac, g.m_real, g.M, g.M > g.m_real);
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      rb[i] = b_active ? load_row_chunk(g.B, k0 + br + (256 / bcw) * i, kend, g.ldb, n0 + 8 * bc, g.N, g.N, false)
+                       : u32x4v{0u, 0u, 0u, 0u};
+  };
+  auto store = [&](bfr_t* st) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) *reinterpret_cast<u32x4v*>(st + (ar + 16 * i) * TLD + 8 * ac) = ra[i];
+    if (b_active)
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        *reinterpret_cast<u32x4v*>(st + TBK * TLD + (br + (256 / bcw) * i) * TLD + 8 * bc) = rb[i];
+  };
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int a = 0; a < MI; ++a)
+#pragma unroll
+    for (int b = 0; b < NI; ++b) acc[a][b] = zero16();
+  if (nt > 0) {
+    load(0);
+    store(smem);
+  }
+  for (int64_t t = 0; t < nt; ++t) {
+    __syncthreads();
+    const bfr_t* As = smem + (t & 1) * STAGE;
+    const bfr_t* Bs = As + TBK * TLD;
+    if (t + 1 < nt) load(t + 1);
+#pragma unroll
+    for (int ks = 0; ks < TBK / 16; ++ks) {
+      bf16x8 av[MI], bv[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) av[mi] = tr_operand(As, wm * 32 * MI + 32 * mi, ks, lane);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) bv[ni] = tr_operand(Bs, wn * 32 * NI + 32 * ni, ks, lane);
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA32B(av[mi], bv[ni], acc[mi][ni]);
+    }
+    if (t + 1 < nt) store(smem + ((t + 1) & 1) * STAGE);
+  }
+  float* C = g.slab + (int64_t)blockIdx.z * g.slab_stride;
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int64_t col = n0 + wn * 32 * NI + ni * 32 + j;
+      if (col >= g.N) continue;
+      const int64_t rbase = m0 + wm * 32 * MI + mi * 32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = rbase + cperm(r, h);
+        if (row < g.M) C[row * g.ldc + col] = acc[mi][ni][r];
+      }
+    }
+}
+
+// ------------------------------------------------------------------ casts / packs
+// y[r][c] = bf16(x[r][c]) for c < cols, 0 for cols <= c < ldy (zero K padding)
+__global__ void cast_rows_bf16_kernel(const float* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx,
+                                      bfr_t* __restrict__ y, int64_t ldy) {
+  const int64_t total = rows * ldy;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / ldy, c = i % ldy;
+    y[i] = c < cols ? f2bf(x[r * ldx + c]) : (bfr_t)0;
+  }
+}
+
+// W [din][dout] (f32, row-major) -> bf16 image: transpose 0: [din][ld] (= W, zero
+// columns dout..ld-1), transpose 1: [dout][ld] (= W^T, zero columns din..ld-1)
+__global__ void pack_w_bf16_kernel(const float* __restrict__ w, int64_t din, int64_t dout, int transpose,
+                                   bfr_t* __restrict__ out, int64_t ld) {
+  const int64_t rows = transpose ? dout : din, cols = transpose ? din : dout;
+  const int64_t total = rows * ld;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / ld, c = i % ld;
+    out[i] = c < cols ? f2bf(transpose ? w[c * dout + r] : w[r * dout + c]) : (bfr_t)0;
+  }
+}
+
+}  // namespace mrl
+
+using namespace mrl;
+
+extern "C" {
+
+int mrl_gemm_bf16(const mrl_gemm_bf16_desc* d, const int32_t* skip, void* stream) {
+  if (!d || !d->a || !d->bt || !d->c) return fail(E_ARG, "mrl_gemm_bf16: null pointer");
+  if ((d->a2 == nullptr) != (d->bt2 == nullptr)) return fail(E_ARG, "mrl_gemm_bf16: a2/bt2 must be both set or both null");
+  if (d->epilogue < MRL_GEMM_STORE || d->epilogue > MRL_GEMM_DTANH) return fail(E_ARG, "mrl_gemm_bf16: bad epilogue");
+  if (d->epilogue == MRL_GEMM_DTANH && !d->h) return fail(E_ARG, "mrl_gemm_bf16: DTANH needs h");
+  if ((d->lda & 7) || (d->ldb & 7) || d->lda < d->k || d->ldb < d->k)
+    return fail(E_ARG, "mrl_gemm_bf16: lda / ldb must be multiples of 8 and >= k (zero padding columns)");
+  const uintptr_t al = reinterpret_cast<uintptr_t>(d->a) | reinterpret_cast<uintptr_t>(d->bt) |
+                       reinterpret_cast<uintptr_t>(d->a2) | reinterpret_cast<uintptr_t>(d->bt2);
+  if (al & 15) return fail(E_ARG, "mrl_gemm_bf16: operands must be 16-byte aligned");
+  if (d->m <= 0 || d->n <= 0) return OK;
+  GemmB16Args g;
+  g.M = d->m;
+  g.N = d->n;
+  g.K = d->k;
+  g.A = d->a;
+  g.Bt = d->bt;
+  g.A2 = d->a2;
+  g.Bt2 = d->bt2;
+  g.lda = d->lda;
+  g.ldb = d->ldb;
+  g.C = d->c;
+  g.ldc = d->ldc;
+  g.bias = d->bias;
+  g.H = d->h;
+  g.ldh = d->ldh;
+  g.epi = d->epilogue;
+  g.skip = skip;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned gm = (unsigned)((g.M + QBM - 1) / QBM);
+  const bool bf = d->c_bf16 != 0;
+#ifndef MRL_GEMM_BF16_BK
+#define MRL_GEMM_BF16_BK 64
+#endif
+  constexpr int BK = MRL_GEMM_BF16_BK;
+  if (g.N <= 32) {
+    const dim3 grid(1, gm);
+    if (bf) hipLaunchKernelGGL((gemm_bf16_kernel<32, true, BK>), grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_bf16_kernel<32, false, BK>), grid, dim3(256), 0, s, g);
+  } else {
+    const dim3 grid((unsigned)((g.N + 127) / 128), gm);
+    if (bf) hipLaunchKernelGGL((gemm_bf16_kernel<128, true, BK>), grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_bf16_kernel<128, false, BK>), grid, dim3(256), 0, s, g);
+  }
+  return hip_check(hipGetLastError(), "mrl_gemm_bf16");
+}
+
+int mrl_gemm_bf16_tn(const mrl_gemm_bf16_tn_desc* d, const int32_t* skip, void* stream) {
+  if (!d || !d->a || !d->b || !d->slab) return fail(E_ARG, "mrl_gemm_bf16_tn: null pointer");
+  const int64_t m_real = d->m - (d->ones_row ? 1 : 0);
+  if ((d->lda & 7) || (d->ldb & 7) || d->lda < m_real || d->ldb < d->n)
+    return fail(E_ARG, "mrl_gemm_bf16_tn: lda / ldb must be multiples of 8 covering the columns");
+  if ((reinterpret_cast<uintptr_t>(d->a) | reinterpret_cast<uintptr_t>(d->b)) & 15)
+    return fail(E_ARG, "mrl_gemm_bf16_tn: operands must be 16-byte aligned");
+  if (d->m <= 0 || d->n <= 0) return OK;
+  GemmTnArgs g;
+  g.M = d->m;
+  g.N = d->n;
+  g.K = d->k;
+  g.A = d->a;
+  g.B = d->b;
+  g.lda = d->lda;
+  g.ldb = d->ldb;
+  g.m_real = m_real;
+  // the split of gemm.hip's slab GEMMs (mrl_gemm_slab_splits slabs of whole 32-row steps)
+  const int64_t req = d->splits < 1 ? 1 : d->splits;
+  g.k_chunk = ((d->k + req - 1) / req + TBK - 1) / TBK * TBK;
+  if (g.k_chunk < TBK) g.k_chunk = TBK;
+  const int64_t z = d->k > 0 ? (d->k + g.k_chunk - 1) / g.k_chunk : 1;
+  if (z > 65535) return fail(E_ARG, "mrl_gemm_bf16_tn: too many splits");
+  g.slab = d->slab;
+  g.slab_stride = d->slab_stride;
+  g.ldc = d->ldc;
+  g.skip = skip;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned gm = (unsigned)((g.M + QBM - 1) / QBM);
+  if (g.N <= 32) hipLaunchKernelGGL((gemm_bf16_tn_kernel<32>), dim3(1, gm, (unsigned)z), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((gemm_bf16_tn_kernel<128>), dim3((unsigned)((g.N + 127) / 128), gm, (unsigned)z), dim3(256), 0,
+                          s, g);
+  return hip_check(hipGetLastError(), "mrl_gemm_bf16_tn");
+}
+
+int mrl_cast_rows_bf16(const float* x, int64_t rows, int64_t cols, int64_t ldx, uint16_t* y, int64_t ldy,
+                       void* stream) {
+  if (!x || !y) return fail(E_ARG, "mrl_cast_rows_bf16: null pointer");
+  if (ldy < cols) return fail(E_ARG, "mrl_cast_rows_bf16: ldy < cols");
+  if (rows <= 0 || ldy <= 0) return OK;
+  int64_t gsz = (rows * ldy + 255) / 256;
+  if (gsz > 8192) gsz = 8192;
+  hipLaunchKernelGGL(cast_rows_bf16_kernel, dim3((unsigned)gsz), dim3(256), 0, (hipStream_t)stream, x, rows, cols, ldx,
+                     y, ldy);
+  return hip_check(hipGetLastError(), "mrl_cast_rows_bf16");
+}
+
+int mrl_pack_w_bf16(const float* w, int64_t din, int64_t dout, int32_t transpose, uint16_t* out, int64_t ld,
+                    void* stream) {
+  if (!w || !out) return fail(E_ARG, "mrl_pack_w_bf16: null pointer");
+  if (ld < (transpose ? din : dout)) return fail(E_ARG, "mrl_pack_w_bf16: ld too small");
+  const int64_t total = (transpose ? dout : din) * ld;
+  if (total <= 0) return OK;
+  int64_t gsz = (total + 255) / 256;
+  if (gsz > 4096) gsz = 4096;
+  hipLaunchKernelGGL(pack_w_bf16_kernel, dim3((unsigned)gsz), dim3(256), 0, (hipStream_t)stream, w, din, dout, transpose,
+                     out, ld);
+  return hip_check(hipGetLastError(), "mrl_pack_w_bf16");
+}
+
+}  // extern "C"

@@ -245,6 +245,11 @@ class LayeredMlpNet:
         self.ws = Workspace(self.device)
         self.desc = None
         self._tape = None  # (key, X, ldx, [H_1..H_L], Z)
+        # bf16 mode keeps the tape, the JVP / gradient chains and packed weight images in
+        # bf16 and runs the large-M passes on the bf16-operand GEMMs (csrc/gemm_bf16.hip);
+        # the rollout's per-step forward (forward_rows) stays on mrl_gemm
+        # (hidden widths a multiple of 8: the bf16 rows are 16-B aligned with no padding)
+        self.tape_bf16 = self.compute == _lib.COMPUTE_BF16 and all(h % 8 == 0 for h in self.hid_sizes)
 
     # ---- flat parameter plumbing
     def get_flat(self):
@@ -301,9 +306,64 @@ class LayeredMlpNet:
     def _key(self, theta, x, n, ep_t):
         return (theta.data_ptr(), theta._version, x.data_ptr(), int(n), None if ep_t is None else ep_t.data_ptr())
 
+    # ---- bf16 tape path
+    @staticmethod
+    def _ld8(d):
+        return (int(d) + 7) // 8 * 8
+
+    def _bf(self, name, rows, ld):
+        return self.ws.get(name, int(rows) * int(ld), torch.int16)
+
+    def _pack_images(self, vec, tag, transpose):
+        """bf16 images of the Dense kernels in flat vector `vec`: transpose 1 -> W^T
+        [dout, ld8(din)] (the B operand of X.W), 0 -> W [din, ld8(dout)] (of G.W^T)."""
+        out = []
+        for l in range(len(self.dims) - 1):
+            din, dout = self.dims[l], self.dims[l + 1]
+            rows, ld = (dout, self._ld8(din)) if transpose else (din, self._ld8(dout))
+            img = self._bf(f"{tag}{l}", rows, ld)
+            call("mrl_pack_w_bf16", self._addr(vec, self.w_off[l]), din, dout, int(transpose), ptr(img), ld, stream())
+            out.append((img, ld))
+        return out
+
+    def _cast_rows(self, x, n, cols, ldx, name):
+        ld = self._ld8(cols)
+        y = self._bf(name, n, ld)
+        call("mrl_cast_rows_bf16", ptr(x), int(n), int(cols), int(ldx), ptr(y), ld, stream())
+        return y, ld
+
+    def _gemm_b16(self, m, n, k, a, lda, bt, ldb, c, ldc, c_bf16, epi, a2=None, bt2=None, bias=None, h=None, ldh=0,
+                  skip=None):
+        g = _lib.GemmBf16Desc(m=m, n=n, k=k, a=ptr(a), lda=lda, bt=ptr(bt), ldb=ldb, a2=ptr(a2), bt2=ptr(bt2),
+                              c=ptr(c), ldc=ldc, c_bf16=int(c_bf16), epilogue=epi, bias=bias, h=ptr(h), ldh=ldh)
+        call("mrl_gemm_bf16", ctypes.byref(g), ptr(skip), stream())
+
+    def _forward_b16(self, Xb, ldx, n, theta, bufs, zbuf, skip=None):
+        """H_l = bf16(tanh(H_{l-1} W + b)) ... Z = H_L W + b (f32)."""
+        L = len(self.dims) - 1
+        wt = self._pack_images(theta, "wt", 1)
+        a, lda = Xb, ldx
+        for l in range(L):
+            din, dout = self.dims[l], self.dims[l + 1]
+            last = l == L - 1
+            out = zbuf if last else bufs[l]
+            self._gemm_b16(n, dout, din, a, lda, wt[l][0], wt[l][1], out, dout, not last,
+                           _lib.GEMM_STORE if last else _lib.GEMM_TANH, bias=self._addr(theta, self.b_off[l]),
+                           skip=skip)
+            a, lda = out, dout
+
     def _record(self, x, n, ep_t, timestep_limit, theta):
         """Forward pass at theta kept as the tape the next vjp_flat / FVP uses."""
         key = self._key(theta, x, n, ep_t)
+        if self.tape_bf16:
+            X, ldx = self._input(x, n, ep_t, timestep_limit, name="tape_x")
+            Xb, ldxb = self._cast_rows(X, n, self.n_in, ldx, "tape_xb")
+            H = [self._bf(f"tape_h{l}", n, d) for l, d in enumerate(self.hid_sizes)]
+            Z = self.ws.get("tape_z", n * self.n_out, torch.float32)
+            self._forward_b16(Xb, ldxb, n, theta, H, Z)
+            self._tape = (key, Xb, ldxb, H, Z, theta)
+            return self._tape
+        X, ldx = self._input(x, n, ep_t, timestep_limit, name="tape_x")
         X, ldx = self._input(x, n, ep_t, timestep_limit, name="tape_x")
         H = [self.ws.get(f"tape_h{l}", n * d, torch.float32) for l, d in enumerate(self.hid_sizes)]
         Z = self.ws.get("tape_z", n * self.n_out, torch.float32)
@@ -340,9 +400,15 @@ class LayeredMlpNet:
                 return
             X, ldx = self._input(x, n, ep_t, timestep_limit)
             Z = self.ws.get("fwd_z", n * self.n_out, torch.float32)
-            s0, s1 = self._scratch(n)
-            bufs = [s0 if l % 2 == 0 else s1 for l in range(len(self.hid_sizes))]
-            self._forward(X, ldx, n, theta, bufs, Z, skip)
+            if self.tape_bf16:
+                Xb, ldxb = self._cast_rows(X, n, self.n_in, ldx, "fwd_xb")
+                w = max(self.hid_sizes)
+                bufs = [self._bf(f"scrb{l % 2}", n, w) for l in range(len(self.hid_sizes))]
+                self._forward_b16(Xb, ldxb, n, theta, bufs, Z, skip)
+            else:
+                s0, s1 = self._scratch(n)
+                bufs = [s0 if l % 2 == 0 else s1 for l in range(len(self.hid_sizes))]
+                self._forward(X, ldx, n, theta, bufs, Z, skip)
         gauss = self.head == _lib.HEAD_GAUSS
         call("mrl_head_rows", int(self.head), self.n_out, int(epi), ptr(Z), ptr(dz),
              self._addr(theta, self.tls) if gauss else None,
@@ -352,6 +418,26 @@ class LayeredMlpNet:
     def _jvp(self, X, ldx, n, theta, tangent, H, dz, skip):
         """dH_1 = (X dW0 + db0)(1-H_1^2); dH_l = (dH W + H dW + db)(1-H_l^2); dZ = dH_L W + H_L dW + db."""
         L = len(self.dims) - 1
+        if self.tape_bf16:
+            wt = self._pack_images(theta, "wt", 1)
+            dwt = self._pack_images(tangent, "dwt", 1)
+            w = max(self.hid_sizes)
+            prev = None
+            for l in range(L):
+                din, dout = self.dims[l], self.dims[l + 1]
+                last = l == L - 1
+                outb = dz if last else self._bf(f"jvpb{l % 2}", n, w)
+                epi = _lib.GEMM_STORE if last else _lib.GEMM_DTANH
+                db = self._addr(tangent, self.b_off[l])
+                h = None if last else H[l]
+                if l == 0:
+                    self._gemm_b16(n, dout, din, X, ldx, dwt[0][0], dwt[0][1], outb, dout, not last, epi, bias=db,
+                                   h=h, ldh=dout, skip=skip)
+                else:
+                    self._gemm_b16(n, dout, din, prev, din, wt[l][0], wt[l][1], outb, dout, not last, epi,
+                                   a2=H[l - 1], bt2=dwt[l][0], bias=db, h=h, ldh=dout, skip=skip)
+                prev = outb
+            return
         scr = self._scratch(n)
         prev_d = None  # dH of the previous layer
         for l in range(L):
@@ -381,6 +467,10 @@ class LayeredMlpNet:
         S = int(self.lib.mrl_gemm_slab_splits(n, self.SLAB_SPLITS))
         slab = self.ws.get("slab", S * self.P, torch.float32)
         L = len(self.dims) - 1
+        if self.tape_bf16:
+            self._vjp_b16(X, ldx, H, theta, n, ghead, slab, S, skip)
+            call("mrl_reduce_rows_f32", ptr(slab), S, self.P, ptr(out), ptr(skip), stream())
+            return out
         scr = self._scratch(n)
         G, ldg = ghead, self.gh
         for l in reversed(range(L)):
@@ -407,6 +497,30 @@ class LayeredMlpNet:
                  stream())
         call("mrl_reduce_rows_f32", ptr(slab), S, self.P, ptr(out), ptr(skip), stream())
         return out
+
+    def _vjp_b16(self, Xb, ldx, H, theta, n, ghead, slab, S, skip):
+        """The bf16 VJP: per layer the weight + bias gradient as split-K slabs (the bias as
+        the ones-column of the TN GEMM) and the input gradient (G W^T)(1 - H^2) in bf16."""
+        L = len(self.dims) - 1
+        w_img = self._pack_images(theta, "wn", 0)
+        G, ldg = self._cast_rows(ghead, n, self.gh, self.gh, "vjp_g0")
+        wmax = max(self.hid_sizes)
+        for l in reversed(range(L)):
+            din, dout = self.dims[l], self.dims[l + 1]
+            inp, lda = (Xb, ldx) if l == 0 else (H[l - 1], din)
+            g = _lib.GemmBf16TnDesc(m=din + 1, n=dout, k=n, a=ptr(inp), lda=lda, b=ptr(G), ldb=ldg, ones_row=1,
+                                    splits=self.SLAB_SPLITS, slab=self._addr(slab, self.w_off[l]),
+                                    slab_stride=self.P, ldc=dout)
+            call("mrl_gemm_bf16_tn", ctypes.byref(g), ptr(skip), stream())
+            if l > 0:
+                Gn = self._bf(f"vjpb{l % 2}", n, wmax)
+                self._gemm_b16(n, din, dout, G, ldg, w_img[l][0], w_img[l][1], Gn, din, True, _lib.GEMM_DTANH,
+                               h=H[l - 1], ldh=din, skip=skip)
+                G, ldg = Gn, din
+        if self.head == _lib.HEAD_GAUSS:
+            A = self.n_out
+            call("mrl_colsum", self._addr(ghead, A), n, A, self.gh, S, self._addr(slab, self.tls), self.P, ptr(skip),
+                 stream())
 
     def forward_hidden_rows(self, x, n, bufs):
         """The hidden layers only, for a step kernel that applies the head itself; returns

@@ -51,6 +51,10 @@ int main(void) {
   P(mrl_gemm_desc, ones_row) P(mrl_gemm_desc, epilogue) P(mrl_gemm_desc, ldh) P(mrl_gemm_desc, slab_stride)
   P(mrl_rows_io, timestep_limit) P(mrl_rows_io, n) P(mrl_rows_io, inv_n_global) P(mrl_rows_io, partial)
   P(mrl_rollout_desc, seed) P(mrl_rollout_bufs, noise)
+  printf("mrl_gemm_bf16_desc %zu\\nmrl_gemm_bf16_tn_desc %zu\\n", sizeof(mrl_gemm_bf16_desc),
+         sizeof(mrl_gemm_bf16_tn_desc));
+  P(mrl_gemm_bf16_desc, c_bf16) P(mrl_gemm_bf16_desc, bias) P(mrl_gemm_bf16_desc, ldh)
+  P(mrl_gemm_bf16_tn_desc, ones_row) P(mrl_gemm_bf16_tn_desc, slab) P(mrl_gemm_bf16_tn_desc, ldc)
   return 0;
 }
 """)
@@ -70,6 +74,12 @@ int main(void) {
     assert int(out["mrl_gemm_desc"]) == ctypes.sizeof(_lib.GemmDesc)
     for f in ("ones_row", "epilogue", "ldh", "slab_stride"):
         assert int(out["mrl_gemm_desc." + f]) == getattr(_lib.GemmDesc, f).offset, f
+    assert int(out["mrl_gemm_bf16_desc"]) == ctypes.sizeof(_lib.GemmBf16Desc)
+    assert int(out["mrl_gemm_bf16_tn_desc"]) == ctypes.sizeof(_lib.GemmBf16TnDesc)
+    for f in ("c_bf16", "bias", "ldh"):
+        assert int(out["mrl_gemm_bf16_desc." + f]) == getattr(_lib.GemmBf16Desc, f).offset, f
+    for f in ("ones_row", "slab", "ldc"):
+        assert int(out["mrl_gemm_bf16_tn_desc." + f]) == getattr(_lib.GemmBf16TnDesc, f).offset, f
 
 
 def test_host_queries_match_the_reference_parameter_layout():

@@ -245,6 +245,101 @@ def test_bf16_gemm_exact_on_rounded_operands():
                 assert err < 1e-5, (M, N, K, at, bt, err)
 
 
+def _bf16_dev(a, ld):
+    """float array [r, c] -> device bf16 bits [r, ld] (RNE, zero padding) via mrl_cast_rows_bf16."""
+    import ctypes
+
+    from modular_rl_amd._lib import call, stream
+    x = _dev(np.ascontiguousarray(a, dtype=np.float32))
+    y = torch.zeros(a.shape[0] * ld, dtype=torch.int16, device="cuda")
+    call("mrl_cast_rows_bf16", ctypes.c_void_p(x.data_ptr()), a.shape[0], a.shape[1], a.shape[1],
+         ctypes.c_void_p(y.data_ptr()), ld, stream())
+    return y
+
+
+def _bf16_host(y, rows, ld, cols):
+    b = y.cpu().numpy().view(np.uint16).astype(np.uint32).reshape(rows, ld)[:, :cols] << 16
+    return b.view(np.float32).astype(np.float64)
+
+
+@pytest.mark.parametrize("epi", ["store", "tanh", "dtanh"])
+def test_bf16_operand_gemm_nn_bt(epi):
+    """mrl_gemm_bf16 (bf16 operands in memory, B as its transpose image from
+    mrl_pack_w_bf16) == the float64 product of the same bf16 operands up to f32
+    accumulation; single and dual products, K tails, both tile widths, f32 and bf16
+    outputs."""
+    import ctypes
+
+    from modular_rl_amd import _lib
+    from modular_rl_amd._lib import call, stream
+    rng = np.random.default_rng(3)
+    E = {"store": _lib.GEMM_STORE, "tanh": _lib.GEMM_TANH, "dtanh": _lib.GEMM_DTANH}[epi]
+    for (M, N, K, dual) in [(300, 200, 77, False), (1000, 17, 512, True), (129, 512, 130, True)]:
+        ldk = (K + 7) // 8 * 8
+        A, A2 = rng.standard_normal((M, K)), rng.standard_normal((M, K))
+        W, W2 = rng.standard_normal((K, N)) * 0.1, rng.standard_normal((K, N)) * 0.1
+        bias = rng.standard_normal(N).astype(np.float32)
+        H = np.tanh(rng.standard_normal((M, N)))
+        dA, dA2, dH = _bf16_dev(A, ldk), _bf16_dev(A2, ldk), _bf16_dev(H, N)
+        dW, dW2 = _dev(W.astype(np.float32)), _dev(W2.astype(np.float32))
+        Bt = torch.zeros(N * ldk, dtype=torch.int16, device="cuda")
+        Bt2 = torch.zeros(N * ldk, dtype=torch.int16, device="cuda")
+        call("mrl_pack_w_bf16", ctypes.c_void_p(dW.data_ptr()), K, N, 1, ctypes.c_void_p(Bt.data_ptr()), ldk, stream())
+        call("mrl_pack_w_bf16", ctypes.c_void_p(dW2.data_ptr()), K, N, 1, ctypes.c_void_p(Bt2.data_ptr()), ldk,
+             stream())
+        db = _dev(bias)
+        want = bfr(A) @ bfr(W)
+        if dual:
+            want = want + bfr(A2) @ bfr(W2)
+        want = want + bias.astype(np.float64)
+        if epi == "tanh":
+            want = np.tanh(want)
+        elif epi == "dtanh":
+            hb = bfr(H)
+            want = want * (1.0 - hb * hb)
+        for out_bf in (0, 1):
+            C = torch.zeros(M * N, dtype=torch.int16 if out_bf else torch.float32, device="cuda")
+            g = _lib.GemmBf16Desc(m=M, n=N, k=K, a=ctypes.c_void_p(dA.data_ptr()), lda=ldk,
+                                  bt=ctypes.c_void_p(Bt.data_ptr()), ldb=ldk,
+                                  a2=ctypes.c_void_p(dA2.data_ptr()) if dual else None,
+                                  bt2=ctypes.c_void_p(Bt2.data_ptr()) if dual else None,
+                                  c=ctypes.c_void_p(C.data_ptr()), ldc=N, c_bf16=out_bf, epilogue=E,
+                                  bias=ctypes.c_void_p(db.data_ptr()), h=ctypes.c_void_p(dH.data_ptr()), ldh=N)
+            call("mrl_gemm_bf16", ctypes.byref(g), None, stream())
+            got = _bf16_host(C, M, N, N) if out_bf else C.cpu().numpy().reshape(M, N).astype(np.float64)
+            err = np.abs(got - want).max() / np.abs(want).max()
+            assert err < (8e-3 if out_bf else 2e-5), (M, N, K, dual, out_bf, err)
+
+
+def test_bf16_operand_gemm_tn_slabs():
+    """mrl_gemm_bf16_tn: split-K weight-gradient slabs of two bf16 row-major operands,
+    with and without the ones-column (bias gradient), summed over the slabs, equal the
+    float64 product of the bf16 operands."""
+    import ctypes
+
+    from modular_rl_amd import _lib
+    from modular_rl_amd._lib import call, stream
+    rng = np.random.default_rng(5)
+    for (R, din, dout, ones) in [(3000, 376, 512, True), (2500, 512, 17, False), (777, 96, 80, True)]:
+        lda, ldb = (din + 7) // 8 * 8, (dout + 7) // 8 * 8
+        X, G = rng.standard_normal((R, din)), rng.standard_normal((R, dout))
+        dX, dG = _bf16_dev(X, lda), _bf16_dev(G, ldb)
+        M = din + (1 if ones else 0)
+        S = int(_lib.load().mrl_gemm_slab_splits(R, 64))
+        slab = torch.full((S * M * dout,), float("nan"), dtype=torch.float32, device="cuda")
+        g = _lib.GemmBf16TnDesc(m=M, n=dout, k=R, a=ctypes.c_void_p(dX.data_ptr()), lda=lda,
+                                b=ctypes.c_void_p(dG.data_ptr()), ldb=ldb, ones_row=int(ones), splits=64,
+                                slab=ctypes.c_void_p(slab.data_ptr()), slab_stride=M * dout, ldc=dout)
+        call("mrl_gemm_bf16_tn", ctypes.byref(g), None, stream())
+        got = slab.cpu().numpy().reshape(S, M, dout).astype(np.float64).sum(0)
+        Xb = bfr(X)
+        if ones:
+            Xb = np.concatenate([Xb, np.ones((R, 1))], axis=1)
+        want = Xb.T @ bfr(G)
+        err = np.abs(got - want).max() / np.abs(want).max()
+        assert err < 2e-5, (R, din, dout, ones, err)
+
+
 @pytest.mark.parametrize("head,nin,nout", [("gauss", 40, 9), ("softmax", 30, 4)])
 def test_bf16_layered_fvp_and_gradient(head, nin, nout):
     """Layered GEMM path (hid 96,80) in bf16: Fisher product and gradient at the bf16 bound."""
