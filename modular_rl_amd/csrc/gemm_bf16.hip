@@ -131,46 +131,60 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmB16Args g) {
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA32B(av[mi], bv[ni], acc[mi][ni]);
+        for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA32B(bv[ni], av[mi], acc[mi][ni]);  // C^T tiles
     }
     if (t + 1 < nt) store(smem + ((t + 1) & 1) * STAGE);
   }
-  // epilogue: lane holds column j, rows cperm(r, h) of each 32x32 tile
+  // epilogue: the accumulators hold C^T tiles, so lane (j, h) holds ROW j of each 32x32
+  // C tile, at columns cperm(r, h): four runs of 4 consecutive columns (8q + 4h + 0..3),
+  // each one 8-B (bf16) / 16-B (f32) store, bias and H loads likewise vectorised
+  const bool vec = (g.ldc & 3) == 0 && (g.epi != MRL_GEMM_DTANH || (g.ldh & 3) == 0);
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
-      const int64_t col = n0 + wn * 32 * NI + ni * 32 + j;
-      if (col >= g.N) continue;
-      const int64_t rbase = m0 + wm * 32 * MI + mi * 32;
-      const float bv = g.bias != nullptr ? g.bias[col] : 0.f;
-      if (rbase + 32 <= g.M) {
-        // full row range: the 16 H loads issue together, then the stores
-        float hv[16];
-        if (g.epi == MRL_GEMM_DTANH) {
+      const int64_t row = m0 + wm * 32 * MI + mi * 32 + j;
+      if (row >= g.M) continue;
+      const int64_t cbase = n0 + wn * 32 * NI + ni * 32;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) hv[r] = bf2f(g.H[(rbase + cperm(r, h)) * g.ldh + col]);
+      for (int q = 0; q < 4; ++q) {
+        const int64_t c0 = cbase + 8 * q + 4 * h;
+        float v[4];
+        if (vec && c0 + 4 <= g.N) {
+          const float4 b = g.bias != nullptr ? *reinterpret_cast<const float4*>(g.bias + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+          v[0] = acc[mi][ni][4 * q + 0] + b.x;
+          v[1] = acc[mi][ni][4 * q + 1] + b.y;
+          v[2] = acc[mi][ni][4 * q + 2] + b.z;
+          v[3] = acc[mi][ni][4 * q + 3] + b.w;
+          if (g.epi == MRL_GEMM_TANH) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = tanh_fast(v[e]);
+          } else if (g.epi == MRL_GEMM_DTANH) {
+            const uint2 hb = *reinterpret_cast<const uint2*>(g.H + row * g.ldh + c0);
+            v[0] *= dtanh(__uint_as_float(hb.x << 16));
+            v[1] *= dtanh(__uint_as_float(hb.x & 0xffff0000u));
+            v[2] *= dtanh(__uint_as_float(hb.y << 16));
+            v[3] *= dtanh(__uint_as_float(hb.y & 0xffff0000u));
+          }
+          if (OUTBF) {
+            const uint2 o = {(uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                             (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)};
+            *reinterpret_cast<uint2*>(reinterpret_cast<bfr_t*>(g.C) + row * g.ldc + c0) = o;
+          } else {
+            *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + row * g.ldc + c0) = make_float4(v[0], v[1], v[2], v[3]);
+          }
+          continue;
         }
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t row = rbase + cperm(r, h);
-          float v = acc[mi][ni][r] + bv;
-          if (g.epi == MRL_GEMM_TANH) v = tanh_fast(v);
-          else if (g.epi == MRL_GEMM_DTANH) v *= dtanh(hv[r]);
-          if (OUTBF) reinterpret_cast<bfr_t*>(g.C)[row * g.ldc + col] = f2bf(v);
-          else reinterpret_cast<float*>(g.C)[row * g.ldc + col] = v;
+        for (int e = 0; e < 4; ++e) {
+          const int64_t col = c0 + e;
+          if (col >= g.N) continue;
+          float x = acc[mi][ni][4 * q + e] + (g.bias != nullptr ? g.bias[col] : 0.f);
+          if (g.epi == MRL_GEMM_TANH) x = tanh_fast(x);
+          else if (g.epi == MRL_GEMM_DTANH) x *= dtanh(bf2f(g.H[row * g.ldh + col]));
+          if (OUTBF) reinterpret_cast<bfr_t*>(g.C)[row * g.ldc + col] = f2bf(x);
+          else reinterpret_cast<float*>(g.C)[row * g.ldc + col] = x;
         }
-        continue;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = rbase + cperm(r, h);
-        if (row >= g.M) continue;
-        float v = acc[mi][ni][r] + bv;
-        if (g.epi == MRL_GEMM_TANH) v = tanh_fast(v);
-        else if (g.epi == MRL_GEMM_DTANH) v *= dtanh(bf2f(g.H[row * g.ldh + col]));
-        if (OUTBF) reinterpret_cast<bfr_t*>(g.C)[row * g.ldc + col] = f2bf(v);
-        else reinterpret_cast<float*>(g.C)[row * g.ldc + col] = v;
       }
     }
 }
