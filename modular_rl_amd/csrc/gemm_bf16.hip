@@ -158,7 +158,11 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmB16Args g) {
           v[3] = acc[mi][ni][4 * q + 3] + b.w;
           if (g.epi == MRL_GEMM_TANH) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = tanh_fast(v[e]);
+            for (int e = 0; e < 4; e += 2) {
+              const f32x2 t = tanh_fast2(f32x2{v[e], v[e + 1]});
+              v[e] = t.x;
+              v[e + 1] = t.y;
+            }
           } else if (g.epi == MRL_GEMM_DTANH) {
             const uint2 hb = *reinterpret_cast<const uint2*>(g.H + row * g.ldh + c0);
             v[0] *= dtanh(__uint_as_float(hb.x << 16));

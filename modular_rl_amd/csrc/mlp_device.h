@@ -111,12 +111,42 @@ __device__ inline float tanh_fast(float x) {
   return ax < 0.125f ? p : r;
 }
 
+// tanh_fast of two values with packed f32 math (v_pk_mul / v_pk_fma / v_pk_add for the
+// polynomial, the exponent argument and the reciprocal's affine step): the same IEEE
+// operations in the same order as tanh_fast, so every element has tanh_fast's bits
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ inline f32x2 tanh_fast2(f32x2 x) {
+  const f32x2 ax = __builtin_elementwise_abs(x);
+  const f32x2 x2 = x * x;
+  f32x2 q = __builtin_elementwise_fma(x2, (f32x2)(-0.0539682545f), (f32x2)(0.133333340f));
+  q = __builtin_elementwise_fma(x2, q, (f32x2)(-0.333333343f));
+  q = __builtin_elementwise_fma(x2, q, (f32x2)(1.f));
+  const f32x2 p = x * q;
+  const f32x2 y = (ax + ax) * (f32x2)(__uint_as_float(0x3fb8aa3bu));  // __expf(2|x|) = exp2(2|x| log2 e)
+  f32x2 e;
+  e.x = __builtin_amdgcn_exp2f(y.x);
+  e.y = __builtin_amdgcn_exp2f(y.y);
+  const f32x2 d = e + (f32x2)(1.f);
+  f32x2 r;
+  r.x = __builtin_amdgcn_rcpf(d.x);
+  r.y = __builtin_amdgcn_rcpf(d.y);
+  const f32x2 t = __builtin_elementwise_fma((f32x2)(-2.f), r, (f32x2)(1.f));
+  f32x2 o;
+  o.x = ax.x < 0.125f ? p.x : copysignf(t.x, x.x);
+  o.y = ax.y < 0.125f ? p.y : copysignf(t.y, x.y);
+  return o;
+}
+
 // tanh' from the activation, 1 - h^2, as one explicit fma (see tanh_fast)
 __device__ inline float dtanh(float h) { return fmaf(-h, h, 1.f); }
 
 __device__ inline void tanh16(f32x16& a) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) a[r] = tanh_fast(a[r]);
+  for (int r = 0; r < 16; r += 2) {
+    const f32x2 t = tanh_fast2(f32x2{a[r], a[r + 1]});
+    a[r] = t.x;
+    a[r + 1] = t.y;
+  }
 }
 
 // Head (A <= 8 outputs) on VALU: a 32-wide MFMA tile would be >= 75 % padding.

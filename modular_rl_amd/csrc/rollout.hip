@@ -222,7 +222,11 @@ __device__ inline void tanh4r(f32x4& a) {
   return;
 #endif
 #pragma unroll
-  for (int r = 0; r < 4; ++r) a[r] = BF ? bf16r(tanh_fast(a[r])) : tanh_fast(a[r]);
+  for (int r = 0; r < 4; r += 2) {
+    const f32x2 t = tanh_fast2(f32x2{a[r], a[r + 1]});
+    a[r] = BF ? bf16r(t.x) : t.x;
+    a[r + 1] = BF ? bf16r(t.y) : t.y;
+  }
 }
 
 // head rows z[o] of the wave's 16 envs (every lane of an env's column ends with all A).
