@@ -365,6 +365,47 @@ def test_bf16_layered_fvp_and_gradient(head, nin, nout):
     assert _rel(fv.cpu().numpy(), want) < BF16_ORACLE_RTOL
 
 
+def test_bf16_layered_humanoid_shape():
+    """C5's net (376-512-512-512-17, DiagGauss) on the bf16 tape: the K = 376 first
+    layer (input rows cast with zero padding), the 512-wide layers whose bias gradient
+    needs an extra ones-row tile (din % 128 == 0), the 17-wide head; Fisher product,
+    policy gradient and the forward against the float64 oracle at the bf16 bound."""
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import make_net
+    N, nin, nout, hid = 1500, 376, 17, [512, 512, 512]
+    rng = np.random.default_rng(13)
+    spec = T.Spec(nin, hid, nout, "gauss")
+    th = (T.mlp_init(rng, spec.shapes, True) + 0.02 * rng.standard_normal(spec.P)).astype(np.float32)
+    th = th.astype(np.float64)
+    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
+    net = make_net(nin, nout, _lib.HEAD_GAUSS, hid, impl="layered", dtype="bf16")
+    assert net.tape_bf16
+    net.set_flat(th)
+    x = _dev(ob)
+    # forward (prob rows: mean, std)
+    out = net.forward(x, N).cpu().numpy().astype(np.float64)
+    z, _ = T.mlp_forward(spec, th, ob)
+    assert _rel(out[:, :nout], z) < BF16_ORACLE_RTOL
+    # Fisher product
+    v = rng.standard_normal(spec.P).astype(np.float32).astype(np.float64)
+    ghead = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+    net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=ghead, tangent=_dev(v))
+    fv = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(x, N, ghead, fv)
+    assert _rel(fv.cpu().numpy(), T.fisher_vector_product(spec, th, v, ob)) < BF16_ORACLE_RTOL
+    # policy gradient of the surrogate (as test_bf16_losses_and_policy_gradient)
+    oldth = th + 0.01 * rng.standard_normal(spec.P)
+    oldprob = T.policy_prob(spec, oldth, ob).astype(np.float32).astype(np.float64)
+    act = T.sample(spec, oldprob, rng.standard_normal((N, nout))).astype(np.float32).astype(np.float64)
+    adv = rng.standard_normal(N).astype(np.float32).astype(np.float64)
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=_dev(act), adv=_dev(adv), oldprob=_dev(oldprob),
+             ghead=ghead, partial=partial)
+    g = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(x, N, ghead, g)
+    assert _rel(g.cpu().numpy(), T.policy_gradient(spec, th, ob, act, adv, oldprob)) < 5e-2
+
+
 @pytest.mark.parametrize("env_id", ["CartPole-v0", "Hopper-v2"])
 def test_bf16_rollout_prob_rows_equal_update_forward(env_id):
     """bf16 mode: the rollout's fused forward rounds W0, W1, x, h1, h2 like
