@@ -317,9 +317,13 @@ __device__ inline void forward16(const RWeightsB<O, A>& w, const XL& xl, int lan
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      hb[p][r] = (__bf16)tanh_fast(h1[2 * p][r]);
-      hb[p][4 + r] = (__bf16)tanh_fast(h1[2 * p + 1][r]);
+    for (int r = 0; r < 4; r += 2) {
+      const f32x2 ta = tanh_fast2(f32x2{h1[2 * p][r], h1[2 * p][r + 1]});
+      const f32x2 tb = tanh_fast2(f32x2{h1[2 * p + 1][r], h1[2 * p + 1][r + 1]});
+      hb[p][r] = (__bf16)ta.x;
+      hb[p][r + 1] = (__bf16)ta.y;
+      hb[p][4 + r] = (__bf16)tb.x;
+      hb[p][4 + r + 1] = (__bf16)tb.y;
     }
 #pragma unroll
   for (int p = 0; p < 2; ++p)
