@@ -72,7 +72,9 @@ class HipTrpoOps:
         net.rows(_lib.EPI_SURRGRAD, b.obs, b.n, inv_n_global=self.inv_ng, act=b.act, adv=b.adv, oldprob=b.prob,
                  ghead=self.ghead, partial=self.partial)
         net.reduce_partial(self.partial, b.n, self.sums)
+        timing.start("pg_vjp")
         net.vjp_flat(b.obs, b.n, self.ghead, self.g)
+        timing.stop("pg_vjp")
         return self.g, self.sums
 
     def losses(self, theta):

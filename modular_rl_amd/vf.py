@@ -15,7 +15,7 @@ import numpy as np
 import scipy.optimize
 import torch
 
-from . import _lib
+from . import _lib, timing
 from ._lib import call, ptr, stream
 from .dist import Comm
 
@@ -71,7 +71,9 @@ class LbfgsOptimizer:
                  ghead=ghead, partial=partial)
         net.reduce_partial(partial, n, self.sums)
         if with_grad:
+            timing.start("vf_vjp")
             net.vjp_flat(x, n, ghead, self.g, ep_t=ep_t, timestep_limit=limit)
+            timing.stop("vf_vjp")
             self.comm.allreduce_(self.g)
         self.comm.allreduce_(self.sums)
         th = net.theta.detach().double().cpu().numpy()
