@@ -260,8 +260,8 @@ def main():
                                                r: {"launches": c, "mean_ms": round(m, 5), "ms_per_iter": round(t / K, 3)}
                                                for r, (c, m, t) in parts.items()})
     if "rollout_steps" in kern:
-        # one timed region per iteration around the T step launches (graph replay on the
-        # rollout stream): the step-to-step mean, so it carries the inter-launch gap
+        # one timed region per iteration around the rollout's launches (the persistent
+        # kernel over the T steps, in a graph on the rollout stream): region / T per step
         cnt, mean_ms, tot_ms = kern["rollout_steps"]
         kinfo["rollout_step"] = dict(launches=cnt * Tn, mean_ms=mean_ms / Tn, total_ms=tot_ms, rows_per_launch=E,
                                      flop_per_row=fpr["policy_forward"], step_to_step=True)
@@ -289,9 +289,9 @@ def main():
                             "evaluations); achieved = their algorithmic FLOP / their summed HIP-event durations; "
                             "traffic: the Fisher-product launch's PMC bytes")
     if dom == "rollout_step":
-        roofline["note"] = ("latency-bound: T dependent step launches, each a filter merge over all envs + the "
-                            "policy forward (the FLOPs counted) + fp64 env substeps, on E/64 CUs; mean is "
-                            "step-to-step (launch gap included)")
+        roofline["note"] = ("latency-bound: one persistent launch runs the T steps, each a filter merge over all "
+                            "envs (cross-block hand-off) + the policy forward (the FLOPs counted) + fp64 env "
+                            "substeps, on E/64 CUs; mean = rollout region / T")
     gae = None
     if "gae_scan" in kern:
         cnt, mean_ms, _ = kern["gae_scan"]
