@@ -41,6 +41,11 @@ typedef struct {
   int32_t head;    /* MRL_HEAD_*                                              */
   int32_t n_hidden;/* must be 64                                              */
   int32_t n_layers;/* must be 2                                               */
+  int32_t cus;     /* CUs the row passes and the VJP are sized for (0: all 256):
+                    * the grid caps scale with it, so passes issued on a stream
+                    * restricted to that many CUs run in whole rounds.  Part of
+                    * the result's identity: the per-wave partial sums follow
+                    * the grid, so runs compared bit for bit use the same value */
 } mrl_mlp_desc;
 
 const char* mrl_last_error(void);
@@ -103,6 +108,9 @@ int64_t mrl_act_cache_floats(int64_t n);
 
 int64_t mrl_partial_rows(int64_t n);  /* rows of `partial` a call over n rows writes */
 int64_t mrl_slab_rows(int64_t n);     /* rows of the mrl_mlp_vjp slab                */
+/* the same for a desc whose `cus` is set (the two above: cus = 0) */
+int64_t mrl_mlp_partial_rows(const mrl_mlp_desc* d, int64_t n);
+int64_t mrl_mlp_slab_rows(const mrl_mlp_desc* d, int64_t n);
 
 /* fused forward (+ JVP for EPI_FVP) with a per-row epilogue.
  * theta: flat fp32 params (for logstd); image: packed primal image;
@@ -132,6 +140,8 @@ int64_t mrl_mlp_image_words_bf16(const mrl_mlp_desc* d);
 int64_t mrl_act_cache_words_bf16(int64_t n);
 int64_t mrl_partial_rows_bf16(int64_t n);
 int64_t mrl_slab_rows_bf16(int64_t n);
+int64_t mrl_mlp_partial_rows_bf16(const mrl_mlp_desc* d, int64_t n);
+int64_t mrl_mlp_slab_rows_bf16(const mrl_mlp_desc* d, int64_t n);
 int mrl_mlp_pack_bf16(const mrl_mlp_desc* d, const float* theta, float* image, int32_t fwd_only,
                       const int32_t* skip, void* stream);
 int mrl_mlp_rows_bf16(const mrl_mlp_desc* d, int32_t epi, const float* theta, const float* image,

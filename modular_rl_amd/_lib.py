@@ -33,7 +33,7 @@ class MrlError(RuntimeError):
 
 
 class MlpDesc(ctypes.Structure):
-    _fields_ = [("n_in", i32), ("n_out", i32), ("head", i32), ("n_hidden", i32), ("n_layers", i32)]
+    _fields_ = [("n_in", i32), ("n_out", i32), ("head", i32), ("n_hidden", i32), ("n_layers", i32), ("cus", i32)]
 
 
 class RowsIO(ctypes.Structure):
@@ -82,12 +82,16 @@ SIGNATURES = {
     "mrl_partial_rows": (i64, [i64]),
     "mrl_act_cache_floats": (i64, [i64]),
     "mrl_slab_rows": (i64, [i64]),
+    "mrl_mlp_partial_rows": (i64, [vp, i64]),
+    "mrl_mlp_slab_rows": (i64, [vp, i64]),
     "mrl_mlp_rows": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_mlp_vjp": (i32, [vp, vp, vp, vp, f64, vp, i64, vp, vp, vp, vp]),
     "mrl_mlp_image_words_bf16": (i64, [vp]),
     "mrl_act_cache_words_bf16": (i64, [i64]),
     "mrl_partial_rows_bf16": (i64, [i64]),
     "mrl_slab_rows_bf16": (i64, [i64]),
+    "mrl_mlp_partial_rows_bf16": (i64, [vp, i64]),
+    "mrl_mlp_slab_rows_bf16": (i64, [vp, i64]),
     "mrl_mlp_pack_bf16": (i32, [vp, vp, vp, i32, vp, vp]),
     "mrl_mlp_rows_bf16": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_mlp_vjp_bf16": (i32, [vp, vp, vp, vp, f64, vp, i64, vp, vp, vp, vp]),

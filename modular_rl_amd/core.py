@@ -212,11 +212,16 @@ class IterationRunner:
         self.pipeline = False
         self.last_phase_events = None
         self.last_drain_events = {}
-        if pipeline and torch.cuda.is_available():
+        if torch.cuda.is_available():
             from . import streams
             need = rollout_cus_needed(collector)
             split = rollout_cu_split(need, streams.cu_count())
-            if split is not None:
+            # the VF passes are sized for the fit's CU set in BOTH orders: their partial
+            # sums follow the grid, and the two orders stay bit-identical
+            vf_net = getattr(getattr(agent, "baseline", None), "net", None)
+            if split is not None and hasattr(vf_net, "size_for_cus"):
+                vf_net.size_for_cus(len(split[1]))
+            if pipeline and split is not None:
                 self.rollout_stream = streams.masked_stream(split[0])
                 self.fit_stream = streams.masked_stream(split[1])
                 # the iteration's own work runs on a non-blocking stream: an event recorded

@@ -643,6 +643,7 @@ static int check_desc_b(const mrl_mlp_desc* d) {
   if (d->n_out < 1 || d->n_out > MAX_OUT) return fail(E_UNSUPPORTED, "n_out must be in [1, 8]");
   if (d->head < 0 || d->head > 2) return fail(E_ARG, "bad head kind");
   if (d->head == MRL_HEAD_LINEAR && d->n_out != 1) return fail(E_ARG, "linear head needs n_out=1");
+  if (d->cus < 0 || d->cus > 1024) return fail(E_ARG, "cus must be in [0, 1024]");
   return OK;
 }
 
@@ -654,20 +655,24 @@ static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // the forward passes (≤ 128 VGPRs) at three rounds and more (3072: surrgrad 0.526,
 // prob 0.299 ms; 2048: 0.538 / 0.303).
 constexpr int ROWS_FVP_BLOCKS_B = 768;
-static int64_t rows_blocks_b(int64_t n, bool fvp = false) {
+// caps per 256 CUs, scaled by the desc's `cus` (mlp_kernels.hip desc_cus)
+static int64_t desc_cus_b(const mrl_mlp_desc* d) { return d != nullptr && d->cus > 0 ? d->cus : 256; }
+static int64_t scaled_cap(int64_t cap, int64_t cus) { return cap * cus / 256 > 0 ? cap * cus / 256 : 1; }
+static int64_t rows_blocks_b(int64_t n, bool fvp = false, int64_t cus = 256) {
   static const int64_t env_cap = [] {
     const char* e = getenv("MRL_ROWS_BF16_BLOCKS");
     return (int64_t)(e ? atoi(e) : 0);
   }();
-  const int64_t cap = env_cap > 0 ? env_cap : (fvp ? ROWS_FVP_BLOCKS_B : ROWS_MAX_BLOCKS_B);
+  const int64_t cap = env_cap > 0 ? env_cap : scaled_cap(fvp ? ROWS_FVP_BLOCKS_B : ROWS_MAX_BLOCKS_B, cus);
   int64_t g = cdiv(cdiv(n, 32), 4);
   if (g < 1) g = 1;
   return g > cap ? cap : g;
 }
-static int64_t vjp_blocks_b(int64_t n) {
+static int64_t vjp_blocks_b(int64_t n, int64_t cus = 256) {
   int64_t g = cdiv(cdiv(n, 32), 4);
   if (g < 1) g = 1;
-  return g > VJP_MAX_BLOCKS_B ? VJP_MAX_BLOCKS_B : g;
+  const int64_t cap = scaled_cap(VJP_MAX_BLOCKS_B, cus);
+  return g > cap ? cap : g;
 }
 
 extern "C" {
@@ -679,6 +684,14 @@ int64_t mrl_mlp_image_words_bf16(const mrl_mlp_desc* d) {
 int64_t mrl_act_cache_words_bf16(int64_t n) { return cdiv(n, 32) * BCACHE_TILE_WORDS; }
 int64_t mrl_partial_rows_bf16(int64_t n) { return rows_blocks_b(n) * 4; }
 int64_t mrl_slab_rows_bf16(int64_t n) { return vjp_blocks_b(n) * 4; }
+int64_t mrl_mlp_partial_rows_bf16(const mrl_mlp_desc* d, int64_t n) {
+  if (check_desc_b(d) != OK) return -1;
+  return rows_blocks_b(n, false, desc_cus_b(d)) * 4;
+}
+int64_t mrl_mlp_slab_rows_bf16(const mrl_mlp_desc* d, int64_t n) {
+  if (check_desc_b(d) != OK) return -1;
+  return vjp_blocks_b(n, desc_cus_b(d)) * 4;
+}
 
 int mrl_mlp_pack_bf16(const mrl_mlp_desc* d, const float* theta, float* image, int32_t fwd_only,
                       const int32_t* skip, void* stream) {
@@ -758,7 +771,8 @@ int mrl_mlp_rows_bf16(const mrl_mlp_desc* d, int32_t epi, const float* theta, co
   const BDims b = bf16_dims(d->n_in, d->n_out);
   const size_t shm = (size_t)b.fwd_words * 4 * (epi == MRL_EPI_FVP ? 2 : 1);
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(epi == MRL_EPI_PPOSGD ? 1 : rows_blocks_b(io->n, epi == MRL_EPI_FVP)), blk(ROWS_BLOCK_B);
+  const dim3 grid(epi == MRL_EPI_PPOSGD ? 1 : rows_blocks_b(io->n, epi == MRL_EPI_FVP, desc_cus_b(d))),
+      blk(ROWS_BLOCK_B);
   // the benchmark nets as static shapes (plain rows; a time-feature column built from
   // ep_t takes the generic kernel); policy epilogues only for the policy shapes
   int sh = 0;
@@ -811,7 +825,7 @@ int mrl_mlp_vjp_bf16(const mrl_mlp_desc* d, const float* image, const float* x, 
   a.slab = slab;
   a.cache = act_cache;
   const size_t shm = (size_t)a.b.total_words * 4;
-  const dim3 grid(vjp_blocks_b(n)), blk(256);
+  const dim3 grid(vjp_blocks_b(n, desc_cus_b(d))), blk(256);
   hipStream_t s = (hipStream_t)stream;
   // the benchmark policies as static shapes (plain rows only; the VF's time feature
   // column takes the generic kernel)

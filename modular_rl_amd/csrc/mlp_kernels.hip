@@ -638,6 +638,7 @@ static int check_desc(const mrl_mlp_desc* d) {
   if (d->n_out < 1 || d->n_out > MAX_OUT) return fail(E_UNSUPPORTED, "n_out must be in [1, 8]");
   if (d->head < 0 || d->head > 2) return fail(E_ARG, "bad head kind");
   if (d->head == MRL_HEAD_LINEAR && d->n_out != 1) return fail(E_ARG, "linear head needs n_out=1");
+  if (d->cus < 0 || d->cus > 1024) return fail(E_ARG, "cus must be in [0, 1024]");
   return OK;
 }
 
@@ -658,15 +659,20 @@ static int static_shape_of(const mrl_mlp_desc* d, bool has_ept) {
 #endif
 }
 
-static int64_t rows_blocks(int64_t n) {
+// grid caps for passes sized for `cus` CUs (the caps are per 256): the VJP runs one
+// block per CU, so on a fit stream of 192 CUs a 256-block grid would take two rounds
+static int64_t desc_cus(const mrl_mlp_desc* d) { return d != nullptr && d->cus > 0 ? d->cus : 256; }
+static int64_t rows_blocks(int64_t n, int64_t cus = 256) {
   int64_t b = ceil_div(ceil_div(n, 32), 4);
   if (b < 1) b = 1;
-  return b > ROWS_MAX_BLOCKS ? ROWS_MAX_BLOCKS : b;
+  const int64_t cap = ROWS_MAX_BLOCKS * cus / 256 > 0 ? ROWS_MAX_BLOCKS * cus / 256 : 1;
+  return b > cap ? cap : b;
 }
-static int64_t vjp_blocks(int64_t n) {
+static int64_t vjp_blocks(int64_t n, int64_t cus = 256) {
   int64_t b = ceil_div(ceil_div(n, 32), 4);
   if (b < 1) b = 1;
-  return b > VJP_MAX_BLOCKS ? VJP_MAX_BLOCKS : b;
+  const int64_t cap = VJP_MAX_BLOCKS * cus / 256 > 0 ? VJP_MAX_BLOCKS * cus / 256 : 1;
+  return b > cap ? cap : b;
 }
 
 extern "C" {
@@ -685,6 +691,14 @@ int64_t mrl_mlp_image_floats(const mrl_mlp_desc* d) {
 int64_t mrl_partial_rows(int64_t n) { return rows_blocks(n) * 4; }
 int64_t mrl_act_cache_floats(int64_t n) { return ceil_div(n, 32) * CACHE_TILE_FLOATS; }
 int64_t mrl_slab_rows(int64_t n) { return vjp_blocks(n) * 4; }
+int64_t mrl_mlp_partial_rows(const mrl_mlp_desc* d, int64_t n) {
+  if (check_desc(d) != OK) return -1;
+  return rows_blocks(n, desc_cus(d)) * 4;
+}
+int64_t mrl_mlp_slab_rows(const mrl_mlp_desc* d, int64_t n) {
+  if (check_desc(d) != OK) return -1;
+  return vjp_blocks(n, desc_cus(d)) * 4;
+}
 
 int mrl_mlp_pack(const mrl_mlp_desc* d, const float* theta, float* image, int32_t fwd_only, const int32_t* skip,
                  void* stream) {
@@ -759,7 +773,7 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
     default:
       return fail(E_ARG, "unknown epilogue");
   }
-  const int64_t blocks = rows_blocks(io->n);
+  const int64_t blocks = rows_blocks(io->n, desc_cus(d));
   size_t shm = (size_t)a.d.fwd_size * 4 * (epi == MRL_EPI_FVP ? 2 : 1);
   hipStream_t s = (hipStream_t)stream;
   const int sh = static_shape_of(d, io->ep_t != nullptr);
@@ -807,7 +821,7 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
   a.n = n;
   a.ghead = ghead;
   a.slab = slab;
-  const int64_t blocks = vjp_blocks(n);
+  const int64_t blocks = vjp_blocks(n, desc_cus(d));
   size_t shm = ((size_t)a.d.total_size + 4 * (size_t)SCR_FLOATS) * 4;
   a.cache = act_cache;
   const bool wide = a.d.O > 16;

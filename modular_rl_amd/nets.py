@@ -171,14 +171,23 @@ class MlpNet:
         words = (self.lib.mrl_act_cache_words_bf16 if self.bf16 else self.lib.mrl_act_cache_floats)(int(n))
         return self.ws.get("act_cache", int(words), torch.float32)
 
+    def size_for_cus(self, cus):
+        """Size the row passes' and the VJP's grids for a stream of ``cus`` CUs (0: the
+        whole device): the VF fit runs beside the rollout on a CU subset, where a grid
+        sized for all CUs would leave a partial second round.  The per-wave partial sums
+        follow the grid, so both iteration orders set the same value (core.IterationRunner)."""
+        self.desc.cus = int(cus)
+
     def partial_rows(self, n):
-        return int((self.lib.mrl_partial_rows_bf16 if self.bf16 else self.lib.mrl_partial_rows)(int(n)))
+        fn = self.lib.mrl_mlp_partial_rows_bf16 if self.bf16 else self.lib.mrl_mlp_partial_rows
+        return int(fn(ctypes.byref(self.desc), int(n)))
 
     def vjp_flat(self, x, n, ghead, out, ep_t=None, timestep_limit=1.0, image=None, skip=None):
         """out[P] (fp32) <- sum_n J_n^T ghead_n (per-wave slab + deterministic reduce); the
         forward comes from the activation cache when the last recording pass was at
         self.theta on the same rows."""
-        rows = int((self.lib.mrl_slab_rows_bf16 if self.bf16 else self.lib.mrl_slab_rows)(int(n)))
+        fn = self.lib.mrl_mlp_slab_rows_bf16 if self.bf16 else self.lib.mrl_mlp_slab_rows
+        rows = int(fn(ctypes.byref(self.desc), int(n)))
         slab = self.ws.get("slab", rows * self.P, torch.float32)
         cache = None
         if self.use_cache and image is None and self._cache_key == self._key(x, n, ep_t, timestep_limit):
@@ -262,6 +271,9 @@ class LayeredMlpNet:
 
     def pack(self, theta=None, image=None, fwd_only=False, skip=None):
         """No image on the layered path: the GEMMs read theta directly."""
+
+    def size_for_cus(self, cus):
+        """The layered path's GEMM grids do not depend on it (no CU split is applied)."""
 
     def partial_rows(self, n):
         return int(self.lib.mrl_partial_rows(int(n)))

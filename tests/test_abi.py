@@ -100,6 +100,27 @@ def test_host_queries_match_the_reference_parameter_layout():
     assert lib.mrl_filter_doubles(_lib.ENV_CARTPOLE) == 2 + 2 * 5
 
 
+def test_grids_sized_for_a_cu_subset():
+    """desc.cus scales the grid caps (VF passes beside the rollout on 192 CUs): the VJP
+    one block per CU, the row passes six; cus = 0 is the whole device (256)."""
+    from modular_rl_amd import _lib
+    lib = _lib.load()
+    n = 4096 * 1024
+    whole = _lib.MlpDesc(12, 1, _lib.HEAD_LINEAR, 64, 2)
+    fit = _lib.MlpDesc(12, 1, _lib.HEAD_LINEAR, 64, 2, 192)
+    for f, bf in [("mrl_mlp_slab_rows", "mrl_slab_rows"), ("mrl_mlp_partial_rows", "mrl_partial_rows"),
+                  ("mrl_mlp_slab_rows_bf16", "mrl_slab_rows_bf16"),
+                  ("mrl_mlp_partial_rows_bf16", "mrl_partial_rows_bf16")]:
+        assert getattr(lib, f)(ctypes.byref(whole), n) == getattr(lib, bf)(n)
+    assert lib.mrl_mlp_slab_rows(ctypes.byref(whole), n) == 256 * 4
+    assert lib.mrl_mlp_slab_rows(ctypes.byref(fit), n) == 192 * 4
+    assert lib.mrl_mlp_partial_rows(ctypes.byref(fit), n) == 6 * 192 * 4
+    assert lib.mrl_mlp_slab_rows_bf16(ctypes.byref(fit), n) == 192 * 4
+    assert lib.mrl_mlp_slab_rows(ctypes.byref(fit), 100) == 4  # small batches: one block
+    bad = _lib.MlpDesc(12, 1, _lib.HEAD_LINEAR, 64, 2, -1)
+    assert lib.mrl_mlp_slab_rows(ctypes.byref(bad), n) < 0
+
+
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU refusal")
 def test_product_path_refuses_without_gpu():
     from modular_rl_amd import _lib
