@@ -101,8 +101,11 @@ def test_fisher_vector_product(head, nin, nout):
     assert _rel(fv.cpu().numpy(), want) < 1e-4
 
 
-@pytest.mark.parametrize("nin", [5, 12])
-def test_value_forward_and_loss_grad_with_time_feature(nin):
+@pytest.mark.parametrize("nin,cus", [(5, 0), (12, 0), (12, 1), (12, 5)])
+def test_value_forward_and_loss_grad_with_time_feature(nin, cus):
+    """cus > 0: the passes sized for a CU subset (the VF fit beside the rollout); at
+    N = 1500 (12 blocks) cus 1 caps the VJP at 1 block and the row passes at 6, cus 5
+    the VJP at 5 -- the partial / slab rows follow and the sums stay exact."""
     from modular_rl_amd import _lib
     N, limit = 1500, 200.0
     rng = np.random.default_rng(3)
@@ -113,8 +116,11 @@ def test_value_forward_and_loss_grad_with_time_feature(nin):
     X = np.concatenate([obs.astype(np.float64), (ept / limit).astype(np.float32).astype(np.float64)[:, None]], axis=1)
     y = rng.standard_normal(N).astype(np.float32)
     net = _net("linear", nin, 1)
+    net.size_for_cus(cus)
     net.set_flat(th)
     xo, et = _dev(obs), _dev(ept, torch.int32)
+    if cus:
+        assert net.partial_rows(N) == 4 * min(12, 6 * cus)
     v = net.forward(xo, N, ep_t=et, timestep_limit=limit).cpu().numpy()
     want_v = T.mlp_forward(spec, th, X)[0][:, 0]
     np.testing.assert_allclose(v, want_v, rtol=2e-5, atol=2e-6)
