@@ -41,7 +41,8 @@ typedef struct {
   int32_t head;    /* MRL_HEAD_*                                              */
   int32_t n_hidden;/* must be 64                                              */
   int32_t n_layers;/* must be 2                                               */
-  int32_t cus;     /* CUs the row passes and the VJP are sized for (0: all 256):
+  int32_t cus;     /* CUs the VJP and the row passes with partial sums are
+                    * sized for (0: all 256; other row passes use the device):
                     * the grid caps scale with it, so passes issued on a stream
                     * restricted to that many CUs run in whole rounds.  Part of
                     * the result's identity: the per-wave partial sums follow

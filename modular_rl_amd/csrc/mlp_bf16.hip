@@ -771,7 +771,7 @@ int mrl_mlp_rows_bf16(const mrl_mlp_desc* d, int32_t epi, const float* theta, co
   const BDims b = bf16_dims(d->n_in, d->n_out);
   const size_t shm = (size_t)b.fwd_words * 4 * (epi == MRL_EPI_FVP ? 2 : 1);
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(epi == MRL_EPI_PPOSGD ? 1 : rows_blocks_b(io->n, epi == MRL_EPI_FVP, desc_cus_b(d))),
+  const dim3 grid(epi == MRL_EPI_PPOSGD ? 1 : rows_blocks_b(io->n, epi == MRL_EPI_FVP, io->partial != nullptr ? desc_cus_b(d) : 256)),
       blk(ROWS_BLOCK_B);
   // the benchmark nets as static shapes (plain rows; a time-feature column built from
   // ep_t takes the generic kernel); policy epilogues only for the policy shapes

@@ -773,7 +773,9 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
     default:
       return fail(E_ARG, "unknown epilogue");
   }
-  const int64_t blocks = rows_blocks(io->n, desc_cus(d));
+  // cus sizes the passes whose sums follow the grid (per-wave partials); the others
+  // (forward / PROB / FVP rows) keep the device-wide grid wherever they run
+  const int64_t blocks = rows_blocks(io->n, io->partial != nullptr ? desc_cus(d) : 256);
   size_t shm = (size_t)a.d.fwd_size * 4 * (epi == MRL_EPI_FVP ? 2 : 1);
   hipStream_t s = (hipStream_t)stream;
   const int sh = static_shape_of(d, io->ep_t != nullptr);
