@@ -73,8 +73,9 @@ __device__ inline RowsArgs rows_shape(const RowsArgs& in) {
 }
 
 template <int EPI_K, int SH>
-// 2 waves/SIMD: layer 2 is evaluated one M-tile at a time so the chain fits 256 registers
-__global__ __launch_bounds__(ROWS_BLOCK, 2) void mlp_rows_kernel(RowsArgs a_in, const float* __restrict__ img,
+// 3 waves/SIMD: layer 2 is evaluated one M-tile at a time so the chain fits 168
+// registers (the cached Fisher-product pass took 176 at a bound of 2, i.e. 2 waves)
+__global__ __launch_bounds__(ROWS_BLOCK, 3) void mlp_rows_kernel(RowsArgs a_in, const float* __restrict__ img,
                                                                const float* __restrict__ imgt,
                                                                const int32_t* __restrict__ skip) {
   const RowsArgs a = rows_shape<SH>(a_in);
