@@ -827,8 +827,9 @@ int mrl_mlp_vjp_bf16(const mrl_mlp_desc* d, const float* image, const float* x, 
   const size_t shm = (size_t)a.b.total_words * 4;
   const dim3 grid(vjp_blocks_b(n, desc_cus_b(d))), blk(256);
   hipStream_t s = (hipStream_t)stream;
-  // the benchmark policies as static shapes (plain rows only; the VF's time feature
-  // column takes the generic kernel)
+  // the benchmark policies and value nets as static shapes (plain rows only: the VF
+  // fit reads its materialised [obs, t / limit] rows; a time feature built from ep_t
+  // takes the generic kernel, which spills at the VF's shape)
   int sh = 0;
   if (!ep_t)
     for (int i = 1; i < N_STATIC_SHAPES; ++i)
@@ -837,6 +838,8 @@ int mrl_mlp_vjp_bf16(const mrl_mlp_desc* d, const float* image, const float* x, 
   do {                                                                                                           \
     if (sh == 1) hipLaunchKernelGGL((mlp_vjp_bf16_kernel<C, 1>), grid, blk, shm, s, a, image, skip);              \
     else if (sh == 2) hipLaunchKernelGGL((mlp_vjp_bf16_kernel<C, 2>), grid, blk, shm, s, a, image, skip);         \
+    else if (sh == 3) hipLaunchKernelGGL((mlp_vjp_bf16_kernel<C, 3>), grid, blk, shm, s, a, image, skip);         \
+    else if (sh == 4) hipLaunchKernelGGL((mlp_vjp_bf16_kernel<C, 4>), grid, blk, shm, s, a, image, skip);         \
     else hipLaunchKernelGGL((mlp_vjp_bf16_kernel<C, 0>), grid, blk, shm, s, a, image, skip);                      \
   } while (0)
   if (act_cache != nullptr) MRL_VJPB(true);
