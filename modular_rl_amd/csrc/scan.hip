@@ -239,6 +239,9 @@ __global__ void vf_target_kernel(const float* __restrict__ ret, const float* __r
 
 // ------------------------------------------------------------------ CG (one workgroup)
 constexpr int CG_T = 1024;
+#ifndef MRL_CG_REG  // 1: the single-block CG update keeps its slices in registers (n <= 8192)
+#define MRL_CG_REG 1
+#endif
 
 __device__ inline double block_sum(double v, double* red) {
   red[threadIdx.x] = v;
@@ -305,6 +308,68 @@ __global__ __launch_bounds__(CG_T) void cg_update_kernel(const float* __restrict
     const double pi = r[i] + mu * p[i];
     p[i] = pi;
     p32[i] = (float)pi;
+  }
+  if (threadIdx.x == 0) {
+    state[0] = newr;
+    state[1] = pz;
+    state[2] += 1.0;
+    if (newr < tol) flag[0] = 1;
+  }
+}
+
+// The same update with each thread's K-element slice of p / r / x / A x held in
+// registers: every operand is loaded once, up front, instead of once per pass
+// (three dependent global passes of the plain kernel).  Per-thread accumulation
+// order and the block_sum tree are the plain kernel's, so the results are identical.
+template <int K>
+__global__ __launch_bounds__(CG_T) void cg_update_reg_kernel(const float* __restrict__ fvp, double damping, double tol,
+                                                             int64_t n, double* x, double* r, double* p, float* p32,
+                                                             double* ax, double* state, int32_t* flag) {
+  __shared__ double red[CG_T];
+  if (flag[0] != 0) return;
+  const double rdotr = state[0];
+  double pr[K], zr[K], rr[K], xr[K], ar[K];
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int64_t i = threadIdx.x + (int64_t)k * CG_T;
+    pr[k] = zr[k] = rr[k] = xr[k] = ar[k] = 0.0;
+    if (i < n) {
+      const double pi = p[i];
+      const double z = (double)fvp[i] + damping * pi;
+      pr[k] = pi;
+      zr[k] = z;
+      rr[k] = r[i];
+      xr[k] = x[i];
+      if (ax) ar[k] = ax[i];
+      s += pi * z;
+    }
+  }
+  const double pz = block_sum(s, red);
+  const double v = rdotr / pz;
+  s = 0.0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int64_t i = threadIdx.x + (int64_t)k * CG_T;
+    if (i < n) {
+      x[i] = xr[k] + v * pr[k];
+      if (ax) ax[i] = ar[k] + v * zr[k];
+      const double ri = rr[k] - v * zr[k];
+      r[i] = ri;
+      rr[k] = ri;
+      s += ri * ri;
+    }
+  }
+  const double newr = block_sum(s, red);
+  const double mu = newr / rdotr;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int64_t i = threadIdx.x + (int64_t)k * CG_T;
+    if (i < n) {
+      const double pi = rr[k] + mu * pr[k];
+      p[i] = pi;
+      p32[i] = (float)pi;
+    }
   }
   if (threadIdx.x == 0) {
     state[0] = newr;
@@ -810,6 +875,9 @@ int mrl_cg_update(const float* fvp, double damping, double residual_tol, int64_t
     hipLaunchKernelGGL(cgm_xr_kernel, dim3(CGB), dim3(CGB_T), 0, s, fvp, damping, n, x, r, p, ax, state, flag);
     hipLaunchKernelGGL(cgm_p_kernel, dim3(CGB), dim3(CGB_T), 0, s, n, r, p, p32, state, flag);
     hipLaunchKernelGGL(cgm_final_kernel, dim3(1), dim3(CGB_T), 0, s, residual_tol, state, flag);
+  } else if (MRL_CG_REG && n <= 8 * CG_T) {
+    hipLaunchKernelGGL(cg_update_reg_kernel<8>, dim3(1), dim3(CG_T), 0, s, fvp, damping, residual_tol, n, x, r, p,
+                       p32, ax, state, flag);
   } else {
     hipLaunchKernelGGL(cg_update_kernel, dim3(1), dim3(CG_T), 0, s, fvp, damping, residual_tol, n, x, r, p, p32, ax,
                        state, flag);
