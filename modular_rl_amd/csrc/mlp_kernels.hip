@@ -542,26 +542,37 @@ __global__ void mlp_pack_kernel(MlpDims d, const float* __restrict__ th, float* 
   if (i < count) image[i] = image_value(d, th, i);
 }
 
-template <class T, class O>
+// RG row groups of 64 columns per block (blockDim = 64 * RG); group g sums rows
+// g, g + RG, ... with 8 independent accumulators (8 loads in flight per lane), then
+// the RG group sums are added in a fixed pairwise order
+template <class T, class O, int RG = 4>
 __global__ void reduce_rows_kernel(const T* __restrict__ slab, int64_t rows, int64_t cols, O* __restrict__ out,
                                    const int32_t* __restrict__ skip) {
-  __shared__ double part[4][64];
+  __shared__ double part[RG][64];
   if (skip != nullptr && *skip != 0) return;
   const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int64_t col = (int64_t)blockIdx.x * 64 + c;
-  // 8 independent accumulators keep 8 loads in flight per lane (latency-bound otherwise)
   double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (col < cols) {
     int64_t r = g;
-    for (; r + 28 < rows; r += 32) {
+    for (; r + 7 * RG < rows; r += 8 * RG) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) s[q] += (double)slab[(r + 4 * q) * cols + col];
+      for (int q = 0; q < 8; ++q) s[q] += (double)slab[(r + RG * q) * cols + col];
     }
-    for (; r < rows; r += 4) s[0] += (double)slab[r * cols + col];
+    for (; r < rows; r += RG) s[0] += (double)slab[r * cols + col];
   }
   part[g][c] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
-  if (g == 0 && col < cols) out[col] = (O)(((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]);
+  if constexpr (RG == 4) {
+    if (g == 0 && col < cols) out[col] = (O)(((part[0][c] + part[1][c]) + part[2][c]) + part[3][c]);
+  } else {
+#pragma unroll
+    for (int w = RG / 2; w >= 1; w >>= 1) {
+      if (g < w) part[g][c] += part[g + w][c];
+      __syncthreads();
+    }
+    if (g == 0 && col < cols) out[col] = (O)part[0][c];
+  }
 }
 
 // few columns (per-wave loss partials): one block per column, 256 threads over rows
@@ -863,8 +874,10 @@ int mrl_probtype_rows(int32_t head, int32_t k, int64_t n, const float* prob, con
 int mrl_reduce_rows_f32(const float* slab, int64_t rows, int64_t cols, float* out, const int32_t* skip, void* stream) {
   if (!slab || !out) return fail(E_ARG, "null pointer");
   if (cols <= 0) return OK;
-  hipLaunchKernelGGL((reduce_rows_kernel<float, float>), dim3(ceil_div(cols, 64)), dim3(256), 0, (hipStream_t)stream,
-                     slab, rows, cols, out, skip);
+  // 16 row groups (1,024 threads): the Hopper VJP slab (1,024 x 5,126) is only 81
+  // column blocks wide, so the row split is what fills the chip
+  hipLaunchKernelGGL((reduce_rows_kernel<float, float, 16>), dim3(ceil_div(cols, 64)), dim3(1024), 0,
+                     (hipStream_t)stream, slab, rows, cols, out, skip);
   return hip_check(hipGetLastError(), "mrl_reduce_rows_f32");
 }
 int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* out, const int32_t* skip,
