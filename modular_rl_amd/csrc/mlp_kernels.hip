@@ -874,10 +874,15 @@ int mrl_probtype_rows(int32_t head, int32_t k, int64_t n, const float* prob, con
 int mrl_reduce_rows_f32(const float* slab, int64_t rows, int64_t cols, float* out, const int32_t* skip, void* stream) {
   if (!slab || !out) return fail(E_ARG, "null pointer");
   if (cols <= 0) return OK;
-  // 16 row groups (1,024 threads): the Hopper VJP slab (1,024 x 5,126) is only 81
-  // column blocks wide, so the row split is what fills the chip
-  hipLaunchKernelGGL((reduce_rows_kernel<float, float, 16>), dim3(ceil_div(cols, 64)), dim3(1024), 0,
-                     (hipStream_t)stream, slab, rows, cols, out, skip);
+  // tall slabs (the fused VJP's per-wave rows: 1,024 x 5,126 for Hopper, only 81
+  // column blocks wide): 16 row groups (1,024 threads) so the row split fills the chip;
+  // short wide ones (the layered GEMMs' split-K slabs, 64 rows) keep 4 groups
+  if (rows >= 256)
+    hipLaunchKernelGGL((reduce_rows_kernel<float, float, 16>), dim3(ceil_div(cols, 64)), dim3(1024), 0,
+                       (hipStream_t)stream, slab, rows, cols, out, skip);
+  else
+    hipLaunchKernelGGL((reduce_rows_kernel<float, float, 4>), dim3(ceil_div(cols, 64)), dim3(256), 0,
+                       (hipStream_t)stream, slab, rows, cols, out, skip);
   return hip_check(hipGetLastError(), "mrl_reduce_rows_f32");
 }
 int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* out, const int32_t* skip,
