@@ -51,6 +51,31 @@ def flops_per_row(net):
     return {"fvp_jvp_rows": fwd + jvp, "fvp_vjp": vjp, "policy_forward": fwd}
 
 
+def vjp_binary_entry(kern, policy_vjp_flop, vf_vjp_flop, rows, iters):
+    """One entry for the VJP kernel binary over its timed roles -- the Fisher products
+    (fvp_vjp), the policy gradient (pg_vjp) and the VF fit evaluations (vf_vjp) --
+    as rocprofv3 sums one kernel name: launches, summed HIP-event time, mean per
+    launch and the launch-weighted algorithmic FLOP per row.  ``kern`` maps a role to
+    (launches, mean_ms, total_ms); None without Fisher-product launches."""
+    roles = {"fvp_vjp": policy_vjp_flop, "pg_vjp": policy_vjp_flop, "vf_vjp": vf_vjp_flop}
+    parts = {r: kern[r] for r in roles if r in kern and roles[r] is not None}
+    if "fvp_vjp" not in parts:
+        return None
+    cnt = sum(c for c, _, _ in parts.values())
+    tot = sum(t for _, _, t in parts.values())
+    flop = sum(c * roles[r] * rows for r, (c, _, _) in parts.items())
+    return dict(launches=cnt, mean_ms=tot / cnt, total_ms=tot, rows_per_launch=rows, flop_per_row=flop / (cnt * rows),
+                roles={r: {"launches": c, "mean_ms": round(m, 5), "ms_per_iter": round(t / iters, 3)}
+                       for r, (c, m, t) in parts.items()})
+
+
+def dominant_kernel(kinfo):
+    """The kernel binary with the largest device time per iteration (fvp_vjp is one
+    role of mlp_vjp_kernel when that entry exists)."""
+    cands = [k for k in kinfo if not (k == "fvp_vjp" and "mlp_vjp_kernel" in kinfo)]
+    return max(cands, key=lambda k: kinfo[k]["total_ms"])
+
+
 DYNAMICS = {"Hopper-v2": "hopper.xml articulated-body dynamics", "Humanoid-v2": "humanoid.xml articulated-body dynamics",
             "CartPole-v0": "gym equations"}
 GAE_BYTES_PER_ROW = 17  # read r 4 + v 4 + flags 1, write adv 4 + ret 4
@@ -248,17 +273,10 @@ def main():
         # VF L-BFGS evaluation (the VF fit's launches run beside the next rollout on the
         # fit's CU set): rocprofv3 sums them into one entry, so the dominance test does too
         vf_net = agent.baseline.net
-        roles = {"fvp_vjp": fpr["fvp_vjp"], "pg_vjp": fpr["fvp_vjp"],
-                 "vf_vjp": flops_per_row(vf_net)["fvp_vjp"] if not vf_net.layered else None}
-        parts = {r: kern[r] for r in roles if r in kern and roles[r] is not None}
-        if "fvp_vjp" in parts:
-            cnt = sum(c for c, _, _ in parts.values())
-            tot = sum(t for _, _, t in parts.values())
-            flop = sum(c * roles[r] * n_local for r, (c, _, _) in parts.items())
-            kinfo["mlp_vjp_kernel"] = dict(launches=cnt, mean_ms=tot / cnt, total_ms=tot, rows_per_launch=n_local,
-                                           flop_per_row=flop / (cnt * n_local), roles={
-                                               r: {"launches": c, "mean_ms": round(m, 5), "ms_per_iter": round(t / K, 3)}
-                                               for r, (c, m, t) in parts.items()})
+        vjp = vjp_binary_entry(kern, fpr["fvp_vjp"], None if vf_net.layered else flops_per_row(vf_net)["fvp_vjp"],
+                               n_local, K)
+        if vjp is not None:
+            kinfo["mlp_vjp_kernel"] = vjp
     if "rollout_steps" in kern:
         # one timed region per iteration around the rollout's launches (the persistent
         # kernel over the T steps, in a graph on the rollout stream): region / T per step
@@ -270,10 +288,7 @@ def main():
         ki["frac_mfma"] = ki["tflops"] / peak
         if pmc.get(name, {}).get("hbm_bytes_per_launch"):
             ki["hbm_gbs_pmc"] = pmc[name]["hbm_bytes_per_launch"] / (ki["mean_ms"] * 1e-3) / 1e9
-    # the dominant kernel = the kernel binary with the largest device time per iteration
-    # (fvp_vjp is one role of mlp_vjp_kernel when that entry exists)
-    cands = [k for k in kinfo if not (k == "fvp_vjp" and "mlp_vjp_kernel" in kinfo)]
-    dom = max(cands, key=lambda k: kinfo[k]["total_ms"])
+    dom = dominant_kernel(kinfo)
     traffic = pmc.get("fvp_vjp" if dom == "mlp_vjp_kernel" else dom, {}).get("hbm_bytes_per_launch")
     roofline = {"bound": "mfma", "achieved": round(kinfo[dom]["tflops"], 3), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(kinfo[dom]["tflops"] / peak, 4), "traffic": traffic,

@@ -91,3 +91,24 @@ def test_bench_flop_and_byte_accounting():
     assert f["fvp_jvp_rows"] == 18560 and f["fvp_vjp"] == 18560 and f["policy_forward"] == 2 * (11 * 64 + 64 * 64 + 64 * 3)
     hum = types.SimpleNamespace(n_in=376, n_out=17, hid_sizes=[512, 512, 512], layered=True)
     assert bench.flops_per_row(hum)["fvp_vjp"] == 2516992
+
+
+def test_bench_roofline_kernel_is_chosen_per_binary():
+    """The VJP binary's roles are summed like rocprofv3 sums one kernel name, and the
+    roofline kernel is the binary with the largest device time per iteration."""
+    import bench
+    rows, K = 1000, 2
+    kern = {"fvp_vjp": (20, 1.0, 20.0), "pg_vjp": (2, 1.0, 2.0), "vf_vjp": (6, 1.5, 9.0)}
+    e = bench.vjp_binary_entry(kern, 100.0, 80.0, rows, K)
+    assert e["launches"] == 28 and e["total_ms"] == 31.0 and abs(e["mean_ms"] - 31.0 / 28) < 1e-12
+    assert abs(e["flop_per_row"] - (22 * 100.0 + 6 * 80.0) / 28) < 1e-9
+    assert e["roles"]["vf_vjp"] == {"launches": 6, "mean_ms": 1.5, "ms_per_iter": 4.5}
+    assert bench.vjp_binary_entry({"pg_vjp": (2, 1.0, 2.0)}, 100.0, 80.0, rows, K) is None
+    assert bench.vjp_binary_entry(kern, 100.0, None, rows, K)["launches"] == 22  # layered VF: not this binary
+    kinfo = {"fvp_vjp": {"total_ms": 20.0}, "mlp_vjp_kernel": {"total_ms": 31.0}, "rollout_step": {"total_ms": 27.0},
+             "fvp_jvp_rows": {"total_ms": 15.0}}
+    assert bench.dominant_kernel(kinfo) == "mlp_vjp_kernel"
+    kinfo["rollout_step"]["total_ms"] = 40.0
+    assert bench.dominant_kernel(kinfo) == "rollout_step"
+    # without the binary entry (layered nets) the Fisher-product role competes itself
+    assert bench.dominant_kernel({"fvp_vjp": {"total_ms": 50.0}, "rollout_step": {"total_ms": 40.0}}) == "fvp_vjp"
