@@ -276,6 +276,9 @@ __device__ inline VjpArgs vjp_shape(const VjpArgs& in) {
   return a;
 }
 
+#ifndef MRL_VJP_BIAS_REG  // 1: bias gradients from per-lane register partials (no per-tile LDS row sums)
+#define MRL_VJP_BIAS_REG 1
+#endif
 #ifndef MRL_VJP_MINW  // minimum waves per SIMD the VJP's registers must allow (build switch)
 #define MRL_VJP_MINW 1
 #endif
@@ -309,6 +312,13 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
   }
   const int i16 = lane & 15, kk = lane >> 4;
   float gb0 = 0.f, gb1 = 0.f, gb2 = 0.f;
+#if MRL_VJP_BIAS_REG
+  // bias gradients as per-lane partials over the wave's tiles (row j of each C tile),
+  // summed over the 32 rows once at the end instead of an LDS row sum per tile
+  f32x16 pb0[2], pb1[2];
+  float pG[4] = {0.f, 0.f, 0.f, 0.f};
+  pb0[0] = pb0[1] = pb1[0] = pb1[1] = zero16();
+#endif
   float gls[MAX_OUT];
 #pragma unroll
   for (int q = 0; q < MAX_OUT; ++q) gls[q] = 0.f;
@@ -348,6 +358,10 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
     float G[4];  // head-gradient rows: register r of half h = output r + 4h
 #pragma unroll
     for (int r = 0; r < 4; ++r) G[r] = (valid && r + 4 * h < A) ? cur.g[r] : 0.f;
+#if MRL_VJP_BIAS_REG
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pG[r] += G[r];
+#endif
 #pragma unroll
     for (int q = 0; q < MAX_OUT; ++q) gls[q] += (valid && h == 0 && q < a.n_sum) ? cur.gs[q] : 0.f;
     // Phase order keeps the MFMA pipe fed: every LDS transpose is issued while an
@@ -394,12 +408,20 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
       __builtin_amdgcn_sched_barrier(0);
 #endif
     }
+#if !MRL_VJP_BIAS_REG
     if (lane < A) gb2 += rowsum32(scrB, lane);
+#endif
     // (d) ga2 = gh2 * (1 - h2^2)
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int r = 0; r < 16; ++r) g2[m][r] *= dtanh(f.h2[m][r]);
+#if MRL_VJP_BIAS_REG
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) pb1[m][r] += g2[m][r];
+#endif
 #if MRL_VJP_MINW > 1
     // two waves per SIMD: h1 is loaded once h2 is dead (the other wave covers the
     // latency), keeping the tile's live registers within 256
@@ -469,11 +491,19 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
       __builtin_amdgcn_sched_barrier(0);  // one k-group's operands live at a time
 #endif
     }
+#if !MRL_VJP_BIAS_REG
     gb1 += rowsum32(scrB, lane);
+#endif
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int r = 0; r < 16; ++r) g1[m][r] *= dtanh(f.h1[m][r]);
+#if MRL_VJP_BIAS_REG
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) pb0[m][r] += g1[m][r];
+#endif
     WAVE_LDS_ORDER();
     write_img(scrB, g1, lane);
     WAVE_LDS_ORDER();
@@ -498,7 +528,9 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
       __builtin_amdgcn_sched_barrier(0);
 #endif
     }
+#if !MRL_VJP_BIAS_REG
     gb0 += rowsum32(scrB, lane);
+#endif
     WAVE_LDS_ORDER();
     (void)row0;
   }
@@ -514,20 +546,58 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
         const int i = 16 * mt + 4 * kk + r;
         if (i < d.O) out[d.tW0 + i * HID + 16 * nt + i16] = gW0[mt][nt][r];
       }
+#if MRL_VJP_BIAS_REG
+  // sum each partial over the 32 rows (lanes j of a half, butterfly), then lane j = 0
+  // of half h holds units 32 m + cperm(r, h)
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        pb0[m][r] += __shfl_xor(pb0[m][r], o);
+        pb1[m][r] += __shfl_xor(pb1[m][r], o);
+      }
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) pG[r] += __shfl_xor(pG[r], o);
+  if (j == 0) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        out[d.tb0 + 32 * m + cperm(r, h)] = pb0[m][r];
+        out[d.tb1 + 32 * m + cperm(r, h)] = pb1[m][r];
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r + 4 * h < A) out[d.tb2 + r + 4 * h] = pG[r];
+  }
+  (void)gb0;
+  (void)gb1;
+  (void)gb2;
+#else
   out[d.tb0 + lane] = gb0;
+#endif
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
     for (int mj = 0; mj < 2; ++mj)
 #pragma unroll
       for (int r = 0; r < 16; ++r) out[d.tW1 + (32 * mi + cperm(r, h)) * HID + 32 * mj + j] = gW1[mi][mj][r];
+#if !MRL_VJP_BIAS_REG
   out[d.tb1 + lane] = gb1;
+#endif
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (i16 < A) out[d.tW2 + (16 * mt + 4 * kk + r) * A + i16] = gW2[mt][r];
+#if !MRL_VJP_BIAS_REG
   if (lane < A) out[d.tb2 + lane] = gb2;
+#endif
   for (int q = 0; q < a.n_sum; ++q) {
     const float s = wave_sumf(gls[q]);
     if (lane == 0) out[d.tls + q] = s;
