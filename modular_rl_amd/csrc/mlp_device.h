@@ -139,6 +139,26 @@ __device__ inline f32x2 tanh_fast2(f32x2 x) {
 
 // tanh' from the activation, 1 - h^2, as one explicit fma (see tanh_fast)
 __device__ inline float dtanh(float h) { return fmaf(-h, h, 1.f); }
+#ifndef MRL_PK_DTANH  // 1: tile products with tanh' on packed f32 pairs
+#define MRL_PK_DTANH 1
+#endif
+// t[r] *= 1 - h[r]^2 over a 16-float C tile: v_pk_fma / v_pk_mul on pairs, each
+// element rounded exactly as t[r] * dtanh(h[r])
+__device__ inline void mul_dtanh16(f32x16& t, const f32x16& h) {
+#if MRL_PK_DTANH
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    const f32x2 hh = f32x2{h[r], h[r + 1]};
+    const f32x2 d = __builtin_elementwise_fma(-hh, hh, (f32x2)(1.f));
+    const f32x2 tt = f32x2{t[r], t[r + 1]} * d;
+    t[r] = tt.x;
+    t[r + 1] = tt.y;
+  }
+#else
+#pragma unroll
+  for (int r = 0; r < 16; ++r) t[r] *= dtanh(h[r]);
+#endif
+}
 
 __device__ inline void tanh16(f32x16& a) {
 #pragma unroll
@@ -282,9 +302,7 @@ __device__ inline void jvp_head_cached(const float* lds, const float* ldt, const
   dh1[1] = load_bias16(ldt, d.fb0, 1, h);
   layer0(ldt, d, xl, lane, dh1);
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dh1[m][r] *= dtanh(h1[m][r]);
+  for (int m = 0; m < 2; ++m) mul_dtanh16(dh1[m], h1[m]);
   float dzt[MAX_OUT];
 #pragma unroll
   for (int o = 0; o < MAX_OUT; ++o) {
@@ -301,8 +319,7 @@ __device__ inline void jvp_head_cached(const float* lds, const float* ldt, const
     __builtin_amdgcn_sched_barrier(0);
     chain1(ldt, d.fa1, mo, h1, lane, da);
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) da[r] *= dtanh(a[r]);
+    mul_dtanh16(da, a);
     if (need_z) head_partial_mt(lds, d, a, mo, h, z);
     head_partial_mt(lds, d, da, mo, h, dz);
     head_partial_mt(ldt, d, a, mo, h, dzt);
@@ -328,9 +345,7 @@ __device__ inline void forward_jvp_head_lowreg(const float* lds, const float* ld
   tanh16(h1[0]);
   tanh16(h1[1]);
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dh1[m][r] *= dtanh(h1[m][r]);
+  for (int m = 0; m < 2; ++m) mul_dtanh16(dh1[m], h1[m]);
 #pragma unroll
   for (int o = 0; o < MAX_OUT; ++o) {
     z[o] = 0.f;
@@ -351,8 +366,7 @@ __device__ inline void forward_jvp_head_lowreg(const float* lds, const float* ld
     chain1(ldt, d.fa1, mo, h1, lane, da);
     __builtin_amdgcn_sched_barrier(0);
     tanh16(a);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) da[r] *= dtanh(a[r]);
+    mul_dtanh16(da, a);
     head_partial_mt(lds, d, a, mo, h, z);
     head_partial_mt(lds, d, da, mo, h, dz);
     head_partial_mt(ldt, d, a, mo, h, dzt);

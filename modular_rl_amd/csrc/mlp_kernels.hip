@@ -413,9 +413,7 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
 #endif
     // (d) ga2 = gh2 * (1 - h2^2)
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) g2[m][r] *= dtanh(f.h2[m][r]);
+    for (int m = 0; m < 2; ++m) mul_dtanh16(g2[m], f.h2[m]);
 #if MRL_VJP_BIAS_REG
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -495,9 +493,7 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
     gb1 += rowsum32(scrB, lane);
 #endif
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) g1[m][r] *= dtanh(f.h1[m][r]);
+    for (int m = 0; m < 2; ++m) mul_dtanh16(g1[m], f.h1[m]);
 #if MRL_VJP_BIAS_REG
 #pragma unroll
     for (int m = 0; m < 2; ++m)
