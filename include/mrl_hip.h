@@ -341,7 +341,7 @@ int64_t mrl_episode_stats_workspace_bytes(int64_t E);
  * stat (Chan merge of per-block Welford partials in block order), then normalised. */
 #define MRL_ENV_CARTPOLE 0  /* CartPole-v0 equations (gym), k = 2            */
 #define MRL_ENV_HOPPER 1    /* Hopper-v2: hopper.xml articulated body, obs 11 / act 3 */
-#define MRL_ENV_HUMANOID 2  /* Humanoid-v2-shaped surrogate, obs 376 / act 17 (layered rollout only) */
+#define MRL_ENV_HUMANOID 2  /* Humanoid-v2: humanoid.xml articulated body, obs 376 / act 17 (layered rollout only) */
 
 typedef struct {
   int32_t env_id;          /* MRL_ENV_*                                          */
@@ -354,7 +354,11 @@ typedef struct {
   int32_t compute;         /* MRL_COMPUTE_*: the policy net's dtype; BF16 rounds the
                               fused forward's W0, W1, x, h1, h2 to bf16 like
                               mrl_mlp_rows_bf16, so rollout prob rows = update's    */
-  int32_t pad_;
+  int32_t launch_cus;      /* mrl_rollout_run's residency check: 0 = the CUs of the
+                              stream it is called on; > 0 = the CUs of the stream a
+                              captured graph will be replayed on (capture streams
+                              carry no CU mask); < 0 = debug only, skip the check
+                              (a non-resident grid then aborts: sync[32] != 0)       */
 } mrl_rollout_desc;
 
 typedef struct {

@@ -63,7 +63,7 @@ class GemmBf16TnDesc(ctypes.Structure):
 
 class RolloutDesc(ctypes.Structure):
     _fields_ = [("env_id", i32), ("n_envs", i32), ("horizon", i32), ("timestep_limit", i32), ("filter", i32),
-                ("env_offset", i32), ("seed", ctypes.c_uint64), ("compute", i32), ("pad_", i32)]
+                ("env_offset", i32), ("seed", ctypes.c_uint64), ("compute", i32), ("launch_cus", i32)]
 
 
 class RolloutBufs(ctypes.Structure):

@@ -21,7 +21,10 @@ state is a flat set of arrays -- nothing executable is ever stored or loaded:
 In the pipelined loop (core.IterationRunner) the callback for iteration k fires
 after iteration k+1 has already been issued; the runner therefore captures the state
 at the end of iteration k on the device (``agent._snapshot_capture``) and snapshots
-taken in that callback read the capture, not the live tensors.
+taken in that callback read the capture, not the live tensors.  The capture is
+dropped when the callback returns (``run_policy_gradient_algorithm``), so a snapshot
+taken later -- after a manual ``set_from_flat`` or another update -- reads the live
+state.
 
 Snapshots are ``.npz`` files (``numpy.load(allow_pickle=False)`` reads them); the run
 log is HDF5 with the reference's layout when ``h5py`` is importable, else an ``.npz``
@@ -35,7 +38,10 @@ from collections import defaultdict
 import numpy as np
 import torch
 
-SNAPSHOT_VERSION = 1
+# 2: updater/* (PPO Adam moments, step count, kl_coeff) and rng/np_* arrays were added;
+# a version-1 snapshot has neither, so it loads only into agents whose updater keeps no
+# state of its own (TRPO)
+SNAPSHOT_VERSION = 2
 
 
 def _jsonable(cfg):
@@ -103,15 +109,20 @@ def load_snapshot(path, agent):
     with np.load(path, allow_pickle=False) as z:
         st = {k.replace("__", "/"): z[k] for k in z.files if k != "meta"}
         meta = json.loads(bytes(z["meta"]).decode())
-    if meta.get("version") != SNAPSHOT_VERSION:
-        raise ValueError(f"{path}: snapshot version {meta.get('version')} != {SNAPSHOT_VERSION}")
+    version = meta.get("version")
+    upd = getattr(agent, "updater", None)
+    if version == 1:
+        if upd is not None and hasattr(upd, "state_arrays"):
+            raise ValueError(f"{path}: version-1 snapshot holds no updater state (Adam moments, kl_coeff), "
+                             f"which this agent's {type(upd).__name__} needs to resume exactly")
+    elif version != SNAPSHOT_VERSION:
+        raise ValueError(f"{path}: snapshot version {version} != {SNAPSHOT_VERSION}")
     pol, vf = agent.policy.net, agent.baseline.net
     if st["policy/theta"].shape != (pol.P,) or st["vf/theta"].shape != (vf.P,):
         raise ValueError(f"{path}: parameter shapes do not match this agent's nets")
     pol.set_flat(st["policy/theta"])
     vf.set_flat(st["vf/theta"])
     upd_state = {k[len("updater/"):]: v for k, v in st.items() if k.startswith("updater/")}
-    upd = getattr(agent, "updater", None)
     if upd_state:
         if upd is None or not hasattr(upd, "load_state_arrays"):
             raise ValueError(f"{path}: snapshot holds updater state this agent's updater cannot take")

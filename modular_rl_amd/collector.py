@@ -32,15 +32,10 @@ from ._lib import call, ptr, stream
 from .dist import Comm
 
 
-def merge_filter_deltas(s0, s1, comm):
-    """Per-iteration cross-rank merge of the running stats.  Every rank started the
-    iteration from the same state s0 = [n_obs, n_rew, M[D], S[D]] and ended at its
-    local s1 = s0 (+) its own pushes.  Each rank's delta (n, mean, M2) is recovered by
-    inverting Chan's formula, all deltas are gathered and merged into s0 in rank
-    order, so all ranks leave with the identical global statistics."""
-    FS = len(s0)
-    D = (FS - 2) // 2
-    delta = np.zeros(FS)
+def _chan_delta(s0, s1, D):
+    """A rank's pushes of one iteration as (n, mean, M2) per column: Chan's merge
+    s1 = s0 (+) delta inverted."""
+    delta = np.zeros(len(s0))
     for which, cols in ((0, range(D - 1)), (1, [D - 1])):
         n0, n1 = s0[which], s1[which]
         nd = n1 - n0
@@ -52,10 +47,26 @@ def merge_filter_deltas(s0, s1, comm):
             md = (n1 * M1 - n0 * M0) / nd
             delta[2 + k] = md
             delta[2 + D + k] = S1 - S0 - (md - M0) ** 2 * n0 * nd / n1
+    return delta
+
+
+def merge_filter_deltas(s0, s1, comm):
+    """Per-iteration cross-rank merge of the running stats.  Every rank started the
+    iteration from the same state s0 = [n_obs, n_rew, M[D], S[D]] and ended at its
+    local s1 = s0 (+) its own pushes.  All ranks' end states are gathered; rank 0's is
+    the base and the pushes of ranks 1, 2, .. (each recovered by inverting Chan's
+    formula against s0) are merged into it in rank order, so all ranks leave with the
+    identical global statistics -- and one rank (a forced communicator at world size 1)
+    leaves with its own s1 exactly."""
+    FS = len(s0)
+    D = (FS - 2) // 2
     dev = "cuda" if comm.enabled and torch.distributed.get_backend() == "nccl" else "cpu"
-    all_d = torch.stack(comm.allgather(torch.as_tensor(delta).to(dev))).cpu().numpy()  # one copy for all ranks
-    out = np.array(s0, dtype=np.float64).copy()
-    for d in all_d:
+    s1_t = torch.as_tensor(np.asarray(s1, dtype=np.float64)).to(dev)
+    all_s1 = torch.stack(comm.allgather(s1_t)).cpu().numpy()  # one copy for all ranks
+    s0 = np.asarray(s0, dtype=np.float64)
+    out = all_s1[0].copy()
+    for s1r in all_s1[1:]:
+        d = _chan_delta(s0, s1r, D)
         for which, cols in ((0, range(D - 1)), (1, [D - 1])):
             nb = d[which]
             if nb <= 0:
@@ -190,6 +201,12 @@ class Collector:
         self.graph = None
         self._ep_ws = torch.zeros(int(lib.mrl_episode_stats_workspace_bytes(self.E)) // 8 + 1, **f64)
         self._ep_out = torch.zeros(8, **f64)
+        # sticky abort status of the persistent launch: sync[32] of every launch is OR-ed
+        # in on the device (the next launch's memset clears sync); read back with the
+        # episode stats each iteration, which raise MrlError when it is set
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.force_persistent = False  # debug: skip the residency check (tests of the abort path)
+        self._graph_cus = None
 
     def _bufs(self):
         return _lib.RolloutBufs(ptr(self.env_state), ptr(self.env_int), ptr(self.filter_state), ptr(self.records),
@@ -217,6 +234,8 @@ class Collector:
         # persistent is off / the stream has too few CUs; identical results)
         call("mrl_rollout_run", ctypes.byref(self.desc), ctypes.byref(net.desc), ptr(net.theta), ptr(self._rimage),
              ctypes.byref(bufs), ptr(self._sync), int(self.persistent), stream())
+        if self.persistent:
+            torch.maximum(self.status, self._sync[32:33], out=self.status)
         call("mrl_rollout_finish", ctypes.byref(self.desc), ctypes.byref(bufs), stream())
 
     def _launch_all_layered(self, bufs, net):
@@ -255,8 +274,15 @@ class Collector:
         if fill_noise:
             self.fill_noise()
         self._fs_start = self.filter_state[:self.FS].clone() if self.comm.enabled else None
+        # the persistent launch's residency check counts the CUs of the stream it runs on:
+        # the stream of this call (a captured graph replays here, not on its capture stream)
+        from . import streams
+        self.desc.launch_cus = -1 if self.force_persistent else streams.launch_cus()
         if self.use_graph and self.noise is None:
+            if self.graph is not None and self._graph_cus != self.desc.launch_cus:
+                self.graph = None  # captured for another CU set
             if self.graph is None:
+                self._graph_cus = self.desc.launch_cus
                 # captured launches are recorded, not executed: state is untouched by the
                 # capture.  No garbage collection inside the capture: collecting a dead
                 # object that owns HIP state (an earlier collector's graph) while the
@@ -279,12 +305,14 @@ class Collector:
             self._launch_all()
             timing.stop("rollout_steps")
 
+    ABORT_MSG = ("persistent rollout: blocks never all arrived (grid not resident), the trajectories are "
+                 "incomplete; run with MRL_ROLLOUT_PERSISTENT=0")
+
     def check(self):
         """Raise if a persistent rollout launch gave up waiting for its blocks (the grid
         was not resident at once); synchronises on the rollout."""
-        if not self.layered and int(self._sync[32].item()) != 0:
-            raise _lib.MrlError("persistent rollout: blocks never all arrived (grid not resident); "
-                                "run with MRL_ROLLOUT_PERSISTENT=0")
+        if int(self.status.item()) != 0:
+            raise _lib.MrlError(self.ABORT_MSG)
 
     def finish(self):
         """Cross-rank filter merge (waits for the rollout) and the iteration's Batch."""
@@ -319,18 +347,20 @@ class Collector:
         returned as a device tensor (no host sync; the pipelined loop reads it later)."""
         call("mrl_episode_stats", ptr(batch.rew), ptr(batch.flags), batch.T, batch.E, ptr(self._ep_out),
              ptr(self._ep_ws), stream())
-        v = self._ep_out[:6].clone()
+        # [6]: the rollout's abort status rides along (summed over ranks: any rank's abort)
+        v = torch.cat([self._ep_out[:6], self.status.double()])
         if self.comm.enabled:
             mx = v[[3, 5]].clone()
             self.comm.allreduce_(v)
-            if self.comm.world > 1:
-                torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX)
-                v[3], v[5] = mx[0], mx[1]
+            torch.distributed.all_reduce(mx, op=torch.distributed.ReduceOp.MAX, group=self.comm.group)
+            v[3], v[5] = mx[0], mx[1]
         return v
 
-    @staticmethod
-    def episode_stats_finish(v):
-        cnt, sr, sr2, mr, sl, ml = (float(x) for x in v.cpu().numpy())
+    @classmethod
+    def episode_stats_finish(cls, v):
+        cnt, sr, sr2, mr, sl, ml, abort = (float(x) for x in v.cpu().numpy())
+        if abort != 0:
+            raise _lib.MrlError(cls.ABORT_MSG)
         mean = sr / cnt
         return dict(NumEpBatch=int(cnt), EpRewMean=mean,
                     EpRewSEM=float(np.sqrt(max(sr2 / cnt - mean * mean, 0.0)) / np.sqrt(cnt)),

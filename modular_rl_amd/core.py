@@ -156,6 +156,9 @@ def run_policy_gradient_algorithm(env, agent, usercfg=None, callback=None):
         stats["TimeElapsed"] = time.time() - tstart
         if callback:
             callback(stats)
+        # the runner's capture describes the iteration just reported; a snapshot taken
+        # after this callback must read the live state
+        agent._snapshot_capture = None
 
     for _ in range(cfg["n_iter"]):
         done = runner.step()

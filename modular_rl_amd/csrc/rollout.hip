@@ -1673,8 +1673,11 @@ int64_t mrl_rollout_sync_bytes(const mrl_rollout_desc* d) {
 
 // The nb blocks fit one per CU of the launch stream (its CU mask) at this kernel's
 // register use: the persistent launch may run (its blocks wait on each other, so the
-// whole grid must be resident at once).
-static bool persistent_fits(int nb, hipStream_t s) {
+// whole grid must be resident at once).  launch_cus > 0: the CUs of the stream a
+// captured graph will replay on (the capture stream's mask says nothing about it);
+// < 0: debug, no check.
+static bool persistent_fits(int nb, hipStream_t s, int launch_cus) {
+  if (launch_cus < 0) return true;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return false;
@@ -1687,6 +1690,7 @@ static bool persistent_fits(int nb, hipStream_t s) {
       for (int w = 0; w < words; ++w) cus += __builtin_popcount(mask[w]);
     }
   }
+  if (launch_cus > 0) cus = min(launch_cus, ncu);
   return nb <= cus;
 }
 
@@ -1702,7 +1706,7 @@ int mrl_rollout_run(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const fl
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   RollArgs a = make_args(d, b);
-  if (!persistent || !sync || !persistent_fits(a.nb, s)) {
+  if (!persistent || !sync || !persistent_fits(a.nb, s, d->launch_cus)) {
     rc = mrl_rollout_reset(d, b, stream);
     for (int32_t t = 0; t < d->horizon && rc == OK; ++t) rc = mrl_rollout_step(d, pol, theta, rimage, b, t, stream);
     return rc;

@@ -11,6 +11,11 @@ every reduction the update consumes is summed over ranks first:
   * VF loss and gradient of every L-BFGS evaluation,
   * the ZFilter running-stat deltas once per iteration (Chan merge, rank order).
 ``backend="nccl"`` is RCCL on ROCm; ``gloo`` is used by the CPU tests.
+
+``Comm(force=True)`` (or ``MRL_COMM_FORCE=1`` with ``init_from_env``) keeps every
+collective on even at world size 1, so one GPU exercises the RCCL path -- its
+communicator, its stream ordering against the rollout's CU-masked streams -- with
+results that must equal the no-communication run bit for bit (a sum over one rank).
 """
 import os
 
@@ -19,9 +24,10 @@ import torch.distributed as dist
 
 
 class Comm:
-    def __init__(self, group=None):
+    def __init__(self, group=None, force=False):
         self.group = group
-        self.enabled = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        up = dist.is_available() and dist.is_initialized()
+        self.enabled = up and (dist.get_world_size(group) > 1 or bool(force))
         self.rank = dist.get_rank(group) if self.enabled else 0
         self.world = dist.get_world_size(group) if self.enabled else 1
 
@@ -54,12 +60,22 @@ class Comm:
 def init_from_env(backend=None):
     """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torchrun) if present.
     ``MRL_DIST_BACKEND=gloo`` rehearses the multi-rank path with several ranks sharing
-    one GPU (each rank uses device LOCAL_RANK mod the visible device count)."""
-    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or dist.is_initialized():
+    one GPU (each rank uses device LOCAL_RANK mod the visible device count).
+    ``MRL_COMM_FORCE=1`` initialises the process group even at world size 1 and keeps
+    every collective on (the RCCL path on one GPU)."""
+    force = os.environ.get("MRL_COMM_FORCE", "0") == "1"
+    if dist.is_initialized():
+        return Comm(force=force)
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 and not force:
         return Comm()
     if backend is None:
         backend = os.environ.get("MRL_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if torch.cuda.is_available():
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
     dist.init_process_group(backend=backend)
-    return Comm()
+    return Comm(force=force)

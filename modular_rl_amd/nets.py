@@ -376,7 +376,6 @@ class LayeredMlpNet:
             self._tape = (key, Xb, ldxb, H, Z, theta)
             return self._tape
         X, ldx = self._input(x, n, ep_t, timestep_limit, name="tape_x")
-        X, ldx = self._input(x, n, ep_t, timestep_limit, name="tape_x")
         H = [self.ws.get(f"tape_h{l}", n * d, torch.float32) for l, d in enumerate(self.hid_sizes)]
         Z = self.ws.get("tape_z", n * self.n_out, torch.float32)
         self._forward(X, ldx, n, theta, H, Z)

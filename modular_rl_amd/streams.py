@@ -70,3 +70,13 @@ def stream_cus(s):
     mask = (ctypes.c_uint32 * words)()
     call("mrl_stream_get_cu_mask", ctypes.c_void_p(s.cuda_stream), words, mask)
     return [i for i in range(n) if (mask[i // 32] >> (i % 32)) & 1]
+
+
+def launch_cus(s=None):
+    """CUs a launch on stream ``s`` (default: the current stream) may use: the CU set of
+    a stream made by masked_stream, else the whole device."""
+    s = torch.cuda.current_stream() if s is None else s
+    for (dev, cus), st in _by_cus.items():
+        if st.cuda_stream == s.cuda_stream:
+            return len(cus)
+    return cu_count()
