@@ -8,16 +8,25 @@ absent: ordinary ModuleNotFoundError), so:
   ``distributions`` are imported as-is through a stub package whose __path__
   points at /root/reference/modular_rl (bypassing its __init__), and
 * ``trpo.cg``, ``trpo.linesearch``, ``trpo.TrpoUpdater.__call__``,
-  ``core.compute_advantage``, ``core.add_episode_stats`` and ``core.pathlength``
-  are AST-extracted from the reference files, with the HEAD-only TF diagnostics
-  removed (trpo.py:82,84,98,100,131,132; core.py:79-96), and executed.
+  ``core.compute_advantage``, ``core.add_episode_stats``, ``core.pathlength``,
+  ``core.NnVf.fit`` / ``preproc``, ``core.NnRegression.fit`` and
+  ``core.LbfgsOptimizer.update`` are AST-extracted from the reference files, with
+  the HEAD-only TF diagnostics removed (trpo.py:82,84,98,100,131,132; core.py:79-96),
+  and executed.
 
 The Theano-compiled callables that ``TrpoUpdater.__call__`` needs
-(compute_policy_gradient / compute_losses / compute_fisher_vector_product) are
-injected from ``oracle/torch_ref.py`` -- torch double-backward, Theano's own
-formulation (trpo.py:29-70).  Everything the fixture records about CG, step
-scaling, the line search and the returned stats is therefore produced by the
-reference's own control flow.
+(compute_policy_gradient / compute_losses / compute_fisher_vector_product) and the
+VF regression's (predict / f_lossgrad / f_losses, core.py:608,670-671) are injected
+from ``oracle/torch_ref.py`` -- torch autograd / double-backward, Theano's own
+formulation (trpo.py:29-70, core.py:607-618).  Everything the fixtures record about
+CG, step scaling, the line search, the L-BFGS fit and the returned stats is
+therefore produced by the reference's own control flow.
+
+Each TRPO / VF case is generated twice: in float64 (truth) and floatX-faithful
+(suffix ``f``): the injected graphs evaluate in float32 and ``set_params_flat`` casts
+to float32, as Theano with ``floatX=float32`` does (keras_theano_setup.py:5-6,
+core.py:540); the reference's numpy code (cg, linesearch, the step scaling) then runs
+on the float32 arrays it receives, under this numpy's (2.x) promotion rules.
 
 Usage:  python tests/golden/make_golden.py      (writes tests/golden/*.npz)
 """
@@ -30,7 +39,9 @@ import types
 from collections import OrderedDict
 
 import numpy as np
+import scipy
 import scipy.signal  # noqa: F401  (misc_utils uses scipy.signal via `import scipy`)
+import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
@@ -184,6 +195,43 @@ def main():
                                        "expected_improve, ratio))"})
     call = ns_tr["__call__"]
     f32 = (lambda a: np.asarray(a, dtype=np.float32).astype(np.float64))
+
+    def run_trpo(k, spec, th0, ob, act, adv, oldprob, cfg, dtype):
+        """One reference TrpoUpdater.__call__ on a 2-path batch; records under key k."""
+        tdt = torch.float64 if dtype == np.float64 else torch.float32
+        state = {"th": th0.astype(dtype)}
+        self = types.SimpleNamespace(
+            cfg=cfg, loss_names=["surr", "kl", "ent"],
+            get_params_flat=lambda: state["th"].copy(),
+            set_params_flat=lambda t: state.__setitem__("th", np.asarray(t, dtype=dtype).copy()),
+            compute_policy_gradient=lambda o, a, ad, op: torch_ref.pg_autograd(spec, state["th"], o, a, ad, op, tdt),
+            compute_losses=(lambda o, a, ad, op: list(trpo_np.surr_kl_ent(spec, state["th"], o, a, ad, op)))
+            if dtype == np.float64 else (lambda o, a, ad, op: torch_ref.losses(spec, state["th"], o, a, ad, op, tdt)),
+            compute_fisher_vector_product=lambda p, o, a, ad, op: torch_ref.fvp_double_backward(
+                spec, state["th"], p, o, tdt),
+        )
+        cast = (lambda a: np.asarray(a).astype(dtype)) if dtype == np.float32 else (lambda a: a)
+        N = ob.shape[0]
+        paths = [dict(prob=cast(oldprob[:N // 2]), observation=cast(ob[:N // 2]), action=cast(act[:N // 2]),
+                      advantage=cast(adv[:N // 2])),
+                 dict(prob=cast(oldprob[N // 2:]), observation=cast(ob[N // 2:]), action=cast(act[N // 2:]),
+                      advantage=cast(adv[N // 2:]))]
+        rec.clear()
+        stats = quiet(call, self, paths)
+        out[f"{k}_theta1"] = state["th"].astype(np.float64)
+        out[f"{k}_stats"] = np.array([stats[n] for n in ("surr_before", "surr_after", "kl_before", "kl_after",
+                                                         "ent_before", "ent_after")], dtype=np.float64)
+        ls = np.array(rec["ls"], dtype=np.float64)  # rows: (stepfrac, actual, expected, ratio)
+        accepted = [i for i, (_, act_i, _, r) in enumerate(ls) if r > 0.1 and act_i > 0]
+        for name in ("g", "stepdir", "fullstep"):
+            out[f"{k}_{name}"] = np.asarray(rec[name], dtype=np.float64)
+        for name in ("shs", "lm", "rate"):
+            out[f"{k}_{name}"] = np.float64(rec[name])
+        out[f"{k}_ls"] = ls
+        out[f"{k}_k"] = np.int64(accepted[0] if accepted else -1)
+        # distance of the accept test from its threshold at the accepted backtrack
+        out[f"{k}_margin"] = np.float64(ls[accepted[0], 3] - 0.1 if accepted else np.nan)
+
     for tag, (nin, nout, head, N) in {"gauss": (11, 3, "gauss", 512), "cat": (4, 2, "softmax", 400)}.items():
         spec = trpo_np.Spec(nin, [64, 64], nout, head)
         th0 = trpo_np.mlp_init(rng, spec.shapes, head == "gauss")
@@ -199,32 +247,12 @@ def main():
         # cfg 1: the battery settings; cfg 2: a trust region so large the line search backtracks
         for cfg_i, cfg in enumerate([dict(cg_damping=1e-3, max_kl=1e-2), dict(cg_damping=0.1, max_kl=0.01),
                                      dict(cg_damping=0.1, max_kl=100.0)]):
-            state = {"th": th0.copy()}
-            self = types.SimpleNamespace(
-                cfg=cfg, loss_names=["surr", "kl", "ent"],
-                get_params_flat=lambda: state["th"].copy(),
-                set_params_flat=lambda t: state.__setitem__("th", np.asarray(t, dtype=np.float64).copy()),
-                compute_policy_gradient=lambda o, a, ad, op: torch_ref.pg_autograd(spec, state["th"], o, a, ad, op),
-                compute_losses=lambda o, a, ad, op: list(trpo_np.surr_kl_ent(spec, state["th"], o, a, ad, op)),
-                compute_fisher_vector_product=lambda p, o, a, ad, op: torch_ref.fvp_double_backward(spec, state["th"], p, o),
-            )
-            paths = [dict(prob=oldprob[:N // 2], observation=ob[:N // 2], action=act[:N // 2], advantage=adv[:N // 2]),
-                     dict(prob=oldprob[N // 2:], observation=ob[N // 2:], action=act[N // 2:], advantage=adv[N // 2:])]
-            rec.clear()
-            stats = quiet(call, self, paths)
             k = f"{tag}{cfg_i}"
-            out[f"{k}_theta0"], out[f"{k}_theta1"] = th0, state["th"]
+            out[f"{k}_theta0"] = th0
             out[f"{k}_ob"], out[f"{k}_act"], out[f"{k}_adv"], out[f"{k}_oldprob"] = ob, act, adv, oldprob
             out[f"{k}_cfg"] = np.array([cfg["cg_damping"], cfg["max_kl"]])
-            out[f"{k}_stats"] = np.array([stats[n] for n in ("surr_before", "surr_after", "kl_before", "kl_after", "ent_before", "ent_after")])
-            ls = np.array(rec["ls"], dtype=np.float64)  # rows: (stepfrac, actual, expected, ratio)
-            accepted = [i for i, (_, act_i, _, r) in enumerate(ls) if r > 0.1 and act_i > 0]
-            out[f"{k}_g"], out[f"{k}_stepdir"], out[f"{k}_fullstep"] = rec["g"], rec["stepdir"], rec["fullstep"]
-            out[f"{k}_shs"], out[f"{k}_lm"], out[f"{k}_rate"] = np.float64(rec["shs"]), np.float64(rec["lm"]), np.float64(rec["rate"])
-            out[f"{k}_ls"] = ls
-            out[f"{k}_k"] = np.int64(accepted[0] if accepted else -1)
-            # distance of the accept test from its threshold at the accepted backtrack
-            out[f"{k}_margin"] = np.float64(ls[accepted[0], 3] - 0.1 if accepted else np.nan)
+            run_trpo(k, spec, th0, ob, act, adv, oldprob, cfg, np.float64)
+            run_trpo(k + "f", spec, th0, ob, act, adv, oldprob, cfg, np.float32)
     np.savez(os.path.join(HERE, "trpo_update.npz"), **out)
 
     # ---------------- compute_advantage (core.py:63-105, TF check 79-96 dropped)
@@ -257,6 +285,82 @@ def main():
             out["stats_vals"] = np.array([v for v in stats.values() if np.ndim(v) == 0], dtype=np.float64)
     out["n_paths"] = len(lens)
     np.savez(os.path.join(HERE, "compute_advantage.npz"), **out)
+
+    # ---------------- TrpoUpdater.__call__ on deep nets (the layered GEMM path): one
+    # Dense layer per hid_sizes entry (agentzoo.py:34-36), three hidden layers here
+    rng = np.random.default_rng(7)
+    out = {}
+    for tag, (nin, hid, nout, head, N) in {"deepg": (40, [64, 64, 64], 9, "gauss", 600),
+                                           "deepc": (20, [64, 48, 32], 5, "softmax", 500)}.items():
+        spec = trpo_np.Spec(nin, hid, nout, head)
+        th0 = trpo_np.mlp_init(rng, spec.shapes, head == "gauss")
+        th0 = f32(th0 + 0.02 * rng.standard_normal(th0.shape))
+        ob = f32(rng.standard_normal((N, nin)))
+        oldprob = f32(trpo_np.policy_prob(spec, th0 + 0.01 * rng.standard_normal(th0.shape), ob))
+        noise = rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N)
+        act = trpo_np.sample(spec, oldprob, noise)
+        act = f32(act) if head == "gauss" else act
+        adv = f32(trpo_np.standardize(rng.standard_normal(N) + 0.3 * ob[:, 0]))
+        for cfg_i, cfg in enumerate([dict(cg_damping=0.1, max_kl=0.01), dict(cg_damping=0.1, max_kl=100.0)]):
+            k = f"{tag}{cfg_i}"
+            out[f"{k}_theta0"], out[f"{k}_hid"] = th0, np.array(hid)
+            out[f"{k}_ob"], out[f"{k}_act"], out[f"{k}_adv"], out[f"{k}_oldprob"] = ob, act, adv, oldprob
+            out[f"{k}_cfg"] = np.array([cfg["cg_damping"], cfg["max_kl"]])
+            run_trpo(k, spec, th0, ob, act, adv, oldprob, cfg, np.float64)
+            run_trpo(k + "f", spec, th0, ob, act, adv, oldprob, cfg, np.float32)
+    np.savez(os.path.join(HERE, "trpo_update_deep.npz"), **out)
+
+    # ---------------- NnVf.fit -> NnRegression.fit -> LbfgsOptimizer.update
+    # (core.py:652-660, 620-637, 674-697): the reference's own fit, scipy L-BFGS-B with
+    # maxiter=2 and mixfrac=0.1 (agentzoo.py:60), on paths of fp32-representable
+    # observations and returns; opt_info (funcalls, nit) recorded after core.py:687.
+    import scipy.optimize  # noqa: F401  (the extracted update calls scipy.optimize)
+    vrec = {}
+    ns_v = extract(cr, ["NnVf.fit", "NnVf.preproc", "NnRegression.fit", "LbfgsOptimizer.update"],
+                   extra_ns={"np": np, "scipy": scipy, "OrderedDict": OrderedDict, "concat": np.concatenate,
+                             "explained_variance_2d": mu.explained_variance_2d, "explained_variance": mu.explained_variance,
+                             "_rec": vrec},
+                   record_after={687: "_rec.update(funcalls=opt_info['funcalls'], nit=opt_info['nit'])"})
+    # NnVf.fit and NnRegression.fit share the name ``fit`` (the later wins in ns_v)
+    nnvf_fit = extract(cr, ["NnVf.fit"], extra_ns={"np": np, "concat": np.concatenate})["fit"]
+    out = {}
+    for tag, (nin, hid, lens, limit, r0) in {"hop": (11, [64, 64], [120, 333, 1, 246], 1000, 3.0),
+                                             "cart": (4, [64, 64], [200, 57, 43], 200, 20.0),
+                                             "deep": (20, [64, 48, 32], [150, 150, 211], 500, -2.0)}.items():
+        spec = trpo_np.Spec(nin + 1, hid, 1, "linear")
+        th0 = f32(trpo_np.mlp_init(rng, spec.shapes, False) + 0.05 * rng.standard_normal(spec.P))
+        obs = [f32(rng.standard_normal((L, nin))) for L in lens]
+        rets = [f32(r0 + 2.0 * rng.standard_normal(L) + np.linspace(0, 1, L)) for L in lens]
+        out[f"{tag}_theta0"], out[f"{tag}_hid"], out[f"{tag}_limit"] = th0, np.array(hid), np.int64(limit)
+        for i, (o, r) in enumerate(zip(obs, rets)):
+            out[f"{tag}_obs{i}"], out[f"{tag}_ret{i}"] = o, r
+        out[f"{tag}_npaths"] = np.int64(len(lens))
+        for sfx, dtype in (("", np.float64), ("f", np.float32)):
+            tdt = torch.float64 if dtype == np.float64 else torch.float32
+            state = {"th": th0.astype(dtype)}
+            opt = types.SimpleNamespace(
+                maxiter=2, all_losses=OrderedDict((n, None) for n in ("loss", "mse", "l2")),
+                get_params_flat=lambda: state["th"].copy(),
+                set_params_flat=lambda t: state.__setitem__("th", np.asarray(t, dtype=dtype).copy()),
+                f_lossgrad=lambda x, y: torch_ref.vf_lossgrad(spec, state["th"], x, y, tdt),
+                f_losses=lambda x, y: torch_ref.vf_losses(spec, state["th"], x, y, tdt))
+            opt.update = types.MethodType(ns_v["update"], opt)
+            reg = types.SimpleNamespace(mixfrac=0.1, opt=opt,
+                                        predict=lambda x: torch_ref.vf_predict(spec, state["th"], x, tdt))
+            reg.fit = types.MethodType(ns_v["fit"], reg)
+            vf = types.SimpleNamespace(reg=reg, timestep_limit=limit)
+            vf.preproc = types.MethodType(ns_v["preproc"], vf)
+            paths = [dict(observation=o, **{"return": r}) for o, r in zip(obs, rets)]
+            vrec.clear()
+            # the HEAD NnVf.fit (core.py:652-657) returns (stats, ob_no, vtarg)
+            stats, X, vtarg = quiet(nnvf_fit, vf, paths)
+            k = tag + sfx
+            out[f"{k}_theta1"] = state["th"].astype(np.float64)
+            out[f"{k}_stat_keys"] = np.array(list(stats))
+            out[f"{k}_stats"] = np.array([float(v) for v in stats.values()], dtype=np.float64)
+            out[f"{k}_funcalls"], out[f"{k}_nit"] = np.int64(vrec["funcalls"]), np.int64(vrec["nit"])
+            out[f"{k}_X"] = np.asarray(X, dtype=np.float64)
+    np.savez(os.path.join(HERE, "vf_fit.npz"), **out)
     print("golden fixtures written to", HERE)
 
 

@@ -68,8 +68,18 @@ def test_per_path_api_matches_oracle():
                                      cat([p["action"] for p in paths]), cat([p["advantage"] for p in paths]),
                                      cat([p["prob"] for p in paths]).astype(np.float64), cg_damping=0.1, max_kl=0.01)
     stats = agent.updater(paths)
-    assert agent.updater.last_diag["k"] == dg_w["k"]
-    np.testing.assert_allclose(stats["kl_after"], st_w["kl_after"], rtol=5e-3)
+    dg = agent.updater.last_diag
+    assert dg["k"] == dg_w["k"]
+    # north_star's 1e-4: theta relative to the step, lm, shs and the six stats
+    th1 = agent.get_flat().astype(np.float64)
+    step = np.abs(th_w - th0).max()
+    assert np.abs(th1 - th_w).max() <= 1e-4 * step, np.abs(th1 - th_w).max() / step
+    np.testing.assert_allclose([dg["lm"], dg["shs"]], [dg_w["lm"], dg_w["shs"]], rtol=1e-4)
+    for k in ("surr_before", "surr_after", "kl_before", "kl_after", "ent_before", "ent_after"):
+        # surr_before = -mean(standardised adv) ~ 0 and kl_before = KL(p_old, p_old) ~ 0:
+        # held absolutely, relative to the after-step values' scale
+        atol = 1e-4 * abs(st_w[k.replace("before", "after")]) if k in ("surr_before", "kl_before") else 0.0
+        np.testing.assert_allclose(stats[k], st_w[k], rtol=1e-4, atol=atol, err_msg=k)
     ob = torch.as_tensor(np.zeros(4, np.float32))
     a, info = agent.act(ob.numpy())
     assert a in (0, 1) and info["prob"].shape == (2,)
