@@ -82,6 +82,27 @@ GAE_BYTES_PER_ROW = 17  # read r 4 + v 4 + flags 1, write adv 4 + ret 4
 PMC_FILE = "pmc_r02.json"
 
 
+def host_info():
+    """The box the CPU baseline ran on: logical CPUs, the affinity set this
+    process may use, the CPU model, and the torch / BLAS thread counts."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        from threadpoolctl import threadpool_info
+        blas = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        blas = None
+    return {"os_cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_model": model,
+            "torch_threads": torch.get_num_threads(), "blas_threads": blas}
+
+
 def cpu_serial_c1(seconds=8.0, seed=0):
     """the reference's serial loop restated -- ONE
     CartPole env, a single-row (M = 1) policy forward per step (core.py:182-221,
@@ -122,6 +143,7 @@ def cpu_serial_c1(seconds=8.0, seed=0):
     limit.unregister()
     torch.set_num_threads(torch_threads)
     return {"value": steps / dt, "unit": "env-steps/s", "trpo_iters_per_sec": iters / dt, "cores": 1, "kind": "port",
+            "box": host_info(),
             "sample": f"C1: {iters} serial TRPO iterations of ONE CartPole-v0 env x 200 steps, one-row policy forward "
                       f"per step, numpy oracle, {dt:.1f} s"}
 
@@ -131,11 +153,9 @@ def cpu_baseline(E, Tn, env_id="Hopper-v2", hid=(64, 64), seed=0):
     from oracle import fma
     from oracle import rollout_np as RO
     from oracle import trpo_np as T
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
-    except Exception:  # pragma: no cover
-        threads = os.cpu_count()
+    box = host_info()
+    # threads the numpy / BLAS work can actually run on: the BLAS pool, within the affinity set
+    threads = min(box["blas_threads"] or box["affinity_cpus"], box["affinity_cpus"])
     rng = np.random.default_rng(seed)
     kind, O, A, limit = {"Hopper-v2": (RO.HOPPER, 11, 3, 1000), "Humanoid-v2": (RO.HUMANOID, 376, 17, 1000),
                          "CartPole-v0": (RO.CARTPOLE, 4, 2, 200)}[env_id]
@@ -161,7 +181,7 @@ def cpu_baseline(E, Tn, env_id="Hopper-v2", hid=(64, 64), seed=0):
     T.trpo_update(spec, th, ob, act[:, 0] if head == "softmax" else act, adv,
                   out["prob"].reshape(N, -1).astype(np.float64), cg_damping=0.1, max_kl=0.01, dtype=np.float32)
     dt = time.perf_counter() - t0
-    return {"value": N / dt, "unit": "env-steps/s", "cores": int(threads), "kind": "port",
+    return {"value": N / dt, "unit": "env-steps/s", "cores": int(threads), "kind": "port", "box": box,
             "sample": f"one full TRPO iteration (rollout+GAE+VF fit+update) of the numpy oracle on {env_id} "
                       f"{E} envs x {Tn} steps = {N} env-steps, net {O}-{'-'.join(map(str, hid))}-{A}, "
                       f"float32 update / float64 rollout (multiply-adds unfused), {dt:.1f} s"}

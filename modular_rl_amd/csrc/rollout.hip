@@ -1671,6 +1671,16 @@ int64_t mrl_rollout_sync_bytes(const mrl_rollout_desc* d) {
   return SYNC_HEAD_BYTES + 2 * (int64_t)(env_info(d->env_id).obs + 1) * nb * 16;
 }
 
+// Zeroes the hand-off workspace before a persistent launch (plain 16-B vector stores;
+// the kernel boundary publishes them).  A kernel, not hipMemsetAsync: replayed from a
+// captured hipGraph after other work had been launched eagerly, the memset node of
+// ROCm 7.2 wrote a repeated 16-B pattern -- {int64 n, double 1/n}, bytes of a later
+// eager launch's arguments -- instead of zeros (tools/dbg/sync_probe.py).
+__global__ __launch_bounds__(256) void sync_clear_kernel(uint4* __restrict__ p, int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256)
+    p[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 // The nb blocks fit one per CU of the launch stream (its CU mask) at this kernel's
 // register use: the persistent launch may run (its blocks wait on each other, so the
 // whole grid must be resident at once).  launch_cus > 0: the CUs of the stream a
@@ -1713,8 +1723,11 @@ int mrl_rollout_run(const mrl_rollout_desc* d, const mrl_mlp_desc* pol, const fl
   }
   const MlpDims md = mlp_dims(pol->n_in, pol->n_out, pol->head == MRL_HEAD_GAUSS);
   const float* logstd = pol->head == MRL_HEAD_GAUSS ? theta + md.tls : nullptr;
-  rc = hip_check(hipMemsetAsync(sync, 0, (size_t)mrl_rollout_sync_bytes(d), s), "mrl_rollout_run");
-  if (rc) return rc;
+  {
+    const int64_t n16 = mrl_rollout_sync_bytes(d) / 16;  // SYNC_HEAD_BYTES + 16-B granules
+    const int nblk = (int)std::min<int64_t>((n16 + 255) / 256, 256);
+    hipLaunchKernelGGL(sync_clear_kernel, dim3(nblk), dim3(256), 0, s, reinterpret_cast<uint4*>(sync), n16);
+  }
   // A plain launch: persistent_fits() guarantees one block per CU of the stream's CU
   // set, so every block becomes resident (kernels of other streams on those CUs finish
   // on their own), and the step hand-off polls are bounded (SPIN_LIMIT).  A cooperative

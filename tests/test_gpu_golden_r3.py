@@ -50,7 +50,7 @@ def _update(d, tag, nin, hid, nout, head):
 
 
 def _check_update(d, tag, th1, stats, dg, tol):
-    th0 = d[f"{tag}_theta0"]
+    th0 = d[f"{tag.rstrip('f')}_theta0"]  # the floatX-faithful run starts from the same inputs
     assert dg["success"] and dg["k"] == int(d[f"{tag}_k"]), (dg["k"], int(d[f"{tag}_k"]))
     want = d[f"{tag}_theta1"]
     step = np.abs(want - th0).max()
@@ -107,8 +107,8 @@ def test_cat0_is_as_close_as_the_references_own_fp32_run():
     assert dg["k"] == int(d["cat0_k"]) == int(d["cat0f_k"])
     err = np.abs(th1 - want).max() / step
     assert err <= 2 * ref32, (err, ref32)
-    lm_ref32 = abs(d["cat0f_lm"] / d["cat0_lm"] - 1)
-    assert abs(dg["lm"] / d["cat0_lm"] - 1) <= max(2 * lm_ref32, 1e-4)
+    # lm = sqrt(s.(F + dI)s / 2 max_kl) depends on the unconverged step direction too
+    assert abs(dg["lm"] / d["cat0_lm"] - 1) <= 2 * ref32
     got = np.array([stats[k] for k in STAT_KEYS])
     np.testing.assert_allclose(got[[0, 2, 4]], d["cat0_stats"][[0, 2, 4]], rtol=1e-4, atol=1e-9)
 
