@@ -285,6 +285,22 @@ int mrl_trpo_step_ax(const double* ax, const double* x, const float* g, double m
 /* theta_out = (float)(theta_old + frac * fullstep)   (linesearch, trpo.py:150, core.py:540) */
 int mrl_axpy_cast(const float* theta_old, const double* fullstep, double frac, int64_t n, float* theta_out,
                   void* stream);
+/* ---------------------------------------------------------------- batched line search
+ * The backtracking line search (trpo.py:143-159) scores candidates theta_k =
+ * (float)(theta_old + 0.5^(k0+k) fullstep) (stepfrac k0+k; SetFromFlat's cast, core.py:540).
+ * candidates: out [K, n], one launch (0 < K, k0 + K <= 64). */
+int mrl_linesearch_candidates(const float* theta_old, const double* fullstep, int32_t k0, int32_t K, int64_t n,
+                              float* out, void* stream);
+/* Fused 64-wide policy: the K candidates scored in one call -- candidates into cand [K, P],
+ * per candidate its forward image (images + k*image_stride; f32 image floats or bf16 image
+ * words by `compute`, MRL_COMPUTE_*), a MRL_EPI_LOSSES pass over io's rows into partials +
+ * k*partial_stride ([partial rows, 4] fp64; io->partial / act_cache ignored) and out[k*4..] =
+ * (sum ratio*adv, sum kl, sum entropy, rows): the caller reads out back ONCE (one all-reduce
+ * of [K, 4] in data-parallel mode) and takes the first k whose ratio passes, as the
+ * reference's serial loop does.  Replaces K rounds of compute_losses + readback. */
+int mrl_linesearch_eval(const mrl_mlp_desc* pol, int32_t compute, const float* theta_old, const double* fullstep,
+                        int32_t k0, int32_t K, const mrl_rows_io* io, float* cand, float* images,
+                        int64_t image_stride, double* partials, int64_t partial_stride, double* out, void* stream);
 /* Adam in floatX (PpoSgdUpdater's adam_updates, ppo.py:231-258): m, v, theta fp32 [n];
  * a_t = lr sqrt(1-b2^t)/(1-b1^t) computed by the caller */
 int mrl_adam_step(float* theta, const float* g, float* m, float* v, double a_t, double beta1, double beta2,

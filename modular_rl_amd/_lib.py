@@ -116,6 +116,8 @@ SIGNATURES = {
     "mrl_stream_get_cu_mask": (i32, [vp, i32, vp]),
     "mrl_stream_destroy": (i32, [vp]),
     "mrl_axpy_cast": (i32, [vp, vp, f64, i64, vp, vp]),
+    "mrl_linesearch_candidates": (i32, [vp, vp, i32, i32, i64, vp, vp]),
+    "mrl_linesearch_eval": (i32, [vp, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i64, vp, vp]),
     "mrl_cast_scale_f32_f64": (i32, [vp, f64, i64, vp, vp]),
     "mrl_adam_step": (i32, [vp, vp, vp, vp, f64, f64, f64, f64, i64, vp]),
     "mrl_gather_rows": (i32, [vp, vp, i64, i64, vp, vp]),

@@ -964,4 +964,36 @@ int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* 
   return hip_check(hipGetLastError(), "mrl_reduce_rows_f64");
 }
 
+// K line-search candidates of the fused policy scored in one call, read back once by the
+// caller (trpo.py:143-159): candidates -> per candidate its forward image + a LOSSES pass
+// into its own partial rows -> out[k] = the candidate's (surr, kl, ent, n) sums.
+int mrl_linesearch_eval(const mrl_mlp_desc* pol, int32_t compute, const float* theta_old, const double* fullstep,
+                        int32_t k0, int32_t K, const mrl_rows_io* io, float* cand, float* images, int64_t image_stride,
+                        double* partials, int64_t partial_stride, double* out, void* stream) {
+  int rc = check_desc(pol);
+  if (rc) return rc;
+  if (!io || !cand || !images || !partials || !out) return fail(E_ARG, "mrl_linesearch_eval: null pointer");
+  if (compute != MRL_COMPUTE_F32 && compute != MRL_COMPUTE_BF16) return fail(E_ARG, "bad compute");
+  const bool bf = compute == MRL_COMPUTE_BF16;
+  const int64_t P = mrl_mlp_num_params(pol);
+  const int64_t img = bf ? mrl_mlp_image_words_bf16(pol) : mrl_mlp_image_floats(pol);
+  const int64_t prow = bf ? mrl_partial_rows_bf16(io->n) : mrl_partial_rows(io->n);
+  if (image_stride < img || partial_stride < prow * 4) return fail(E_ARG, "mrl_linesearch_eval: strides too small");
+  rc = mrl_linesearch_candidates(theta_old, fullstep, k0, K, P, cand, stream);
+  for (int32_t k = 0; k < K && rc == OK; ++k) {
+    const float* th = cand + (int64_t)k * P;
+    float* im = images + (int64_t)k * image_stride;
+    mrl_rows_io iok = *io;
+    iok.partial = partials + (int64_t)k * partial_stride;
+    iok.cache_mode = MRL_CACHE_NONE;
+    iok.act_cache = nullptr;
+    rc = bf ? mrl_mlp_pack_bf16(pol, th, im, 1, nullptr, stream) : mrl_mlp_pack(pol, th, im, 1, nullptr, stream);
+    if (rc == OK)
+      rc = bf ? mrl_mlp_rows_bf16(pol, MRL_EPI_LOSSES, th, im, nullptr, nullptr, &iok, nullptr, stream)
+              : mrl_mlp_rows(pol, MRL_EPI_LOSSES, th, im, nullptr, nullptr, &iok, nullptr, stream);
+    if (rc == OK) rc = mrl_reduce_rows_f64(iok.partial, prow, 4, out + 4 * (int64_t)k, nullptr, stream);
+  }
+  return rc;
+}
+
 }  // extern "C"

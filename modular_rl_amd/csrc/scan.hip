@@ -591,6 +591,16 @@ __global__ void axpy_cast_kernel(const float* __restrict__ a, const double* __re
     o[i] = (float)((double)a[i] + frac * b[i]);
 }
 
+// K line-search candidates (trpo.py:149-150): row k = (float)(theta_old + 0.5^(k0+k) fullstep)
+// -- axpy_cast_kernel's arithmetic per row (linesearch's stepfrac is an exact power of two)
+__global__ void ls_candidates_kernel(const float* __restrict__ a, const double* __restrict__ b, int k0, int K,
+                                     int64_t n, float* __restrict__ o) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double ai = (double)a[i], bi = b[i];
+    for (int k = 0; k < K; ++k) o[(int64_t)k * n + i] = (float)(ai + ldexp(1.0, -(k0 + k)) * bi);
+  }
+}
+
 // Adam step in floatX (ppo.py:231-258): m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
 // theta -= a_t m / (sqrt(v) + eps), a_t = lr sqrt(1-b2^t)/(1-b1^t) from the host
 __global__ void adam_kernel(float* __restrict__ th, const float* __restrict__ g, float* __restrict__ m,
@@ -912,6 +922,15 @@ int mrl_axpy_cast(const float* theta_old, const double* fullstep, double frac, i
   hipLaunchKernelGGL(axpy_cast_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, theta_old, fullstep, frac,
                      n, theta_out);
   return hip_check(hipGetLastError(), "mrl_axpy_cast");
+}
+
+int mrl_linesearch_candidates(const float* theta_old, const double* fullstep, int32_t k0, int32_t K, int64_t n,
+                              float* out, void* stream) {
+  if (!theta_old || !fullstep || !out) return fail(E_ARG, "null pointer");
+  if (K <= 0 || k0 < 0 || k0 + K > 64) return fail(E_ARG, "mrl_linesearch_candidates: need 0 < K, 0 <= k0, k0 + K <= 64");
+  hipLaunchKernelGGL(ls_candidates_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, theta_old, fullstep,
+                     (int)k0, (int)K, n, out);
+  return hip_check(hipGetLastError(), "mrl_linesearch_candidates");
 }
 
 int mrl_adam_step(float* theta, const float* g, float* m, float* v, double a_t, double beta1, double beta2,

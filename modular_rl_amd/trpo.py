@@ -14,13 +14,17 @@ collector.  The numerics run in libmrl_hip:
                         updates (z_k = the damped Fisher product of p_k; linearity),
                         so the Fvp(stepdir) of trpo.py:119-122 costs no pass over the
                         rows (the duplicate diagnostic Fvp of trpo.py:111 is dropped)
-  linesearch            per candidate: theta = theta_old + frac*fullstep (fp64,
-                        cast to fp32 like SetFromFlat) + one fused loss pass; the
+  linesearch            candidates theta = theta_old + frac*fullstep (fp64, cast to
+                        fp32 like SetFromFlat) scored in batches (mrl_linesearch_eval:
+                        K candidates, one readback / one [K, 4] all-reduce per batch;
+                        batches of 1, 3 and 6 cover the reference's 10 backtracks), the
+                        first accepted k in order exactly as the serial loop; the
                         accepted candidate's (surr, kl, ent) are losses_after.
 
 In data-parallel mode every sum above is all-reduced over ranks (dist.Comm)
 before it is used, so all ranks take the identical step.
 """
+import ctypes
 from collections import OrderedDict
 
 import numpy as np
@@ -59,6 +63,7 @@ class HipTrpoOps:
         self.step_out = torch.zeros(ns, **f64)
         self.sums = torch.zeros(4, **f64)
         self.batch = None
+        self._ls = None  # batched line search: (K, candidates [K, P], images, partials, sums [K, 4])
 
     def bind(self, batch, inv_n_global):
         self.batch = batch
@@ -118,6 +123,42 @@ class HipTrpoOps:
         call("mrl_axpy_cast", ptr(theta_old), ptr(self.fullstep), float(frac), self.P, ptr(self.cand), stream())
         return self.cand
 
+    def _ls_bufs(self, K):
+        net, n = self.net, self.batch.n
+        prow = net.partial_rows(n) * 4
+        if self._ls is None or self._ls[0] < K or self._ls[3].shape[1] < prow:
+            Kc = max(K, self._ls[0] if self._ls is not None else 0)
+            dev = net.device
+            imgs = (torch.zeros(Kc, net.image.numel(), dtype=torch.float32, device=dev)
+                    if not getattr(net, "layered", False) else None)
+            self._ls = (Kc, torch.zeros(Kc, self.P, dtype=torch.float32, device=dev), imgs,
+                        torch.zeros(Kc, prow, dtype=torch.float64, device=dev),
+                        torch.zeros(Kc, 4, dtype=torch.float64, device=dev))
+        return self._ls
+
+    def losses_batch(self, theta_old, k0, K):
+        """(surr, kl, ent, n) sums of the K candidates theta_old + .5^(k0+k) fullstep
+        (trpo.py:149-150) as a device [K, 4] tensor: one call on the fused path
+        (mrl_linesearch_eval), candidates + K loss passes on the layered one."""
+        b, net = self.batch, self.net
+        _, cand, imgs, partials, sums = self._ls_bufs(K)
+        if not getattr(net, "layered", False):
+            io = _lib.RowsIO(ptr(b.obs), None, 1.0, int(b.n), float(self.inv_ng), ptr(b.act), ptr(b.adv), ptr(b.prob),
+                             None, None, None, None, 0.0, 0.0, 0.0, 0, _lib.CACHE_NONE, None)
+            call("mrl_linesearch_eval", ctypes.byref(net.desc), _lib.COMPUTE[net.dtype], ptr(theta_old),
+                 ptr(self.fullstep), int(k0), int(K), ctypes.byref(io), ptr(cand), ptr(imgs), int(imgs.shape[1]),
+                 ptr(partials), int(partials.shape[1]), ptr(sums), stream())
+        else:
+            call("mrl_linesearch_candidates", ptr(theta_old), ptr(self.fullstep), int(k0), int(K), self.P, ptr(cand),
+                 stream())
+            for k in range(K):
+                th = cand[k]
+                net.pack(theta=th, image=self.cand_image, fwd_only=True)
+                net.rows(_lib.EPI_LOSSES, b.obs, b.n, inv_n_global=self.inv_ng, act=b.act, adv=b.adv, oldprob=b.prob,
+                         partial=self.partial, theta=th, image=self.cand_image)
+                net.reduce_partial(self.partial, b.n, sums[k])
+        return sums[:K], cand
+
 
 def _losses(sums, n_glob):
     s = sums.detach().double().cpu().numpy() if torch.is_tensor(sums) else np.asarray(sums, dtype=np.float64)
@@ -149,6 +190,10 @@ class TrpoUpdater:
     ]
     CG_ITERS = 10
     RESIDUAL_TOL = 1e-10
+    MAX_BACKTRACKS = 10
+    # candidates scored per readback: the first batch is k = 0 alone (accepted in most
+    # updates), then 3, then the remaining 6; None: the serial one-candidate loop
+    LS_BATCHES = (1, 3, 6)
 
     def __init__(self, stochpol, usercfg, comm=None, ops=None):
         self.cfg = update_default_config(self.options, usercfg)
@@ -204,15 +249,18 @@ class TrpoUpdater:
                 timing.drop_last("fvp_jvp_rows", skipped)
                 timing.drop_last("fvp_vjp", skipped)
             fval = losses_before[0]
-
-            def f(stepfrac):
-                l = _losses(self._candidate_losses(thprev, stepfrac), n_glob)
-                return l[0], l
-
             trace = []
-            success, frac, k, laux = linesearch(f, fval, rate, trace=trace)
+            if self.LS_BATCHES:
+                success, frac, k, laux, accepted = self._linesearch_batched(thprev, fval, rate, n_glob, trace)
+            else:
+                def f(stepfrac):
+                    l = _losses(self._candidate_losses(thprev, stepfrac), n_glob)
+                    return l[0], l
+
+                success, frac, k, laux = linesearch(f, fval, rate, max_backtracks=self.MAX_BACKTRACKS, trace=trace)
+                accepted = ops.cand  # the accepted (last evaluated) candidate
             if success:
-                net.theta.copy_(ops.cand)  # the accepted (last evaluated) candidate
+                net.theta.copy_(accepted)
                 losses_after = laux
             else:
                 net.theta.copy_(thprev)
@@ -226,6 +274,32 @@ class TrpoUpdater:
             out[lname + "_before"] = lbefore
             out[lname + "_after"] = lafter
         return out
+
+    def _linesearch_batched(self, thprev, fval, rate, n_glob, trace, accept_ratio=.1):
+        """`trpo.py:143-159` with the candidates scored in batches (LS_BATCHES): each batch
+        is one device call, one all-reduce of its [K, 4] sums and one readback; the
+        accept test runs in the reference's order, so the first accepted k (and the
+        trace up to it) equal the serial loop's."""
+        k0 = 0
+        for K in self.LS_BATCHES:
+            K = min(K, self.MAX_BACKTRACKS - k0)
+            if K <= 0:
+                break
+            sums, cand = self.ops.losses_batch(thprev, k0, K)
+            self.comm.allreduce_(sums)
+            host = sums.cpu().numpy()
+            for j in range(K):
+                k = k0 + j
+                stepfrac = .5 ** k
+                l = _losses(host[j], n_glob)
+                actual = fval - l[0]
+                expected = rate * stepfrac
+                ratio = actual / expected
+                trace.append((stepfrac, actual, expected, ratio))
+                if ratio > accept_ratio and actual > 0:
+                    return True, stepfrac, k, l, cand[j]
+            k0 += K
+        return False, None, -1, None, None
 
     def _candidate_losses(self, thprev, stepfrac):
         th = self.ops.candidate(thprev, stepfrac)

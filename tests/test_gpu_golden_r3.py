@@ -145,3 +145,30 @@ def test_vf_fit_matches_reference_golden(tag):
         for k, v in ref.items():
             atol = 1e-4 if k.startswith("EV") else 1e-9
             np.testing.assert_allclose(stats[k], v, rtol=1e-4, atol=atol, err_msg=f"{tag}{sfx} {k}")
+
+
+@pytest.mark.parametrize("fname,tag", [("trpo_update.npz", "gauss2"), ("trpo_update.npz", "cat2"),
+                                       ("trpo_update.npz", "gauss1"), ("trpo_update_deep.npz", "deepg1"),
+                                       ("trpo_update_deep.npz", "deepc1")])
+def test_batched_linesearch_equals_serial(fname, tag, monkeypatch):
+    """mrl_linesearch_eval's batches (1, 3, 6 candidates per readback) take the same k,
+    the same theta bit for bit and the same backtrack trace as the serial one-candidate
+    loop of trpo.py:143-159, on the golden cases that backtrack (k = 1..3) and one that
+    accepts at k = 0."""
+    from modular_rl_amd.trpo import TrpoUpdater
+    d = np.load(os.path.join(G, fname))
+    deep = tag.startswith("deep")
+    head = "gauss" if "gauss" in tag or tag.startswith("deepg") else "softmax"
+    nin, nout = {(False, "gauss"): (11, 3), (False, "softmax"): (4, 2), (True, "gauss"): (40, 9),
+                 (True, "softmax"): (20, 5)}[(deep, head)]
+    hid = [int(h) for h in d[f"{tag}_hid"]] if deep else [64, 64]
+    out = []
+    for batches in (TrpoUpdater.LS_BATCHES, None):
+        monkeypatch.setattr(TrpoUpdater, "LS_BATCHES", batches)
+        _, th1, stats, dg = _update(d, tag, nin, hid, nout, head)
+        out.append((th1, stats, dg))
+    (ta, sa, da), (tb, sb, db) = out
+    assert da["k"] == db["k"] == int(d[f"{tag}_k"])
+    np.testing.assert_array_equal(ta, tb)
+    np.testing.assert_array_equal(da["ls"], db["ls"])
+    assert [sa[k] for k in STAT_KEYS] == [sb[k] for k in STAT_KEYS]
