@@ -80,6 +80,8 @@ DYNAMICS = {"Hopper-v2": "hopper.xml articulated-body dynamics", "Humanoid-v2": 
             "CartPole-v0": "gym equations"}
 GAE_BYTES_PER_ROW = 17  # read r 4 + v 4 + flags 1, write adv 4 + ret 4
 PMC_FILE = "pmc_r02.json"
+ROLLOUT_ISSUE_FILE = "rollout_issue_r03.json"  # tools/rollout_issue.py: SQ issue cycles per rollout step
+CLOCK_GHZ = 2.4  # MI355X max shader clock (MI355X_MICROARCH.md)
 
 
 def host_info():
@@ -185,6 +187,35 @@ def cpu_baseline(E, Tn, env_id="Hopper-v2", hid=(64, 64), seed=0):
             "sample": f"one full TRPO iteration (rollout+GAE+VF fit+update) of the numpy oracle on {env_id} "
                       f"{E} envs x {Tn} steps = {N} env-steps, net {O}-{'-'.join(map(str, hid))}-{A}, "
                       f"float32 update / float64 rollout (multiply-adds unfused), {dt:.1f} s"}
+
+
+def rollout_latency_roofline(ki, key, pmc, K):
+    """The rollout step is a latency chain (one wave per SIMD, a cross-block hand-off per
+    step), bound by neither MFMA nor HBM: its roof is the wave's own instruction issue
+    time per step (SQ_ACTIVE_INST_ANY per wave per step from a committed PMC pass,
+    tools/rollout_issue.py) at the 2.4 GHz clock.  achieved = the live step time,
+    frac = issue floor / achieved."""
+    us = ki["mean_ms"] * 1e3
+    issue = {}
+    path = os.path.join(ROOT, "profiles", ROLLOUT_ISSUE_FILE)
+    if os.path.exists(path):
+        with open(path) as f:
+            issue = json.load(f).get(key, {})
+    floor = issue["issue_cycles_per_step"] / (CLOCK_GHZ * 1e3) if issue else None
+    out = {"bound": "latency", "achieved": round(us, 3), "peak": round(floor, 3) if floor else None, "unit": "us/step",
+           "frac": round(floor / us, 4) if floor else None,
+           "traffic": pmc.get("rollout_step", {}).get("hbm_bytes_per_launch"),
+           "kernel": "rollout_persistent_kernel (per step)", "cycles_per_step_at_2.4GHz": round(us * CLOCK_GHZ * 1e3),
+           "issue_cycles_per_step": round(issue["issue_cycles_per_step"]) if issue else None,
+           "valu_insts_per_step": round(issue["valu_insts_per_step"]) if issue else None,
+           "issue_source": f"profiles/{ROLLOUT_ISSUE_FILE}[{key}] (rocprofv3 SQ pass)" if issue else None,
+           "mean_launch_ms": round(ki["mean_ms"], 5), "launches_timed": ki["launches"],
+           "ms_per_iter": round(ki["total_ms"] / K, 3),
+           "mfma_frac_of_forward": round(ki["frac_mfma"], 5),
+           "note": ("latency-bound: one persistent launch runs the T steps, each a filter merge over all envs "
+                    "(cross-block hand-off) + the policy forward + fp64 env substeps, one wave per SIMD on E/64 CUs; "
+                    "peak = the wave's instruction-issue time per step (PMC), achieved = rollout region / T")}
+    return out
 
 
 def main():
@@ -324,9 +355,7 @@ def main():
                             "evaluations); achieved = their algorithmic FLOP / their summed HIP-event durations; "
                             "traffic: the Fisher-product launch's PMC bytes")
     if dom == "rollout_step":
-        roofline["note"] = ("latency-bound: one persistent launch runs the T steps, each a filter merge over all "
-                            "envs (cross-block hand-off) + the policy forward (the FLOPs counted) + fp64 env "
-                            "substeps, on E/64 CUs; mean = rollout region / T")
+        roofline = rollout_latency_roofline(kinfo[dom], f"{args.env}/{args.dtype}", pmc, K)
     gae = None
     if "gae_scan" in kern:
         cnt, mean_ms, _ = kern["gae_scan"]
