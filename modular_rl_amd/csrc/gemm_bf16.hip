@@ -19,6 +19,7 @@
 // heads), global -> registers -> LDS double-buffered (the next K step's loads are in
 // flight under this step's MFMAs), blocks dealt to the XCDs in contiguous tile runs.
 #include <math.h>
+#include <stdlib.h>
 
 #include "../../include/mrl_hip.h"
 #include "mlp_device.h"
@@ -193,6 +194,166 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmB16Args g) {
     }
 }
 
+// ------------------------------------------------------------------ streaming NN GEMM
+// For the tall layered-path GEMMs (M ~ 1 M rows, K <= 512, N = 512: HBM-bound at their
+// 256 FLOP per byte) the tiled kernel above re-stages B for every 128-row tile and pays
+// a prologue / epilogue per 8-step K loop.  Here B stays put and A streams:
+//  * one 512-thread block per CU (persistent); its LDS holds one BN-column slice of Bt
+//    for all of K (BN = 128; two 64-column slices of Bt and Bt2 for the dual product),
+//    pitch KP + 8 bf16 (conflict-free ds_read_b128 fragments);
+//  * each wave owns 32 rows at a time and streams their A fragments straight from
+//    global memory into registers, one chunk of CK k-steps ahead of the MFMAs
+//    (register double buffer; two waves per SIMD cover each other's gaps);
+//  * block -> (XCD, column slice, row group): the nslice blocks that need the same A
+//    rows sit on one XCD and walk the same row tiles in the same order, so each A line
+//    comes from HBM once and from that XCD's L2 for the other slices (placement is a
+//    speed assumption only; any placement gives the same result);
+//  * epilogue as above (C^T accumulators: lane j holds row j): bias, tanh / * (1 - H^2),
+//    bf16 or f32 stores.
+// Same operands, same per-output k order as gemm_bf16_kernel (MFMA k-steps of 16 in
+// order, one f32 accumulator per output): bit-identical results.
+struct StreamPlan {
+  int nslice, groups_per_xcd;
+};
+
+template <int KP, bool DUAL, bool OUTBF>
+__global__ __launch_bounds__(512, 2) void gemm_bf16_stream_kernel(GemmB16Args g, StreamPlan pl) {
+  constexpr int BN = DUAL ? 64 : 128;  // output columns per block
+  constexpr int NI = BN / 32;          // 32-column tiles per wave
+  constexpr int NOPS = DUAL ? 2 : 1;
+  constexpr int PITCH = KP + 8;        // bf16 per LDS row
+  constexpr int KS = KP / 16, CPT = 4, CK = KS / CPT;
+  static_assert(KS % CPT == 0, "k-steps must split into 4 chunks");
+  __shared__ __attribute__((aligned(16))) bfr_t sB[NOPS * BN * PITCH];
+  if (g.skip != nullptr && *g.skip != 0) return;
+  const int per_xcd = gridDim.x / 8;
+  const int x = blockIdx.x % 8, l = blockIdx.x / 8;
+  if (l >= pl.groups_per_xcd * pl.nslice) return;
+  const int sl = l % pl.nslice;
+  const int64_t gid = (int64_t)x * pl.groups_per_xcd + l / pl.nslice, NG = 8 * (int64_t)pl.groups_per_xcd;
+  (void)per_xcd;
+  const int64_t n0 = (int64_t)sl * BN;
+  // stage the Bt slice(s): row r of slice op = Bt[n0 + r][0..KP), zero past N and ldb
+  constexpr int CPR = KP / 8;  // 16-B chunks per row
+  for (int i = threadIdx.x; i < NOPS * BN * CPR; i += 512) {
+    const int op = i / (BN * CPR), rem = i % (BN * CPR), r = rem / CPR, c = rem % CPR;
+    const bfr_t* Bt = (DUAL && op) ? g.Bt2 : g.Bt;
+    const int64_t n = n0 + r, kc = 8 * c;
+    u32x4v v = u32x4v{0u, 0u, 0u, 0u};
+    if (n < g.N && kc < g.ldb) v = *reinterpret_cast<const u32x4v*>(Bt + n * g.ldb + kc);
+    *reinterpret_cast<u32x4v*>(sB + (op * BN + r) * PITCH + kc) = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
+  const int64_t ntiles = (g.M + 255) / 256;  // 256 rows per block step: 8 waves x 32
+  if (gid >= ntiles) return;
+  const int64_t my_tiles = (ntiles - 1 - gid) / NG + 1;
+  const int64_t last = g.M - 1;
+  // Chunk c of a tile: operand op = c / CPT (A, then A2 for the dual product -- all of
+  // A.Bt's k-steps before A2.Bt2's, the tiled kernel's accumulation order), k-steps
+  // (c % CPT) * CK .. + CK.  Fragments of row j of the wave's 32, k 16 ks + 8h.
+  constexpr int NCH = CPT * NOPS;
+  auto load = [&](int64_t t, int c, bf16x8 (&a)[CK]) {
+    const int64_t rr = (gid + t * NG) * 256 + 32 * wave + j;
+    const int64_t row = rr < last ? rr : last;
+    const bfr_t* A = (DUAL && c >= CPT) ? g.A2 : g.A;
+    const int cc = c % CPT;
+#pragma unroll
+    for (int i = 0; i < CK; ++i) {
+      const int64_t kc = 16 * (cc * CK + i) + 8 * h;
+      if (cc * CK + i < KS - 1 || kc < g.lda) a[i] = *reinterpret_cast<const bf16x8*>(A + row * g.lda + kc);
+      else a[i] = bf16x8{};
+    }
+  };
+  f32x16 acc[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) acc[ni] = zero16();
+  auto compute = [&](int c, const bf16x8 (&a)[CK]) {
+    const bfr_t* Bs = sB + (c / CPT) * BN * PITCH;
+    const int cc = c % CPT;
+#pragma unroll
+    for (int i = 0; i < CK; ++i) {
+      const int ks = cc * CK + i;
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(Bs + (32 * ni + j) * PITCH + 16 * ks + 8 * h);
+        acc[ni] = MFMA32B(bv, a[i], acc[ni]);
+      }
+    }
+  };
+  bf16x8 b0[CK], b1[CK];
+  load(0, 0, b0);
+  const bool vec = (g.ldc & 3) == 0 && (g.epi != MRL_GEMM_DTANH || (g.ldh & 3) == 0);
+  for (int64_t t = 0; t < my_tiles; ++t) {
+    const int64_t tn = t + 1 < my_tiles ? t + 1 : t;  // the last tile re-loads itself (unused)
+#pragma unroll
+    for (int c = 0; c < NCH; c += 2) {
+      // the fences keep the scheduler from hoisting later chunks' loads and LDS reads
+      // (all of them live at once spilled the whole register file)
+      load(t, c + 1, b1);
+      compute(c, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + 2 < NCH) load(t, c + 2, b0);
+      else load(tn, 0, b0);
+      compute(c + 1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // epilogue of the wave's 32 rows
+    const int64_t row = (gid + t * NG) * 256 + 32 * wave + j;
+    if (row < g.M) {
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int64_t cbase = n0 + 32 * ni;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t cc = cbase + 8 * q + 4 * h;
+          if (vec && cc + 4 <= g.N) {
+            const float4 bb = g.bias != nullptr ? *reinterpret_cast<const float4*>(g.bias + cc)
+                                                : make_float4(0.f, 0.f, 0.f, 0.f);
+            float v[4] = {acc[ni][4 * q + 0] + bb.x, acc[ni][4 * q + 1] + bb.y, acc[ni][4 * q + 2] + bb.z,
+                          acc[ni][4 * q + 3] + bb.w};
+            if (g.epi == MRL_GEMM_TANH) {
+#pragma unroll
+              for (int e = 0; e < 4; e += 2) {
+                const f32x2 tt = tanh_fast2(f32x2{v[e], v[e + 1]});
+                v[e] = tt.x;
+                v[e + 1] = tt.y;
+              }
+            } else if (g.epi == MRL_GEMM_DTANH) {
+              const uint2 hb = *reinterpret_cast<const uint2*>(g.H + row * g.ldh + cc);
+              v[0] *= dtanh(__uint_as_float(hb.x << 16));
+              v[1] *= dtanh(__uint_as_float(hb.x & 0xffff0000u));
+              v[2] *= dtanh(__uint_as_float(hb.y << 16));
+              v[3] *= dtanh(__uint_as_float(hb.y & 0xffff0000u));
+            }
+            if (OUTBF) {
+              const uint2 o = {(uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                               (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)};
+              *reinterpret_cast<uint2*>(reinterpret_cast<bfr_t*>(g.C) + row * g.ldc + cc) = o;
+            } else {
+              *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + row * g.ldc + cc) =
+                  make_float4(v[0], v[1], v[2], v[3]);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int64_t col = cc + e;
+              if (col >= g.N) continue;
+              float xv = acc[ni][4 * q + e] + (g.bias != nullptr ? g.bias[col] : 0.f);
+              if (g.epi == MRL_GEMM_TANH) xv = tanh_fast(xv);
+              else if (g.epi == MRL_GEMM_DTANH) xv *= dtanh(bf2f(g.H[row * g.ldh + col]));
+              if (OUTBF) reinterpret_cast<bfr_t*>(g.C)[row * g.ldc + col] = f2bf(xv);
+              else reinterpret_cast<float*>(g.C)[row * g.ldc + col] = xv;
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) acc[ni] = zero16();
+  }
+}
+
 // ------------------------------------------------------------------ TN (weight grads)
 // K step: 32 rows; LDS images [32 rows][BM or BN columns], pitch 160 bf16 (320 B): a
 // 32-lane half's transposed read (rows q = 0..3, 8 B at columns 16G + 4p) covers all
@@ -348,6 +509,39 @@ __global__ void pack_w_bf16_kernel(const float* __restrict__ w, int64_t din, int
 
 using namespace mrl;
 
+#ifndef MRL_GEMM_STREAM_MIN_M  // rows from which the streaming kernel takes the NN GEMM (0: never)
+#define MRL_GEMM_STREAM_MIN_M 32768
+#endif
+// The streaming kernel for a tall NN product (K of 257..512, N >= 64, one block per CU):
+// launched here and true, or false (the tiled kernel runs).
+static bool stream_gemm_launch(const GemmB16Args& g, bool outbf, bool dual, hipStream_t s) {
+  const int env_min = []() {
+    const char* e = getenv("MRL_GEMM_STREAM_MIN_M");
+    return e ? atoi(e) : MRL_GEMM_STREAM_MIN_M;
+  }();
+  if (env_min <= 0 || g.M < env_min || g.N < 64 || g.K <= 256 || g.K > 512) return false;
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return false;
+  if (ncu < 8 || ncu % 8) return false;
+  const int bn = dual ? 64 : 128;
+  StreamPlan pl;
+  pl.nslice = (int)((g.N + bn - 1) / bn);
+  pl.groups_per_xcd = (ncu / 8) / pl.nslice;
+  if (pl.groups_per_xcd < 1) return false;
+  const dim3 grid((unsigned)ncu), blk(512);
+#define MRL_STREAM(KP, DU, OB) hipLaunchKernelGGL((gemm_bf16_stream_kernel<KP, DU, OB>), grid, blk, 0, s, g, pl)
+  if (g.K <= 384) {
+    if (dual) { if (outbf) MRL_STREAM(384, true, true); else MRL_STREAM(384, true, false); }
+    else { if (outbf) MRL_STREAM(384, false, true); else MRL_STREAM(384, false, false); }
+  } else {
+    if (dual) { if (outbf) MRL_STREAM(512, true, true); else MRL_STREAM(512, true, false); }
+    else { if (outbf) MRL_STREAM(512, false, true); else MRL_STREAM(512, false, false); }
+  }
+#undef MRL_STREAM
+  return true;
+}
+
 extern "C" {
 
 int mrl_gemm_bf16(const mrl_gemm_bf16_desc* d, const int32_t* skip, void* stream) {
@@ -385,6 +579,7 @@ int mrl_gemm_bf16(const mrl_gemm_bf16_desc* d, const int32_t* skip, void* stream
 #define MRL_GEMM_BF16_BK 64
 #endif
   constexpr int BK = MRL_GEMM_BF16_BK;
+  if (stream_gemm_launch(g, bf, d->a2 != nullptr, s)) return hip_check(hipGetLastError(), "mrl_gemm_bf16");
   if (g.N <= 32) {
     const dim3 grid(1, gm);
     if (bf) hipLaunchKernelGGL((gemm_bf16_kernel<32, true, BK>), grid, dim3(256), 0, s, g);
