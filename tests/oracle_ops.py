@@ -93,6 +93,11 @@ class OracleOps:
         self.cand.copy_(theta_old + frac * self.fullstep)
         return self.cand
 
+    def losses_batch(self, theta_old, k0, K):
+        """Stand-in for HipTrpoOps.losses_batch: [K, 4] sums of theta_old + .5^(k0+k) fullstep."""
+        cand = torch.stack([theta_old + (.5 ** (k0 + k)) * self.fullstep for k in range(K)])
+        return torch.stack([self.losses(c) for c in cand]), cand
+
 
 class OracleVfNet:
     """Oracle-backed stand-in for the value-function MlpNet under vf.LbfgsOptimizer --

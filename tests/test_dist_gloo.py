@@ -97,6 +97,20 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _get(q, procs, timeout):
+    """q.get that fails as soon as a rank has died instead of waiting out the timeout."""
+    import queue
+    import time
+    end = time.time() + timeout
+    while time.time() < end:
+        try:
+            return q.get(timeout=2)
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, "rank exited with %s" % dead
+    raise AssertionError("no result within %ss" % timeout)
+
+
 def test_two_rank_update_equals_single_rank_and_oracle():
     from modular_rl_amd.dist import Comm
     ctx = mp.get_context("spawn")
@@ -105,7 +119,7 @@ def test_two_rank_update_equals_single_rank_and_oracle():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    th2, stats2, k2, merged, thv2, infov2 = q.get(timeout=300)
+    th2, stats2, k2, merged, thv2, infov2 = _get(q, procs, 300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
