@@ -15,6 +15,10 @@
 // JVP -> per-row KL metric -> VJP.
 #include <math.h>
 
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "../../include/mrl_hip.h"
 #include "mlp_device.h"
 #include "rows_epilogue.h"
@@ -278,6 +282,9 @@ __device__ inline VjpArgs vjp_shape(const VjpArgs& in) {
 
 #ifndef MRL_VJP_BIAS_REG  // 1: bias gradients from per-lane register partials (no per-tile LDS row sums)
 #define MRL_VJP_BIAS_REG 1
+#endif
+#ifndef MRL_VJP16  // 1: cached VJPs run the transpose-free 16-row kernel (mlp_vjp16_kernel)
+#define MRL_VJP16 1
 #endif
 #ifndef MRL_VJP_MINW  // minimum waves per SIMD the VJP's registers must allow (build switch)
 #define MRL_VJP_MINW 1
@@ -597,6 +604,343 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
   for (int q = 0; q < a.n_sum; ++q) {
     const float s = wave_sumf(gls[q]);
     if (lane == 0) out[d.tls + q] = s;
+  }
+}
+
+// ------------------------------------------------------------------ cached VJP, 16-row tiles
+// The weight gradients sum over rows (K = rows), so their MFMA operands need the row
+// index on the lane groups; the backprop chain sums over units, so its operands need
+// the unit index there.  The kernel above gets both from one layout through LDS
+// transposes.  This one never transposes: on v_mfma_f32_16x16x4_f32 a 16-row tile has
+// two register layouts (c = lane & 15, g = lane >> 4, r = register 0..3 of a tile):
+//   R  D[unit][row]: lane holds row c, units 16 nt + 4 g + r   (K = units operand)
+//   T  D[row][unit]: lane holds unit 16 nt + c, rows 4 g + r   (K = rows operand)
+// and every product is issued in the orientation that yields the layout its consumer
+// needs: gh2 = W2 G in both (4 MFMAs each: K = head outputs), ga2_R . W1^T gives gh1 in
+// T, so ga1 is born in T; the primal activations are read from the cache in the layout
+// each use needs (h1 in T, h2 in R and T; the second read of a tile hits L2).
+//   gW2 += h2_T^T . G     gW1 += h1_T^T . ga2_T     gW0 += x^T . ga1_T     (K = rows)
+//   gh1_T = ga2_R . W1^T                                                   (K = units)
+// MFMA work per 16 rows: 4 + 4 + 16 + 64 + 64 + 16 MT0 (168 at O <= 16), the same cycles
+// per row as the 32-row kernel minus every LDS transpose; the tile state fits 256
+// registers, so a CU runs 8 waves (2 per SIMD) and one wave's loads and VALU work issue
+// under the other's MFMAs.  Same sums as the kernel above in a different row / k order
+// (fp32 rounding differs, not bitwise equal to it).  The W1 and W2 fragments are read
+// straight from the BA1 / BA2 segments of the image (mlp_layout.h).
+constexpr int VJP16_WAVES = 8;
+// a 0 / 1 factor the optimiser cannot see through: v * opaque(m) stays a multiply, so the
+// load of v is not sunk into a branch on m (hipcc drains every outstanding load at such a
+// branch's join, the prefetch with it)
+__device__ inline float opaque(float m) {
+  asm volatile("" : "+v"(m));
+  return m;
+}
+// accumulator registers a wave hands to its partner: gW1 64, gW2 16, gW0 16 MT0, b1 4, b2 1
+#define VJP16_NREG(MT0) (64 + 16 + 16 * (MT0) + 4 + 1)
+// cache offset (floats) of element (32-row tile's row j, unit w of 32-unit slot `slot`)
+__device__ inline int cache_off(int slot, int j, int w) {
+  return ((slot * 4 + (w >> 3)) * 64 + 32 * ((w >> 2) & 1) + j) * 4 + (w & 3);
+}
+
+template <bool WIDE, bool EPT>
+__global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs a, const float* __restrict__ img,
+                                                                     const int32_t* __restrict__ skip) {
+  constexpr int MT0 = WIDE ? 2 : 1;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (skip != nullptr && *skip != 0) return;
+  const MlpDims& d = a.d;
+  // BA1 (W1 fragments, 4096 floats) then BA2 (W2 fragments, 512): contiguous in the image
+  for (int i = threadIdx.x; i < (2 * 32 * 64 + 2 * 4 * 64) / 4; i += 64 * VJP16_WAVES)
+    reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img + d.ba1)[i];
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform tile bases
+  const int A = d.A, gh = a.gh;
+  const int KS2 = (A + 3) >> 2;  // head k-steps (A <= 8)
+  // W2 fragment (nt, ks) = W2[16 nt + c][4 ks + g] (zero past A): BA2 holds W2[i][o] at
+  // ((i >> 5) * 64 + 32 (o >> 2) + (i & 31)) * 4 + (o & 3)
+  const float* w2l = lds + 2 * 32 * 64 + 4 * c + g;
+  auto w2frag = [&](int nt, int ks) { return w2l[((nt >> 1) * 64 + 32 * ks + 16 * (nt & 1)) * 4]; };
+  __syncthreads();
+  // W1 fragment (nt, mt): W1[16 nt + c][16 mt + 4 g + 0..3] as one float4 of BA1
+  const float* w1l = lds + (32 * (g & 1) + c) * 4;
+  auto w1frag = [&](int nt, int mt) {
+    const int s4 = 4 * (mt >> 1) + 2 * (mt & 1) + (g >> 1);
+    return ld4(w1l + (((nt >> 1) * 8 + s4) * 64 + 16 * (nt & 1)) * 4);
+  };
+  // per-lane parts of the cache offsets (cache_off): T gathers (unit 16 p + c, row 4 g + r)
+  // and R float4s (row c, units 16 p + 4 g .. + 3); the (slot, p, r) parts are constants
+  const int offT = ((c >> 3) * 64 + 32 * ((c >> 2) & 1) + 4 * g) * 4 + (c & 3);
+  const int offR = ((g >> 1) * 64 + 32 * (g & 1) + c) * 4;
+
+  f32x4 gW1[4][4], gW2[4], gW0[MT0][4];
+  f32x4 zero4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    gW2[m] = zero4;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) gW1[m][n] = zero4;
+#pragma unroll
+    for (int m0 = 0; m0 < MT0; ++m0) gW0[m0][m] = zero4;
+  }
+  float pb1[4] = {0.f, 0.f, 0.f, 0.f}, pG = 0.f;
+
+  const int64_t ntiles = (a.n + 15) / 16, last = a.n - 1;
+  const int64_t stride = (int64_t)gridDim.x * VJP16_WAVES;
+  // Tile inputs, loaded one tile ahead (software pipeline at two waves per SIMD): the
+  // head-gradient operands and h2 of tile t+1 are issued once tile t's chain has consumed
+  // half of ga2_R (its registers are free), h1 and x once the chain is done.  The loads
+  // keep raw values; the row / column masks are applied when the tile uses them (a mask
+  // at load time would wait for the load there).  Every load is unconditional (clamped
+  // addresses) and masked by opaque 0 / 1 factors: a select on a loaded value lets hipcc
+  // sink the load into a branch and drain every outstanding load at the join.
+  float gq[2], GB[4], xA[MT0][4];
+  int32_t et[4];
+  f32x4 h2R[4], h2T[4], h1T[4];
+  // G[row0 + c][4 ks + g] (operand of both gh2 products), G[row0 + 4 g + r][c] (B operand of
+  // gW2, bias / logstd sums), h2 in R and T layouts
+  auto load_g_h2 = [&](int64_t t) {
+    const float* ct = a.cache + (t >> 1) * CACHE_TILE_FLOATS + 16 * (int)(t & 1) * 4;
+    const int64_t row0 = t * 16;
+    {
+      const int64_t rr = row0 + c;
+      const float* gr = a.ghead + (rr < last ? rr : last) * gh;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int o = 4 * ks + g;
+        gq[ks] = gr[o < gh ? o : gh - 1];
+      }
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const float4 v = ld4(ct + (2 + (nt >> 1)) * 1024 + 512 * (nt & 1) + offR);
+      h2R[nt] = f32x4{v.x, v.y, v.z, v.w};
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h2T[nt][r] = ct[(2 + (nt >> 1)) * 1024 + 512 * (nt & 1) + 4 * r + offT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t rr = row0 + 4 * g + r;
+      GB[r] = a.ghead[(rr < last ? rr : last) * gh + (c < gh ? c : gh - 1)];
+    }
+  };
+  auto mask_g = [&](int64_t t) {
+    const int64_t row0 = t * 16;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) gq[ks] *= opaque((row0 + c < a.n && 4 * ks + g < A && ks < KS2) ? 1.f : 0.f);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) GB[r] *= opaque((row0 + 4 * g + r < a.n && c < gh) ? 1.f : 0.f);
+  };
+  // h1 in T layout, x[row0 + 4 g + r][16 m0 + c] (A operand of gW0; rows past n: any
+  // finite value, their ga1 is 0)
+  auto load_h1_x = [&](int64_t t) {
+    const float* ct = a.cache + (t >> 1) * CACHE_TILE_FLOATS + 16 * (int)(t & 1) * 4;
+    const int64_t row0 = t * 16;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h1T[nt][r] = ct[(nt >> 1) * 1024 + 512 * (nt & 1) + 4 * r + offT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t rr = row0 + 4 * g + r, rc = rr < last ? rr : last;
+#pragma unroll
+      for (int m0 = 0; m0 < MT0; ++m0) {
+        const int col = 16 * m0 + c;
+        xA[m0][r] = a.x[rc * a.n_obs + (col < a.n_obs ? col : a.n_obs - 1)];
+      }
+      if constexpr (EPT) et[r] = a.ept[rc];
+    }
+  };
+  // column O reads 1 (a ones column: gW0's row O is the bias gradient sum_rows ga1); the
+  // VF time feature t / timestep_limit at column n_obs as XGlobal computes it
+  auto mask_x = [&]() {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int m0 = 0; m0 < MT0; ++m0) {
+        const int col = 16 * m0 + c;
+        float xv = xA[m0][r] * opaque(col < a.n_obs ? 1.f : 0.f) + (col == d.O ? 1.f : 0.f);
+        if constexpr (EPT) xv += (float)((double)et[r] / a.ts_limit) * opaque(col == a.n_obs ? 1.f : 0.f);
+        xA[m0][r] = xv;
+      }
+  };
+  int64_t t = (int64_t)blockIdx.x * VJP16_WAVES + wave;
+  if (t < ntiles) {
+    load_g_h2(t);
+    load_h1_x(t);
+  }
+  for (; t < ntiles; t += stride) {
+    // the next tile of this wave (the last one re-reads its own tile: loads only)
+    const int64_t tn = t + stride < ntiles ? t + stride : t;
+    mask_g(t);
+    // ---- gh2 in both layouts (K = head outputs), then ga2 = gh2 (1 - h2^2)
+    f32x4 ga2R[4], ga2T[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const float w = w2frag(nt, 0);
+      ga2R[nt] = MFMA16(w, gq[0], zero4);
+      ga2T[nt] = MFMA16(gq[0], w, zero4);
+    }
+    if (KS2 > 1) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const float w = w2frag(nt, 1);
+        ga2R[nt] = MFMA16(w, gq[1], ga2R[nt]);
+        ga2T[nt] = MFMA16(gq[1], w, ga2T[nt]);
+      }
+    }
+    // gW2 += h2_T^T G  (k-step r: rows 4 g + r)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) gW2[nt] = MFMA16(h2T[nt][r], GB[r], gW2[nt]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pG += GB[r];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ga2R[nt][r] *= dtanh(h2R[nt][r]);
+        ga2T[nt][r] *= dtanh(h2T[nt][r]);
+      }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) pb1[nt] += (ga2T[nt][0] + ga2T[nt][1]) + (ga2T[nt][2] + ga2T[nt][3]);
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- gh1_T = ga2_R . W1^T (K = units, k-step (mt, r)) interleaved with
+    //      gW1 += h1_T^T ga2_T (K = rows): independent chains, one MFMA stream
+    f32x4 g1T[4] = {zero4, zero4, zero4, zero4};
+    // 16 steps (mt, nt), each W1 fragment read from LDS one step ahead of its MFMAs
+    float4 wf = w1frag(0, 0);
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int mt = st >> 2, nt = st & 3;
+      const float4 wn = st + 1 < 16 ? w1frag((st + 1) & 3, (st + 1) >> 2) : wf;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        g1T[nt] = MFMA16(ga2R[mt][r], f4get(wf, r), g1T[nt]);
+        gW1[mt][nt] = MFMA16(h1T[mt][r], ga2T[nt][r], gW1[mt][nt]);
+      }
+      wf = wn;
+      __builtin_amdgcn_sched_barrier(0);
+      // the next tile's G / h2 loads, once ga2_R of mt 0 and 1 is consumed (its registers
+      // are free), under the rest of the chain
+      if (st == 7) {
+        load_g_h2(tn);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // ---- ga1 = gh1 (1 - h1^2) in T;  gW0 += x^T ga1
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g1T[nt][r] *= dtanh(h1T[nt][r]);
+    mask_x();
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int m0 = 0; m0 < MT0; ++m0)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) gW0[m0][nt] = MFMA16(xA[m0][r], g1T[nt][r], gW0[m0][nt]);
+    __builtin_amdgcn_sched_barrier(0);
+    load_h1_x(tn);  // under the next tile's first phase
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  // ---- bias / logstd partials: sum over the four lane groups (rows)
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    pb1[nt] += __shfl_xor(pb1[nt], 16);
+    pb1[nt] += __shfl_xor(pb1[nt], 32);
+  }
+  pG += __shfl_xor(pG, 16);
+  pG += __shfl_xor(pG, 32);
+
+  // ---- waves w and w + 4 of the block add their partials (LDS), waves 0..3 store one
+  // slab row each: the slab keeps mrl_slab_rows = 4 per block
+  constexpr int NREG = VJP16_NREG(MT0);
+  __syncthreads();  // every wave is done with the W1 fragments
+  float* pair = lds + (wave & 3) * NREG * 64;
+  auto xfer = [&](float v, int k) {
+    if (wave >= 4) pair[k * 64 + lane] = v;
+  };
+  {
+    int k = 0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xfer(gW1[m][n][r], k++);
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xfer(gW2[n][r], k++);
+#pragma unroll
+    for (int m0 = 0; m0 < MT0; ++m0)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xfer(gW0[m0][n][r], k++);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) xfer(pb1[n], k++);
+    xfer(pG, k++);
+  }
+  __syncthreads();
+  if (wave >= 4) return;
+  auto pl = [&](int k) { return pair[k * 64 + lane]; };
+  {
+    int k = 0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gW1[m][n][r] += pl(k++);
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gW2[n][r] += pl(k++);
+#pragma unroll
+    for (int m0 = 0; m0 < MT0; ++m0)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gW0[m0][n][r] += pl(k++);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) pb1[n] += pl(k++);
+    pG += pl(k++);
+  }
+  float* out = a.slab + ((int64_t)blockIdx.x * 4 + wave) * d.P;
+  // gW1 [in][out]: in = 16 mt + 4 g + r, out = 16 nt + c
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[d.tW1 + (16 * m + 4 * g + r) * HID + 16 * n + c] = gW1[m][n][r];
+  // gW2 [u][o]: u = 16 nt + 4 g + r, o = c
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (c < A) out[d.tW2 + (16 * n + 4 * g + r) * A + c] = gW2[n][r];
+  // gW0 [i][u]: i = 16 m0 + 4 g + r, u = 16 nt + c; row O (the ones column) is b0's
+#pragma unroll
+  for (int m0 = 0; m0 < MT0; ++m0)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * m0 + 4 * g + r;
+        if (i < d.O) out[d.tW0 + i * HID + 16 * n + c] = gW0[m0][n][r];
+        else if (i == d.O) out[d.tb0 + 16 * n + c] = gW0[m0][n][r];
+      }
+  if (g == 0) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) out[d.tb1 + 16 * n + c] = pb1[n];
+    if (c < A) out[d.tb2 + c] = pG;
+    else if (c < gh) out[d.tls + (c - A)] = pG;
   }
 }
 
@@ -920,6 +1264,25 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
     else if (!wide) hipLaunchKernelGGL((mlp_vjp_kernel<C, false, 0>), grid, blk, shm, s, a, image, skip);   \
     else hipLaunchKernelGGL((mlp_vjp_kernel<C, true, 0>), grid, blk, shm, s, a, image, skip);               \
   } while (0)
+  static const bool use16 = []() {  // MRL_VJP16=0 in the environment: the 32-row kernel (A/B probes)
+    const char* e = getenv("MRL_VJP16");
+    return e ? atoi(e) != 0 : MRL_VJP16 != 0;
+  }();
+  // the 16-row kernel takes the bias gradient b0 through a ones column of gW0's padding
+  if (use16 && act_cache != nullptr && a.d.O % 16 != 0) {
+    // the transpose-free 16-row kernel (8 waves per block, same slab rows per block)
+    const size_t shm16 = std::max<size_t>(2 * 32 * 64, 4 * 64 * (size_t)VJP16_NREG(wide ? 2 : 1)) * 4;
+    const dim3 blk16(64 * VJP16_WAVES);
+    const bool ept = ep_t != nullptr;
+    if (wide) {
+      if (ept) hipLaunchKernelGGL((mlp_vjp16_kernel<true, true>), grid, blk16, shm16, s, a, image, skip);
+      else hipLaunchKernelGGL((mlp_vjp16_kernel<true, false>), grid, blk16, shm16, s, a, image, skip);
+    } else {
+      if (ept) hipLaunchKernelGGL((mlp_vjp16_kernel<false, true>), grid, blk16, shm16, s, a, image, skip);
+      else hipLaunchKernelGGL((mlp_vjp16_kernel<false, false>), grid, blk16, shm16, s, a, image, skip);
+    }
+    return hip_check(hipGetLastError(), "mrl_mlp_vjp");
+  }
   if (act_cache != nullptr) MRL_VJP_LAUNCH(true);
   else MRL_VJP_LAUNCH(false);
 #undef MRL_VJP_LAUNCH

@@ -139,8 +139,11 @@ def test_value_forward_and_loss_grad_with_time_feature(nin, cus):
 
 @pytest.mark.parametrize("head,nin,nout", [("gauss", 11, 3), ("softmax", 4, 2)])
 def test_activation_cache_is_bitwise_transparent(head, nin, nout):
-    """SURRGRAD stores h1/h2; the FVP and VJP that follow read them instead of
-    recomputing the forward -- results must equal the uncached kernels bit for bit."""
+    """SURRGRAD stores h1/h2; the FVP rows pass that follows reads them instead of
+    recomputing the forward -- its head rows must equal the uncached kernel's bit for bit.
+    The cached VJP is the transpose-free 16-row kernel (mlp_vjp16_kernel): the same sums
+    in another row order, so its gradients agree with the uncached 32-row kernel to fp32
+    rounding and both with the float64 oracle."""
     from modular_rl_amd import _lib
     N = 3000
     spec, th, ob, act, adv, oldprob = _setup(head, nin, nout, N, seed=9)
@@ -167,7 +170,43 @@ def test_activation_cache_is_bitwise_transparent(head, nin, nout):
         outs.append((g.cpu(), gh.cpu(), fv.cpu()))
         if use_cache:
             assert net._cache_key is not None
-    for u, c in zip(*outs):
-        assert torch.equal(u, c)
+    (g_u, gh_u, fv_u), (g_c, gh_c, fv_c) = outs
+    assert torch.equal(gh_u, gh_c)
+    assert _rel(g_c.numpy(), g_u.numpy()) < 1e-5
+    assert _rel(fv_c.numpy(), fv_u.numpy()) < 1e-5
     want = T.fisher_vector_product(spec, th, v.astype(np.float64), ob)
-    assert _rel(outs[1][2].numpy(), want) < 1e-4
+    for fv in (fv_u, fv_c):
+        assert _rel(fv.numpy(), want) < 1e-4
+    gw = T.policy_gradient(spec, th, ob, act, adv, oldprob)
+    for g in (g_u, g_c):
+        assert _rel(g.numpy(), gw) < 1e-4
+
+
+@pytest.mark.parametrize("head,nin,nout", CASES)
+@pytest.mark.parametrize("N", [1, 17, 3001])
+def test_cached_fisher_product_and_gradient(head, nin, nout, N):
+    """The cached VJP (16-row transpose-free kernel) after a recording SURRGRAD pass:
+    policy gradient and Fisher product vs the float64 oracle on ragged row counts
+    (partial 16- and 32-row tiles), wide inputs (nin 17: two gW0 tiles) and heads of
+    more than four outputs (two head k-steps)."""
+    from modular_rl_amd import _lib
+    spec, th, ob, act, adv, oldprob = _setup(head, nin, nout, N, seed=11)
+    v = np.random.default_rng(4).standard_normal(spec.P).astype(np.float32)
+    net = _net(head, nin, nout)
+    net.set_flat(th)
+    x, vt = _dev(ob), _dev(v)
+    a = _dev(act, torch.int32 if head == "softmax" else torch.float32)
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    ghead = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(adv), oldprob=_dev(oldprob),
+             ghead=ghead, partial=partial)
+    assert net._cache_key is not None
+    g = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(x, N, ghead, g)
+    assert _rel(g.cpu().numpy(), T.policy_gradient(spec, th, ob, act, adv, oldprob)) < 1e-4
+    imgt = torch.zeros_like(net.image)
+    net.pack(theta=vt, image=imgt, fwd_only=True)
+    net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=ghead, tangent=vt, image_t=imgt)
+    fv = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(x, N, ghead, fv)
+    assert _rel(fv.cpu().numpy(), T.fisher_vector_product(spec, th, v.astype(np.float64), ob)) < 1e-4
