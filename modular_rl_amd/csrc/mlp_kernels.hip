@@ -635,8 +635,14 @@ __device__ inline float opaque(float m) {
   asm volatile("" : "+v"(m));
   return m;
 }
-// accumulator registers a wave hands to its partner: gW1 64, gW2 16, gW0 16 MT0, b1 4, b2 1
-#define VJP16_NREG(MT0) (64 + 16 + 16 * (MT0) + 4 + 1)
+// 16 B per lane global -> LDS (global_load_lds_dwordx4): lane L's bytes land at l + 16 L
+// (l wave-uniform); no VGPR destination
+__device__ inline void glds16(const float* g, float* l) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+constexpr int VJP16_W_FLOATS = 2 * 32 * 64 + 2 * 4 * 64;  // BA1 + BA2 of the image
+constexpr int VJP16_H1_FLOATS = 16 * 64;                  // h1 of one 16-row tile
 // cache offset (floats) of element (32-row tile's row j, unit w of 32-unit slot `slot`)
 __device__ inline int cache_off(int slot, int j, int w) {
   return ((slot * 4 + (w >> 3)) * 64 + 32 * ((w >> 2) & 1) + j) * 4 + (w & 3);
@@ -646,11 +652,14 @@ template <bool WIDE, bool EPT>
 __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs a, const float* __restrict__ img,
                                                                      const int32_t* __restrict__ skip) {
   constexpr int MT0 = WIDE ? 2 : 1;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+  // two LDS objects: the LDS-DMA target (h1 staging) apart from the weight fragments, so
+  // the compiler's wait for an LDS-DMA in flight is not put in front of fragment reads
+  __shared__ __attribute__((aligned(16))) float lds[VJP16_W_FLOATS];
+  __shared__ __attribute__((aligned(16))) float sH[VJP16_WAVES * 2 * VJP16_H1_FLOATS];
   if (skip != nullptr && *skip != 0) return;
   const MlpDims& d = a.d;
   // BA1 (W1 fragments, 4096 floats) then BA2 (W2 fragments, 512): contiguous in the image
-  for (int i = threadIdx.x; i < (2 * 32 * 64 + 2 * 4 * 64) / 4; i += 64 * VJP16_WAVES)
+  for (int i = threadIdx.x; i < VJP16_W_FLOATS / 4; i += 64 * VJP16_WAVES)
     reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img + d.ba1)[i];
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform tile bases
@@ -693,8 +702,8 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
   // at load time would wait for the load there).  Every load is unconditional (clamped
   // addresses) and masked by opaque 0 / 1 factors: a select on a loaded value lets hipcc
   // sink the load into a branch and drain every outstanding load at the join.
-  float gq[2], GB[4], xA[MT0][4];
-  int32_t et[4];
+  float gq[2], GB[4], xA[MT0][4], xN[MT0][4];  // xN: the next tile's x, moved to xA after gW0
+  int32_t et[4], eN[4];
   f32x4 h2R[4], h2T[4], h1T[4];
   // G[row0 + c][4 ks + g] (operand of both gh2 products), G[row0 + 4 g + r][c] (B operand of
   // gW2, bias / logstd sums), h2 in R and T layouts
@@ -732,25 +741,54 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
 #pragma unroll
     for (int r = 0; r < 4; ++r) GB[r] *= opaque((row0 + 4 * g + r < a.n && c < gh) ? 1.f : 0.f);
   };
-  // h1 in T layout, x[row0 + 4 g + r][16 m0 + c] (A operand of gW0; rows past n: any
-  // finite value, their ga1 is 0)
-  auto load_h1_x = [&](int64_t t) {
-    const float* ct = a.cache + (t >> 1) * CACHE_TILE_FLOATS + 16 * (int)(t & 1) * 4;
+  // x[row0 + 4 g + r][16 m0 + c] (A operand of gW0; rows past n: any finite value, their
+  // ga1 is 0)
+  auto take_x = [&]() {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int m0 = 0; m0 < MT0; ++m0) xA[m0][r] = xN[m0][r];
+      if constexpr (EPT) et[r] = eN[r];
+    }
+  };
+  auto load_x = [&](int64_t t) {
     const int64_t row0 = t * 16;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) h1T[nt][r] = ct[(nt >> 1) * 1024 + 512 * (nt & 1) + 4 * r + offT];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int64_t rr = row0 + 4 * g + r, rc = rr < last ? rr : last;
 #pragma unroll
       for (int m0 = 0; m0 < MT0; ++m0) {
         const int col = 16 * m0 + c;
-        xA[m0][r] = a.x[rc * a.n_obs + (col < a.n_obs ? col : a.n_obs - 1)];
+        xN[m0][r] = a.x[rc * a.n_obs + (col < a.n_obs ? col : a.n_obs - 1)];
       }
-      if constexpr (EPT) et[r] = a.ept[rc];
+      if constexpr (EPT) eN[r] = a.ept[rc];
     }
+  };
+  // h1 of a tile staged in LDS by four LDS-DMA instructions (no registers while in
+  // flight).  The 16-B chunks (run = (slot * 4 + q) * 2 + h, row j) of the cache tile land
+  // at (run * 16 + jj) * 4 with the rows of each 4-row group rotated by k = 2 (q & 1) + h,
+  // jj = 4 (j >> 2) + ((j + k) & 3): the T reads below (lane (c, g): run of unit 16 p + c,
+  // row 4 g + r) then hit 64 distinct banks.  The rotation is applied on the source side
+  // (an LDS-DMA destination is lane-linear).
+  float* const h1s = sH + wave * 2 * VJP16_H1_FLOATS;
+  auto dma_h1 = [&](int64_t t, int b) {
+    const float* ct = a.cache + (t >> 1) * CACHE_TILE_FLOATS + 16 * (int)(t & 1) * 4;
+    const int jj = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int run = 4 * i + (lane >> 4), sq = run >> 1, hh = run & 1, k = 2 * (sq & 1) + hh;
+      const int j = 4 * (jj >> 2) + ((jj - k) & 3);
+      glds16(ct + (sq * 64 + 32 * hh + j) * 4, h1s + b * VJP16_H1_FLOATS + i * 256);
+    }
+  };
+  // lane parts of the T read offsets: run bits from c, rotated row 4 g + ((r + (c >> 2)) & 3)
+  int offH[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    offH[r] = ((c >> 3) * 2 + ((c >> 2) & 1)) * 64 + 16 * g + 4 * ((r + (c >> 2)) & 3) + (c & 3);
+  auto read_h1 = [&](int b, int nt) {
+    const float* p = h1s + b * VJP16_H1_FLOATS + (nt >> 1) * 512 + (nt & 1) * 256;
+    h1T[nt] = f32x4{p[offH[0]], p[offH[1]], p[offH[2]], p[offH[3]]};
   };
   // column O reads 1 (a ones column: gW0's row O is the bias gradient sum_rows ga1); the
   // VF time feature t / timestep_limit at column n_obs as XGlobal computes it
@@ -768,8 +806,11 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
   int64_t t = (int64_t)blockIdx.x * VJP16_WAVES + wave;
   if (t < ntiles) {
     load_g_h2(t);
-    load_h1_x(t);
+    load_x(t);
+    dma_h1(t, 0);
+    take_x();
   }
+  int buf = 0;
   for (; t < ntiles; t += stride) {
     // the next tile of this wave (the last one re-reads its own tile: loads only)
     const int64_t tn = t + stride < ntiles ? t + stride : t;
@@ -810,6 +851,11 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
     // ---- gh1_T = ga2_R . W1^T (K = units, k-step (mt, r)) interleaved with
     //      gW1 += h1_T^T ga2_T (K = rows): independent chains, one MFMA stream
     f32x4 g1T[4] = {zero4, zero4, zero4, zero4};
+    // this tile's h1 (its DMA was issued with the loads phase 1 waited for): all of it is
+    // read before the next tile's DMA is issued
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) read_h1(buf, nt);
     // 16 steps (mt, nt), each W1 fragment read from LDS one step ahead of its MFMAs
     float4 wf = w1frag(0, 0);
 #pragma unroll
@@ -827,6 +873,8 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
       // are free), under the rest of the chain
       if (st == 7) {
         load_g_h2(tn);
+        load_x(tn);
+        dma_h1(tn, buf ^ 1);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -842,9 +890,8 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
       for (int m0 = 0; m0 < MT0; ++m0)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) gW0[m0][nt] = MFMA16(xA[m0][r], g1T[nt][r], gW0[m0][nt]);
-    __builtin_amdgcn_sched_barrier(0);
-    load_h1_x(tn);  // under the next tile's first phase
-    __builtin_amdgcn_sched_barrier(0);
+    take_x();
+    buf ^= 1;
   }
 
   // ---- bias / logstd partials: sum over the four lane groups (rows)
@@ -856,22 +903,35 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
   pG += __shfl_xor(pG, 16);
   pG += __shfl_xor(pG, 32);
 
-  // ---- waves w and w + 4 of the block add their partials (LDS), waves 0..3 store one
-  // slab row each: the slab keeps mrl_slab_rows = 4 per block
-  constexpr int NREG = VJP16_NREG(MT0);
-  __syncthreads();  // every wave is done with the W1 fragments
-  float* pair = lds + (wave & 3) * NREG * 64;
-  auto xfer = [&](float v, int k) {
-    if (wave >= 4) pair[k * 64 + lane] = v;
-  };
-  {
-    int k = 0;
+  // ---- waves w and w + 4 of the block add their partials through sH (two rounds: gW1,
+  // then the rest), waves 0..3 store one slab row each: the slab keeps mrl_slab_rows = 4
+  // per block
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) h1 DMA has landed
+  __syncthreads();  // every wave is done with its h1 buffers
+  float* pair = sH + (wave & 3) * 64 * 64;
+  if (wave >= 4) {
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
       for (int n = 0; n < 4; ++n)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xfer(gW1[m][n][r], k++);
+        for (int r = 0; r < 4; ++r) pair[((m * 4 + n) * 4 + r) * 64 + lane] = gW1[m][n][r];
+  }
+  __syncthreads();
+  if (wave < 4) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gW1[m][n][r] += pair[((m * 4 + n) * 4 + r) * 64 + lane];
+  }
+  __syncthreads();
+  {
+    auto xfer = [&](float v, int k) {
+      if (wave >= 4) pair[k * 64 + lane] = v;
+    };
+    int k = 0;
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
@@ -888,15 +948,9 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
   }
   __syncthreads();
   if (wave >= 4) return;
-  auto pl = [&](int k) { return pair[k * 64 + lane]; };
   {
+    auto pl = [&](int k) { return pair[k * 64 + lane]; };
     int k = 0;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) gW1[m][n][r] += pl(k++);
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
@@ -1271,7 +1325,7 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
   // the 16-row kernel takes the bias gradient b0 through a ones column of gW0's padding
   if (use16 && act_cache != nullptr && a.d.O % 16 != 0) {
     // the transpose-free 16-row kernel (8 waves per block, same slab rows per block)
-    const size_t shm16 = std::max<size_t>(2 * 32 * 64, 4 * 64 * (size_t)VJP16_NREG(wide ? 2 : 1)) * 4;
+    const size_t shm16 = 0;  // static LDS: weight fragments + h1 staging (82 KB)
     const dim3 blk16(64 * VJP16_WAVES);
     const bool ept = ep_t != nullptr;
     if (wide) {
