@@ -69,17 +69,21 @@ def vjp_binary_entry(kern, policy_vjp_flop, vf_vjp_flop, rows, iters):
                        for r, (c, m, t) in parts.items()})
 
 
+VJP_BINARY = {"fp32": "mlp_vjp16_kernel", "bf16": "mlp_vjp_bf16_kernel"}  # the cached VJP per dtype
+
+
 def dominant_kernel(kinfo):
     """The kernel binary with the largest device time per iteration (fvp_vjp is one
-    role of mlp_vjp_kernel when that entry exists)."""
-    cands = [k for k in kinfo if not (k == "fvp_vjp" and "mlp_vjp_kernel" in kinfo)]
+    role of the VJP binary when that entry exists)."""
+    vjp = [k for k in kinfo if k in VJP_BINARY.values()]
+    cands = [k for k in kinfo if not (k == "fvp_vjp" and vjp)]
     return max(cands, key=lambda k: kinfo[k]["total_ms"])
 
 
 DYNAMICS = {"Hopper-v2": "hopper.xml articulated-body dynamics", "Humanoid-v2": "humanoid.xml articulated-body dynamics",
             "CartPole-v0": "gym equations"}
 GAE_BYTES_PER_ROW = 17  # read r 4 + v 4 + flags 1, write adv 4 + ret 4
-PMC_FILE = "pmc_r02.json"
+PMC_FILE = "pmc_r03.json"
 ROLLOUT_ISSUE_FILE = "rollout_issue_r03.json"  # tools/rollout_issue.py: SQ issue cycles per rollout step
 CLOCK_GHZ = 2.4  # MI355X max shader clock (MI355X_MICROARCH.md)
 
@@ -320,14 +324,14 @@ def main():
                 kinfo[name]["bytes_per_row"] = row_b
                 kinfo[name]["hbm_gbs_alg"] = row_b * n_local / (mean_ms * 1e-3) / 1e9
     if not net.layered:
-        # the same kernel binary (mlp_vjp_kernel) also serves the policy gradient and every
+        # the same kernel binary (the cached VJP) also serves the policy gradient and every
         # VF L-BFGS evaluation (the VF fit's launches run beside the next rollout on the
         # fit's CU set): rocprofv3 sums them into one entry, so the dominance test does too
         vf_net = agent.baseline.net
         vjp = vjp_binary_entry(kern, fpr["fvp_vjp"], None if vf_net.layered else flops_per_row(vf_net)["fvp_vjp"],
                                n_local, K)
         if vjp is not None:
-            kinfo["mlp_vjp_kernel"] = vjp
+            kinfo[VJP_BINARY[args.dtype]] = vjp
     if "rollout_steps" in kern:
         # one timed region per iteration around the rollout's launches (the persistent
         # kernel over the T steps, in a graph on the rollout stream): region / T per step
@@ -340,7 +344,8 @@ def main():
         if pmc.get(name, {}).get("hbm_bytes_per_launch"):
             ki["hbm_gbs_pmc"] = pmc[name]["hbm_bytes_per_launch"] / (ki["mean_ms"] * 1e-3) / 1e9
     dom = dominant_kernel(kinfo)
-    traffic = pmc.get("fvp_vjp" if dom == "mlp_vjp_kernel" else dom, {}).get("hbm_bytes_per_launch")
+    is_vjp = dom in VJP_BINARY.values()
+    traffic = pmc.get("fvp_vjp" if is_vjp else dom, {}).get("hbm_bytes_per_launch")
     roofline = {"bound": "mfma", "achieved": round(kinfo[dom]["tflops"], 3), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(kinfo[dom]["tflops"] / peak, 4), "traffic": traffic,
                 "traffic_source": f"profiles/{PMC_FILE} (PMC FETCH_SIZE x2 + WRITE_SIZE, separate passes; "
@@ -349,7 +354,7 @@ def main():
                 "rows_per_launch": kinfo[dom]["rows_per_launch"],
                 "mean_launch_ms": round(kinfo[dom]["mean_ms"], 5), "launches_timed": kinfo[dom]["launches"],
                 "ms_per_iter": round(kinfo[dom]["total_ms"] / K, 3)}
-    if dom == "mlp_vjp_kernel":
+    if is_vjp:
         roofline["roles"] = kinfo[dom]["roles"]
         roofline["note"] = ("all launches of the VJP kernel binary (Fisher products, policy gradient, VF fit "
                             "evaluations); achieved = their algorithmic FLOP / their summed HIP-event durations; "

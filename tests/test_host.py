@@ -105,9 +105,9 @@ def test_bench_roofline_kernel_is_chosen_per_binary():
     assert e["roles"]["vf_vjp"] == {"launches": 6, "mean_ms": 1.5, "ms_per_iter": 4.5}
     assert bench.vjp_binary_entry({"pg_vjp": (2, 1.0, 2.0)}, 100.0, 80.0, rows, K) is None
     assert bench.vjp_binary_entry(kern, 100.0, None, rows, K)["launches"] == 22  # layered VF: not this binary
-    kinfo = {"fvp_vjp": {"total_ms": 20.0}, "mlp_vjp_kernel": {"total_ms": 31.0}, "rollout_step": {"total_ms": 27.0},
+    kinfo = {"fvp_vjp": {"total_ms": 20.0}, "mlp_vjp16_kernel": {"total_ms": 31.0}, "rollout_step": {"total_ms": 27.0},
              "fvp_jvp_rows": {"total_ms": 15.0}}
-    assert bench.dominant_kernel(kinfo) == "mlp_vjp_kernel"
+    assert bench.dominant_kernel(kinfo) == "mlp_vjp16_kernel"
     kinfo["rollout_step"]["total_ms"] = 40.0
     assert bench.dominant_kernel(kinfo) == "rollout_step"
     # without the binary entry (layered nets) the Fisher-product role competes itself

@@ -15,7 +15,8 @@ import os
 # role -> kernel-name substring (first match wins, most specific first)
 ROLES = [
     ("fvp_jvp_rows", "mlp_rows_kernel<100"),
-    ("fvp_vjp", "mlp_vjp_kernel<true"),
+    ("fvp_vjp", "mlp_vjp16_kernel<false, false"),  # the cached VJP (16-row kernel)
+    ("fvp_vjp_r02", "mlp_vjp_kernel<true"),          # its round-2 32-row predecessor
     ("fvp_jvp_rows_bf16", "mlp_rows_bf16_kernel<100"),
     ("fvp_vjp_bf16", "mlp_vjp_bf16_kernel<true"),
     ("vjp_uncached", "mlp_vjp_kernel<false"),
