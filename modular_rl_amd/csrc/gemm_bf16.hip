@@ -354,6 +354,244 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_stream_kernel(GemmB16Args g,
   }
 }
 
+// ------------------------------------------------------------------ 256 x 256 NN GEMM
+// The tall layered-path products (M ~ 1 M rows, K <= 512, N = 512) are bound by how many
+// operand bytes reach the CU per MFMA: a 128 x 128 tile needs 2 B x 2048 MACs x (1/128 +
+// 1/128) = 64 B per CU cycle from L2 at full MFMA rate, a 256 x 256 tile 32 B (L2 serves
+// about 30: MI355X_MICROARCH.md, indexed rows).  So: 256 x 256 tiles, 8 waves (2 per SIMD,
+// 64 x 128 each, 128 accumulator registers), K staged 32 at a time by LDS-DMA
+// (global_load_lds_dwordx4: no staging registers, no ds_write pass) into four 32 KB
+// stages, three in flight ahead of the one being read (an L2 / HBM fetch outlasts one
+// stage's MFMAs): a counted vmcnt and a raw barrier per stage (a __syncthreads would
+// wait for every DMA in flight), the four stages separate LDS objects so the compiler's
+// wait for an LDS-DMA in flight is not put in front of another stage's fragment reads.
+// Rows of a stage image are 64 B (32 k of one row of A or Bt); the 16-B chunk c of row r
+// sits at position c ^ ((r >> 2) & 3) -- applied on the DMA source side, the destination
+// being lane-linear -- so a 16-lane ds_read_b128 group (rows r..r+15, one chunk) covers
+// the 64 banks once.  Chunks past K read a zero block.  Persistent blocks walk the tiles
+// as one stream of stages (the next tile's first stages load under this tile's last
+// stages and epilogue); the ntn column tiles of a row block run on blocks of one XCD at
+// the same time (A from HBM once, from that XCD's L2 for the others).  Same operands and
+// the same per-output k order as gemm_bf16_kernel (k-steps of 16 in order, A.Bt before
+// A2.Bt2): bit-identical results.
+__device__ const uint32_t kZero16[4] = {0u, 0u, 0u, 0u};
+constexpr int BBM = 256, BBN = 256, BBK = 32;
+constexpr int BSTAGE = (BBM + BBN) * BBK;  // bf16 per stage: A rows, then Bt rows (16 K each)
+
+struct BigPlan {
+  int64_t ntm;  // row tiles
+  int ntn;      // column tiles
+  int per_xcd;  // blocks per XCD
+};
+
+__device__ inline void glds16b(const void* g, bfr_t* l) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+template <bool DUAL, bool OUTBF>
+__global__ __launch_bounds__(512, 2) void gemm_bf16_big_kernel(GemmB16Args g, BigPlan pl) {
+  __shared__ __attribute__((aligned(16))) bfr_t sb0[BSTAGE];
+  __shared__ __attribute__((aligned(16))) bfr_t sb1[BSTAGE];
+  __shared__ __attribute__((aligned(16))) bfr_t sb2[BSTAGE];
+  __shared__ __attribute__((aligned(16))) bfr_t sb3[BSTAGE];
+  if (g.skip != nullptr && *g.skip != 0) return;
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;  // 4 x 2 waves of 64 rows x 128 columns
+  const int xcd = blockIdx.x % 8, y = blockIdx.x / 8;
+  if (y >= pl.per_xcd) return;
+  const int tn = y % pl.ntn, lr = y / pl.ntn, rows_per_round = pl.per_xcd / pl.ntn;
+  const int64_t tstride = 8 * (int64_t)rows_per_round;
+  const int64_t ntk = (g.K + BBK - 1) / BBK, nst = (DUAL ? 2 : 1) * ntk;
+  // DMA of stage s of row tile tm into `dst`: waves 0..3 fetch A rows 64 w .. + 63, waves
+  // 4..7 Bt rows 64 (w - 4) .. + 63; instruction i covers 16 rows (lane: row L >> 2,
+  // position L & 3, i.e. chunk (L & 3) ^ ((row >> 2) & 3) = (L & 3) ^ (L >> 4))
+  const bool isA = wave < 4;
+  const int lrow = 64 * (wave & 3) + (lane >> 2);
+  const int coff = 8 * ((lane & 3) ^ (lane >> 4));
+  auto issue = [&](bfr_t* dst, int64_t tm, int64_t s) {
+    const bool second = DUAL && s >= ntk;
+    const int64_t k0 = (second ? s - ntk : s) * BBK;
+    const bfr_t* base = isA ? (second ? g.A2 : g.A) : (second ? g.Bt2 : g.Bt);
+    const int64_t ld = isA ? g.lda : g.ldb, lim = isA ? g.M : g.N;
+    const int64_t r0 = isA ? tm * BBM : (int64_t)tn * BBN;
+    bfr_t* d0 = dst + (isA ? 0 : BBM * BBK) + 64 * (wave & 3) * BBK;
+    if (r0 + BBM <= lim && k0 + BBK <= g.K) {
+      // interior: a wave-uniform base per instruction and a 32-bit lane offset
+      const bfr_t* tb = base + (r0 + 64 * (wave & 3)) * ld + k0;
+      const uint32_t lo = (uint32_t)((lane >> 2) * ld + coff);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) glds16b(tb + 16 * i * ld + lo, d0 + 16 * i * BBK);
+    } else {
+      // a tile crossing M / N (rows clamped: their outputs are not stored) or the K tail
+      // (chunks past K read the zero block)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t k = k0 + coff;
+        int64_t row = r0 + lrow + 16 * i;
+        row = row < lim ? row : lim - 1;
+        const void* src = k < g.K ? (const void*)(base + row * ld + k) : (const void*)kZero16;
+        glds16b(src, d0 + 16 * i * BBK);
+      }
+    }
+  };
+  // the stage stream: (row tile itm, stage is) is the next stage to load
+  int64_t itm = (int64_t)xcd * rows_per_round + lr, is = 0;
+  int issued = 0, consumed = 0;
+  auto issue_next = [&](bfr_t* dst) {
+    if (itm < pl.ntm) {
+      issue(dst, itm, is);
+      ++issued;
+      if (++is == nst) {
+        is = 0;
+        itm += tstride;
+      }
+    }
+  };
+  f32x16 acc[2][4];
+  // fragments of one 16-deep k-step: A rows of the wave's two 32-row tiles, Bt rows of its
+  // four 32-column tiles (chunk 2 ks + h of each row)
+  struct Frag {
+    bf16x8 a[2], b[4];
+  };
+  auto read = [&](const bfr_t* cur, int ks, Frag& f) {
+    const bfr_t* As = cur;
+    const bfr_t* Bs = cur + BBM * BBK;
+    const int c = 2 * ks + h;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int r = 64 * wm + 32 * mi + j;
+      f.a[mi] = *reinterpret_cast<const bf16x8*>(As + r * BBK + 8 * (c ^ ((r >> 2) & 3)));
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int r = 128 * wn + 32 * ni + j;
+      f.b[ni] = *reinterpret_cast<const bf16x8*>(Bs + r * BBK + 8 * (c ^ ((r >> 2) & 3)));
+    }
+  };
+  auto mfma = [&](const Frag& f) {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = MFMA32B(f.b[ni], f.a[mi], acc[mi][ni]);  // C^T tiles
+  };
+  // One stage (two k-steps).  Its first k-step's fragments are already in f0 (read under
+  // the previous stage); the barrier here certifies the NEXT stage's DMA has landed for
+  // every wave (at most the stage after it still in flight) and that every wave is done
+  // with the stage loaded next; then that DMA goes out, and the fragment reads of the
+  // second k-step and of the next stage's first k-step run under the MFMAs.
+  Frag f0, f1;
+  auto stage = [&](const bfr_t* cur, const bfr_t* next, bfr_t* load) {
+    const int later = issued - consumed - 2;  // stages issued after the next one
+    if (later >= 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_next(load);
+    read(cur, 1, f1);
+    mfma(f0);
+    if (issued - consumed >= 2) read(next, 0, f0);  // the next stage exists
+    mfma(f1);
+    ++consumed;
+  };
+  // 16-B vector epilogue (ldc, ldh multiples of 8)
+  const bool vec = (g.ldc & 7) == 0 && (g.epi != MRL_GEMM_DTANH || (g.ldh & 7) == 0);
+  issue_next(sb0);
+  issue_next(sb1);
+  issue_next(sb2);
+  if (issued > 0) {  // the first stage's first k-step (once per block: wait for all three)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    read(sb0, 0, f0);
+  }
+  for (int64_t tm = (int64_t)xcd * rows_per_round + lr; tm < pl.ntm; tm += tstride) {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = zero16();
+    for (int64_t s = 0; s < nst; s += 4) {  // nst % 4 == 0 (host check): stage s in sb0
+      stage(sb0, sb1, sb3);
+      stage(sb1, sb2, sb0);
+      stage(sb2, sb3, sb1);
+      stage(sb3, sb0, sb2);
+    }
+    // epilogue: lane (j, h) holds row j of each 32 x 32 C tile at columns cperm(r, h) --
+    // four runs of 4 consecutive columns, 8q + 4h.  One v_permlane32_swap per register
+    // pair (runs q = 2p and 2p + 1) leaves lane (j, h) with the 8 consecutive columns
+    // 16p + 8h .. + 7: half the store instructions, 16-B bf16 stores (the epilogue is
+    // store-issue-bound: 8-B stores ran 1.1-1.2 x slower).  The next tile's first stages
+    // are already in flight.
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int64_t row = tm * BBM + 64 * wm + 32 * mi + j;
+        const int64_t cbase = (int64_t)tn * BBN + 128 * wn + 32 * ni;
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[mi][ni][8 * pp + e]),
+                                                             __float_as_uint(acc[mi][ni][8 * pp + 4 + e]), false, false);
+            v[e] = __uint_as_float(sw[0]);
+            v[4 + e] = __uint_as_float(sw[1]);
+          }
+          if (row >= g.M) continue;
+          const int64_t c0 = cbase + 16 * pp + 8 * h;
+          if (vec && c0 + 8 <= g.N) {
+            if (g.bias != nullptr) {
+              const float4 b0 = *reinterpret_cast<const float4*>(g.bias + c0);
+              const float4 b1 = *reinterpret_cast<const float4*>(g.bias + c0 + 4);
+              v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+              v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+            }
+            if (g.epi == MRL_GEMM_TANH) {
+#pragma unroll
+              for (int e = 0; e < 8; e += 2) {
+                const f32x2 t = tanh_fast2(f32x2{v[e], v[e + 1]});
+                v[e] = t.x;
+                v[e + 1] = t.y;
+              }
+            } else if (g.epi == MRL_GEMM_DTANH) {
+              const uint4 hb = *reinterpret_cast<const uint4*>(g.H + row * g.ldh + c0);
+              const uint32_t hw[4] = {hb.x, hb.y, hb.z, hb.w};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                v[2 * e] *= dtanh(__uint_as_float(hw[e] << 16));
+                v[2 * e + 1] *= dtanh(__uint_as_float(hw[e] & 0xffff0000u));
+              }
+            }
+            if (OUTBF) {
+              uint4 o;
+              o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+              o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+              o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+              o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+              *reinterpret_cast<uint4*>(reinterpret_cast<bfr_t*>(g.C) + row * g.ldc + c0) = o;
+            } else {
+              float* cp = reinterpret_cast<float*>(g.C) + row * g.ldc + c0;
+              *reinterpret_cast<float4*>(cp) = make_float4(v[0], v[1], v[2], v[3]);
+              *reinterpret_cast<float4*>(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            }
+            continue;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int64_t col = c0 + e;
+            if (col >= g.N) continue;
+            float xv = v[e] + (g.bias != nullptr ? g.bias[col] : 0.f);
+            if (g.epi == MRL_GEMM_TANH) xv = tanh_fast(xv);
+            else if (g.epi == MRL_GEMM_DTANH) xv *= dtanh(bf2f(g.H[row * g.ldh + col]));
+            if (OUTBF) reinterpret_cast<bfr_t*>(g.C)[row * g.ldc + col] = f2bf(xv);
+            else reinterpret_cast<float*>(g.C)[row * g.ldc + col] = xv;
+          }
+        }
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the block
+}
+
 // ------------------------------------------------------------------ TN (weight grads)
 // K step: 32 rows; LDS images [32 rows][BM or BN columns], pitch 160 bf16 (320 B): a
 // 32-lane half's transposed read (rows q = 0..3, 8 B at columns 16G + 4p) covers all
@@ -512,6 +750,33 @@ using namespace mrl;
 #ifndef MRL_GEMM_STREAM_MIN_M  // rows from which the streaming kernel takes the NN GEMM (0: never)
 #define MRL_GEMM_STREAM_MIN_M 32768
 #endif
+#ifndef MRL_GEMM_BIG_MIN_M  // rows from which the 256 x 256 LDS-DMA kernel takes the NN GEMM (0: never)
+#define MRL_GEMM_BIG_MIN_M 65536
+#endif
+// The 256 x 256 kernel for a tall NN product (a multiple of four 32-deep K stages, N >= 128,
+// one 512-thread block per CU): launched here and true, or false.
+static bool big_gemm_launch(const GemmB16Args& g, bool outbf, bool dual, hipStream_t s) {
+  const char* e = getenv("MRL_GEMM_BIG_MIN_M");
+  const int64_t min_m = e ? atoll(e) : MRL_GEMM_BIG_MIN_M;
+  const int64_t ntk = (g.K + BBK - 1) / BBK, nst = (dual ? 2 : 1) * ntk;
+  if (min_m <= 0 || g.M < min_m || g.N < 128 || nst % 4 != 0) return false;
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return false;
+  if (ncu < 8 || ncu % 8) return false;
+  BigPlan pl;
+  pl.ntm = (g.M + BBM - 1) / BBM;
+  pl.ntn = (int)((g.N + BBN - 1) / BBN);
+  pl.per_xcd = (ncu / 8) / pl.ntn * pl.ntn;  // whole groups of the ntn column tiles
+  if (pl.per_xcd < pl.ntn) return false;
+  const dim3 grid((unsigned)(8 * pl.per_xcd)), blk(512);
+#define MRL_BIG(DU, OB) hipLaunchKernelGGL((gemm_bf16_big_kernel<DU, OB>), grid, blk, 0, s, g, pl)
+  if (dual) { if (outbf) MRL_BIG(true, true); else MRL_BIG(true, false); }
+  else { if (outbf) MRL_BIG(false, true); else MRL_BIG(false, false); }
+#undef MRL_BIG
+  return true;
+}
+
 // The streaming kernel for a tall NN product (K of 257..512, N >= 64, one block per CU):
 // launched here and true, or false (the tiled kernel runs).
 static bool stream_gemm_launch(const GemmB16Args& g, bool outbf, bool dual, hipStream_t s) {
@@ -519,7 +784,9 @@ static bool stream_gemm_launch(const GemmB16Args& g, bool outbf, bool dual, hipS
     const char* e = getenv("MRL_GEMM_STREAM_MIN_M");
     return e ? atoi(e) : MRL_GEMM_STREAM_MIN_M;
   }();
-  if (env_min <= 0 || g.M < env_min || g.N < 64 || g.K <= 256 || g.K > 512) return false;
+  // the dual product (JVP: A.B + A2.B2) measured slower streamed (2.72 vs 1.93 ms at
+  // M = 1 M, K = N = 512: twice the A traffic per MFMA through one BN = 64 slice) -> tiled
+  if (env_min <= 0 || dual || g.M < env_min || g.N < 64 || g.K <= 256 || g.K > 512) return false;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return false;
@@ -532,11 +799,9 @@ static bool stream_gemm_launch(const GemmB16Args& g, bool outbf, bool dual, hipS
   const dim3 grid((unsigned)ncu), blk(512);
 #define MRL_STREAM(KP, DU, OB) hipLaunchKernelGGL((gemm_bf16_stream_kernel<KP, DU, OB>), grid, blk, 0, s, g, pl)
   if (g.K <= 384) {
-    if (dual) { if (outbf) MRL_STREAM(384, true, true); else MRL_STREAM(384, true, false); }
-    else { if (outbf) MRL_STREAM(384, false, true); else MRL_STREAM(384, false, false); }
+    if (outbf) MRL_STREAM(384, false, true); else MRL_STREAM(384, false, false);
   } else {
-    if (dual) { if (outbf) MRL_STREAM(512, true, true); else MRL_STREAM(512, true, false); }
-    else { if (outbf) MRL_STREAM(512, false, true); else MRL_STREAM(512, false, false); }
+    if (outbf) MRL_STREAM(512, false, true); else MRL_STREAM(512, false, false);
   }
 #undef MRL_STREAM
   return true;
@@ -579,6 +844,7 @@ int mrl_gemm_bf16(const mrl_gemm_bf16_desc* d, const int32_t* skip, void* stream
 #define MRL_GEMM_BF16_BK 64
 #endif
   constexpr int BK = MRL_GEMM_BF16_BK;
+  if (big_gemm_launch(g, bf, d->a2 != nullptr, s)) return hip_check(hipGetLastError(), "mrl_gemm_bf16");
   if (stream_gemm_launch(g, bf, d->a2 != nullptr, s)) return hip_check(hipGetLastError(), "mrl_gemm_bf16");
   if (g.N <= 32) {
     const dim3 grid(1, gm);

@@ -479,6 +479,7 @@ def test_bf16_streaming_gemm_equals_tiled(epi, monkeypatch):
         for out_bf in (0, 1):
             outs = []
             for min_m in ("0", "1"):  # 0: the tiled kernel; 1: streaming for every M
+                monkeypatch.setenv("MRL_GEMM_BIG_MIN_M", "0")
                 monkeypatch.setenv("MRL_GEMM_STREAM_MIN_M", min_m)
                 C = torch.full((M * N,), -7, dtype=torch.int16, device="cuda") if out_bf else \
                     torch.full((M * N,), float("nan"), dtype=torch.float32, device="cuda")
@@ -492,6 +493,72 @@ def test_bf16_streaming_gemm_equals_tiled(epi, monkeypatch):
                 torch.cuda.synchronize()
                 outs.append(C)
             assert torch.equal(outs[0], outs[1]), (M, N, K, dual, out_bf)
+            if not out_bf:
+                f32_out = outs[1]
+        rows = rng.choice(M, 300, replace=False)
+        rows[0] = M - 1
+        want = bfr(A[rows]) @ bfr(W)
+        if dual:
+            want = want + bfr(A2[rows]) @ bfr(W2)
+        want = want + bias.astype(np.float64)
+        if epi == "tanh":
+            want = np.tanh(want)
+        elif epi == "dtanh":
+            hb = bfr(H[rows])
+            want = want * (1.0 - hb * hb)
+        got = f32_out.cpu().numpy().reshape(M, N)[rows].astype(np.float64)
+        assert np.abs(got - want).max() / np.abs(want).max() < 2e-5, (M, N, K, dual)
+
+
+@pytest.mark.parametrize("epi", ["store", "tanh", "dtanh"])
+def test_bf16_big_tile_gemm_equals_tiled(epi, monkeypatch):
+    """The 256 x 256 LDS-DMA NN kernel (persistent, two 64-deep K stages, XOR-swizzled
+    stage images) against the 128 x 128 tiled kernel, bit for bit, and against the
+    float64 product: row tails (M not a multiple of 256, fewer row tiles than a round),
+    K tails at lda (376: the chunks past K read the zero block) and inside lda (377 ->
+    384), N tails (200, 300: partial column tiles, clamped Bt rows), single / dual,
+    f32 / bf16 outputs, and two launches of the same call (deterministic)."""
+    import ctypes
+
+    from modular_rl_amd import _lib
+    from modular_rl_amd._lib import call, stream
+    rng = np.random.default_rng(12)
+    E = {"store": _lib.GEMM_STORE, "tanh": _lib.GEMM_TANH, "dtanh": _lib.GEMM_DTANH}[epi]
+    monkeypatch.setenv("MRL_GEMM_STREAM_MIN_M", "0")
+    for (M, N, K, ldk, dual) in [(70001, 512, 512, 512, False), (40000, 512, 512, 512, True),
+                                 (3333, 200, 376, 376, False), (35000, 300, 377, 384, True),
+                                 (100000, 512, 376, 376, True)]:
+        A, A2 = rng.standard_normal((M, K)), rng.standard_normal((M, K))
+        W, W2 = rng.standard_normal((K, N)) * 0.05, rng.standard_normal((K, N)) * 0.05
+        bias = rng.standard_normal(N).astype(np.float32)
+        H = np.tanh(rng.standard_normal((M, N)))
+        dA, dA2, dH = _bf16_dev(A, ldk), _bf16_dev(A2, ldk), _bf16_dev(H, N)
+        Bt = torch.zeros(N * ldk, dtype=torch.int16, device="cuda")
+        Bt2 = torch.zeros(N * ldk, dtype=torch.int16, device="cuda")
+        for w, bt in ((W, Bt), (W2, Bt2)):
+            dw = _dev(w.astype(np.float32))
+            call("mrl_pack_w_bf16", ctypes.c_void_p(dw.data_ptr()), K, N, 1, ctypes.c_void_p(bt.data_ptr()), ldk,
+                 stream())
+        db = _dev(bias)
+        for out_bf in (0, 1):
+            outs = []
+            for big in ("0", "1", "1"):  # the tiled kernel, then the 256 x 256 kernel twice
+                monkeypatch.setenv("MRL_GEMM_BIG_MIN_M", big)
+                C = torch.full((M * N,), -7, dtype=torch.int16, device="cuda") if out_bf else \
+                    torch.full((M * N,), float("nan"), dtype=torch.float32, device="cuda")
+                g = _lib.GemmBf16Desc(m=M, n=N, k=K, a=ctypes.c_void_p(dA.data_ptr()), lda=ldk,
+                                      bt=ctypes.c_void_p(Bt.data_ptr()), ldb=ldk,
+                                      a2=ctypes.c_void_p(dA2.data_ptr()) if dual else None,
+                                      bt2=ctypes.c_void_p(Bt2.data_ptr()) if dual else None,
+                                      c=ctypes.c_void_p(C.data_ptr()), ldc=N, c_bf16=out_bf, epilogue=E,
+                                      bias=ctypes.c_void_p(db.data_ptr()), h=ctypes.c_void_p(dH.data_ptr()), ldh=N)
+                call("mrl_gemm_bf16", ctypes.byref(g), None, stream())
+                torch.cuda.synchronize()
+                outs.append(C)
+            assert torch.equal(outs[1], outs[2]), (M, N, K, dual, out_bf)
+            diff = (outs[0] != outs[1]).sum().item()
+            assert diff == 0, (M, N, K, dual, out_bf, diff,
+                               (outs[0].float() - outs[1].float()).abs().max().item() if not out_bf else None)
             if not out_bf:
                 f32_out = outs[1]
         rows = rng.choice(M, 300, replace=False)

@@ -1,4 +1,4 @@
-"""Diagnostic: the streaming bf16 NN kernel vs the tiled one at the Humanoid layer shapes
+"""Diagnostic: the 256 x 256 LDS-DMA and streaming bf16 NN kernels vs the tiled one at the Humanoid layer shapes
 (M = 1,048,576 rows): ms per launch, TFLOP/s, and algorithmic HBM GB/s (A + A2 read once,
 C and H once; Bt from L2)."""
 import ctypes
@@ -43,8 +43,12 @@ for (K, N, dual, epi, outbf) in [(512, 512, False, _lib.GEMM_TANH, 1), (512, 512
     gb = _lib.GemmBf16Desc(m=M, n=N, k=K, a=P(Ab), lda=ldk, bt=P(Bt), ldb=ldk, a2=P(Ab) if dual else None,
                            bt2=P(Bt) if dual else None, c=P(Cb), ldc=N, c_bf16=outbf, epilogue=epi, h=P(Hb), ldh=N)
     res = []
-    for mm in ("0", "1"):
+    outs = []
+    for name, big, mm in (("tiled", "0", "0"), ("stream", "0", "1"), ("big256", "1", "0")):
+        os.environ["MRL_GEMM_BIG_MIN_M"] = big
         os.environ["MRL_GEMM_STREAM_MIN_M"] = mm
         t = timed(lambda: call("mrl_gemm_bf16", ctypes.byref(gb), None, stream()))
-        res.append(f"{'stream' if mm == '1' else 'tiled'} {t:.3f} ms {flop / t / 1e9:.0f} TF {byts / t / 1e6:.0f} GB/s")
+        outs.append(Cb.clone())
+        res.append(f"{name} {t:.3f} ms {flop / t / 1e9:.0f} TF {byts / t / 1e6:.0f} GB/s")
+    res.append("big==tiled" if torch.equal(outs[0], outs[2]) else "BIG DIFFERS")
     print(f"NN K={K} N={N} dual={dual} epi={epi} outbf={outbf}: " + " | ".join(res), flush=True)
