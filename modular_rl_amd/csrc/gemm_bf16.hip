@@ -389,12 +389,16 @@ __device__ inline void glds16b(const void* g, bfr_t* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
-template <bool DUAL, bool OUTBF>
+// DT: the DTANH epilogue (H operand), compiled apart so the others carry no H registers
+template <bool DUAL, bool OUTBF, bool DT>
 __global__ __launch_bounds__(512, 2) void gemm_bf16_big_kernel(GemmB16Args g, BigPlan pl) {
   __shared__ __attribute__((aligned(16))) bfr_t sb0[BSTAGE];
   __shared__ __attribute__((aligned(16))) bfr_t sb1[BSTAGE];
   __shared__ __attribute__((aligned(16))) bfr_t sb2[BSTAGE];
   __shared__ __attribute__((aligned(16))) bfr_t sb3[BSTAGE];
+  // the block's bias columns (its column tile is fixed): an epilogue read from LDS, not a
+  // global load, whose wait would drain every DMA and store in flight (vmcnt is in order)
+  __shared__ __attribute__((aligned(16))) float sbias[BBN];
   if (g.skip != nullptr && *g.skip != 0) return;
   const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -402,6 +406,10 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_big_kernel(GemmB16Args g, Bi
   const int xcd = blockIdx.x % 8, y = blockIdx.x / 8;
   if (y >= pl.per_xcd) return;
   const int tn = y % pl.ntn, lr = y / pl.ntn, rows_per_round = pl.per_xcd / pl.ntn;
+  if (threadIdx.x < BBN) {
+    const int64_t c = (int64_t)tn * BBN + threadIdx.x;
+    sbias[threadIdx.x] = (g.bias != nullptr && c < g.N) ? g.bias[c] : 0.f;
+  }
   const int64_t tstride = 8 * (int64_t)rows_per_round;
   const int64_t ntk = (g.K + BBK - 1) / BBK, nst = (DUAL ? 2 : 1) * ntk;
   // DMA of stage s of row tile tm into `dst`: waves 0..3 fetch A rows 64 w .. + 63, waves
@@ -482,20 +490,45 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_big_kernel(GemmB16Args g, Bi
   // with the stage loaded next; then that DMA goes out, and the fragment reads of the
   // second k-step and of the next stage's first k-step run under the MFMAs.
   Frag f0, f1;
+  // vmcnt retires in issue order and counts stores too: the epilogue's stores of an
+  // interior tile (16 per wave with bf16 output, 32 with f32) are issued after the loads
+  // of the next tile's first two stages, so those two stages' waits let them stay in
+  // flight (vmcnt 4 + stores) instead of draining them.
+  int post = 0;
   auto stage = [&](const bfr_t* cur, const bfr_t* next, bfr_t* load) {
     const int later = issued - consumed - 2;  // stages issued after the next one
+#ifndef MRL_BIG_NO_STORE_COUNT
+    if (later >= 1 && post > 0) {
+      if (OUTBF) asm volatile("s_waitcnt vmcnt(20) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(36) lgkmcnt(0)" ::: "memory");
+    } else
+#endif
     if (later >= 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    post = post > 0 ? post - 1 : 0;
     __builtin_amdgcn_s_barrier();
+#ifdef MRL_BIG_OLD_ORDER
     issue_next(load);
     read(cur, 1, f1);
     mfma(f0);
     if (issued - consumed >= 2) read(next, 0, f0);  // the next stage exists
     mfma(f1);
+#else
+    // the f0 MFMAs go first (their fragments are in registers), the DMA and the second
+    // k-step's reads under them; the next stage's first reads are unconditional (past
+    // the stream's end they read a stale stage, unused) so the compiler's lgkmcnt
+    // tracking stays exact and the first MFMA waits only for f0
+    read(cur, 1, f1);
+    mfma(f0);
+    issue_next(load);
+    read(next, 0, f0);
+    mfma(f1);
+#endif
     ++consumed;
   };
   // 16-B vector epilogue (ldc, ldh multiples of 8)
   const bool vec = (g.ldc & 7) == 0 && (g.epi != MRL_GEMM_DTANH || (g.ldh & 7) == 0);
+  __syncthreads();  // sbias
   issue_next(sb0);
   issue_next(sb1);
   issue_next(sb2);
@@ -504,6 +537,7 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_big_kernel(GemmB16Args g, Bi
     __builtin_amdgcn_s_barrier();
     read(sb0, 0, f0);
   }
+  const bool ncols_full = (int64_t)(tn + 1) * BBN <= g.N;
   for (int64_t tm = (int64_t)xcd * rows_per_round + lr; tm < pl.ntm; tm += tstride) {
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -521,11 +555,35 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_big_kernel(GemmB16Args g, Bi
     // 16p + 8h .. + 7: half the store instructions, 16-B bf16 stores (the epilogue is
     // store-issue-bound: 8-B stores ran 1.1-1.2 x slower).  The next tile's first stages
     // are already in flight.
+#ifdef MRL_BIG_ABL_NOEPI  // diagnostic timing build only (tools/build_ablate.sh): no epilogue
+    {
+      float sacc = 0.f;
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc += acc[mi][ni][r];
+      if (sacc == 1234.5f) reinterpret_cast<float*>(g.C)[tm] = sacc;
+      continue;
+    }
+#endif
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int64_t row = tm * BBM + 64 * wm + 32 * mi + j;
+      // DTANH: the H chunks of the 32-row tile issued together (one wait, not eight)
+      uint4 hv[DT ? 4 : 1][2];
+#pragma unroll
+      for (int ni = 0; ni < (DT ? 4 : 1); ++ni)
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          const int64_t c0 = (int64_t)tn * BBN + 128 * wn + 32 * ni + 16 * pp + 8 * h;
+          hv[ni][pp] = (DT && vec && row < g.M && c0 + 8 <= g.N)
+                           ? *reinterpret_cast<const uint4*>(g.H + row * g.ldh + c0)
+                           : make_uint4(0u, 0u, 0u, 0u);
+        }
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
-        const int64_t row = tm * BBM + 64 * wm + 32 * mi + j;
         const int64_t cbase = (int64_t)tn * BBN + 128 * wn + 32 * ni;
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
@@ -541,20 +599,21 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_big_kernel(GemmB16Args g, Bi
           const int64_t c0 = cbase + 16 * pp + 8 * h;
           if (vec && c0 + 8 <= g.N) {
             if (g.bias != nullptr) {
-              const float4 b0 = *reinterpret_cast<const float4*>(g.bias + c0);
-              const float4 b1 = *reinterpret_cast<const float4*>(g.bias + c0 + 4);
+              const float* bp = sbias + 128 * wn + 32 * ni + 16 * pp + 8 * h;
+              const float4 b0 = *reinterpret_cast<const float4*>(bp);
+              const float4 b1 = *reinterpret_cast<const float4*>(bp + 4);
               v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
               v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
             }
-            if (g.epi == MRL_GEMM_TANH) {
+            if (!DT && g.epi == MRL_GEMM_TANH) {
 #pragma unroll
               for (int e = 0; e < 8; e += 2) {
                 const f32x2 t = tanh_fast2(f32x2{v[e], v[e + 1]});
                 v[e] = t.x;
                 v[e + 1] = t.y;
               }
-            } else if (g.epi == MRL_GEMM_DTANH) {
-              const uint4 hb = *reinterpret_cast<const uint4*>(g.H + row * g.ldh + c0);
+            } else if (DT) {
+              const uint4 hb = hv[DT ? ni : 0][pp];
               const uint32_t hw[4] = {hb.x, hb.y, hb.z, hb.w};
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
@@ -581,13 +640,16 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_big_kernel(GemmB16Args g, Bi
             const int64_t col = c0 + e;
             if (col >= g.N) continue;
             float xv = v[e] + (g.bias != nullptr ? g.bias[col] : 0.f);
-            if (g.epi == MRL_GEMM_TANH) xv = tanh_fast(xv);
-            else if (g.epi == MRL_GEMM_DTANH) xv *= dtanh(bf2f(g.H[row * g.ldh + col]));
+            if (!DT && g.epi == MRL_GEMM_TANH) xv = tanh_fast(xv);
+            else if (DT) xv *= dtanh(bf2f(g.H[row * g.ldh + col]));
             if (OUTBF) reinterpret_cast<bfr_t*>(g.C)[row * g.ldc + col] = f2bf(xv);
             else reinterpret_cast<float*>(g.C)[row * g.ldc + col] = xv;
           }
         }
       }
+    }
+    // every lane of an interior tile issued all its vector stores (the count above)
+    post = (vec && ncols_full && (tm + 1) * BBM <= g.M) ? 2 : 0;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the block
 }
@@ -770,7 +832,11 @@ static bool big_gemm_launch(const GemmB16Args& g, bool outbf, bool dual, hipStre
   pl.per_xcd = (ncu / 8) / pl.ntn * pl.ntn;  // whole groups of the ntn column tiles
   if (pl.per_xcd < pl.ntn) return false;
   const dim3 grid((unsigned)(8 * pl.per_xcd)), blk(512);
-#define MRL_BIG(DU, OB) hipLaunchKernelGGL((gemm_bf16_big_kernel<DU, OB>), grid, blk, 0, s, g, pl)
+#define MRL_BIG(DU, OB)                                                                       \
+  do {                                                                                        \
+    if (g.epi == MRL_GEMM_DTANH) hipLaunchKernelGGL((gemm_bf16_big_kernel<DU, OB, true>), grid, blk, 0, s, g, pl); \
+    else hipLaunchKernelGGL((gemm_bf16_big_kernel<DU, OB, false>), grid, blk, 0, s, g, pl);   \
+  } while (0)
   if (dual) { if (outbf) MRL_BIG(true, true); else MRL_BIG(true, false); }
   else { if (outbf) MRL_BIG(false, true); else MRL_BIG(false, false); }
 #undef MRL_BIG

@@ -512,7 +512,7 @@ def test_bf16_streaming_gemm_equals_tiled(epi, monkeypatch):
 
 @pytest.mark.parametrize("epi", ["store", "tanh", "dtanh"])
 def test_bf16_big_tile_gemm_equals_tiled(epi, monkeypatch):
-    """The 256 x 256 LDS-DMA NN kernel (persistent, two 64-deep K stages, XOR-swizzled
+    """The 256 x 256 LDS-DMA NN kernel (persistent, four 32-deep K stages, XOR-swizzled
     stage images) against the 128 x 128 tiled kernel, bit for bit, and against the
     float64 product: row tails (M not a multiple of 256, fewer row tiles than a round),
     K tails at lda (376: the chunks past K read the zero block) and inside lda (377 ->
