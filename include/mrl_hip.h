@@ -442,6 +442,11 @@ int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, cons
 int mrl_rollout_act_head(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const float* hidden,
                          int32_t n_hidden, const float* w_head, const float* b_head, const float* logstd,
                          const mrl_rollout_bufs* b, int32_t t, void* stream);
+/* the same with the last hidden layer as bf16 rows (hidden16 [E, n_hidden] uint16 bf16
+ * bits, the bf16 tape's activations from mrl_gemm_bf16): MRL_COMPUTE_BF16 only */
+int mrl_rollout_act_head_bf16(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const uint16_t* hidden16,
+                              int32_t n_hidden, const float* w_head, const float* b_head, const float* logstd,
+                              const mrl_rollout_bufs* b, int32_t t, void* stream);
 /* after step T-1: fold the last reward partials into the reward stat, advance the
  * iteration counter (obs_T is never pushed: the horizon cuts the episode) */
 int mrl_rollout_finish(const mrl_rollout_desc* d, const mrl_rollout_bufs* b, void* stream);

@@ -148,6 +148,7 @@ SIGNATURES = {
     "mrl_rollout_obs": (i32, [vp, vp, i32, vp]),
     "mrl_rollout_act": (i32, [vp, i32, i32, vp, vp, vp, i32, vp]),
     "mrl_rollout_act_head": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
+    "mrl_rollout_act_head_bf16": (i32, [vp, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
 }
 
 _lib = None

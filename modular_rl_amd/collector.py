@@ -183,12 +183,19 @@ class Collector:
         if env.kind == _lib.ENV_HUMANOID and not self.layered:
             raise _lib.MrlError("Humanoid-v2 needs a layered policy net (its 376-d obs exceeds the fused kernel)")
         self.raw_obs = None
+        self.hidden_b16 = False
         if self.layered:
             # persistent per-step buffers (their addresses are baked into the captured graph)
             self.raw_obs = torch.zeros((O + 1) * self.E, **f64)
             self._zrows = torch.zeros(self.E * A, dtype=torch.float32, device=self.dev)
             w = max(net.hid_sizes)
             self._fwd_bufs = [torch.zeros(self.E * w, dtype=torch.float32, device=self.dev) for _ in range(2)]
+            # bf16 tape mode, Humanoid: the hidden layers on the bf16 GEMMs (bf16 rows)
+            self.hidden_b16 = self.wave_per_env and bool(getattr(net, "tape_bf16", False))
+            if self.hidden_b16:
+                i16 = dict(dtype=torch.int16, device=self.dev)
+                self._fwd_b16 = [torch.zeros(self.E * w, **i16) for _ in range(2)]
+                self._xb16 = torch.zeros(self.E * ((O + 7) // 8 * 8), **i16)
         else:
             # fused step kernel: its own policy image, repacked from theta at every collect
             n = int(lib.mrl_rollout_image_floats(ctypes.byref(net.desc)))
@@ -244,10 +251,16 @@ class Collector:
         logstd = net._addr(net.theta, net.tls) if net.head == _lib.HEAD_GAUSS else None
         call("mrl_rollout_reset_rows", d, ctypes.byref(bufs), stream())
         L = len(net.dims) - 1
+        wt = net.rollout_images() if self.hidden_b16 else None
         for t in range(self.T):
             call("mrl_rollout_obs", d, ctypes.byref(bufs), int(t), stream())
             x = self.obs[t * E:(t + 1) * E]
-            if self.wave_per_env:
+            if self.hidden_b16:
+                hid = net.forward_hidden_rows_b16(x, E, wt, self._fwd_b16, self._xb16)
+                call("mrl_rollout_act_head_bf16", d, int(net.head), int(net.n_out), ptr(hid), int(net.dims[L - 1]),
+                     net._addr(net.theta, net.w_off[L - 1]), net._addr(net.theta, net.b_off[L - 1]), logstd,
+                     ctypes.byref(bufs), int(t), stream())
+            elif self.wave_per_env:
                 # Humanoid: the head (1024 x 512 x 17, a thin GEMM) runs inside the step
                 hid = net.forward_hidden_rows(x, E, self._fwd_bufs)
                 call("mrl_rollout_act_head", d, int(net.head), int(net.n_out), ptr(hid), int(net.dims[L - 1]),

@@ -654,6 +654,127 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_big_kernel(GemmB16Args g, Bi
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the block
 }
 
+// ------------------------------------------------------------------ small-M NN GEMM
+// The Humanoid rollout's per-step hidden layers (M = E = 1024 rows, K <= 512, N = 512)
+// are latency-bound: the 128 x 128 tiled kernel gives 32 blocks a serial 8-stage K loop.
+// Here a block takes a 64 x 64 tile (four waves of 32 x 32, one accumulator each) and
+// stages its whole A / Bt panels (K <= 512) by LDS-DMA at entry, as four K quarters
+// (128 k each) in separate LDS objects: quarter q's MFMAs start as soon as its DMA has
+// landed (counted vmcnt + barrier) while the later quarters are still in flight.  Image
+// [row][16 chunks] per quarter (256-B rows), chunk c of row r at c ^ (r & 15): the 16
+// rows of a ds_read_b128 lane group cover the 64 banks once.  Same k order per output
+// as gemm_bf16_kernel (k-steps of 16 ascending): bit-identical results.
+constexpr int SBM = 64, SBN = 64, SQK = 128;  // tile, K per quarter
+constexpr int SQ_ELEMS = SBM * SQK;            // bf16 per quarter image (16 KB)
+
+template <bool OUTBF>
+__global__ __launch_bounds__(256) void gemm_bf16_small_kernel(GemmB16Args g) {
+  __shared__ __attribute__((aligned(16))) bfr_t a0[SQ_ELEMS], a1[SQ_ELEMS], a2[SQ_ELEMS], a3[SQ_ELEMS];
+  __shared__ __attribute__((aligned(16))) bfr_t b0[SQ_ELEMS], b1[SQ_ELEMS], b2[SQ_ELEMS], b3[SQ_ELEMS];
+  if (g.skip != nullptr && *g.skip != 0) return;
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t m0 = (int64_t)blockIdx.y * SBM, n0 = (int64_t)blockIdx.x * SBN;
+  const int nq = (int)((g.K + SQK - 1) / SQK);  // quarters (host: K <= 512); k past K reads zeros
+  // DMA: wave w, instruction i covers rows 16 w + 4 i + (lane >> 4), position lane & 15
+  const int pos = lane & 15;
+  auto dma = [&](bfr_t* qa, bfr_t* qb, int q) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 16 * wave + 4 * i + (lane >> 4);
+      const int c = pos ^ (r & 15);
+      const int64_t k = (int64_t)q * SQK + 8 * c;
+      const int64_t ra = min(m0 + r, g.M - 1), rb = min(n0 + r, g.N - 1);
+      const void* sa = k < g.K ? (const void*)(g.A + ra * g.lda + k) : (const void*)kZero16;
+      const void* sb = k < g.K ? (const void*)(g.Bt + rb * g.ldb + k) : (const void*)kZero16;
+      glds16b(sa, qa + (16 * wave + 4 * i) * 128);
+      glds16b(sb, qb + (16 * wave + 4 * i) * 128);
+    }
+  };
+  dma(a0, b0, 0);
+  if (nq > 1) dma(a1, b1, 1);
+  if (nq > 2) dma(a2, b2, 2);
+  if (nq > 3) dma(a3, b3, 3);
+  f32x16 acc = zero16();
+  const int ra = 32 * wm + j, rb = 32 * wn + j;
+  // quarter q: this wave's DMA of it has landed (8 instructions per later quarter still
+  // in flight), then every wave's (the barrier); 8 k-steps, branch-free (zeros past K)
+  auto quarter = [&](const bfr_t* As, const bfr_t* Bs, int later) {
+    if (later >= 3) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (later == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // the fragment reads as inline asm: the compiler's LDS-DMA alias tracking (a few
+    // DMAs deep) would otherwise drain every quarter still in flight (vmcnt 0) before
+    // them; their completion is this lambda's explicit lgkmcnt wait, which takes the
+    // fragments as operands so no MFMA is scheduled above it
+    u32x4v av[8], bv[8];
+    const uint32_t la = (uint32_t)reinterpret_cast<uintptr_t>(As) + 2 * ra * 128;
+    const uint32_t lb = (uint32_t)reinterpret_cast<uintptr_t>(Bs) + 2 * rb * 128;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int c = 2 * ks + h;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(av[ks]) : "v"(la + 16 * (c ^ (ra & 15))));
+      asm volatile("ds_read_b128 %0, %1" : "=v"(bv[ks]) : "v"(lb + 16 * (c ^ (rb & 15))));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]), "+v"(av[4]), "+v"(av[5]), "+v"(av[6]),
+                   "+v"(av[7]), "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]), "+v"(bv[4]), "+v"(bv[5]),
+                   "+v"(bv[6]), "+v"(bv[7]));
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)  // C^T tile: lane (j, h) holds row j
+      acc = MFMA32B(__builtin_bit_cast(bf16x8, bv[ks]), __builtin_bit_cast(bf16x8, av[ks]), acc);
+  };
+  quarter(a0, b0, nq - 1);
+  if (nq > 1) quarter(a1, b1, nq - 2);
+  if (nq > 2) quarter(a2, b2, nq - 3);
+  if (nq > 3) quarter(a3, b3, 0);
+  // epilogue (gemm_bf16_kernel's, one 32 x 32 tile per wave)
+  const int64_t row = m0 + 32 * wm + j;
+  if (row >= g.M) return;
+  const bool vec = (g.ldc & 3) == 0;
+  const int64_t cbase = n0 + 32 * wn;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t c0 = cbase + 8 * q + 4 * h;
+    float v[4];
+    if (vec && c0 + 4 <= g.N) {
+      const float4 b = g.bias != nullptr ? *reinterpret_cast<const float4*>(g.bias + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[0] = acc[4 * q + 0] + b.x;
+      v[1] = acc[4 * q + 1] + b.y;
+      v[2] = acc[4 * q + 2] + b.z;
+      v[3] = acc[4 * q + 3] + b.w;
+      if (g.epi == MRL_GEMM_TANH) {
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const f32x2 t = tanh_fast2(f32x2{v[e], v[e + 1]});
+          v[e] = t.x;
+          v[e + 1] = t.y;
+        }
+      }
+      if (OUTBF) {
+        const uint2 o = {(uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                         (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16)};
+        *reinterpret_cast<uint2*>(reinterpret_cast<bfr_t*>(g.C) + row * g.ldc + c0) = o;
+      } else {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.C) + row * g.ldc + c0) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      continue;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t col = c0 + e;
+      if (col >= g.N) continue;
+      float x = acc[4 * q + e] + (g.bias != nullptr ? g.bias[col] : 0.f);
+      if (g.epi == MRL_GEMM_TANH) x = tanh_fast(x);
+      if (OUTBF) reinterpret_cast<bfr_t*>(g.C)[row * g.ldc + col] = f2bf(x);
+      else reinterpret_cast<float*>(g.C)[row * g.ldc + col] = x;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ TN (weight grads)
 // K step: 32 rows; LDS images [32 rows][BM or BN columns], pitch 160 bf16 (320 B): a
 // 32-lane half's transposed read (rows q = 0..3, 8 B at columns 16G + 4p) covers all
@@ -812,6 +933,9 @@ using namespace mrl;
 #ifndef MRL_GEMM_STREAM_MIN_M  // rows from which the streaming kernel takes the NN GEMM (0: never)
 #define MRL_GEMM_STREAM_MIN_M 32768
 #endif
+#ifndef MRL_GEMM_SMALL_MAX_M  // rows up to which the whole-K 64 x 64 kernel takes the NN GEMM (0: never)
+#define MRL_GEMM_SMALL_MAX_M 8192
+#endif
 #ifndef MRL_GEMM_BIG_MIN_M  // rows from which the 256 x 256 LDS-DMA kernel takes the NN GEMM (0: never)
 #define MRL_GEMM_BIG_MIN_M 65536
 #endif
@@ -911,6 +1035,17 @@ int mrl_gemm_bf16(const mrl_gemm_bf16_desc* d, const int32_t* skip, void* stream
 #endif
   constexpr int BK = MRL_GEMM_BF16_BK;
   if (big_gemm_launch(g, bf, d->a2 != nullptr, s)) return hip_check(hipGetLastError(), "mrl_gemm_bf16");
+  {
+    // small M (the Humanoid rollout's per-step layers): whole-K panels, 64 x 64 tiles
+    const char* e = getenv("MRL_GEMM_SMALL_MAX_M");
+    const int64_t max_m = e ? atoll(e) : MRL_GEMM_SMALL_MAX_M;
+    if (d->a2 == nullptr && g.M <= max_m && g.K <= 4 * SQK && g.N >= 64 && g.epi != MRL_GEMM_DTANH) {
+      const dim3 grid((unsigned)((g.N + SBN - 1) / SBN), (unsigned)((g.M + SBM - 1) / SBM));
+      if (bf) hipLaunchKernelGGL((gemm_bf16_small_kernel<true>), grid, dim3(256), 0, s, g);
+      else hipLaunchKernelGGL((gemm_bf16_small_kernel<false>), grid, dim3(256), 0, s, g);
+      return hip_check(hipGetLastError(), "mrl_gemm_bf16");
+    }
+  }
   if (stream_gemm_launch(g, bf, d->a2 != nullptr, s)) return hip_check(hipGetLastError(), "mrl_gemm_bf16");
   if (g.N <= 32) {
     const dim3 grid(1, gm);

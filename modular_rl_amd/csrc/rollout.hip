@@ -1330,6 +1330,7 @@ struct HeadRows {
   const float* w;    // [nh, A] head kernel (Keras layout)
   const float* b;    // [A]
   int nh, bf;
+  const uint16_t* hid16;  // the hidden rows as bf16 bits instead of hid (the bf16 tape's)
 };
 
 __device__ inline float head_z(const HeadRows& hr, int e, int lane) {
@@ -1338,8 +1339,9 @@ __device__ inline float head_z(const HeadRows& hr, int e, int lane) {
 #pragma unroll
   for (int o = 0; o < A; ++o) acc[o] = 0.f;
   const float* hrow = hr.hid + (int64_t)e * hr.nh;
+  const uint16_t* hrow16 = hr.hid16 + (int64_t)e * hr.nh;
   for (int k = lane; k < hr.nh; k += 64) {
-    const float hv = hr.bf ? bf16r(hrow[k]) : hrow[k];
+    const float hv = hr.hid16 ? __uint_as_float((uint32_t)hrow16[k] << 16) : (hr.bf ? bf16r(hrow[k]) : hrow[k]);
     const float* wr = hr.w + (int64_t)k * A;
 #pragma unroll
     for (int o = 0; o < A; ++o) acc[o] = fmaf(hv, hr.bf ? bf16r(wr[o]) : wr[o], acc[o]);
@@ -1362,11 +1364,12 @@ __global__ __launch_bounds__(64) void hm_act_kernel(RollArgs a, const float* __r
   __shared__ hm::Shared S;
   hm::load_shared(S, lane);
   if (lane < HM_NS) W.s[lane] = a.b.env_state[(int64_t)lane * E + e];
-  const float zh = hr.hid != nullptr ? head_z(hr, e, lane) : 0.f;
+  const bool fused = hr.hid != nullptr || hr.hid16 != nullptr;
+  const float zh = fused ? head_z(hr, e, lane) : 0.f;
   WAVE_SYNC();
   // sample (DiagGauss, core.py:432-435): a = z + sd * noise in fp32; the action is the ctrl
   if (lane < A) {
-    const float z = hr.hid != nullptr ? zh : zrows[(int64_t)e * A + lane];
+    const float z = fused ? zh : zrows[(int64_t)e * A + lane];
     const float sd = expf(logstd[lane]);
     const double zn = reinterpret_cast<const double*>(a.b.noise)[row * A + lane];
     const float av = __fadd_rn(__fmul_rn((float)zn, sd), z);
@@ -1597,9 +1600,10 @@ static int rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, c
                        const float* logstd, const mrl_rollout_bufs* b, int32_t t, void* stream) {
   int rc = check_rows(d, b);
   if (rc) return rc;
-  if (!b->act || !b->prob || !b->rew || !b->flags || !b->ep_t || (!z && !hr.hid))
+  if (!b->act || !b->prob || !b->rew || !b->flags || !b->ep_t || (!z && !hr.hid && !hr.hid16))
     return fail(E_ARG, "null trajectory buffer");
-  if (hr.hid && d->env_id != MRL_ENV_HUMANOID) return fail(E_UNSUPPORTED, "the fused head is the Humanoid step's");
+  if ((hr.hid || hr.hid16) && d->env_id != MRL_ENV_HUMANOID)
+    return fail(E_UNSUPPORTED, "the fused head is the Humanoid step's");
   if (!b->noise) return fail(E_ARG, "bufs.noise: sampling-noise rows (mrl_rollout_noise or injected) required");
   EnvInfo ei = env_info(d->env_id);
   const bool gauss = head == MRL_HEAD_GAUSS;
@@ -1624,7 +1628,7 @@ static int rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, c
 int mrl_rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const float* z, const float* logstd,
                     const mrl_rollout_bufs* b, int32_t t, void* stream) {
   if (!z) return fail(E_ARG, "null z rows");
-  return rollout_act(d, head, n_out, z, HeadRows{nullptr, nullptr, nullptr, 0, 0}, logstd, b, t, stream);
+  return rollout_act(d, head, n_out, z, HeadRows{nullptr, nullptr, nullptr, 0, 0, nullptr}, logstd, b, t, stream);
 }
 
 int mrl_rollout_act_head(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const float* hidden,
@@ -1634,7 +1638,19 @@ int mrl_rollout_act_head(const mrl_rollout_desc* d, int32_t head, int32_t n_out,
   if (d->env_id != MRL_ENV_HUMANOID || n_out != HM_ACT)
     return fail(E_UNSUPPORTED, "mrl_rollout_act_head: the fused head is the Humanoid step's (17 outputs)");
   return rollout_act(d, head, n_out, nullptr,
-                     HeadRows{hidden, w_head, b_head, n_hidden, (int)(d->compute == MRL_COMPUTE_BF16)}, logstd, b, t,
+                     HeadRows{hidden, w_head, b_head, n_hidden, (int)(d->compute == MRL_COMPUTE_BF16), nullptr}, logstd,
+                     b, t, stream);
+}
+
+int mrl_rollout_act_head_bf16(const mrl_rollout_desc* d, int32_t head, int32_t n_out, const uint16_t* hidden16,
+                              int32_t n_hidden, const float* w_head, const float* b_head, const float* logstd,
+                              const mrl_rollout_bufs* b, int32_t t, void* stream) {
+  if (!d || !hidden16 || !w_head || !b_head || n_hidden <= 0)
+    return fail(E_ARG, "mrl_rollout_act_head_bf16: bad arguments");
+  if (d->env_id != MRL_ENV_HUMANOID || n_out != HM_ACT)
+    return fail(E_UNSUPPORTED, "mrl_rollout_act_head_bf16: the fused head is the Humanoid step's (17 outputs)");
+  if (d->compute != MRL_COMPUTE_BF16) return fail(E_ARG, "mrl_rollout_act_head_bf16: bf16 hidden rows need MRL_COMPUTE_BF16");
+  return rollout_act(d, head, n_out, nullptr, HeadRows{nullptr, w_head, b_head, n_hidden, 1, hidden16}, logstd, b, t,
                      stream);
 }
 

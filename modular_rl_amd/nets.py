@@ -256,7 +256,8 @@ class LayeredMlpNet:
         self._tape = None  # (key, X, ldx, [H_1..H_L], Z)
         # bf16 mode keeps the tape, the JVP / gradient chains and packed weight images in
         # bf16 and runs the large-M passes on the bf16-operand GEMMs (csrc/gemm_bf16.hip);
-        # the rollout's per-step forward (forward_rows) stays on mrl_gemm
+        # the rollout's per-step forward (forward_rows) stays on mrl_gemm, except the
+        # Humanoid step's hidden layers (forward_hidden_rows_b16)
         # (hidden widths a multiple of 8: the bf16 rows are 16-B aligned with no padding)
         self.tape_bf16 = self.compute == _lib.COMPUTE_BF16 and all(h % 8 == 0 for h in self.hid_sizes)
 
@@ -545,6 +546,27 @@ class LayeredMlpNet:
             self._gemm(int(n), dout, din, a, lda, self._addr(self.theta, self.w_off[l]), dout, self._addr(out), dout,
                        epi=_lib.GEMM_TANH, bias=self._addr(self.theta, self.b_off[l]))
             a, lda = self._addr(out), dout
+        return out
+
+    def rollout_images(self):
+        """bf16 W^T images of theta for forward_hidden_rows_b16 (packed once per collect,
+        inside its captured graph, so every replay sees the current policy)."""
+        return self._pack_images(self.theta, "rwt", 1)
+
+    def forward_hidden_rows_b16(self, x, n, wt, bufs16, xb):
+        """forward_hidden_rows on the bf16 tape's kernels (bf16 tape mode): obs rows cast
+        to bf16 into xb, the hidden layers by mrl_gemm_bf16 into the bf16 row buffers
+        bufs16 (the values the f32 path rounds at staging); returns the last one."""
+        L = len(self.dims) - 1
+        ldx = self._ld8(self.n_in)
+        call("mrl_cast_rows_bf16", ptr(x), int(n), self.n_in, self.n_in, ptr(xb), ldx, stream())
+        a, lda, out = xb, ldx, None
+        for l in range(L - 1):
+            din, dout = self.dims[l], self.dims[l + 1]
+            out = bufs16[l % 2]
+            self._gemm_b16(int(n), dout, din, a, lda, wt[l][0], wt[l][1], out, dout, True, _lib.GEMM_TANH,
+                           bias=self._addr(self.theta, self.b_off[l]))
+            a, lda = out, dout
         return out
 
     def forward_rows(self, x, n, z, bufs):

@@ -431,6 +431,29 @@ def test_bf16_rollout_prob_rows_equal_update_forward(env_id):
     assert d32 > 1e-4, d32
 
 
+def test_bf16_humanoid_rollout_hidden_rows_on_bf16_gemms():
+    """bf16 mode, Humanoid (wave-per-env step, head fused into the step): the rollout's
+    hidden layers run on mrl_gemm_bf16 with bf16 rows (mrl_rollout_act_head_bf16), the
+    same kernels and rounding points as the update's bf16 tape, so the prob rows the
+    rollout stores equal the update's forward on the stored observations up to the
+    head's f32 summation order."""
+    from modular_rl_amd.agentzoo import TrpoAgent
+    from modular_rl_amd.envs import make
+    env = make("Humanoid-v2")
+    cfg = dict(timestep_limit=env.spec.max_episode_steps, n_envs=256, horizon=16, seed=3, mlp_dtype="bf16",
+               hid_sizes=[128, 64])
+    agent = TrpoAgent(env.observation_space, env.action_space, cfg)
+    net = agent.policy.net
+    col = agent.make_collector(env, cfg)
+    assert col.hidden_b16
+    b = col.collect()
+    got = b.prob.reshape(b.n, -1)
+    fwd = net.forward(b.obs, b.n).reshape(b.n, -1)
+    err = (got - fwd).abs().max().item() / fwd.abs().max().item()
+    assert err < 2e-5, err
+    assert torch.isfinite(got).all()
+
+
 def test_bf16_trpo_learns_cartpole():
     """C2's throughput mode end to end: TRPO with every MLP pass in bf16 still learns."""
     from modular_rl_amd.agentzoo import TrpoAgent
@@ -508,6 +531,55 @@ def test_bf16_streaming_gemm_equals_tiled(epi, monkeypatch):
             want = want * (1.0 - hb * hb)
         got = f32_out.cpu().numpy().reshape(M, N)[rows].astype(np.float64)
         assert np.abs(got - want).max() / np.abs(want).max() < 2e-5, (M, N, K, dual)
+
+
+@pytest.mark.parametrize("epi", ["store", "tanh"])
+def test_bf16_small_m_gemm_equals_tiled(epi, monkeypatch):
+    """The whole-K 64 x 64 kernel for small M (the Humanoid rollout's per-step layers:
+    K quarters staged by LDS-DMA, fragment reads as inline asm) against the tiled kernel,
+    bit for bit, and the float64 product: M 1024 and ragged (1000, 37), K 512 / 376 (the
+    376-d obs) / 200 (a partial last quarter) / 17 (one chunk past K), N 512 / 200 / 64,
+    f32 / bf16 outputs, with bias."""
+    import ctypes
+
+    from modular_rl_amd import _lib
+    from modular_rl_amd._lib import call, stream
+    rng = np.random.default_rng(21)
+    E = {"store": _lib.GEMM_STORE, "tanh": _lib.GEMM_TANH}[epi]
+    monkeypatch.setenv("MRL_GEMM_STREAM_MIN_M", "0")
+    monkeypatch.setenv("MRL_GEMM_BIG_MIN_M", "0")
+    for (M, N, K) in [(1024, 512, 512), (1024, 512, 376), (1000, 200, 200), (37, 64, 17), (4096, 512, 512)]:
+        ldk = (K + 7) // 8 * 8
+        A = rng.standard_normal((M, K))
+        W = rng.standard_normal((K, N)) * 0.05
+        bias = rng.standard_normal(N).astype(np.float32)
+        dA = _bf16_dev(A, ldk)
+        Bt = torch.zeros(N * ldk, dtype=torch.int16, device="cuda")
+        dw = _dev(W.astype(np.float32))
+        call("mrl_pack_w_bf16", ctypes.c_void_p(dw.data_ptr()), K, N, 1, ctypes.c_void_p(Bt.data_ptr()), ldk, stream())
+        db = _dev(bias)
+        for out_bf in (0, 1):
+            outs = []
+            for small in ("0", "8192"):
+                monkeypatch.setenv("MRL_GEMM_SMALL_MAX_M", small)
+                C = torch.full((M * N,), -7, dtype=torch.int16, device="cuda") if out_bf else \
+                    torch.full((M * N,), float("nan"), dtype=torch.float32, device="cuda")
+                g = _lib.GemmBf16Desc(m=M, n=N, k=K, a=ctypes.c_void_p(dA.data_ptr()), lda=ldk,
+                                      bt=ctypes.c_void_p(Bt.data_ptr()), ldb=ldk, c=ctypes.c_void_p(C.data_ptr()),
+                                      ldc=N, c_bf16=out_bf, epilogue=E, bias=ctypes.c_void_p(db.data_ptr()))
+                call("mrl_gemm_bf16", ctypes.byref(g), None, stream())
+                torch.cuda.synchronize()
+                outs.append(C)
+            diff = (outs[0] != outs[1]).sum().item()
+            assert diff == 0, (M, N, K, out_bf, diff)
+            if not out_bf:
+                ab = np.asarray(torch.tensor(A, dtype=torch.float32).to(torch.bfloat16).to(torch.float64))
+                wb = np.asarray(torch.tensor(W, dtype=torch.float32).to(torch.bfloat16).to(torch.float64))
+                want = ab @ wb + bias
+                if epi == "tanh":
+                    want = np.tanh(want)
+                got = outs[1].cpu().numpy().reshape(M, N).astype(np.float64)
+                assert np.abs(got - want).max() / np.abs(want).max() < 2e-5, (M, N, K)
 
 
 @pytest.mark.parametrize("epi", ["store", "tanh", "dtanh"])
