@@ -460,30 +460,40 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_big_kernel(GemmB16Args g, Bi
   f32x16 acc[2][4];
   // fragments of one 16-deep k-step: A rows of the wave's two 32-row tiles, Bt rows of its
   // four 32-column tiles (chunk 2 ks + h of each row)
+  // The fragment reads are inline asm: the compiler, which tracks only a few LDS-DMAs
+  // per object, otherwise drains every DMA and epilogue store in flight (vmcnt 0) in
+  // front of the first reads of a tile.  Their completion is the stage's explicit
+  // lgkmcnt waits, which take the fragments as operands (no MFMA moves above them).
   struct Frag {
-    bf16x8 a[2], b[4];
+    u32x4v a[2], b[4];
   };
+  // lane byte offsets of k-step ks's first A / Bt fragment; the other 32-row tiles sit
+  // 2048 B apart with the same swizzle ((r >> 2) & 3 does not see the 32-row step)
+  uint32_t offA[2], offB[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int c = (2 * ks + h) ^ ((j >> 2) & 3);
+    offA[ks] = 2 * ((64 * wm + j) * BBK + 8 * c);
+    offB[ks] = 2 * ((BBM + 128 * wn + j) * BBK + 8 * c);
+  }
   auto read = [&](const bfr_t* cur, int ks, Frag& f) {
-    const bfr_t* As = cur;
-    const bfr_t* Bs = cur + BBM * BBK;
-    const int c = 2 * ks + h;
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      const int r = 64 * wm + 32 * mi + j;
-      f.a[mi] = *reinterpret_cast<const bf16x8*>(As + r * BBK + 8 * (c ^ ((r >> 2) & 3)));
-    }
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int r = 128 * wn + 32 * ni + j;
-      f.b[ni] = *reinterpret_cast<const bf16x8*>(Bs + r * BBK + 8 * (c ^ ((r >> 2) & 3)));
-    }
+    const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(cur);
+    const uint32_t va = base + offA[ks], vb = base + offB[ks];
+    asm volatile("ds_read_b128 %0, %1" : "=v"(f.a[0]) : "v"(va));
+    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(f.a[1]) : "v"(va));
+    asm volatile("ds_read_b128 %0, %1" : "=v"(f.b[0]) : "v"(vb));
+    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(f.b[1]) : "v"(vb));
+    asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(f.b[2]) : "v"(vb));
+    asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(f.b[3]) : "v"(vb));
   };
   auto mfma = [&](const Frag& f) {
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = MFMA32B(f.b[ni], f.a[mi], acc[mi][ni]);  // C^T tiles
+      for (int ni = 0; ni < 4; ++ni)  // C^T tiles
+        acc[mi][ni] = MFMA32B(__builtin_bit_cast(bf16x8, f.b[ni]), __builtin_bit_cast(bf16x8, f.a[mi]), acc[mi][ni]);
   };
+#define MRL_FRAG_OPS(f) "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.b[0]), "+v"(f.b[1]), "+v"(f.b[2]), "+v"(f.b[3])
   // One stage (two k-steps).  Its first k-step's fragments are already in f0 (read under
   // the previous stage); the barrier here certifies the NEXT stage's DMA has landed for
   // every wave (at most the stage after it still in flight) and that every wave is done
@@ -497,33 +507,25 @@ __global__ __launch_bounds__(512, 2) void gemm_bf16_big_kernel(GemmB16Args g, Bi
   int post = 0;
   auto stage = [&](const bfr_t* cur, const bfr_t* next, bfr_t* load) {
     const int later = issued - consumed - 2;  // stages issued after the next one
-#ifndef MRL_BIG_NO_STORE_COUNT
     if (later >= 1 && post > 0) {
-      if (OUTBF) asm volatile("s_waitcnt vmcnt(20) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(36) lgkmcnt(0)" ::: "memory");
-    } else
-#endif
-    if (later >= 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if (OUTBF) asm volatile("s_waitcnt vmcnt(20) lgkmcnt(0)" : MRL_FRAG_OPS(f0)::"memory");
+      else asm volatile("s_waitcnt vmcnt(36) lgkmcnt(0)" : MRL_FRAG_OPS(f0)::"memory");
+    } else if (later >= 1) {
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" : MRL_FRAG_OPS(f0)::"memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : MRL_FRAG_OPS(f0)::"memory");
+    }
     post = post > 0 ? post - 1 : 0;
     __builtin_amdgcn_s_barrier();
-#ifdef MRL_BIG_OLD_ORDER
-    issue_next(load);
-    read(cur, 1, f1);
-    mfma(f0);
-    if (issued - consumed >= 2) read(next, 0, f0);  // the next stage exists
-    mfma(f1);
-#else
     // the f0 MFMAs go first (their fragments are in registers), the DMA and the second
     // k-step's reads under them; the next stage's first reads are unconditional (past
-    // the stream's end they read a stale stage, unused) so the compiler's lgkmcnt
-    // tracking stays exact and the first MFMA waits only for f0
+    // the stream's end they read a stale stage, unused)
     read(cur, 1, f1);
     mfma(f0);
     issue_next(load);
     read(next, 0, f0);
+    asm volatile("s_waitcnt lgkmcnt(6)" : MRL_FRAG_OPS(f1)::"memory");  // f1 (f0's six still in flight)
     mfma(f1);
-#endif
     ++consumed;
   };
   // 16-B vector epilogue (ldc, ldh multiples of 8)

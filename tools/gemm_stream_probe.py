@@ -34,8 +34,9 @@ for (K, N, dual, epi, outbf) in [(512, 512, False, _lib.GEMM_TANH, 1), (512, 512
     ldk = (K + 7) // 8 * 8
     flop = 2.0 * M * N * K * (2 if dual else 1)
     byts = M * ldk * 2 * (2 if dual else 1) + M * N * (2 if outbf else 4) + (M * N * 2 if epi == _lib.GEMM_DTANH else 0)
-    Ab = torch.randint(-16000, 16000, (M * ldk,), dtype=torch.int16, device="cuda")
-    Hb = torch.randint(-16000, 16000, (M * N,), dtype=torch.int16, device="cuda")
+    # finite bf16 operands (random int16 bit patterns hold NaNs, whose payloads need not agree)
+    Ab = (torch.randn(M * ldk, device="cuda") * 0.5).to(torch.bfloat16).view(torch.int16)
+    Hb = (torch.rand(M * N, device="cuda") * 1.8 - 0.9).to(torch.bfloat16).view(torch.int16)
     W = torch.randn(K * N, device="cuda") * 0.05
     Bt = torch.zeros(N * ldk, dtype=torch.int16, device="cuda")
     call("mrl_pack_w_bf16", P(W), K, N, 1, P(Bt), ldk, stream())
