@@ -905,6 +905,208 @@ __global__ __launch_bounds__(256) void gemm_bf16_tn_kernel(GemmTnArgs g) {
     }
 }
 
+// ------------------------------------------------------------------ TN on 256 x 256 tiles
+// The layered VJP's weight gradients at Humanoid scale (C = A^T B over K = 1 M rows,
+// M = N = 512, 64 split-K slabs): the 128 x 128 kernel above re-reads each operand row
+// four times through L2 and stages through registers.  Here a block owns one 256 x 256
+// tile of one slab: 8 waves (4 x 2, 64 x 128 each), 32-row stages of A and B (512-B
+// image rows, 16 KB each) filled by LDS-DMA, four stage buffers with three in flight
+// (the NN big kernel's counted-vmcnt / raw-barrier stream), transposed MFMA operands by
+// ds_read_b64_tr_b16.  Chunk c of image row R sits at position c ^ ((R & 3) << 2): the
+// four rows of a transposing read's 32-lane half land on distinct 64-B bank segments.
+// The four tiles of a slab run on one XCD (A and B chunk rows from HBM once).  Reads are
+// inline asm (the compiler's LDS-DMA alias tracking would drain the DMA in flight).
+// Same per-slab k order as gemm_bf16_tn_kernel: bit-identical slabs.  The ones-row of
+// the bias gradient (ONES) is not a mostly-empty third tile: the blocks of row tile 0
+// issue one more (16 x 16 x 32) MFMA per k-step on their B fragment of column group wm
+// (the eight waves cover the 256 columns), read as a 16 x 16 x 32 operand: a 0 / 1
+// selector A makes its output rows 0 and 1 the column sums of columns 0-15 and 16-31.
+constexpr int TBM = 256, TBN = 256, TSK = 32;  // tile, rows per stage
+constexpr int TSTAGE = (TBM + TBN) * TSK;      // bf16 per stage (A image, then B)
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+
+struct TnPlan {
+  int ntm, ntn, nsplit;
+};
+
+template <bool ONES>
+__global__ __launch_bounds__(512, 2) void gemm_bf16_tn_big_kernel(GemmTnArgs g, TnPlan pl) {
+  __shared__ __attribute__((aligned(16))) bfr_t sb0[TSTAGE];
+  __shared__ __attribute__((aligned(16))) bfr_t sb1[TSTAGE];
+  __shared__ __attribute__((aligned(16))) bfr_t sb2[TSTAGE];
+  __shared__ __attribute__((aligned(16))) bfr_t sb3[TSTAGE];
+  if (g.skip != nullptr && *g.skip != 0) return;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // block -> (slab z, tile): the tiles of a slab on one XCD
+  const int ntile = pl.ntm * pl.ntn;
+  const int xcd = blockIdx.x % 8, y = blockIdx.x / 8;
+  const int z = xcd + 8 * (y / ntile), tile = y % ntile;
+  if (z >= pl.nsplit) return;
+  const int tm = tile / pl.ntn, tn = tile % pl.ntn;
+  const int64_t m0 = (int64_t)tm * TBM, n0 = (int64_t)tn * TBN;
+  const int64_t kbeg = (int64_t)z * g.k_chunk, kend = min(g.K, kbeg + g.k_chunk);
+  const int64_t nst = kend > kbeg ? (kend - kbeg + TSK - 1) / TSK : 0;
+  // DMA: waves 0..3 the A image, 4..7 the B image; instruction i of wave w covers image
+  // rows 8 (w & 3) + 2 i + (lane >> 5), position lane & 31 (chunk pos ^ ((row & 3) << 2))
+  const bool isA = wave < 4;
+  const int pos = lane & 31;
+  auto issue = [&](bfr_t* dst, int64_t st) {
+    const bfr_t* base = isA ? g.A : g.B;
+    const int64_t ld = isA ? g.lda : g.ldb, cols = isA ? g.m_real : g.N, c0 = isA ? m0 : n0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 8 * (wave & 3) + 2 * i + (lane >> 5);
+      const int c = pos ^ ((row & 3) << 2);
+      const int64_t r = kbeg + st * TSK + row, col = c0 + 8 * c;
+      const void* src = (r < kend && col < cols) ? (const void*)(base + r * ld + col) : (const void*)kZero16;
+      glds16b(src, dst + (isA ? 0 : TBM * TSK) + (8 * (wave & 3) + 2 * i) * 256);
+    }
+  };
+  int64_t issued = 0, consumed = 0;
+  auto issue_next = [&](bfr_t* dst) {
+    if (issued < nst) {
+      issue(dst, issued);
+      ++issued;
+    }
+  };
+  // transposing reads (tr_operand's lane map): lane (G = lane >> 4, q, p) reads 8 B at
+  // row 16 ks + 8 (G >> 1) + q (+ 4: the second read) and column c0 + 16 (G & 1) + 4 p
+  const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  auto lane_off = [&](int img_col0, int c0) {  // byte offset in the stage of k-step 0's first read
+    const int col = c0 + 16 * (G & 1) + 4 * p;
+    const int R = 8 * (G >> 1) + q;
+    return (uint32_t)(2 * (img_col0 * TSK) + R * 512 + (((col >> 3) ^ (q << 2)) << 4) + ((col & 7) << 1));
+  };
+  uint32_t offA[2], offB[4];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) offA[mi] = lane_off(0, 64 * wm + 32 * mi);
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) offB[ni] = lane_off(TBM, 128 * wn + 32 * ni);
+  struct Frag {
+    u32x2v a[2][2], b[4][2];  // [tile][lo / hi]
+  };
+  // k-step ks (0 / 1) of a stage: rows 16 ks .. (8 KB apart), hi = +4 rows (2 KB)
+  auto read = [&](const bfr_t* cur, int ks, Frag& f) {
+    const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(cur);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const uint32_t v = base + offA[mi];
+      if (ks == 0) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.a[mi][0]) : "v"(v));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(f.a[mi][1]) : "v"(v));
+      } else {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:8192" : "=v"(f.a[mi][0]) : "v"(v));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:10240" : "=v"(f.a[mi][1]) : "v"(v));
+      }
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const uint32_t v = base + offB[ni];
+      if (ks == 0) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f.b[ni][0]) : "v"(v));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(f.b[ni][1]) : "v"(v));
+      } else {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:8192" : "=v"(f.b[ni][0]) : "v"(v));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:10240" : "=v"(f.b[ni][1]) : "v"(v));
+      }
+    }
+  };
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = zero16();
+  // ONES: the 32-column group wm's B fragment (lane l: column l & 31, k 8 (l >> 5) ..)
+  // as a 16x16x32 B operand is column l & 15 at k-group l >> 4, i.e. k-groups 0 / 2 hold
+  // columns 0-15 and 1 / 3 columns 16-31; selector rows 0 / 1 sum either pair
+  f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+  const bool ones_blk = ONES && tm == 0;
+  bf16x8 sel8;
+  {
+    const int r = lane & 15, kg = lane >> 4;
+    const bool on = (r == 0 && (kg & 1) == 0) || (r == 1 && (kg & 1) == 1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sel8[e] = (__bf16)(on ? 1.0f : 0.0f);
+  }
+  auto op = [](const u32x2v* lohi) {
+    const bf16x4 lo = __builtin_bit_cast(bf16x4, lohi[0]);
+    const bf16x4 hi = __builtin_bit_cast(bf16x4, lohi[1]);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto mfma = [&](const Frag& f) {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = MFMA32B(op(f.a[mi]), op(f.b[ni]), acc[mi][ni]);
+    if (ONES && ones_blk) {  // wave-uniform branches: no copies of the fragment
+      if (wm == 0) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel8, op(f.b[0]), acc1, 0, 0, 0);
+      else if (wm == 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel8, op(f.b[1]), acc1, 0, 0, 0);
+      else if (wm == 2) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel8, op(f.b[2]), acc1, 0, 0, 0);
+      else acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel8, op(f.b[3]), acc1, 0, 0, 0);
+    }
+  };
+#define MRL_TN_FRAG(f)                                                                                      \
+  "+v"(f.a[0][0]), "+v"(f.a[0][1]), "+v"(f.a[1][0]), "+v"(f.a[1][1]), "+v"(f.b[0][0]), "+v"(f.b[0][1]),    \
+      "+v"(f.b[1][0]), "+v"(f.b[1][1]), "+v"(f.b[2][0]), "+v"(f.b[2][1]), "+v"(f.b[3][0]), "+v"(f.b[3][1])
+  Frag f0, f1;
+  // one stage (two k-steps), the NN big kernel's stream: the next stage's DMA has landed
+  // for every wave (at most one more in flight), then the stage after next is issued
+  auto stage = [&](const bfr_t* cur, const bfr_t* next, bfr_t* load) {
+    const int64_t later = issued - consumed - 2;
+    if (later >= 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" : MRL_TN_FRAG(f0)::"memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : MRL_TN_FRAG(f0)::"memory");
+    __builtin_amdgcn_s_barrier();
+    read(cur, 1, f1);
+    mfma(f0);
+    issue_next(load);
+    read(next, 0, f0);
+    asm volatile("s_waitcnt lgkmcnt(12)" : MRL_TN_FRAG(f1)::"memory");
+    mfma(f1);
+    ++consumed;
+  };
+  issue_next(sb0);
+  issue_next(sb1);
+  issue_next(sb2);
+  if (nst > 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    read(sb0, 0, f0);
+  }
+  // nst stages in groups of four (sb0..sb3); a tail stage past nst reads a zero-filled
+  // image?  No: stages past nst are skipped by the guard, their buffers never read.
+  for (int64_t st = 0; st < nst; st += 4) {
+    stage(sb0, sb1, sb3);
+    if (st + 1 < nst) stage(sb1, sb2, sb0);
+    if (st + 2 < nst) stage(sb2, sb3, sb1);
+    if (st + 3 < nst) stage(sb3, sb0, sb2);
+  }
+#undef MRL_TN_FRAG
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  // slab tile: lane j holds column n0 + .. + j, rows cperm(r, h) (gemm_bf16_tn_kernel's)
+  float* C = g.slab + (int64_t)z * g.slab_stride;
+  const int h = lane >> 5, j = lane & 31;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int64_t col = n0 + 128 * wn + 32 * ni + j;
+      if (col >= g.N) continue;
+      const int64_t rbase = m0 + 64 * wm + 32 * mi;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = rbase + cperm(r, h);
+        if (row < g.m_real) C[row * g.ldc + col] = acc[mi][ni][r];
+      }
+    }
+  if (ONES && ones_blk && lane < 16) {  // 16x16 output: lane l holds rows 0..3 of column l
+    const int64_t col = n0 + 128 * wn + 32 * wm + lane;
+    if (col < g.N) C[g.m_real * g.ldc + col] = acc1[0];
+    if (col + 16 < g.N) C[g.m_real * g.ldc + col + 16] = acc1[1];
+  }
+}
+
 // ------------------------------------------------------------------ casts / packs
 // y[r][c] = bf16(x[r][c]) for c < cols, 0 for cols <= c < ldy (zero K padding)
 __global__ void cast_rows_bf16_kernel(const float* __restrict__ x, int64_t rows, int64_t cols, int64_t ldx,
@@ -1089,6 +1291,24 @@ int mrl_gemm_bf16_tn(const mrl_gemm_bf16_tn_desc* d, const int32_t* skip, void* 
   g.ldc = d->ldc;
   g.skip = skip;
   hipStream_t s = (hipStream_t)stream;
+  {
+    // 256 x 256 tiles for the wide layers (m_real, N >= 256; the ones-row rides row tile 0)
+    const char* e = getenv("MRL_GEMM_TN_BIG");
+    const bool big = e ? atoi(e) != 0 : true;
+    if (big && g.m_real >= TBM && g.N >= TBN && g.m_real % 8 == 0 && g.N % 8 == 0) {
+      TnPlan pl;
+      pl.ntm = (int)((g.m_real + TBM - 1) / TBM);
+      pl.ntn = (int)((g.N + TBN - 1) / TBN);
+      pl.nsplit = (int)z;
+      const int ntile = pl.ntm * pl.ntn;
+      const int64_t rounds = (z + 7) / 8;  // slabs per XCD
+      if (g.M > g.m_real)
+        hipLaunchKernelGGL(gemm_bf16_tn_big_kernel<true>, dim3((unsigned)(8 * rounds * ntile)), dim3(512), 0, s, g, pl);
+      else
+        hipLaunchKernelGGL(gemm_bf16_tn_big_kernel<false>, dim3((unsigned)(8 * rounds * ntile)), dim3(512), 0, s, g, pl);
+      return hip_check(hipGetLastError(), "mrl_gemm_bf16_tn");
+    }
+  }
   const unsigned gm = (unsigned)((g.M + QBM - 1) / QBM);
   if (g.N <= 32) hipLaunchKernelGGL((gemm_bf16_tn_kernel<32>), dim3(1, gm, (unsigned)z), dim3(256), 0, s, g);
   else hipLaunchKernelGGL((gemm_bf16_tn_kernel<128>), dim3((unsigned)((g.N + 127) / 128), gm, (unsigned)z), dim3(256), 0,

@@ -340,6 +340,44 @@ def test_bf16_operand_gemm_tn_slabs():
         assert err < 2e-5, (R, din, dout, ones, err)
 
 
+def test_bf16_tn_big_tiles_equal_tiled(monkeypatch):
+    """The 256 x 256 LDS-DMA TN kernel (split-K slabs, transposing reads of swizzled
+    images) writes the same weight-gradient slab rows as the 128 x 128 kernel bit for bit
+    (same per-slab k order); its ones-row (bias gradient: one selector MFMA per k-step in
+    row tile 0's blocks, another summation order) and every row hold the float64 sums.  Ragged rows (slab and stage tails), m / n tails (376 = one full and one
+    partial tile, 300), with and without the ones-row, slab counts 64 and 7."""
+    import ctypes
+
+    from modular_rl_amd import _lib
+    from modular_rl_amd._lib import call, stream
+    rng = np.random.default_rng(8)
+    for (R, din, dout, ones, splits) in [(40000, 512, 512, True, 64), (33333, 376, 512, True, 64),
+                                         (5000, 512, 300, False, 7), (1000, 256, 256, True, 64)]:
+        lda, ldb = (din + 7) // 8 * 8, (dout + 7) // 8 * 8
+        X, G = rng.standard_normal((R, din)), rng.standard_normal((R, dout))
+        dX, dG = _bf16_dev(X, lda), _bf16_dev(G, ldb)
+        M = din + (1 if ones else 0)
+        S = int(_lib.load().mrl_gemm_slab_splits(R, splits))
+        outs = []
+        for big in ("0", "1"):
+            monkeypatch.setenv("MRL_GEMM_TN_BIG", big)
+            slab = torch.full((S * M * dout,), float("nan"), dtype=torch.float32, device="cuda")
+            g = _lib.GemmBf16TnDesc(m=M, n=dout, k=R, a=ctypes.c_void_p(dX.data_ptr()), lda=lda,
+                                    b=ctypes.c_void_p(dG.data_ptr()), ldb=ldb, ones_row=int(ones), splits=splits,
+                                    slab=ctypes.c_void_p(slab.data_ptr()), slab_stride=M * dout, ldc=dout)
+            call("mrl_gemm_bf16_tn", ctypes.byref(g), None, stream())
+            torch.cuda.synchronize()
+            outs.append(slab.view(S, M, dout))
+        assert torch.equal(outs[0][:, :din], outs[1][:, :din]), (R, din, dout)
+        got = outs[1].cpu().numpy().astype(np.float64).sum(0)
+        Xb = bfr(X)
+        if ones:
+            Xb = np.concatenate([Xb, np.ones((R, 1))], axis=1)
+        want = Xb.T @ bfr(G)
+        err = np.abs(got - want).max() / np.abs(want).max()
+        assert err < 2e-5, (R, din, dout, ones, err)
+
+
 @pytest.mark.parametrize("head,nin,nout", [("gauss", 40, 9), ("softmax", 30, 4)])
 def test_bf16_layered_fvp_and_gradient(head, nin, nout):
     """Layered GEMM path (hid 96,80) in bf16: Fisher product and gradient at the bf16 bound."""
