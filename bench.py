@@ -193,7 +193,7 @@ def cpu_baseline(E, Tn, env_id="Hopper-v2", hid=(64, 64), seed=0):
                       f"float32 update / float64 rollout (multiply-adds unfused), {dt:.1f} s"}
 
 
-def rollout_latency_roofline(ki, key, pmc, K):
+def rollout_latency_roofline(ki, key, pmc, K, layered=False):
     """The rollout step is a latency chain (one wave per SIMD, a cross-block hand-off per
     step), bound by neither MFMA nor HBM: its roof is the wave's own instruction issue
     time per step (SQ_ACTIVE_INST_ANY per wave per step from a committed PMC pass,
@@ -219,6 +219,13 @@ def rollout_latency_roofline(ki, key, pmc, K):
            "note": ("latency-bound: one persistent launch runs the T steps, each a filter merge over all envs "
                     "(cross-block hand-off) + the policy forward + fp64 env substeps, one wave per SIMD on E/64 CUs; "
                     "peak = the wave's instruction-issue time per step (PMC), achieved = rollout region / T")}
+    if layered:
+        # the layered (Humanoid) rollout is a chain of launches per step, no persistent kernel
+        out["kernel"] = ("layered rollout step (lrollout_obs, the hidden-layer GEMMs, hm_act_kernel: fused head + "
+                         "wave-per-env fp64 dynamics, lrollout_partials)")
+        out["note"] = ("latency-bound: per step a filter-merge launch, the policy's hidden layers as GEMMs over the "
+                       "E rows, and the env step with one wave per env (hm_act_kernel, the largest part); no issue "
+                       "floor measured for this chain (peak null); achieved = rollout region / T")
     return out
 
 
@@ -360,7 +367,7 @@ def main():
                             "evaluations); achieved = their algorithmic FLOP / their summed HIP-event durations; "
                             "traffic: the Fisher-product launch's PMC bytes")
     if dom == "rollout_step":
-        roofline = rollout_latency_roofline(kinfo[dom], f"{args.env}/{args.dtype}", pmc, K)
+        roofline = rollout_latency_roofline(kinfo[dom], f"{args.env}/{args.dtype}", pmc, K, layered=net.layered)
     gae = None
     if "gae_scan" in kern:
         cnt, mean_ms, _ = kern["gae_scan"]
