@@ -444,6 +444,74 @@ def test_bf16_layered_humanoid_shape():
     assert _rel(g.cpu().numpy(), T.policy_gradient(spec, th, ob, act, adv, oldprob)) < 5e-2
 
 
+def test_bf16_fisher_product_full_c2_size():
+    """C2 at its full size (CartPole net 4-64-64-2, bf16, 4096 x 1024 = 4,194,304 rows):
+    the cached Fisher product against the float64 oracle at the bf16 bound, cached ==
+    uncached, F(2v) == 2 F(v) bit for bit (scaling by 2 is exact through every rounding
+    point) and the symmetry w^T F v = v^T F w (size-independent properties)."""
+    from modular_rl_amd import _lib
+    N = 4096 * 1024
+    head, nin, nout = "softmax", 4, 2
+    rng, spec, th, ob = _setup(head, nin, nout, N, 9)
+    net = _net(head, nin, nout)
+    net.set_flat(th)
+    x = _dev(ob)
+    ghead = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+
+    def fvp(v, cached=True):
+        vt = _dev(v)
+        imgt = torch.zeros_like(net.image)
+        net.pack(theta=vt, image=imgt, fwd_only=True)
+        net.use_cache = cached
+        net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=ghead, tangent=vt, image_t=imgt)
+        fv = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+        net.vjp_flat(x, N, ghead, fv)
+        net.use_cache = True
+        return fv.cpu().numpy().astype(np.float64)
+
+    part = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=_dev(rng.integers(0, nout, N), torch.int32),
+             adv=_dev(rng.standard_normal(N)), oldprob=_dev(T.policy_prob(spec, th, ob)), ghead=torch.zeros_like(ghead),
+             partial=part)  # the recording pass: writes the bf16 activation cache
+    v = rng.standard_normal(spec.P).astype(np.float32).astype(np.float64)
+    w = rng.standard_normal(spec.P).astype(np.float32).astype(np.float64)
+    fv, fw = fvp(v), fvp(w)
+    assert np.array_equal(fvp(2.0 * v), 2.0 * fv)
+    assert _rel(fvp(v, cached=False), fv) < 1e-6
+    a, b = w @ fv, v @ fw
+    assert abs(a - b) <= 1e-3 * max(abs(a), abs(b)), (a, b)
+    want = T.fisher_vector_product(spec, th, v, ob)
+    assert _rel(fv, want) < BF16_ORACLE_RTOL, _rel(fv, want)
+
+
+@pytest.mark.parametrize("env_id", ["CartPole-v0", "Hopper-v2"])
+def test_bf16_persistent_rollout_full_width_equals_step_launches(env_id):
+    """bf16 mode at the C2 / C3 env count (4096 envs = 64 blocks: the full cross-block
+    hand-off of the persistent launch with the bf16 forward): the persistent launch and
+    T step launches give bit-identical trajectories, filter and env state."""
+    from modular_rl_amd.agentzoo import TrpoAgent
+    from modular_rl_amd.envs import make
+    env = make(env_id)
+    cfg = dict(timestep_limit=env.spec.max_episode_steps, n_envs=4096, horizon=24, seed=6, mlp_dtype="bf16")
+    outs = []
+    for persistent in (False, True):
+        # one agent each (the running filter belongs to the agent), same seed and policy
+        agent = TrpoAgent(env.observation_space, env.action_space, cfg)
+        col = agent.make_collector(env, cfg)
+        col.persistent = persistent
+        got = []
+        for _ in range(2):
+            b = col.collect()
+            if persistent:
+                col.check()
+            got += [t.clone() for t in (b.obs, b.act, b.prob, b.rew, b.flags, b.ep_t)]
+        got += [col.filter_state[:col.FS].clone(), col.env_state.clone(), col.env_int.clone(),
+                agent.policy.net.theta.clone()]
+        outs.append(got)
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), i
+
+
 @pytest.mark.parametrize("env_id", ["CartPole-v0", "Hopper-v2"])
 def test_bf16_rollout_prob_rows_equal_update_forward(env_id):
     """bf16 mode: the rollout's fused forward rounds W0, W1, x, h1, h2 like
