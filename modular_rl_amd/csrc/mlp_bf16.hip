@@ -336,7 +336,7 @@ __global__ __launch_bounds__(ROWS_BLOCK_B, 2) void mlp_rows_bf16_kernel(RowsArgs
   for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
     const int64_t row = tile * 32 + (lane & 31);
     const bool valid = row < a.n;
-    XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
+    XGlobalNB xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
     float z[MAX_OUT], dz[MAX_OUT];
     float* ctile = a.cache != nullptr ? a.cache + tile * BCACHE_TILE_WORDS : nullptr;
     bf16x8 h1b[4], h2b[4];
@@ -410,6 +410,8 @@ __device__ inline f32x16 transpose_f(const bf16x8* fr, int mt, const bf16x8* ip)
   return t;
 }
 
+typedef uint32_t vu4 __attribute__((ext_vector_type(4)));  // a 16-B register quad (asm operands)
+
 constexpr int VJP_MAX_BLOCKS_B = 256;  // one block (4 waves) per CU at one wave per SIMD
 
 // SH != 0: a static shape of mlp_layout.h (plain rows), every dimension a constant
@@ -434,6 +436,8 @@ template <bool CACHED, int SH>
 __global__ __launch_bounds__(256, 1) void mlp_vjp_bf16_kernel(VjpArgsB a_in, const float* __restrict__ img_g,
                                                              const int32_t* __restrict__ skip) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  // the staged cache tiles of the next tile pair (PF), 16 KB per wave
+  __shared__ __attribute__((aligned(16))) bf16x8 vjp_stage[(CACHED && SH != 0) ? 4 * 2 * 2 * 4 * 64 : 1];
   if (skip != nullptr && *skip != 0) return;
   const VjpArgsB a = vjp_shape_b<SH>(a_in);
   const MlpDims& d = a.d;
@@ -469,17 +473,114 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_bf16_kernel(VjpArgsB a_in, con
   // all its contributions vanish.
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t stride = (int64_t)gridDim.x * 4;
+  // PF (the cached static-shape kernels, one wave per SIMD): the cache tiles of the next
+  // tile pair are staged by LDS-DMA into this wave's own 16 KB of vjp_stage while this
+  // pair computes (no registers held across the loop, no barrier: a wave reads only what
+  // it staged); read back by inline-asm ds_reads, which the compiler's LDS-DMA alias
+  // tracking cannot turn into vmcnt(0) drains in front of the image reads.
+  constexpr bool PF = CACHED && SH != 0;
+  auto tile_of = [&](int64_t t0, int u) {
+    const int64_t tu = t0 + u * stride;
+    return tu < ntiles ? tu : ntiles - 1;
+  };
+  bf16x8* const stg = vjp_stage + wave * (2 * 2 * 4 * 64);  // [u][layer][s][lane]
+  auto dma_pair = [&](int64_t t0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(a.cache + tile_of(t0, u) * BCACHE_TILE_WORDS);
+#pragma unroll
+      for (int f = 0; f < 8; ++f)  // f = layer * 4 + s
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + f * 64 + lane),
+                                         (__attribute__((address_space(3))) void*)(stg + (u * 8 + f) * 64), 16, 0, 0);
+    }
+  };
+  // the pair's input and head rows: every load unconditional from a clamped address
+  // (static n_obs / A / n_sum), issued together one pair ahead, validity applied as 0 / 1
+  // factors at use (a select on a loaded value becomes a branch and a vmcnt(0) drain)
+  float xr[2][8 * MAX_KS0B], gr_[2][8], glr[2][MAX_OUT];
+  auto load_rows = [&](int64_t t0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t row = tile_of(t0, u) * 32 + j32;
+      const int64_t rc = row < a.n ? row : 0;
+      const float* xp = a.x + rc * a.n_obs;
+#pragma unroll
+      for (int s0 = 0; s0 < MAX_KS0B; ++s0)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const int k = 16 * s0 + 8 * h + jj;
+          xr[u][8 * s0 + jj] = s0 < b.KS0B ? xp[k < a.n_obs ? k : a.n_obs - 1] : 0.f;
+        }
+      const float* gp = a.ghead + rc * a.gh;
+#pragma unroll
+      for (int o = 0; o < 8; ++o) gr_[u][o] = gp[o < A ? o : A - 1];
+#pragma unroll
+      for (int q = 0; q < MAX_OUT; ++q) glr[u][q] = q < a.n_sum ? gp[A + q] : 0.f;
+    }
+  };
+  if constexpr (PF) {
+    const int64_t t0 = (int64_t)blockIdx.x * 4 + wave;
+    if (t0 < ntiles) {
+      load_rows(t0);
+      dma_pair(t0);
+    }
+  }
   for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += 2 * stride) {
     bf16x8 h1b[2][4], h2b[2][4], gB[2], xb[2][MAX_KS0B];
     bool live[2];
+    if constexpr (PF) {
+      // this pair's staged tiles: own DMA landed -> registers -> the next pair's DMA
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(stg) + 16 * lane;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int sI = 0; sI < 4; ++sI) {
+          vu4 v1, v2;
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v1) : "v"(base), "i"(((u * 8 + sI) * 64) * 16));
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v2) : "v"(base), "i"(((u * 8 + 4 + sI) * 64) * 16));
+          h1b[u][sI] = __builtin_bit_cast(bf16x8, v1);
+          h2b[u][sI] = __builtin_bit_cast(bf16x8, v2);
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(h1b[0][0]), "+v"(h1b[0][1]), "+v"(h1b[0][2]), "+v"(h1b[0][3]),
+                   "+v"(h1b[1][0]), "+v"(h1b[1][1]), "+v"(h1b[1][2]), "+v"(h1b[1][3]), "+v"(h2b[0][0]),
+                   "+v"(h2b[0][1]), "+v"(h2b[0][2]), "+v"(h2b[0][3]), "+v"(h2b[1][0]), "+v"(h2b[1][1]),
+                   "+v"(h2b[1][2]), "+v"(h2b[1][3])::"memory");
+    }
+    if constexpr (PF) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t tu = tile + u * stride;
+        live[u] = tu < ntiles;
+        const int64_t row = (live[u] ? tu : ntiles - 1) * 32 + j32;
+        float fv = (live[u] && row < a.n && h == 0) ? 1.f : 0.f, fx = row < a.n ? 1.f : 0.f;
+        asm volatile("" : "+v"(fv), "+v"(fx));
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+          const float g = o < A ? gr_[u][o] * fv : 0.f;
+          gb2[o] += g;
+          gB[u][o] = (__bf16)g;
+        }
+#pragma unroll
+        for (int q = 0; q < MAX_OUT; ++q) gls[q] += q < a.n_sum ? glr[u][q] * fv : 0.f;
+#pragma unroll
+        for (int s0 = 0; s0 < MAX_KS0B; ++s0)
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            const int k = 16 * s0 + 8 * h + jj;
+            xb[u][s0][jj] = (__bf16)((s0 < b.KS0B && k < a.n_obs) ? xr[u][8 * s0 + jj] * fx : 0.f);
+          }
+      }
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
+      if constexpr (PF) break;
       const int64_t tu = tile + u * stride;
       live[u] = tu < ntiles;
       const int64_t tc = live[u] ? tu : ntiles - 1;
       const int64_t row = tc * 32 + j32;
       const bool valid = live[u] && row < a.n;
-      XGlobal xl{a.x, a.ept, a.ts_limit, a.n_obs, row, row < a.n};
+      XGlobalNB xl{a.x, a.ept, a.ts_limit, a.n_obs, row, row < a.n};
       if constexpr (CACHED) {
         bcache_load(a.cache + tc * BCACHE_TILE_WORDS, 1, lane, h2b[u]);
         bcache_load(a.cache + tc * BCACHE_TILE_WORDS, 0, lane, h1b[u]);
@@ -499,6 +600,12 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_bf16_kernel(VjpArgsB a_in, con
       }
 #pragma unroll
       for (int q = 0; q < MAX_OUT; ++q) gls[q] += (valid && h == 0 && q < a.n_sum) ? gr[A + q] : 0.f;
+    }
+    if constexpr (PF) {  // the next pair's rows and cache tiles, under this pair's MFMAs
+      if (tile + 2 * stride < ntiles) {
+        load_rows(tile + 2 * stride);
+        dma_pair(tile + 2 * stride);
+      }
     }
     // gh2 = W2 . G (F layout), ga2 = gh2 (1 - h2^2)
     bf16x8 ga2b[2][4];

@@ -55,6 +55,28 @@ struct XGlobal {
   }
 };
 
+// XGlobal with branch-free column reads (the bf16 kernels): columns past n_obs read the
+// last one and, like rows past the batch, are zeroed by an opaque 0 / 1 factor -- k
+// depends on the lane, and a select on the loaded value became a branch around the load
+// and a vmcnt(0) drain per column.  (The fp32 row kernels keep XGlobal: this form spilled
+// there.)
+struct XGlobalNB {
+  const float* x;
+  const int32_t* ept;
+  double ts_limit;
+  int n_obs;
+  int64_t row;
+  bool valid;
+  __device__ inline float operator()(int k) const {
+    const int64_t r = valid ? row : 0;
+    float f = (valid && k < n_obs) ? 1.f : 0.f;
+    asm volatile("" : "+v"(f));
+    float v = x[r * n_obs + (k < n_obs ? k : n_obs - 1)] * f;
+    if (ept != nullptr && k == n_obs) v = valid ? (float)((double)ept[r] / ts_limit) : 0.f;
+    return v;
+  }
+};
+
 template <class XL>
 __device__ inline void layer0(const float* lds, const MlpDims& d, const XL& xl, int lane, f32x16* acc) {
   const int h = lane >> 5;

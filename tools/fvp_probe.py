@@ -61,8 +61,13 @@ def main():
 
     lib = os.environ.get("MRL_LIB_PATH", "default")
     surrgrad()
-    print(f"[{os.path.basename(lib)} {nin},{nout},{hname}] surrgrad {timed(surrgrad):.3f} ms  fvp_jvp_rows {timed(jvp):.3f} ms  "
-          f"vjp {timed(vjp):.3f} ms  prob {timed(prob_pass):.3f} ms", flush=True)
+    print(f"[{os.path.basename(lib)} {net.dtype} {nin},{nout},{hname}] surrgrad {timed(surrgrad):.3f} ms  "
+          f"fvp_jvp_rows {timed(jvp):.3f} ms  vjp {timed(vjp):.3f} ms  prob {timed(prob_pass):.3f} ms", flush=True)
+    # the same Fisher-product pair recomputing the primal activations (no cache reads)
+    net.use_cache = False
+    print(f"[{os.path.basename(lib)} {net.dtype} {nin},{nout},{hname}] uncached: fvp_jvp_rows {timed(jvp):.3f} ms  "
+          f"vjp {timed(vjp):.3f} ms", flush=True)
+    net.use_cache = True
 
 
 if __name__ == "__main__":
