@@ -253,9 +253,10 @@ int mrl_colsum(const float* g, int64_t m, int64_t n, int64_t ldg, int32_t splits
 int mrl_head_rows(int32_t head, int32_t n_out, int32_t epilogue, const float* z, const float* dz,
                   const float* logstd, const float* dlogstd, const mrl_rows_io* io, const int32_t* skip,
                   void* stream);
-/* X[N, n_obs+1] = [obs, ep_t/timestep_limit]  (value-net input, core.py:659-660) */
+/* X[N, n_obs+1] = [obs, ep_t/timestep_limit]  (value-net input, core.py:659-660);
+ * max_blocks > 0 caps the grid (a copy run beside other work), 0: the whole device */
 int mrl_concat_time(const float* obs, const int32_t* ep_t, int64_t n, int32_t n_obs, double timestep_limit,
-                    float* x, void* stream);
+                    float* x, int32_t max_blocks, void* stream);
 
 /* ---------------------------------------------------------------- conjugate gradient
  * Device-resident Demmel CG on flat fp64 vectors (trpo.py:165-200).

@@ -105,7 +105,7 @@ SIGNATURES = {
     "mrl_pack_w_bf16": (i32, [vp, i64, i64, i32, vp, i64, vp]),
     "mrl_colsum": (i32, [vp, i64, i64, i64, i32, vp, i64, vp, vp]),
     "mrl_head_rows": (i32, [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
-    "mrl_concat_time": (i32, [vp, vp, i64, i32, f64, vp, vp]),
+    "mrl_concat_time": (i32, [vp, vp, i64, i32, f64, vp, i32, vp]),
     "mrl_cg_state_doubles": (i64, [i64]),
     "mrl_cg_init": (i32, [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_cg_update": (i32, [vp, f64, f64, i64, vp, vp, vp, vp, vp, vp, vp, vp]),

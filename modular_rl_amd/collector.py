@@ -91,7 +91,7 @@ class Batch:
         self.obs, self.act, self.prob, self.rew, self.flags, self.ep_t = obs, act, prob, rew, flags, ep_t
         self.T, self.E = T, E
         self.adv = self.ret = self.vpred = None
-        self.vf_x = None  # (VF features tensor, NnVf feature generation) set by NnVf.predict_batch
+        self.vf_x = None  # (VF features, NnVf feature generation, ready event or None) set by NnVf.predict_batch
         self.episode = None
 
     @staticmethod

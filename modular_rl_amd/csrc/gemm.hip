@@ -317,13 +317,15 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ G
 }
 
 // X = [obs, ep_t / limit] for the value net's time feature (core.py:659-660)
+template <typename I>
 __global__ void concat_time_kernel(const float* __restrict__ obs, const int32_t* __restrict__ ept, int64_t n, int O,
                                    double limit, float* __restrict__ X) {
-  const int64_t total = n * (O + 1);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / (O + 1);
-    const int c = (int)(i % (O + 1));
-    X[i] = c < O ? obs[r * O + c] : (float)((double)ept[r] / limit);
+  // I: 32-bit element indices when the output fits (the row / column split is one
+  // 32-bit division instead of a 64-bit one per element)
+  const I total = (I)(n * (O + 1)), w = (I)(O + 1);
+  for (I i = (I)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (I)gridDim.x * blockDim.x) {
+    const I r = i / w, c = i - r * w;
+    X[i] = c < (I)O ? obs[(int64_t)r * O + c] : (float)((double)ept[r] / limit);
   }
 }
 
@@ -556,13 +558,20 @@ int mrl_colsum(const float* g, int64_t m, int64_t n, int64_t ldg, int32_t splits
 }
 
 int mrl_concat_time(const float* obs, const int32_t* ep_t, int64_t n, int32_t n_obs, double timestep_limit, float* X,
-                    void* stream) {
+                    int32_t max_blocks, void* stream) {
   if (!obs || !ep_t || !X) return fail(E_ARG, "null pointer");
+  if (n_obs < 0 || max_blocks < 0) return fail(E_ARG, "bad n_obs / max_blocks");
   if (n <= 0) return OK;
-  int64_t g = (n * (n_obs + 1) + 255) / 256;
-  if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(concat_time_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, ep_t, n, n_obs,
-                     timestep_limit, X);
+  const int64_t total = n * (n_obs + 1);
+  int64_t g = (total + 255) / 256;
+  const int64_t cap = max_blocks > 0 ? max_blocks : 4096;
+  if (g > cap) g = cap;
+  if (total + (int64_t)g * 256 < (int64_t)INT32_MAX)
+    hipLaunchKernelGGL(concat_time_kernel<uint32_t>, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, ep_t, n, n_obs,
+                       timestep_limit, X);
+  else
+    hipLaunchKernelGGL(concat_time_kernel<int64_t>, dim3(g), dim3(256), 0, (hipStream_t)stream, obs, ep_t, n, n_obs,
+                       timestep_limit, X);
   return hip_check(hipGetLastError(), "mrl_concat_time");
 }
 

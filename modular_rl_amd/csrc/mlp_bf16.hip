@@ -287,17 +287,19 @@ constexpr int ROWS_BLOCK_B = 256;
 constexpr int ROWS_MAX_BLOCKS_B = 3072;
 constexpr int EPI_FVP_CACHED_B = 100;
 
-// the kernel arguments with a static shape's dimensions substituted (SH == 0: run time)
+// the kernel arguments with a static shape's dimensions substituted (SH == 0: run time;
+// SH | SH_TIME keeps ep_t for the time-feature column)
 template <int SH>
 __device__ inline void rows_shape_b(RowsArgs& a, BDims& b) {
-  if constexpr (SH != 0) {
-    constexpr StaticShape S = STATIC_SHAPES[SH];
-    a.d = static_dims(SH);
+  if constexpr ((SH & ~SH_TIME) != 0) {
+    constexpr int B = SH & ~SH_TIME;
+    constexpr StaticShape S = STATIC_SHAPES[B];
+    a.d = static_dims(B);
     a.A = S.A;
     a.head = S.head;
-    a.n_obs = S.O;
+    a.n_obs = (SH & SH_TIME) ? S.O - 1 : S.O;
     a.gh = S.head == MRL_HEAD_GAUSS ? 2 * S.A : S.A;
-    a.ept = nullptr;
+    if constexpr (!(SH & SH_TIME)) a.ept = nullptr;
     b = bf16_dims(S.O, S.A);
   }
 }
@@ -886,6 +888,11 @@ int mrl_mlp_rows_bf16(const mrl_mlp_desc* d, int32_t epi, const float* theta, co
   if (!io->ep_t)
     for (int i = 1; i < N_STATIC_SHAPES; ++i)
       if (STATIC_SHAPES[i].O == d->n_in && STATIC_SHAPES[i].A == d->n_out && STATIC_SHAPES[i].head == d->head) sh = i;
+  // the value nets' prediction pass reads the time feature from ep_t (SH_TIME variants)
+  int sht = 0;
+  if (io->ep_t && epi == MRL_EPI_PROB && d->head == MRL_HEAD_LINEAR)
+    for (int i = 3; i <= 4; ++i)
+      if (STATIC_SHAPES[i].O == d->n_in && STATIC_SHAPES[i].A == d->n_out) sht = i | SH_TIME;
   const bool pol = sh == 1 || sh == 2, vf = sh == 3 || sh == 4;
 #define MRL_ROWSB(EK, OK)                                                                                          \
   do {                                                                                                             \
@@ -896,7 +903,11 @@ int mrl_mlp_rows_bf16(const mrl_mlp_desc* d, int32_t epi, const float* theta, co
     else hipLaunchKernelGGL((mlp_rows_bf16_kernel<EK, 0>), grid, blk, shm, s, a, b, image, image_t, skip);               \
   } while (0)
   switch (epi) {
-    case MRL_EPI_PROB: MRL_ROWSB(MRL_EPI_PROB, true); break;
+    case MRL_EPI_PROB:
+      if (sht == (3 | SH_TIME)) hipLaunchKernelGGL((mlp_rows_bf16_kernel<MRL_EPI_PROB, 3 | SH_TIME>), grid, blk, shm, s, a, b, image, image_t, skip);
+      else if (sht == (4 | SH_TIME)) hipLaunchKernelGGL((mlp_rows_bf16_kernel<MRL_EPI_PROB, 4 | SH_TIME>), grid, blk, shm, s, a, b, image, image_t, skip);
+      else MRL_ROWSB(MRL_EPI_PROB, true);
+      break;
     case MRL_EPI_LOSSES: MRL_ROWSB(MRL_EPI_LOSSES, pol); break;
     case MRL_EPI_SURRGRAD: MRL_ROWSB(MRL_EPI_SURRGRAD, pol); break;
     case MRL_EPI_VFLOSS: MRL_ROWSB(MRL_EPI_VFLOSS, vf); break;

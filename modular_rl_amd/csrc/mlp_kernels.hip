@@ -60,18 +60,20 @@ static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 constexpr int EPI_FVP_CACHED = 100;  // internal: MRL_EPI_FVP reading the activation cache
 
 // the kernel arguments with a static shape's dimensions substituted (compile-time
-// constants after inlining); SH == 0 leaves the run-time shape
+// constants after inlining); SH == 0 leaves the run-time shape; SH | SH_TIME (mlp_layout.h)
+// keeps ep_t for the time-feature column
 template <int SH>
 __device__ inline RowsArgs rows_shape(const RowsArgs& in) {
   RowsArgs a = in;
-  if constexpr (SH != 0) {
-    constexpr StaticShape S = STATIC_SHAPES[SH];
-    a.d = static_dims(SH);
+  if constexpr ((SH & ~SH_TIME) != 0) {
+    constexpr int B = SH & ~SH_TIME;
+    constexpr StaticShape S = STATIC_SHAPES[B];
+    a.d = static_dims(B);
     a.A = S.A;
     a.head = S.head;
-    a.n_obs = S.O;
+    a.n_obs = (SH & SH_TIME) ? S.O - 1 : S.O;
     a.gh = S.head == MRL_HEAD_GAUSS ? 2 * S.A : S.A;
-    a.ept = nullptr;
+    if constexpr (!(SH & SH_TIME)) a.ept = nullptr;
   }
   return a;
 }
@@ -1121,16 +1123,21 @@ static int check_desc(const mrl_mlp_desc* d) {
 static MlpDims dims_of(const mrl_mlp_desc* d) { return mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS); }
 
 // the static shape (mlp_layout.h) a launch matches, or 0: plain rows only (a time
-// feature column built from ep_t takes the generic kernels)
-static int static_shape_of(const mrl_mlp_desc* d, bool has_ept) {
+// feature column built from ep_t takes the generic kernels, except the value nets'
+// prediction pass: time_ok, SH_TIME variants)
+static int static_shape_of(const mrl_mlp_desc* d, bool has_ept, bool time_ok = false) {
 #ifdef MRL_NO_STATIC_SHAPES
   (void)d;
   (void)has_ept;
+  (void)time_ok;
   return 0;
 #else
-  if (has_ept) return 0;
+  if (has_ept && !time_ok) return 0;
   for (int i = 1; i < N_STATIC_SHAPES; ++i)
-    if (STATIC_SHAPES[i].O == d->n_in && STATIC_SHAPES[i].A == d->n_out && STATIC_SHAPES[i].head == d->head) return i;
+    if (STATIC_SHAPES[i].O == d->n_in && STATIC_SHAPES[i].A == d->n_out && STATIC_SHAPES[i].head == d->head) {
+      if (!has_ept) return i;
+      return STATIC_SHAPES[i].head == MRL_HEAD_LINEAR ? (i | SH_TIME) : 0;
+    }
   return 0;
 #endif
 }
@@ -1254,7 +1261,7 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
   const int64_t blocks = rows_blocks(io->n, io->partial != nullptr ? desc_cus(d) : 256);
   size_t shm = (size_t)a.d.fwd_size * 4 * (epi == MRL_EPI_FVP ? 2 : 1);
   hipStream_t s = (hipStream_t)stream;
-  const int sh = static_shape_of(d, io->ep_t != nullptr);
+  const int sh = static_shape_of(d, io->ep_t != nullptr, epi == MRL_EPI_PROB);
   const bool pol = sh == 1 || sh == 2, vf = sh == 3 || sh == 4;
   const dim3 grid(epi == MRL_EPI_PPOSGD ? 1 : blocks), blk(ROWS_BLOCK);
 #define MRL_ROWS_LAUNCH(EK, OK)                                                                                     \
@@ -1266,7 +1273,11 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
     else hipLaunchKernelGGL((mlp_rows_kernel<EK, 0>), grid, blk, shm, s, a, image, image_t, skip);                  \
   } while (0)
   switch (epi) {
-    case MRL_EPI_PROB: MRL_ROWS_LAUNCH(MRL_EPI_PROB, true); break;
+    case MRL_EPI_PROB:
+      if (sh == (3 | SH_TIME)) hipLaunchKernelGGL((mlp_rows_kernel<MRL_EPI_PROB, 3 | SH_TIME>), grid, blk, shm, s, a, image, image_t, skip);
+      else if (sh == (4 | SH_TIME)) hipLaunchKernelGGL((mlp_rows_kernel<MRL_EPI_PROB, 4 | SH_TIME>), grid, blk, shm, s, a, image, image_t, skip);
+      else MRL_ROWS_LAUNCH(MRL_EPI_PROB, true);
+      break;
     case MRL_EPI_LOSSES: MRL_ROWS_LAUNCH(MRL_EPI_LOSSES, pol); break;
     case MRL_EPI_SURRGRAD: MRL_ROWS_LAUNCH(MRL_EPI_SURRGRAD, pol); break;
     case MRL_EPI_VFLOSS: MRL_ROWS_LAUNCH(MRL_EPI_VFLOSS, vf); break;

@@ -76,6 +76,10 @@ constexpr StaticShape STATIC_SHAPES[N_STATIC_SHAPES] = {
     {12, 1, MRL_HEAD_LINEAR},  // Hopper-v2 value net ([obs, t / limit])
     {5, 1, MRL_HEAD_LINEAR},   // CartPole-v0 value net
 };
+// SH | SH_TIME: a value-net shape whose last input column is the time feature
+// ep_t / limit, read beside O - 1 observation columns (the prediction pass straight
+// from the rollout's rows, no materialised [obs, t] copy)
+constexpr int SH_TIME = 8;
 __host__ __device__ constexpr MlpDims static_dims(int sh) {
   return mlp_dims(STATIC_SHAPES[sh].O, STATIC_SHAPES[sh].A, STATIC_SHAPES[sh].head == MRL_HEAD_GAUSS);
 }

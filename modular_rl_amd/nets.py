@@ -300,7 +300,7 @@ class LayeredMlpNet:
         if ep_t is None:
             return x, self.n_in
         X = self.ws.get(name, n * self.n_in, torch.float32)
-        call("mrl_concat_time", ptr(x), ptr(ep_t), int(n), self.n_in - 1, float(timestep_limit), ptr(X), stream())
+        call("mrl_concat_time", ptr(x), ptr(ep_t), int(n), self.n_in - 1, float(timestep_limit), ptr(X), 0, stream())
         return X, self.n_in
 
     def _forward(self, X, ldx, n, theta, bufs, zbuf, skip=None):

@@ -236,7 +236,19 @@ class TrpoUpdater:
             comm.allreduce_(fv)
             ops.cg_update(fv, damping, self.RESIDUAL_TOL)
         step = ops.trpo_step(g, max_kl)[:4]
-        host = torch.cat([step, sums.double()[:3], g.abs().max().double().reshape(1), ops.state[:3]]).cpu().numpy()
+        # the first line-search batch (k = 0, accepted in most updates) is issued before
+        # the readback and returns in the same copy: one host round trip instead of two
+        # (a zero gradient discards it unread)
+        first = None
+        parts = [step, sums.double()[:3], g.abs().max().double().reshape(1), ops.state[:3]]
+        if self.LS_BATCHES:
+            K0 = min(self.LS_BATCHES[0], self.MAX_BACKTRACKS)
+            ls_sums, ls_cand = ops.losses_batch(thprev, 0, K0)
+            comm.allreduce_(ls_sums)
+            parts.append(ls_sums.reshape(-1))
+        host = torch.cat(parts).cpu().numpy()
+        if self.LS_BATCHES:
+            first = (host[11:].reshape(K0, -1), ls_cand)
         losses_before = _losses(host[4:7], n_glob)
         losses_after = losses_before
         if host[7] <= 1e-8:
@@ -251,7 +263,8 @@ class TrpoUpdater:
             fval = losses_before[0]
             trace = []
             if self.LS_BATCHES:
-                success, frac, k, laux, accepted = self._linesearch_batched(thprev, fval, rate, n_glob, trace)
+                success, frac, k, laux, accepted = self._linesearch_batched(thprev, fval, rate, n_glob, trace,
+                                                                            first=first)
             else:
                 def f(stepfrac):
                     l = _losses(self._candidate_losses(thprev, stepfrac), n_glob)
@@ -275,19 +288,23 @@ class TrpoUpdater:
             out[lname + "_after"] = lafter
         return out
 
-    def _linesearch_batched(self, thprev, fval, rate, n_glob, trace, accept_ratio=.1):
+    def _linesearch_batched(self, thprev, fval, rate, n_glob, trace, accept_ratio=.1, first=None):
         """`trpo.py:143-159` with the candidates scored in batches (LS_BATCHES): each batch
         is one device call, one all-reduce of its [K, 4] sums and one readback; the
         accept test runs in the reference's order, so the first accepted k (and the
-        trace up to it) equal the serial loop's."""
+        trace up to it) equal the serial loop's.  ``first``: the first batch's (host
+        sums, device candidates), already evaluated."""
         k0 = 0
         for K in self.LS_BATCHES:
             K = min(K, self.MAX_BACKTRACKS - k0)
             if K <= 0:
                 break
-            sums, cand = self.ops.losses_batch(thprev, k0, K)
-            self.comm.allreduce_(sums)
-            host = sums.cpu().numpy()
+            if k0 == 0 and first is not None:
+                host, cand = first
+            else:
+                sums, cand = self.ops.losses_batch(thprev, k0, K)
+                self.comm.allreduce_(sums)
+                host = sums.cpu().numpy()
             for j in range(K):
                 k = k0 + j
                 stepfrac = .5 ** k

@@ -70,12 +70,12 @@ class OracleOps:
             return
         rdotr = float(self.state[0])
         z = fv + damping * self.p
-        v = rdotr / float(self.p.dot(z))
+        v = np.float64(rdotr) / np.float64(self.p.dot(z))  # 0 / 0 = NaN like the device (zero gradient)
         self.x += v * self.p
         self.ax += v * z
         self.r -= v * z
         newr = float(self.r.dot(self.r))
-        self.p.copy_(self.r + (newr / rdotr) * self.p)
+        self.p.copy_(self.r + float(np.float64(newr) / np.float64(rdotr)) * self.p)
         self.p32.copy_(self.p)
         self.state[0] = newr
         self.state[2] += 1

@@ -380,3 +380,33 @@ def test_episode_stats_matches_oracle(Tn, E):
     np.testing.assert_allclose(np.sqrt(max(sr2 / cnt - (sr / cnt) ** 2, 0.0)), st["EpisodeRewards"].std(), rtol=1e-6)
     np.testing.assert_allclose(mr, st["EpRewMax"], rtol=1e-12)
     assert sl / cnt == st["EpLenMean"] and ml == st["EpLenMax"] and sl == st["EpisodeLengths"].sum()
+
+
+@pytest.mark.parametrize("O,dtype,N", [(11, "fp32", 70001), (4, "fp32", 4099), (11, "bf16", 70001), (4, "bf16", 33)])
+def test_vf_predict_time_feature_equals_materialised_rows(O, dtype, N):
+    """The value nets' prediction straight from the rollout's rows (the SH_TIME static
+    shapes: time feature ep_t / limit derived per row) equals the prediction on the
+    materialised [obs, t / limit] rows bit for bit, and the oracle at 1e-5."""
+    from modular_rl_amd import _lib
+    from modular_rl_amd._lib import call, ptr, stream
+    from modular_rl_amd.nets import MlpNet
+    rng = np.random.default_rng(O * 10 + N)
+    spec = T.Spec(O + 1, [64, 64], 1, "linear")
+    th = (T.mlp_init(rng, spec.shapes, False) + 0.05 * rng.standard_normal(spec.P)).astype(np.float32)
+    net = MlpNet(O + 1, 1, _lib.HEAD_LINEAR, dtype=dtype)
+    net.set_flat(th)
+    limit = 1000.0
+    obs = _dev(rng.standard_normal((N, O)))
+    ep_t = _dev(rng.integers(0, 1000, N), torch.int32)
+    y_t = net.forward(obs, N, ep_t=ep_t, timestep_limit=limit)
+    X = torch.empty(N * (O + 1), dtype=torch.float32, device="cuda")
+    call("mrl_concat_time", ptr(obs), ptr(ep_t), N, O, limit, ptr(X), 0, stream())
+    X3 = torch.full_like(X, float("nan"))
+    call("mrl_concat_time", ptr(obs), ptr(ep_t), N, O, limit, ptr(X3), 3, stream())  # a 3-block grid
+    assert torch.equal(X, X3)
+    y_x = net.forward(X, N)
+    assert torch.equal(y_t, y_x)
+    if dtype == "fp32":
+        Xh = X.cpu().numpy().reshape(N, O + 1).astype(np.float64)
+        want = T.mlp_forward(spec, th.astype(np.float64), Xh)[0].reshape(-1)
+        np.testing.assert_allclose(y_t.cpu().numpy(), want, rtol=1e-5, atol=1e-5)
