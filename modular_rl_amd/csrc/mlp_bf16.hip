@@ -304,8 +304,21 @@ __device__ inline void rows_shape_b(RowsArgs& a, BDims& b) {
   }
 }
 
+// waves per SIMD the row kernels are compiled for: 3 (168 VGPRs) for the cached FVP pass
+// of the static shapes -- it waits on memory for half its wave time and a third wave
+// hides some of it (CartPole 0.313 -> 0.265 ms, Hopper 0.353 -> 0.286 ms at 4.19 M
+// rows; Hopper's spills 16 bytes a lane) -- 2 for the others (the loss / gradient passes
+// measured level or slower at 3; the run-time shape and the uncached FVP pass spill)
+#ifndef MRL_ROWS_B_OCC3
+#define MRL_ROWS_B_OCC3 1
+#endif
 template <int EPI_K, int SH>
-__global__ __launch_bounds__(ROWS_BLOCK_B, 2) void mlp_rows_bf16_kernel(RowsArgs a, BDims b,
+constexpr int rows_b_occ() {
+  return (MRL_ROWS_B_OCC3 && (SH & ~SH_TIME) != 0 && EPI_K == EPI_FVP_CACHED_B) ? 3 : 2;
+}
+
+template <int EPI_K, int SH>
+__global__ __launch_bounds__(ROWS_BLOCK_B, (rows_b_occ<EPI_K, SH>())) void mlp_rows_bf16_kernel(RowsArgs a, BDims b,
                                                                        const float* __restrict__ img_g,
                                                                        const float* __restrict__ imt_g,
                                                                        const int32_t* __restrict__ skip) {
