@@ -312,8 +312,15 @@ __device__ inline void rows_shape_b(RowsArgs& a, BDims& b) {
 #ifndef MRL_ROWS_B_OCC3
 #define MRL_ROWS_B_OCC3 1
 #endif
+// MRL_ROWS_B_OCC4=1: the PROB / LOSSES / SURRGRAD passes of the static shapes at 4 waves
+// (48-64 bytes a lane spilled).  Measured and not kept (tools/occ4_ab.sh): SURRGRAD
+// 0.47 -> 0.50 ms (CartPole), 0.52 -> 0.58 ms (Hopper); PROB level
+#ifndef MRL_ROWS_B_OCC4
+#define MRL_ROWS_B_OCC4 0
+#endif
 template <int EPI_K, int SH>
 constexpr int rows_b_occ() {
+  if (MRL_ROWS_B_OCC4 && (SH & ~SH_TIME) != 0 && EPI_K <= MRL_EPI_SURRGRAD) return 4;
   return (MRL_ROWS_B_OCC3 && (SH & ~SH_TIME) != 0 && EPI_K == EPI_FVP_CACHED_B) ? 3 : 2;
 }
 
