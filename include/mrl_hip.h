@@ -94,6 +94,10 @@ typedef struct {
   int32_t reverse_kl;      /* kl[new, old] instead of kl[old, new] (PpoLbfgs)     */
   int32_t cache_mode;      /* MRL_CACHE_* (fused path; act_cache NULL = no cache) */
   float* act_cache;        /* [mrl_act_cache_floats(n)] primal h1/h2 of theta     */
+  float* feat_out;         /* MRL_EPI_PROB with ep_t only, else NULL: the rows the
+                            * pass reads, [N, n_obs + 1] = [x, ep_t / timestep_limit]
+                            * (NnVf.preproc, core.py:659-660), written beside the
+                            * values for the VF fit -- bitwise mrl_concat_time's X   */
 } mrl_rows_io;
 
 /* Primal activation cache of the fused path: the forward of one theta is shared by

@@ -40,7 +40,7 @@ class RowsIO(ctypes.Structure):
     _fields_ = [("x", vp), ("ep_t", vp), ("timestep_limit", f64), ("n", i64), ("inv_n_global", f64),
                 ("act", vp), ("adv", vp), ("oldprob", vp), ("target", vp), ("out", vp), ("ghead", vp),
                 ("partial", vp), ("kl_coeff", f64), ("kl_cutoff", f64), ("cutoff_coeff", f64), ("reverse_kl", i32),
-                ("cache_mode", i32), ("act_cache", vp)]
+                ("cache_mode", i32), ("act_cache", vp), ("feat_out", vp)]
 
 
 class GemmDesc(ctypes.Structure):

@@ -91,7 +91,7 @@ class Batch:
         self.obs, self.act, self.prob, self.rew, self.flags, self.ep_t = obs, act, prob, rew, flags, ep_t
         self.T, self.E = T, E
         self.adv = self.ret = self.vpred = None
-        self.vf_x = None  # (VF features, NnVf feature generation, ready event or None) set by NnVf.predict_batch
+        self.vf_x = None  # (VF features, NnVf feature generation) set by NnVf.predict_batch
         self.episode = None
 
     @staticmethod
@@ -328,10 +328,18 @@ class Collector:
             raise _lib.MrlError(self.ABORT_MSG)
 
     def finish(self):
-        """Cross-rank filter merge (waits for the rollout) and the iteration's Batch."""
+        """Cross-rank filter merge (waits for the rollout) and the iteration's Batch.  The
+        batch carries the device abort status, which the policy update reads back with its
+        step scalars before it touches theta."""
         if self.comm.enabled:
+            # the merge synchronises on the rollout anyway: an aborted rollout must not
+            # merge its partial filter deltas into every rank's filter
+            self.check()
             self._merge_filter_across_ranks(self._fs_start)
-        return Batch(self.N, self.obs, self.act, self.prob, self.rew, self.flags, self.ep_t, T=self.T, E=self.E)
+        b = Batch(self.N, self.obs, self.act, self.prob, self.rew, self.flags, self.ep_t, T=self.T, E=self.E)
+        if not self.layered and self.persistent:
+            b.abort, b.abort_msg = self.status, self.ABORT_MSG
+        return b
 
     # ------------------------------------------------------------ filter state
     def _merge_filter_across_ranks(self, fs_start):

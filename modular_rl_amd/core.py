@@ -232,11 +232,6 @@ class IterationRunner:
                 # serialise the fit behind it
                 self.main_stream = torch.cuda.Stream()
                 self.pipeline = True
-                # the VF features of each batch are built on the fit stream beside the
-                # value prediction (NnVf.predict_batch); no extra stream: the box runs 4
-                # hardware queues per process and a fifth would share one
-                if hasattr(getattr(agent, "baseline", None), "side_stream"):
-                    agent.baseline.side_stream = self.fit_stream
 
     @staticmethod
     def _stats(ep, vf_stats, pol_stats):
@@ -295,11 +290,6 @@ class IterationRunner:
         ev["upd0"] = self._event()
         pol_stats = agent.updater.update(batch)
         ev["upd1"] = self._event()
-        vf_x = getattr(batch, "vf_x", None)
-        if vf_x is not None and vf_x[2] is not None:
-            # the VF features were built from this batch's rows on the fit stream: the next
-            # rollout (ordered after this stream) must not overwrite the rows before
-            main.wait_event(vf_x[2])
         if self.pipeline:
             # read back with the deferred VF fit's stats (no host sync here); the state at
             # the end of this iteration (the VF after its fit is added then) is captured

@@ -495,6 +495,7 @@ int mrl_head_rows(int32_t head, int32_t n_out, int32_t epi, const float* z, cons
   if (n_out < 1 || n_out > MRL_LAYERED_MAX_OUT) return fail(E_UNSUPPORTED, "n_out must be in [1, 32]");
   if (head == MRL_HEAD_LINEAR && n_out != 1) return fail(E_ARG, "linear head needs n_out=1");
   if (head == MRL_HEAD_GAUSS && !logstd) return fail(E_ARG, "DiagGauss needs logstd");
+  if (io->feat_out) return fail(E_ARG, "mrl_head_rows: no feat_out (the layered path materialises X itself)");
   switch (epi) {
     case MRL_EPI_PROB:
       if (!io->out) return fail(E_ARG, "EPI_PROB needs out");

@@ -392,6 +392,8 @@ __global__ __launch_bounds__(ROWS_BLOCK_B, (rows_b_occ<EPI_K, SH>())) void mlp_r
       if (valid && h == 0) row_epilogue<MRL_EPI_PPOGRAD, MAX_OUT>(c, row, z, dz, ls, sd, dls, d0, d1, d2);
       continue;
     } else {
+      if constexpr (EPI == MRL_EPI_PROB)
+        if (a.feat != nullptr && valid) write_feature_row(a, row, h, xl);
       if (!valid || h != 0) continue;
       row_epilogue<EPI, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
     }
@@ -868,6 +870,9 @@ int mrl_mlp_rows_bf16(const mrl_mlp_desc* d, int32_t epi, const float* theta, co
   a.reverse_kl = io->reverse_kl;
   a.cache = io->act_cache;
   a.cache_mode = io->act_cache != nullptr ? io->cache_mode : 0;
+  a.feat = io->feat_out;
+  if (a.feat != nullptr && (epi != MRL_EPI_PROB || io->ep_t == nullptr))
+    return fail(E_ARG, "feat_out is for MRL_EPI_PROB with ep_t (the value prediction)");
   if (a.cache_mode == MRL_CACHE_READ && epi != MRL_EPI_FVP) return fail(E_ARG, "MRL_CACHE_READ is for MRL_EPI_FVP");
   if (a.cache_mode == MRL_CACHE_WRITE && (epi == MRL_EPI_FVP || epi == MRL_EPI_PPOSGD))
     return fail(E_ARG, "MRL_CACHE_WRITE is for the plain forward epilogues");

@@ -134,6 +134,8 @@ __global__ __launch_bounds__(ROWS_BLOCK, 3) void mlp_rows_kernel(RowsArgs a_in, 
       if (valid && h == 0) row_epilogue<MRL_EPI_PPOGRAD, MAX_OUT>(b, row, z, dz, ls, sd, dls, d0, d1, d2);
       continue;
     } else {
+      if constexpr (EPI == MRL_EPI_PROB)
+        if (a.feat != nullptr && valid) write_feature_row(a, row, h, xl);
       if (!valid || h != 0) continue;
       row_epilogue<EPI, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
     }
@@ -1227,6 +1229,9 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
   a.reverse_kl = io->reverse_kl;
   a.cache = io->act_cache;
   a.cache_mode = io->act_cache != nullptr ? io->cache_mode : 0;
+  a.feat = io->feat_out;
+  if (a.feat != nullptr && (epi != MRL_EPI_PROB || io->ep_t == nullptr))
+    return fail(E_ARG, "feat_out is for MRL_EPI_PROB with ep_t (the value prediction)");
   if (a.cache_mode == MRL_CACHE_READ && epi != MRL_EPI_FVP) return fail(E_ARG, "MRL_CACHE_READ is for MRL_EPI_FVP");
   if (a.cache_mode == MRL_CACHE_WRITE && (epi == MRL_EPI_FVP || epi == MRL_EPI_PPOSGD))
     return fail(E_ARG, "MRL_CACHE_WRITE is for the plain forward epilogues");
@@ -1405,7 +1410,8 @@ int mrl_linesearch_eval(const mrl_mlp_desc* pol, int32_t compute, const float* t
   const bool bf = compute == MRL_COMPUTE_BF16;
   const int64_t P = mrl_mlp_num_params(pol);
   const int64_t img = bf ? mrl_mlp_image_words_bf16(pol) : mrl_mlp_image_floats(pol);
-  const int64_t prow = bf ? mrl_partial_rows_bf16(io->n) : mrl_partial_rows(io->n);
+  // the LOSSES pass sizes its grid (and so its partial rows) by the desc's CU count
+  const int64_t prow = bf ? mrl_mlp_partial_rows_bf16(pol, io->n) : mrl_mlp_partial_rows(pol, io->n);
   if (image_stride < img || partial_stride < prow * 4) return fail(E_ARG, "mrl_linesearch_eval: strides too small");
   rc = mrl_linesearch_candidates(theta_old, fullstep, k0, K, P, cand, stream);
   for (int32_t k = 0; k < K && rc == OK; ++k) {

@@ -31,7 +31,18 @@ struct RowsArgs {
   int reverse_kl;        // kl[new, old] instead of kl[old, new]
   float* cache;          // primal activation cache (fused path) or nullptr
   int cache_mode;        // MRL_CACHE_WRITE: the forward stores h1/h2; MRL_CACHE_READ: FVP reads them
+  float* feat;           // EPI_PROB with ep_t: the input rows [obs, t / limit] written beside the values
 };
+
+// [obs, t / timestep_limit] of one row (the VF fit's materialised features, core.py:659-660)
+// written by the value prediction that reads them anyway: lane half h writes columns
+// h, h + 2, ... of the row both halves of a 32-row tile hold
+template <class XL>
+__device__ __forceinline__ void write_feature_row(const RowsArgs& a, int64_t row, int h, const XL& xl) {
+  const int w = a.n_obs + 1;
+  float* f = a.feat + row * w;
+  for (int k = h; k < w; k += 2) f[k] = xl(k);
+}
 
 constexpr float LOG2PI_F = 1.8378770664093453f;
 constexpr float LOG2PIE_F = 2.8378770664093453f;

@@ -145,7 +145,7 @@ class MlpNet:
     # ---- fused passes
     def rows(self, epi, x, n, ep_t=None, timestep_limit=1.0, inv_n_global=1.0, act=None, adv=None, oldprob=None,
              target=None, out=None, ghead=None, partial=None, theta=None, image=None, tangent=None, image_t=None,
-             skip=None, kl_coeff=0.0, kl_cutoff=0.0, cutoff_coeff=0.0, reverse_kl=0):
+             skip=None, kl_coeff=0.0, kl_cutoff=0.0, cutoff_coeff=0.0, reverse_kl=0, feat_out=None):
         own = (theta is None or theta is self.theta) and (image is None or image is self.image)
         theta = self.theta if theta is None else theta
         image = self.image if image is None else image
@@ -159,7 +159,7 @@ class MlpNet:
                 mode, cache = _lib.CACHE_READ, self._cache(n)
         io = _lib.RowsIO(ptr(x), ptr(ep_t), float(timestep_limit), int(n), float(inv_n_global), ptr(act), ptr(adv),
                          ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial), float(kl_coeff),
-                         float(kl_cutoff), float(cutoff_coeff), int(reverse_kl), mode, ptr(cache))
+                         float(kl_cutoff), float(cutoff_coeff), int(reverse_kl), mode, ptr(cache), ptr(feat_out))
         call("mrl_mlp_rows" + self._sfx, ctypes.byref(self.desc), int(epi), ptr(theta), ptr(image), ptr(tangent),
              ptr(image_t), ctypes.byref(io), ptr(skip), stream())
 
@@ -203,12 +203,13 @@ class MlpNet:
         call("mrl_reduce_rows_f64", ptr(partial), rows, 4, ptr(out), None, stream())
         return out
 
-    def forward(self, x, n, ep_t=None, timestep_limit=1.0, out=None):
-        """prob rows (policy) or values (VF) for n rows of x."""
+    def forward(self, x, n, ep_t=None, timestep_limit=1.0, out=None, feat_out=None):
+        """prob rows (policy) or values (VF) for n rows of x.  feat_out (value nets, with
+        ep_t): [n, n_in] receives the input rows [x, t / limit] the pass derives anyway."""
         width = 1 if self.head == _lib.HEAD_LINEAR else self.gh
         if out is None:
             out = torch.empty((int(n), width) if width > 1 else (int(n),), dtype=torch.float32, device=self.device)
-        self.rows(_lib.EPI_PROB, x, n, ep_t=ep_t, timestep_limit=timestep_limit, out=out)
+        self.rows(_lib.EPI_PROB, x, n, ep_t=ep_t, timestep_limit=timestep_limit, out=out, feat_out=feat_out)
         return out
 
 
@@ -295,11 +296,12 @@ class LayeredMlpNet:
                           splits=splits, slab_stride=slab_stride, compute=self.compute)
         call("mrl_gemm", ctypes.byref(g), ptr(skip), stream())
 
-    def _input(self, x, n, ep_t, timestep_limit, name="x_time"):
-        """(X, ldx): obs rows, or [obs, t/limit] materialised for a value net."""
+    def _input(self, x, n, ep_t, timestep_limit, name="x_time", out=None):
+        """(X, ldx): obs rows, or [obs, t/limit] materialised for a value net (into
+        ``out`` when given)."""
         if ep_t is None:
             return x, self.n_in
-        X = self.ws.get(name, n * self.n_in, torch.float32)
+        X = self.ws.get(name, n * self.n_in, torch.float32) if out is None else out
         call("mrl_concat_time", ptr(x), ptr(ep_t), int(n), self.n_in - 1, float(timestep_limit), ptr(X), 0, stream())
         return X, self.n_in
 
@@ -389,8 +391,10 @@ class LayeredMlpNet:
 
     def rows(self, epi, x, n, ep_t=None, timestep_limit=1.0, inv_n_global=1.0, act=None, adv=None, oldprob=None,
              target=None, out=None, ghead=None, partial=None, theta=None, image=None, tangent=None, image_t=None,
-             skip=None, kl_coeff=0.0, kl_cutoff=0.0, cutoff_coeff=0.0, reverse_kl=0):
+             skip=None, kl_coeff=0.0, kl_cutoff=0.0, cutoff_coeff=0.0, reverse_kl=0, feat_out=None):
         n = int(n)
+        if feat_out is not None and (epi != _lib.EPI_PROB or ep_t is None):
+            raise MrlError("feat_out is for the value prediction (EPI_PROB with ep_t)")
         theta = self.theta if theta is None else theta
         io = _lib.RowsIO(ptr(x), ptr(ep_t), float(timestep_limit), n, float(inv_n_global), ptr(act), ptr(adv),
                          ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial), float(kl_coeff),
@@ -410,7 +414,7 @@ class LayeredMlpNet:
         else:
             if n == 0:
                 return
-            X, ldx = self._input(x, n, ep_t, timestep_limit)
+            X, ldx = self._input(x, n, ep_t, timestep_limit, out=feat_out)
             Z = self.ws.get("fwd_z", n * self.n_out, torch.float32)
             if self.tape_bf16:
                 Xb, ldxb = self._cast_rows(X, n, self.n_in, ldx, "fwd_xb")
@@ -575,9 +579,9 @@ class LayeredMlpNet:
         hb = [bufs[l % 2] for l in range(len(self.hid_sizes))]
         self._forward(x, self.n_in, int(n), self.theta, hb, z)
 
-    def forward(self, x, n, ep_t=None, timestep_limit=1.0, out=None):
+    def forward(self, x, n, ep_t=None, timestep_limit=1.0, out=None, feat_out=None):
         width = 1 if self.head == _lib.HEAD_LINEAR else self.gh
         if out is None:
             out = torch.empty((int(n), width) if width > 1 else (int(n),), dtype=torch.float32, device=self.device)
-        self.rows(_lib.EPI_PROB, x, n, ep_t=ep_t, timestep_limit=timestep_limit, out=out)
+        self.rows(_lib.EPI_PROB, x, n, ep_t=ep_t, timestep_limit=timestep_limit, out=out, feat_out=feat_out)
         return out

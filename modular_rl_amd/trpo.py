@@ -241,14 +241,24 @@ class TrpoUpdater:
         # (a zero gradient discards it unread)
         first = None
         parts = [step, sums.double()[:3], g.abs().max().double().reshape(1), ops.state[:3]]
+        # the rollout's abort status (a persistent launch that gave up: incomplete rows)
+        # rides in the same copy, so an aborted batch never reaches theta
+        abort = getattr(batch, "abort", None)
+        if abort is not None:
+            abort = abort.double().reshape(1)
+            comm.allreduce_(abort)  # any rank's abort stops every rank
+            parts.append(abort)
         if self.LS_BATCHES:
             K0 = min(self.LS_BATCHES[0], self.MAX_BACKTRACKS)
             ls_sums, ls_cand = ops.losses_batch(thprev, 0, K0)
             comm.allreduce_(ls_sums)
             parts.append(ls_sums.reshape(-1))
         host = torch.cat(parts).cpu().numpy()
+        if abort is not None and host[11] != 0:
+            raise _lib.MrlError("policy update on an aborted rollout: " + getattr(batch, "abort_msg", ""))
         if self.LS_BATCHES:
-            first = (host[11:].reshape(K0, -1), ls_cand)
+            o = 11 + (abort is not None)
+            first = (host[o:].reshape(K0, -1), ls_cand)
         losses_before = _losses(host[4:7], n_glob)
         losses_after = losses_before
         if host[7] <= 1e-8:
@@ -294,11 +304,12 @@ class TrpoUpdater:
         accept test runs in the reference's order, so the first accepted k (and the
         trace up to it) equal the serial loop's.  ``first``: the first batch's (host
         sums, device candidates), already evaluated."""
-        k0 = 0
-        for K in self.LS_BATCHES:
-            K = min(K, self.MAX_BACKTRACKS - k0)
-            if K <= 0:
-                break
+        k0, bi = 0, 0
+        while k0 < self.MAX_BACKTRACKS:
+            # the batch sizes in order, the last one repeated until every backtrack of the
+            # serial loop has been scored
+            K = min(self.LS_BATCHES[min(bi, len(self.LS_BATCHES) - 1)], self.MAX_BACKTRACKS - k0)
+            bi += 1
             if k0 == 0 and first is not None:
                 host, cand = first
             else:

@@ -9,7 +9,6 @@ the host, while every loss+gradient evaluation is one fused forward pass
 (``mrl_mlp_rows`` VFLOSS) + one VJP (``mrl_mlp_vjp``) on the GPU, all-reduced over
 ranks in data-parallel mode.
 """
-import os
 from collections import OrderedDict
 
 import numpy as np
@@ -127,8 +126,8 @@ class NnRegression:
         self.opt = LbfgsOptimizer(net, maxiter=maxiter, comm=self.comm)
         self.moments = DeviceMoments(net.device, self.comm)
 
-    def predict(self, x, n, ep_t=None, timestep_limit=1.0, out=None):
-        return self.net.forward(x, n, ep_t=ep_t, timestep_limit=timestep_limit, out=out)
+    def predict(self, x, n, ep_t=None, timestep_limit=1.0, out=None, feat_out=None):
+        return self.net.forward(x, n, ep_t=ep_t, timestep_limit=timestep_limit, out=out, feat_out=feat_out)
 
     def fit(self, x, n, ytarg, ep_t=None, timestep_limit=1.0, ypredold=None):
         """ytarg: [n] device returns. ypredold: V_old predictions if already computed
@@ -163,7 +162,6 @@ class NnVf:
         self.reg = NnRegression(net, comm=comm, **regression_params)
         self.timestep_limit = timestep_limit
         self._feat_gen = 0
-        self.side_stream = None  # set by the pipelined IterationRunner (its fit stream)
 
     @property
     def net(self):
@@ -178,51 +176,35 @@ class NnVf:
         ep_t = torch.arange(n, dtype=torch.int32, device=self.net.device)
         return self.reg.predict(ob, n, ep_t, self.timestep_limit).cpu().numpy().astype(np.float64)
 
-    # grid cap of the features copy beside the prediction (0: the fit stream's whole CU
-    # set).  Measured on one box, Hopper fp32: the full grid finishes inside the
-    # prediction (34.99 / 35.52 ms per iteration); 64 blocks trickle on for 3.6 ms into
-    # the policy update and slow it by 0.4 ms (35.48 / 35.59)
-    SIDE_COPY_BLOCKS = int(os.environ.get("MRL_VF_SIDE_COPY_BLOCKS", "0"))
+    def _features_buf(self, n):
+        self._feat_gen += 1
+        return self.net.ws.get("vf_features", int(n) * self.net.n_in, torch.float32)
 
-    def features(self, obs, n, ep_t, max_blocks=0):
+    def features(self, obs, n, ep_t):
         """X = [obs, t / timestep_limit] materialised once per batch (`core.py:659-660`):
         every VF pass of the fit then reads plain rows instead of re-deriving the time
         feature per tile."""
         n = int(n)
-        self._feat_gen += 1
-        X = self.net.ws.get("vf_features", n * self.net.n_in, torch.float32)
-        call("mrl_concat_time", ptr(obs), ptr(ep_t), n, self.net.n_in - 1, float(self.timestep_limit), ptr(X),
-             int(max_blocks), stream())
+        X = self._features_buf(n)
+        call("mrl_concat_time", ptr(obs), ptr(ep_t), n, self.net.n_in - 1, float(self.timestep_limit), ptr(X), 0,
+             stream())
         return X
 
     def predict_batch(self, batch, out=None):
         """V_old of the batch (`core.py:70`) straight from the rollout's rows, the time
-        feature derived per row (the value nets' static-shape SH_TIME pass).  The fit's
-        materialised features: on ``side_stream`` when the pipelined loop set one (its
-        fit stream: idle here, on the CUs the rollout does not use), concurrent with the
-        prediction and off the path from the rollout to the policy update; else after
-        the prediction on the current stream."""
-        side = self.side_stream if batch.obs.is_cuda else None
-        ev = None
-        if side is not None:
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                X = self.features(batch.obs, batch.n, batch.ep_t, max_blocks=self.SIDE_COPY_BLOCKS)
-                ev = torch.cuda.Event()
-                ev.record()
-        y = self.reg.predict(batch.obs, batch.n, batch.ep_t, self.timestep_limit, out=out)
-        if side is None:
-            X = self.features(batch.obs, batch.n, batch.ep_t)
+        feature derived per row; the same pass writes the rows it derived, [obs, t /
+        limit], as the fit's materialised features (``feat_out``: no separate copy, all
+        on the caller's stream, so nothing reads the rollout's rows after this returns)."""
+        X = self._features_buf(batch.n)
+        y = self.reg.predict(batch.obs, batch.n, batch.ep_t, self.timestep_limit, out=out, feat_out=X)
         # the fit of this batch reuses the features while no other batch's have replaced them
-        batch.vf_x = (X, self._feat_gen, ev)
+        batch.vf_x = (X, self._feat_gen)
         return y
 
     def fit_batch(self, batch):
         cached = getattr(batch, "vf_x", None)
         if cached is not None and cached[1] == self._feat_gen:
             X = cached[0]
-            if cached[2] is not None:
-                torch.cuda.current_stream().wait_event(cached[2])
         else:
             X = self.features(batch.obs, batch.n, batch.ep_t)
         return self.reg.fit(X, batch.n, batch.ret, None, 1.0, ypredold=batch.vpred)

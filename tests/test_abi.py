@@ -50,6 +50,7 @@ int main(void) {
          sizeof(mrl_gemm_desc));
   P(mrl_gemm_desc, ones_row) P(mrl_gemm_desc, epilogue) P(mrl_gemm_desc, ldh) P(mrl_gemm_desc, slab_stride)
   P(mrl_rows_io, timestep_limit) P(mrl_rows_io, n) P(mrl_rows_io, inv_n_global) P(mrl_rows_io, partial)
+  P(mrl_rows_io, act_cache) P(mrl_rows_io, feat_out)
   P(mrl_rollout_desc, seed) P(mrl_rollout_bufs, noise)
   printf("mrl_gemm_bf16_desc %zu\\nmrl_gemm_bf16_tn_desc %zu\\n", sizeof(mrl_gemm_bf16_desc),
          sizeof(mrl_gemm_bf16_tn_desc));
@@ -69,6 +70,8 @@ int main(void) {
     assert int(out["mrl_rows_io.n"]) == _lib.RowsIO.n.offset
     assert int(out["mrl_rows_io.inv_n_global"]) == _lib.RowsIO.inv_n_global.offset
     assert int(out["mrl_rows_io.partial"]) == _lib.RowsIO.partial.offset
+    assert int(out["mrl_rows_io.act_cache"]) == _lib.RowsIO.act_cache.offset
+    assert int(out["mrl_rows_io.feat_out"]) == _lib.RowsIO.feat_out.offset
     assert int(out["mrl_rollout_desc.seed"]) == _lib.RolloutDesc.seed.offset
     assert int(out["mrl_rollout_bufs.noise"]) == _lib.RolloutBufs.noise.offset
     assert int(out["mrl_gemm_desc"]) == ctypes.sizeof(_lib.GemmDesc)

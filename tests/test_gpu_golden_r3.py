@@ -28,13 +28,13 @@ def _dev(a, dtype=torch.float32):
     return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).cuda()
 
 
-def _update(d, tag, nin, hid, nout, head):
+def _update(d, tag, nin, hid, nout, head, dtype="fp32"):
     from modular_rl_amd import _lib
     from modular_rl_amd.collector import Batch
     from modular_rl_amd.core import Categorical, DiagGauss, StochPolicyMLP
     from modular_rl_amd.nets import make_net
     from modular_rl_amd.trpo import TrpoUpdater
-    net = make_net(nin, nout, _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX, hid)
+    net = make_net(nin, nout, _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX, hid, dtype=dtype)
     th0 = d[f"{tag}_theta0"]
     assert np.array_equal(th0.astype(np.float32).astype(np.float64), th0)
     net.set_flat(th0)
@@ -169,6 +169,30 @@ def test_batched_linesearch_equals_serial(fname, tag, monkeypatch):
         out.append((th1, stats, dg))
     (ta, sa, da), (tb, sb, db) = out
     assert da["k"] == db["k"] == int(d[f"{tag}_k"])
+    np.testing.assert_array_equal(ta, tb)
+    np.testing.assert_array_equal(da["ls"], db["ls"])
+    assert [sa[k] for k in STAT_KEYS] == [sb[k] for k in STAT_KEYS]
+
+
+@pytest.mark.parametrize("tag", ["gauss2", "cat2", "gauss1"])
+@pytest.mark.parametrize("batches", [(1, 3, 6), (1, 2)])
+def test_batched_linesearch_equals_serial_bf16(tag, batches, monkeypatch):
+    """The bf16 branch of mrl_linesearch_eval (bf16 forward images of the K candidates,
+    bf16 LOSSES passes into strided partial rows; the default on the bf16 C2 / C3 lines)
+    against the serial one-candidate loop: the same k, theta bit for bit and the same
+    backtrack trace.  (1, 2): batch sizes that do not sum to MAX_BACKTRACKS -- the last
+    size repeats until every backtrack has been scored, as the serial loop would."""
+    from modular_rl_amd.trpo import TrpoUpdater
+    d = np.load(os.path.join(G, "trpo_update.npz"))
+    head = "gauss" if "gauss" in tag else "softmax"
+    nin, nout = (11, 3) if head == "gauss" else (4, 2)
+    out = []
+    for b in (batches, None):
+        monkeypatch.setattr(TrpoUpdater, "LS_BATCHES", b)
+        _, th1, stats, dg = _update(d, tag, nin, [64, 64], nout, head, dtype="bf16")
+        out.append((th1, stats, dg))
+    (ta, sa, da), (tb, sb, db) = out
+    assert da["k"] == db["k"]
     np.testing.assert_array_equal(ta, tb)
     np.testing.assert_array_equal(da["ls"], db["ls"])
     assert [sa[k] for k in STAT_KEYS] == [sb[k] for k in STAT_KEYS]

@@ -382,7 +382,8 @@ def test_episode_stats_matches_oracle(Tn, E):
     assert sl / cnt == st["EpLenMean"] and ml == st["EpLenMax"] and sl == st["EpisodeLengths"].sum()
 
 
-@pytest.mark.parametrize("O,dtype,N", [(11, "fp32", 70001), (4, "fp32", 4099), (11, "bf16", 70001), (4, "bf16", 33)])
+@pytest.mark.parametrize("O,dtype,N", [(11, "fp32", 70001), (4, "fp32", 4099), (11, "bf16", 70001), (4, "bf16", 33),
+                                     (7, "fp32", 1001), (7, "bf16", 1001)])
 def test_vf_predict_time_feature_equals_materialised_rows(O, dtype, N):
     """The value nets' prediction straight from the rollout's rows (the SH_TIME static
     shapes: time feature ep_t / limit derived per row) equals the prediction on the
@@ -406,6 +407,11 @@ def test_vf_predict_time_feature_equals_materialised_rows(O, dtype, N):
     assert torch.equal(X, X3)
     y_x = net.forward(X, N)
     assert torch.equal(y_t, y_x)
+    # the prediction writes the features it derives (feat_out): bitwise the copy's X
+    F = torch.full_like(X, float("nan"))
+    y_f = net.forward(obs, N, ep_t=ep_t, timestep_limit=limit, feat_out=F)
+    assert torch.equal(y_f, y_t)
+    assert torch.equal(F, X)
     if dtype == "fp32":
         Xh = X.cpu().numpy().reshape(N, O + 1).astype(np.float64)
         want = T.mlp_forward(spec, th.astype(np.float64), Xh)[0].reshape(-1)

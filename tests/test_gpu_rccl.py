@@ -122,12 +122,14 @@ def test_persistent_abort_raises_in_the_iteration(pipeline):
     """64 persistent blocks forced onto 2 CUs (debug flag past the residency check):
     the resident blocks give up after their bounded polls, the rest exit on the abort
     word, and IterationRunner.step() raises MrlError instead of reporting the
-    iteration (pipelined: when the iteration's stats are read, one step later)."""
+    iteration: the policy update reads the status back with its step scalars and raises
+    before it touches theta."""
     from modular_rl_amd import streams
     from modular_rl_amd._lib import MrlError
     runner, col = _runner(pipeline=pipeline)
     col.force_persistent = True
     two = streams.masked_stream([0, 1])
+    theta0 = runner.agent.policy.net.theta.clone()
     with pytest.raises(MrlError, match="resident"):
         if pipeline:
             assert runner.pipeline
@@ -139,5 +141,8 @@ def test_persistent_abort_raises_in_the_iteration(pipeline):
                 runner.step()
     torch.cuda.synchronize()
     assert int(col.status.item()) != 0
+    # the update read the abort status back with its step scalars: the policy never
+    # consumed the incomplete trajectories
+    assert torch.equal(runner.agent.policy.net.theta, theta0)
     with pytest.raises(MrlError, match="resident"):
         col.check()
