@@ -84,7 +84,10 @@ DYNAMICS = {"Hopper-v2": "hopper.xml articulated-body dynamics", "Humanoid-v2": 
             "CartPole-v0": "gym equations"}
 GAE_BYTES_PER_ROW = 17  # read r 4 + v 4 + flags 1, write adv 4 + ret 4
 PMC_FILE = "pmc_r03.json"
-ROLLOUT_ISSUE_FILE = "rollout_issue_r03.json"  # tools/rollout_issue.py: SQ issue cycles per rollout step
+GEMM_PMC_FILE = "pmc_gemm_r04.json"  # tools/pmc_traffic.py --gemm: HBM bytes per layered GEMM launch
+# SQ issue cycles per rollout step (tools/rollout_issue.py: persistent kernel; tools/step_issue.py: the
+# layered Humanoid step's launch chain), newest first: the first file holding the line's key is used
+ROLLOUT_ISSUE_FILES = ("rollout_issue_r04.json", "rollout_issue_r03.json")
 CLOCK_GHZ = 2.4  # MI355X max shader clock (MI355X_MICROARCH.md)
 
 
@@ -105,8 +108,20 @@ def host_info():
         blas = max([p.get("num_threads", 1) for p in threadpool_info()] or [1])
     except Exception:  # pragma: no cover
         blas = None
-    return {"os_cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_model": model,
-            "torch_threads": torch.get_num_threads(), "blas_threads": blas}
+    aff = os.sched_getaffinity(0)
+    cores = set()
+    for c in aff:  # physical cores of the affinity set (SMT siblings share one)
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                cores.add(f.read().strip())
+        except OSError:
+            cores.add(str(c))
+    return {"os_cpu_count": os.cpu_count(), "affinity_cpus": len(aff), "affinity_physical_cores": len(cores),
+            "cpu_model": model, "torch_threads": torch.get_num_threads(), "blas_threads": blas,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "threads_note": "the GPU box gives each one-GPU job a 16-CPU share of the host (OMP_NUM_THREADS=16, set "
+                            "by the harness, which asks jobs to keep their pools to that share); the affinity set "
+                            "lists the whole host, so the baseline uses the share, not every physical core"}
 
 
 def cpu_serial_c1(seconds=8.0, seed=0):
@@ -200,11 +215,15 @@ def rollout_latency_roofline(ki, key, pmc, K, layered=False):
     tools/rollout_issue.py) at the 2.4 GHz clock.  achieved = the live step time,
     frac = issue floor / achieved."""
     us = ki["mean_ms"] * 1e3
-    issue = {}
-    path = os.path.join(ROOT, "profiles", ROLLOUT_ISSUE_FILE)
-    if os.path.exists(path):
-        with open(path) as f:
-            issue = json.load(f).get(key, {})
+    issue, src = {}, None
+    for fn in ROLLOUT_ISSUE_FILES:
+        path = os.path.join(ROOT, "profiles", fn)
+        if os.path.exists(path):
+            with open(path) as f:
+                issue = json.load(f).get(key, {})
+            if issue:
+                src = fn
+                break
     floor = issue["issue_cycles_per_step"] / (CLOCK_GHZ * 1e3) if issue else None
     out = {"bound": "latency", "achieved": round(us, 3), "peak": round(floor, 3) if floor else None, "unit": "us/step",
            "frac": round(floor / us, 4) if floor else None,
@@ -212,7 +231,7 @@ def rollout_latency_roofline(ki, key, pmc, K, layered=False):
            "kernel": "rollout_persistent_kernel (per step)", "cycles_per_step_at_2.4GHz": round(us * CLOCK_GHZ * 1e3),
            "issue_cycles_per_step": round(issue["issue_cycles_per_step"]) if issue else None,
            "valu_insts_per_step": round(issue["valu_insts_per_step"]) if issue else None,
-           "issue_source": f"profiles/{ROLLOUT_ISSUE_FILE}[{key}] (rocprofv3 SQ pass)" if issue else None,
+           "issue_source": f"profiles/{src}[{key}] (rocprofv3 SQ pass)" if issue else None,
            "mean_launch_ms": round(ki["mean_ms"], 5), "launches_timed": ki["launches"],
            "ms_per_iter": round(ki["total_ms"] / K, 3),
            "mfma_frac_of_forward": round(ki["frac_mfma"], 5),
@@ -224,9 +243,67 @@ def rollout_latency_roofline(ki, key, pmc, K, layered=False):
         out["kernel"] = ("layered rollout step (lrollout_obs, the hidden-layer GEMMs, hm_act_kernel: fused head + "
                          "wave-per-env fp64 dynamics, lrollout_partials)")
         out["note"] = ("latency-bound: per step a filter-merge launch, the policy's hidden layers as GEMMs over the "
-                       "E rows, and the env step with one wave per env (hm_act_kernel, the largest part); no issue "
-                       "floor measured for this chain (peak null); achieved = rollout region / T")
+                       "E rows, and the env step with one wave per env (hm_act_kernel, the largest part); peak = the "
+                       "sum over the step's launches of one wave's instruction-issue time (SQ pass over the rollout, "
+                       "tools/step_issue.py); achieved = rollout region / T")
+        if issue.get("kernels"):
+            out["issue_per_kernel_us"] = {k: round(v["per_step"] * v["issue_cycles_per_wave"] / (CLOCK_GHZ * 1e3), 3)
+                                          for k, v in issue["kernels"].items()}
     return out
+
+
+def policy_gemm_roofline(kern, kinfo, net, dtype, n_rows, K, pmc, gemm_pmc):
+    """north_star's "MFMA roofline for the policy GEMM" (agentzoo.py:34-37 Dense layers):
+    the policy MLP's largest GEMM binary by device time per iteration -- on the fused
+    64-wide path the Fisher-product kernels (each a whole forward-mode / reverse-mode MLP
+    pass of K = 64 GEMMs on MFMA), on the layered path the largest of the individually
+    timed GEMM launches -- its algorithmic FLOP / mean HIP-event launch time / the dtype's
+    dense MFMA peak, and the PMC traffic / algorithmic bytes ratio where a pass measured it."""
+    peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_FP32_TFLOPS
+    if not net.layered:
+        cands = {k: v for k, v in kinfo.items() if k in ("fvp_jvp_rows",) + tuple(VJP_BINARY.values())}
+        if not cands:
+            return None
+        name = max(cands, key=lambda k: cands[k]["total_ms"])
+        ki = cands[name]
+        role = "fvp_vjp" if name in VJP_BINARY.values() else name
+        alg = ki.get("bytes_per_row", 0) * ki["rows_per_launch"]
+        traffic = pmc.get(role, {}).get("hbm_bytes_per_launch")
+        return {"bound": "mfma", "achieved": round(ki["tflops"], 3), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ki["tflops"] / peak, 4), "traffic": traffic,
+                "traffic_over_algorithmic": round(traffic / alg, 3) if traffic and alg else None,
+                "algorithmic_bytes": alg or None,
+                "kernel": "mlp_rows_kernel (JVP + KL metric)" if name == "fvp_jvp_rows" else name,
+                "flop_per_row": ki["flop_per_row"], "rows_per_launch": ki["rows_per_launch"],
+                "mean_launch_ms": round(ki["mean_ms"], 5), "launches_timed": ki["launches"],
+                "ms_per_iter": round(ki["total_ms"] / K, 3),
+                "note": "fused 64-wide policy MLP: each Fisher-product / gradient pass is one kernel whose GEMMs "
+                        "(K = 64 hidden units, N = rows) run on MFMA; achieved = its algorithmic FLOP / HIP-event time"}
+    from modular_rl_amd import timing
+    g = {k: v for k, v in kern.items() if k.startswith("gemm:")}
+    if not g:
+        return None
+    name = max(g, key=lambda k: g[k][2])
+    cnt, mean_ms, tot_ms = g[name]
+    m = timing.meta.get(name, {})
+    tf = m["flop"] / (mean_ms * 1e-3) / 1e12
+    gemm_peak = PEAK_BF16_TFLOPS if m.get("dtype") == "bf16" else PEAK_FP32_TFLOPS
+    traffic = gemm_pmc.get(name, {}).get("hbm_bytes_per_launch") if gemm_pmc else None
+    by_shape = {k: {"launches": c, "mean_ms": round(mm, 4), "ms_per_iter": round(t / K, 3),
+                    "frac_mfma": round(timing.meta[k]["flop"] / (mm * 1e-3) / 1e12 /
+                                       (PEAK_BF16_TFLOPS if timing.meta[k].get("dtype") == "bf16"
+                                        else PEAK_FP32_TFLOPS), 4)}
+                for k, (c, mm, t) in sorted(g.items(), key=lambda kv: -kv[1][2])}
+    return {"bound": "mfma", "achieved": round(tf, 3), "peak": gemm_peak, "unit": "TFLOP/s",
+            "frac": round(tf / gemm_peak, 4), "traffic": traffic,
+            "traffic_over_algorithmic": round(traffic / m["bytes"], 3) if traffic else None,
+            "traffic_source": f"profiles/{GEMM_PMC_FILE} (PMC, separate passes)" if traffic else None,
+            "algorithmic_bytes": m["bytes"], "hbm_gbs_alg": round(m["bytes"] / (mean_ms * 1e-3) / 1e9, 1),
+            "kernel": f"{m.get('kernel')} {name}", "flop_per_launch": m["flop"],
+            "mean_launch_ms": round(mean_ms, 5), "launches_timed": cnt, "ms_per_iter": round(tot_ms / K, 3),
+            "gemms": by_shape,
+            "note": "layered path: every GEMM launch over >= 65,536 rows timed on its own (HIP events on its stream); "
+                    "the shape with the largest device time per iteration; flop = 2mnk per product"}
 
 
 def main():
@@ -368,6 +445,12 @@ def main():
                             "traffic: the Fisher-product launch's PMC bytes")
     if dom == "rollout_step":
         roofline = rollout_latency_roofline(kinfo[dom], f"{args.env}/{args.dtype}", pmc, K, layered=net.layered)
+    gemm_pmc = {}
+    gp = os.path.join(ROOT, "profiles", GEMM_PMC_FILE)
+    if os.path.exists(gp) and net.layered:
+        with open(gp) as f:
+            gemm_pmc = json.load(f).get(f"{args.env}/{args.dtype}/{E}", {})
+    pg_roof = policy_gemm_roofline(kern, kinfo, net, args.dtype, n_local, K, pmc, gemm_pmc)
     gae = None
     if "gae_scan" in kern:
         cnt, mean_ms, _ = kern["gae_scan"]
@@ -394,6 +477,7 @@ def main():
         "kernels": {k: {kk: (round(vv, 5) if isinstance(vv, float) else vv) for kk, vv in v.items()} for k, v in kinfo.items()},
         "roofline": roofline,
         "roofline_gae": gae,
+        "roofline_policy_gemm": pg_roof,
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(cpu_E, cpu_T, args.env, hid)

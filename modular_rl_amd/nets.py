@@ -20,8 +20,12 @@ import ctypes
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, timing
 from ._lib import MrlError, call, ptr, stream
+
+# GEMM launches over at least this many rows are timed one by one when bench.py enables
+# timing (the update's and the VF fit's passes; not the rollout's per-step GEMMs)
+GEMM_TIMING_MIN_ROWS = 1 << 16
 
 HIDDEN = 64
 N_LAYERS = 2
@@ -294,6 +298,16 @@ class LayeredMlpNet:
         g = _lib.GemmDesc(m=m, n=n, k=k, a=a, lda=lda, a_trans=a_trans, ones_row=ones_row, b=b, ldb=ldb,
                           b_trans=b_trans, epilogue=epi, a2=a2, b2=b2, c=c, ldc=ldc, bias=bias, h=h, ldh=ldh,
                           splits=splits, slab_stride=slab_stride, compute=self.compute)
+        if timing.enabled() and max(m, k) >= GEMM_TIMING_MIN_ROWS:
+            # algorithmic work of the launch: 2mnk per product; bytes = f32 operands read
+            # once, C written once (SLAB: one [m, n] slab per K split), H read (DTANH)
+            prods = 2 if a2 is not None else 1
+            S = int(self.lib.mrl_gemm_slab_splits(k, splits)) if epi == _lib.GEMM_SLAB else 1
+            nbytes = 4 * (prods * (m * k + k * n) + S * m * n + (m * n if epi == _lib.GEMM_DTANH else 0))
+            kind = "TN" if a_trans else ("NT" if b_trans else ("NN_dual" if a2 is not None else "NN"))
+            timing.region(f"gemm:f32:{kind}:{m}x{n}x{k}", call, "mrl_gemm", ctypes.byref(g), ptr(skip), stream(),
+                          flop=2 * prods * m * n * k, bytes=nbytes, kernel="gemm_f32_kernel", dtype="fp32")
+            return
         call("mrl_gemm", ctypes.byref(g), ptr(skip), stream())
 
     def _input(self, x, n, ep_t, timestep_limit, name="x_time", out=None):
@@ -351,6 +365,14 @@ class LayeredMlpNet:
                   skip=None):
         g = _lib.GemmBf16Desc(m=m, n=n, k=k, a=ptr(a), lda=lda, bt=ptr(bt), ldb=ldb, a2=ptr(a2), bt2=ptr(bt2),
                               c=ptr(c), ldc=ldc, c_bf16=int(c_bf16), epilogue=epi, bias=bias, h=ptr(h), ldh=ldh)
+        if timing.enabled() and m >= GEMM_TIMING_MIN_ROWS:
+            prods = 2 if a2 is not None else 1
+            nbytes = 2 * prods * (m * k + n * k) + (2 if c_bf16 else 4) * m * n + (2 * m * n if h is not None else 0)
+            kind = ("NN_dual" if a2 is not None else "NN") + {_lib.GEMM_TANH: "_tanh", _lib.GEMM_DTANH: "_dtanh"}.get(
+                epi, "")
+            timing.region(f"gemm:bf16:{kind}:{m}x{n}x{k}", call, "mrl_gemm_bf16", ctypes.byref(g), ptr(skip), stream(),
+                          flop=2 * prods * m * n * k, bytes=nbytes, kernel="mrl_gemm_bf16", dtype="bf16")
+            return
         call("mrl_gemm_bf16", ctypes.byref(g), ptr(skip), stream())
 
     def _forward_b16(self, Xb, ldx, n, theta, bufs, zbuf, skip=None):
@@ -527,7 +549,13 @@ class LayeredMlpNet:
             g = _lib.GemmBf16TnDesc(m=din + 1, n=dout, k=n, a=ptr(inp), lda=lda, b=ptr(G), ldb=ldg, ones_row=1,
                                     splits=self.SLAB_SPLITS, slab=self._addr(slab, self.w_off[l]),
                                     slab_stride=self.P, ldc=dout)
-            call("mrl_gemm_bf16_tn", ctypes.byref(g), ptr(skip), stream())
+            if timing.enabled() and n >= GEMM_TIMING_MIN_ROWS:
+                timing.region(f"gemm:bf16:TN:{din + 1}x{dout}x{n}", call, "mrl_gemm_bf16_tn", ctypes.byref(g),
+                              ptr(skip), stream(), flop=2 * (din + 1) * dout * n,
+                              bytes=2 * n * (lda + ldg) + 4 * S * (din + 1) * dout, kernel="mrl_gemm_bf16_tn",
+                              dtype="bf16")
+            else:
+                call("mrl_gemm_bf16_tn", ctypes.byref(g), ptr(skip), stream())
             if l > 0:
                 Gn = self._bf(f"vjpb{l % 2}", n, wmax)
                 self._gemm_b16(n, din, dout, G, ldg, w_img[l][0], w_img[l][1], Gn, din, True, _lib.GEMM_DTANH,

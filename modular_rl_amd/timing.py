@@ -10,6 +10,7 @@ import torch
 _ENABLED = False
 _open = {}
 _events = collections.defaultdict(list)
+meta = {}  # name -> per-launch algorithmic work of the region (e.g. a GEMM's FLOP / bytes)
 
 
 def enable(on=True):
@@ -17,6 +18,7 @@ def enable(on=True):
     _ENABLED = on
     _open.clear()
     _events.clear()
+    meta.clear()
 
 
 def enabled():
@@ -35,6 +37,18 @@ def stop(name):
         e = torch.cuda.Event(enable_timing=True)
         e.record()
         _events[name].append((_open.pop(name), e))
+
+
+def region(name, fn, *args, **info):
+    """fn(*args) timed as one region `name` (when enabled), with the region's per-launch
+    work recorded in ``meta[name]``."""
+    if not _ENABLED:
+        return fn(*args)
+    meta.setdefault(name, info)
+    start(name)
+    out = fn(*args)
+    stop(name)
+    return out
 
 
 def drop_last(name, k):

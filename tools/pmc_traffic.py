@@ -56,6 +56,33 @@ def per_role(d, counter):
     return {k: (n, tot / n) for k, (n, tot) in acc.items()}
 
 
+def gemm_dispatches(d, counter):
+    vals = [float(r["Counter_Value"]) for r in _rows(d) if r.get("Counter_Name") == counter
+            and "gemm" in r.get("Kernel_Name", "") and "cast_rows" not in r["Kernel_Name"]
+            and "pack_w" not in r["Kernel_Name"]]
+    if not vals:
+        raise SystemExit(f"no GEMM dispatches with {counter} under {d}")
+    return len(vals), sum(vals) / len(vals)
+
+
+def gemm_entry(a):
+    nf, f = gemm_dispatches(a.fetch_dir, "FETCH_SIZE")
+    nw, w = gemm_dispatches(a.write_dir, "WRITE_SIZE")
+    e = {"FETCH_SIZE_KB_mean": f, "WRITE_SIZE_KB_mean": w, "launches_FETCH_SIZE": nf, "launches_WRITE_SIZE": nw,
+         "hbm_bytes_per_launch": int(round((2.0 * f + w) * 1024)),
+         "note": "tools/gemm_pmc_probe.py on this one shape; FETCH_SIZE x2 (gfx950), KB->bytes, separate passes"}
+    out = {}
+    if a.out and os.path.exists(a.out):
+        with open(a.out) as fh:
+            out = json.load(fh)
+    out.setdefault(a.key or "probe", {})[a.gemm] = e
+    s = json.dumps(out, indent=1)
+    if a.out:
+        with open(a.out, "w") as fh:
+            fh.write(s + "\n")
+    print(json.dumps({a.gemm: e}, indent=1))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
@@ -63,7 +90,12 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--horizon", type=int, default=1024,
                     help="steps per persistent rollout launch: its bytes / horizon = the per-step rollout_step figure")
+    ap.add_argument("--gemm", default=None, help="a tools/gemm_pmc_probe.py label: average the probe's GEMM "
+                                                 "dispatches (cast / pack setup kernels skipped) into --out[--key][label]")
+    ap.add_argument("--key", default=None, help="bench line of the --gemm entry, e.g. Humanoid-v2/bf16/1024")
     a = ap.parse_args()
+    if a.gemm:
+        return gemm_entry(a)
     fe = per_role(a.fetch_dir, "FETCH_SIZE")
     wr = per_role(a.write_dir, "WRITE_SIZE")
     out = {}
