@@ -2,7 +2,7 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := modular_rl_amd/csrc
-SRCS := $(CSRC)/mlp_kernels.hip $(CSRC)/mlp_bf16.hip $(CSRC)/scan.hip $(CSRC)/rollout.hip $(CSRC)/gemm.hip $(CSRC)/gemm_bf16.hip $(CSRC)/runtime.hip
+SRCS := $(CSRC)/mlp_kernels.hip $(CSRC)/mlp_bf16.hip $(CSRC)/mlp_split.hip $(CSRC)/scan.hip $(CSRC)/rollout.hip $(CSRC)/gemm.hip $(CSRC)/gemm_bf16.hip $(CSRC)/runtime.hip
 HDRS := $(wildcard $(CSRC)/*.h) include/mrl_hip.h
 OBJS := $(patsubst $(CSRC)/%.hip,build/%.o,$(SRCS))
 LIB := modular_rl_amd/libmrl_hip.so

@@ -193,6 +193,12 @@ def rollout_cu_split(n_rollout, n_cus):
     return r, list(range(n_rollout, n_cus))
 
 
+def fit_comm_for(comm, beside_rollout):
+    """The Comm the VF fit reduces over: a host (gloo) group when the fit runs beside the
+    rollout on more than one rank, else the iteration's own (RCCL) Comm."""
+    return comm.host() if beside_rollout and comm.enabled and comm.world > 1 else comm
+
+
 class IterationRunner:
     """One iteration of `core.py:146-157` per ``step()``: rollout -> compute_advantage
     -> VF fit -> policy update -> stats.
@@ -232,6 +238,12 @@ class IterationRunner:
                 # serialise the fit behind it
                 self.main_stream = torch.cuda.Stream()
                 self.pipeline = True
+                # data-parallel: the fit's per-evaluation reductions go over a host group
+                # while it overlaps the persistent rollout (RCCL's kernels would land on
+                # the rollout's CUs); fit_comm_for keeps it unchanged otherwise
+                reg = getattr(getattr(agent, "baseline", None), "reg", None)
+                if reg is not None and hasattr(reg, "set_comm"):
+                    reg.set_comm(fit_comm_for(getattr(reg, "comm", self.comm), True))
 
     @staticmethod
     def _stats(ep, vf_stats, pol_stats):

@@ -1,0 +1,643 @@
+// fp32-accurate Fisher-vector product on bf16 MFMA: split operands.
+//
+// The TRPO update spends ~90 % of its time in the ten Fisher products of CG
+// (trpo.py:45-58, 86-92: fvp = grad(grad(kl_ff) . v)).  On gfx950 the exact-f32 MFMA
+// (v_mfma_f32_32x32x2_f32) runs at 1/16 of the bf16 rate, and the f32 pair of kernels
+// (mlp_kernels.hip) sits at the f32 MFMA floor of the chip's power-held clock.  Here every
+// f32 MFMA operand v is split exactly into three bf16 parts, v = v0 + v1 + v2 (RNE
+// splits: v0 = bf16(v), v1 = bf16(v - v0), v2 = bf16(v - v0 - v1); each subtraction is
+// exact and the last remainder has at most 8 significant bits), and a product a.b is
+// the sum of the part products a_i.b_j on v_mfma_f32_32x32x16_bf16 with f32 accumulation:
+//   NPROD = 9: all nine products -- every a_i.b_j is exact in f32, so a.b is formed
+//              exactly and the only rounding is the f32 accumulation, as in the f32 MFMA;
+//   NPROD = 6: drops a1.b2, a2.b1, a2.b2 (each <= 2^-25 |a.b|, below one f32 ulp).
+// The parts are accumulated smallest first, 16 k-terms per MFMA (fewer roundings than a
+// per-product f32 fma chain).  So this is fp32 arithmetic in its accuracy -- checked
+// against the float64 oracle at the same 1e-4 and against the exact-f32 kernels to f32
+// rounding (tests/test_gpu_split.py) -- on the bf16 matrix cores.
+//
+// Layouts are those of the bf16 mode (bf16_frag.h, mlp_bf16.hip header): F tiles
+// D[unit][row] chain as B fragments; the split image is the bf16 image's f32 section
+// (biases, VALU head) followed by three copies of its bf16 section, part p at +p * PS.
+// The primal activations come from the f32 activation cache of the update's SURRGRAD
+// pass (mlp_kernels.hip cache layout = the F-tile register order), split on load.
+#include <math.h>
+#include <stdlib.h>
+
+#include "../../include/mrl_hip.h"
+#include "bf16_frag.h"
+#include "mlp_device.h"
+#include "rows_epilogue.h"
+
+namespace mrl {
+
+// Split image: the f32 section [0, fa0), then the three parts of the forward fragments
+// (fa0, fa1: FW words each, part p of a forward segment at its bf16-image offset + p FW),
+// then the three parts of the backward fragments (bw2, bt1: BW words each, part p at its
+// bf16-image offset + 2 FW + p BW).  A pass that needs only the forward segments (the JVP,
+// the tangent's image) stages the first fa0 + 3 FW words.
+__host__ __device__ constexpr int split_fw(const BDims& b) { return b.fwd_words - b.fa0; }
+__host__ __device__ constexpr int split_bw(const BDims& b) { return b.total_words - b.fwd_words; }
+__host__ __device__ constexpr int split_fwd_words(const BDims& b) { return b.fa0 + 3 * split_fw(b); }
+__host__ __device__ constexpr int split_image_words(const BDims& b) { return split_fwd_words(b) + 3 * split_bw(b); }
+// offset of part 0 of a backward segment (bw2 / bt1 of the bf16 image)
+__host__ __device__ constexpr int split_bwd_seg(const BDims& b, int seg) { return seg + 2 * split_fw(b); }
+
+// part p (0, 1, 2) of an f32 value's exact three-way bf16 split
+__device__ inline float bf16_part(float v, int p) {
+  const __bf16 a = (__bf16)v;
+  if (p == 0) return (float)a;
+  const float r = v - (float)a;
+  const __bf16 c = (__bf16)r;
+  if (p == 1) return (float)c;
+  return r - (float)c;
+}
+
+__global__ void mlp_pack_split_kernel(MlpDims d, BDims b, const float* __restrict__ th, float* __restrict__ image,
+                                      int words, const int32_t* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= words) return;
+  if (w < b.fa0) {  // f32 section: biases and the VALU head, the bf16 image's order
+    int idx;
+    if (w < b.fb1) idx = d.fb0 + (w - b.fb0);
+    else if (w < b.hv) idx = d.fb1 + (w - b.fb1);
+    else if (w < b.hb) idx = d.hv + (w - b.hv);
+    else idx = d.hb + (w - b.hb);
+    image[w] = image_value(d, th, idx);
+    return;
+  }
+  const int FW = split_fw(b), BW = split_bw(b), f0 = split_fwd_words(b);
+  const int part = w < f0 ? (w - b.fa0) / FW : (w - f0) / BW;
+  const int wp = w < f0 ? b.fa0 + (w - b.fa0) % FW : b.fwd_words + (w - f0) % BW;
+  int seg, rel;
+  if (wp < b.fa1) { seg = 0; rel = wp - b.fa0; }
+  else if (wp < b.bw2) { seg = 1; rel = wp - b.fa1; }
+  else if (wp < b.bt1) { seg = 2; rel = wp - b.bw2; }
+  else { seg = 3; rel = wp - b.bt1; }
+  const int frag = rel >> 2, q = rel & 3;
+  const __bf16 lo = (__bf16)bf16_part(bimage_elem(d, b, th, seg, frag, 2 * q), part);
+  const __bf16 hi = (__bf16)bf16_part(bimage_elem(d, b, th, seg, frag, 2 * q + 1), part);
+  const uint32_t v = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+  image[w] = __uint_as_float(v);
+}
+
+// the three parts of registers 8 sp .. 8 sp + 7 of an F tile (the B fragment pack8 forms)
+__device__ inline void split8(const f32x16& t, int sp, bf16x8* out) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = t[8 * sp + j];
+    const __bf16 a = (__bf16)v;
+    const float r = v - (float)a;
+    const __bf16 c = (__bf16)r;
+    out[0][j] = a;
+    out[1][j] = c;
+    out[2][j] = (__bf16)(r - (float)c);
+  }
+}
+__device__ inline void split8v(const float* v, bf16x8* out) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 a = (__bf16)v[j];
+    const float r = v[j] - (float)a;
+    const __bf16 c = (__bf16)r;
+    out[0][j] = a;
+    out[1][j] = c;
+    out[2][j] = (__bf16)(r - (float)c);
+  }
+}
+
+// acc += W . X for one k-step: W = the image fragment f of segment `seg` (parts at
+// +p * PS), X = three parts; smallest products first
+template <int NPROD>
+__device__ inline void mfma_split(const float* img, int seg, int PS, int f, int lane, const bf16x8* x, f32x16& acc) {
+  const bf16x8 w0 = frag_at(img, seg, f, lane), w1 = frag_at(img, seg + PS, f, lane);
+  const bf16x8 w2 = frag_at(img, seg + 2 * PS, f, lane);
+  if constexpr (NPROD == 9) {
+    acc = MFMA32B(w2, x[2], acc);
+    acc = MFMA32B(w2, x[1], acc);
+    acc = MFMA32B(w1, x[2], acc);
+  }
+  acc = MFMA32B(w2, x[0], acc);
+  acc = MFMA32B(w0, x[2], acc);
+  acc = MFMA32B(w1, x[1], acc);
+  acc = MFMA32B(w1, x[0], acc);
+  acc = MFMA32B(w0, x[1], acc);
+  acc = MFMA32B(w0, x[0], acc);
+}
+
+#ifndef MRL_SPLIT_NPROD
+#define MRL_SPLIT_NPROD 6
+#endif
+
+template <int SH>
+__device__ inline void split_shape(RowsArgs& a, BDims& b) {
+  if constexpr (SH != 0) {
+    constexpr StaticShape S = STATIC_SHAPES[SH];
+    a.d = static_dims(SH);
+    a.A = S.A;
+    a.head = S.head;
+    a.n_obs = S.O;
+    a.gh = S.head == MRL_HEAD_GAUSS ? 2 * S.A : S.A;
+    a.ept = nullptr;
+    b = bf16_dims(S.O, S.A);
+  }
+}
+
+constexpr int SPLIT_ROWS_BLOCK = 256;
+
+// The Fisher product's forward half (trpo.py:45-58): JVP of the head along the tangent
+// from the cached f32 h1 / h2, then the KL-metric head-gradient rows (row_epilogue FVP),
+// exactly what mlp_rows_kernel<EPI_FVP_CACHED> computes, with split-operand products.
+template <int SH>
+__global__ __launch_bounds__(SPLIT_ROWS_BLOCK, 2) void mlp_fvp_split_kernel(RowsArgs a, BDims b,
+                                                                           const float* __restrict__ img_g,
+                                                                           const float* __restrict__ imt_g,
+                                                                           const int32_t* __restrict__ skip) {
+  split_shape<SH>(a, b);
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (skip != nullptr && *skip != 0) return;
+  const int W = split_fwd_words(b), PS = split_fw(b);  // forward segments only
+  for (int i = threadIdx.x; i < W / 4; i += SPLIT_ROWS_BLOCK) {
+    reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img_g)[i];
+    reinterpret_cast<float4*>(lds + W)[i] = reinterpret_cast<const float4*>(imt_g)[i];
+  }
+  __syncthreads();
+  const float* img = lds;
+  const float* imt = lds + W;
+  const MlpDims dd = head_dims(a.d, b);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int A = a.A;
+  float ls[MAX_OUT], sd[MAX_OUT], dls[MAX_OUT];
+#pragma unroll
+  for (int j = 0; j < MAX_OUT; ++j) {
+    ls[j] = (a.logstd != nullptr && j < A) ? a.logstd[j] : 0.f;
+    sd[j] = expf(ls[j]);
+    dls[j] = (a.dlogstd != nullptr && j < A) ? a.dlogstd[j] : 0.f;
+  }
+  const bool need_z = a.head != MRL_HEAD_GAUSS;  // the DiagGauss metric does not use the mean
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+  const int64_t ntiles = (a.n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t row = tile * 32 + (lane & 31);
+    const bool valid = row < a.n;
+    XGlobalNB xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
+    const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
+    f32x16 h1[2], dh[2];
+    cache_load(ct, lane, 0, h1[0]);
+    cache_load(ct, lane, 1, h1[1]);
+    // layer 0 tangent: dh = (x dW0 + db0) (1 - h1^2)
+    dh[0] = load_bias16(imt, b.fb0, 0, h);
+    dh[1] = load_bias16(imt, b.fb0, 1, h);
+#pragma unroll
+    for (int s0 = 0; s0 < MAX_KS0B; ++s0) {
+      if (s0 < b.KS0B) {
+        float xv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = xl(16 * s0 + 8 * h + j);
+        bf16x8 xs[3];
+        split8v(xv, xs);
+        mfma_split<MRL_SPLIT_NPROD>(imt, b.fa0, PS, 0 * b.KS0B + s0, lane, xs, dh[0]);
+        mfma_split<MRL_SPLIT_NPROD>(imt, b.fa0, PS, 1 * b.KS0B + s0, lane, xs, dh[1]);
+      }
+    }
+    mul_dtanh16(dh[0], h1[0]);
+    mul_dtanh16(dh[1], h1[1]);
+    // layer 1 tangent per output tile: da = (dh W1 + h1 dW1 + db1) (1 - h2^2)
+    float z[MAX_OUT], dz[MAX_OUT], dzt[MAX_OUT];
+#pragma unroll
+    for (int o = 0; o < MAX_OUT; ++o) z[o] = dz[o] = dzt[o] = 0.f;
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo) {
+      f32x16 da = load_bias16(imt, b.fb1, mo, h);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8 ps[3];
+        split8(dh[s >> 1], s & 1, ps);
+        mfma_split<MRL_SPLIT_NPROD>(img, b.fa1, PS, mo * 4 + s, lane, ps, da);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8 ps[3];
+        split8(h1[s >> 1], s & 1, ps);
+        mfma_split<MRL_SPLIT_NPROD>(imt, b.fa1, PS, mo * 4 + s, lane, ps, da);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 h2;
+      cache_load(ct, lane, 2 + mo, h2);
+      mul_dtanh16(da, h2);
+      // the head on the f32 VALU: dz = da . W2 + h2 . dW2 (+ db2 in head_finish), z = h2 . W2
+      if (need_z) head_partial_mt(img, dd, h2, mo, h, z);
+      head_partial_mt(img, dd, da, mo, h, dz);
+      head_partial_mt(imt, dd, h2, mo, h, dzt);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (need_z) head_finish(img, dd, z);
+#pragma unroll
+    for (int o = 0; o < MAX_OUT; ++o) dz[o] += dzt[o];
+    head_finish(imt, dd, dz);
+    if (!valid || h != 0) continue;
+    row_epilogue<MRL_EPI_FVP, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+  }
+  (void)acc0;
+  (void)acc1;
+  (void)acc2;
+}
+
+
+// ------------------------------------------------------------------ VJP
+// acc += A . B over the split parts of both operands (A[p], B[p]: part p), smallest first
+template <int NPROD>
+__device__ inline void mma_split(const bf16x8* A, const bf16x8* B, f32x16& acc) {
+  if constexpr (NPROD == 9) {
+    acc = MFMA32B(A[2], B[2], acc);
+    acc = MFMA32B(A[2], B[1], acc);
+    acc = MFMA32B(A[1], B[2], acc);
+  }
+  acc = MFMA32B(A[2], B[0], acc);
+  acc = MFMA32B(A[0], B[2], acc);
+  acc = MFMA32B(A[1], B[1], acc);
+  acc = MFMA32B(A[1], B[0], acc);
+  acc = MFMA32B(A[0], B[1], acc);
+  acc = MFMA32B(A[0], B[0], acc);
+}
+
+struct VjpSplitArgs {
+  MlpDims d;
+  BDims b;
+  int n_obs, gh, n_sum;
+  const float* x;
+  int64_t n;
+  const float* ghead;
+  float* slab;
+  const float* cache;
+};
+
+template <int SH>
+__device__ inline VjpSplitArgs vjp_shape_s(const VjpSplitArgs& in) {
+  VjpSplitArgs a = in;
+  if constexpr (SH != 0) {
+    constexpr StaticShape S = STATIC_SHAPES[SH];
+    a.d = static_dims(SH);
+    a.b = bf16_dims(S.O, S.A);
+    a.n_obs = S.O;
+    a.n_sum = S.head == MRL_HEAD_GAUSS ? S.A : 0;
+    a.gh = S.A + a.n_sum;
+  }
+  return a;
+}
+
+// T tile (D[row][unit]) of the F tile whose two fragments are f0 (registers 0-7) and f1
+__device__ inline f32x16 transpose_ff(const bf16x8& f0, const bf16x8& f1, const bf16x8* ip) {
+  f32x16 t = MFMA32B(f0, ip[0], zero16());
+  return MFMA32B(f1, ip[1], t);
+}
+
+constexpr int VJP_SPLIT_MAX_BLOCKS = 256;  // one block (4 waves) per CU, one wave per SIMD
+
+// The Fisher product's reverse half and the policy gradient's VJP (trpo.py:42-43, 58):
+// per-wave partials of sum_rows J^T ghead in flat theta layout (one slab row per wave,
+// reduced in fixed order by mrl_reduce_rows_f32), from the cached f32 h1 / h2, with the
+// split-operand products.  The bf16 mode's transpose-free scheme (mlp_bf16.hip): F tiles
+// become T tiles by identity MFMAs -- one per split part, exact, since each part is a
+// bf16 value -- and the weight gradients take T tiles as both operands.
+template <int SH>
+__global__ __launch_bounds__(256, 1) void mlp_vjp_split_kernel(VjpSplitArgs a_in, const float* __restrict__ img_g,
+                                                              const int32_t* __restrict__ skip) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (skip != nullptr && *skip != 0) return;
+  const VjpSplitArgs a = vjp_shape_s<SH>(a_in);
+  const MlpDims& d = a.d;
+  const BDims& b = a.b;
+  // the backward parts of the split image: W2 (bw2) and W1^T (bt1) fragments, part p of
+  // a segment at (seg - fwd_words) + p BW
+  const int BW = split_bw(b), f0 = split_fwd_words(b);
+  for (int i = threadIdx.x; i < 3 * BW / 4; i += 256)
+    reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img_g + f0)[i];
+  __syncthreads();
+  auto wfrag = [&](int seg, int p, int f, int lane) { return frag_at(lds, seg - b.fwd_words + p * BW, f, lane); };
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j32 = lane & 31;
+  const int A = d.A;
+  const bf16x8 ip[2] = {ident_perm(0, lane), ident_perm(1, lane)};
+
+  f32x16 gW2[2], gW1[2][2], gW0[2];  // T-tile products: [u2][o], [u1][u2], [in][u1]
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    gW2[m] = zero16();
+    gW0[m] = zero16();
+#pragma unroll
+    for (int n = 0; n < 2; ++n) gW1[m][n] = zero16();
+  }
+  float gb0[2] = {0.f, 0.f}, gb1[2] = {0.f, 0.f};  // per lane = unit, this half's rows
+  float gb2[MAX_OUT], gls[MAX_OUT];
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    gb2[o] = 0.f;
+    gls[o] = 0.f;
+  }
+  const int64_t ntiles = (a.n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t row = tile * 32 + j32;
+    const int64_t rc = row < a.n ? row : 0;
+    // validity as opaque 0 / 1 factors (a select on a loaded value becomes a branch and a
+    // vmcnt(0) drain); rows past the batch read row 0 and contribute zero head gradients
+    float fv = (row < a.n && h == 0) ? 1.f : 0.f, fx = row < a.n ? 1.f : 0.f;
+    asm volatile("" : "+v"(fv), "+v"(fx));
+    const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
+    f32x16 h1[2], h2[2];
+    cache_load(ct, lane, 0, h1[0]);
+    cache_load(ct, lane, 1, h1[1]);
+    cache_load(ct, lane, 2, h2[0]);
+    cache_load(ct, lane, 3, h2[1]);
+    const float* gp = a.ghead + rc * a.gh;
+    float g8[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+      g8[o] = o < A ? gp[o < A ? o : 0] * fv : 0.f;
+      gb2[o] += g8[o];
+    }
+#pragma unroll
+    for (int q = 0; q < MAX_OUT; ++q) gls[q] += q < a.n_sum ? gp[A + (q < a.n_sum ? q : 0)] * fv : 0.f;
+    float xv[8 * MAX_KS0B];
+    const float* xp = a.x + rc * a.n_obs;
+#pragma unroll
+    for (int s0 = 0; s0 < MAX_KS0B; ++s0)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int k = 16 * s0 + 8 * h + jj;
+        xv[8 * s0 + jj] = (s0 < b.KS0B && k < a.n_obs) ? xp[k < a.n_obs ? k : 0] * fx : 0.f;
+      }
+
+    // gh2 = W2 . G (F layout, K = head outputs), ga2 = gh2 (1 - h2^2)
+    bf16x8 gB[3];
+    split8v(g8, gB);
+    f32x16 ga2[2];
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo) {
+      const bf16x8 w[3] = {wfrag(b.bw2, 0, mo, lane), wfrag(b.bw2, 1, mo, lane), wfrag(b.bw2, 2, mo, lane)};
+      ga2[mo] = zero16();
+      mma_split<MRL_SPLIT_NPROD>(w, gB, ga2[mo]);
+      mul_dtanh16(ga2[mo], h2[mo]);
+    }
+    // gW2 += H2^T G: T parts of G (D[row][o]) and of H2 (D[row][u2])
+    {
+      bf16x8 gT[2][3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const f32x16 t = MFMA32B(gB[p], ident_nat(0, lane), zero16());
+        gT[0][p] = pack8(t, 0);
+        gT[1][p] = pack8(t, 1);
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        bf16x8 f0[3], f1[3];
+        split8(h2[m], 0, f0);
+        split8(h2[m], 1, f1);
+        bf16x8 hT[2][3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const f32x16 t = transpose_ff(f0[p], f1[p], ip);
+          hT[0][p] = pack8(t, 0);
+          hT[1][p] = pack8(t, 1);
+        }
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) mma_split<MRL_SPLIT_NPROD>(hT[sp], gT[sp], gW2[m]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // ga2 as F-fragment parts (A operand of gh1) and T-fragment parts (B operand of gW1)
+    bf16x8 gaF[4][3], gaT[2][2][3];  // [s][p], [m][sp][p]
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      split8(ga2[m], 0, gaF[2 * m]);
+      split8(ga2[m], 1, gaF[2 * m + 1]);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const f32x16 t = transpose_ff(gaF[2 * m][p], gaF[2 * m + 1][p], ip);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) gb1[m] += t[r];
+        gaT[m][0][p] = pack8(t, 0);
+        gaT[m][1][p] = pack8(t, 1);
+      }
+    }
+    // the inputs in T layout (D[row][in]), per part
+    bf16x8 xT[2][3];
+    {
+      bf16x8 xs[MAX_KS0B][3];
+#pragma unroll
+      for (int s0 = 0; s0 < MAX_KS0B; ++s0) split8v(xv + 8 * s0, xs[s0]);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        f32x16 t = zero16();
+#pragma unroll
+        for (int s0 = 0; s0 < MAX_KS0B; ++s0)
+          if (s0 < b.KS0B) t = MFMA32B(xs[s0][p], ident_nat(16 * s0, lane), t);
+        xT[0][p] = pack8(t, 0);
+        xT[1][p] = pack8(t, 1);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // per u1 tile: gh1 (T layout) = ga2 . W1^T, ga1 = gh1 (1 - h1^2), then
+    // gW1 += H1^T GA2 and gW0 += X^T GA1
+#pragma unroll
+    for (int no = 0; no < 2; ++no) {
+      f32x16 ga1 = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 w[3] = {wfrag(b.bt1, 0, no * 4 + s, lane), wfrag(b.bt1, 1, no * 4 + s, lane),
+                             wfrag(b.bt1, 2, no * 4 + s, lane)};
+        mma_split<MRL_SPLIT_NPROD>(gaF[s], w, ga1);
+      }
+      bf16x8 f0[3], f1[3];
+      split8(h1[no], 0, f0);
+      split8(h1[no], 1, f1);
+      bf16x8 hT[2][3];
+      f32x16 h1T = zero16();
+#pragma unroll
+      for (int p = 2; p >= 0; --p) {  // h1 = (lo + mid) + hi: exact, the parts reassemble the f32 value
+        const f32x16 t = transpose_ff(f0[p], f1[p], ip);
+        h1T += t;
+        hT[0][p] = pack8(t, 0);
+        hT[1][p] = pack8(t, 1);
+      }
+      mul_dtanh16(ga1, h1T);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gb0[no] += ga1[r];
+      bf16x8 g1[2][3];
+      split8(ga1, 0, g1[0]);
+      split8(ga1, 1, g1[1]);
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        mma_split<MRL_SPLIT_NPROD>(hT[sp], gaT[0][sp], gW1[no][0]);
+        mma_split<MRL_SPLIT_NPROD>(hT[sp], gaT[1][sp], gW1[no][1]);
+        mma_split<MRL_SPLIT_NPROD>(xT[sp], g1[sp], gW0[no]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // per-wave partial gradient in flat theta layout; accumulator tiles are D[i][j] with
+  // j = lane & 31 and i = cperm(r, h)
+  float* out = a.slab + ((int64_t)blockIdx.x * 4 + wave) * d.P;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = cperm(r, h);
+      if (i < d.O) out[d.tW0 + i * HID + 32 * m + j32] = gW0[m][r];
+      if (j32 < A) out[d.tW2 + (32 * m + i) * A + j32] = gW2[m][r];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) out[d.tW1 + (32 * m + i) * HID + 32 * n + j32] = gW1[m][n][r];
+    }
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const float s0 = gb0[m] + __shfl_xor(gb0[m], 32);
+    const float s1 = gb1[m] + __shfl_xor(gb1[m], 32);
+    if (h == 0) {
+      out[d.tb0 + 32 * m + j32] = s0;
+      out[d.tb1 + 32 * m + j32] = s1;
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    const float sum = wave_sumf(gb2[o]);
+    if (lane == 0 && o < A) out[d.tb2 + o] = sum;
+  }
+  for (int q = 0; q < a.n_sum; ++q) {
+    const float sum = wave_sumf(gls[q]);
+    if (lane == 0) out[d.tls + q] = sum;
+  }
+}
+
+}  // namespace mrl
+
+using namespace mrl;
+
+static int check_desc_s(const mrl_mlp_desc* d) {
+  if (d == nullptr) return fail(E_ARG, "null mlp desc");
+  if (d->n_hidden != HID || d->n_layers != 2)
+    return fail(E_UNSUPPORTED, "only hid_sizes=[64,64] is implemented on the fused HIP path");
+  if (d->n_in < 1 || d->n_in > MAX_IN) return fail(E_UNSUPPORTED, "n_in must be in [1, 32]");
+  if (d->n_out < 1 || d->n_out > MAX_OUT) return fail(E_UNSUPPORTED, "n_out must be in [1, 8]");
+  if (d->head < 0 || d->head > 2) return fail(E_ARG, "bad head kind");
+  if (d->head == MRL_HEAD_LINEAR && d->n_out != 1) return fail(E_ARG, "linear head needs n_out=1");
+  return OK;
+}
+
+static int static_shape_split(const mrl_mlp_desc* d) {
+#ifdef MRL_NO_STATIC_SHAPES
+  (void)d;
+  return 0;
+#else
+  for (int i = 1; i < N_STATIC_SHAPES; ++i)
+    if (STATIC_SHAPES[i].O == d->n_in && STATIC_SHAPES[i].A == d->n_out && STATIC_SHAPES[i].head == d->head) return i;
+  return 0;
+#endif
+}
+
+// grid: two resident rounds of 2 blocks per CU (MRL_SPLIT_BLOCKS overrides)
+static int64_t split_rows_blocks(int64_t n) {
+  static const int64_t env_cap = [] {
+    const char* e = getenv("MRL_SPLIT_BLOCKS");
+    return (int64_t)(e ? atoi(e) : 0);
+  }();
+  const int64_t cap = env_cap > 0 ? env_cap : 1024;
+  int64_t g = ((n + 31) / 32 + 3) / 4;
+  if (g < 1) g = 1;
+  return g > cap ? cap : g;
+}
+
+extern "C" {
+
+int64_t mrl_mlp_image_words_split(const mrl_mlp_desc* d) {
+  if (check_desc_s(d) != OK) return -1;
+  return split_image_words(bf16_dims(d->n_in, d->n_out));
+}
+
+int mrl_mlp_pack_split(const mrl_mlp_desc* d, const float* theta, float* image, int32_t fwd_only, const int32_t* skip,
+                       void* stream) {
+  int rc = check_desc_s(d);
+  if (rc) return rc;
+  if (!theta || !image) return fail(E_ARG, "null pointer");
+  const MlpDims m = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
+  const BDims b = bf16_dims(d->n_in, d->n_out);
+  const int words = fwd_only ? split_fwd_words(b) : split_image_words(b);
+  hipLaunchKernelGGL(mlp_pack_split_kernel, dim3((words + 255) / 256), dim3(256), 0, (hipStream_t)stream, m, b, theta,
+                     image, words, skip);
+  return hip_check(hipGetLastError(), "mrl_mlp_pack_split");
+}
+
+int mrl_mlp_fvp_split(const mrl_mlp_desc* d, const float* theta, const float* image, const float* tangent,
+                      const float* image_t, const mrl_rows_io* io, const int32_t* skip, void* stream) {
+  int rc = check_desc_s(d);
+  if (rc) return rc;
+  if (!io || !image || !image_t || !tangent || !io->x || !io->ghead) return fail(E_ARG, "null pointer");
+  if (!io->act_cache || io->cache_mode != MRL_CACHE_READ)
+    return fail(E_ARG, "mrl_mlp_fvp_split reads the f32 activation cache (MRL_CACHE_READ)");
+  if (io->ep_t) return fail(E_ARG, "mrl_mlp_fvp_split: policy rows only (no time feature)");
+  if (d->head == MRL_HEAD_LINEAR) return fail(E_ARG, "Fisher product of a value net");
+  if (d->head == MRL_HEAD_GAUSS && !theta) return fail(E_ARG, "DiagGauss needs theta (logstd)");
+  if (io->n <= 0) return OK;
+  RowsArgs a{};
+  a.d = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
+  a.head = d->head;
+  a.n_obs = d->n_in;
+  a.gh = d->head == MRL_HEAD_GAUSS ? 2 * d->n_out : d->n_out;
+  a.A = d->n_out;
+  a.x = io->x;
+  a.n = io->n;
+  a.inv_ng = io->inv_n_global;
+  a.ghead = io->ghead;
+  a.logstd = (d->head == MRL_HEAD_GAUSS && theta) ? theta + a.d.tls : nullptr;
+  a.dlogstd = (d->head == MRL_HEAD_GAUSS && tangent) ? tangent + a.d.tls : nullptr;
+  a.cache = io->act_cache;
+  a.cache_mode = MRL_CACHE_READ;
+  const BDims b = bf16_dims(d->n_in, d->n_out);
+  const size_t shm = (size_t)split_fwd_words(b) * 4 * 2;
+  const dim3 grid(split_rows_blocks(io->n)), blk(SPLIT_ROWS_BLOCK);
+  hipStream_t s = (hipStream_t)stream;
+  switch (static_shape_split(d)) {
+    case 1: hipLaunchKernelGGL((mlp_fvp_split_kernel<1>), grid, blk, shm, s, a, b, image, image_t, skip); break;
+    case 2: hipLaunchKernelGGL((mlp_fvp_split_kernel<2>), grid, blk, shm, s, a, b, image, image_t, skip); break;
+    default: hipLaunchKernelGGL((mlp_fvp_split_kernel<0>), grid, blk, shm, s, a, b, image, image_t, skip); break;
+  }
+  return hip_check(hipGetLastError(), "mrl_mlp_fvp_split");
+}
+
+int mrl_mlp_vjp_split(const mrl_mlp_desc* d, const float* image, const float* x, const float* ghead, int64_t n,
+                      float* slab, const float* act_cache, const int32_t* skip, void* stream) {
+  int rc = check_desc_s(d);
+  if (rc) return rc;
+  if (!image || !x || !ghead || !slab || !act_cache) return fail(E_ARG, "null pointer");
+  if (d->head == MRL_HEAD_LINEAR) return fail(E_ARG, "mrl_mlp_vjp_split: policy nets only");
+  if (n <= 0) return OK;
+  VjpSplitArgs a{};
+  a.d = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
+  a.b = bf16_dims(d->n_in, d->n_out);
+  a.n_obs = d->n_in;
+  a.n_sum = d->head == MRL_HEAD_GAUSS ? d->n_out : 0;
+  a.gh = d->n_out + a.n_sum;
+  a.x = x;
+  a.n = n;
+  a.ghead = ghead;
+  a.slab = slab;
+  a.cache = act_cache;
+  // the slab rows of mrl_mlp_slab_rows(d, n): one row per wave of a 4-wave block
+  const int64_t cus = d->cus > 0 ? d->cus : 256;
+  int64_t blocks = ((n + 31) / 32 + 3) / 4;
+  const int64_t cap = VJP_SPLIT_MAX_BLOCKS * cus / 256 > 0 ? VJP_SPLIT_MAX_BLOCKS * cus / 256 : 1;
+  if (blocks < 1) blocks = 1;
+  if (blocks > cap) blocks = cap;
+  const size_t shm = (size_t)3 * split_bw(a.b) * 4;
+  const dim3 grid(blocks), blk(256);
+  hipStream_t s = (hipStream_t)stream;
+  switch (static_shape_split(d)) {
+    case 1: hipLaunchKernelGGL((mlp_vjp_split_kernel<1>), grid, blk, shm, s, a, image, skip); break;
+    case 2: hipLaunchKernelGGL((mlp_vjp_split_kernel<2>), grid, blk, shm, s, a, image, skip); break;
+    default: hipLaunchKernelGGL((mlp_vjp_split_kernel<0>), grid, blk, shm, s, a, image, skip); break;
+  }
+  return hip_check(hipGetLastError(), "mrl_mlp_vjp_split");
+}
+
+}  // extern "C"

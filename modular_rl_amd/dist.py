@@ -24,12 +24,24 @@ import torch.distributed as dist
 
 
 class Comm:
-    def __init__(self, group=None, force=False):
+    def __init__(self, group=None, force=False, host_group=None):
         self.group = group
         up = dist.is_available() and dist.is_initialized()
         self.enabled = up and (dist.get_world_size(group) > 1 or bool(force))
         self.rank = dist.get_rank(group) if self.enabled else 0
         self.world = dist.get_world_size(group) if self.enabled else 1
+        self.host_group = host_group
+
+    def host(self):
+        """The same ranks over a host (gloo) group: collectives on host copies of the
+        tensors, no GPU collective kernels.  For the VF fit that runs beside the
+        persistent rollout: its per-evaluation loss / gradient sums are
+        read back by the L-BFGS host loop anyway, and reducing them on the host keeps
+        RCCL's kernels -- not CU-masked -- off the rollout's CUs during its hand-offs.
+        Without a host group (one rank, or a gloo default group): this Comm."""
+        if not self.enabled or self.world <= 1 or self.host_group is None:
+            return self
+        return HostComm(self.host_group)
 
     def allreduce_(self, t):
         """In-place sum over ranks (no-op on one rank)."""
@@ -57,6 +69,30 @@ class Comm:
             dist.barrier(group=self.group)
 
 
+class HostComm(Comm):
+    """Comm over a gloo group: device tensors are reduced through host copies."""
+
+    def allreduce_(self, t):
+        if self.enabled:
+            if t.is_cuda:
+                h = t.cpu()
+                dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def allreduce_int(self, v):
+        if not self.enabled:
+            return int(v)
+        t = torch.tensor([int(v)], dtype=torch.int64)
+        dist.all_reduce(t, group=self.group)
+        return int(t.item())
+
+    def host(self):
+        return self
+
+
 def init_from_env(backend=None):
     """Initialise torch.distributed from RANK/WORLD_SIZE/MASTER_* (torchrun) if present.
     ``MRL_DIST_BACKEND=gloo`` rehearses the multi-rank path with several ranks sharing
@@ -78,4 +114,7 @@ def init_from_env(backend=None):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
     dist.init_process_group(backend=backend)
-    return Comm(force=force)
+    # a gloo group over the same ranks (collective: every rank creates it here) for the
+    # host-side reductions of the VF fit that overlaps the rollout (Comm.host)
+    host = dist.new_group(backend="gloo") if backend == "nccl" and dist.get_world_size() > 1 else None
+    return Comm(force=force, host_group=host)

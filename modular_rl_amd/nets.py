@@ -16,6 +16,7 @@ implementations share one interface (``rows`` / ``vjp_flat`` / ``forward``):
 ``make_net`` picks the fused path whenever the shape allows it.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -126,6 +127,13 @@ class MlpNet:
         # the Fisher products of an update and the VJP after a loss pass reuse it
         self.use_cache = True
         self._cache_key = None
+        # fp32 Fisher products on bf16 MFMA with exactly split operands (csrc/mlp_split.hip):
+        # MRL_FISHER=split (default) | f32 (the exact-f32 MFMA kernels)
+        self.fisher_split = (not self.bf16) and os.environ.get("MRL_FISHER", "f32") == "split"
+        self.image_s = None
+        if self.fisher_split:
+            w = int(self.lib.mrl_mlp_image_words_split(ctypes.byref(self.desc)))
+            self.image_s = torch.zeros(w, dtype=torch.float32, device=self.device)
 
     # ---- flat parameter plumbing (GetFlat / SetFromFlat, core.py:518-557)
     def get_flat(self):
@@ -145,6 +153,23 @@ class MlpNet:
             self._cache_key = None
         call("mrl_mlp_pack" + self._sfx, ctypes.byref(self.desc), ptr(theta), ptr(image), int(fwd_only), ptr(skip),
              stream())
+        if image is self.image and self.fisher_split:
+            call("mrl_mlp_pack_split", ctypes.byref(self.desc), ptr(theta), ptr(self.image_s), 0, ptr(skip), stream())
+
+    def new_tangent_image(self):
+        """Image buffer for Fisher-product tangents (pack_tangent): a split image when the
+        Fisher products run on split operands."""
+        if self.fisher_split:
+            t = torch.zeros_like(self.image_s)
+            t._mrl_split = True  # rows(EPI_FVP) takes the split kernel for images marked so
+            return t
+        return torch.zeros_like(self.image)
+
+    def pack_tangent(self, v, image, skip=None):
+        if self.fisher_split:
+            call("mrl_mlp_pack_split", ctypes.byref(self.desc), ptr(v), ptr(image), 1, ptr(skip), stream())
+        else:
+            self.pack(theta=v, image=image, fwd_only=True, skip=skip)
 
     # ---- fused passes
     def rows(self, epi, x, n, ep_t=None, timestep_limit=1.0, inv_n_global=1.0, act=None, adv=None, oldprob=None,
@@ -161,6 +186,19 @@ class MlpNet:
                 self._cache_key = key
             elif epi == _lib.EPI_FVP and self._cache_key == key:
                 mode, cache = _lib.CACHE_READ, self._cache(n)
+        if epi == _lib.EPI_FVP and getattr(image_t, "_mrl_split", False):
+            if mode != _lib.CACHE_READ:
+                # split products read the f32 activation cache; without one the tangent is
+                # repacked as an f32 image for the exact-f32 kernel
+                t32 = self.ws.get("tan_f32_image", self.image.numel(), torch.float32)
+                self.pack(theta=tangent, image=t32, fwd_only=True, skip=skip)
+                image_t = t32
+            else:
+                io = _lib.RowsIO(ptr(x), ptr(ep_t), float(timestep_limit), int(n), float(inv_n_global), None, None,
+                                 None, None, None, ptr(ghead), None, 0.0, 0.0, 0.0, 0, mode, ptr(cache), None)
+                call("mrl_mlp_fvp_split", ctypes.byref(self.desc), ptr(theta), ptr(self.image_s), ptr(tangent),
+                     ptr(image_t), ctypes.byref(io), ptr(skip), stream())
+                return
         io = _lib.RowsIO(ptr(x), ptr(ep_t), float(timestep_limit), int(n), float(inv_n_global), ptr(act), ptr(adv),
                          ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial), float(kl_coeff),
                          float(kl_cutoff), float(cutoff_coeff), int(reverse_kl), mode, ptr(cache), ptr(feat_out))
@@ -196,9 +234,15 @@ class MlpNet:
         cache = None
         if self.use_cache and image is None and self._cache_key == self._key(x, n, ep_t, timestep_limit):
             cache = self._cache(n)
-        image = self.image if image is None else image
-        call("mrl_mlp_vjp" + self._sfx, ctypes.byref(self.desc), ptr(image), ptr(x), ptr(ep_t),
-             float(timestep_limit), ptr(ghead), int(n), ptr(slab), ptr(cache), ptr(skip), stream())
+        if (cache is not None and self.fisher_split and ep_t is None and self.head != _lib.HEAD_LINEAR
+                and os.environ.get("MRL_VJP_SPLIT", "0") != "0"):
+            # the policy's cached VJPs (Fisher products, policy gradient) on split operands
+            call("mrl_mlp_vjp_split", ctypes.byref(self.desc), ptr(self.image_s), ptr(x), ptr(ghead), int(n),
+                 ptr(slab), ptr(cache), ptr(skip), stream())
+        else:
+            image = self.image if image is None else image
+            call("mrl_mlp_vjp" + self._sfx, ctypes.byref(self.desc), ptr(image), ptr(x), ptr(ep_t),
+                 float(timestep_limit), ptr(ghead), int(n), ptr(slab), ptr(cache), ptr(skip), stream())
         call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
         return out
 
@@ -277,6 +321,12 @@ class LayeredMlpNet:
 
     def pack(self, theta=None, image=None, fwd_only=False, skip=None):
         """No image on the layered path: the GEMMs read theta directly."""
+
+    def new_tangent_image(self):
+        return torch.zeros_like(self.image)
+
+    def pack_tangent(self, v, image, skip=None):
+        """No tangent image on the layered path."""
 
     def size_for_cus(self, cus):
         """The layered path's GEMM grids do not depend on it (no CU split is applied)."""

@@ -17,8 +17,9 @@ def enable(on=True):
     global _ENABLED
     _ENABLED = on
     _open.clear()
-    _events.clear()
-    meta.clear()
+    if on:  # a new measurement; turning timing off keeps the last one's records readable
+        _events.clear()
+        meta.clear()
 
 
 def enabled():

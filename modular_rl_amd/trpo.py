@@ -56,7 +56,7 @@ class HipTrpoOps:
         self.fullstep = torch.zeros(P, **f64)
         self.cand = torch.zeros(P, **f32)
         self.cand_image = torch.zeros_like(net.image)
-        self.tan_image = torch.zeros_like(net.image)
+        self.tan_image = net.new_tangent_image()
         ns = int(_lib.load().mrl_cg_state_doubles(self.P))  # scalars + block partials (wide nets)
         self.state = torch.zeros(ns, **f64)
         self.flag = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -91,7 +91,7 @@ class HipTrpoOps:
 
     def fvp(self, v32, skip=None):
         b, net = self.batch, self.net
-        net.pack(theta=v32, image=self.tan_image, fwd_only=True, skip=skip)
+        net.pack_tangent(v32, self.tan_image, skip=skip)
         timing.start("fvp_jvp_rows")
         net.rows(_lib.EPI_FVP, b.obs, b.n, inv_n_global=self.inv_ng, ghead=self.ghead, tangent=v32,
                  image_t=self.tan_image, skip=skip)

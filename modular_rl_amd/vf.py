@@ -126,6 +126,14 @@ class NnRegression:
         self.opt = LbfgsOptimizer(net, maxiter=maxiter, comm=self.comm)
         self.moments = DeviceMoments(net.device, self.comm)
 
+    def set_comm(self, comm):
+        """Rebind every collective of the fit (loss / gradient sums, row count, the VF
+        statistics' moments) to `comm` -- e.g. Comm.host() while the fit overlaps the
+        rollout in data-parallel mode."""
+        self.comm = comm
+        self.opt.comm = comm
+        self.moments.comm = comm
+
     def predict(self, x, n, ep_t=None, timestep_limit=1.0, out=None, feat_out=None):
         return self.net.forward(x, n, ep_t=ep_t, timestep_limit=timestep_limit, out=out, feat_out=feat_out)
 

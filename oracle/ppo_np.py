@@ -32,23 +32,59 @@ def losses(spec, theta, ob, act, adv, oldprob, reverse_kl=False):
 
 
 def pensurr_and_grad(spec, theta, ob, act, adv, oldprob, kl_coeff, kl_cutoff, cutoff_coeff=1000.0,
-                     reverse_kl=False):
-    t = TR._params(spec, theta)
+                     reverse_kl=False, dtype=torch.float64):
+    """pensurr and its autograd gradient (`ppo.py:46-48`); dtype=torch.float32 evaluates
+    the graph the way Theano floatX=float32 does (inputs and parameters downcast)."""
+    t = TR._params(spec, theta, dtype)
     p = TR._forward(spec, t, ob)
     N = ob.shape[0]
     logp = TR._loglik(spec, act, p)
-    po = torch.tensor(np.asarray(oldprob, dtype=np.float64))
+    po = torch.tensor(np.asarray(oldprob), dtype=dtype)
     oldlogp = TR._loglik(spec, act, po)
-    surr = (-1.0 / N) * (torch.exp(logp - oldlogp) * torch.tensor(adv, dtype=torch.float64)).sum()
+    surr = (-1.0 / N) * (torch.exp(logp - oldlogp) * torch.tensor(np.asarray(adv), dtype=dtype)).sum()
     kl = _kl_rows(spec, po, p, reverse_kl).mean()
-    pen = surr + kl_coeff * kl + cutoff_coeff * (kl > kl_cutoff).double() * (kl - kl_cutoff) ** 2
+    pen = surr + kl_coeff * kl + cutoff_coeff * (kl > kl_cutoff).to(dtype) * (kl - kl_cutoff) ** 2
     (g,) = torch.autograd.grad(pen, t)
     return float(pen.item()), g.numpy()
 
 
-def lbfgs_update(spec, theta, ob, act, adv, oldprob, kl_coeff, kl_target=1e-2, maxiter=25, reverse_kl=False):
-    """One PpoLbfgsUpdater.__call__ without do_split: returns (theta_new, info, kl_coeff_new)."""
+def losses_t(spec, theta, ob, act, adv, oldprob, reverse_kl=False, dtype=torch.float64):
+    """[surr, kl, ent] (`ppo.py:50`) on the torch graph in `dtype` (the fixtures' floatX runs)."""
+    with torch.no_grad():
+        t = torch.tensor(np.asarray(theta), dtype=dtype)
+        p = TR._forward(spec, t, ob)
+        po = torch.tensor(np.asarray(oldprob), dtype=dtype)
+        N = ob.shape[0]
+        surr = (-1.0 / N) * (torch.exp(TR._loglik(spec, act, p) - TR._loglik(spec, act, po))
+                             * torch.tensor(np.asarray(adv), dtype=dtype)).sum()
+        kl = _kl_rows(spec, po, p, reverse_kl).mean()
+        if spec.head == "softmax":
+            ent = (-(p * torch.log(p)).sum(1)).mean()
+        else:
+            d = spec.n_out
+            ent = (torch.log(p[:, d:]).sum(1) + 0.5 * np.log(2 * np.pi * np.e) * d).mean()
+        return [surr.numpy(), kl.numpy(), ent.numpy()]
+
+
+def policy_prob_t(spec, theta, ob, dtype=torch.float64):
+    with torch.no_grad():
+        return TR._forward(spec, torch.tensor(np.asarray(theta), dtype=dtype), ob).numpy()
+
+
+def lbfgs_update(spec, theta, ob, act, adv, oldprob, kl_coeff, kl_target=1e-2, maxiter=25, reverse_kl=False,
+                 do_split=False):
+    """One PpoLbfgsUpdater.__call__ (`ppo.py:59-112`): returns (theta_new, info, kl_coeff_new);
+    do_split trains on the first 75 % of the rows and adds the test_* stats of the rest."""
     kl_cutoff = 2.0 * kl_target
+    N = ob.shape[0]
+    if do_split:
+        s = int(0.75 * N)
+        th, info, kc = lbfgs_update(spec, theta, ob[:s], act[:s], adv[:s], oldprob[:s], kl_coeff, kl_target, maxiter,
+                                    reverse_kl)
+        tb = losses(spec, theta, ob[s:], act[s:], adv[s:], oldprob[s:], reverse_kl)
+        ta = losses(spec, th, ob[s:], act[s:], adv[s:], oldprob[s:], reverse_kl)
+        info.update({"test_" + k: v for k, v in _info(tb, ta).items()})
+        return th, info, kc
 
     def lossandgrad(th):
         th32 = th.astype(np.float32).astype(np.float64)  # set_params_flat casts to floatX
@@ -82,14 +118,24 @@ def _info(before, after):
 
 
 def sgd_update(spec, theta, ob, act, adv, perms, kl_coeff, kl_target=1e-2, stepsize=1e-3, cutoff_coeff=1000.0,
-               batchsize=128, adam_state=None):
-    """PpoSgdUpdater.__call__ (no split) for the given epoch permutations, float32 Adam.
+               batchsize=128, adam_state=None, do_split=False):
+    """PpoSgdUpdater.__call__ (`ppo.py:169-229`) for the given epoch permutations (over the
+    training rows), float32 Adam.  do_split: the training rows are the first
+    (0.75 N // batchsize) * batchsize, the test_* stats come from the rest.
     Returns (theta_new, info, kl_coeff_new, adam_state)."""
     kl_cutoff = 2.0 * kl_target
     oldprob = T.policy_prob(spec, theta, ob)          # old net = params at update start
     th = theta.astype(np.float32)
     m, v, t = adam_state if adam_state is not None else (np.zeros_like(th), np.zeros_like(th), 0)
     N = ob.shape[0]
+    if do_split:
+        s = (int(.75 * N) // batchsize) * batchsize
+        tb = losses(spec, theta, ob[s:], act[s:], adv[s:], oldprob[s:])
+        th1, info, kc, st = sgd_update(spec, theta, ob[:s], act[:s], adv[:s], perms, kl_coeff, kl_target, stepsize,
+                                       cutoff_coeff, batchsize, adam_state)
+        ta = losses(spec, th1, ob[s:], act[s:], adv[s:], oldprob[s:])
+        info.update({"test_" + k: v for k, v in _info(tb, ta).items()})
+        return th1, info, kc, st
     before = losses(spec, th.astype(np.float64), ob, act, adv, oldprob)
     b1, b2, eps = np.float32(0.9), np.float32(0.999), np.float32(1e-8)
     train_losses = before

@@ -12,7 +12,8 @@ absent: ordinary ModuleNotFoundError), so:
   ``core.NnVf.fit`` / ``preproc``, ``core.NnRegression.fit`` and
   ``core.LbfgsOptimizer.update`` are AST-extracted from the reference files, with
   the HEAD-only TF diagnostics removed (trpo.py:82,84,98,100,131,132; core.py:79-96),
-  and executed.
+  and executed; ``ppo.PpoLbfgsUpdater.__call__`` / ``PpoSgdUpdater.__call__`` the same way
+  (``python make_golden.py ppo`` writes only ppo_update.npz).
 
 The Theano-compiled callables that ``TrpoUpdater.__call__`` needs
 (compute_policy_gradient / compute_losses / compute_fisher_vector_product) and the
@@ -361,8 +362,151 @@ def main():
             out[f"{k}_funcalls"], out[f"{k}_nit"] = np.int64(vrec["funcalls"]), np.int64(vrec["nit"])
             out[f"{k}_X"] = np.asarray(X, dtype=np.float64)
     np.savez(os.path.join(HERE, "vf_fit.npz"), **out)
+    ppo_fixtures(mods)
     print("golden fixtures written to", HERE)
 
 
+def ppo_fixtures(mods):
+    """ppo_update.npz: the reference's own PpoLbfgsUpdater.__call__ (ppo.py:59-112) and
+    PpoSgdUpdater.__call__ (ppo.py:169-229), AST-extracted, with the Theano functions
+    injected from torch autograd (oracle/ppo_np.py: pensurr = surr + kl_coeff kl + 1000
+    (kl > 2 kl_target) (kl - cutoff)^2, ppo.py:46-49, 153; adam_updates ppo.py:231-258).
+    Each case in float64 and floatX-faithful float32 (suffix f); inputs fp32-representable.
+    Recorded: theta after, the returned info, the adapted kl_coeff, scipy's opt_info
+    (L-BFGS) and the epoch permutations drawn (SGD, np.random seeded before the call)."""
+    from oracle import ppo_np
+    import scipy.optimize  # noqa: F401  (the extracted __call__ calls scipy.optimize)
+    mu = mods["misc_utils"]
+    pp = os.path.join(REF, "ppo.py")
+    rec = {}
+    base_ns = {"np": np, "scipy": scipy, "OrderedDict": OrderedDict, "concat": np.concatenate,
+               "zipsame": mu.zipsame, "fmt_row": mu.fmt_row, "xrange": range, "_rec": rec}
+    lb_call = extract(pp, ["PpoLbfgsUpdater.__call__"], extra_ns=dict(base_ns),
+                      record_after={90: "_rec.update(funcalls=opt_info['funcalls'], nit=opt_info['nit'], "
+                                        "warnflag=opt_info['warnflag'])"})["__call__"]
+    # the two epoch-table header prints (ppo.py:185, 190) add a str to a list and raise
+    # TypeError in any Python; they are display-only and dropped like the TRPO diagnostics
+    sgd_call = extract(pp, ["PpoSgdUpdater.__call__"], drop_lines={185, 190}, extra_ns=dict(base_ns))["__call__"]
+    f32 = (lambda a: np.asarray(a, dtype=np.float32).astype(np.float64))
+    rng = np.random.default_rng(21)
+    out = {}
+
+    def case_inputs(nin, nout, head, N):
+        spec = trpo_np.Spec(nin, [64, 64], nout, head)
+        th0 = trpo_np.mlp_init(rng, spec.shapes, head == "gauss") + 0.05 * rng.standard_normal(spec.P)
+        if head == "gauss":
+            th0[-nout:] = -0.3 + 0.1 * rng.standard_normal(nout)
+        th0 = f32(th0)
+        ob = f32(rng.standard_normal((N, nin)))
+        oldprob = f32(trpo_np.policy_prob(spec, th0 + 0.02 * rng.standard_normal(spec.P), ob))
+        noise = rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N)
+        act = trpo_np.sample(spec, oldprob, noise)
+        act = f32(act) if head == "gauss" else act
+        adv = f32(trpo_np.standardize(rng.standard_normal(N) + 0.3 * ob[:, 0]))
+        return spec, th0, ob, act, adv, oldprob
+
+    info_keys = ["surr_before", "surr_after", "surr_change", "kl_before", "kl_after", "kl_change",
+                 "ent_before", "ent_after", "ent_change"]
+    test_keys = ["test_" + k for k in info_keys]
+    # ---- PpoLbfgsUpdater: (head, N, do_split, reverse_kl, maxiter, kl_coeff0)
+    for k, (head, N, split, rev, maxiter, kc0) in {"lbg0": ("gauss", 600, 0, 0, 4, 1.0),
+                                                   "lbg1": ("gauss", 600, 1, 1, 4, 0.3),
+                                                   "lbc0": ("softmax", 500, 0, 0, 4, 1.0),
+                                                   "lbg2": ("gauss", 600, 0, 0, 25, 1.0)}.items():
+        nin, nout = (11, 3) if head == "gauss" else (4, 2)
+        spec, th0, ob, act, adv, oldprob = case_inputs(nin, nout, head, N)
+        out[f"{k}_theta0"], out[f"{k}_ob"], out[f"{k}_act"], out[f"{k}_adv"], out[f"{k}_oldprob"] = \
+            th0, ob, act, adv, oldprob
+        out[f"{k}_cfg"] = np.array([0.01, maxiter, rev, split, kc0])
+        for sfx, dtype in (("", np.float64), ("f", np.float32)):
+            tdt = torch.float64 if dtype == np.float64 else torch.float32
+            st = {"th": th0.astype(dtype)}
+            cfg = mu.update_default_config([("kl_target", float, 1e-2, ""), ("maxiter", int, 25, ""),
+                                            ("reverse_kl", int, 0, ""), ("do_split", int, 0, "")],
+                                           dict(maxiter=maxiter, reverse_kl=rev, do_split=split))
+
+            def lossgrad(kc, o, a, ad, op, st=st, tdt=tdt):
+                l, g = ppo_np.pensurr_and_grad(spec, st["th"], o, a, ad, op, kc, 2 * 0.01, 1000.0, bool(rev), tdt)
+                return l, g
+
+            self = types.SimpleNamespace(
+                cfg=cfg, kl_coeff=kc0, loss_names=["surr", "kl", "ent"],
+                get_params_flat=lambda st=st: st["th"].copy(),
+                set_params_flat=lambda t, st=st, dtype=dtype: st.__setitem__("th", np.asarray(t, dtype=dtype).copy()),
+                compute_lossgrad=lossgrad,
+                compute_losses=lambda o, a, ad, op, st=st, tdt=tdt: ppo_np.losses_t(spec, st["th"], o, a, ad, op,
+                                                                                    bool(rev), tdt))
+            cast = (lambda a: np.asarray(a).astype(dtype)) if dtype == np.float32 else (lambda a: a)
+            h = N // 2
+            paths = [dict(prob=cast(oldprob[:h]), observation=cast(ob[:h]), action=cast(act[:h]), advantage=cast(adv[:h])),
+                     dict(prob=cast(oldprob[h:]), observation=cast(ob[h:]), action=cast(act[h:]), advantage=cast(adv[h:]))]
+            rec.clear()
+            info = quiet(lb_call, self, paths)
+            kk = k + sfx
+            out[f"{kk}_theta1"] = st["th"].astype(np.float64)
+            keys = info_keys + (test_keys if split else [])
+            out[f"{kk}_info"] = np.array([float(info[n]) for n in keys], dtype=np.float64)
+            out[f"{kk}_kl_coeff"] = np.float64(self.kl_coeff)
+            out[f"{kk}_funcalls"], out[f"{kk}_nit"] = np.int64(rec["funcalls"]), np.int64(rec["nit"])
+    # ---- PpoSgdUpdater: (head, N, do_split, epochs, stepsize, kl_coeff0, seed)
+    for k, (head, N, split, epochs, lr, kc0, seed) in {"sgg0": ("gauss", 600, 0, 2, 1e-3, 1.0, 123),
+                                                       "sgc0": ("softmax", 600, 0, 2, 1e-3, 1.0, 7),
+                                                       "sgg1": ("gauss", 700, 1, 3, 3e-3, 0.3, 99)}.items():
+        nin, nout = (11, 3) if head == "gauss" else (4, 3)
+        spec, th0, ob, act, adv, _ = case_inputs(nin, nout, head, N)
+        out[f"{k}_theta0"], out[f"{k}_ob"], out[f"{k}_act"], out[f"{k}_adv"] = th0, ob, act, adv
+        out[f"{k}_cfg"] = np.array([0.01, epochs, lr, split, kc0, seed])
+        for sfx, dtype in (("", np.float64), ("f", np.float32)):
+            tdt = torch.float64 if dtype == np.float64 else torch.float32
+            st = {"th": th0.astype(dtype), "old": None, "m": np.zeros(spec.P, dtype), "v": np.zeros(spec.P, dtype),
+                  "t": dtype(0)}
+            cfg = mu.update_default_config([("kl_target", float, 1e-2, ""), ("epochs", int, 10, ""),
+                                            ("stepsize", float, 1e-3, ""), ("do_split", int, 0, ""),
+                                            ("kl_cutoff_coeff", float, 1000.0, "")],
+                                           dict(epochs=epochs, stepsize=lr, do_split=split))
+
+            def oldp(o, st=st, tdt=tdt):  # the old net: theta at update_old_net (ppo.py:160, 175)
+                return ppo_np.policy_prob_t(spec, st["old"], o, tdt)
+
+            def train(kc, o, a, ad, st=st, tdt=tdt, dtype=dtype, cfg=cfg):
+                # outputs at the pre-update params, then the Adam update (ppo.py:155-157, 231-258)
+                op = oldp(o)
+                l = ppo_np.losses_t(spec, st["th"], o, a, ad, op, False, tdt)
+                _, g = ppo_np.pensurr_and_grad(spec, st["th"], o, a, ad, op, kc, 2 * cfg["kl_target"],
+                                               cfg["kl_cutoff_coeff"], False, tdt)
+                g = g.astype(dtype)
+                b1, b2, eps, lr_ = dtype(0.9), dtype(0.999), dtype(1e-8), dtype(cfg["stepsize"])
+                st["t"] = st["t"] + dtype(1)
+                a_t = lr_ * np.sqrt(dtype(1) - b2 ** st["t"]) / (dtype(1) - b1 ** st["t"])
+                st["m"] = b1 * st["m"] + (dtype(1) - b1) * g
+                st["v"] = b2 * st["v"] + (dtype(1) - b2) * g ** 2
+                st["th"] = (st["th"] - a_t * st["m"] / (np.sqrt(st["v"]) + eps)).astype(dtype)
+                return l
+
+            self = types.SimpleNamespace(
+                cfg=cfg, kl_coeff=kc0, loss_names=["surr", "kl", "ent"],
+                update_old_net=lambda st=st: st.__setitem__("old", st["th"].copy()),
+                test=lambda o, a, ad, st=st, tdt=tdt: ppo_np.losses_t(spec, st["th"], o, a, ad, oldp(o), False, tdt),
+                train=train)
+            cast = (lambda a: np.asarray(a).astype(dtype)) if dtype == np.float32 else (lambda a: a)
+            h = N // 2
+            paths = [dict(observation=cast(ob[:h]), action=cast(act[:h]), advantage=cast(adv[:h])),
+                     dict(observation=cast(ob[h:]), action=cast(act[h:]), advantage=cast(adv[h:]))]
+            np.random.seed(seed)
+            info = quiet(sgd_call, self, paths)
+            kk = k + sfx
+            out[f"{kk}_theta1"] = st["th"].astype(np.float64)
+            keys = info_keys + (test_keys if split else [])
+            out[f"{kk}_info"] = np.array([float(info[n]) for n in keys], dtype=np.float64)
+            out[f"{kk}_kl_coeff"] = np.float64(self.kl_coeff)
+        train_stop = (int(.75 * N) // 128) * 128 if split else N
+        np.random.seed(seed)
+        out[f"{k}_perms"] = np.array([np.random.permutation(train_stop) for _ in range(epochs)])
+    np.savez(os.path.join(HERE, "ppo_update.npz"), **out)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["ppo"]:
+        ppo_fixtures(ref_pkg())
+    else:
+        main()

@@ -8,7 +8,8 @@
 * vf.LbfgsOptimizer (the VF fit, `core.py:663-697`) with the rows split over 2 ranks
   (loss sums and gradients all-reduced per L-BFGS evaluation, scaled by 1/N_global)
   ends where one rank holding all rows does, and where scipy L-BFGS-B on the float64
-  oracle loss does.
+  oracle loss does -- also with its reductions over a host (gloo) group (Comm.host,
+  what the pipelined loop uses while the fit overlaps the rollout at world > 1).
 """
 import os
 import types
@@ -92,8 +93,16 @@ def _worker(rank, world, port, q):
     s1 = np.concatenate([[rs.n, rr.n], np.append(rs.M, rr.M), np.append(rs.S, rr.S)])
     merged = merge_filter_deltas(s0, s1, comm)
     th_vf, info_vf = _vf_fit(rows, comm)
+    # the fit's reductions over a host group (Comm.host: what the pipelined loop uses
+    # while the fit overlaps the rollout in data-parallel mode) take the same path
+    from modular_rl_amd.core import fit_comm_for
+    from modular_rl_amd.dist import HostComm
+    hcomm = Comm(host_group=dist.new_group(backend="gloo"))
+    fc = fit_comm_for(hcomm, True)
+    assert isinstance(fc, HostComm) and fit_comm_for(hcomm, False) is hcomm
+    th_vf_h, info_vf_h = _vf_fit(rows, fc)
     if rank == 0:
-        q.put((th, dict(stats), diag["k"], merged, th_vf, dict(info_vf)))
+        q.put((th, dict(stats), diag["k"], merged, th_vf, dict(info_vf), th_vf_h, dict(info_vf_h)))
     dist.destroy_process_group()
 
 
@@ -119,7 +128,7 @@ def test_two_rank_update_equals_single_rank_and_oracle():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    th2, stats2, k2, merged, thv2, infov2 = _get(q, procs, 300)
+    th2, stats2, k2, merged, thv2, infov2, thv2h, infov2h = _get(q, procs, 300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -162,4 +171,7 @@ def test_two_rank_update_equals_single_rank_and_oracle():
     assert np.abs(thv1 - thw.astype(np.float32)).max() <= 1e-5 * move
     for k in ("loss_before", "loss_after", "mse_before", "mse_after"):
         np.testing.assert_allclose(infov2[k], infov1[k], rtol=1e-6)
+    # host-group reductions: the same sums, the same fit
+    np.testing.assert_array_equal(thv2h, thv2)
+    assert infov2h == infov2
     assert infov1["loss_after"] < infov1["loss_before"]

@@ -125,3 +125,68 @@ def test_ppo_agents_run_iterations(agent):
     seen = []
     run_policy_gradient_algorithm(env, ag, callback=lambda st: seen.append(dict(st)), usercfg=cfg)
     assert len(seen) == 2 and all(np.isfinite(st["pol_kl_after"]) for st in seen)
+
+
+# ---------------------------------------------------------------- against the reference's own updaters
+# tests/golden/ppo_update.npz: PpoLbfgsUpdater.__call__ / PpoSgdUpdater.__call__ of the
+# reference executed (tests/golden/make_golden.py; Theano graphs injected from torch
+# autograd), in float64 and floatX-faithful float32 (suffix f).  The device is held to
+# north_star's 1e-4 (theta relative to the step), or to twice the reference's own
+# float32-vs-float64 distance where that is larger (the default maxiter 25, lbg2: the
+# way trpo cat0 is held).
+PPO_KEYS = ["surr_before", "surr_after", "surr_change", "kl_before", "kl_after", "kl_change",
+            "ent_before", "ent_after", "ent_change"]
+
+
+def _golden_ppo(k, layered):
+    import os
+    from modular_rl_amd import _lib
+    from modular_rl_amd.core import Categorical, DiagGauss, StochPolicyMLP
+    from modular_rl_amd.nets import make_net
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "ppo_update.npz"))
+    head = "gauss" if k[2] == "g" else "softmax"
+    lbfgs = k.startswith("lb")
+    nin, nout = (11, 3) if head == "gauss" else ((4, 2) if lbfgs else (4, 3))
+    net = make_net(nin, nout, _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX, [64, 64],
+                   impl="layered" if layered else "auto")
+    th0 = d[k + "_theta0"]
+    net.set_flat(th0)
+    pol = StochPolicyMLP(net, DiagGauss(nout) if head == "gauss" else Categorical(nout))
+    split = bool(d[k + "_cfg"][3])
+    keys = PPO_KEYS + (["test_" + x for x in PPO_KEYS] if split else [])
+    want = d[k + "_theta1"]
+    step = np.abs(want - th0).max()
+    tol = max(1e-4, 2 * np.abs(d[k + "f_theta1"] - want).max() / step)
+    return d, head, pol, th0, want, step, tol, keys
+
+
+@pytest.mark.parametrize("layered", [False, True])
+@pytest.mark.parametrize("k", ["lbg0", "lbg1", "lbc0", "lbg2"])
+def test_ppo_lbfgs_matches_reference_golden(k, layered):
+    from modular_rl_amd.ppo import PpoLbfgsUpdater
+    d, head, pol, th0, want, step, tol, keys = _golden_ppo(k, layered)
+    kt, maxiter, rev, split, kc0 = d[k + "_cfg"]
+    up = PpoLbfgsUpdater(pol, dict(kl_target=kt, maxiter=int(maxiter), reverse_kl=int(rev), do_split=int(split)))
+    up.kl_coeff = float(kc0)
+    info = up.update(_batch(d[k + "_ob"], d[k + "_act"], d[k + "_adv"], d[k + "_oldprob"], head))
+    th1 = pol.get_flat().astype(np.float64)
+    assert np.abs(th1 - want).max() <= tol * step, (np.abs(th1 - want).max() / step, tol)
+    np.testing.assert_allclose([info[x] for x in keys], d[k + "_info"], rtol=max(tol, 1e-4), atol=1e-6)
+    assert up.kl_coeff == d[k + "_kl_coeff"]
+
+
+@pytest.mark.parametrize("layered", [False, True])
+@pytest.mark.parametrize("k", ["sgg0", "sgc0", "sgg1"])
+def test_ppo_sgd_matches_reference_golden(k, layered):
+    from modular_rl_amd.ppo import PpoSgdUpdater
+    d, head, pol, th0, want, step, tol, keys = _golden_ppo(k, layered)
+    kt, epochs, lr, split, kc0, seed = d[k + "_cfg"]
+    up = PpoSgdUpdater(pol, dict(kl_target=kt, epochs=int(epochs), stepsize=lr, do_split=int(split)))
+    up.kl_coeff = float(kc0)
+    N = d[k + "_ob"].shape[0]
+    np.random.seed(int(seed))  # the epoch permutations the reference drew
+    info = up.update(_batch(d[k + "_ob"], d[k + "_act"], d[k + "_adv"], np.zeros((N, 1)), head))
+    th1 = pol.get_flat().astype(np.float64)
+    assert np.abs(th1 - want).max() <= tol * step, (np.abs(th1 - want).max() / step, tol)
+    np.testing.assert_allclose([info[x] for x in keys], d[k + "_info"], rtol=1e-4, atol=1e-6)
+    assert up.kl_coeff == d[k + "_kl_coeff"]

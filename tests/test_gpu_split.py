@@ -1,0 +1,106 @@
+"""The split-operand Fisher product (csrc/mlp_split.hip: fp32 operands split exactly into
+three bf16 parts, the part products on bf16 MFMA with f32 accumulation) against the
+float64 oracle at north_star's 1e-4 and against the exact-f32 kernels to f32 rounding."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import trpo_np as T
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("gauss", 11, 3), ("softmax", 4, 2), ("gauss", 17, 6), ("softmax", 6, 5), ("gauss", 32, 8)]
+
+
+def _dev(a, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).cuda()
+
+
+def _rel(a, b):
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+@pytest.mark.parametrize("head,nin,nout", CASES)
+@pytest.mark.parametrize("N", [1, 33, 3001])
+def test_split_fisher_product(head, nin, nout, N, monkeypatch):
+    monkeypatch.setenv("MRL_FISHER", "split")
+    monkeypatch.setenv("MRL_VJP_SPLIT", "1")
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import MlpNet
+    rng = np.random.default_rng(nin * 7 + N)
+    spec = T.Spec(nin, [64, 64], nout, head)
+    th = T.mlp_init(rng, spec.shapes, head == "gauss") + 0.05 * rng.standard_normal(spec.P)
+    if head == "gauss":
+        th[-nout:] = 0.3 * rng.standard_normal(nout)
+    th = th.astype(np.float32).astype(np.float64)
+    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
+    oldprob = T.policy_prob(spec, th + 0.01 * rng.standard_normal(spec.P), ob).astype(np.float32).astype(np.float64)
+    act = T.sample(spec, oldprob, rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N))
+    adv = rng.standard_normal(N).astype(np.float32).astype(np.float64)
+    v = rng.standard_normal(spec.P).astype(np.float32)
+    net = MlpNet(nin, nout, _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX)
+    assert net.fisher_split
+    net.set_flat(th)
+    x, vt = _dev(ob), _dev(v)
+    a = _dev(act, torch.int32 if head == "softmax" else torch.float32)
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    gh = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(adv), oldprob=_dev(oldprob), ghead=gh,
+             partial=partial)
+    # exact-f32 kernel (f32 tangent image) and the split kernel (split tangent image)
+    img32 = torch.zeros_like(net.image)
+    net.pack(theta=vt, image=img32, fwd_only=True)
+    gh32 = torch.zeros_like(gh)
+    net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=gh32, tangent=vt, image_t=img32)
+    imgs = net.new_tangent_image()
+    net.pack_tangent(vt, imgs)
+    ghs = torch.full_like(gh, float("nan"))
+    net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=ghs, tangent=vt, image_t=imgs)
+    a32, asp = gh32.cpu().numpy(), ghs.cpu().numpy()
+    assert np.isfinite(asp).all()
+    # the same rows to f32 rounding (different summation order of exact products)
+    np.testing.assert_allclose(asp, a32, rtol=2e-5, atol=2e-6 * np.abs(a32).max())
+    fv = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(x, N, ghs, fv)  # the split VJP (policy net, cached)
+    want = T.fisher_vector_product(spec, th, v.astype(np.float64), ob)
+    assert _rel(fv.cpu().numpy(), want) < 1e-4
+    # the split VJP against the exact-f32 VJP on the same head rows: f32 rounding apart
+    fs, f32 = torch.zeros_like(fv), torch.zeros_like(fv)
+    net.vjp_flat(x, N, gh32, fs)
+    monkeypatch.setenv("MRL_VJP_SPLIT", "0")
+    net.vjp_flat(x, N, gh32, f32)
+    assert _rel(fs.cpu().numpy(), f32.cpu().numpy()) < 1e-5
+    assert _rel(f32.cpu().numpy(), want) < 1e-4
+
+
+def test_split_image_parts_sum_to_the_f32_weights():
+    """The split image's three bf16 parts of every weight add up to the f32 weight
+    exactly (the exact split the kernel's products rely on)."""
+    import os
+    os.environ["MRL_FISHER"] = "split"
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import MlpNet
+    net = MlpNet(11, 3, _lib.HEAD_GAUSS)
+    rng = np.random.default_rng(1)
+    th = (rng.standard_normal(net.P) * np.exp(rng.uniform(-20, 5, net.P))).astype(np.float32)
+    net.set_flat(th)
+    img = net.image_s.cpu().numpy().view(np.uint32)
+    w = int(net.lib.mrl_mlp_image_words_bf16(__import__("ctypes").byref(net.desc)))
+    fa0 = 64 + 64 + 2 * 8 * 32 + 16
+    fwd_words = fa0 + 2 * 1 * 64 * 4 + 2 * 4 * 64 * 4
+    FW, BW = fwd_words - fa0, w - fwd_words
+    def bf(u):  # bf16 bits (low / high halves of the words) -> f32
+        return (u.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+    for lo, n in ((fa0, FW), (fa0 + 3 * FW, BW)):
+        stride = FW if lo == fa0 else BW
+        parts = [img[lo + p * stride: lo + p * stride + n] for p in range(3)]
+        for half in (0, 1):
+            vals = [bf((pp >> (16 * half)) & 0xFFFF) for pp in parts]
+            tot = vals[0] + vals[1] + vals[2]
+            # every weight is an f32 value and the three parts reproduce it exactly
+            assert np.array_equal(tot.astype(np.float32).astype(np.float64), tot)
+            assert np.all(np.abs(vals[1]) <= np.abs(vals[0]) * 2.0 ** -7 + 1e-45)
+    w32 = set(np.abs(th).astype(np.float64).tolist()) | {0.0}
+    tot0 = np.abs(bf(img[fa0:fa0 + FW] & 0xFFFF) + bf(img[fa0 + FW:fa0 + 2 * FW] & 0xFFFF) +
+                  bf(img[fa0 + 2 * FW:fa0 + 3 * FW] & 0xFFFF))
+    assert set(tot0.tolist()) <= w32
