@@ -73,11 +73,10 @@ def test_split_fisher_product(head, nin, nout, N, monkeypatch):
     assert _rel(f32.cpu().numpy(), want) < 1e-4
 
 
-def test_split_image_parts_sum_to_the_f32_weights():
+def test_split_image_parts_sum_to_the_f32_weights(monkeypatch):
     """The split image's three bf16 parts of every weight add up to the f32 weight
     exactly (the exact split the kernel's products rely on)."""
-    import os
-    os.environ["MRL_FISHER"] = "split"
+    monkeypatch.setenv("MRL_FISHER", "split")
     from modular_rl_amd import _lib
     from modular_rl_amd.nets import MlpNet
     net = MlpNet(11, 3, _lib.HEAD_GAUSS)
