@@ -230,9 +230,18 @@ class IterationRunner:
             vf_net = getattr(getattr(agent, "baseline", None), "net", None)
             if split is not None and hasattr(vf_net, "size_for_cus"):
                 vf_net.size_for_cus(len(split[1]))
-            if pipeline and split is not None:
-                self.rollout_stream = streams.masked_stream(split[0])
-                self.fit_stream = streams.masked_stream(split[1])
+            cosched = (pipeline and split is None and getattr(collector, "wave_per_env", False)
+                       and os.environ.get("MRL_COSCHED_FIT", "0") == "1")
+            if cosched:
+                # Humanoid's wave-per-env step wants every CU (E / 4), so no disjoint split:
+                # the fit of iteration k shares the CUs with the rollout of k+1 (two plain
+                # streams; one wave per SIMD in the step kernel leaves issue slots free)
+                self.rollout_stream = torch.cuda.Stream()
+                self.fit_stream = torch.cuda.Stream()
+            if pipeline and (split is not None or cosched):
+                if not cosched:
+                    self.rollout_stream = streams.masked_stream(split[0])
+                    self.fit_stream = streams.masked_stream(split[1])
                 # the iteration's own work runs on a non-blocking stream: an event recorded
                 # on the legacy NULL stream would wait for the rollout stream's work and
                 # serialise the fit behind it

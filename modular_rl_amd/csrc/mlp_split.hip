@@ -129,6 +129,16 @@ __device__ inline void mfma_split(const float* img, int seg, int PS, int f, int 
 #ifndef MRL_SPLIT_NPROD
 #define MRL_SPLIT_NPROD 6
 #endif
+// diagnostic switch: explicit wait states after each MFMA chain, before the VALU reads of
+// its accumulator (tools/determinism_probe.py)
+#ifndef MRL_SPLIT_NOPS
+#define MRL_SPLIT_NOPS 0
+#endif
+__device__ inline void mfma_drain() {
+#if MRL_SPLIT_NOPS
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#endif
+}
 
 template <int SH>
 __device__ inline void split_shape(RowsArgs& a, BDims& b) {
@@ -201,6 +211,7 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, 2) void mlp_fvp_split_kernel(Rows
         mfma_split<MRL_SPLIT_NPROD>(imt, b.fa0, PS, 1 * b.KS0B + s0, lane, xs, dh[1]);
       }
     }
+    mfma_drain();
     mul_dtanh16(dh[0], h1[0]);
     mul_dtanh16(dh[1], h1[1]);
     // layer 1 tangent per output tile: da = (dh W1 + h1 dW1 + db1) (1 - h2^2)
@@ -226,6 +237,7 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, 2) void mlp_fvp_split_kernel(Rows
       __builtin_amdgcn_sched_barrier(0);
       f32x16 h2;
       cache_load(ct, lane, 2 + mo, h2);
+      mfma_drain();
       mul_dtanh16(da, h2);
       // the head on the f32 VALU: dz = da . W2 + h2 . dW2 (+ db2 in head_finish), z = h2 . W2
       if (need_z) head_partial_mt(img, dd, h2, mo, h, z);

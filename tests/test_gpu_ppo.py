@@ -171,7 +171,10 @@ def test_ppo_lbfgs_matches_reference_golden(k, layered):
     info = up.update(_batch(d[k + "_ob"], d[k + "_act"], d[k + "_adv"], d[k + "_oldprob"], head))
     th1 = pol.get_flat().astype(np.float64)
     assert np.abs(th1 - want).max() <= tol * step, (np.abs(th1 - want).max() / step, tol)
-    np.testing.assert_allclose([info[x] for x in keys], d[k + "_info"], rtol=max(tol, 1e-4), atol=1e-6)
+    # each info entry to 1e-4, or to twice the reference's own float32-vs-float64 distance
+    want_i, floor_i = d[k + "_info"], np.abs(d[k + "f_info"] - d[k + "_info"])
+    got = np.array([info[x] for x in keys])
+    assert (np.abs(got - want_i) <= np.maximum(1e-4 * np.abs(want_i) + 1e-6, 2 * floor_i)).all(), (got, want_i)
     assert up.kl_coeff == d[k + "_kl_coeff"]
 
 

@@ -4,7 +4,7 @@
 set -e
 name=$1; shift
 out=tools/ablate/$name; mkdir -p $out
-for f in mlp_kernels mlp_bf16 scan rollout gemm gemm_bf16 runtime; do
+for f in mlp_kernels mlp_bf16 mlp_split scan rollout gemm gemm_bf16 runtime; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude "$@" \
     -c modular_rl_amd/csrc/$f.hip -o $out/$f.o &
 done

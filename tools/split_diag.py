@@ -39,3 +39,16 @@ for N in (3001, 65536, 1 << 22):
     if big.sum():
         rows = np.nonzero(big)[0][:5]
         print("  f32  :", a[rows][:, :3], "\n  split:", b[rows][:, :3], flush=True)
+        # float64 truth of the mean-head rows: central differences of the oracle forward
+        sys.path.insert(0, '.')
+        from oracle import trpo_np as T
+        spec = T.Spec(nin, [64, 64], nout, "gauss")
+        th = net.theta.double().cpu().numpy()
+        vv = v.double().cpu().numpy()
+        xr = x[rows].double().cpu().numpy()
+        eps = 1e-3
+        mp = T.policy_prob(spec, th + eps * vv, xr)[:, :nout]
+        mm = T.policy_prob(spec, th - eps * vv, xr)[:, :nout]
+        sd = np.exp(th[-nout:])
+        want = (mp - mm) / (2 * eps) / sd ** 2 / N
+        print("  f64  :", want, flush=True)
