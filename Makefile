@@ -10,6 +10,11 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-functi
 
 all: $(LIB)
 
+# mlp_split.hip: no SLP vectorisation -- the packed-f32 (v_pk_fma_f32) head sums it formed
+# gave run-to-run different results in a few 16-row groups per 4 M rows on gfx950
+# (tools/determinism_probe.py); the explicit packed builtins stay
+build/mlp_split.o: HIPFLAGS += -fno-slp-vectorize
+
 build/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

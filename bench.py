@@ -252,6 +252,17 @@ def rollout_latency_roofline(ki, key, pmc, K, layered=False):
     return out
 
 
+def fisher_arith(net):
+    """How the line's Fisher-vector products multiply (config.fisher_product)."""
+    if getattr(net, "layered", False) or getattr(net, "bf16", False):
+        return "as the MLP dtype"
+    jvp = "split-operand bf16 MFMA (fp32 operands split exactly into 3 bf16 parts, f32 accumulate)" \
+        if getattr(net, "fisher_split", False) else "exact f32 MFMA"
+    vjp = "split-operand bf16 MFMA" if getattr(net, "fisher_split", False) and \
+        os.environ.get("MRL_VJP_SPLIT", "0") != "0" else "exact f32 MFMA"
+    return {"jvp_rows": jvp, "vjp": vjp}
+
+
 def policy_gemm_roofline(kern, kinfo, net, dtype, n_rows, K, pmc, gemm_pmc):
     """north_star's "MFMA roofline for the policy GEMM" (agentzoo.py:34-37 Dense layers):
     the policy MLP's largest GEMM binary by device time per iteration -- on the fused
@@ -415,6 +426,7 @@ def main():
         vjp = vjp_binary_entry(kern, fpr["fvp_vjp"], None if vf_net.layered else flops_per_row(vf_net)["fvp_vjp"],
                                n_local, K)
         if vjp is not None:
+            vjp["bytes_per_row"] = row_b  # the Fisher-product launch's algorithmic bytes (PMC: the same)
             kinfo[VJP_BINARY[args.dtype]] = vjp
     if "rollout_steps" in kern:
         # one timed region per iteration around the rollout's launches (the persistent
@@ -470,7 +482,8 @@ def main():
                              f"({'layered GEMM' if agent.policy.net.layered else 'fused'} path)",
                    "mlp_dtype": args.dtype, "gamma": 0.995, "lam": 0.97,
                    "max_kl": 0.01, "cg_damping": 0.1,
-                   "vf_fit_beside_next_rollout": runner.pipeline},
+                   "vf_fit_beside_next_rollout": runner.pipeline,
+                   "fisher_product": fisher_arith(agent.policy.net)},
         "trpo_iters_per_sec": round(K / elapsed, 4),
         "rollout_env_steps_per_sec": round(n_local * world * K / (phases["rollout"] * 1e-3), 1),
         "phase_ms_per_iter": {k: round(v / K, 3) for k, v in phases.items()},

@@ -134,6 +134,18 @@ __device__ inline void mfma_split(const float* img, int seg, int PS, int f, int 
 #ifndef MRL_SPLIT_NOPS
 #define MRL_SPLIT_NOPS 0
 #endif
+// scheduling fences between the passes' phases (0: let the compiler interleave one
+// phase's VALU splits with the previous phase's MFMAs)
+#ifndef MRL_SPLIT_FENCES
+#define MRL_SPLIT_FENCES 1
+#endif
+#if MRL_SPLIT_FENCES
+#define VJP_SPLIT_FENCE() __builtin_amdgcn_sched_barrier(0)
+#define FVP_SPLIT_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define VJP_SPLIT_FENCE() ((void)0)
+#define FVP_SPLIT_FENCE() ((void)0)
+#endif
 __device__ inline void mfma_drain() {
 #if MRL_SPLIT_NOPS
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
@@ -154,13 +166,24 @@ __device__ inline void split_shape(RowsArgs& a, BDims& b) {
   }
 }
 
-constexpr int SPLIT_ROWS_BLOCK = 256;
+// waves per block of the JVP rows kernel: 4 (two blocks per CU at 2 waves per SIMD: the
+// staged images take 67 KB of LDS per block) or 12 (one block per CU at 3 waves per SIMD)
+#ifndef MRL_SPLIT_ROWS_WAVES
+#define MRL_SPLIT_ROWS_WAVES 4
+#endif
+constexpr int SPLIT_ROWS_WAVES = MRL_SPLIT_ROWS_WAVES;
+constexpr int SPLIT_ROWS_BLOCK = 64 * SPLIT_ROWS_WAVES;
 
 // The Fisher product's forward half (trpo.py:45-58): JVP of the head along the tangent
 // from the cached f32 h1 / h2, then the KL-metric head-gradient rows (row_epilogue FVP),
 // exactly what mlp_rows_kernel<EPI_FVP_CACHED> computes, with split-operand products.
+#ifndef MRL_SPLIT_FVP_OCC  // waves per SIMD the JVP rows kernel is compiled for
+#define MRL_SPLIT_FVP_OCC 2
+#endif
 template <int SH>
-__global__ __launch_bounds__(SPLIT_ROWS_BLOCK, 2) void mlp_fvp_split_kernel(RowsArgs a, BDims b,
+__global__ __launch_bounds__(SPLIT_ROWS_BLOCK, (4 * MRL_SPLIT_FVP_OCC / SPLIT_ROWS_WAVES > 0
+                                                 ? 4 * MRL_SPLIT_FVP_OCC / SPLIT_ROWS_WAVES : 1))
+    void mlp_fvp_split_kernel(RowsArgs a, BDims b,
                                                                            const float* __restrict__ img_g,
                                                                            const float* __restrict__ imt_g,
                                                                            const int32_t* __restrict__ skip) {
@@ -188,7 +211,8 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, 2) void mlp_fvp_split_kernel(Rows
   const bool need_z = a.head != MRL_HEAD_GAUSS;  // the DiagGauss metric does not use the mean
   double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
   const int64_t ntiles = (a.n + 31) / 32;
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+  for (int64_t tile = (int64_t)blockIdx.x * SPLIT_ROWS_WAVES + wave; tile < ntiles;
+       tile += (int64_t)gridDim.x * SPLIT_ROWS_WAVES) {
     const int64_t row = tile * 32 + (lane & 31);
     const bool valid = row < a.n;
     XGlobalNB xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
@@ -227,14 +251,14 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, 2) void mlp_fvp_split_kernel(Rows
         split8(dh[s >> 1], s & 1, ps);
         mfma_split<MRL_SPLIT_NPROD>(img, b.fa1, PS, mo * 4 + s, lane, ps, da);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      FVP_SPLIT_FENCE();
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         bf16x8 ps[3];
         split8(h1[s >> 1], s & 1, ps);
         mfma_split<MRL_SPLIT_NPROD>(imt, b.fa1, PS, mo * 4 + s, lane, ps, da);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      FVP_SPLIT_FENCE();
       f32x16 h2;
       cache_load(ct, lane, 2 + mo, h2);
       mfma_drain();
@@ -243,7 +267,7 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, 2) void mlp_fvp_split_kernel(Rows
       if (need_z) head_partial_mt(img, dd, h2, mo, h, z);
       head_partial_mt(img, dd, da, mo, h, dz);
       head_partial_mt(imt, dd, h2, mo, h, dzt);
-      __builtin_amdgcn_sched_barrier(0);
+      FVP_SPLIT_FENCE();
     }
     if (need_z) head_finish(img, dd, z);
 #pragma unroll
@@ -417,7 +441,7 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_split_kernel(VjpSplitArgs a_in
         for (int sp = 0; sp < 2; ++sp) mma_split<MRL_SPLIT_NPROD>(hT[sp], gT[sp], gW2[m]);
       }
     }
-    __builtin_amdgcn_sched_barrier(0);
+    VJP_SPLIT_FENCE();
     // ga2 as F-fragment parts (A operand of gh1) and T-fragment parts (B operand of gW1)
     bf16x8 gaF[4][3], gaT[2][2][3];  // [s][p], [m][sp][p]
 #pragma unroll
@@ -449,7 +473,7 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_split_kernel(VjpSplitArgs a_in
         xT[1][p] = pack8(t, 1);
       }
     }
-    __builtin_amdgcn_sched_barrier(0);
+    VJP_SPLIT_FENCE();
     // per u1 tile: gh1 (T layout) = ga2 . W1^T, ga1 = gh1 (1 - h1^2), then
     // gW1 += H1^T GA2 and gW0 += X^T GA1
 #pragma unroll
@@ -485,7 +509,7 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_split_kernel(VjpSplitArgs a_in
         mma_split<MRL_SPLIT_NPROD>(hT[sp], gaT[1][sp], gW1[no][1]);
         mma_split<MRL_SPLIT_NPROD>(xT[sp], g1[sp], gW0[no]);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      VJP_SPLIT_FENCE();
     }
   }
 
@@ -548,14 +572,16 @@ static int static_shape_split(const mrl_mlp_desc* d) {
 #endif
 }
 
-// grid: two resident rounds of 2 blocks per CU (MRL_SPLIT_BLOCKS overrides)
+// grid: two resident rounds (MRL_SPLIT_BLOCKS overrides)
 static int64_t split_rows_blocks(int64_t n) {
   static const int64_t env_cap = [] {
     const char* e = getenv("MRL_SPLIT_BLOCKS");
     return (int64_t)(e ? atoi(e) : 0);
   }();
-  const int64_t cap = env_cap > 0 ? env_cap : 1024;
-  int64_t g = ((n + 31) / 32 + 3) / 4;
+  // two resident rounds: 256 CUs x (4 waves per SIMD worth of blocks)
+  const int64_t cap = env_cap > 0 ? env_cap : 2 * 256 * (4 * MRL_SPLIT_FVP_OCC / SPLIT_ROWS_WAVES > 0
+                                                         ? 4 * MRL_SPLIT_FVP_OCC / SPLIT_ROWS_WAVES : 1);
+  int64_t g = ((n + 31) / 32 + SPLIT_ROWS_WAVES - 1) / SPLIT_ROWS_WAVES;
   if (g < 1) g = 1;
   return g > cap ? cap : g;
 }

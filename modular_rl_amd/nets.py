@@ -128,8 +128,9 @@ class MlpNet:
         self.use_cache = True
         self._cache_key = None
         # fp32 Fisher products on bf16 MFMA with exactly split operands (csrc/mlp_split.hip):
-        # MRL_FISHER=split | f32 (default: the exact-f32 MFMA kernels)
-        self.fisher_split = (not self.bf16) and os.environ.get("MRL_FISHER", "f32") == "split"
+        # MRL_FISHER=split (default) | f32 (the exact-f32 MFMA kernels); MRL_VJP_SPLIT=1 also
+        # runs the cached VJP on split operands (measured slower, off)
+        self.fisher_split = (not self.bf16) and os.environ.get("MRL_FISHER", "split") == "split"
         self.image_s = None
         if self.fisher_split:
             w = int(self.lib.mrl_mlp_image_words_split(ctypes.byref(self.desc)))

@@ -137,3 +137,50 @@ def test_humanoid_agent_iterations():
     assert len(seen) == 2
     for st in seen:
         assert np.isfinite(st["EpRewMean"]) and st["pol_kl_after"] <= 1.5 * 0.01
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_c5_width_rollout_invariants_and_update(dtype):
+    """C5 at its per-GPU width (1024 Humanoid-v2 envs x 1024 steps, the
+    376-512-512-512-17 policy, the wave-per-env step on all 256 CUs, captured graph):
+    the size-independent properties of the lock-step batch (as the C3 full-size test:
+    episode counters, terminations, the ZFilter clip and count, episode lengths adding up
+    to the horizon, finite rewards, std = exp(logstd) rows), then one TRPO iteration whose
+    step stays in the trust region: line search accepted, lm finite and positive, KL after
+    the step within 2 max_kl, the surrogate improved."""
+    from modular_rl_amd.agentzoo import TrpoAgent
+    from modular_rl_amd.core import IterationRunner
+    from modular_rl_amd.envs import make
+    env = make("Humanoid-v2")
+    E, Tn, max_kl = 1024, 1024, 0.01
+    cfg = dict(timestep_limit=env.spec.max_episode_steps, gamma=0.995, lam=0.97, max_kl=max_kl, cg_damping=0.1,
+               n_envs=E, horizon=Tn, filter=1, seed=3, hid_sizes=[512, 512, 512], activation="tanh", use_graph=1,
+               mlp_dtype=dtype)
+    agent = TrpoAgent(env.observation_space, env.action_space, cfg)
+    col = agent.make_collector(env, cfg)
+    assert col.layered and col.wave_per_env
+    runner = IterationRunner(agent, col, cfg, pipeline=False)
+    stats = runner.step()
+    torch.cuda.synchronize()
+    flags = col.flags.cpu().numpy().reshape(Tn, E)
+    ep_t = col.ep_t.cpu().numpy().reshape(Tn, E).astype(np.int64)
+    last, term = (flags & 1) > 0, (flags & 2) > 0
+    assert not (term & ~last).any()
+    assert (ep_t[0] == 0).all() and last[-1].all()
+    np.testing.assert_array_equal(ep_t[1:], np.where(last[:-1], 0, ep_t[:-1] + 1))
+    np.testing.assert_array_equal(np.where(last, ep_t + 1, 0).sum(0), np.full(E, Tn))
+    assert term.any()  # the articulated Humanoid falls within the horizon under a random policy
+    obs = col.obs.cpu().numpy()
+    assert np.isfinite(obs).all() and np.abs(obs).max() <= 5.0
+    (n, _, var), (nr, _, _) = col.filter_stats()
+    assert n == E * Tn and nr == E * Tn and np.isfinite(var).all()
+    assert np.isfinite(col.rew.cpu().numpy()).all()
+    prob = col.prob.cpu().numpy().reshape(Tn * E, -1)
+    np.testing.assert_array_equal(prob[:, 17:], np.broadcast_to(prob[:1, 17:], prob[:, 17:].shape))
+    # the update
+    dg = agent.updater.last_diag
+    assert dg["success"] and 0 <= dg["k"] < 10, dg
+    assert np.isfinite(dg["lm"]) and dg["lm"] > 0
+    assert 0 <= stats["pol_kl_after"] <= 2 * max_kl, stats["pol_kl_after"]
+    assert stats["pol_surr_after"] < stats["pol_surr_before"]
+    assert np.isfinite(stats["vf_loss_after"]) and stats["vf_loss_after"] <= stats["vf_loss_before"]

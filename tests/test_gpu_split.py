@@ -103,3 +103,33 @@ def test_split_image_parts_sum_to_the_f32_weights(monkeypatch):
     tot0 = np.abs(bf(img[fa0:fa0 + FW] & 0xFFFF) + bf(img[fa0 + FW:fa0 + 2 * FW] & 0xFFFF) +
                   bf(img[fa0 + 2 * FW:fa0 + 3 * FW] & 0xFFFF))
     assert set(tot0.tolist()) <= w32
+
+
+def test_split_fisher_product_is_deterministic(monkeypatch):
+    """The same split JVP-rows launch on the same 1 M rows gives the same bits every time
+    (an SLP-vectorised build of the kernel did not: a few 16-row groups per 4 M rows
+    differed run to run in one head column; Makefile builds mlp_split.hip without SLP)."""
+    monkeypatch.setenv("MRL_FISHER", "split")
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import MlpNet, glorot_init
+    N = 1 << 20
+    rng = np.random.default_rng(0)
+    net = MlpNet(11, 3, _lib.HEAD_GAUSS)
+    net.set_flat(glorot_init(rng, 11, 3, _lib.HEAD_GAUSS))
+    g = torch.Generator(device="cuda").manual_seed(0)
+    x = torch.randn(N, 11, device="cuda", generator=g)
+    act = torch.randn(N, 3, device="cuda", generator=g)
+    adv = torch.randn(N, device="cuda", generator=g)
+    prob = net.forward(x, N).clone()
+    gh = torch.zeros(N * net.gh, device="cuda")
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=act, adv=adv, oldprob=prob, ghead=gh, partial=partial)
+    v = torch.randn(net.P, device="cuda", generator=g) * 1e-2
+    imgt = net.new_tangent_image()
+    net.pack_tangent(v, imgt)
+    outs = []
+    for _ in range(4):
+        net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=gh, tangent=v, image_t=imgt)
+        outs.append(gh.clone())
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])

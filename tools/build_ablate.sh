@@ -5,7 +5,8 @@ set -e
 name=$1; shift
 out=tools/ablate/$name; mkdir -p $out
 for f in mlp_kernels mlp_bf16 mlp_split scan rollout gemm gemm_bf16 runtime; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude "$@" \
+  extra=""; [ $f = mlp_split ] && extra="-fno-slp-vectorize"  # as the Makefile
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude $extra "$@" \
     -c modular_rl_amd/csrc/$f.hip -o $out/$f.o &
 done
 wait
