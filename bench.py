@@ -363,8 +363,8 @@ def main():
              "trpo_update": ("upd0", "upd1")}
     recs = []
 
-    for _ in range(args.warmup):
-        runner.step()
+    for i in range(args.warmup):
+        runner.step(prelaunch_next=i + 1 < args.warmup)
     runner.drain()
     timing.enable(True)
     comm.barrier()
@@ -372,8 +372,8 @@ def main():
     t0 = time.perf_counter()
     # K whole iterations: K rollouts, advantages, VF fits and policy updates (the last
     # VF fit drains inside the timed region)
-    for _ in range(args.steps):
-        runner.step()
+    for i in range(args.steps):
+        runner.step(prelaunch_next=i + 1 < args.steps)  # the next rollout issued as theta is final
         recs.append(runner.last_phase_events)
     runner.drain()
     recs.append(runner.last_drain_events if runner.pipeline else {})

@@ -160,8 +160,8 @@ def run_policy_gradient_algorithm(env, agent, usercfg=None, callback=None):
         # after this callback must read the live state
         agent._snapshot_capture = None
 
-    for _ in range(cfg["n_iter"]):
-        done = runner.step()
+    for i in range(cfg["n_iter"]):
+        done = runner.step(prelaunch_next=i + 1 < cfg["n_iter"])
         if done is not None:
             emit(done)
     done = runner.drain()
@@ -218,6 +218,7 @@ class IterationRunner:
         self.agent, self.col, self.cfg = agent, collector, cfg
         self.comm = comm if comm is not None else Comm()
         self.pending = None
+        self._prelaunched = None  # events of a rollout issued by the previous step
         self.pipeline = False
         self.last_phase_events = None
         self.last_drain_events = {}
@@ -277,49 +278,79 @@ class IterationRunner:
         caller.wait_stream(self.main_stream)
         return out
 
-    def step(self):
-        return self._on_main(self._step)
+    def step(self, prelaunch_next=False):
+        """One iteration.  ``prelaunch_next``: another step follows, so the next
+        iteration's rollout is issued as soon as the policy update has set the new theta
+        (TrpoUpdater.after_theta) -- the stats, the snapshot capture and the loop's host
+        Python then run under that rollout instead of in front of it."""
+        return self._on_main(lambda: self._step(prelaunch_next))
 
-    def _step(self):
-        cfg, agent, col = self.cfg, self.agent, self.col
-        main = torch.cuda.current_stream()
-        ev = {}
-        done = None
+    def _launch_rollout(self):
+        """Issue one iteration's rollout (the noise fill and the step chain); its events."""
+        col, ev = self.col, {}
+        ev["rollout0"] = self._event()
         if self.pipeline:
-            ev["rollout0"] = self._event()
+            main = torch.cuda.current_stream()
             col.fill_noise()  # one wide kernel: on every CU, ahead of the step chain
             self.rollout_stream.wait_stream(main)
             with torch.cuda.stream(self.rollout_stream):
                 col.launch(fill_noise=False)
                 ev["rollout1"] = self._event()
+        else:
+            col.launch()
+            ev["rollout1"] = self._event()
+        return ev
+
+    def _step(self, prelaunch_next=False):
+        cfg, agent, col = self.cfg, self.agent, self.col
+        main = torch.cuda.current_stream()
+        ev = self._prelaunched if getattr(self, "_prelaunched", None) is not None else self._launch_rollout()
+        self._prelaunched = None
+        done = None
+        if self.pipeline:
             if self.pending is not None:
                 done = self._fit_pending(self.fit_stream, ev)
             main.wait_stream(self.rollout_stream)
-        else:
-            ev["rollout0"] = self._event()
-            col.launch()
-            ev["rollout1"] = self._event()
         batch = col.finish()
         ev["adv0"] = self._event()
         compute_advantage_batch(agent.baseline, batch, cfg["gamma"], cfg["lam"], self.comm)
         ev["adv1"] = self._event()
+        # the episode statistics read this batch's rewards / flags: issued before the next
+        # rollout (launched from the update below) can overwrite them
+        ep_dev = col.episode_stats_launch(batch)
         vf_stats = None
         if not self.pipeline:
             ev["vf0"] = self._event()
             vf_stats = agent.baseline.fit_batch(batch)
             ev["vf1"] = self._event()
         ev["upd0"] = self._event()
-        pol_stats = agent.updater.update(batch)
-        ev["upd1"] = self._event()
+        post = {}
+
+        def after_theta():
+            """The next iteration's theta is final: snapshot capture (the filter state and
+            RNG counters the next rollout advances), then that rollout."""
+            if "cap" in post:
+                return
+            ev["upd1"] = self._event()
+            post["cap"] = capture_state(agent, with_vf=False) if self.pipeline else None
+            if prelaunch_next:
+                self._prelaunched = self._launch_rollout()
+
+        upd = agent.updater
+        upd.after_theta = after_theta
+        try:
+            pol_stats = upd.update(batch)
+        finally:
+            upd.after_theta = None
+        after_theta()  # updaters without the hook
         if self.pipeline:
             # read back with the deferred VF fit's stats (no host sync here); the state at
             # the end of this iteration (the VF after its fit is added then) is captured
             # for snapshots taken in the callback that reports it
-            cap = capture_state(agent, with_vf=False)
-            self.pending = (batch, col.episode_stats_launch(batch), pol_stats, cap)
+            self.pending = (batch, ep_dev, pol_stats, post["cap"])
         else:
             agent._snapshot_capture = None
-            done = self._stats(col.episode_stats(batch), vf_stats, pol_stats)
+            done = self._stats(col.episode_stats_finish(ep_dev), vf_stats, pol_stats)
         self.last_phase_events = ev
         return done
 

@@ -202,6 +202,9 @@ class TrpoUpdater:
         self.ops = ops if ops is not None else HipTrpoOps(stochpol.net)
         self.loss_names = ["surr", "kl", "ent"]
         self.last_diag = {}
+        # set by core.IterationRunner: called once theta (and its image) is final, so the
+        # next iteration's rollout is issued before the stats / host bookkeeping
+        self.after_theta = None
 
     # EzFlat surface (core.py:544-554)
     def get_params_flat(self):
@@ -264,6 +267,8 @@ class TrpoUpdater:
         if host[7] <= 1e-8:
             print("got zero gradient. not updating")
             diag["skipped"] = True
+            if self.after_theta is not None:
+                self.after_theta()
         else:
             shs, lm, neggdotstepdir, rate = (float(v) for v in host[:4])
             if timing.enabled():
@@ -288,6 +293,8 @@ class TrpoUpdater:
             else:
                 net.theta.copy_(thprev)
             net.pack()
+            if self.after_theta is not None:
+                self.after_theta()
             diag.update(skipped=False, shs=shs, lm=lm, neggdotstepdir=neggdotstepdir, expected_rate=rate,
                         success=success, k=k, stepfrac=frac, cg_iters=int(host[10]), rdotr=float(host[8]),
                         ls=np.array(trace, dtype=np.float64))

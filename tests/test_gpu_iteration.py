@@ -8,7 +8,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(env_id, pipeline, n_iter=3, agent_cls="TrpoAgent", **kw):
+def _run(env_id, pipeline, n_iter=3, agent_cls="TrpoAgent", prelaunch=False, **kw):
     from modular_rl_amd import agentzoo
     from modular_rl_amd.core import IterationRunner
     from modular_rl_amd.envs import make
@@ -20,8 +20,8 @@ def _run(env_id, pipeline, n_iter=3, agent_cls="TrpoAgent", **kw):
     col = agent.make_collector(env, cfg)
     runner = IterationRunner(agent, col, cfg, pipeline=pipeline)
     stats = []
-    for _ in range(n_iter):
-        s = runner.step()
+    for i in range(n_iter):
+        s = runner.step(prelaunch_next=prelaunch and i + 1 < n_iter)
         if s is not None:
             stats.append(s)
     s = runner.drain()
@@ -35,9 +35,12 @@ def _run(env_id, pipeline, n_iter=3, agent_cls="TrpoAgent", **kw):
                                                  ("Hopper-v2", "PpoLbfgsAgent", {}),
                                                  ("Humanoid-v2", "TrpoAgent", dict(n_envs=128, horizon=16,
                                                                                    hid_sizes=[128, 96]))])
-def test_pipelined_loop_is_bit_identical(env_id, agent_cls, kw):
+@pytest.mark.parametrize("prelaunch", [False, True])
+def test_pipelined_loop_is_bit_identical(env_id, agent_cls, kw, prelaunch):
+    """...and with the next rollout issued from the update (prelaunch: as soon as theta is
+    final, before the stats / capture / loop Python), in both orders."""
     r0, a0, c0, s0 = _run(env_id, False, agent_cls=agent_cls, **kw)
-    r1, a1, c1, s1 = _run(env_id, True, agent_cls=agent_cls, **kw)
+    r1, a1, c1, s1 = _run(env_id, True, agent_cls=agent_cls, prelaunch=prelaunch, **kw)
     assert not r0.pipeline and r1.pipeline  # few rollout blocks: the CU split applies
     assert len(s0) == len(s1) == 3
     np.testing.assert_array_equal(a0.policy.net.get_flat(), a1.policy.net.get_flat())
@@ -57,3 +60,18 @@ def test_masked_streams_are_disjoint():
     R, V = streams.masked_stream(rc), streams.masked_stream(vc)
     assert streams.stream_cus(R) == rc and streams.stream_cus(V) == vc
     assert rollout_cu_split(n, n) is None
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_prelaunched_rollout_is_bit_identical(pipeline):
+    """Hopper, TRPO: the loop with every next rollout issued from the update equals the
+    plain loop bit for bit (parameters, filter, every reported stat)."""
+    r0, a0, c0, s0 = _run("Hopper-v2", pipeline, n_iter=4)
+    r1, a1, c1, s1 = _run("Hopper-v2", pipeline, n_iter=4, prelaunch=True)
+    np.testing.assert_array_equal(a0.policy.net.get_flat(), a1.policy.net.get_flat())
+    np.testing.assert_array_equal(a0.baseline.net.get_flat(), a1.baseline.net.get_flat())
+    np.testing.assert_array_equal(c0.filter_state.cpu().numpy(), c1.filter_state.cpu().numpy())
+    assert len(s0) == len(s1) == 4
+    for x, y in zip(s0, s1):
+        for k in x:
+            assert x[k] == y[k] or (np.isnan(x[k]) and np.isnan(y[k])), k
