@@ -546,6 +546,185 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_split_kernel(VjpSplitArgs a_in
   }
 }
 
+
+// ---- VJP, second form: no identity transposes.  The T-layout operands come straight
+// from memory (h1 / h2 gathered from the f32 cache in T order -- the tile was just
+// streamed, the gathers hit L2 --, the inputs and head rows from their row arrays) and
+// ga2 is formed in both layouts by MFMA (K = head outputs, one k-step): gh2_F = W2 . G
+// for gh1 and gh2_T = G . W2^T for gW1.  168 part MFMAs per 32-row tile instead of 198.
+// element (row j, unit w of 32-unit slot `slot`) of an f32 cache tile
+__device__ inline int cache_off_s(int slot, int j, int w) {
+  return ((slot * 4 + (w >> 3)) * 64 + 32 * ((w >> 2) & 1) + j) * 4 + (w & 3);
+}
+
+template <int SH>
+__global__ __launch_bounds__(256, 1) void mlp_vjp_split2_kernel(VjpSplitArgs a_in, const float* __restrict__ img_g,
+                                                               const int32_t* __restrict__ skip) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (skip != nullptr && *skip != 0) return;
+  const VjpSplitArgs a = vjp_shape_s<SH>(a_in);
+  const MlpDims& d = a.d;
+  const BDims& b = a.b;
+  const int BW = split_bw(b), f0 = split_fwd_words(b);
+  for (int i = threadIdx.x; i < 3 * BW / 4; i += 256)
+    reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img_g + f0)[i];
+  __syncthreads();
+  auto wfrag = [&](int seg, int p, int f, int lane) { return frag_at(lds, seg - b.fwd_words + p * BW, f, lane); };
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j32 = lane & 31;
+  const int A = d.A;
+  f32x16 gW2[2], gW1[2][2], gW0[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    gW2[m] = zero16();
+    gW0[m] = zero16();
+#pragma unroll
+    for (int n = 0; n < 2; ++n) gW1[m][n] = zero16();
+  }
+  float gb0[2] = {0.f, 0.f}, gb1[2] = {0.f, 0.f};
+  float gb2[MAX_OUT], gls[MAX_OUT];
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    gb2[o] = 0.f;
+    gls[o] = 0.f;
+  }
+  // T-layout lane roles: column c = lane & 31 (a unit, an input or a head output), register
+  // r of lane half h holds row cperm(r, h) of the tile
+  const int c = j32;
+  const int64_t ntiles = (a.n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t row0 = tile * 32, row = row0 + j32;
+    const int64_t rc = row < a.n ? row : 0;
+    float fv = (row < a.n && h == 0) ? 1.f : 0.f;
+    asm volatile("" : "+v"(fv));
+    const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
+    // F-layout h2 (tanh' of gh2_F); the T-layout operands are gathered phase by phase
+    f32x16 h2F[2];
+    cache_load(ct, lane, 2, h2F[0]);
+    cache_load(ct, lane, 3, h2F[1]);
+    // row of register r in a T tile, and its validity factor
+    auto trow = [&](int r) {
+      const int64_t rw = row0 + cperm(r, h);
+      return rw < a.n ? rw : (int64_t)0;
+    };
+    auto tval = [&](int r) {
+      float f = row0 + cperm(r, h) < a.n ? 1.f : 0.f;
+      asm volatile("" : "+v"(f));
+      return f;
+    };
+    auto gather_cache = [&](int slot, f32x16& t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t[r] = ct[cache_off_s(slot, cperm(r, h), c)];
+    };
+    const float* gp = a.ghead + rc * a.gh;
+    float g8[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+      g8[o] = o < A ? gp[o < A ? o : 0] * fv : 0.f;
+      gb2[o] += g8[o];
+    }
+#pragma unroll
+    for (int q = 0; q < MAX_OUT; ++q) gls[q] += q < a.n_sum ? gp[A + (q < a.n_sum ? q : 0)] * fv : 0.f;
+
+    bf16x8 gB[3];
+    split8v(g8, gB);
+    bf16x8 gs[2][3];  // G in T layout (D[row][o])
+    {
+      f32x16 gT;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gT[r] = (c < A ? a.ghead[trow(r) * a.gh + (c < A ? c : 0)] : 0.f) * tval(r);
+      split8(gT, 0, gs[0]);
+      split8(gT, 1, gs[1]);
+    }
+    // ga2 in both layouts (gb1 from the T one); gW2 += H2^T G
+    bf16x8 gaF[4][3], gaT[2][2][3];
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo) {
+      f32x16 h2T;
+      gather_cache(2 + mo, h2T);
+      const bf16x8 w[3] = {wfrag(b.bw2, 0, mo, lane), wfrag(b.bw2, 1, mo, lane), wfrag(b.bw2, 2, mo, lane)};
+      f32x16 gf = zero16(), gt = zero16();
+      mma_split<MRL_SPLIT_NPROD>(w, gB, gf);   // D[u2][row]
+      mma_split<MRL_SPLIT_NPROD>(gB, w, gt);   // D[row][u2]
+      mul_dtanh16(gf, h2F[mo]);
+      mul_dtanh16(gt, h2T);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gb1[mo] += gt[r];
+      split8(gf, 0, gaF[2 * mo]);
+      split8(gf, 1, gaF[2 * mo + 1]);
+      split8(gt, 0, gaT[mo][0]);
+      split8(gt, 1, gaT[mo][1]);
+      bf16x8 hs[2][3];
+      split8(h2T, 0, hs[0]);
+      split8(h2T, 1, hs[1]);
+      mma_split<MRL_SPLIT_NPROD>(hs[0], gs[0], gW2[mo]);
+      mma_split<MRL_SPLIT_NPROD>(hs[1], gs[1], gW2[mo]);
+    }
+    bf16x8 xs[2][3];
+    {
+      f32x16 xT;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xT[r] = (c < a.n_obs ? a.x[trow(r) * a.n_obs + (c < a.n_obs ? c : 0)] : 0.f) * tval(r);
+      split8(xT, 0, xs[0]);
+      split8(xT, 1, xs[1]);
+    }
+#pragma unroll
+    for (int no = 0; no < 2; ++no) {
+      f32x16 h1T;
+      gather_cache(no, h1T);
+      f32x16 ga1 = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 w[3] = {wfrag(b.bt1, 0, no * 4 + s, lane), wfrag(b.bt1, 1, no * 4 + s, lane),
+                             wfrag(b.bt1, 2, no * 4 + s, lane)};
+        mma_split<MRL_SPLIT_NPROD>(gaF[s], w, ga1);
+      }
+      mul_dtanh16(ga1, h1T);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gb0[no] += ga1[r];
+      bf16x8 hs[2][3], g1[2][3];
+      split8(h1T, 0, hs[0]);
+      split8(h1T, 1, hs[1]);
+      split8(ga1, 0, g1[0]);
+      split8(ga1, 1, g1[1]);
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        mma_split<MRL_SPLIT_NPROD>(hs[sp], gaT[0][sp], gW1[no][0]);
+        mma_split<MRL_SPLIT_NPROD>(hs[sp], gaT[1][sp], gW1[no][1]);
+        mma_split<MRL_SPLIT_NPROD>(xs[sp], g1[sp], gW0[no]);
+      }
+    }
+  }
+  float* out = a.slab + ((int64_t)blockIdx.x * 4 + wave) * d.P;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = cperm(r, h);
+      if (i < d.O) out[d.tW0 + i * HID + 32 * m + j32] = gW0[m][r];
+      if (j32 < A) out[d.tW2 + (32 * m + i) * A + j32] = gW2[m][r];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) out[d.tW1 + (32 * m + i) * HID + 32 * n + j32] = gW1[m][n][r];
+    }
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const float s0 = gb0[m] + __shfl_xor(gb0[m], 32);
+    const float s1 = gb1[m] + __shfl_xor(gb1[m], 32);
+    if (h == 0) {
+      out[d.tb0 + 32 * m + j32] = s0;
+      out[d.tb1 + 32 * m + j32] = s1;
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    const float sum = wave_sumf(gb2[o]);
+    if (lane == 0 && o < A) out[d.tb2 + o] = sum;
+  }
+  for (int q = 0; q < a.n_sum; ++q) {
+    const float sum = wave_sumf(gls[q]);
+    if (lane == 0) out[d.tls + q] = sum;
+  }
+}
+
 }  // namespace mrl
 
 using namespace mrl;
@@ -670,10 +849,19 @@ int mrl_mlp_vjp_split(const mrl_mlp_desc* d, const float* image, const float* x,
   const size_t shm = (size_t)3 * split_bw(a.b) * 4;
   const dim3 grid(blocks), blk(256);
   hipStream_t s = (hipStream_t)stream;
-  switch (static_shape_split(d)) {
-    case 1: hipLaunchKernelGGL((mlp_vjp_split_kernel<1>), grid, blk, shm, s, a, image, skip); break;
-    case 2: hipLaunchKernelGGL((mlp_vjp_split_kernel<2>), grid, blk, shm, s, a, image, skip); break;
-    default: hipLaunchKernelGGL((mlp_vjp_split_kernel<0>), grid, blk, shm, s, a, image, skip); break;
+  static const int form = [] {  // MRL_VJP_SPLIT=2: the transpose-free second form
+    const char* e = getenv("MRL_VJP_SPLIT");
+    return e ? atoi(e) : 1;
+  }();
+  const int sh = static_shape_split(d);
+  if (form == 2) {
+    if (sh == 1) hipLaunchKernelGGL((mlp_vjp_split2_kernel<1>), grid, blk, shm, s, a, image, skip);
+    else if (sh == 2) hipLaunchKernelGGL((mlp_vjp_split2_kernel<2>), grid, blk, shm, s, a, image, skip);
+    else hipLaunchKernelGGL((mlp_vjp_split2_kernel<0>), grid, blk, shm, s, a, image, skip);
+  } else {
+    if (sh == 1) hipLaunchKernelGGL((mlp_vjp_split_kernel<1>), grid, blk, shm, s, a, image, skip);
+    else if (sh == 2) hipLaunchKernelGGL((mlp_vjp_split_kernel<2>), grid, blk, shm, s, a, image, skip);
+    else hipLaunchKernelGGL((mlp_vjp_split_kernel<0>), grid, blk, shm, s, a, image, skip);
   }
   return hip_check(hipGetLastError(), "mrl_mlp_vjp_split");
 }
