@@ -332,7 +332,9 @@ class IterationRunner:
             if "cap" in post:
                 return
             ev["upd1"] = self._event()
-            post["cap"] = capture_state(agent, with_vf=False) if self.pipeline else None
+            # pipelined: the VF of this iteration is fitted during the next step and added
+            # to the capture then; in order it is final already
+            post["cap"] = capture_state(agent, with_vf=not self.pipeline)
             if prelaunch_next:
                 self._prelaunched = self._launch_rollout()
 
@@ -349,7 +351,9 @@ class IterationRunner:
             # for snapshots taken in the callback that reports it
             self.pending = (batch, ep_dev, pol_stats, post["cap"])
         else:
-            agent._snapshot_capture = None
+            # a snapshot taken in this iteration's callback reads the state at its end, not
+            # the live one (the next rollout may already be running)
+            agent._snapshot_capture = post["cap"]
             done = self._stats(col.episode_stats_finish(ep_dev), vf_stats, pol_stats)
         self.last_phase_events = ev
         return done
