@@ -22,4 +22,7 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out
 python tools/pmc_traffic.py gpurun_out/${tag}_gemm_fetch gpurun_out/${tag}_gemm_write --gemm $L --key Humanoid-v2/bf16/1024 --out gpurun_out/${tag}_pmc_gemm.json || exit 1
 cat gpurun_out/${tag}_rollout_issue.json | head -30
 run humanoid 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 3 --warmup 1
+# A/B: the VF fit co-scheduled with the wave-per-env rollout on shared CUs
+export MRL_COSCHED_FIT=1; run humanoid_bf16_cosched 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 5 --warmup 1 --dtype bf16 --no-cpu-baseline
+unset MRL_COSCHED_FIT
 echo R04_B_OK
