@@ -849,10 +849,9 @@ int mrl_mlp_vjp_split(const mrl_mlp_desc* d, const float* image, const float* x,
   const size_t shm = (size_t)3 * split_bw(a.b) * 4;
   const dim3 grid(blocks), blk(256);
   hipStream_t s = (hipStream_t)stream;
-  static const int form = [] {  // MRL_VJP_SPLIT=2: the transpose-free second form
-    const char* e = getenv("MRL_VJP_SPLIT");
-    return e ? atoi(e) : 1;
-  }();
+  // MRL_VJP_SPLIT_FORM=2: the transpose-free second form (read per call: tests switch it)
+  const char* fe = getenv("MRL_VJP_SPLIT_FORM");
+  const int form = fe ? atoi(fe) : 1;
   const int sh = static_shape_split(d);
   if (form == 2) {
     if (sh == 1) hipLaunchKernelGGL((mlp_vjp_split2_kernel<1>), grid, blk, shm, s, a, image, skip);

@@ -129,7 +129,8 @@ class MlpNet:
         self._cache_key = None
         # fp32 Fisher products on bf16 MFMA with exactly split operands (csrc/mlp_split.hip):
         # MRL_FISHER=split (default) | f32 (the exact-f32 MFMA kernels); MRL_VJP_SPLIT=1 also
-        # runs the cached VJP on split operands (measured slower, off)
+        # runs the cached VJP on split operands (form 1 measured slower, off), in the kernel
+        # form MRL_VJP_SPLIT_FORM (1: identity-MFMA transposes, 2: transpose-free gathers)
         self.fisher_split = (not self.bf16) and os.environ.get("MRL_FISHER", "split") == "split"
         self.image_s = None
         if self.fisher_split:

@@ -22,9 +22,11 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("head,nin,nout", CASES)
 @pytest.mark.parametrize("N", [1, 33, 3001])
-def test_split_fisher_product(head, nin, nout, N, monkeypatch):
+@pytest.mark.parametrize("form", ["1", "2"])
+def test_split_fisher_product(head, nin, nout, N, form, monkeypatch):
     monkeypatch.setenv("MRL_FISHER", "split")
     monkeypatch.setenv("MRL_VJP_SPLIT", "1")
+    monkeypatch.setenv("MRL_VJP_SPLIT_FORM", form)  # the VJP kernel (mlp_split.hip)
     from modular_rl_amd import _lib
     from modular_rl_amd.nets import MlpNet
     rng = np.random.default_rng(nin * 7 + N)
@@ -133,3 +135,12 @@ def test_split_fisher_product_is_deterministic(monkeypatch):
         outs.append(gh.clone())
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
+    # and the split VJP of those rows, both kernel forms
+    monkeypatch.setenv("MRL_VJP_SPLIT", "1")
+    for form in ("1", "2"):
+        monkeypatch.setenv("MRL_VJP_SPLIT_FORM", form)
+        fv = [torch.zeros(net.P, device="cuda") for _ in range(3)]
+        for f in fv:
+            net.vjp_flat(x, N, gh, f)
+        for f in fv[1:]:
+            assert torch.equal(f, fv[0]), form

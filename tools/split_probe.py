@@ -62,7 +62,7 @@ for nin, nout, head in ((11, 3, _lib.HEAD_GAUSS), (4, 2, _lib.HEAD_SOFTMAX)):
     fs = torch.zeros(net.P, device='cuda')
     os.environ["MRL_VJP_SPLIT"] = "0"
     tv32 = timed(lambda: net.vjp_flat(x, N, gh, f32))
-    os.environ["MRL_VJP_SPLIT"] = "1"
+    os.environ["MRL_VJP_SPLIT"] = "1"  # the kernel form: MRL_VJP_SPLIT_FORM (1 | 2)
     tvs = timed(lambda: net.vjp_flat(x, N, gh_s, fs))
     fss = torch.zeros(net.P, device='cuda')
     net.vjp_flat(x, N, gh, fss)  # split VJP of the f32 head rows
