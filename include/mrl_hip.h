@@ -171,6 +171,14 @@ int mrl_mlp_fvp_split(const mrl_mlp_desc* d, const float* theta, const float* im
 /* the VJP (slab rows as mrl_mlp_vjp: mrl_mlp_slab_rows(d, n)) from the f32 cache */
 int mrl_mlp_vjp_split(const mrl_mlp_desc* d, const float* image, const float* x, const float* ghead, int64_t n,
                       float* slab, const float* act_cache, const int32_t* skip, void* stream);
+/* the whole Fisher product in one pass (JVP -> KL metric -> VJP per 32-row tile, the
+ * cache read once, the head rows kept in registers; replaces the pair above and the
+ * reference's Fvp, trpo.py:45-58): slab rows as mrl_mlp_vjp (mrl_mlp_slab_rows(d, n)),
+ * bit-identical to mrl_mlp_fvp_split + mrl_mlp_vjp_split form 2; io->ghead optional
+ * (the head rows, written as mrl_mlp_fvp_split writes them) */
+int mrl_mlp_fisher_split(const mrl_mlp_desc* d, const float* theta, const float* image, const float* tangent,
+                         const float* image_t, const mrl_rows_io* io, float* slab, const int32_t* skip,
+                         void* stream);
 
 int mrl_reduce_rows_f32(const float* slab, int64_t rows, int64_t cols, float* out, const int32_t* skip, void* stream);
 int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* out, const int32_t* skip, void* stream);

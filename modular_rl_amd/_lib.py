@@ -99,6 +99,7 @@ SIGNATURES = {
     "mrl_mlp_pack_split": (i32, [vp, vp, vp, i32, vp, vp]),
     "mrl_mlp_fvp_split": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_mlp_vjp_split": (i32, [vp, vp, vp, vp, i64, vp, vp, vp, vp]),
+    "mrl_mlp_fisher_split": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_reduce_rows_f32": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_reduce_rows_f64": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_gemm": (i32, [vp, vp, vp]),

@@ -597,23 +597,25 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_split2_kernel(VjpSplitArgs a_i
     float fv = (row < a.n && h == 0) ? 1.f : 0.f;
     asm volatile("" : "+v"(fv));
     const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
+    int hq = h, cq = c;  // opaque lane coordinates (see mlp_fisher_split_kernel)
+    asm volatile("" : "+v"(hq), "+v"(cq));
     // F-layout h2 (tanh' of gh2_F); the T-layout operands are gathered phase by phase
     f32x16 h2F[2];
     cache_load(ct, lane, 2, h2F[0]);
     cache_load(ct, lane, 3, h2F[1]);
     // row of register r in a T tile, and its validity factor
     auto trow = [&](int r) {
-      const int64_t rw = row0 + cperm(r, h);
+      const int64_t rw = row0 + cperm(r, hq);
       return rw < a.n ? rw : (int64_t)0;
     };
     auto tval = [&](int r) {
-      float f = row0 + cperm(r, h) < a.n ? 1.f : 0.f;
+      float f = row0 + cperm(r, hq) < a.n ? 1.f : 0.f;
       asm volatile("" : "+v"(f));
       return f;
     };
     auto gather_cache = [&](int slot, f32x16& t) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) t[r] = ct[cache_off_s(slot, cperm(r, h), c)];
+      for (int r = 0; r < 16; ++r) t[r] = ct[cache_off_s(slot, cperm(r, hq), cq)];
     };
     const float* gp = a.ghead + rc * a.gh;
     float g8[8];
@@ -720,6 +722,291 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_split2_kernel(VjpSplitArgs a_i
     if (lane == 0 && o < A) out[d.tb2 + o] = sum;
   }
   for (int q = 0; q < a.n_sum; ++q) {
+    const float sum = wave_sumf(gls[q]);
+    if (lane == 0) out[d.tls + q] = sum;
+  }
+}
+
+
+// An LDS pointer the compiler cannot see through: accesses at constant offsets from it
+// fold into the ds instructions' 16-bit offset field.  LDS data past 64 KB addressed from
+// the segment base instead needs one address register per fragment, which the compiler
+// hoists out of the row loop -- dozens of loop-invariant registers, spilled.
+__device__ inline const float* lds_opaque(const float* p) {
+  auto q = (const __attribute__((address_space(3))) float*)p;
+  asm volatile("" : "+v"(q));
+  return (const float*)q;
+}
+
+// ---- the whole Fisher product in one pass (trpo.py:45-58, 86-92): per 32-row tile the
+// JVP of mlp_fvp_split_kernel, the KL-metric head rows (fvp_metric_row) kept in
+// registers, then the VJP of mlp_vjp_split2_kernel on them -- the activation cache is
+// read once (h1 / h2 streamed in F order; the T-order gathers of the VJP hit the lines
+// just streamed) and the head rows never go to memory.  The G tile in T order (B operand
+// of gW2 += H2^T G) comes through a 1 KB LDS tile per wave instead of a global gather.
+// Grid and tile order are the VJP's (one slab row per wave, the same tiles per wave), so
+// the slab -- and the Fisher product -- is bit-identical to the two-pass split path
+// (split JVP rows, then mlp_vjp_split2_kernel on the rows it wrote).
+template <int SH>
+__global__ __launch_bounds__(256, 1) void mlp_fisher_split_kernel(RowsArgs a, BDims b, float* __restrict__ slab,
+                                                                 const float* __restrict__ img_g,
+                                                                 const float* __restrict__ imt_g,
+                                                                 const int32_t* __restrict__ skip) {
+  split_shape<SH>(a, b);
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (skip != nullptr && *skip != 0) return;
+  // LDS: the primal split image whole (forward + backward parts), the tangent's forward
+  // parts, then one 32 x 8 head-row tile per wave
+  const int WP = split_image_words(b), WT = split_fwd_words(b), PS = split_fw(b), BW = split_bw(b);
+  for (int i = threadIdx.x; i < WP / 4; i += 256)
+    reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img_g)[i];
+  for (int i = threadIdx.x; i < WT / 4; i += 256)
+    reinterpret_cast<float4*>(lds + WP)[i] = reinterpret_cast<const float4*>(imt_g)[i];
+  __syncthreads();
+  const float* img = lds;
+  const float* imt = lds_opaque(lds + WP);  // the tangent image lies past 64 KB
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j32 = lane & 31;
+  float* gtile = lds + WP + WT + wave * 256;
+  auto wfrag = [&](int seg, int p, int f) { return frag_at(lds, WT + seg - b.fwd_words + p * BW, f, lane); };
+  const MlpDims dd = head_dims(a.d, b);
+  const MlpDims& d = a.d;
+  const int A = a.A;
+  const int n_sum = a.head == MRL_HEAD_GAUSS ? A : 0;
+  float ls[MAX_OUT], sd[MAX_OUT], dls[MAX_OUT];
+#pragma unroll
+  for (int j = 0; j < MAX_OUT; ++j) {
+    ls[j] = (a.logstd != nullptr && j < A) ? a.logstd[j] : 0.f;
+    sd[j] = expf(ls[j]);
+    dls[j] = (a.dlogstd != nullptr && j < A) ? a.dlogstd[j] : 0.f;
+  }
+  const bool need_z = a.head != MRL_HEAD_GAUSS;
+  f32x16 gW2[2], gW1[2][2], gW0[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    gW2[m] = zero16();
+    gW0[m] = zero16();
+#pragma unroll
+    for (int n = 0; n < 2; ++n) gW1[m][n] = zero16();
+  }
+  float gb0[2] = {0.f, 0.f}, gb1[2] = {0.f, 0.f};
+  float gb2[MAX_OUT], gls[MAX_OUT];
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    gb2[o] = 0.f;
+    gls[o] = 0.f;
+  }
+  const int c = j32;
+  const int64_t ntiles = (a.n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t row0 = tile * 32, row = row0 + j32;
+    const bool valid = row < a.n;
+    float fv = (valid && h == 0) ? 1.f : 0.f, fx = valid ? 1.f : 0.f;
+    asm volatile("" : "+v"(fv), "+v"(fx));
+    const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
+    XGlobalNB xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
+    // per-lane T-order indices from opaque copies of the lane coordinates: derived anew
+    // each tile next to their use, not hoisted out of the loop as ~50 live registers
+    int hq = h, cq = c;
+    asm volatile("" : "+v"(hq), "+v"(cq));
+    // ---- JVP (mlp_fvp_split_kernel): dh = (x dW0 + db0) (1 - h1^2), then per output
+    // tile da = (dh W1 + h1 dW1 + db1) (1 - h2^2) and the head on the f32 VALU
+    f32x16 h2F[2];
+    float z[MAX_OUT], dz[MAX_OUT];
+    {
+      f32x16 h1[2], dh[2];
+      cache_load(ct, lane, 0, h1[0]);
+      cache_load(ct, lane, 1, h1[1]);
+      dh[0] = load_bias16(imt, b.fb0, 0, h);
+      dh[1] = load_bias16(imt, b.fb0, 1, h);
+#pragma unroll
+      for (int s0 = 0; s0 < MAX_KS0B; ++s0) {
+        if (s0 < b.KS0B) {
+          float xv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) xv[j] = xl(16 * s0 + 8 * h + j);
+          bf16x8 xs[3];
+          split8v(xv, xs);
+          mfma_split<MRL_SPLIT_NPROD>(imt, b.fa0, PS, 0 * b.KS0B + s0, lane, xs, dh[0]);
+          mfma_split<MRL_SPLIT_NPROD>(imt, b.fa0, PS, 1 * b.KS0B + s0, lane, xs, dh[1]);
+        }
+      }
+      mul_dtanh16(dh[0], h1[0]);
+      mul_dtanh16(dh[1], h1[1]);
+      float dzt[MAX_OUT];
+#pragma unroll
+      for (int o = 0; o < MAX_OUT; ++o) z[o] = dz[o] = dzt[o] = 0.f;
+#pragma unroll
+      for (int mo = 0; mo < 2; ++mo) {
+        f32x16 da = load_bias16(imt, b.fb1, mo, h);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          bf16x8 ps[3];
+          split8(dh[s >> 1], s & 1, ps);
+          mfma_split<MRL_SPLIT_NPROD>(img, b.fa1, PS, mo * 4 + s, lane, ps, da);
+        }
+        FVP_SPLIT_FENCE();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          bf16x8 ps[3];
+          split8(h1[s >> 1], s & 1, ps);
+          mfma_split<MRL_SPLIT_NPROD>(imt, b.fa1, PS, mo * 4 + s, lane, ps, da);
+        }
+        FVP_SPLIT_FENCE();
+        cache_load(ct, lane, 2 + mo, h2F[mo]);
+        mul_dtanh16(da, h2F[mo]);
+        if (need_z) head_partial_mt(img, dd, h2F[mo], mo, h, z);
+        head_partial_mt(img, dd, da, mo, h, dz);
+        head_partial_mt(imt, dd, h2F[mo], mo, h, dzt);
+        FVP_SPLIT_FENCE();
+      }
+      if (need_z) head_finish(img, dd, z);
+#pragma unroll
+      for (int o = 0; o < MAX_OUT; ++o) dz[o] += dzt[o];
+      head_finish(imt, dd, dz);
+    }
+    FVP_SPLIT_FENCE();
+    // ---- the metric's head rows (every lane forms its row's; lane half 0 owns them)
+    static_assert(MAX_OUT == 8, "the head-row tile holds 8 columns");
+    float gm[MAX_OUT], gl[MAX_OUT];
+    fvp_metric_row<MAX_OUT>(a, z, dz, sd, dls, gm, gl);
+    float g8[8];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+      g8[o] = o < A ? gm[o] * fv : 0.f;
+      gb2[o] += g8[o];
+    }
+#pragma unroll
+    for (int q = 0; q < MAX_OUT; ++q) gls[q] += q < n_sum ? gl[q] * fv : 0.f;
+    // G in T order through the wave's LDS tile: row j32's values from lane half 0
+    if (h == 0) {
+      reinterpret_cast<float4*>(gtile + 8 * j32)[0] = make_float4(gm[0], gm[1], gm[2], gm[3]);
+      reinterpret_cast<float4*>(gtile + 8 * j32)[1] = make_float4(gm[4], gm[5], gm[6], gm[7]);
+    }
+    WAVE_LDS_ORDER();
+    bf16x8 gs[2][3];
+    {
+      f32x16 gT;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float f = row0 + cperm(r, hq) < a.n ? 1.f : 0.f;
+        asm volatile("" : "+v"(f));
+        gT[r] = (c < A ? gtile[8 * cperm(r, hq) + (cq & 7)] : 0.f) * f;
+      }
+      split8(gT, 0, gs[0]);
+      split8(gT, 1, gs[1]);
+    }
+    WAVE_LDS_ORDER();  // the next tile's writes stay behind these reads
+    VJP_SPLIT_FENCE();
+    // ---- VJP (mlp_vjp_split2_kernel) of the head rows
+    auto trow = [&](int r) {
+      const int64_t rw = row0 + cperm(r, hq);
+      return rw < a.n ? rw : (int64_t)0;
+    };
+    auto tval = [&](int r) {
+      float f = row0 + cperm(r, hq) < a.n ? 1.f : 0.f;
+      asm volatile("" : "+v"(f));
+      return f;
+    };
+    auto gather_cache = [&](int slot, f32x16& t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t[r] = ct[cache_off_s(slot, cperm(r, hq), cq)];
+    };
+    bf16x8 gB[3];
+    split8v(g8, gB);
+    bf16x8 gaF[4][3], gaT[2][2][3];
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo) {
+      f32x16 h2T;
+      gather_cache(2 + mo, h2T);
+      const bf16x8 w[3] = {wfrag(b.bw2, 0, mo), wfrag(b.bw2, 1, mo), wfrag(b.bw2, 2, mo)};
+      f32x16 gf = zero16(), gt = zero16();
+      mma_split<MRL_SPLIT_NPROD>(w, gB, gf);
+      mma_split<MRL_SPLIT_NPROD>(gB, w, gt);
+      mul_dtanh16(gf, h2F[mo]);
+      mul_dtanh16(gt, h2T);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gb1[mo] += gt[r];
+      split8(gf, 0, gaF[2 * mo]);
+      split8(gf, 1, gaF[2 * mo + 1]);
+      split8(gt, 0, gaT[mo][0]);
+      split8(gt, 1, gaT[mo][1]);
+      bf16x8 hs[2][3];
+      split8(h2T, 0, hs[0]);
+      split8(h2T, 1, hs[1]);
+      mma_split<MRL_SPLIT_NPROD>(hs[0], gs[0], gW2[mo]);
+      mma_split<MRL_SPLIT_NPROD>(hs[1], gs[1], gW2[mo]);
+      VJP_SPLIT_FENCE();
+    }
+    bf16x8 xs[2][3];
+    {
+      f32x16 xT;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xT[r] = (c < a.n_obs ? a.x[trow(r) * a.n_obs + (c < a.n_obs ? c : 0)] : 0.f) * tval(r);
+      split8(xT, 0, xs[0]);
+      split8(xT, 1, xs[1]);
+    }
+#pragma unroll
+    for (int no = 0; no < 2; ++no) {
+      f32x16 h1T;
+      gather_cache(no, h1T);
+      f32x16 ga1 = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 w[3] = {wfrag(b.bt1, 0, no * 4 + s), wfrag(b.bt1, 1, no * 4 + s), wfrag(b.bt1, 2, no * 4 + s)};
+        mma_split<MRL_SPLIT_NPROD>(gaF[s], w, ga1);
+      }
+      mul_dtanh16(ga1, h1T);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gb0[no] += ga1[r];
+      bf16x8 hs[2][3], g1[2][3];
+      split8(h1T, 0, hs[0]);
+      split8(h1T, 1, hs[1]);
+      split8(ga1, 0, g1[0]);
+      split8(ga1, 1, g1[1]);
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        mma_split<MRL_SPLIT_NPROD>(hs[sp], gaT[0][sp], gW1[no][0]);
+        mma_split<MRL_SPLIT_NPROD>(hs[sp], gaT[1][sp], gW1[no][1]);
+        mma_split<MRL_SPLIT_NPROD>(xs[sp], g1[sp], gW0[no]);
+      }
+      VJP_SPLIT_FENCE();
+    }
+    if (a.ghead != nullptr && valid && h == 0) {  // diagnostic: the head rows as the two-pass path writes them
+#pragma unroll
+      for (int j = 0; j < MAX_OUT; ++j) {
+        if (j < A) {
+          a.ghead[row * a.gh + j] = gm[j];
+          if (a.head == MRL_HEAD_GAUSS) a.ghead[row * a.gh + A + j] = gl[j];
+        }
+      }
+    }
+  }
+  float* out = slab + ((int64_t)blockIdx.x * 4 + wave) * d.P;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = cperm(r, h);
+      if (i < d.O) out[d.tW0 + i * HID + 32 * m + j32] = gW0[m][r];
+      if (j32 < A) out[d.tW2 + (32 * m + i) * A + j32] = gW2[m][r];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) out[d.tW1 + (32 * m + i) * HID + 32 * n + j32] = gW1[m][n][r];
+    }
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const float s0 = gb0[m] + __shfl_xor(gb0[m], 32);
+    const float s1 = gb1[m] + __shfl_xor(gb1[m], 32);
+    if (h == 0) {
+      out[d.tb0 + 32 * m + j32] = s0;
+      out[d.tb1 + 32 * m + j32] = s1;
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) {
+    const float sum = wave_sumf(gb2[o]);
+    if (lane == 0 && o < A) out[d.tb2 + o] = sum;
+  }
+  for (int q = 0; q < n_sum; ++q) {
     const float sum = wave_sumf(gls[q]);
     if (lane == 0) out[d.tls + q] = sum;
   }
@@ -863,6 +1150,51 @@ int mrl_mlp_vjp_split(const mrl_mlp_desc* d, const float* image, const float* x,
     else hipLaunchKernelGGL((mlp_vjp_split_kernel<0>), grid, blk, shm, s, a, image, skip);
   }
   return hip_check(hipGetLastError(), "mrl_mlp_vjp_split");
+}
+
+int mrl_mlp_fisher_split(const mrl_mlp_desc* d, const float* theta, const float* image, const float* tangent,
+                         const float* image_t, const mrl_rows_io* io, float* slab, const int32_t* skip,
+                         void* stream) {
+  int rc = check_desc_s(d);
+  if (rc) return rc;
+  if (!io || !image || !image_t || !tangent || !io->x || !slab) return fail(E_ARG, "null pointer");
+  if (!io->act_cache || io->cache_mode != MRL_CACHE_READ)
+    return fail(E_ARG, "mrl_mlp_fisher_split reads the f32 activation cache (MRL_CACHE_READ)");
+  if (io->ep_t) return fail(E_ARG, "mrl_mlp_fisher_split: policy rows only (no time feature)");
+  if (d->head == MRL_HEAD_LINEAR) return fail(E_ARG, "Fisher product of a value net");
+  if (d->head == MRL_HEAD_GAUSS && !theta) return fail(E_ARG, "DiagGauss needs theta (logstd)");
+  if (io->n <= 0) return OK;
+  RowsArgs a{};
+  a.d = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
+  a.head = d->head;
+  a.n_obs = d->n_in;
+  a.gh = d->head == MRL_HEAD_GAUSS ? 2 * d->n_out : d->n_out;
+  a.A = d->n_out;
+  a.x = io->x;
+  a.n = io->n;
+  a.inv_ng = io->inv_n_global;
+  a.ghead = io->ghead;  // optional: the head rows, as the two-pass path writes them
+  a.logstd = (d->head == MRL_HEAD_GAUSS && theta) ? theta + a.d.tls : nullptr;
+  a.dlogstd = (d->head == MRL_HEAD_GAUSS && tangent) ? tangent + a.d.tls : nullptr;
+  a.cache = io->act_cache;
+  a.cache_mode = MRL_CACHE_READ;
+  const BDims b = bf16_dims(d->n_in, d->n_out);
+  // the VJP's grid (mrl_mlp_slab_rows): one slab row per wave of a 4-wave block
+  const int64_t cus = d->cus > 0 ? d->cus : 256;
+  int64_t blocks = ((io->n + 31) / 32 + 3) / 4;
+  const int64_t cap = VJP_SPLIT_MAX_BLOCKS * cus / 256 > 0 ? VJP_SPLIT_MAX_BLOCKS * cus / 256 : 1;
+  if (blocks < 1) blocks = 1;
+  if (blocks > cap) blocks = cap;
+  const size_t shm = ((size_t)split_image_words(b) + split_fwd_words(b) + 4 * 256) * 4;
+  if (shm > 160 * 1024) return fail(E_UNSUPPORTED, "mrl_mlp_fisher_split: images exceed LDS");
+  const dim3 grid(blocks), blk(256);
+  hipStream_t s = (hipStream_t)stream;
+  switch (static_shape_split(d)) {
+    case 1: hipLaunchKernelGGL((mlp_fisher_split_kernel<1>), grid, blk, shm, s, a, b, slab, image, image_t, skip); break;
+    case 2: hipLaunchKernelGGL((mlp_fisher_split_kernel<2>), grid, blk, shm, s, a, b, slab, image, image_t, skip); break;
+    default: hipLaunchKernelGGL((mlp_fisher_split_kernel<0>), grid, blk, shm, s, a, b, slab, image, image_t, skip); break;
+  }
+  return hip_check(hipGetLastError(), "mrl_mlp_fisher_split");
 }
 
 }  // extern "C"

@@ -64,6 +64,35 @@ __device__ __forceinline__ float gauss_loglik(float q, float sumlog, int A) {
 }
 __device__ __forceinline__ float gauss_entropy(float sumlog, int A) { return sumlog + 0.5f * LOG2PIE_F * A; }
 
+// The Fisher product's head-gradient row: the GGN metric of the KL at the old policy
+// applied to the head tangent dz (== Theano's double backprop, trpo.py:45-58); g: the
+// head-output part, gl: DiagGauss's log-std part (the same for every row).  Shared by the
+// FVP row epilogue and the fused split Fisher product (mlp_split.hip), so both form
+// these values with the same operations.
+template <int MA>
+__device__ __forceinline__ void fvp_metric_row(const RowsArgs& a, const float (&z)[MA], const float (&dz)[MA],
+                                               const float (&sd)[MA], const float (&dls)[MA], float (&g)[MA],
+                                               float (&gl)[MA]) {
+  const int A = a.A;
+  const float s = (float)a.inv_ng;
+  for (int j = 0; j < MA; ++j) g[j] = gl[j] = 0.f;
+  if (a.head == MRL_HEAD_SOFTMAX) {
+    float m = z[0];
+    for (int j = 1; j < A; ++j) m = fmaxf(m, z[j]);
+    float p[MA], se = 0.f, pd = 0.f;
+    for (int j = 0; j < A; ++j) { p[j] = expf(z[j] - m); se += p[j]; }
+    for (int j = 0; j < A; ++j) { p[j] = p[j] / se; pd += p[j] * dz[j]; }
+    for (int j = 0; j < A; ++j) g[j] = p[j] * (dz[j] - pd) * s;
+  } else if (a.head == MRL_HEAD_GAUSS) {
+    for (int j = 0; j < A; ++j) {
+      g[j] = dz[j] / (sd[j] * sd[j]) * s;
+      gl[j] = 2.f * dls[j] * s;
+    }
+  } else {
+    g[0] = dz[0] * s;
+  }
+}
+
 template <int EPI, int MA>
 __device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, const float (&z)[MA],
                                              const float (&dz)[MA], const float (&ls)[MA], const float (&sd)[MA],
@@ -164,22 +193,15 @@ __device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, con
     acc0 += (double)err * (double)err;
     a.ghead[row] = (float)(2.0 * a.inv_ng) * err;
   } else if (EPI == MRL_EPI_FVP) {
-    // GGN metric of the KL at the old policy (== Theano's double backprop, trpo.py:45-58)
-    const float s = (float)a.inv_ng;
-    if (a.head == MRL_HEAD_SOFTMAX) {
-      float m = z[0];
-      for (int j = 1; j < A; ++j) m = fmaxf(m, z[j]);
-      float p[MA], se = 0.f, pd = 0.f;
-      for (int j = 0; j < A; ++j) { p[j] = expf(z[j] - m); se += p[j]; }
-      for (int j = 0; j < A; ++j) { p[j] = p[j] / se; pd += p[j] * dz[j]; }
-      for (int j = 0; j < A; ++j) a.ghead[row * a.gh + j] = p[j] * (dz[j] - pd) * s;
-    } else if (a.head == MRL_HEAD_GAUSS) {
+    float g[MA], gl[MA];
+    fvp_metric_row<MA>(a, z, dz, sd, dls, g, gl);
+    if (a.head == MRL_HEAD_GAUSS) {
       for (int j = 0; j < A; ++j) {
-        a.ghead[row * a.gh + j] = dz[j] / (sd[j] * sd[j]) * s;
-        a.ghead[row * a.gh + A + j] = 2.f * dls[j] * s;
+        a.ghead[row * a.gh + j] = g[j];
+        a.ghead[row * a.gh + A + j] = gl[j];
       }
     } else {
-      a.ghead[row * a.gh] = dz[0] * s;
+      for (int j = 0; j < A; ++j) a.ghead[row * a.gh + j] = g[j];
     }
   }
 }

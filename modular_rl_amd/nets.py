@@ -248,6 +248,28 @@ class MlpNet:
         call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
         return out
 
+    def fisher_fusable(self, x, n, image_t):
+        return bool(self.fisher_split and getattr(image_t, "_mrl_split", False) and self.use_cache
+                    and self.head != _lib.HEAD_LINEAR and os.environ.get("MRL_FISHER_FUSED", "1") != "0"
+                    and self._cache_key == self._key(x, n, None, 1.0))
+
+    def fisher_product(self, x, n, inv_n_global, tangent, image_t, out, skip=None, ghead=None):
+        """out[P] <- the Fisher product along ``tangent`` over the n cached rows in ONE pass
+        (mrl_mlp_fisher_split: JVP, KL metric and VJP per tile, the activation cache read
+        once), when the split path applies: split tangent image, a current cache of these
+        rows, a policy head, no time feature.  False: not applicable (the caller runs
+        rows(EPI_FVP) + vjp_flat).  MRL_FISHER_FUSED=0 keeps the two passes."""
+        if not self.fisher_fusable(x, n, image_t):
+            return False
+        rows = int(self.lib.mrl_mlp_slab_rows(ctypes.byref(self.desc), int(n)))
+        slab = self.ws.get("slab", rows * self.P, torch.float32)
+        io = _lib.RowsIO(ptr(x), None, 1.0, int(n), float(inv_n_global), None, None, None, None, None, ptr(ghead),
+                         None, 0.0, 0.0, 0.0, 0, _lib.CACHE_READ, ptr(self._cache(n)), None)
+        call("mrl_mlp_fisher_split", ctypes.byref(self.desc), ptr(self.theta), ptr(self.image_s), ptr(tangent),
+             ptr(image_t), ctypes.byref(io), ptr(slab), ptr(skip), stream())
+        call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
+        return True
+
     def reduce_partial(self, partial, n, out):
         rows = self.partial_rows(n)
         call("mrl_reduce_rows_f64", ptr(partial), rows, 4, ptr(out), None, stream())

@@ -144,3 +144,89 @@ def test_split_fisher_product_is_deterministic(monkeypatch):
             net.vjp_flat(x, N, gh, f)
         for f in fv[1:]:
             assert torch.equal(f, fv[0]), form
+
+
+@pytest.mark.parametrize("head,nin,nout", CASES)
+@pytest.mark.parametrize("N", [1, 33, 3001, 70001])
+def test_fused_fisher_product_equals_two_passes(head, nin, nout, N, monkeypatch):
+    """mrl_mlp_fisher_split (JVP, KL metric and VJP per tile in one kernel) gives the
+    two-pass split product bit for bit -- the split JVP rows, then the split VJP (form 2)
+    of the rows they wrote -- and its optional head rows equal the JVP kernel's; the
+    product holds the float64 oracle at 1e-4."""
+    monkeypatch.setenv("MRL_FISHER", "split")
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import MlpNet
+    rng = np.random.default_rng(nin * 11 + N)
+    spec = T.Spec(nin, [64, 64], nout, head)
+    th = T.mlp_init(rng, spec.shapes, head == "gauss") + 0.05 * rng.standard_normal(spec.P)
+    if head == "gauss":
+        th[-nout:] = 0.3 * rng.standard_normal(nout)
+    th = th.astype(np.float32).astype(np.float64)
+    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
+    oldprob = T.policy_prob(spec, th + 0.01 * rng.standard_normal(spec.P), ob).astype(np.float32).astype(np.float64)
+    act = T.sample(spec, oldprob, rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N))
+    adv = rng.standard_normal(N).astype(np.float32).astype(np.float64)
+    v = rng.standard_normal(spec.P).astype(np.float32)
+    net = MlpNet(nin, nout, _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX)
+    net.set_flat(th)
+    x, vt = _dev(ob), _dev(v)
+    a = _dev(act, torch.int32 if head == "softmax" else torch.float32)
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    gh = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(adv), oldprob=_dev(oldprob), ghead=gh,
+             partial=partial)
+    imgs = net.new_tangent_image()
+    net.pack_tangent(vt, imgs)
+    assert net.fisher_fusable(x, N, imgs)
+    # two passes: split JVP rows, split VJP form 2
+    monkeypatch.setenv("MRL_VJP_SPLIT", "1")
+    monkeypatch.setenv("MRL_VJP_SPLIT_FORM", "2")
+    gh2 = torch.full_like(gh, float("nan"))
+    net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=gh2, tangent=vt, image_t=imgs)
+    f2 = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(x, N, gh2, f2)
+    # one pass, with the diagnostic head rows
+    ghf = torch.full_like(gh, float("nan"))
+    ff = torch.full((net.P,), float("nan"), dtype=torch.float32, device="cuda")
+    assert net.fisher_product(x, N, 1.0 / N, vt, imgs, ff, ghead=ghf)
+    torch.cuda.synchronize()
+    assert torch.equal(ghf, gh2)
+    assert torch.equal(ff, f2)
+    want = T.fisher_vector_product(spec, th, v.astype(np.float64), ob)
+    assert _rel(ff.cpu().numpy(), want) < 1e-4
+
+
+def test_fused_fisher_product_grid_for_a_cu_subset(monkeypatch):
+    """The fused kernel sizes its grid (and so its slab rows) like the VJP for the net's
+    CU count; with a CU subset it stays equal to the two-pass product."""
+    monkeypatch.setenv("MRL_FISHER", "split")
+    monkeypatch.setenv("MRL_VJP_SPLIT", "1")
+    monkeypatch.setenv("MRL_VJP_SPLIT_FORM", "2")
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import MlpNet, glorot_init
+    N = 200003
+    rng = np.random.default_rng(5)
+    net = MlpNet(11, 3, _lib.HEAD_GAUSS)
+    net.set_flat(glorot_init(rng, 11, 3, _lib.HEAD_GAUSS))
+    net.size_for_cus(48)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(N, 11, device="cuda", generator=g)
+    act = torch.randn(N, 3, device="cuda", generator=g)
+    adv = torch.randn(N, device="cuda", generator=g)
+    prob = net.forward(x, N).clone()
+    gh = torch.zeros(N * net.gh, device="cuda")
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=act, adv=adv, oldprob=prob, ghead=gh, partial=partial)
+    v = torch.randn(net.P, device="cuda", generator=g) * 1e-2
+    imgt = net.new_tangent_image()
+    net.pack_tangent(v, imgt)
+    net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=gh, tangent=v, image_t=imgt)
+    f2 = torch.zeros(net.P, device="cuda")
+    net.vjp_flat(x, N, gh, f2)
+    ff = torch.zeros(net.P, device="cuda")
+    outs = []
+    for _ in range(3):
+        assert net.fisher_product(x, N, 1.0 / N, v, imgt, ff)
+        outs.append(ff.clone())
+    for o in outs:
+        assert torch.equal(o, f2)

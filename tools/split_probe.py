@@ -70,3 +70,8 @@ for nin, nout, head in ((11, 3, _lib.HEAD_GAUSS), (4, 2, _lib.HEAD_SOFTMAX)):
     print(f"[{nin},{nout},{head}] fvp rows: f32 {t32:.4f} ms  split {ts:.4f} ms | vjp(+reduce): f32 {tv32:.4f} ms  "
           f"split {tvs:.4f} ms | ghead rel diff {rel(gh_s, gh):.3e}  split-VJP rel diff {rel(fss, f32):.3e}  "
           f"Fv (both split) rel diff {rel(fs, f32):.3e}", flush=True)
+    ff = torch.zeros(net.P, device='cuda')
+    tf = timed(lambda: net.fisher_product(x, N, 1.0 / N, v, imgs, ff))
+    torch.cuda.synchronize()
+    print(f"[{nin},{nout},{head}] fused one-pass Fisher product (+reduce) {tf:.4f} ms vs f32 pair {t32 + tv32:.4f} ms "
+          f"| rel diff vs the f32 pair {rel(ff, f32):.3e}  vs two-pass split {rel(ff, fs):.3e}", flush=True)
