@@ -259,7 +259,7 @@ def fisher_arith(net):
     jvp = "split-operand bf16 MFMA (fp32 operands split exactly into 3 bf16 parts, f32 accumulate)" \
         if getattr(net, "fisher_split", False) else "exact f32 MFMA"
     split = getattr(net, "fisher_split", False)
-    if split and os.environ.get("MRL_FISHER_FUSED", "1") != "0":
+    if split and os.environ.get("MRL_FISHER_FUSED", "0") != "0":
         return {"pass": "one kernel per product (mlp_fisher_split_kernel: JVP, KL metric and VJP per 32-row tile, "
                         "the activation cache read once)", "jvp_rows": jvp, "vjp": jvp}
     vjp = "split-operand bf16 MFMA" if split and os.environ.get("MRL_VJP_SPLIT", "0") != "0" else "exact f32 MFMA"

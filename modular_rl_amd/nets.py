@@ -250,15 +250,16 @@ class MlpNet:
 
     def fisher_fusable(self, x, n, image_t):
         return bool(self.fisher_split and getattr(image_t, "_mrl_split", False) and self.use_cache
-                    and self.head != _lib.HEAD_LINEAR and os.environ.get("MRL_FISHER_FUSED", "1") != "0"
+                    and self.head != _lib.HEAD_LINEAR and os.environ.get("MRL_FISHER_FUSED", "0") != "0"
                     and self._cache_key == self._key(x, n, None, 1.0))
 
     def fisher_product(self, x, n, inv_n_global, tangent, image_t, out, skip=None, ghead=None):
         """out[P] <- the Fisher product along ``tangent`` over the n cached rows in ONE pass
         (mrl_mlp_fisher_split: JVP, KL metric and VJP per tile, the activation cache read
         once), when the split path applies: split tangent image, a current cache of these
-        rows, a policy head, no time feature.  False: not applicable (the caller runs
-        rows(EPI_FVP) + vjp_flat).  MRL_FISHER_FUSED=0 keeps the two passes."""
+        rows, a policy head, no time feature, and MRL_FISHER_FUSED=1 (measured slower than
+        the split JVP + exact-f32 VJP pair, so off by default: DESIGN §3).  False: not
+        applicable (the caller runs rows(EPI_FVP) + vjp_flat)."""
         if not self.fisher_fusable(x, n, image_t):
             return False
         rows = int(self.lib.mrl_mlp_slab_rows(ctypes.byref(self.desc), int(n)))

@@ -75,3 +75,21 @@ def test_prelaunched_rollout_is_bit_identical(pipeline):
     for x, y in zip(s0, s1):
         for k in x:
             assert x[k] == y[k] or (np.isnan(x[k]) and np.isnan(y[k])), k
+
+
+def test_cosched_fit_beside_wave_per_env_rollout_is_bit_identical(monkeypatch):
+    """C5's per-GPU width (1024 Humanoid envs: the wave-per-env step wants E / 4 = 256 CUs,
+    so no disjoint CU split): with MRL_COSCHED_FIT=1 the VF fit of iteration k shares the
+    CUs with the rollout of k+1 on two plain streams, bit-identical to the reference order."""
+    monkeypatch.setenv("MRL_COSCHED_FIT", "1")
+    kw = dict(n_envs=1024, horizon=8, hid_sizes=[64, 64])
+    r0, a0, c0, s0 = _run("Humanoid-v2", False, **kw)
+    r1, a1, c1, s1 = _run("Humanoid-v2", True, prelaunch=True, **kw)
+    assert not r0.pipeline and r1.pipeline
+    np.testing.assert_array_equal(a0.policy.net.get_flat(), a1.policy.net.get_flat())
+    np.testing.assert_array_equal(a0.baseline.net.get_flat(), a1.baseline.net.get_flat())
+    np.testing.assert_array_equal(c0.filter_state.cpu().numpy(), c1.filter_state.cpu().numpy())
+    assert len(s0) == len(s1) == 3
+    for x, y in zip(s0, s1):
+        for k in x:
+            assert x[k] == y[k] or (np.isnan(x[k]) and np.isnan(y[k])), k

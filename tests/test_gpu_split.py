@@ -154,6 +154,7 @@ def test_fused_fisher_product_equals_two_passes(head, nin, nout, N, monkeypatch)
     of the rows they wrote -- and its optional head rows equal the JVP kernel's; the
     product holds the float64 oracle at 1e-4."""
     monkeypatch.setenv("MRL_FISHER", "split")
+    monkeypatch.setenv("MRL_FISHER_FUSED", "1")
     from modular_rl_amd import _lib
     from modular_rl_amd.nets import MlpNet
     rng = np.random.default_rng(nin * 11 + N)
@@ -200,6 +201,7 @@ def test_fused_fisher_product_grid_for_a_cu_subset(monkeypatch):
     """The fused kernel sizes its grid (and so its slab rows) like the VJP for the net's
     CU count; with a CU subset it stays equal to the two-pass product."""
     monkeypatch.setenv("MRL_FISHER", "split")
+    monkeypatch.setenv("MRL_FISHER_FUSED", "1")
     monkeypatch.setenv("MRL_VJP_SPLIT", "1")
     monkeypatch.setenv("MRL_VJP_SPLIT_FORM", "2")
     from modular_rl_amd import _lib

@@ -70,6 +70,7 @@ for nin, nout, head in ((11, 3, _lib.HEAD_GAUSS), (4, 2, _lib.HEAD_SOFTMAX)):
     print(f"[{nin},{nout},{head}] fvp rows: f32 {t32:.4f} ms  split {ts:.4f} ms | vjp(+reduce): f32 {tv32:.4f} ms  "
           f"split {tvs:.4f} ms | ghead rel diff {rel(gh_s, gh):.3e}  split-VJP rel diff {rel(fss, f32):.3e}  "
           f"Fv (both split) rel diff {rel(fs, f32):.3e}", flush=True)
+    os.environ["MRL_FISHER_FUSED"] = "1"
     ff = torch.zeros(net.P, device='cuda')
     tf = timed(lambda: net.fisher_product(x, N, 1.0 / N, v, imgs, ff))
     torch.cuda.synchronize()
