@@ -367,19 +367,21 @@ def main():
              "trpo_update": ("upd0", "upd1")}
     recs = []
 
-    for i in range(args.warmup):
-        runner.step(prelaunch_next=i + 1 < args.warmup)
-    runner.drain()
+    with runner.loop_stream():  # no legacy-stream operations between the steps (IterationRunner.loop_stream)
+        for i in range(args.warmup):
+            runner.step(prelaunch_next=i + 1 < args.warmup)
+        runner.drain()
     timing.enable(True)
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     # K whole iterations: K rollouts, advantages, VF fits and policy updates (the last
     # VF fit drains inside the timed region)
-    for i in range(args.steps):
-        runner.step(prelaunch_next=i + 1 < args.steps)  # the next rollout issued as theta is final
-        recs.append(runner.last_phase_events)
-    runner.drain()
+    with runner.loop_stream():
+        for i in range(args.steps):
+            runner.step(prelaunch_next=i + 1 < args.steps)  # the next rollout issued as theta is final
+            recs.append(runner.last_phase_events)
+        runner.drain()
     recs.append(runner.last_drain_events if runner.pipeline else {})
     torch.cuda.synchronize()
     comm.barrier()

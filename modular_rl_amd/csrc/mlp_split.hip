@@ -82,29 +82,37 @@ __global__ void mlp_pack_split_kernel(MlpDims d, BDims b, const float* __restric
   image[w] = __uint_as_float(v);
 }
 
-// the three parts of registers 8 sp .. 8 sp + 7 of an F tile (the B fragment pack8 forms)
-__device__ inline void split8(const f32x16& t, int sp, bf16x8* out) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float v = t[8 * sp + j];
-    const __bf16 a = (__bf16)v;
-    const float r = v - (float)a;
-    const __bf16 c = (__bf16)r;
-    out[0][j] = a;
-    out[1][j] = c;
-    out[2][j] = (__bf16)(r - (float)c);
-  }
+// The exact three-way split of 8 values, two at a time: one v_cvt_pk_bf16_f32 per part
+// pair, the widening and the remainders on packed f32 (v_pk_add_f32) -- the same RNE
+// conversions and exact subtractions as the element-wise form, about 4.5 VALU per value
+// instead of 7 (the split is most of these kernels' VALU work).  Explicit vector types,
+// not the SLP vectoriser (which this file is built without, see the Makefile).
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ inline void split2(f32x2 v, bf16x2& a, bf16x2& c, bf16x2& e) {
+  a = __builtin_convertvector(v, bf16x2);
+  const f32x2 r = v - __builtin_convertvector(a, f32x2);
+  c = __builtin_convertvector(r, bf16x2);
+  e = __builtin_convertvector(r - __builtin_convertvector(c, f32x2), bf16x2);
 }
 __device__ inline void split8v(const float* v, bf16x8* out) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 a = (__bf16)v[j];
-    const float r = v[j] - (float)a;
-    const __bf16 c = (__bf16)r;
-    out[0][j] = a;
-    out[1][j] = c;
-    out[2][j] = (__bf16)(r - (float)c);
+  for (int j = 0; j < 8; j += 2) {
+    bf16x2 a, c, e;
+    split2(f32x2{v[j], v[j + 1]}, a, c, e);
+    out[0][j] = a[0];
+    out[0][j + 1] = a[1];
+    out[1][j] = c[0];
+    out[1][j + 1] = c[1];
+    out[2][j] = e[0];
+    out[2][j + 1] = e[1];
   }
+}
+// the three parts of registers 8 sp .. 8 sp + 7 of an F tile (the B fragment pack8 forms)
+__device__ inline void split8(const f32x16& t, int sp, bf16x8* out) {
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = t[8 * sp + j];
+  split8v(v, out);
 }
 
 // acc += W . X for one k-step: W = the image fragment f of segment `seg` (parts at
@@ -238,27 +246,32 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, (4 * MRL_SPLIT_FVP_OCC / SPLIT_RO
     mfma_drain();
     mul_dtanh16(dh[0], h1[0]);
     mul_dtanh16(dh[1], h1[1]);
-    // layer 1 tangent per output tile: da = (dh W1 + h1 dW1 + db1) (1 - h2^2)
+    // layer 1 tangent: da = (dh W1 + h1 dW1 + db1) (1 - h2^2); each input fragment is
+    // split once and feeds both output tiles (per tile the k order is unchanged: the four
+    // dh fragments, then the four h1 fragments)
     float z[MAX_OUT], dz[MAX_OUT], dzt[MAX_OUT];
 #pragma unroll
     for (int o = 0; o < MAX_OUT; ++o) z[o] = dz[o] = dzt[o] = 0.f;
+    f32x16 da2[2] = {load_bias16(imt, b.fb1, 0, h), load_bias16(imt, b.fb1, 1, h)};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 ps[3];
+      split8(dh[s >> 1], s & 1, ps);
+      mfma_split<MRL_SPLIT_NPROD>(img, b.fa1, PS, 0 * 4 + s, lane, ps, da2[0]);
+      mfma_split<MRL_SPLIT_NPROD>(img, b.fa1, PS, 1 * 4 + s, lane, ps, da2[1]);
+    }
+    FVP_SPLIT_FENCE();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 ps[3];
+      split8(h1[s >> 1], s & 1, ps);
+      mfma_split<MRL_SPLIT_NPROD>(imt, b.fa1, PS, 0 * 4 + s, lane, ps, da2[0]);
+      mfma_split<MRL_SPLIT_NPROD>(imt, b.fa1, PS, 1 * 4 + s, lane, ps, da2[1]);
+    }
+    FVP_SPLIT_FENCE();
 #pragma unroll
     for (int mo = 0; mo < 2; ++mo) {
-      f32x16 da = load_bias16(imt, b.fb1, mo, h);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        bf16x8 ps[3];
-        split8(dh[s >> 1], s & 1, ps);
-        mfma_split<MRL_SPLIT_NPROD>(img, b.fa1, PS, mo * 4 + s, lane, ps, da);
-      }
-      FVP_SPLIT_FENCE();
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        bf16x8 ps[3];
-        split8(h1[s >> 1], s & 1, ps);
-        mfma_split<MRL_SPLIT_NPROD>(imt, b.fa1, PS, mo * 4 + s, lane, ps, da);
-      }
-      FVP_SPLIT_FENCE();
+      f32x16& da = da2[mo];
       f32x16 h2;
       cache_load(ct, lane, 2 + mo, h2);
       mfma_drain();
@@ -835,23 +848,26 @@ __global__ __launch_bounds__(256, 1) void mlp_fisher_split_kernel(RowsArgs a, BD
       float dzt[MAX_OUT];
 #pragma unroll
       for (int o = 0; o < MAX_OUT; ++o) z[o] = dz[o] = dzt[o] = 0.f;
+      f32x16 da2[2] = {load_bias16(imt, b.fb1, 0, h), load_bias16(imt, b.fb1, 1, h)};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {  // each input fragment split once (mlp_fvp_split_kernel)
+        bf16x8 ps[3];
+        split8(dh[s >> 1], s & 1, ps);
+        mfma_split<MRL_SPLIT_NPROD>(img, b.fa1, PS, 0 * 4 + s, lane, ps, da2[0]);
+        mfma_split<MRL_SPLIT_NPROD>(img, b.fa1, PS, 1 * 4 + s, lane, ps, da2[1]);
+      }
+      FVP_SPLIT_FENCE();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8 ps[3];
+        split8(h1[s >> 1], s & 1, ps);
+        mfma_split<MRL_SPLIT_NPROD>(imt, b.fa1, PS, 0 * 4 + s, lane, ps, da2[0]);
+        mfma_split<MRL_SPLIT_NPROD>(imt, b.fa1, PS, 1 * 4 + s, lane, ps, da2[1]);
+      }
+      FVP_SPLIT_FENCE();
 #pragma unroll
       for (int mo = 0; mo < 2; ++mo) {
-        f32x16 da = load_bias16(imt, b.fb1, mo, h);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          bf16x8 ps[3];
-          split8(dh[s >> 1], s & 1, ps);
-          mfma_split<MRL_SPLIT_NPROD>(img, b.fa1, PS, mo * 4 + s, lane, ps, da);
-        }
-        FVP_SPLIT_FENCE();
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          bf16x8 ps[3];
-          split8(h1[s >> 1], s & 1, ps);
-          mfma_split<MRL_SPLIT_NPROD>(imt, b.fa1, PS, mo * 4 + s, lane, ps, da);
-        }
-        FVP_SPLIT_FENCE();
+        f32x16& da = da2[mo];
         cache_load(ct, lane, 2 + mo, h2F[mo]);
         mul_dtanh16(da, h2F[mo]);
         if (need_z) head_partial_mt(img, dd, h2F[mo], mo, h, z);

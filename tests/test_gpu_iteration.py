@@ -20,11 +20,12 @@ def _run(env_id, pipeline, n_iter=3, agent_cls="TrpoAgent", prelaunch=False, **k
     col = agent.make_collector(env, cfg)
     runner = IterationRunner(agent, col, cfg, pipeline=pipeline)
     stats = []
-    for i in range(n_iter):
-        s = runner.step(prelaunch_next=prelaunch and i + 1 < n_iter)
-        if s is not None:
-            stats.append(s)
-    s = runner.drain()
+    with runner.loop_stream():
+        for i in range(n_iter):
+            s = runner.step(prelaunch_next=prelaunch and i + 1 < n_iter)
+            if s is not None:
+                stats.append(s)
+        s = runner.drain()
     if s is not None:
         stats.append(s)
     torch.cuda.synchronize()
@@ -93,3 +94,14 @@ def test_cosched_fit_beside_wave_per_env_rollout_is_bit_identical(monkeypatch):
     for x, y in zip(s0, s1):
         for k in x:
             assert x[k] == y[k] or (np.isnan(x[k]) and np.isnan(y[k])), k
+
+
+def test_fit_runs_beside_the_prelaunched_rollout():
+    """With the next rollout issued from the update, the deferred VF fit of the previous
+    iteration still starts while that rollout runs (loop_stream: no legacy-stream event
+    that would wait for the CU-masked rollout stream): its first event precedes the
+    rollout's end event on the device timeline."""
+    runner, agent, col, stats = _run("Hopper-v2", True, n_iter=3, prelaunch=True, n_envs=256, horizon=1024)
+    ev = runner.last_phase_events
+    assert "vf0" in ev and "rollout1" in ev
+    assert ev["vf0"].elapsed_time(ev["rollout1"]) > 0.5  # ms of the rollout left when the fit began
