@@ -207,7 +207,8 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, (4 * MRL_SPLIT_FVP_OCC / SPLIT_RO
   const float* img = lds;
   const float* imt = lds + W;
   const MlpDims dd = head_dims(a.d, b);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform tile indices
   const int A = a.A;
   float ls[MAX_OUT], sd[MAX_OUT], dls[MAX_OUT];
 #pragma unroll
@@ -366,7 +367,8 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_split_kernel(VjpSplitArgs a_in
     reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img_g + f0)[i];
   __syncthreads();
   auto wfrag = [&](int seg, int p, int f, int lane) { return frag_at(lds, seg - b.fwd_words + p * BW, f, lane); };
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j32 = lane & 31;
+  const int lane = threadIdx.x & 63, h = lane >> 5, j32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform tile indices
   const int A = d.A;
   const bf16x8 ip[2] = {ident_perm(0, lane), ident_perm(1, lane)};
 
@@ -570,6 +572,37 @@ __device__ inline int cache_off_s(int slot, int j, int w) {
   return ((slot * 4 + (w >> 3)) * 64 + 32 * ((w >> 2) & 1) + j) * 4 + (w & 3);
 }
 
+// T-order row r of a 32-row tile relative to lane half hq's first row: cperm(r, hq) - 4 hq
+__device__ constexpr int trow_c(int r) { return (r & 3) + 8 * (r >> 2); }
+// lane part of the T-order cache gathers (cache_off_s minus the slot and row constants):
+// element (slot, cperm(r, hq), cq) sits at this + slot * 1024 + 4 trow_c(r), so every
+// gather is one base register plus an immediate offset
+__device__ inline int cache_lane_off(int hq, int cq) {
+  return ((cq >> 3) * 64 + 32 * ((cq >> 2) & 1)) * 4 + (cq & 3) + 16 * hq;
+}
+// a T-order row gather of a [rows][w] f32 array (inputs, head rows): column col of the
+// tile's row cperm(r, hq); rows past n read as 0 (full tiles take the immediate-offset
+// path, the batch's last tile the clamped one)
+template <int NR>
+__device__ inline void trow_gather(const float* base, int64_t w, int64_t row0, int hq, int col, bool col_ok, int64_t n,
+                                   float* out) {
+  const float fc = col_ok ? 1.f : 0.f;
+  const int cc = col_ok ? col : 0;
+  if (row0 + 32 <= n) {
+    const float* p = base + (row0 + 4 * hq) * w + cc;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) out[r] = p[trow_c(r) * w] * fc;
+  } else {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int64_t rw = row0 + 4 * hq + trow_c(r);
+      float f = rw < n ? fc : 0.f;
+      asm volatile("" : "+v"(f));
+      out[r] = base[(rw < n ? rw : 0) * w + cc] * f;
+    }
+  }
+}
+
 template <int SH>
 __global__ __launch_bounds__(256, 1) void mlp_vjp_split2_kernel(VjpSplitArgs a_in, const float* __restrict__ img_g,
                                                                const int32_t* __restrict__ skip) {
@@ -583,7 +616,8 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_split2_kernel(VjpSplitArgs a_i
     reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img_g + f0)[i];
   __syncthreads();
   auto wfrag = [&](int seg, int p, int f, int lane) { return frag_at(lds, seg - b.fwd_words + p * BW, f, lane); };
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j32 = lane & 31;
+  const int lane = threadIdx.x & 63, h = lane >> 5, j32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform tile indices
   const int A = d.A;
   f32x16 gW2[2], gW1[2][2], gW0[2];
 #pragma unroll
@@ -617,18 +651,10 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_split2_kernel(VjpSplitArgs a_i
     cache_load(ct, lane, 2, h2F[0]);
     cache_load(ct, lane, 3, h2F[1]);
     // row of register r in a T tile, and its validity factor
-    auto trow = [&](int r) {
-      const int64_t rw = row0 + cperm(r, hq);
-      return rw < a.n ? rw : (int64_t)0;
-    };
-    auto tval = [&](int r) {
-      float f = row0 + cperm(r, hq) < a.n ? 1.f : 0.f;
-      asm volatile("" : "+v"(f));
-      return f;
-    };
+    const float* cb = ct + cache_lane_off(hq, cq);
     auto gather_cache = [&](int slot, f32x16& t) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) t[r] = ct[cache_off_s(slot, cperm(r, hq), cq)];
+      for (int r = 0; r < 16; ++r) t[r] = cb[slot * 1024 + 4 * trow_c(r)];
     };
     const float* gp = a.ghead + rc * a.gh;
     float g8[8];
@@ -645,8 +671,10 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_split2_kernel(VjpSplitArgs a_i
     bf16x8 gs[2][3];  // G in T layout (D[row][o])
     {
       f32x16 gT;
+float gv[16];
+      trow_gather<16>(a.ghead, a.gh, row0, hq, cq, c < A, a.n, gv);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) gT[r] = (c < A ? a.ghead[trow(r) * a.gh + (c < A ? c : 0)] : 0.f) * tval(r);
+      for (int r = 0; r < 16; ++r) gT[r] = gv[r];
       split8(gT, 0, gs[0]);
       split8(gT, 1, gs[1]);
     }
@@ -677,8 +705,10 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_split2_kernel(VjpSplitArgs a_i
     bf16x8 xs[2][3];
     {
       f32x16 xT;
+float xv[16];
+      trow_gather<16>(a.x, a.n_obs, row0, hq, cq, c < a.n_obs, a.n, xv);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) xT[r] = (c < a.n_obs ? a.x[trow(r) * a.n_obs + (c < a.n_obs ? c : 0)] : 0.f) * tval(r);
+      for (int r = 0; r < 16; ++r) xT[r] = xv[r];
       split8(xT, 0, xs[0]);
       split8(xT, 1, xs[1]);
     }
@@ -778,7 +808,8 @@ __global__ __launch_bounds__(256, 1) void mlp_fisher_split_kernel(RowsArgs a, BD
   __syncthreads();
   const float* img = lds;
   const float* imt = lds_opaque(lds + WP);  // the tangent image lies past 64 KB
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j32 = lane & 31;
+  const int lane = threadIdx.x & 63, h = lane >> 5, j32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform tile indices
   float* gtile = lds + WP + WT + wave * 256;
   auto wfrag = [&](int seg, int p, int f) { return frag_at(lds, WT + seg - b.fwd_words + p * BW, f, lane); };
   const MlpDims dd = head_dims(a.d, b);
@@ -902,11 +933,13 @@ __global__ __launch_bounds__(256, 1) void mlp_fisher_split_kernel(RowsArgs a, BD
     bf16x8 gs[2][3];
     {
       f32x16 gT;
+      const float* gb = gtile + 32 * hq + (cq & 7);
+      const float fc = c < A ? 1.f : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float f = row0 + cperm(r, hq) < a.n ? 1.f : 0.f;
+        float f = row0 + 4 * hq + trow_c(r) < a.n ? fc : 0.f;
         asm volatile("" : "+v"(f));
-        gT[r] = (c < A ? gtile[8 * cperm(r, hq) + (cq & 7)] : 0.f) * f;
+        gT[r] = gb[8 * trow_c(r)] * f;
       }
       split8(gT, 0, gs[0]);
       split8(gT, 1, gs[1]);
@@ -914,18 +947,10 @@ __global__ __launch_bounds__(256, 1) void mlp_fisher_split_kernel(RowsArgs a, BD
     WAVE_LDS_ORDER();  // the next tile's writes stay behind these reads
     VJP_SPLIT_FENCE();
     // ---- VJP (mlp_vjp_split2_kernel) of the head rows
-    auto trow = [&](int r) {
-      const int64_t rw = row0 + cperm(r, hq);
-      return rw < a.n ? rw : (int64_t)0;
-    };
-    auto tval = [&](int r) {
-      float f = row0 + cperm(r, hq) < a.n ? 1.f : 0.f;
-      asm volatile("" : "+v"(f));
-      return f;
-    };
+    const float* cb = ct + cache_lane_off(hq, cq);
     auto gather_cache = [&](int slot, f32x16& t) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) t[r] = ct[cache_off_s(slot, cperm(r, hq), cq)];
+      for (int r = 0; r < 16; ++r) t[r] = cb[slot * 1024 + 4 * trow_c(r)];
     };
     bf16x8 gB[3];
     split8v(g8, gB);
@@ -956,8 +981,10 @@ __global__ __launch_bounds__(256, 1) void mlp_fisher_split_kernel(RowsArgs a, BD
     bf16x8 xs[2][3];
     {
       f32x16 xT;
+float xv[16];
+      trow_gather<16>(a.x, a.n_obs, row0, hq, cq, c < a.n_obs, a.n, xv);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) xT[r] = (c < a.n_obs ? a.x[trow(r) * a.n_obs + (c < a.n_obs ? c : 0)] : 0.f) * tval(r);
+      for (int r = 0; r < 16; ++r) xT[r] = xv[r];
       split8(xT, 0, xs[0]);
       split8(xT, 1, xs[1]);
     }
