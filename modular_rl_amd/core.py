@@ -192,7 +192,11 @@ def rollout_cu_split(n_rollout, n_cus):
     if n_rollout <= 0 or 2 * n_rollout > n_cus:
         return None
     r = list(range(n_rollout))
-    return r, list(range(n_rollout, n_cus))
+    # MRL_FIT_CUS caps the fit's share (diagnostic A/B: the fit beside the rollout slows
+    # the rollout's latency chain through shared clock / memory)
+    cap = int(os.environ.get("MRL_FIT_CUS", "0"))
+    hi = n_cus if cap <= 0 else min(n_cus, n_rollout + cap)
+    return r, list(range(n_rollout, hi))
 
 
 def fit_comm_for(comm, beside_rollout):

@@ -79,8 +79,28 @@ constexpr double HP_MB3 = HP_MASS[3], HP_MB2 = HP_MASS[2] + HP_MB3, HP_MB1 = HP_
 constexpr double HP_MB[4] = {HP_MB0, HP_MB1, HP_MB2, HP_MB3};
 constexpr double HP_IMT = 1.0 / HP_MB0;
 
+// a0..a3 by k.  With k a run-time lane value (HopperQuad: the lane's row) the select
+// tree is formed from bit masks the optimiser cannot see through: a plain ternary chain
+// on doubles was compiled into a switch on k -- exec-masked branches around every
+// selection, all four arms issued by the divergent rows, about a dozen times per
+// substep.  Exact either way (a selection).
+__device__ inline double pick_bits(uint32_t m, double x, double y) {  // m ? y : x, m all ones or zero
+  const uint64_t xb = (uint64_t)__double_as_longlong(x), yb = (uint64_t)__double_as_longlong(y);
+  const uint32_t lo = ((uint32_t)yb & m) | ((uint32_t)xb & ~m);
+  const uint32_t hi = ((uint32_t)(yb >> 32) & m) | ((uint32_t)(xb >> 32) & ~m);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+#ifndef MRL_HP_SEL_BITS  // 0: the plain ternary chain (A/B builds, tools/build_ablate.sh)
+#define MRL_HP_SEL_BITS 1
+#endif
+#ifndef MRL_HP_LIM_BITS  // 1: joint limits and the health test without branches as well
+#define MRL_HP_LIM_BITS 0
+#endif
 __device__ inline double sel4(int k, double a0, double a1, double a2, double a3) {
-  return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
+  if (!MRL_HP_SEL_BITS || __builtin_constant_p(k)) return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
+  uint32_t m0 = 0u - (uint32_t)(k & 1), m1 = 0u - (uint32_t)((k >> 1) & 1);
+  asm volatile("" : "+v"(m0), "+v"(m1));
+  return pick_bits(m1, pick_bits(m0, a0, a1), pick_bits(m0, a2, a3));
 }
 
 __device__ inline void hopper_reset(const double* u, double* s) {
@@ -296,8 +316,18 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
   for (int i = 1; i < 4; ++i) {
     const int jj = i - 1, j = 2 + i;
     C[i][i] = C[i][i] + HP_ARM;
+#if MRL_HP_LIM_BITS
+    // joint-limit force: both one-sided forms evaluated, the active one selected by bit
+    // masks (divergent rows make the ternary an exec-masked branch pair per joint)
+    const double cv = -(HP_CL * v[j]);
+    const double flo = fmad(HP_KL, HP_LO[jj] - q[j], cv), fhi = fmad(HP_KL, HP_HI[jj] - q[j], cv);
+    uint32_t mlo = q[j] < HP_LO[jj] ? ~0u : 0u, mhi = q[j] > HP_HI[jj] ? ~0u : 0u;
+    asm volatile("" : "+v"(mlo), "+v"(mhi));
+    const double lim = pick_bits(mlo, pick_bits(mhi, 0.0, fhi), flo);
+#else
     const double lim = q[j] < HP_LO[jj] ? fmad(HP_KL, HP_LO[jj] - q[j], -(HP_CL * v[j]))
                                         : (q[j] > HP_HI[jj] ? fmad(HP_KL, HP_HI[jj] - q[j], -(HP_CL * v[j])) : 0.0);
+#endif
     rhs[j] = fmad(-HP_DAMP, v[j], rhs[j] + tau[jj]) + lim;
   }
   // Schur complement of the translational block, 4x4 LDL^T (oracle hopper_solve)
@@ -338,9 +368,15 @@ __device__ inline void hopper_step(double* s, const float* a, double& rew, bool&
   for (int k = 0; k < HP_FRAME_SKIP; ++k) hopper_substep(q, v, tau, par);
   rew = (q[0] - x_before) / (HP_DT * HP_FRAME_SKIP) + 1.0 - 1e-3 * asq;
   bool healthy = true;
+#if MRL_HP_LIM_BITS  // every test evaluated and combined with & (the && chain: nested branches)
+  for (int i = 0; i < 12; ++i) healthy = healthy & (bool)isfinite(s[i]);
+  for (int i = 2; i < 12; ++i) healthy = healthy & (fabs(s[i]) < 100.0);
+  healthy = healthy & (q[1] > 0.7) & (fabs(q[2]) < 0.2);
+#else
   for (int i = 0; i < 12; ++i) healthy = healthy && isfinite(s[i]);
   for (int i = 2; i < 12; ++i) healthy = healthy && (fabs(s[i]) < 100.0);
   healthy = healthy && (q[1] > 0.7) && (fabs(q[2]) < 0.2);
+#endif
   done = !healthy;
 }
 

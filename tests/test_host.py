@@ -112,3 +112,15 @@ def test_bench_roofline_kernel_is_chosen_per_binary():
     assert bench.dominant_kernel(kinfo) == "rollout_step"
     # without the binary entry (layered nets) the Fisher-product role competes itself
     assert bench.dominant_kernel({"fvp_vjp": {"total_ms": 50.0}, "rollout_step": {"total_ms": 40.0}}) == "fvp_vjp"
+
+
+def test_rollout_cu_split(monkeypatch):
+    """The pipelined loop's CU sets: the rollout's blocks first, the VF fit on the rest
+    (or on MRL_FIT_CUS of them); no split when the rollout wants more than half."""
+    from modular_rl_amd.core import rollout_cu_split
+    r, f = rollout_cu_split(64, 256)
+    assert r == list(range(64)) and f == list(range(64, 256))
+    assert rollout_cu_split(200, 256) is None and rollout_cu_split(0, 256) is None
+    monkeypatch.setenv("MRL_FIT_CUS", "96")
+    r, f = rollout_cu_split(64, 256)
+    assert r == list(range(64)) and f == list(range(64, 160))
