@@ -22,7 +22,28 @@ build/%.o: $(CSRC)/%.hip $(HDRS)
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
+# Host-side UndefinedBehaviorSanitizer build of the same sources (the device code is
+# unchanged: -fsanitize applies to the host compilation only, -Xarch_host before each
+# flag).  tests/test_abi.py::test_host_code_under_ubsan runs the host queries and the
+# argument checks of the C ABI against it in a child process.
+CLANG_RT := $(firstword $(wildcard /opt/rocm/lib/llvm/lib/clang/*/lib/linux))
+UBSAN_FLAGS := -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined
+UBSAN_OBJS := $(patsubst $(CSRC)/%.hip,build/ubsan/%.o,$(SRCS))
+UBSAN_LIB := build/ubsan/libmrl_hip_ubsan.so
+
+ubsan: $(UBSAN_LIB)
+
+build/ubsan/mlp_split.o: HIPFLAGS += -fno-slp-vectorize
+
+build/ubsan/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p build/ubsan
+	$(HIPCC) $(HIPFLAGS) -O1 $(UBSAN_FLAGS) -c $< -o $@
+
+$(UBSAN_LIB): $(UBSAN_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -shared-libsan -Xarch_host -fsanitize=undefined \
+	  -Wl,-rpath,$(CLANG_RT) -o $@ $(UBSAN_OBJS)
+
 clean:
 	rm -rf build $(LIB)
 
-.PHONY: all clean
+.PHONY: all clean ubsan

@@ -174,3 +174,58 @@ def test_gemm_refuses_bad_descriptors():
     rc = lib.mrl_gemm(ctypes.byref(d), None, None)
     assert rc < 0 and b"null" in lib.mrl_last_error()
     assert lib.mrl_gemm_slab_splits(1000, 4) == 4 and lib.mrl_gemm_slab_splits(10, 64) == 1
+
+
+_UBSAN_PROBE = r"""
+import ctypes, sys
+from modular_rl_amd import _lib
+lib = _lib.load()
+# every status-returning entry point with null buffers: an error status, no fault
+for name, (res, args) in _lib.SIGNATURES.items():
+    if name in ("mrl_last_error", "mrl_version", "mrl_stream_destroy"):
+        continue
+    r = getattr(lib, name)(*[None if a is ctypes.c_void_p else 0 for a in args])
+    if res is ctypes.c_int:
+        assert r != 0, name
+# the host-side sizing queries over valid and invalid descriptors and row counts
+for n_in in (1, 4, 11, 16, 17, 32, 33):
+    for n_out in (1, 2, 3, 8, 9):
+        for head in (0, 1, 2):
+            for hid in (64, 128):
+                for cus in (0, 1, 64, 192, 256, 1024):
+                    d = _lib.MlpDesc(n_in, n_out, head, hid, 2, cus)
+                    b = ctypes.byref(d)
+                    for f in ("mrl_mlp_num_params", "mrl_mlp_image_floats", "mrl_mlp_image_words_bf16",
+                              "mrl_mlp_image_words_split"):
+                        getattr(lib, f)(b)
+                    for n in (0, 1, 31, 33, 4194304, 1 << 31):
+                        lib.mrl_mlp_partial_rows(b, n); lib.mrl_mlp_slab_rows(b, n)
+                        lib.mrl_mlp_partial_rows_bf16(b, n); lib.mrl_mlp_slab_rows_bf16(b, n)
+for n in (0, 1, 31, 32, 33, 4194304, 1 << 31):
+    lib.mrl_partial_rows(n); lib.mrl_slab_rows(n); lib.mrl_act_cache_floats(n); lib.mrl_act_cache_words_bf16(n)
+    lib.mrl_cg_state_doubles(n); lib.mrl_moments_workspace_bytes(n); lib.mrl_episode_stats_workspace_bytes(n)
+    lib.mrl_gae_workspace_bytes(n, 1024)
+    for s in (1, 8, 64):
+        lib.mrl_gemm_slab_splits(n, s)
+for e in (-1, 0, 1, 2, 3, 99):
+    lib.mrl_env_state_doubles(e); lib.mrl_filter_doubles(e); lib.mrl_record_doubles(e); lib.mrl_rollout_blocks(e)
+print("UBSAN_PROBE_OK")
+"""
+
+
+def test_host_code_under_ubsan():
+    """The C ABI's host code (argument checks, sizing queries, error paths) built with
+    -fsanitize=undefined on the host side (`make ubsan`; -fno-sanitize-recover: any
+    undefined behaviour aborts) and driven with null buffers and a sweep of valid and
+    invalid descriptors in a child process -- no GPU needed."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    so = os.path.join(root, "build", "ubsan", "libmrl_hip_ubsan.so")
+    subprocess.run(["make", "-j8", "ubsan"], cwd=root, check=True, capture_output=True, timeout=900)
+    env = dict(os.environ, MRL_LIB_PATH=so, PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", _UBSAN_PROBE], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "UBSAN_PROBE_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "runtime error" not in r.stderr, r.stderr[-4000:]
