@@ -232,3 +232,50 @@ def test_fused_fisher_product_grid_for_a_cu_subset(monkeypatch):
         outs.append(ff.clone())
     for o in outs:
         assert torch.equal(o, f2)
+
+
+@pytest.mark.parametrize("head,nin,nout", [("gauss", 11, 3), ("softmax", 4, 2), ("linear", 12, 1), ("gauss", 17, 4)])
+@pytest.mark.parametrize("N", [1, 33, 70001])
+def test_vjp16_valu_head_gradient(head, nin, nout, N, monkeypatch):
+    """The cached 16-row VJP with the head-weight gradient on the VALU (MRL_VJP16_VG2=1,
+    heads of <= 4 outputs) against its MFMA form: the same sums in another order (f32
+    rounding apart), and against the float64 J^T g of the oracle at 1e-4."""
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import MlpNet
+    rng = np.random.default_rng(nin + N)
+    spec = T.Spec(nin, [64, 64], nout, head)
+    th = T.mlp_init(rng, spec.shapes, head == "gauss") + 0.05 * rng.standard_normal(spec.P)
+    th = th.astype(np.float32).astype(np.float64)
+    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
+    kind = {"gauss": _lib.HEAD_GAUSS, "softmax": _lib.HEAD_SOFTMAX, "linear": _lib.HEAD_LINEAR}[head]
+    net = MlpNet(nin, nout, kind)
+    net.set_flat(th)
+    x = _dev(ob)
+    # a recording pass writes the activation cache the VJP reads
+    if head == "linear":
+        tgt = _dev(rng.standard_normal(N))
+        gh = torch.zeros(N, dtype=torch.float32, device="cuda")
+        part = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+        net.rows(_lib.EPI_VFLOSS, x, N, inv_n_global=1.0 / N, target=tgt, ghead=gh, partial=part)
+    else:
+        oldprob = T.policy_prob(spec, th, ob).astype(np.float32).astype(np.float64)
+        act = T.sample(spec, oldprob, rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N))
+        gh = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+        part = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+        a = _dev(act, torch.int32 if head == "softmax" else torch.float32)
+        net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(rng.standard_normal(N)),
+                 oldprob=_dev(oldprob), ghead=gh, partial=part)
+    outs = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("MRL_VJP16_VG2", v)
+        o = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+        net.vjp_flat(x, N, gh, o)
+        outs[v] = o.cpu().numpy().astype(np.float64)
+    assert _rel(outs["1"], outs["0"]) < 1e-5
+    g = gh.cpu().numpy().astype(np.float64).reshape(N, -1)
+    _, acts = T.mlp_forward(spec, th, ob)
+    parts = [p.ravel() for p in T.mlp_vjp(spec, th, acts, g[:, :nout])]
+    if head == "gauss":
+        parts.append(g[:, nout:].sum(axis=0))  # the logstd slot: the rows' own log-std gradients
+    want = np.concatenate(parts)
+    assert _rel(outs["1"], want) < 1e-4
