@@ -90,8 +90,8 @@ __device__ inline double pick_bits(uint32_t m, double x, double y) {  // m ? y :
   const uint32_t hi = ((uint32_t)(yb >> 32) & m) | ((uint32_t)(xb >> 32) & ~m);
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
-#ifndef MRL_HP_SEL_BITS  // 0: the plain ternary chain (A/B builds, tools/build_ablate.sh)
-#define MRL_HP_SEL_BITS 1
+#ifndef MRL_HP_SEL_BITS  // 1: bit-mask selections (A/B build tools/ablate sel1; default once measured)
+#define MRL_HP_SEL_BITS 0
 #endif
 #ifndef MRL_HP_LIM_BITS  // 1: joint limits and the health test without branches as well
 #define MRL_HP_LIM_BITS 0
