@@ -90,11 +90,11 @@ __device__ inline double pick_bits(uint32_t m, double x, double y) {  // m ? y :
   const uint32_t hi = ((uint32_t)(yb >> 32) & m) | ((uint32_t)(xb >> 32) & ~m);
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
-#ifndef MRL_HP_SEL_BITS  // 1: bit-mask selections (A/B build tools/ablate sel1; default once measured)
-#define MRL_HP_SEL_BITS 0
+#ifndef MRL_HP_SEL_BITS  // 0: the plain ternary chain (A/B: r04x rollout 13.87 ms with, 14.05 without)
+#define MRL_HP_SEL_BITS 1
 #endif
-#ifndef MRL_HP_LIM_BITS  // 1: joint limits and the health test without branches as well
-#define MRL_HP_LIM_BITS 0
+#ifndef MRL_HP_LIM_BITS  // 1: joint limits and the health test without branches as well (measured
+#define MRL_HP_LIM_BITS 0  // slower: 14.56 ms, the extra live values spill)
 #endif
 __device__ inline double sel4(int k, double a0, double a1, double a2, double a3) {
   if (!MRL_HP_SEL_BITS || __builtin_constant_p(k)) return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));

@@ -9,7 +9,7 @@ run() {  # name, timeout, bench args...
   timeout -k 10 $t python bench.py "$@" > gpurun_out/${tag}_bench_${n}.json 2> gpurun_out/${tag}_bench_${n}.err || { echo BENCH_FAILED $n; tail -5 gpurun_out/${tag}_bench_${n}.err; exit 1; }
   cat gpurun_out/${tag}_bench_${n}.json
 }
-run humanoid_bf16 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 5 --warmup 1 --dtype bf16
+run humanoid_bf16 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 10 --warmup 1 --dtype bf16
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS"
 for dt in bf16 fp32; do
@@ -22,7 +22,7 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out
 python tools/pmc_traffic.py gpurun_out/${tag}_gemm_fetch gpurun_out/${tag}_gemm_write --gemm $L --key Humanoid-v2/bf16/1024 --out gpurun_out/${tag}_pmc_gemm.json || exit 1
 cat gpurun_out/${tag}_rollout_issue.json | head -30
 run humanoid 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 3 --warmup 1
-# A/B: the VF fit co-scheduled with the wave-per-env rollout on shared CUs
-export MRL_COSCHED_FIT=1; run humanoid_bf16_cosched 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 5 --warmup 1 --dtype bf16 --no-cpu-baseline
+# A/B: the VF fit after the rollout (the default co-schedules it on shared CUs)
+export MRL_COSCHED_FIT=0; run humanoid_bf16_serial_fit 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 10 --warmup 1 --dtype bf16 --no-cpu-baseline
 unset MRL_COSCHED_FIT
 echo R04_B_OK
