@@ -1136,9 +1136,17 @@ __global__ __launch_bounds__(RB) void lrollout_partials_kernel(RollArgs a, int D
   const int k = blockIdx.y * LCOLS + c;
   double* r = a.b.records + (int64_t)rec_parity * a.nb * a.RS + (int64_t)blockIdx.x * a.RS;
   const double* col = a.b.raw_obs + (int64_t)(k < D ? k : 0) * E + e0;
+  // this thread's values (rows g, g + 8, ...) loaded once, all issued together, for both
+  // passes; the sums stay in row order
+  constexpr int PR = ENVS_PER_BLOCK / 8;
+  double cv[PR];
+#pragma unroll
+  for (int q = 0; q < PR; ++q) cv[q] = col[min(g + 8 * q, max(nvalid - 1, 0))];  // clamped: in the column
   double sm = 0.0;
   if (k < D)
-    for (int i = g; i < nvalid; i += 8) sm += col[i];
+#pragma unroll
+    for (int q = 0; q < PR; ++q)
+      if (g + 8 * q < nvalid) sm += cv[q];
   red[g][c] = sm;
   __syncthreads();
   double tot = 0.0;
@@ -1148,10 +1156,12 @@ __global__ __launch_bounds__(RB) void lrollout_partials_kernel(RollArgs a, int D
   __syncthreads();
   double m2 = 0.0;
   if (k < D)
-    for (int i = g; i < nvalid; i += 8) {
-      const double dv = col[i] - mean;
-      m2 += dv * dv;
-    }
+#pragma unroll
+    for (int q = 0; q < PR; ++q)
+      if (g + 8 * q < nvalid) {
+        const double dv = cv[q] - mean;
+        m2 += dv * dv;
+      }
   red[g][c] = m2;
   __syncthreads();
   if (g == 0 && k < D) {
@@ -1203,23 +1213,44 @@ __global__ __launch_bounds__(RB) void lrollout_obs_kernel(RollArgs a, int t) {
   if (threadIdx.x < LCOLS && kbase + (int)threadIdx.x < D) {
     const int k = kbase + threadIdx.x;
     const bool isr = (k == O);
+    // the block records in chunks of LREC: every load of a chunk issued before the
+    // chunk's sums (the sums themselves stay sequential in block order, as the oracle's);
+    // one dependent global load per block per pass had made this launch ~14 us of waiting
+    constexpr int LREC = 16;
     double bn = 0.0, sm = 0.0;
-    for (int b = 0; b < a.nb; ++b) {
-      const double* r = rec + (int64_t)b * a.RS;
-      const double nb_ = r[isr ? 1 : 0];
-      bn += nb_;
-      sm += nb_ * r[2 + k];
+    for (int b0 = 0; b0 < a.nb; b0 += LREC) {
+      double rn[LREC], rm[LREC];
+#pragma unroll
+      for (int q = 0; q < LREC; ++q) {
+        const double* r = rec + (int64_t)min(b0 + q, a.nb - 1) * a.RS;
+        rn[q] = r[isr ? 1 : 0];
+        rm[q] = r[2 + k];
+      }
+#pragma unroll
+      for (int q = 0; q < LREC; ++q)
+        if (b0 + q < a.nb) {
+          bn += rn[q];
+          sm += rn[q] * rm[q];
+        }
     }
     double bm = 0.0, bs = 0.0;
     if (bn > 0.0) {
       bm = sm / bn;
-      for (int b = 0; b < a.nb; ++b) {
-        const double* r = rec + (int64_t)b * a.RS;
-        const double nb_ = r[isr ? 1 : 0];
-        if (nb_ > 0.0) {
-          const double dm = r[2 + k] - bm;
-          bs += r[2 + D + k] + nb_ * dm * dm;
+      for (int b0 = 0; b0 < a.nb; b0 += LREC) {
+        double rn[LREC], rm[LREC], rs[LREC];
+#pragma unroll
+        for (int q = 0; q < LREC; ++q) {
+          const double* r = rec + (int64_t)min(b0 + q, a.nb - 1) * a.RS;
+          rn[q] = r[isr ? 1 : 0];
+          rm[q] = r[2 + k];
+          rs[q] = r[2 + D + k];
         }
+#pragma unroll
+        for (int q = 0; q < LREC; ++q)
+          if (b0 + q < a.nb && rn[q] > 0.0) {
+            const double dm = rm[q] - bm;
+            bs += rs[q] + rn[q] * dm * dm;
+          }
       }
     }
     double n = fs_in[isr ? 1 : 0], M = fs_in[2 + k], S = fs_in[2 + D + k];

@@ -26,7 +26,8 @@ STEP_KERNELS = ("lrollout_obs_kernel", "cast_rows_bf16_kernel", "gemm_bf16_small
 
 
 def short(name):
-    return name.split("(")[0].split("<")[0].replace("void ", "").strip()
+    # "void mrl::gemm_bf16_small_kernel<true>(...)" -> "gemm_bf16_small_kernel"
+    return name.split("(")[0].split("<")[0].replace("void ", "").strip().split("::")[-1]
 
 
 def main():
