@@ -12,4 +12,5 @@ run() {  # name, bench args...
 run hopper_bf16 --dtype bf16
 run cartpole_bf16 --env CartPole-v0 --dtype bf16
 run cartpole --env CartPole-v0
+run humanoid_bf16 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 10 --warmup 1 --dtype bf16
 echo R04_LINES_OK
