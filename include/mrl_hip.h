@@ -243,6 +243,9 @@ typedef struct {
   const float* bias;    /* [n] or NULL                                                    */
   const uint16_t* h;    /* DTANH: bf16 [m, ldh] activations                               */
   int64_t ldh;
+  int32_t lds_limit;    /* 0, or the LDS bytes per block the GEMM may use: only kernels of
+                         * at most that footprint, never the persistent CU-holding ones (a
+                         * GEMM co-scheduled beside the wave-per-env rollout); same results */
 } mrl_gemm_bf16_desc;
 int mrl_gemm_bf16(const mrl_gemm_bf16_desc* g, const int32_t* skip, void* stream);
 
@@ -260,6 +263,7 @@ typedef struct {
   int32_t splits;
   float* slab;
   int64_t slab_stride, ldc;
+  int32_t lds_limit;    /* as mrl_gemm_bf16_desc.lds_limit */
 } mrl_gemm_bf16_tn_desc;
 int mrl_gemm_bf16_tn(const mrl_gemm_bf16_tn_desc* g, const int32_t* skip, void* stream);
 /* y[r, c] = bf16(x[r, c]) (RNE) for c < cols, 0 for cols <= c < ldy */

@@ -53,12 +53,13 @@ class GemmDesc(ctypes.Structure):
 class GemmBf16Desc(ctypes.Structure):
     _fields_ = [("m", i64), ("n", i64), ("k", i64), ("a", vp), ("lda", i64), ("bt", vp), ("ldb", i64), ("a2", vp),
                 ("bt2", vp), ("c", vp), ("ldc", i64), ("c_bf16", i32), ("epilogue", i32), ("bias", vp), ("h", vp),
-                ("ldh", i64)]
+                ("ldh", i64), ("lds_limit", i32)]
 
 
 class GemmBf16TnDesc(ctypes.Structure):
     _fields_ = [("m", i64), ("n", i64), ("k", i64), ("a", vp), ("lda", i64), ("b", vp), ("ldb", i64),
-                ("ones_row", i32), ("splits", i32), ("slab", vp), ("slab_stride", i64), ("ldc", i64)]
+                ("ones_row", i32), ("splits", i32), ("slab", vp), ("slab_stride", i64), ("ldc", i64),
+                ("lds_limit", i32)]
 
 
 class RolloutDesc(ctypes.Structure):

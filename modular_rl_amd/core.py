@@ -240,8 +240,13 @@ class IterationRunner:
             # C5 (r04x, Humanoid bf16, 1024 envs): 487 -> 450 ms per iteration at 3 steps
             # (the rollout 235 -> 289 ms beside the fit, the 124 ms fit hidden); MRL_COSCHED_FIT=0
             # keeps the fit after the rollout
-            cosched = (pipeline and split is None and getattr(collector, "wave_per_env", False)
-                       and os.environ.get("MRL_COSCHED_FIT", "1") == "1")
+            cosched_ok = (split is None and getattr(collector, "wave_per_env", False)
+                          and os.environ.get("MRL_COSCHED_FIT", "1") == "1")
+            cosched = pipeline and cosched_ok
+            if cosched_ok and hasattr(vf_net, "lds_limit"):
+                # in BOTH orders (its kernels' choice must not depend on the order):
+                # MRL_COSCHED_LDS bytes of LDS per GEMM block, 0 = no limit
+                vf_net.lds_limit = int(os.environ.get("MRL_COSCHED_LDS", "0"))
             if cosched:
                 # Humanoid's wave-per-env step wants every CU (E / 4), so no disjoint split:
                 # the fit of iteration k shares the CUs with the rollout of k+1 (two plain

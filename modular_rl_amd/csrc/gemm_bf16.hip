@@ -1238,6 +1238,29 @@ int mrl_gemm_bf16(const mrl_gemm_bf16_desc* d, const int32_t* skip, void* stream
 #define MRL_GEMM_BF16_BK 64
 #endif
   constexpr int BK = MRL_GEMM_BF16_BK;
+  // lds_limit: the tiled kernel only (the big, streaming and small-M kernels hold 100-132 KB
+  // of LDS per block, the first two for the whole product), with 32-deep K stages when the
+  // 64-deep ones do not fit the limit; every NN kernel sums each output's k-steps of 16 in
+  // the same order, so the results do not change
+  const int64_t lim = d->lds_limit > 0 ? d->lds_limit : 0;
+  if (lim > 0) {
+    const bool k64 = (int64_t)sizeof(bfr_t) * 2 * (QBM + (g.N <= 32 ? 32 : 128)) * (64 + 8) <= lim;
+#define MRL_TILED(BKX)                                                                                      \
+  do {                                                                                                      \
+    if (g.N <= 32) {                                                                                        \
+      if (bf) hipLaunchKernelGGL((gemm_bf16_kernel<32, true, BKX>), dim3(1, gm), dim3(256), 0, s, g);        \
+      else hipLaunchKernelGGL((gemm_bf16_kernel<32, false, BKX>), dim3(1, gm), dim3(256), 0, s, g);          \
+    } else {                                                                                                \
+      const dim3 grid((unsigned)((g.N + 127) / 128), gm);                                                   \
+      if (bf) hipLaunchKernelGGL((gemm_bf16_kernel<128, true, BKX>), grid, dim3(256), 0, s, g);              \
+      else hipLaunchKernelGGL((gemm_bf16_kernel<128, false, BKX>), grid, dim3(256), 0, s, g);                \
+    }                                                                                                       \
+  } while (0)
+    if (k64) MRL_TILED(64);
+    else MRL_TILED(32);
+#undef MRL_TILED
+    return hip_check(hipGetLastError(), "mrl_gemm_bf16");
+  }
   if (big_gemm_launch(g, bf, d->a2 != nullptr, s)) return hip_check(hipGetLastError(), "mrl_gemm_bf16");
   {
     // small M (the Humanoid rollout's per-step layers): whole-K panels, 64 x 64 tiles
@@ -1294,7 +1317,7 @@ int mrl_gemm_bf16_tn(const mrl_gemm_bf16_tn_desc* d, const int32_t* skip, void* 
   {
     // 256 x 256 tiles for the wide layers (m_real, N >= 256; the ones-row rides row tile 0)
     const char* e = getenv("MRL_GEMM_TN_BIG");
-    const bool big = e ? atoi(e) != 0 : true;
+    const bool big = (e ? atoi(e) != 0 : true) && d->lds_limit <= 0;  // lds_limit: the 41 KB tiled kernel
     if (big && g.m_real >= TBM && g.N >= TBN && g.m_real % 8 == 0 && g.N % 8 == 0) {
       TnPlan pl;
       pl.ntm = (int)((g.m_real + TBM - 1) / TBM);

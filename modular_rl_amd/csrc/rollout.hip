@@ -1333,11 +1333,48 @@ __global__ __launch_bounds__(RB) void lrollout_act_kernel(RollArgs a, const floa
 
 // Humanoid-v2 on the layered rollout: one wave per env (humanoid.h), its state in LDS.
 // hm_reset_kernel = lrollout_reset_kernel, hm_act_kernel = lrollout_act_kernel.
-__global__ __launch_bounds__(64) void hm_reset_kernel(RollArgs a) {
-  __shared__ hm::Wave W;
-  const int E = a.d.n_envs, e = blockIdx.x, lane = threadIdx.x;
+// WPB waves (envs) per block: 1 -- a one-wave block per env, padded so that at most four
+// share a CU (hm_lds_pad) -- or 4 -- four envs per block sharing one copy of the model
+// tables (94 KB of LDS, so one block per CU; the LDS left beside it takes a co-scheduled
+// kernel's blocks without displacing an env).  Waves are independent after the tables'
+// barrier (a wave's LDS operations complete in issue order).
+// The tables and (WPB = 1) the env's state are static LDS objects -- their addresses are
+// constants the ds instructions take as offsets; the WPB = 4 states sit in dynamic LDS
+// after them, one wave-uniform base each.
+template <int WPB>
+__device__ inline hm::Wave& hm_block(int& e, int& lane) {
+  extern __shared__ __attribute__((aligned(16))) double hm_dyn[];
+  lane = threadIdx.x & 63;
+  if constexpr (WPB == 1) {
+    __shared__ hm::Wave W1;
+    e = blockIdx.x;
+    return W1;
+  } else {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    e = blockIdx.x * WPB + wave;
+    return reinterpret_cast<hm::Wave*>(hm_dyn)[wave];
+  }
+}
+template <int WPB>
+__device__ inline void hm_load_tables(hm::Shared& S, int lane) {
+  if (WPB == 1) {
+    hm::load_shared(S, lane);
+  } else {  // the block's waves copy disjoint parts, then wait for each other
+    const double* src = reinterpret_cast<const double*>(&hm::SHARED);
+    double* dst = reinterpret_cast<double*>(&S);
+    for (int i = threadIdx.x; i < (int)(sizeof(hm::Shared) / 8); i += 64 * WPB) dst[i] = src[i];
+    __syncthreads();
+  }
+}
+
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void hm_reset_kernel(RollArgs a) {
   __shared__ hm::Shared S;
-  hm::load_shared(S, lane);
+  int e, lane;
+  hm::Wave& W = hm_block<WPB>(e, lane);
+  const int E = a.d.n_envs;
+  hm_load_tables<WPB>(S, lane);
+  if (e >= E) return;  // after the tables' barrier
   const uint32_t w = (uint32_t)a.b.env_int[E + e];
   hm::reset(W, lane, a.d.seed, (uint32_t)(a.d.env_offset + e), (uint64_t)w);
   hm::forward(W, S, lane);
@@ -1386,14 +1423,17 @@ __device__ inline float head_z(const HeadRows& hr, int e, int lane) {
   return z;
 }
 
-__global__ __launch_bounds__(64) void hm_act_kernel(RollArgs a, const float* __restrict__ zrows, HeadRows hr,
-                                                    const float* __restrict__ logstd, int t) {
-  __shared__ hm::Wave W;
-  constexpr int A = HM_ACT;
-  const int E = a.d.n_envs, e = blockIdx.x, lane = threadIdx.x;
-  const int64_t row = (int64_t)t * E + e;
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB) void hm_act_kernel(RollArgs a, const float* __restrict__ zrows, HeadRows hr,
+                                                          const float* __restrict__ logstd, int t) {
   __shared__ hm::Shared S;
-  hm::load_shared(S, lane);
+  int e, lane;
+  hm::Wave& W = hm_block<WPB>(e, lane);
+  constexpr int A = HM_ACT;
+  const int E = a.d.n_envs;
+  hm_load_tables<WPB>(S, lane);
+  if (e >= E) return;  // after the tables' barrier
+  const int64_t row = (int64_t)t * E + e;
   if (lane < HM_NS) W.s[lane] = a.b.env_state[(int64_t)lane * E + e];
   const bool fused = hr.hid != nullptr || hr.hid16 != nullptr;
   const float zh = fused ? head_z(hr, e, lane) : 0.f;
@@ -1416,7 +1456,7 @@ __global__ __launch_bounds__(64) void hm_act_kernel(RollArgs a, const float* __r
   double x_before = 0.0, rew = 0.0;
   // diagnostic stamps of block 0 (cols 0-11: phases of pass 1, 12/15 realtime and
   // 13/14 shader clock at kernel start / end) -- never set in production
-  int64_t* st = (a.b.stamps != nullptr && blockIdx.x == 0) ? a.b.stamps + (int64_t)t * 16 : nullptr;
+  int64_t* st = (a.b.stamps != nullptr && e == 0) ? a.b.stamps + (int64_t)t * 16 : nullptr;
   if (st != nullptr && lane == 0) {
     st[12] = (int64_t)__builtin_amdgcn_s_memrealtime();
     st[13] = (int64_t)__builtin_amdgcn_s_memtime();
@@ -1479,6 +1519,15 @@ static size_t hm_lds_pad(int n_envs) {
   if (ncu <= 0 || n_envs > 4 * ncu) return 0;
   constexpr size_t LDS_CU = 160 * 1024, used = sizeof(hm::Wave) + sizeof(hm::Shared), want = LDS_CU / 5 + 1024;
   return used < want ? want - used : 0;
+}
+// MRL_HM_WPB=4 (per launch): four envs per block (hm_block); default 1
+static int hm_wpb() {
+  const char* e = getenv("MRL_HM_WPB");
+  return (e && atoi(e) == 4) ? 4 : 1;
+}
+// dynamic LDS of a launch (the static tables / state come on top)
+static size_t hm_lds_bytes(int wpb, int n_envs) {
+  return wpb == 1 ? hm_lds_pad(n_envs) : (size_t)wpb * sizeof(hm::Wave);
 }
 
 __global__ void rollout_finish_kernel(RollArgs a, int O) {
@@ -1606,9 +1655,13 @@ int mrl_rollout_reset_rows(const mrl_rollout_desc* d, const mrl_rollout_bufs* b,
   const int D = env_info(d->env_id).obs + 1;
   // one wave per block: the per-env step is latency-bound, so spread the waves over CUs
   const dim3 genv((d->n_envs + 63) / 64), gpart(a.nb, (D + LCOLS - 1) / LCOLS);
-  if (d->env_id == MRL_ENV_HUMANOID)
-    hipLaunchKernelGGL(hm_reset_kernel, dim3(d->n_envs), dim3(64), 0, (hipStream_t)stream, a);
-  else if (d->env_id == MRL_ENV_CARTPOLE)
+  if (d->env_id == MRL_ENV_HUMANOID) {
+    const int wpb = hm_wpb();
+    const dim3 gb((d->n_envs + wpb - 1) / wpb), bb(64 * wpb);
+    const size_t lds = wpb == 1 ? 0 : (size_t)wpb * sizeof(hm::Wave);
+    if (wpb == 4) hipLaunchKernelGGL(hm_reset_kernel<4>, gb, bb, lds, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL(hm_reset_kernel<1>, gb, bb, lds, (hipStream_t)stream, a);
+  } else if (d->env_id == MRL_ENV_CARTPOLE)
     hipLaunchKernelGGL(lrollout_reset_kernel<MRL_ENV_CARTPOLE>, genv, dim3(64), 0, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(lrollout_reset_kernel<MRL_ENV_HOPPER>, genv, dim3(64), 0, (hipStream_t)stream, a);
@@ -1645,10 +1698,13 @@ static int rollout_act(const mrl_rollout_desc* d, int32_t head, int32_t n_out, c
   RollArgs a = make_args(d, b);
   const int D = ei.obs + 1;
   const dim3 genv((d->n_envs + 63) / 64), gpart(a.nb, (D + LCOLS - 1) / LCOLS);
-  if (d->env_id == MRL_ENV_HUMANOID)
-    hipLaunchKernelGGL(hm_act_kernel, dim3(d->n_envs), dim3(64), hm_lds_pad(d->n_envs), (hipStream_t)stream, a, z, hr,
-                       logstd, t);
-  else if (d->env_id == MRL_ENV_CARTPOLE)
+  if (d->env_id == MRL_ENV_HUMANOID) {
+    const int wpb = hm_wpb();
+    const dim3 gb((d->n_envs + wpb - 1) / wpb), bb(64 * wpb);
+    const size_t lds = hm_lds_bytes(wpb, d->n_envs);
+    if (wpb == 4) hipLaunchKernelGGL(hm_act_kernel<4>, gb, bb, lds, (hipStream_t)stream, a, z, hr, logstd, t);
+    else hipLaunchKernelGGL(hm_act_kernel<1>, gb, bb, lds, (hipStream_t)stream, a, z, hr, logstd, t);
+  } else if (d->env_id == MRL_ENV_CARTPOLE)
     hipLaunchKernelGGL(lrollout_act_kernel<MRL_ENV_CARTPOLE>, genv, dim3(64), 0, (hipStream_t)stream, a, z, logstd, t);
   else
     hipLaunchKernelGGL(lrollout_act_kernel<MRL_ENV_HOPPER>, genv, dim3(64), 0, (hipStream_t)stream, a, z, logstd, t);

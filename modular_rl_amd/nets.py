@@ -334,6 +334,10 @@ class LayeredMlpNet:
         # Humanoid step's hidden layers (forward_hidden_rows_b16)
         # (hidden widths a multiple of 8: the bf16 rows are 16-B aligned with no padding)
         self.tape_bf16 = self.compute == _lib.COMPUTE_BF16 and all(h % 8 == 0 for h in self.hid_sizes)
+        # LDS bytes per block the bf16 GEMMs may use (0: any kernel): a net whose passes run
+        # co-scheduled beside the wave-per-env rollout takes the tiled kernels only, whose
+        # short-lived blocks leave room for the rollout's (core.IterationRunner)
+        self.lds_limit = 0
 
     # ---- flat parameter plumbing
     def get_flat(self):
@@ -439,7 +443,8 @@ class LayeredMlpNet:
     def _gemm_b16(self, m, n, k, a, lda, bt, ldb, c, ldc, c_bf16, epi, a2=None, bt2=None, bias=None, h=None, ldh=0,
                   skip=None):
         g = _lib.GemmBf16Desc(m=m, n=n, k=k, a=ptr(a), lda=lda, bt=ptr(bt), ldb=ldb, a2=ptr(a2), bt2=ptr(bt2),
-                              c=ptr(c), ldc=ldc, c_bf16=int(c_bf16), epilogue=epi, bias=bias, h=ptr(h), ldh=ldh)
+                              c=ptr(c), ldc=ldc, c_bf16=int(c_bf16), epilogue=epi, bias=bias, h=ptr(h), ldh=ldh,
+                              lds_limit=self.lds_limit)
         if timing.enabled() and m >= GEMM_TIMING_MIN_ROWS:
             prods = 2 if a2 is not None else 1
             nbytes = 2 * prods * (m * k + n * k) + (2 if c_bf16 else 4) * m * n + (2 * m * n if h is not None else 0)
@@ -623,7 +628,7 @@ class LayeredMlpNet:
             inp, lda = (Xb, ldx) if l == 0 else (H[l - 1], din)
             g = _lib.GemmBf16TnDesc(m=din + 1, n=dout, k=n, a=ptr(inp), lda=lda, b=ptr(G), ldb=ldg, ones_row=1,
                                     splits=self.SLAB_SPLITS, slab=self._addr(slab, self.w_off[l]),
-                                    slab_stride=self.P, ldc=dout)
+                                    slab_stride=self.P, ldc=dout, lds_limit=self.lds_limit)
             if timing.enabled() and n >= GEMM_TIMING_MIN_ROWS:
                 timing.region(f"gemm:bf16:TN:{din + 1}x{dout}x{n}", call, "mrl_gemm_bf16_tn", ctypes.byref(g),
                               ptr(skip), stream(), flop=2 * (din + 1) * dout * n,

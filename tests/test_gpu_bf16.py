@@ -752,3 +752,66 @@ def test_bf16_big_tile_gemm_equals_tiled(epi, monkeypatch):
             want = want * (1.0 - hb * hb)
         got = f32_out.cpu().numpy().reshape(M, N)[rows].astype(np.float64)
         assert np.abs(got - want).max() / np.abs(want).max() < 2e-5, (M, N, K, dual)
+
+
+def test_bf16_lds_limited_gemms_equal_default(monkeypatch):
+    """The LDS-capped dispatch (desc.lds_limit > 0: the VF fit's GEMMs while they share CUs
+    with the Humanoid rollout) takes only the non-persistent 128-row tiled kernels -- BK 64
+    under an 80 KB cap, BK 32 under 64 KB -- and must write what the default dispatch (the
+    persistent 256 x 256 kernels at these sizes) writes, bit for bit: NN single / dual,
+    tanh / dtanh epilogues, f32 / bf16 outputs, row / K / N tails; TN slabs with the
+    ones-row."""
+    import ctypes
+
+    from modular_rl_amd import _lib
+    from modular_rl_amd._lib import call, stream
+    rng = np.random.default_rng(21)
+    monkeypatch.setenv("MRL_GEMM_STREAM_MIN_M", "0")
+    for (M, N, K, ldk, dual, E) in [(70001, 512, 512, 512, True, _lib.GEMM_DTANH),
+                                    (35000, 300, 377, 384, False, _lib.GEMM_TANH),
+                                    (20000, 17, 512, 512, False, _lib.GEMM_STORE)]:
+        A, A2 = rng.standard_normal((M, K)), rng.standard_normal((M, K))
+        W, W2 = rng.standard_normal((K, N)) * 0.05, rng.standard_normal((K, N)) * 0.05
+        bias = _dev(rng.standard_normal(N).astype(np.float32))
+        dA, dA2, dH = _bf16_dev(A, ldk), _bf16_dev(A2, ldk), _bf16_dev(np.tanh(rng.standard_normal((M, N))), N)
+        Bt = torch.zeros(N * ldk, dtype=torch.int16, device="cuda")
+        Bt2 = torch.zeros(N * ldk, dtype=torch.int16, device="cuda")
+        for w, bt in ((W, Bt), (W2, Bt2)):
+            dw = _dev(w.astype(np.float32))
+            call("mrl_pack_w_bf16", ctypes.c_void_p(dw.data_ptr()), K, N, 1, ctypes.c_void_p(bt.data_ptr()), ldk,
+                 stream())
+        for out_bf in (0, 1):
+            outs = []
+            for lim in (0, 81920, 65536):
+                C = torch.full((M * N,), -7, dtype=torch.int16, device="cuda") if out_bf else \
+                    torch.full((M * N,), float("nan"), dtype=torch.float32, device="cuda")
+                g = _lib.GemmBf16Desc(m=M, n=N, k=K, a=ctypes.c_void_p(dA.data_ptr()), lda=ldk,
+                                      bt=ctypes.c_void_p(Bt.data_ptr()), ldb=ldk,
+                                      a2=ctypes.c_void_p(dA2.data_ptr()) if dual else None,
+                                      bt2=ctypes.c_void_p(Bt2.data_ptr()) if dual else None,
+                                      c=ctypes.c_void_p(C.data_ptr()), ldc=N, c_bf16=out_bf, epilogue=E,
+                                      bias=ctypes.c_void_p(bias.data_ptr()), h=ctypes.c_void_p(dH.data_ptr()),
+                                      ldh=N, lds_limit=lim)
+                call("mrl_gemm_bf16", ctypes.byref(g), None, stream())
+                torch.cuda.synchronize()
+                outs.append(C)
+            for i in (1, 2):
+                assert torch.equal(outs[0], outs[i]), (M, N, K, dual, out_bf, i, (outs[0] != outs[i]).sum().item())
+    for (R, din, dout, ones, splits) in [(40000, 512, 512, True, 64), (5000, 376, 300, True, 7)]:
+        lda, ldb = (din + 7) // 8 * 8, (dout + 7) // 8 * 8
+        dX, dG = _bf16_dev(rng.standard_normal((R, din)), lda), _bf16_dev(rng.standard_normal((R, dout)), ldb)
+        Mr = din + (1 if ones else 0)
+        S = int(_lib.load().mrl_gemm_slab_splits(R, splits))
+        outs = []
+        for lim in (0, 65536):
+            slab = torch.full((S * Mr * dout,), float("nan"), dtype=torch.float32, device="cuda")
+            g = _lib.GemmBf16TnDesc(m=Mr, n=dout, k=R, a=ctypes.c_void_p(dX.data_ptr()), lda=lda,
+                                    b=ctypes.c_void_p(dG.data_ptr()), ldb=ldb, ones_row=int(ones), splits=splits,
+                                    slab=ctypes.c_void_p(slab.data_ptr()), slab_stride=Mr * dout, ldc=dout,
+                                    lds_limit=lim)
+            call("mrl_gemm_bf16_tn", ctypes.byref(g), None, stream())
+            torch.cuda.synchronize()
+            outs.append(slab.view(S, Mr, dout))
+        # the rows above the ones-row: same per-slab k order in both kernels (the ones-row
+        # differs in summation order between the 256 and 128 kernels, as tested above)
+        assert torch.equal(outs[0][:, :din], outs[1][:, :din]), (R, din, dout)

@@ -184,3 +184,28 @@ def test_c5_width_rollout_invariants_and_update(dtype):
     assert 0 <= stats["pol_kl_after"] <= 2 * max_kl, stats["pol_kl_after"]
     assert stats["pol_surr_after"] < stats["pol_surr_before"]
     assert np.isfinite(stats["vf_loss_after"]) and stats["vf_loss_after"] <= stats["vf_loss_before"]
+
+
+@pytest.mark.parametrize("E,Tn,hid", [(1026, 6, [256, 256]), (64, 60, [64, 64])])
+def test_humanoid_four_envs_per_block_equals_one(E, Tn, hid, monkeypatch):
+    """MRL_HM_WPB=4 (four env waves per Humanoid block, the wave state in dynamic LDS, the
+    model tables loaded once per block) against the default one-wave blocks: the same
+    per-env arithmetic, so flags, observations, actions, rewards and the filter state
+    agree bit for bit -- a ragged last block (1026 = 256 x 4 + 2) and mid-horizon
+    terminations with auto-reset (64 envs x 60 steps)."""
+    from modular_rl_amd.collector import Collector
+    from modular_rl_amd.envs import make
+    env = make("Humanoid-v2")
+    _, _, pol = _layered_policy("gauss", 376, 17, hid, seed=5)
+    outs = []
+    for wpb in ("1", "4"):
+        monkeypatch.setenv("MRL_HM_WPB", wpb)
+        col = Collector(env, pol, E, Tn, 1000, seed=11, use_graph=False)
+        for _ in range(2):
+            b = col.collect()
+        torch.cuda.synchronize()
+        outs.append((b.flags.clone(), b.obs.clone(), b.act.clone(), b.rew.clone(), col.filter_state.clone()))
+    if Tn >= 60:
+        assert ((outs[0][0] & 2) != 0).any()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

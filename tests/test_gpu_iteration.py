@@ -78,11 +78,15 @@ def test_prelaunched_rollout_is_bit_identical(pipeline):
             assert x[k] == y[k] or (np.isnan(x[k]) and np.isnan(y[k])), k
 
 
-def test_cosched_fit_beside_wave_per_env_rollout_is_bit_identical(monkeypatch):
+@pytest.mark.parametrize("lds,wpb", [("0", "1"), ("65536", "4")])
+def test_cosched_fit_beside_wave_per_env_rollout_is_bit_identical(lds, wpb, monkeypatch):
     """C5's per-GPU width (1024 Humanoid envs: the wave-per-env step wants E / 4 = 256 CUs,
     so no disjoint CU split): with MRL_COSCHED_FIT=1 the VF fit of iteration k shares the
-    CUs with the rollout of k+1 on two plain streams, bit-identical to the reference order."""
+    CUs with the rollout of k+1 on two plain streams, bit-identical to the reference order;
+    also with the fit's GEMMs capped at 64 KB of LDS and four-env Humanoid blocks."""
     monkeypatch.setenv("MRL_COSCHED_FIT", "1")
+    monkeypatch.setenv("MRL_COSCHED_LDS", lds)
+    monkeypatch.setenv("MRL_HM_WPB", wpb)
     kw = dict(n_envs=1024, horizon=8, hid_sizes=[64, 64])
     r0, a0, c0, s0 = _run("Humanoid-v2", False, **kw)
     r1, a1, c1, s1 = _run("Humanoid-v2", True, prelaunch=True, **kw)
