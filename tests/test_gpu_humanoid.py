@@ -189,7 +189,7 @@ def test_c5_width_rollout_invariants_and_update(dtype):
 @pytest.mark.parametrize("E,Tn,hid", [(1026, 6, [256, 256]), (64, 60, [64, 64])])
 def test_humanoid_four_envs_per_block_equals_one(E, Tn, hid, monkeypatch):
     """MRL_HM_WPB=4 (four env waves per Humanoid block, the wave state in dynamic LDS, the
-    model tables loaded once per block) against the default one-wave blocks: the same
+    model tables loaded once per block; the default) against one-wave blocks: the same
     per-env arithmetic, so flags, observations, actions, rewards and the filter state
     agree bit for bit -- a ragged last block (1026 = 256 x 4 + 2) and mid-horizon
     terminations with auto-reset (64 envs x 60 steps)."""
