@@ -251,9 +251,9 @@ class IterationRunner:
                 # Humanoid's wave-per-env step wants every CU (E / 4), so no disjoint split:
                 # the fit of iteration k shares the CUs with the rollout of k+1 (two plain
                 # streams; one wave per SIMD in the step kernel leaves issue slots free)
-                # MRL_COSCHED_PRIO=1: the rollout's stream at high priority, so the
+                # MRL_COSCHED_PRIO (default 1; r04j +1 %): the rollout stream at high priority, so the
                 # dispatcher places its per-step blocks ahead of the fit's when both wait
-                prio = -1 if os.environ.get("MRL_COSCHED_PRIO", "0") == "1" else 0
+                prio = -1 if os.environ.get("MRL_COSCHED_PRIO", "1") == "1" else 0
                 self.rollout_stream = torch.cuda.Stream(priority=prio)
                 self.fit_stream = torch.cuda.Stream()
             if pipeline and (split is not None or cosched):
