@@ -426,6 +426,9 @@ typedef struct {
                               mrl_rollout_noise, or injected (parity tests)       */
   int64_t* stamps;         /* optional diagnostic: [T, 16] s_memrealtime of block 0 phases (NULL in production) */
   double* raw_obs;         /* layered rollout: [obs_dim+1, E] raw next obs + reward (SoA) */
+  uint16_t* obs_bf16;      /* layered rollout, optional: [E, ld8(obs_dim)] the step's filtered
+                              rows also as bf16 (RNE; the first hidden GEMM's operand), columns
+                              obs_dim.. left as they are (caller zeroes them once); NULL: none */
 } mrl_rollout_bufs;
 
 int64_t mrl_env_state_doubles(int32_t env_id);

@@ -70,7 +70,7 @@ class RolloutDesc(ctypes.Structure):
 class RolloutBufs(ctypes.Structure):
     _fields_ = [("env_state", vp), ("env_int", vp), ("filter_state", vp), ("records", vp), ("iteration", vp),
                 ("obs", vp), ("act", vp), ("prob", vp), ("rew", vp), ("flags", vp), ("ep_t", vp), ("noise", vp),
-                ("stamps", vp), ("raw_obs", vp)]
+                ("stamps", vp), ("raw_obs", vp), ("obs_bf16", vp)]
 
 
 # name -> (restype, argtypes); every symbol include/mrl_hip.h declares

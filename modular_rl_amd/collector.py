@@ -220,7 +220,7 @@ class Collector:
                                 ptr(self.iteration), ptr(self.obs), ptr(self.act), ptr(self.prob), ptr(self.rew),
                                 ptr(self.flags), ptr(self.ep_t),
                                 ptr(self.noise if self.noise is not None else self._noise_rows), ptr(self.stamps),
-                                ptr(self.raw_obs))
+                                ptr(self.raw_obs), ptr(self._xb16 if self.hidden_b16 else None))
 
     def fill_noise(self):
         """This iteration's sampling noise, one parallel draw over every row (no-op when
@@ -256,7 +256,8 @@ class Collector:
             call("mrl_rollout_obs", d, ctypes.byref(bufs), int(t), stream())
             x = self.obs[t * E:(t + 1) * E]
             if self.hidden_b16:
-                hid = net.forward_hidden_rows_b16(x, E, wt, self._fwd_b16, self._xb16)
+                # mrl_rollout_obs wrote the step's rows into _xb16 as bf16 too (obs_bf16)
+                hid = net.forward_hidden_rows_b16(x, E, wt, self._fwd_b16, self._xb16, cast=False)
                 call("mrl_rollout_act_head_bf16", d, int(net.head), int(net.n_out), ptr(hid), int(net.dims[L - 1]),
                      net._addr(net.theta, net.w_off[L - 1]), net._addr(net.theta, net.b_off[L - 1]), logstd,
                      ctypes.byref(bufs), int(t), stream())

@@ -1295,10 +1295,16 @@ __global__ __launch_bounds__(RB) void lrollout_obs_kernel(RollArgs a, int t) {
     const int el = threadIdx.x / G, part = threadIdx.x % G;
     if (el < nvalid) {
       float* dst = a.b.obs + (row0 + el) * O;
+      // the bf16 twin of the row for the first hidden GEMM (mrl_cast_rows_bf16's RNE)
+      uint16_t* dsb = a.b.obs_bf16 ? a.b.obs_bf16 + (int64_t)(e0 + el) * ((O + 7) / 8 * 8) : nullptr;
 #pragma unroll
       for (int q = 0; q < CPT; ++q) {
         const int k = kbase + part * CPT + q;
-        if (k < O) dst[k] = tile[(part * CPT + q) * (ENVS_PER_BLOCK + 1) + el];
+        const float v = tile[(part * CPT + q) * (ENVS_PER_BLOCK + 1) + el];
+        if (k < O) {
+          dst[k] = v;
+          if (dsb) dsb[k] = __builtin_bit_cast(uint16_t, (__bf16)v);
+        }
       }
     }
   }

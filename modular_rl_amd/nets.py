@@ -15,6 +15,7 @@ implementations share one interface (``rows`` / ``vjp_flat`` / ``forward``):
 
 ``make_net`` picks the fused path whenever the shape allows it.
 """
+import contextlib
 import ctypes
 import os
 
@@ -338,6 +339,10 @@ class LayeredMlpNet:
         # co-scheduled beside the wave-per-env rollout takes the tiled kernels only, whose
         # short-lived blocks leave room for the rollout's (core.IterationRunner)
         self.lds_limit = 0
+        # rows pinned by pin_input (the VF fit's features, read by every L-BFGS
+        # evaluation): (x ptr, n, ep_t ptr) -> the tape's input (X, ldx) as last built
+        self._pinned = None
+        self._pinned_input = None
 
     # ---- flat parameter plumbing
     def get_flat(self):
@@ -469,18 +474,41 @@ class LayeredMlpNet:
                            skip=skip)
             a, lda = out, dout
 
+    @contextlib.contextmanager
+    def pin_input(self, x, n, ep_t=None):
+        """While open, the caller promises that rows x[:n] (and ep_t) do not change: the
+        tape's input -- [obs, t/limit] and its bf16 cast -- is built once for every
+        recording pass over them instead of once per pass (the VF fit's evaluations)."""
+        self._pinned = (x.data_ptr(), int(n), None if ep_t is None else ep_t.data_ptr())
+        self._pinned_input = None
+        try:
+            yield self
+        finally:
+            self._pinned = None
+            self._pinned_input = None
+
+    def _tape_input(self, x, n, ep_t, timestep_limit):
+        pin = self._pinned == (x.data_ptr(), int(n), None if ep_t is None else ep_t.data_ptr())
+        if pin and self._pinned_input is not None:
+            return self._pinned_input
+        X, ldx = self._input(x, n, ep_t, timestep_limit, name="tape_x")
+        if self.tape_bf16:
+            X, ldx = self._cast_rows(X, n, self.n_in, ldx, "tape_xb")
+        if pin:
+            self._pinned_input = (X, ldx)
+        return X, ldx
+
     def _record(self, x, n, ep_t, timestep_limit, theta):
         """Forward pass at theta kept as the tape the next vjp_flat / FVP uses."""
         key = self._key(theta, x, n, ep_t)
         if self.tape_bf16:
-            X, ldx = self._input(x, n, ep_t, timestep_limit, name="tape_x")
-            Xb, ldxb = self._cast_rows(X, n, self.n_in, ldx, "tape_xb")
+            Xb, ldxb = self._tape_input(x, n, ep_t, timestep_limit)
             H = [self._bf(f"tape_h{l}", n, d) for l, d in enumerate(self.hid_sizes)]
             Z = self.ws.get("tape_z", n * self.n_out, torch.float32)
             self._forward_b16(Xb, ldxb, n, theta, H, Z)
             self._tape = (key, Xb, ldxb, H, Z, theta)
             return self._tape
-        X, ldx = self._input(x, n, ep_t, timestep_limit, name="tape_x")
+        X, ldx = self._tape_input(x, n, ep_t, timestep_limit)
         H = [self.ws.get(f"tape_h{l}", n * d, torch.float32) for l, d in enumerate(self.hid_sizes)]
         Z = self.ws.get("tape_z", n * self.n_out, torch.float32)
         self._forward(X, ldx, n, theta, H, Z)
@@ -665,13 +693,15 @@ class LayeredMlpNet:
         inside its captured graph, so every replay sees the current policy)."""
         return self._pack_images(self.theta, "rwt", 1)
 
-    def forward_hidden_rows_b16(self, x, n, wt, bufs16, xb):
+    def forward_hidden_rows_b16(self, x, n, wt, bufs16, xb, cast=True):
         """forward_hidden_rows on the bf16 tape's kernels (bf16 tape mode): obs rows cast
-        to bf16 into xb, the hidden layers by mrl_gemm_bf16 into the bf16 row buffers
-        bufs16 (the values the f32 path rounds at staging); returns the last one."""
+        to bf16 into xb (cast=False: xb already holds them), the hidden layers by
+        mrl_gemm_bf16 into the bf16 row buffers bufs16 (the values the f32 path rounds at
+        staging); returns the last one."""
         L = len(self.dims) - 1
         ldx = self._ld8(self.n_in)
-        call("mrl_cast_rows_bf16", ptr(x), int(n), self.n_in, self.n_in, ptr(xb), ldx, stream())
+        if cast:
+            call("mrl_cast_rows_bf16", ptr(x), int(n), self.n_in, self.n_in, ptr(xb), ldx, stream())
         a, lda, out = xb, ldx, None
         for l in range(L - 1):
             din, dout = self.dims[l], self.dims[l + 1]

@@ -9,6 +9,7 @@ the host, while every loss+gradient evaluation is one fused forward pass
 (``mrl_mlp_rows`` VFLOSS) + one VJP (``mrl_mlp_vjp``) on the GPU, all-reduced over
 ranks in data-parallel mode.
 """
+import contextlib
 from collections import OrderedDict
 
 import numpy as np
@@ -104,9 +105,13 @@ class LbfgsOptimizer:
             l, _, _, g = evaluate(th.astype(np.float32), True)
             return l, g.astype("float64")
 
-        lb, mb, l2b, _ = evaluate(thprev.astype(np.float32), True)  # scipy's first point is thprev
-        theta, _, opt_info = scipy.optimize.fmin_l_bfgs_b(lossandgrad, thprev.astype(np.float64), maxiter=self.maxiter)
-        la, ma, l2a, _ = evaluate(theta.astype(np.float32), False)
+        x, ep_t, n = data[0], data[1], data[3]
+        pin = getattr(self.net, "pin_input", None)  # the fit's rows are fixed: build the tape input once
+        with (pin(x, n, ep_t) if pin is not None else contextlib.nullcontext()):
+            lb, mb, l2b, _ = evaluate(thprev.astype(np.float32), True)  # scipy's first point is thprev
+            theta, _, opt_info = scipy.optimize.fmin_l_bfgs_b(lossandgrad, thprev.astype(np.float64),
+                                                              maxiter=self.maxiter)
+            la, ma, l2a, _ = evaluate(theta.astype(np.float32), False)
         self.set_params_flat(theta)
         info = OrderedDict()
         for name, b, a in (("loss", lb, la), ("mse", mb, ma), ("l2", l2b, l2a)):

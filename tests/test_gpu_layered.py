@@ -227,3 +227,70 @@ def test_gemm_orientations_and_epilogues(M, N, K):
     got = slab.view(S, stride)[:, :(M + 1) * N].sum(0).view(M + 1, N).cpu().double()
     ref = torch.cat([A.double(), torch.ones(1, K, dtype=torch.float64)], 0) @ B.double()
     assert (got - ref).abs().max().item() < 1e-4 * max(ref.abs().max().item(), 1.0)
+
+
+@pytest.mark.parametrize("M,N,ldg,S", [(5000, 17, 34, 3), (1048576, 17, 34, 256), (777, 70, 70, 5), (40, 3, 3, 7)])
+def test_colsum_slabs_follow_their_summation_order(M, N, ldg, S):
+    """mrl_colsum (the bias / log-std gradient slabs) bit for bit against a float32
+    restatement of its order: per slab, wave w (of 4) keeps four accumulators over rows
+    r0 + w + 4q + 16j, a tail of rows into the first, then ((s0 + s1) + (s2 + s3)) per wave
+    and ((w0 + w1) + (w2 + w3)) per slab -- the batched loads must not change it."""
+    import ctypes
+
+    from modular_rl_amd._lib import call, stream
+    rng = np.random.default_rng(M)
+    G = rng.standard_normal((M, ldg)).astype(np.float32)
+    dG = torch.as_tensor(G).cuda()
+    st = (N + 63) // 64 * 64
+    slab = torch.full((S * st,), float("nan"), dtype=torch.float32, device="cuda")
+    call("mrl_colsum", ctypes.c_void_p(dG.data_ptr()), M, N, ldg, S, ctypes.c_void_p(slab.data_ptr()), st, None,
+         stream())
+    got = slab.cpu().numpy()
+    chunk = (M + S - 1) // S
+    for z in range(S):
+        r0, r1 = z * chunk, min(M, z * chunk + chunk)
+        waves = []
+        for w in range(4):
+            s = [np.zeros(N, np.float32) for _ in range(4)]
+            r = r0 + w
+            while r + 12 < r1:
+                for q in range(4):
+                    s[q] = s[q] + G[r + 4 * q, :N]
+                r += 16
+            while r < r1:
+                s[0] = s[0] + G[r, :N]
+                r += 4
+            waves.append((s[0] + s[1]) + (s[2] + s[3]))
+        want = (waves[0] + waves[1]) + (waves[2] + waves[3])
+        np.testing.assert_array_equal(got[z * st:z * st + N], want)
+
+
+@pytest.mark.parametrize("dtype,ep", [("fp32", True), ("bf16", True), ("bf16", False)])
+def test_vf_fit_with_pinned_rows_equals_unpinned(dtype, ep):
+    """LbfgsOptimizer.update pins the fit's rows (LayeredMlpNet.pin_input): the tape's
+    input ([obs, t/limit] and its bf16 cast) is built once for all evaluations. The
+    fitted theta and every stat equal the fit that rebuilds it per evaluation, bit for
+    bit; the pin is released after the fit (a later pass over other rows rebuilds)."""
+    from modular_rl_amd.nets import LayeredMlpNet
+    from modular_rl_amd import _lib
+    from modular_rl_amd.vf import LbfgsOptimizer
+    from modular_rl_amd.dist import Comm
+    N, nin, hid, limit = 3000, 41, [128, 128], 1000.0
+    rng = np.random.default_rng(4)
+    spec = T.Spec(nin, hid, 1, "linear")
+    th = (T.mlp_init(rng, spec.shapes, False) + 0.02 * rng.standard_normal(spec.P)).astype(np.float32)
+    obs = _dev(rng.standard_normal((N, nin - 1 if ep else nin)).astype(np.float32))
+    ept = _dev(rng.integers(0, 1000, size=N).astype(np.int32), torch.int32) if ep else None
+    y = _dev(rng.standard_normal(N).astype(np.float32))
+    outs = []
+    for pinned in (True, False):
+        net = LayeredMlpNet(nin, 1, _lib.HEAD_LINEAR, hid, dtype=dtype)
+        net.set_flat(th.astype(np.float64))
+        if not pinned:
+            net.pin_input = None
+        opt = LbfgsOptimizer(net, maxiter=4, comm=Comm())
+        info = opt.update((obs, ept, limit, N, y, N))
+        assert net._pinned is None and net._pinned_input is None
+        outs.append((net.get_flat(), info, opt.n_evals))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    assert outs[0][1] == outs[1][1] and outs[0][2] == outs[1][2] > 2
