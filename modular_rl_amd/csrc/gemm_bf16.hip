@@ -825,12 +825,7 @@ __device__ inline bf16x8 tr_operand(const bfr_t* img, int c0, int ks, int lane) 
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-// D: register stages in flight (the staging of stage t + 1 .. t + D overlaps the MFMAs of
-// stage t; D = 1 is the plain double buffer).  A block owns one slab of one tile and the
-// thin layers' grids are a few hundred blocks, so one stage in flight per block left
-// the kernel latency-bound (513 x 17 x 1 M: 0.59 ms, 1.8 TB/s); the k order is the same
-// for every D (bit-identical slabs).
-template <int BN, int D>
+template <int BN>
 __global__ __launch_bounds__(256) void gemm_bf16_tn_kernel(GemmTnArgs g) {
   constexpr int MI = BN == 128 ? 2 : 1, NI = MI;
   constexpr int NA = TBK * (QBM / 8) / 256, NB = TBK * (BN / 8) / 256 > 0 ? TBK * (BN / 8) / 256 : 1;
@@ -847,24 +842,24 @@ __global__ __launch_bounds__(256) void gemm_bf16_tn_kernel(GemmTnArgs g) {
   const int ac = threadIdx.x & 15, ar = threadIdx.x >> 4;
   const int bcw = BN / 8, bc = threadIdx.x % bcw, br = threadIdx.x / bcw;
   const bool b_active = threadIdx.x < TBK * bcw;
-  u32x4v ra[D][NA], rb[D][NB];  // slot d holds stage 1 + d (mod D)
-  auto load = [&](int d, int64_t t) {
+  u32x4v ra[NA], rb[NB];
+  auto load = [&](int64_t t) {
     const int64_t k0 = kbeg + t * TBK;
 #pragma unroll
     for (int i = 0; i < NA; ++i)
-      ra[d][i] = load_row_chunk(g.A, k0 + ar + 16 * i, kend, g.lda, m0 + 8 * ac, g.m_real, g.M, g.M > g.m_real);
+      ra[i] = load_row_chunk(g.A, k0 + ar + 16 * i, kend, g.lda, m0 + 8 * ac, g.m_real, g.M, g.M > g.m_real);
 #pragma unroll
     for (int i = 0; i < NB; ++i)
-      rb[d][i] = b_active ? load_row_chunk(g.B, k0 + br + (256 / bcw) * i, kend, g.ldb, n0 + 8 * bc, g.N, g.N, false)
-                          : u32x4v{0u, 0u, 0u, 0u};
+      rb[i] = b_active ? load_row_chunk(g.B, k0 + br + (256 / bcw) * i, kend, g.ldb, n0 + 8 * bc, g.N, g.N, false)
+                       : u32x4v{0u, 0u, 0u, 0u};
   };
-  auto store = [&](int d, bfr_t* st) {
+  auto store = [&](bfr_t* st) {
 #pragma unroll
-    for (int i = 0; i < NA; ++i) *reinterpret_cast<u32x4v*>(st + (ar + 16 * i) * TLD + 8 * ac) = ra[d][i];
+    for (int i = 0; i < NA; ++i) *reinterpret_cast<u32x4v*>(st + (ar + 16 * i) * TLD + 8 * ac) = ra[i];
     if (b_active)
 #pragma unroll
       for (int i = 0; i < NB; ++i)
-        *reinterpret_cast<u32x4v*>(st + TBK * TLD + (br + (256 / bcw) * i) * TLD + 8 * bc) = rb[d][i];
+        *reinterpret_cast<u32x4v*>(st + TBK * TLD + (br + (256 / bcw) * i) * TLD + 8 * bc) = rb[i];
   };
   f32x16 acc[MI][NI];
 #pragma unroll
@@ -872,38 +867,27 @@ __global__ __launch_bounds__(256) void gemm_bf16_tn_kernel(GemmTnArgs g) {
 #pragma unroll
     for (int b = 0; b < NI; ++b) acc[a][b] = zero16();
   if (nt > 0) {
-    load(0, 0);
-    store(0, smem);
-#pragma unroll
-    for (int d = 0; d < D; ++d)
-      if (1 + d < nt) load(d, 1 + d);
+    load(0);
+    store(smem);
   }
-  for (int64_t t0 = 0; t0 < nt; t0 += D) {
+  for (int64_t t = 0; t < nt; ++t) {
+    __syncthreads();
+    const bfr_t* As = smem + (t & 1) * STAGE;
+    const bfr_t* Bs = As + TBK * TLD;
+    if (t + 1 < nt) load(t + 1);
 #pragma unroll
-    for (int u = 0; u < D; ++u) {
-      const int64_t t = t0 + u;
-      if (t < nt) {
-        __syncthreads();
-        const bfr_t* As = smem + (t & 1) * STAGE;
-        const bfr_t* Bs = As + TBK * TLD;
+    for (int ks = 0; ks < TBK / 16; ++ks) {
+      bf16x8 av[MI], bv[NI];
 #pragma unroll
-        for (int ks = 0; ks < TBK / 16; ++ks) {
-          bf16x8 av[MI], bv[NI];
+      for (int mi = 0; mi < MI; ++mi) av[mi] = tr_operand(As, wm * 32 * MI + 32 * mi, ks, lane);
 #pragma unroll
-          for (int mi = 0; mi < MI; ++mi) av[mi] = tr_operand(As, wm * 32 * MI + 32 * mi, ks, lane);
+      for (int ni = 0; ni < NI; ++ni) bv[ni] = tr_operand(Bs, wn * 32 * NI + 32 * ni, ks, lane);
 #pragma unroll
-          for (int ni = 0; ni < NI; ++ni) bv[ni] = tr_operand(Bs, wn * 32 * NI + 32 * ni, ks, lane);
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-          for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA32B(av[mi], bv[ni], acc[mi][ni]);
-        }
-        if (t + 1 < nt) {
-          store(u, smem + ((t + 1) & 1) * STAGE);  // stage t + 1 sits in slot u
-          if (t + 1 + D < nt) load(u, t + 1 + D);
-        }
-      }
+        for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA32B(av[mi], bv[ni], acc[mi][ni]);
     }
+    if (t + 1 < nt) store(smem + ((t + 1) & 1) * STAGE);
   }
   float* C = g.slab + (int64_t)blockIdx.z * g.slab_stride;
 #pragma unroll
@@ -1349,17 +1333,9 @@ int mrl_gemm_bf16_tn(const mrl_gemm_bf16_tn_desc* d, const int32_t* skip, void* 
     }
   }
   const unsigned gm = (unsigned)((g.M + QBM - 1) / QBM);
-  // MRL_GEMM_TN_DEPTH (per call): register stages in flight, 4 (default) or 1
-  const char* de = getenv("MRL_GEMM_TN_DEPTH");
-  const bool deep = !(de && atoi(de) == 1);
-  const dim3 g32(1, gm, (unsigned)z), g128((unsigned)((g.N + 127) / 128), gm, (unsigned)z);
-  if (g.N <= 32) {
-    if (deep) hipLaunchKernelGGL((gemm_bf16_tn_kernel<32, 4>), g32, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((gemm_bf16_tn_kernel<32, 1>), g32, dim3(256), 0, s, g);
-  } else {
-    if (deep) hipLaunchKernelGGL((gemm_bf16_tn_kernel<128, 4>), g128, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((gemm_bf16_tn_kernel<128, 1>), g128, dim3(256), 0, s, g);
-  }
+  if (g.N <= 32) hipLaunchKernelGGL((gemm_bf16_tn_kernel<32>), dim3(1, gm, (unsigned)z), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((gemm_bf16_tn_kernel<128>), dim3((unsigned)((g.N + 127) / 128), gm, (unsigned)z), dim3(256), 0,
+                          s, g);
   return hip_check(hipGetLastError(), "mrl_gemm_bf16_tn");
 }
 

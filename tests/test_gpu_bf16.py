@@ -815,34 +815,3 @@ def test_bf16_lds_limited_gemms_equal_default(monkeypatch):
         # the rows above the ones-row: same per-slab k order in both kernels (the ones-row
         # differs in summation order between the 256 and 128 kernels, as tested above)
         assert torch.equal(outs[0][:, :din], outs[1][:, :din]), (R, din, dout)
-
-
-def test_bf16_tn_tiled_deep_staging_equals_double_buffer(monkeypatch):
-    """The tiled TN kernel with four register stages in flight (MRL_GEMM_TN_DEPTH default)
-    writes the same slabs, bit for bit, as the plain double buffer (depth 1): thin heads
-    (17 columns), the VF input layer (377 rows + the ones-row, lda 384), slabs shorter than
-    the stage ring (a few 32-row steps), ragged slab tails."""
-    import ctypes
-
-    from modular_rl_amd import _lib
-    from modular_rl_amd._lib import call, stream
-    rng = np.random.default_rng(31)
-    monkeypatch.setenv("MRL_GEMM_TN_BIG", "0")
-    for (R, din, dout, ones, splits) in [(1048576, 512, 17, True, 64), (33333, 377, 512, True, 64),
-                                         (100, 64, 17, True, 64), (5000, 300, 32, False, 7), (70001, 129, 200, True, 3)]:
-        lda, ldb = (din + 7) // 8 * 8, (dout + 7) // 8 * 8
-        dX, dG = _bf16_dev(rng.standard_normal((R, din)), lda), _bf16_dev(rng.standard_normal((R, dout)), ldb)
-        M = din + (1 if ones else 0)
-        S = int(_lib.load().mrl_gemm_slab_splits(R, splits))
-        outs = []
-        for depth in ("1", "4"):
-            monkeypatch.setenv("MRL_GEMM_TN_DEPTH", depth)
-            slab = torch.full((S * M * dout,), float("nan"), dtype=torch.float32, device="cuda")
-            g = _lib.GemmBf16TnDesc(m=M, n=dout, k=R, a=ctypes.c_void_p(dX.data_ptr()), lda=lda,
-                                    b=ctypes.c_void_p(dG.data_ptr()), ldb=ldb, ones_row=int(ones), splits=splits,
-                                    slab=ctypes.c_void_p(slab.data_ptr()), slab_stride=M * dout, ldc=dout)
-            call("mrl_gemm_bf16_tn", ctypes.byref(g), None, stream())
-            torch.cuda.synchronize()
-            outs.append(slab)
-        assert not torch.isnan(outs[1]).any(), (R, din, dout)
-        assert torch.equal(outs[0], outs[1]), (R, din, dout, (outs[0] != outs[1]).sum().item())
