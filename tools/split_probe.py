@@ -32,7 +32,8 @@ def rel(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
-for nin, nout, head in ((11, 3, _lib.HEAD_GAUSS), (4, 2, _lib.HEAD_SOFTMAX)):
+CASES = ((11, 3, _lib.HEAD_GAUSS), (4, 2, _lib.HEAD_SOFTMAX))
+for nin, nout, head in CASES[:int(os.environ.get("MRL_PROBE_NCASES", len(CASES)))]:  # 1: Hopper's net only
     rng = np.random.default_rng(0)
     net = MlpNet(nin, nout, head)
     net.set_flat(glorot_init(rng, nin, nout, head))
