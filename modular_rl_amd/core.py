@@ -245,14 +245,15 @@ class IterationRunner:
             cosched = pipeline and cosched_ok
             if cosched_ok and hasattr(vf_net, "lds_limit"):
                 # in BOTH orders (its kernels' choice must not depend on the order):
-                # MRL_COSCHED_LDS bytes of LDS per GEMM block, 0 = no limit
+                # MRL_COSCHED_LDS bytes of LDS per GEMM block, 0 = no limit (r04i: a 64 KB
+                # cap slowed the fit 15 ms and not the rollout's slowdown; off)
                 vf_net.lds_limit = int(os.environ.get("MRL_COSCHED_LDS", "0"))
             if cosched:
                 # Humanoid's wave-per-env step wants every CU (E / 4), so no disjoint split:
                 # the fit of iteration k shares the CUs with the rollout of k+1 (two plain
                 # streams; one wave per SIMD in the step kernel leaves issue slots free)
-                # MRL_COSCHED_PRIO (default 1; r04j +1 %): the rollout stream at high priority, so the
-                # dispatcher places its per-step blocks ahead of the fit's when both wait
+                # MRL_COSCHED_PRIO (default 1; r04j: +1 %, within box noise): the rollout
+                # stream at high priority, its per-step blocks dispatched ahead of the fit's
                 prio = -1 if os.environ.get("MRL_COSCHED_PRIO", "1") == "1" else 0
                 self.rollout_stream = torch.cuda.Stream(priority=prio)
                 self.fit_stream = torch.cuda.Stream()
