@@ -59,9 +59,11 @@ def _host(v):
     return v.detach().cpu().numpy().copy() if torch.is_tensor(v) else np.array(v, copy=True)
 
 
-def capture_state(agent, with_vf=True):
+def capture_state(agent, with_vf=True, host=True):
     """Device-side copies (stream-ordered, no host sync) of everything agent_state
-    saves; the pipelined runner takes one at the end of each iteration."""
+    saves; the pipelined runner takes one at the end of each iteration.  host=False:
+    only the state the next rollout advances (taken before that rollout is issued; the
+    rest, capture_host_state, after it)."""
     cap = {"policy/theta": agent.policy.net.theta.detach().clone()}
     if with_vf:
         cap["vf/theta"] = agent.baseline.net.theta.detach().clone()
@@ -70,6 +72,15 @@ def capture_state(agent, with_vf=True):
         cap["filter/state"] = col.filter_state[:col.FS].detach().clone()
         cap["rng/iteration"] = col.iteration.detach().clone()
         cap["rng/episodes"] = col.env_int[col.E:].detach().clone()
+    if host:
+        cap.update(capture_host_state(agent))
+    return cap
+
+
+def capture_host_state(agent):
+    """The part of capture_state no rollout touches: numpy's RNG and the updater's
+    own state arrays."""
+    cap = {}
     # numpy's global MT19937 (PpoSgd draws its minibatch permutations from it, as the
     # reference does): saved as arrays so a resumed run permutes identically
     name, keys, pos, has_gauss, gauss = np.random.get_state()

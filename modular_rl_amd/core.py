@@ -26,7 +26,7 @@ from . import _lib, timing
 from ._lib import call, ptr, stream
 from .collector import Batch, Collector
 from .dist import Comm
-from .checkpoint import capture_state
+from .checkpoint import capture_host_state, capture_state
 from .misc_utils import update_default_config
 from .vf import LbfgsOptimizer, NnRegression, NnVf  # noqa: F401  (reference names live in core)
 
@@ -368,9 +368,12 @@ class IterationRunner:
             ev["upd1"] = self._event()
             # pipelined: the VF of this iteration is fitted during the next step and added
             # to the capture then; in order it is final already
-            post["cap"] = capture_state(agent, with_vf=not self.pipeline)
+            post["cap"] = capture_state(agent, with_vf=not self.pipeline, host=False)
             if prelaunch_next:
                 self._prelaunched = self._launch_rollout()
+            # numpy's RNG and the updater's arrays: nothing the rollout touches, so taken
+            # under it (≈30 us of host time off the update-to-rollout seam)
+            post["cap"].update(capture_host_state(agent))
 
         upd = agent.updater
         upd.after_theta = after_theta
