@@ -165,3 +165,19 @@ def test_episode_counters_of_another_env_count_are_refused(tmp_path):
     load_snapshot(path, b)
     with pytest.raises(ValueError):
         apply_collector_state(_Col(16, 14, 0), b._pending_state)
+
+
+def test_capture_in_two_parts_equals_one():
+    """The runner captures the state the next rollout advances before issuing it
+    (capture_state(host=False)) and the host-only rest after (capture_host_state): the
+    two parts hold exactly the keys and values of one whole capture."""
+    from modular_rl_amd.checkpoint import capture_host_state, capture_state
+    a = _Agent(5)
+    whole = capture_state(a)
+    dev = capture_state(a, host=False)
+    host = capture_host_state(a)
+    assert not set(dev) & set(host) and set(dev) | set(host) == set(whole)
+    assert all(k.startswith(("policy/", "vf/", "filter/", "rng/iteration", "rng/episodes")) for k in dev)
+    for k, v in {**dev, **host}.items():
+        w = whole[k]
+        assert (torch.equal(v, w) if torch.is_tensor(v) else np.array_equal(v, w)), k
