@@ -8,12 +8,11 @@ OBJS := $(patsubst $(CSRC)/%.hip,build/%.o,$(SRCS))
 LIB := modular_rl_amd/libmrl_hip.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude
 
-all: $(LIB)
+# C restatement of the TRPO graph's batch means (test infrastructure: tests only)
+ORACLE_LIB := oracle/libmrl_oracle.so
 
-# mlp_split.hip: no SLP vectorisation -- the packed-f32 (v_pk_fma_f32) head sums it formed
-# gave run-to-run different results in a few 16-row groups per 4 M rows on gfx950
-# (tools/determinism_probe.py); the explicit packed builtins stay
-build/mlp_split.o: HIPFLAGS += -fno-slp-vectorize
+all: $(LIB) $(ORACLE_LIB)
+
 
 build/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p build
@@ -33,8 +32,6 @@ UBSAN_LIB := build/ubsan/libmrl_hip_ubsan.so
 
 ubsan: $(UBSAN_LIB)
 
-build/ubsan/mlp_split.o: HIPFLAGS += -fno-slp-vectorize
-
 build/ubsan/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p build/ubsan
 	$(HIPCC) $(HIPFLAGS) -O1 $(UBSAN_FLAGS) -c $< -o $@
@@ -43,7 +40,11 @@ $(UBSAN_LIB): $(UBSAN_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -shared-libsan -Xarch_host -fsanitize=undefined \
 	  -Wl,-rpath,$(CLANG_RT) -o $@ $(UBSAN_OBJS)
 
-clean:
-	rm -rf build $(LIB)
+oracle: $(ORACLE_LIB)
+$(ORACLE_LIB): oracle/mlp_c.c
+	gcc -O3 -mavx2 -ffp-contract=off -fopenmp -shared -fPIC -o $@ $<
 
-.PHONY: all clean ubsan
+clean:
+	rm -rf build $(LIB) $(ORACLE_LIB)
+
+.PHONY: all clean ubsan oracle

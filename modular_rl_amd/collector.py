@@ -93,6 +93,24 @@ class Batch:
         self.adv = self.ret = self.vpred = None
         self.vf_x = None  # (VF features, NnVf feature generation) set by NnVf.predict_batch
         self.episode = None
+        self.n_global = None  # rows over all ranks when the producer knows it (Collector)
+        self.rows_owner = self.rows_gen = None  # the collector whose buffers hold the rows
+
+    def rows_valid(self):
+        """False once the producing collector has launched another rollout into the same
+        buffers (the pipelined loop issues the next rollout before this batch's VF fit)."""
+        return self.rows_owner is None or self.rows_owner.rows_gen == self.rows_gen
+
+    def check_abort(self, comm):
+        """Raise before an update touches theta if this batch's persistent rollout gave up
+        (any rank).  TrpoUpdater reads the status inside its first readback instead."""
+        abort = getattr(self, "abort", None)
+        if abort is None:
+            return
+        a = abort.double().reshape(1).clone()
+        comm.allreduce_(a)
+        if float(a.item()) != 0:
+            raise _lib.MrlError("policy update on an aborted rollout: " + getattr(self, "abort_msg", ""))
 
     @staticmethod
     def from_paths(paths, stochpol, device, need_policy=True):
@@ -148,6 +166,10 @@ class Collector:
         self.comm = comm if comm is not None else Comm()
         self.E, self.T = int(n_envs), int(horizon)
         self.N = self.E * self.T
+        # rows over all ranks, once per collector: the updates and the VF fit scale by it
+        # without a host-synchronising all-reduce of a constant per call (core.py:123-124)
+        self.N_global = self.comm.allreduce_int(self.N) if self.comm.enabled else self.N
+        self.rows_gen = 0  # bumped by every launch: the batch rows it overwrites
         self.dev = torch.device(device)
         self.desc = _lib.RolloutDesc(env.kind, self.E, self.T, int(timestep_limit), int(filter),
                                      self.comm.rank * self.E, int(seed) & 0xFFFFFFFFFFFFFFFF,
@@ -287,6 +309,7 @@ class Collector:
         ``fill_noise=False``: the caller already issued fill_noise() in stream order."""
         if fill_noise:
             self.fill_noise()
+        self.rows_gen += 1
         self._fs_start = self.filter_state[:self.FS].clone() if self.comm.enabled else None
         # the persistent launch's residency check counts the CUs of the stream it runs on:
         # the stream of this call (a captured graph replays here, not on its capture stream)
@@ -338,6 +361,8 @@ class Collector:
             self.check()
             self._merge_filter_across_ranks(self._fs_start)
         b = Batch(self.N, self.obs, self.act, self.prob, self.rew, self.flags, self.ep_t, T=self.T, E=self.E)
+        b.n_global = self.N_global
+        b.rows_owner, b.rows_gen = self, self.rows_gen
         if not self.layered and self.persistent:
             b.abort, b.abort_msg = self.status, self.ABORT_MSG
         return b

@@ -615,8 +615,8 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_bf16_kernel(VjpArgsB a_in, con
   // bias sums: this half's rows, then the other half's (lanes l, l ^ 32 hold one unit)
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
-    const float s0 = gb0[m] + __shfl_xor(gb0[m], 32);
-    const float s1 = gb1[m] + __shfl_xor(gb1[m], 32);
+    const float s0 = xor32_add(gb0[m]);
+    const float s1 = xor32_add(gb1[m]);
     if (h == 0) {
       out[d.tb0 + 32 * m + j32] = s0;
       out[d.tb1 + 32 * m + j32] = s1;

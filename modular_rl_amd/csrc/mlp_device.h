@@ -215,10 +215,44 @@ __device__ inline void head_partial(const float* lds, const MlpDims& d, const f3
   }
 }
 
+// ---- cross-lane sums on VALU permutes only (v_permlane32/16_swap, DPP), never
+// ds_bpermute.  Round 5: a ds_bpermute whose data register a packed-f32 VALU op
+// (v_pk_add_f32 of SLP-vectorised head sums) had just written delivered stale values of
+// the wave's last 16 lanes, run to run (tools/det_locate.py); hipcc pads
+// packed-f32 -> VALU dependencies but not -> LDS ones.  The VALU permutes' hazards are
+// the compiler's to pad.  Each helper is bit-identical to the __shfl_xor form it
+// replaces (IEEE addition commutes).
+// x + x(lane ^ 32)
+__device__ inline float xor32_add(float x) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+// x + x(lane ^ 16)
+__device__ inline float xor16_add(float x) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+template <int CTRL>
+__device__ inline float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+// the xor butterfly over each 32-lane half, offsets 16, 8, 4, 2, 1 in that order: every
+// lane of the half ends with the half's sum.  Offset 8 is row_ror:8 (= lane ^ 8 in a
+// 16-lane row); offset 4 is row_ror:4, which reads lane ^ 4 or (lane ^ 4) ^ 8 -- equal
+// values once the ^8 stage has run; offsets 2 and 1 are quad_perm
+__device__ inline float half_sum(float x) {
+  x = xor16_add(x);
+  x += dpp_f<0x128>(x);  // row_ror:8
+  x += dpp_f<0x124>(x);  // row_ror:4
+  x += dpp_f<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
+  return x;
+}
+
 __device__ inline void head_finish(const float* lds, const MlpDims& d, float* z) {
 #pragma unroll
   for (int o = 0; o < MAX_OUT; ++o)
-    if (o < d.A) z[o] = (z[o] + __shfl_xor(z[o], 32)) + lds[d.hb + o];
+    if (o < d.A) z[o] = xor32_add(z[o]) + lds[d.hb + o];
 }
 
 // head partial from ONE 32-unit M-tile (mt) of a layer-2 activation
@@ -552,10 +586,7 @@ __device__ inline double wave_sum(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
-__device__ inline float wave_sumf(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+// the xor butterfly over the wave, offsets 32 .. 1 (every lane ends with the sum)
+__device__ inline float wave_sumf(float v) { return half_sum(xor32_add(v)); }
 
 }  // namespace mrl

@@ -563,16 +563,11 @@ __global__ __launch_bounds__(256, MRL_VJP_MINW) void mlp_vjp_kernel(VjpArgs a_in
   for (int m = 0; m < 2; ++m)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
-        pb0[m][r] += __shfl_xor(pb0[m][r], o);
-        pb1[m][r] += __shfl_xor(pb1[m][r], o);
-      }
+      pb0[m][r] = half_sum(pb0[m][r]);
+      pb1[m][r] = half_sum(pb1[m][r]);
     }
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) pG[r] += __shfl_xor(pG[r], o);
+  for (int r = 0; r < 4; ++r) pG[r] = half_sum(pG[r]);
   if (j == 0) {
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -928,18 +923,11 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        vg2[nt][o] += __shfl_xor(vg2[nt][o], 16);
-        vg2[nt][o] += __shfl_xor(vg2[nt][o], 32);
-      }
+      for (int o = 0; o < 4; ++o) vg2[nt][o] = xor32_add(xor16_add(vg2[nt][o]));
   }
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    pb1[nt] += __shfl_xor(pb1[nt], 16);
-    pb1[nt] += __shfl_xor(pb1[nt], 32);
-  }
-  pG += __shfl_xor(pG, 16);
-  pG += __shfl_xor(pG, 32);
+  for (int nt = 0; nt < 4; ++nt) pb1[nt] = xor32_add(xor16_add(pb1[nt]));
+  pG = xor32_add(xor16_add(pG));
 
   // ---- waves w and w + 4 of the block add their partials through sH (two rounds: gW1,
   // then the rest), waves 0..3 store one slab row each: the slab keeps mrl_slab_rows = 4

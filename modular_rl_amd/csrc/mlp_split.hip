@@ -85,8 +85,8 @@ __global__ void mlp_pack_split_kernel(MlpDims d, BDims b, const float* __restric
 // The exact three-way split of 8 values, two at a time: one v_cvt_pk_bf16_f32 per part
 // pair, the widening and the remainders on packed f32 (v_pk_add_f32) -- the same RNE
 // conversions and exact subtractions as the element-wise form, about 4.5 VALU per value
-// instead of 7 (the split is most of these kernels' VALU work).  Explicit vector types,
-// not the SLP vectoriser (which this file is built without, see the Makefile).
+// instead of 7 (the split is most of these kernels' VALU work).  Explicit vector types, so
+// the packing does not depend on the SLP vectoriser.
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ inline void split2(f32x2 v, bf16x2& a, bf16x2& c, bf16x2& e) {
   a = __builtin_convertvector(v, bf16x2);
@@ -137,11 +137,6 @@ __device__ inline void mfma_split(const float* img, int seg, int PS, int f, int 
 #ifndef MRL_SPLIT_NPROD
 #define MRL_SPLIT_NPROD 6
 #endif
-// diagnostic switch: explicit wait states after each MFMA chain, before the VALU reads of
-// its accumulator (tools/determinism_probe.py)
-#ifndef MRL_SPLIT_NOPS
-#define MRL_SPLIT_NOPS 0
-#endif
 // scheduling fences between the passes' phases (0: let the compiler interleave one
 // phase's VALU splits with the previous phase's MFMAs)
 #ifndef MRL_SPLIT_FENCES
@@ -154,11 +149,6 @@ __device__ inline void mfma_split(const float* img, int seg, int PS, int f, int 
 #define VJP_SPLIT_FENCE() ((void)0)
 #define FVP_SPLIT_FENCE() ((void)0)
 #endif
-__device__ inline void mfma_drain() {
-#if MRL_SPLIT_NOPS
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-#endif
-}
 
 template <int SH>
 __device__ inline void split_shape(RowsArgs& a, BDims& b) {
@@ -244,7 +234,6 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, (4 * MRL_SPLIT_FVP_OCC / SPLIT_RO
         mfma_split<MRL_SPLIT_NPROD>(imt, b.fa0, PS, 1 * b.KS0B + s0, lane, xs, dh[1]);
       }
     }
-    mfma_drain();
     mul_dtanh16(dh[0], h1[0]);
     mul_dtanh16(dh[1], h1[1]);
     // layer 1 tangent: da = (dh W1 + h1 dW1 + db1) (1 - h2^2); each input fragment is
@@ -275,8 +264,7 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, (4 * MRL_SPLIT_FVP_OCC / SPLIT_RO
       f32x16& da = da2[mo];
       f32x16 h2;
       cache_load(ct, lane, 2 + mo, h2);
-      mfma_drain();
-      mul_dtanh16(da, h2);
+        mul_dtanh16(da, h2);
       // the head on the f32 VALU: dz = da . W2 + h2 . dW2 (+ db2 in head_finish), z = h2 . W2
       if (need_z) head_partial_mt(img, dd, h2, mo, h, z);
       head_partial_mt(img, dd, da, mo, h, dz);
@@ -543,8 +531,8 @@ __global__ __launch_bounds__(256, 1) void mlp_vjp_split_kernel(VjpSplitArgs a_in
     }
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
-    const float s0 = gb0[m] + __shfl_xor(gb0[m], 32);
-    const float s1 = gb1[m] + __shfl_xor(gb1[m], 32);
+    const float s0 = xor32_add(gb0[m]);
+    const float s1 = xor32_add(gb1[m]);
     if (h == 0) {
       out[d.tb0 + 32 * m + j32] = s0;
       out[d.tb1 + 32 * m + j32] = s1;
@@ -752,8 +740,8 @@ float xv[16];
     }
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
-    const float s0 = gb0[m] + __shfl_xor(gb0[m], 32);
-    const float s1 = gb1[m] + __shfl_xor(gb1[m], 32);
+    const float s0 = xor32_add(gb0[m]);
+    const float s1 = xor32_add(gb1[m]);
     if (h == 0) {
       out[d.tb0 + 32 * m + j32] = s0;
       out[d.tb1 + 32 * m + j32] = s1;
@@ -1037,8 +1025,8 @@ float xv[16];
     }
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
-    const float s0 = gb0[m] + __shfl_xor(gb0[m], 32);
-    const float s1 = gb1[m] + __shfl_xor(gb1[m], 32);
+    const float s0 = xor32_add(gb0[m]);
+    const float s1 = xor32_add(gb1[m]);
     if (h == 0) {
       out[d.tb0 + 32 * m + j32] = s0;
       out[d.tb1 + 32 * m + j32] = s1;

@@ -101,7 +101,11 @@ def init_from_env(backend=None):
     every collective on (the RCCL path on one GPU)."""
     force = os.environ.get("MRL_COMM_FORCE", "0") == "1"
     if dist.is_initialized():
-        return Comm(force=force)
+        # initialised by the caller: still give the fit its host group (collective: every
+        # rank reaches this call), else Comm.host() would keep RCCL on the rollout's CUs
+        multi = dist.get_world_size() > 1 and dist.get_backend() == "nccl"
+        host = dist.new_group(backend="gloo") if multi else None
+        return Comm(force=force, host_group=host)
     if int(os.environ.get("WORLD_SIZE", "1")) <= 1 and not force:
         return Comm()
     if backend is None:

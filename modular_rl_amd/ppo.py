@@ -122,6 +122,8 @@ class PpoLbfgsUpdater(_PpoBase):
 
     def update(self, batch):
         cfg, net, comm = self.cfg, self.stochpol.net, self.comm
+        if hasattr(batch, "check_abort"):
+            batch.check_abort(comm)  # an aborted persistent rollout never reaches theta
         N = batch.n
         train_stop = int(0.75 * N) if cfg["do_split"] else N
         train = _Rows(batch, 0, train_stop)
@@ -209,6 +211,8 @@ class PpoSgdUpdater(_PpoBase):
 
     def update(self, batch):
         cfg, net, comm = self.cfg, self.stochpol.net, self.comm
+        if hasattr(batch, "check_abort"):
+            batch.check_abort(comm)  # an aborted persistent rollout never reaches theta
         N, bs = batch.n, self.BATCHSIZE
         # the old network = the parameters at the start of the update (update_old_net, ppo.py:171)
         oldprob = net.forward(batch.obs, N).reshape(N, -1)

@@ -227,7 +227,7 @@ class TrpoUpdater:
 
     def update(self, batch):
         cfg, ops, comm, net = self.cfg, self.ops, self.comm, self.stochpol.net
-        n_glob = comm.allreduce_int(batch.n)
+        n_glob = batch.n_global if getattr(batch, "n_global", None) else comm.allreduce_int(batch.n)
         ops.bind(batch, 1.0 / n_glob)
         thprev = net.theta.clone()
         g, sums = ops.surrgrad()

@@ -142,7 +142,7 @@ class NnRegression:
     def predict(self, x, n, ep_t=None, timestep_limit=1.0, out=None, feat_out=None):
         return self.net.forward(x, n, ep_t=ep_t, timestep_limit=timestep_limit, out=out, feat_out=feat_out)
 
-    def fit(self, x, n, ytarg, ep_t=None, timestep_limit=1.0, ypredold=None):
+    def fit(self, x, n, ytarg, ep_t=None, timestep_limit=1.0, ypredold=None, n_global=None):
         """ytarg: [n] device returns. ypredold: V_old predictions if already computed
         (compute_advantage evaluates the same net on the same rows, core.py:70)."""
         net = self.net
@@ -150,7 +150,7 @@ class NnRegression:
             ypredold = self.predict(x, n, ep_t, timestep_limit)
         target = net.ws.get("vf_target", n, torch.float32)
         call("mrl_vf_target", ptr(ytarg), ptr(ypredold), float(self.mixfrac), int(n), ptr(target), stream())
-        n_glob = self.comm.allreduce_int(n)
+        n_glob = n_global if n_global else self.comm.allreduce_int(n)
         out = self.opt.update((x, ep_t, timestep_limit, n, target, n_glob))
         yprednew = self.predict(x, n, ep_t, timestep_limit, out=net.ws.get("vf_pred_new", n, torch.float32))
         out["PredStdevBefore"] = self.moments.std(ypredold, None, n)
@@ -219,8 +219,14 @@ class NnVf:
         if cached is not None and cached[1] == self._feat_gen:
             X = cached[0]
         else:
+            # the features must come from this batch's own rows: once the next rollout is
+            # issued into the same buffers (the pipelined loop), they are another iteration's
+            if hasattr(batch, "rows_valid") and not batch.rows_valid():
+                raise _lib.MrlError("NnVf.fit_batch: the batch's VF features were replaced and its rows already "
+                               "hold the next rollout; predict_batch must be the last VF pass before the fit")
             X = self.features(batch.obs, batch.n, batch.ep_t)
-        return self.reg.fit(X, batch.n, batch.ret, None, 1.0, ypredold=batch.vpred)
+        return self.reg.fit(X, batch.n, batch.ret, None, 1.0, ypredold=batch.vpred,
+                            n_global=getattr(batch, "n_global", None))
 
     def fit(self, paths):
         from .core import Batch

@@ -360,13 +360,59 @@ def linesearch(f, x, fullstep, expected_improve_rate, max_backtracks=10, accept_
     return False, x, -1, ratios, fvals
 
 
-def trpo_update(spec, theta, ob, act, adv, oldprob, cg_damping=1e-3, max_kl=1e-2, dtype=np.float64):
+class RowChunks:
+    """The batch means of the TRPO graph (pg, Fvp, [surr, kl, ent]) evaluated over row
+    chunks on a thread pool (numpy's BLAS calls and large ufuncs release the GIL), so the
+    float64 oracle finishes at the benchmark's 4.19 M rows in seconds.  Every quantity
+    of `trpo.py:29-70` is a mean over rows plus a row-independent term (the DiagGauss
+    logstd parts), so the full-batch value is the chunk values weighted by n_c / N; the
+    float64 sums differ from the one-pass evaluation only in summation order."""
+
+    def __init__(self, ob, act, adv, oldprob, workers=16, chunk=1 << 18):
+        from concurrent.futures import ThreadPoolExecutor
+        self.n = ob.shape[0]
+        self.sl = [slice(lo, min(lo + chunk, self.n)) for lo in range(0, self.n, chunk)]
+        self.ob, self.act, self.adv, self.oldprob = ob, act, adv, oldprob
+        self.pool = ThreadPoolExecutor(max_workers=workers)
+
+    def _mean(self, fn):
+        parts = list(self.pool.map(lambda s: fn(s) * ((s.stop - s.start) / self.n), self.sl))
+        out = parts[0].astype(np.float64)
+        for p in parts[1:]:
+            out = out + p
+        return out
+
+    def pg(self, spec, theta, dtype=np.float64):
+        return self._mean(lambda s: policy_gradient(spec, theta, self.ob[s], self.act[s], self.adv[s], self.oldprob[s],
+                                                    dtype))
+
+    def fvp(self, spec, theta, v, dtype=np.float64):
+        return self._mean(lambda s: fisher_vector_product(spec, theta, v, self.ob[s], dtype))
+
+    def losses(self, spec, theta, dtype=np.float64):
+        return self._mean(lambda s: surr_kl_ent(spec, theta, self.ob[s], self.act[s], self.adv[s], self.oldprob[s],
+                                                dtype))
+
+
+def trpo_update(spec, theta, ob, act, adv, oldprob, cg_damping=1e-3, max_kl=1e-2, dtype=np.float64, rows=None):
     """TrpoUpdater.__call__ (`trpo.py:72-140`, HEAD diagnostics 82-84/97-100/131-132
-    and the duplicate beta Fvp at 111 dropped).  Returns (theta_new, stats, diag)."""
+    and the duplicate beta Fvp at 111 dropped).  Returns (theta_new, stats, diag).
+    rows: a RowChunks over the same batch evaluates the graph's means chunk-parallel."""
     cast = (lambda t: t.astype(dtype))
     thprev = cast(theta)
-    g = policy_gradient(spec, thprev, ob, act, adv, oldprob, dtype)
-    losses_before = surr_kl_ent(spec, thprev, ob, act, adv, oldprob, dtype)
+    if rows is not None:
+        def policy_gradient_(sp, th, _ob, _act, _adv, _oldprob, dt):
+            return rows.pg(sp, th, dt)
+
+        def surr_kl_ent_(sp, th, _ob, _act, _adv, _oldprob, dt):
+            return rows.losses(sp, th, dt)
+
+        def fisher_vector_product_(sp, th, v, _ob, dt):
+            return rows.fvp(sp, th, v, dt)
+    else:
+        policy_gradient_, surr_kl_ent_, fisher_vector_product_ = policy_gradient, surr_kl_ent, fisher_vector_product
+    g = policy_gradient_(spec, thprev, ob, act, adv, oldprob, dtype)
+    losses_before = surr_kl_ent_(spec, thprev, ob, act, adv, oldprob, dtype)
     diag = {"g": g}
     th = thprev
     if np.allclose(g, 0):
@@ -374,7 +420,7 @@ def trpo_update(spec, theta, ob, act, adv, oldprob, cg_damping=1e-3, max_kl=1e-2
     else:
         def fvp(p):
             # flat_tangent is a T.fvector (trpo.py:48): the tangent is downcast to floatX
-            return fisher_vector_product(spec, thprev, p.astype(dtype), ob, dtype).astype(np.float64) + cg_damping * p
+            return fisher_vector_product_(spec, thprev, p.astype(dtype), ob, dtype).astype(np.float64) + cg_damping * p
 
         stepdir, its, rdotr = cg(fvp, -g.astype(np.float64))
         shs = .5 * stepdir.dot(fvp(stepdir))
@@ -383,14 +429,14 @@ def trpo_update(spec, theta, ob, act, adv, oldprob, cg_damping=1e-3, max_kl=1e-2
         neggdotstepdir = -g.astype(np.float64).dot(stepdir)
 
         def loss(t):
-            return surr_kl_ent(spec, cast(t), ob, act, adv, oldprob, dtype)[0]
+            return surr_kl_ent_(spec, cast(t), ob, act, adv, oldprob, dtype)[0]
 
         success, theta_new, k, ratios, fvals = linesearch(loss, thprev.astype(np.float64), fullstep, neggdotstepdir / lm)
         th = cast(theta_new)  # SetFromFlat casts to floatX (core.py:540)
         diag.update(stepdir=stepdir, cg_iters=its, rdotr=rdotr, shs=shs, lm=lm, fullstep=fullstep,
                     neggdotstepdir=neggdotstepdir, success=success, k=k, ratios=np.array(ratios),
                     fvals=np.array(fvals), skipped=False)
-    losses_after = surr_kl_ent(spec, th, ob, act, adv, oldprob, dtype)
+    losses_after = surr_kl_ent_(spec, th, ob, act, adv, oldprob, dtype)
     stats = OrderedDict()
     for name, lb, la in zip(["surr", "kl", "ent"], losses_before, losses_after):
         stats[name + "_before"] = lb

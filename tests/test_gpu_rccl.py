@@ -93,14 +93,14 @@ def test_rccl_world1_forced_comm_is_bit_identical():
 
 
 # ------------------------------------------------------------------ abort path
-def _runner(pipeline):
-    from modular_rl_amd.agentzoo import TrpoAgent
+def _runner(pipeline, agent_cls="TrpoAgent"):
+    from modular_rl_amd import agentzoo
     from modular_rl_amd.core import IterationRunner
     from modular_rl_amd.envs import make
     env = make("Hopper-v2")
     cfg = dict(timestep_limit=1000, gamma=0.995, lam=0.97, max_kl=0.01, cg_damping=0.1, n_envs=4096, horizon=4,
                seed=3, use_graph=0)
-    agent = TrpoAgent(env.observation_space, env.action_space, cfg)
+    agent = getattr(agentzoo, agent_cls)(env.observation_space, env.action_space, cfg)
     col = agent.make_collector(env, cfg)
     return IterationRunner(agent, col, cfg, pipeline=pipeline), col
 
@@ -117,16 +117,18 @@ def test_rollout_on_too_few_cus_falls_back_to_step_launches():
     col.check()
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
-def test_persistent_abort_raises_in_the_iteration(pipeline):
+@pytest.mark.parametrize("pipeline,agent_cls", [(False, "TrpoAgent"), (True, "TrpoAgent"),
+                                                (False, "PpoLbfgsAgent"), (True, "PpoSgdAgent")])
+def test_persistent_abort_raises_in_the_iteration(pipeline, agent_cls):
     """64 persistent blocks forced onto 2 CUs (debug flag past the residency check):
     the resident blocks give up after their bounded polls, the rest exit on the abort
     word, and IterationRunner.step() raises MrlError instead of reporting the
-    iteration: the policy update reads the status back with its step scalars and raises
-    before it touches theta."""
+    iteration: the policy update reads the status back with its step scalars (TRPO) or
+    checks it first (Batch.check_abort, both PPO updaters) and raises before it touches
+    theta."""
     from modular_rl_amd import streams
     from modular_rl_amd._lib import MrlError
-    runner, col = _runner(pipeline=pipeline)
+    runner, col = _runner(pipeline=pipeline, agent_cls=agent_cls)
     col.force_persistent = True
     two = streams.masked_stream([0, 1])
     theta0 = runner.agent.policy.net.theta.clone()

@@ -109,8 +109,11 @@ def test_split_image_parts_sum_to_the_f32_weights(monkeypatch):
 
 def test_split_fisher_product_is_deterministic(monkeypatch):
     """The same split JVP-rows launch on the same 1 M rows gives the same bits every time
-    (an SLP-vectorised build of the kernel did not: a few 16-row groups per 4 M rows
-    differed run to run in one head column; Makefile builds mlp_split.hip without SLP)."""
+    (round 4's kernel did not: head_finish's ds_bpermute read packed-f32 head sums one
+    instruction after their v_pk_add_f32 and returned stale values of lanes 48-63, a few
+    16-row groups per 4 M rows; the cross-lane sums now use VALU permutes, DESIGN §3, and
+    tools/isa_hazard_check.py guards the built code; the 4.19 M-row check is
+    tests/test_gpu_fullsize.py)."""
     monkeypatch.setenv("MRL_FISHER", "split")
     from modular_rl_amd import _lib
     from modular_rl_amd.nets import MlpNet, glorot_init

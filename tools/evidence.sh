@@ -1,0 +1,55 @@
+# Round evidence on one MI355X, one parametrised recipe (replaces the per-round r0x_*.sh).
+# Usage (on the box): bash tools/evidence.sh TAG STEP [STEP ...]  -> gpurun_out/TAG_*
+#   tests        the whole GPU suite (pytest -m gpu)
+#   hopper       the default bench line (C3 Hopper-v2 fp32, the driver's command)
+#   prof         rocprofv3 --kernel-trace --stats of the default line + host gaps
+#   pmc          separate FETCH_SIZE / WRITE_SIZE passes of the default line -> TAG_pmc.json
+#   lines        C3 bf16, C2 bf16 / fp32, C5 bf16 / fp32 lines
+#   det          run-to-run determinism of the Fisher-product kernels (tools/det_locate.py)
+# Every GPU step has its own time limit; the first failure ends the script.
+set -o pipefail
+tag=${1:?tag}
+shift
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+bench() {  # name, timeout, bench args...
+  n=$1; t=$2; shift 2
+  timeout -k 10 $t python bench.py "$@" > gpurun_out/${tag}_bench_${n}.json 2> gpurun_out/${tag}_bench_${n}.err ||
+    { echo BENCH_FAILED $n; tail -5 gpurun_out/${tag}_bench_${n}.err; exit 1; }
+  python -c "import json;d=json.load(open('gpurun_out/${tag}_bench_${n}.json'));print('$n', d['value'], d.get('trpo_iters_per_sec'), d.get('phase_ms_per_iter'), d['roofline']['frac'])"
+}
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        > gpurun_out/${tag}_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/${tag}_tests.log; exit 1; }
+      tail -1 gpurun_out/${tag}_tests.log ;;
+    hopper) bench hopper 400 ;;
+    prof)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv \
+        -- python3 bench.py --steps 10 --warmup 1 --no-cpu-baseline > gpurun_out/${tag}_prof.log 2>&1 ||
+        { echo PROF_FAILED; tail -5 gpurun_out/${tag}_prof.log; exit 1; }
+      python tools/host_gap.py gpurun_out/${tag}_prof/run_kernel_trace.csv > gpurun_out/${tag}_host_gap.txt &&
+        tail -4 gpurun_out/${tag}_host_gap.txt ;;
+    pmc)
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${tag}_pmc_fetch -o run \
+        -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${tag}_pmc_f.log 2>&1 || exit 1
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${tag}_pmc_write -o run \
+        -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${tag}_pmc_w.log 2>&1 || exit 1
+      python tools/pmc_traffic.py gpurun_out/${tag}_pmc_fetch gpurun_out/${tag}_pmc_write \
+        --out gpurun_out/${tag}_pmc.json > /dev/null && echo PMC_OK ;;
+    lines)
+      bench hopper_bf16 400 --dtype bf16 --no-cpu-baseline
+      bench cartpole_bf16 400 --env CartPole-v0 --dtype bf16 --no-cpu-baseline
+      bench cartpole 400 --env CartPole-v0 --no-cpu-baseline
+      bench humanoid_bf16 500 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 10 --warmup 1 --dtype bf16 --no-cpu-baseline
+      bench humanoid 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    det)
+      REPS=8 timeout -k 10 200 python -u tools/det_locate.py > gpurun_out/${tag}_det.log 2>&1 ||
+        { tail -5 gpurun_out/${tag}_det.log; exit 1; }
+      grep -v amdgpu.ids gpurun_out/${tag}_det.log | head -4 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo EVIDENCE_OK $tag "$@"
