@@ -159,6 +159,30 @@ __device__ inline f32x2 tanh_fast2(f32x2 x) {
   return o;
 }
 
+// The exact three-way bf16 split of two f32 values (v = a + c + e exactly: RNE parts,
+// each remainder exact by Sterbenz, the last one has <= 8 significant bits): one
+// v_cvt_pk_bf16_f32 per part pair, the widening and the remainders on packed f32.  The
+// split-operand products (mlp_split.hip, the hybrid VJP) take f32 operands as these parts.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ inline void split2(f32x2 v, bf16x2& a, bf16x2& c, bf16x2& e) {
+  a = __builtin_convertvector(v, bf16x2);
+  const f32x2 r = v - __builtin_convertvector(a, f32x2);
+  c = __builtin_convertvector(r, bf16x2);
+  e = __builtin_convertvector(r - __builtin_convertvector(c, f32x2), bf16x2);
+}
+// the three parts of four values (one 16x16 f32 MFMA accumulator tile of a lane)
+__device__ inline void split4(const f32x4& v, bf16x4* p) {
+  bf16x2 a0, c0, e0, a1, c1, e1;
+  split2(f32x2{v[0], v[1]}, a0, c0, e0);
+  split2(f32x2{v[2], v[3]}, a1, c1, e1);
+  p[0] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3);
+  p[1] = __builtin_shufflevector(c0, c1, 0, 1, 2, 3);
+  p[2] = __builtin_shufflevector(e0, e1, 0, 1, 2, 3);
+}
+__device__ inline bf16x8 cat4(const bf16x4& lo, const bf16x4& hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 // tanh' from the activation, 1 - h^2, as one explicit fma (see tanh_fast)
 __device__ inline float dtanh(float h) { return fmaf(-h, h, 1.f); }
 #ifndef MRL_PK_DTANH  // 1: tile products with tanh' on packed f32 pairs

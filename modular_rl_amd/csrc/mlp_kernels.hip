@@ -653,7 +653,16 @@ __device__ inline int cache_off(int slot, int j, int w) {
 // VG2 (heads of A <= 4 outputs): gW2 += h2^T G on the VALU -- 48 fmas and 12 row
 // broadcasts per 16-row tile instead of 16 MFMAs, whose 16 output columns the head uses
 // only A of (MRL_VJP16_VG2=0 in the environment: the MFMA form)
-template <bool WIDE, bool EPT, bool VG2 = false>
+// HYB: the two 64x64x16 products of a tile -- gh1_T = ga2_R W1^T and gW1 += h1_T^T ga2_T,
+// 128 of its 168 f32 MFMAs -- on v_mfma_f32_16x16x32_bf16 with every f32 operand split
+// exactly into three bf16 parts (split2) and the six part products i + j <= 2 kept (each
+// dropped one <= 2^-25 |ab|, below one f32 ulp; mlp_split.hip header).  gh1: K = 64 units
+// in two k-steps of 32, k = 8 g + e <-> unit 16 (2 s + (e >> 2)) + 4 g + (e & 3), so the A
+// fragment is this lane's own ga2_R registers and W1^T comes from a split image built in
+// LDS at entry.  gW1: K = the tile's 16 rows, two part products stacked per MFMA (k < 4:
+// part P of rows 4 g + k, k >= 4: part Q), three MFMAs for the six products.  MFMA cycles
+// per 16-row tile 5,376 -> 2,816; the split costs 48 values of VALU per lane.
+template <bool WIDE, bool EPT, bool VG2 = false, bool HYB = false>
 __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs a, const float* __restrict__ img,
                                                                      const int32_t* __restrict__ skip) {
   constexpr int MT0 = WIDE ? 2 : 1;
@@ -661,6 +670,8 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
   // the compiler's wait for an LDS-DMA in flight is not put in front of fragment reads
   __shared__ __attribute__((aligned(16))) float lds[VJP16_W_FLOATS];
   __shared__ __attribute__((aligned(16))) float sH[VJP16_WAVES * 2 * VJP16_H1_FLOATS];
+  // HYB: B fragments of gh1 = ga2 W1^T, [k-step s][tile nt][part p][lane], 24 KB
+  __shared__ __attribute__((aligned(16))) bf16x8 wbs[HYB ? 2 * 4 * 3 * 64 : 1];
   if (skip != nullptr && *skip != 0) return;
   const MlpDims& d = a.d;
   // BA1 (W1 fragments, 4096 floats) then BA2 (W2 fragments, 512): contiguous in the image
@@ -685,6 +696,19 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
   // and R float4s (row c, units 16 p + 4 g .. + 3); the (slot, p, r) parts are constants
   const int offT = ((c >> 3) * 64 + 32 * ((c >> 2) & 1) + 4 * g) * 4 + (c & 3);
   const int offR = ((g >> 1) * 64 + 32 * (g & 1) + c) * 4;
+  if constexpr (HYB) {
+    // wave w builds (k-step s = w >> 2, tile nt = w & 3): lane (c, g) element e is
+    // W1[16 nt + c][16 (2 s + (e >> 2)) + 4 g + (e & 3)], i.e. w1frag(nt, 2 s + (e >> 2))
+    static_assert(VJP16_WAVES == 8, "one (s, nt) per wave");
+    const int s = wave >> 2, nt = wave & 3;
+    const float4 u = w1frag(nt, 2 * s), v = w1frag(nt, 2 * s + 1);
+    bf16x4 pu[3], pv[3];
+    split4(f32x4{u.x, u.y, u.z, u.w}, pu);
+    split4(f32x4{v.x, v.y, v.z, v.w}, pv);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) wbs[((s * 4 + nt) * 3 + p) * 64 + lane] = cat4(pu[p], pv[p]);
+    __syncthreads();
+  }
 
   f32x4 gW1[4][4], gW2[4], gW0[MT0][4];
   float vg2[4][4];  // VG2: [nt][o] of unit 16 nt + c, this lane group's rows
@@ -880,6 +904,52 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) read_h1(buf, nt);
+    if constexpr (HYB) {
+      // gW1 += h1_T^T ga2_T first (ga2_T's registers are free after it): K = 16 rows, two
+      // part products per MFMA
+      {
+        bf16x4 gp[4][3];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) split4(ga2T[nt], gp[nt]);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          bf16x4 hp[3];
+          split4(h1T[mt], hp);
+          const bf16x8 H21 = cat4(hp[2], hp[1]), H01 = cat4(hp[0], hp[1]), H00 = cat4(hp[0], hp[0]);
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            gW1[mt][nt] = MFMAB16(H21, cat4(gp[nt][0], gp[nt][1]), gW1[mt][nt]);  // h2 g0 + h1 g1
+            gW1[mt][nt] = MFMAB16(H01, cat4(gp[nt][2], gp[nt][0]), gW1[mt][nt]);  // h0 g2 + h1 g0
+            gW1[mt][nt] = MFMAB16(H00, cat4(gp[nt][1], gp[nt][0]), gW1[mt][nt]);  // h0 g1 + h0 g0
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // the next tile's G / h2 / x / h1 loads, under the gh1 chain
+      load_g_h2(tn);
+      load_x(tn);
+      dma_h1(tn, buf ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+      // gh1_T = ga2_R W1^T: two k-steps of 32 units, six part products each (smallest first)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x4 pa[3], pb[3];
+        split4(ga2R[2 * s], pa);
+        split4(ga2R[2 * s + 1], pb);
+        const bf16x8 A0 = cat4(pa[0], pb[0]), A1 = cat4(pa[1], pb[1]), A2 = cat4(pa[2], pb[2]);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const bf16x8* w = wbs + (s * 4 + nt) * 3 * 64 + lane;
+          const bf16x8 B0 = w[0], B1 = w[64], B2 = w[128];
+          g1T[nt] = MFMAB16(A2, B0, g1T[nt]);
+          g1T[nt] = MFMAB16(A0, B2, g1T[nt]);
+          g1T[nt] = MFMAB16(A1, B1, g1T[nt]);
+          g1T[nt] = MFMAB16(A1, B0, g1T[nt]);
+          g1T[nt] = MFMAB16(A0, B1, g1T[nt]);
+          g1T[nt] = MFMAB16(A0, B0, g1T[nt]);
+        }
+      }
+    } else {
     // 16 steps (mt, nt), each W1 fragment read from LDS one step ahead of its MFMAs
     float4 wf = w1frag(0, 0);
 #pragma unroll
@@ -901,6 +971,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
         dma_h1(tn, buf ^ 1);
         __builtin_amdgcn_sched_barrier(0);
       }
+    }
     }
     // ---- ga1 = gh1 (1 - h1^2) in T;  gW0 += x^T ga1
 #pragma unroll
@@ -1383,8 +1454,8 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
     } else if (vg2) {
       hipLaunchKernelGGL((mlp_vjp16_kernel<false, false, true>), grid, blk16, shm16, s, a, image, skip);
     } else {
-      if (ept) hipLaunchKernelGGL((mlp_vjp16_kernel<false, true>), grid, blk16, shm16, s, a, image, skip);
-      else hipLaunchKernelGGL((mlp_vjp16_kernel<false, false>), grid, blk16, shm16, s, a, image, skip);
+      if (ept) hipLaunchKernelGGL((mlp_vjp16_kernel<false, true, false, true>), grid, blk16, shm16, s, a, image, skip);
+      else hipLaunchKernelGGL((mlp_vjp16_kernel<false, false, false, true>), grid, blk16, shm16, s, a, image, skip);
     }
     return hip_check(hipGetLastError(), "mrl_mlp_vjp");
   }

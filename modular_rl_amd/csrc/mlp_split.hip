@@ -87,13 +87,7 @@ __global__ void mlp_pack_split_kernel(MlpDims d, BDims b, const float* __restric
 // conversions and exact subtractions as the element-wise form, about 4.5 VALU per value
 // instead of 7 (the split is most of these kernels' VALU work).  Explicit vector types, so
 // the packing does not depend on the SLP vectoriser.
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-__device__ inline void split2(f32x2 v, bf16x2& a, bf16x2& c, bf16x2& e) {
-  a = __builtin_convertvector(v, bf16x2);
-  const f32x2 r = v - __builtin_convertvector(a, f32x2);
-  c = __builtin_convertvector(r, bf16x2);
-  e = __builtin_convertvector(r - __builtin_convertvector(c, f32x2), bf16x2);
-}
+// (split2: mlp_device.h)
 __device__ inline void split8v(const float* v, bf16x8* out) {
 #pragma unroll
   for (int j = 0; j < 8; j += 2) {

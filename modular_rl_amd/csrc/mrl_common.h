@@ -20,6 +20,10 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 // rate): lane l supplies A[i = l&31][k = 8(l>>5) + j] and B[k = 8(l>>5) + j][col l&31]
 // in element j; the C/D layout is the f32 form's (cperm below).
 #define MFMA32B(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+// v_mfma_f32_16x16x32_bf16 (16 cycles/SIMD): lane l supplies A[i = l&15][k = 8(l>>4) + j]
+// and B[k = 8(l>>4) + j][col l&15]; D[i][j] in lane j (+16 per row group), register r holds
+// row i = 4(l>>4) + r (the 16x16x4 f32 form's layout)
+#define MFMAB16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
 namespace mrl {
 
