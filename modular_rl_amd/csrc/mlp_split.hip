@@ -204,26 +204,47 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, (4 * MRL_SPLIT_FVP_OCC / SPLIT_RO
   const bool need_z = a.head != MRL_HEAD_GAUSS;  // the DiagGauss metric does not use the mean
   double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
   const int64_t ntiles = (a.n + 31) / 32;
-  for (int64_t tile = (int64_t)blockIdx.x * SPLIT_ROWS_WAVES + wave; tile < ntiles;
-       tile += (int64_t)gridDim.x * SPLIT_ROWS_WAVES) {
+  const int64_t stride = (int64_t)gridDim.x * SPLIT_ROWS_WAVES;
+  // Software pipeline (SQ, round 4: 0.39 of the wave time parked on s_waitcnt): a tile's
+  // inputs x and h1 are loaded during the previous tile; at a tile's start its h2 loads
+  // are issued first, then the next tile's x / h1 (vmcnt retires in order, so the wait
+  // for h2 before the head leaves the prefetch in flight)
+  int64_t tile = (int64_t)blockIdx.x * SPLIT_ROWS_WAVES + wave;
+  float xv[MAX_KS0B][8];
+  f32x16 h1[2];
+  auto load_xh1 = [&](int64_t t, float (&x)[MAX_KS0B][8], f32x16* hh) {
+    const int64_t r = t * 32 + (lane & 31);
+    XGlobalNB xl{a.x, a.ept, a.ts_limit, a.n_obs, r, r < a.n};
+#pragma unroll
+    for (int s0 = 0; s0 < MAX_KS0B; ++s0)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[s0][j] = s0 < b.KS0B ? xl(16 * s0 + 8 * h + j) : 0.f;
+    cache_load(a.cache + t * CACHE_TILE_FLOATS, lane, 0, hh[0]);
+    cache_load(a.cache + t * CACHE_TILE_FLOATS, lane, 1, hh[1]);
+  };
+  if (tile < ntiles) load_xh1(tile, xv, h1);
+  for (; tile < ntiles; tile += stride) {
     const int64_t row = tile * 32 + (lane & 31);
     const bool valid = row < a.n;
-    XGlobalNB xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
     const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
-    f32x16 h1[2], dh[2];
-    cache_load(ct, lane, 0, h1[0]);
-    cache_load(ct, lane, 1, h1[1]);
+    f32x16 h2[2];
+    cache_load(ct, lane, 2, h2[0]);
+    cache_load(ct, lane, 3, h2[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    const int64_t tn = tile + stride < ntiles ? tile + stride : tile;  // the last tile re-reads itself
+    float xn[MAX_KS0B][8];
+    f32x16 h1n[2];
+    load_xh1(tn, xn, h1n);
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16 dh[2];
     // layer 0 tangent: dh = (x dW0 + db0) (1 - h1^2)
     dh[0] = load_bias16(imt, b.fb0, 0, h);
     dh[1] = load_bias16(imt, b.fb0, 1, h);
 #pragma unroll
     for (int s0 = 0; s0 < MAX_KS0B; ++s0) {
       if (s0 < b.KS0B) {
-        float xv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xv[j] = xl(16 * s0 + 8 * h + j);
         bf16x8 xs[3];
-        split8v(xv, xs);
+        split8v(xv[s0], xs);
         mfma_split<MRL_SPLIT_NPROD>(imt, b.fa0, PS, 0 * b.KS0B + s0, lane, xs, dh[0]);
         mfma_split<MRL_SPLIT_NPROD>(imt, b.fa0, PS, 1 * b.KS0B + s0, lane, xs, dh[1]);
       }
@@ -256,21 +277,24 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, (4 * MRL_SPLIT_FVP_OCC / SPLIT_RO
 #pragma unroll
     for (int mo = 0; mo < 2; ++mo) {
       f32x16& da = da2[mo];
-      f32x16 h2;
-      cache_load(ct, lane, 2 + mo, h2);
-        mul_dtanh16(da, h2);
+      mul_dtanh16(da, h2[mo]);
       // the head on the f32 VALU: dz = da . W2 + h2 . dW2 (+ db2 in head_finish), z = h2 . W2
-      if (need_z) head_partial_mt(img, dd, h2, mo, h, z);
+      if (need_z) head_partial_mt(img, dd, h2[mo], mo, h, z);
       head_partial_mt(img, dd, da, mo, h, dz);
-      head_partial_mt(imt, dd, h2, mo, h, dzt);
+      head_partial_mt(imt, dd, h2[mo], mo, h, dzt);
       FVP_SPLIT_FENCE();
     }
     if (need_z) head_finish(img, dd, z);
 #pragma unroll
     for (int o = 0; o < MAX_OUT; ++o) dz[o] += dzt[o];
     head_finish(imt, dd, dz);
-    if (!valid || h != 0) continue;
-    row_epilogue<MRL_EPI_FVP, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+    if (valid && h == 0) row_epilogue<MRL_EPI_FVP, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+#pragma unroll
+    for (int s0 = 0; s0 < MAX_KS0B; ++s0)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[s0][j] = xn[s0][j];
+    h1[0] = h1n[0];
+    h1[1] = h1n[1];
   }
   (void)acc0;
   (void)acc1;

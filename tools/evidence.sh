@@ -5,6 +5,7 @@
 #   prof         rocprofv3 --kernel-trace --stats of the default line + host gaps
 #   pmc          separate FETCH_SIZE / WRITE_SIZE passes of the default line -> TAG_pmc.json
 #   lines        C3 bf16, C2 bf16 / fp32, C5 bf16 / fp32 lines
+#   sq           SQ wave-time split of the Fisher-product kernels (tools/sq_split.py)
 #   det          run-to-run determinism of the Fisher-product kernels (tools/det_locate.py)
 # Every GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
@@ -45,6 +46,13 @@ for step in "$@"; do
       bench cartpole 400 --env CartPole-v0 --no-cpu-baseline
       bench humanoid_bf16 500 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 10 --warmup 1 --dtype bf16 --no-cpu-baseline
       bench humanoid 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    sq)  # SQ wave-time split of the Fisher-product kernels (one 8-counter pass of the probe)
+      timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+        SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_BUSY_CYCLES --output-format csv \
+        -d gpurun_out/${tag}_sq -o run -- python3 tools/split_probe.py > gpurun_out/${tag}_sq.log 2>&1 ||
+        { echo SQ_FAILED; tail -5 gpurun_out/${tag}_sq.log; exit 1; }
+      python tools/sq_split.py gpurun_out/${tag}_sq mlp_fvp_split_kernel mlp_vjp16_kernel \
+        > gpurun_out/${tag}_sq.txt && cat gpurun_out/${tag}_sq.txt ;;
     det)
       REPS=8 timeout -k 10 200 python -u tools/det_locate.py > gpurun_out/${tag}_det.log 2>&1 ||
         { tail -5 gpurun_out/${tag}_det.log; exit 1; }
