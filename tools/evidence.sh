@@ -6,6 +6,8 @@
 #   pmc          separate FETCH_SIZE / WRITE_SIZE passes of the default line -> TAG_pmc.json
 #   lines        C3 bf16, C2 bf16 / fp32, C5 bf16 / fp32 lines
 #   sq           SQ wave-time split of the Fisher-product kernels (tools/sq_split.py)
+#   issue        SQ issue floor of the persistent rollout per bench line (tools/rollout_issue.py)
+#   stamps       per-phase stamps of the persistent Hopper rollout (tools/persistent_stamps.py)
 #   det          run-to-run determinism of the Fisher-product kernels (tools/det_locate.py)
 # Every GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
@@ -53,6 +55,19 @@ for step in "$@"; do
         { echo SQ_FAILED; tail -5 gpurun_out/${tag}_sq.log; exit 1; }
       python tools/sq_split.py gpurun_out/${tag}_sq mlp_fvp_split_kernel mlp_vjp16_kernel \
         > gpurun_out/${tag}_sq.txt && cat gpurun_out/${tag}_sq.txt ;;
+    issue)  # the persistent rollout's SQ issue floor per step -> profiles-style TAG_rollout_issue.json
+      for line in "Hopper-v2 fp32" "Hopper-v2 bf16" "CartPole-v0 bf16" "CartPole-v0 fp32"; do
+        set -- $line
+        timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY \
+          SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d gpurun_out/${tag}_issue_$1_$2 -o run \
+          -- python3 bench.py --env $1 --dtype $2 --steps 2 --warmup 1 --no-cpu-baseline \
+          > gpurun_out/${tag}_issue_$1_$2.log 2>&1 || { echo ISSUE_FAILED $1 $2; tail -5 gpurun_out/${tag}_issue_$1_$2.log; exit 1; }
+        python tools/rollout_issue.py gpurun_out/${tag}_issue_$1_$2 $1/$2 1024 --out gpurun_out/${tag}_rollout_issue.json
+      done ;;
+    stamps)
+      timeout -k 10 300 python -u tools/persistent_stamps.py Hopper-v2 > gpurun_out/${tag}_stamps.txt 2>&1 ||
+        { tail -5 gpurun_out/${tag}_stamps.txt; exit 1; }
+      grep -v amdgpu.ids gpurun_out/${tag}_stamps.txt | tail -20 ;;
     det)
       REPS=8 timeout -k 10 200 python -u tools/det_locate.py > gpurun_out/${tag}_det.log 2>&1 ||
         { tail -5 gpurun_out/${tag}_det.log; exit 1; }
