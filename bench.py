@@ -47,8 +47,8 @@ def flops_per_row(net):
     fwd = 2 * sum(mm)
     if getattr(net, "layered", False) or getattr(net, "use_cache", False):
         # the primal forward comes from the activation cache / recorded tape
-        return {"fvp_jvp_rows": jvp, "fvp_vjp": vjp, "fvp_fused": jvp + vjp, "policy_forward": fwd}
-    return {"fvp_jvp_rows": fwd + jvp, "fvp_vjp": vjp, "fvp_fused": fwd + jvp + vjp, "policy_forward": fwd}
+        return {"fvp_jvp_rows": jvp, "fvp_vjp": vjp, "policy_forward": fwd}
+    return {"fvp_jvp_rows": fwd + jvp, "fvp_vjp": vjp, "policy_forward": fwd}
 
 
 def vjp_binary_entry(kern, policy_vjp_flop, vf_vjp_flop, rows, iters):
@@ -258,11 +258,8 @@ def fisher_arith(net):
         return "as the MLP dtype"
     jvp = "split-operand bf16 MFMA (fp32 operands split exactly into 3 bf16 parts, f32 accumulate)" \
         if getattr(net, "fisher_split", False) else "exact f32 MFMA"
-    split = getattr(net, "fisher_split", False)
-    if split and os.environ.get("MRL_FISHER_FUSED", "0") != "0":
-        return {"pass": "one kernel per product (mlp_fisher_split_kernel: JVP, KL metric and VJP per 32-row tile, "
-                        "the activation cache read once)", "jvp_rows": jvp, "vjp": jvp}
-    vjp = "split-operand bf16 MFMA" if split and os.environ.get("MRL_VJP_SPLIT", "0") != "0" else "exact f32 MFMA"
+    vjp = ("hybrid: the two 64x64 products of each 16-row tile (gh1, gW1) on split-operand bf16 MFMA, "
+           "the rest exact f32 MFMA (mlp_vjp16_kernel<HYB>)")
     return {"pass": "two kernels per product (JVP + metric rows, then the VJP)", "jvp_rows": jvp, "vjp": vjp}
 
 
@@ -275,7 +272,7 @@ def policy_gemm_roofline(kern, kinfo, net, dtype, n_rows, K, pmc, gemm_pmc):
     dense MFMA peak, and the PMC traffic / algorithmic bytes ratio where a pass measured it."""
     peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_FP32_TFLOPS
     if not net.layered:
-        cands = {k: v for k, v in kinfo.items() if k in ("fvp_fused", "fvp_jvp_rows") + tuple(VJP_BINARY.values())}
+        cands = {k: v for k, v in kinfo.items() if k in ("fvp_jvp_rows",) + tuple(VJP_BINARY.values())}
         if not cands:
             return None
         name = max(cands, key=lambda k: cands[k]["total_ms"])
@@ -287,8 +284,9 @@ def policy_gemm_roofline(kern, kinfo, net, dtype, n_rows, K, pmc, gemm_pmc):
                 "frac": round(ki["tflops"] / peak, 4), "traffic": traffic,
                 "traffic_over_algorithmic": round(traffic / alg, 3) if traffic and alg else None,
                 "algorithmic_bytes": alg or None,
-                "kernel": {"fvp_jvp_rows": "mlp_rows_kernel (JVP + KL metric)",
-                           "fvp_fused": "mlp_fisher_split_kernel (JVP + KL metric + VJP)"}.get(name, name),
+                "kernel": {"fvp_jvp_rows": ("mlp_fvp_split_kernel (JVP + KL metric)"
+                                            if getattr(net, "fisher_split", False)
+                                            else "mlp_rows_kernel (JVP + KL metric)")}.get(name, name),
                 "flop_per_row": ki["flop_per_row"], "rows_per_launch": ki["rows_per_launch"],
                 "mean_launch_ms": round(ki["mean_ms"], 5), "launches_timed": ki["launches"],
                 "ms_per_iter": round(ki["total_ms"] / K, 3),
@@ -409,7 +407,6 @@ def main():
     # activation cache (h1 + h2: 512 B fp32, 256 B bf16), the obs row, the head rows
     cache_b = 0 if net.layered else (256 if args.dtype == "bf16" else 512)
     row_b = cache_b + 4 * net.n_in + 4 * net.gh
-    fused_b = cache_b + 4 * net.n_in  # one pass: the cache and the obs row; the head rows stay in registers
     pmc = {}
     pmc_path = os.path.join(ROOT, "profiles", PMC_FILE)  # measured on the default Hopper config
     if (os.path.exists(pmc_path) and args.env == "Hopper-v2" and not agent.policy.net.layered and E == 4096
@@ -419,15 +416,14 @@ def main():
         if "fvp_jvp_rows" not in pmc and "fvp_jvp_rows_split" in pmc:  # the JVP half's kernel this round
             pmc["fvp_jvp_rows"] = pmc["fvp_jvp_rows_split"]
     kinfo = {}
-    for name in ("fvp_fused", "fvp_jvp_rows", "fvp_vjp"):
+    for name in ("fvp_jvp_rows", "fvp_vjp"):
         if name in kern:
             cnt, mean_ms, tot_ms = kern[name]
             kinfo[name] = dict(launches=cnt, mean_ms=mean_ms, total_ms=tot_ms, rows_per_launch=n_local,
                                flop_per_row=fpr[name])
             if not net.layered:
-                rb = fused_b if name == "fvp_fused" else row_b
-                kinfo[name]["bytes_per_row"] = rb
-                kinfo[name]["hbm_gbs_alg"] = rb * n_local / (mean_ms * 1e-3) / 1e9
+                kinfo[name]["bytes_per_row"] = row_b
+                kinfo[name]["hbm_gbs_alg"] = row_b * n_local / (mean_ms * 1e-3) / 1e9
     if not net.layered:
         # the same kernel binary (the cached VJP) also serves the policy gradient and every
         # VF L-BFGS evaluation (the VF fit's launches run beside the next rollout on the

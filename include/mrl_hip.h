@@ -156,29 +156,17 @@ int mrl_mlp_vjp_bf16(const mrl_mlp_desc* d, const float* image, const float* x, 
                      const float* ghead, int64_t n, float* slab, const float* act_cache, const int32_t* skip,
                      void* stream);
 
-/* fp32-accurate Fisher-vector product on bf16 MFMA (csrc/mlp_split.hip): every f32 MFMA
- * operand split exactly into three bf16 parts, the part products accumulated in f32
- * (6 of the 9, the dropped three <= 2^-25 of the product: below one f32 ulp).  Same
- * semantics as mrl_mlp_rows(MRL_EPI_FVP) with MRL_CACHE_READ (the f32 activation cache
- * of a preceding f32 SURRGRAD / LOSSES pass) -- trpo.py:45-58, 70 -- and as
- * mrl_mlp_vjp with a cache; the images are split images (mrl_mlp_pack_split;
- * fwd_only for the tangent), the partial / slab buffers sized as the f32 ones. */
+/* The fp32-accurate Fisher product's JVP half on bf16 MFMA (csrc/mlp_split.hip): every
+ * f32 MFMA operand split exactly into three bf16 parts, the part products accumulated in
+ * f32 (6 of the 9, the dropped three <= 2^-25 of the product: below one f32 ulp).  Same
+ * semantics as mrl_mlp_rows(MRL_EPI_FVP) with MRL_CACHE_READ (the f32 activation cache of
+ * a preceding f32 SURRGRAD / LOSSES pass) -- trpo.py:45-58, 70; the images are split
+ * images of the forward weights (mrl_mlp_pack_split, for theta and for the tangent).  The
+ * VJP half is mrl_mlp_vjp with the cache. */
 int64_t mrl_mlp_image_words_split(const mrl_mlp_desc* d);
-int mrl_mlp_pack_split(const mrl_mlp_desc* d, const float* theta, float* image, int32_t fwd_only,
-                       const int32_t* skip, void* stream);
+int mrl_mlp_pack_split(const mrl_mlp_desc* d, const float* theta, float* image, const int32_t* skip, void* stream);
 int mrl_mlp_fvp_split(const mrl_mlp_desc* d, const float* theta, const float* image, const float* tangent,
                       const float* image_t, const mrl_rows_io* io, const int32_t* skip, void* stream);
-/* the VJP (slab rows as mrl_mlp_vjp: mrl_mlp_slab_rows(d, n)) from the f32 cache */
-int mrl_mlp_vjp_split(const mrl_mlp_desc* d, const float* image, const float* x, const float* ghead, int64_t n,
-                      float* slab, const float* act_cache, const int32_t* skip, void* stream);
-/* the whole Fisher product in one pass (JVP -> KL metric -> VJP per 32-row tile, the
- * cache read once, the head rows kept in registers; replaces the pair above and the
- * reference's Fvp, trpo.py:45-58): slab rows as mrl_mlp_vjp (mrl_mlp_slab_rows(d, n)),
- * bit-identical to mrl_mlp_fvp_split + mrl_mlp_vjp_split form 2; io->ghead optional
- * (the head rows, written as mrl_mlp_fvp_split writes them) */
-int mrl_mlp_fisher_split(const mrl_mlp_desc* d, const float* theta, const float* image, const float* tangent,
-                         const float* image_t, const mrl_rows_io* io, float* slab, const int32_t* skip,
-                         void* stream);
 
 int mrl_reduce_rows_f32(const float* slab, int64_t rows, int64_t cols, float* out, const int32_t* skip, void* stream);
 int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* out, const int32_t* skip, void* stream);

@@ -97,10 +97,8 @@ SIGNATURES = {
     "mrl_mlp_rows_bf16": (i32, [vp, i32, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_mlp_vjp_bf16": (i32, [vp, vp, vp, vp, f64, vp, i64, vp, vp, vp, vp]),
     "mrl_mlp_image_words_split": (i64, [vp]),
-    "mrl_mlp_pack_split": (i32, [vp, vp, vp, i32, vp, vp]),
+    "mrl_mlp_pack_split": (i32, [vp, vp, vp, vp, vp]),
     "mrl_mlp_fvp_split": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
-    "mrl_mlp_vjp_split": (i32, [vp, vp, vp, vp, i64, vp, vp, vp, vp]),
-    "mrl_mlp_fisher_split": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_reduce_rows_f32": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_reduce_rows_f64": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_gemm": (i32, [vp, vp, vp]),

@@ -287,12 +287,6 @@ __device__ inline VjpArgs vjp_shape(const VjpArgs& in) {
 #ifndef MRL_VJP_BIAS_REG  // 1: bias gradients from per-lane register partials (no per-tile LDS row sums)
 #define MRL_VJP_BIAS_REG 1
 #endif
-#ifndef MRL_VJP16_VG2  // 1: the policy-shape VJP16 forms gW2 on the VALU (A/B: MRL_VJP16_VG2 env)
-#define MRL_VJP16_VG2 0
-#endif
-#ifndef MRL_VJP16  // 1: cached VJPs run the transpose-free 16-row kernel (mlp_vjp16_kernel)
-#define MRL_VJP16 1
-#endif
 #ifndef MRL_VJP_MINW  // minimum waves per SIMD the VJP's registers must allow (build switch)
 #define MRL_VJP_MINW 1
 #endif
@@ -650,9 +644,6 @@ __device__ inline int cache_off(int slot, int j, int w) {
   return ((slot * 4 + (w >> 3)) * 64 + 32 * ((w >> 2) & 1) + j) * 4 + (w & 3);
 }
 
-// VG2 (heads of A <= 4 outputs): gW2 += h2^T G on the VALU -- 48 fmas and 12 row
-// broadcasts per 16-row tile instead of 16 MFMAs, whose 16 output columns the head uses
-// only A of (MRL_VJP16_VG2=0 in the environment: the MFMA form)
 // HYB: the two 64x64x16 products of a tile -- gh1_T = ga2_R W1^T and gW1 += h1_T^T ga2_T,
 // 128 of its 168 f32 MFMAs -- on v_mfma_f32_16x16x32_bf16 with every f32 operand split
 // exactly into three bf16 parts (split2) and the six part products i + j <= 2 kept (each
@@ -662,7 +653,7 @@ __device__ inline int cache_off(int slot, int j, int w) {
 // LDS at entry.  gW1: K = the tile's 16 rows, two part products stacked per MFMA (k < 4:
 // part P of rows 4 g + k, k >= 4: part Q), three MFMAs for the six products.  MFMA cycles
 // per 16-row tile 5,376 -> 2,816; the split costs 48 values of VALU per lane.
-template <bool WIDE, bool EPT, bool VG2 = false, bool HYB = false>
+template <bool WIDE, bool EPT, bool HYB = false>
 __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs a, const float* __restrict__ img,
                                                                      const int32_t* __restrict__ skip) {
   constexpr int MT0 = WIDE ? 2 : 1;
@@ -711,11 +702,6 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
   }
 
   f32x4 gW1[4][4], gW2[4], gW0[MT0][4];
-  float vg2[4][4];  // VG2: [nt][o] of unit 16 nt + c, this lane group's rows
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-    for (int o = 0; o < 4; ++o) vg2[nt][o] = 0.f;
   f32x4 zero4 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
@@ -866,24 +852,10 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
       }
     }
     // gW2 += h2_T^T G  (k-step r: rows 4 g + r)
-    if constexpr (VG2) {
-      // G[row 4 g + r][o] from lane (o, g) of the same lane group
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int o = 0; o < 4; ++o) {
-          if (o < A) {
-            const float go = __shfl(GB[r], (lane & 48) | o);
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) vg2[nt][o] = fmaf(h2T[nt][r], go, vg2[nt][o]);
-          }
-        }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) gW2[nt] = MFMA16(h2T[nt][r], GB[r], gW2[nt]);
-    }
+      for (int nt = 0; nt < 4; ++nt) gW2[nt] = MFMA16(h2T[nt][r], GB[r], gW2[nt]);
 #pragma unroll
     for (int r = 0; r < 4; ++r) pG += GB[r];
 #pragma unroll
@@ -990,12 +962,6 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
   }
 
   // ---- bias / logstd partials: sum over the four lane groups (rows)
-  if constexpr (VG2) {  // over the four lane groups (rows)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int o = 0; o < 4; ++o) vg2[nt][o] = xor32_add(xor16_add(vg2[nt][o]));
-  }
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) pb1[nt] = xor32_add(xor16_add(pb1[nt]));
   pG = xor32_add(xor16_add(pG));
@@ -1032,7 +998,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) xfer(VG2 ? vg2[n][r] : gW2[n][r], k++);
+      for (int r = 0; r < 4; ++r) xfer(gW2[n][r], k++);
 #pragma unroll
     for (int m0 = 0; m0 < MT0; ++m0)
 #pragma unroll
@@ -1051,10 +1017,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if constexpr (VG2) vg2[n][r] += pl(k++);
-        else gW2[n][r] += pl(k++);
-      }
+      for (int r = 0; r < 4; ++r) gW2[n][r] += pl(k++);
 #pragma unroll
     for (int m0 = 0; m0 < MT0; ++m0)
 #pragma unroll
@@ -1078,11 +1041,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
   for (int n = 0; n < 4; ++n)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if constexpr (VG2) {
-        if (g == 0 && r < A) out[d.tW2 + (16 * n + c) * A + r] = vg2[n][r];  // r: the output o
-      } else if (c < A) {
-        out[d.tW2 + (16 * n + 4 * g + r) * A + c] = gW2[n][r];
-      }
+      if (c < A) out[d.tW2 + (16 * n + 4 * g + r) * A + c] = gW2[n][r];
   // gW0 [i][u]: i = 16 m0 + 4 g + r, u = 16 nt + c; row O (the ones column) is b0's
 #pragma unroll
   for (int m0 = 0; m0 < MT0; ++m0)
@@ -1434,28 +1393,18 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
     else if (!wide) hipLaunchKernelGGL((mlp_vjp_kernel<C, false, 0>), grid, blk, shm, s, a, image, skip);   \
     else hipLaunchKernelGGL((mlp_vjp_kernel<C, true, 0>), grid, blk, shm, s, a, image, skip);               \
   } while (0)
-  static const bool use16 = []() {  // MRL_VJP16=0 in the environment: the 32-row kernel (A/B probes)
-    const char* e = getenv("MRL_VJP16");
-    return e ? atoi(e) != 0 : MRL_VJP16 != 0;
-  }();
   // the 16-row kernel takes the bias gradient b0 through a ones column of gW0's padding
-  if (use16 && act_cache != nullptr && a.d.O % 16 != 0) {
+  if (act_cache != nullptr && a.d.O % 16 != 0) {
     // the transpose-free 16-row kernel (8 waves per block, same slab rows per block)
     const size_t shm16 = 0;  // static LDS: weight fragments + h1 staging (82 KB)
     const dim3 blk16(64 * VJP16_WAVES);
     const bool ept = ep_t != nullptr;
-    // MRL_VJP16_VG2: gW2 on the VALU for heads of <= 4 outputs (read per call: tests switch it)
-    const char* vg2_env = getenv("MRL_VJP16_VG2");
-    const bool vg2_on = vg2_env ? atoi(vg2_env) != 0 : MRL_VJP16_VG2 != 0;
-    const bool vg2 = vg2_on && a.d.A <= 4 && !wide && !ept;
     if (wide) {
       if (ept) hipLaunchKernelGGL((mlp_vjp16_kernel<true, true>), grid, blk16, shm16, s, a, image, skip);
       else hipLaunchKernelGGL((mlp_vjp16_kernel<true, false>), grid, blk16, shm16, s, a, image, skip);
-    } else if (vg2) {
-      hipLaunchKernelGGL((mlp_vjp16_kernel<false, false, true>), grid, blk16, shm16, s, a, image, skip);
     } else {
-      if (ept) hipLaunchKernelGGL((mlp_vjp16_kernel<false, true, false, true>), grid, blk16, shm16, s, a, image, skip);
-      else hipLaunchKernelGGL((mlp_vjp16_kernel<false, false, false, true>), grid, blk16, shm16, s, a, image, skip);
+      if (ept) hipLaunchKernelGGL((mlp_vjp16_kernel<false, true, true>), grid, blk16, shm16, s, a, image, skip);
+      else hipLaunchKernelGGL((mlp_vjp16_kernel<false, false, true>), grid, blk16, shm16, s, a, image, skip);
     }
     return hip_check(hipGetLastError(), "mrl_mlp_vjp");
   }

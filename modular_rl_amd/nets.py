@@ -128,10 +128,8 @@ class MlpNet:
         # the Fisher products of an update and the VJP after a loss pass reuse it
         self.use_cache = True
         self._cache_key = None
-        # fp32 Fisher products on bf16 MFMA with exactly split operands (csrc/mlp_split.hip):
-        # MRL_FISHER=split (default) | f32 (the exact-f32 MFMA kernels); MRL_VJP_SPLIT=1 also
-        # runs the cached VJP on split operands (form 1 measured slower, off), in the kernel
-        # form MRL_VJP_SPLIT_FORM (1: identity-MFMA transposes, 2: transpose-free gathers)
+        # the fp32 Fisher product's JVP half on bf16 MFMA with exactly split operands
+        # (csrc/mlp_split.hip): MRL_FISHER=split (default) | f32 (the exact-f32 MFMA rows kernel)
         self.fisher_split = (not self.bf16) and os.environ.get("MRL_FISHER", "split") == "split"
         self.image_s = None
         if self.fisher_split:
@@ -157,7 +155,7 @@ class MlpNet:
         call("mrl_mlp_pack" + self._sfx, ctypes.byref(self.desc), ptr(theta), ptr(image), int(fwd_only), ptr(skip),
              stream())
         if image is self.image and self.fisher_split:
-            call("mrl_mlp_pack_split", ctypes.byref(self.desc), ptr(theta), ptr(self.image_s), 0, ptr(skip), stream())
+            call("mrl_mlp_pack_split", ctypes.byref(self.desc), ptr(theta), ptr(self.image_s), ptr(skip), stream())
 
     def new_tangent_image(self):
         """Image buffer for Fisher-product tangents (pack_tangent): a split image when the
@@ -170,7 +168,7 @@ class MlpNet:
 
     def pack_tangent(self, v, image, skip=None):
         if self.fisher_split:
-            call("mrl_mlp_pack_split", ctypes.byref(self.desc), ptr(v), ptr(image), 1, ptr(skip), stream())
+            call("mrl_mlp_pack_split", ctypes.byref(self.desc), ptr(v), ptr(image), ptr(skip), stream())
         else:
             self.pack(theta=v, image=image, fwd_only=True, skip=skip)
 
@@ -237,40 +235,11 @@ class MlpNet:
         cache = None
         if self.use_cache and image is None and self._cache_key == self._key(x, n, ep_t, timestep_limit):
             cache = self._cache(n)
-        if (cache is not None and self.fisher_split and ep_t is None and self.head != _lib.HEAD_LINEAR
-                and os.environ.get("MRL_VJP_SPLIT", "0") != "0"):
-            # the policy's cached VJPs (Fisher products, policy gradient) on split operands
-            call("mrl_mlp_vjp_split", ctypes.byref(self.desc), ptr(self.image_s), ptr(x), ptr(ghead), int(n),
-                 ptr(slab), ptr(cache), ptr(skip), stream())
-        else:
-            image = self.image if image is None else image
-            call("mrl_mlp_vjp" + self._sfx, ctypes.byref(self.desc), ptr(image), ptr(x), ptr(ep_t),
-                 float(timestep_limit), ptr(ghead), int(n), ptr(slab), ptr(cache), ptr(skip), stream())
+        image = self.image if image is None else image
+        call("mrl_mlp_vjp" + self._sfx, ctypes.byref(self.desc), ptr(image), ptr(x), ptr(ep_t),
+             float(timestep_limit), ptr(ghead), int(n), ptr(slab), ptr(cache), ptr(skip), stream())
         call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
         return out
-
-    def fisher_fusable(self, x, n, image_t):
-        return bool(self.fisher_split and getattr(image_t, "_mrl_split", False) and self.use_cache
-                    and self.head != _lib.HEAD_LINEAR and os.environ.get("MRL_FISHER_FUSED", "0") != "0"
-                    and self._cache_key == self._key(x, n, None, 1.0))
-
-    def fisher_product(self, x, n, inv_n_global, tangent, image_t, out, skip=None, ghead=None):
-        """out[P] <- the Fisher product along ``tangent`` over the n cached rows in ONE pass
-        (mrl_mlp_fisher_split: JVP, KL metric and VJP per tile, the activation cache read
-        once), when the split path applies: split tangent image, a current cache of these
-        rows, a policy head, no time feature, and MRL_FISHER_FUSED=1 (measured slower than
-        the split JVP + exact-f32 VJP pair, so off by default: DESIGN §3).  False: not
-        applicable (the caller runs rows(EPI_FVP) + vjp_flat)."""
-        if not self.fisher_fusable(x, n, image_t):
-            return False
-        rows = int(self.lib.mrl_mlp_slab_rows(ctypes.byref(self.desc), int(n)))
-        slab = self.ws.get("slab", rows * self.P, torch.float32)
-        io = _lib.RowsIO(ptr(x), None, 1.0, int(n), float(inv_n_global), None, None, None, None, None, ptr(ghead),
-                         None, 0.0, 0.0, 0.0, 0, _lib.CACHE_READ, ptr(self._cache(n)), None)
-        call("mrl_mlp_fisher_split", ctypes.byref(self.desc), ptr(self.theta), ptr(self.image_s), ptr(tangent),
-             ptr(image_t), ctypes.byref(io), ptr(slab), ptr(skip), stream())
-        call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
-        return True
 
     def reduce_partial(self, partial, n, out):
         rows = self.partial_rows(n)

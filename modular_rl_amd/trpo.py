@@ -92,12 +92,6 @@ class HipTrpoOps:
     def fvp(self, v32, skip=None):
         b, net = self.batch, self.net
         net.pack_tangent(v32, self.tan_image, skip=skip)
-        if getattr(net, "fisher_fusable", None) is not None and net.fisher_fusable(b.obs, b.n, self.tan_image):
-            # the whole product in one pass over the activation cache
-            timing.start("fvp_fused")
-            net.fisher_product(b.obs, b.n, self.inv_ng, v32, self.tan_image, self.fv, skip=skip)
-            timing.stop("fvp_fused")
-            return self.fv
         timing.start("fvp_jvp_rows")
         net.rows(_lib.EPI_FVP, b.obs, b.n, inv_n_global=self.inv_ng, ghead=self.ghead, tangent=v32,
                  image_t=self.tan_image, skip=skip)

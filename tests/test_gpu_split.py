@@ -1,6 +1,8 @@
-"""The split-operand Fisher product (csrc/mlp_split.hip: fp32 operands split exactly into
-three bf16 parts, the part products on bf16 MFMA with f32 accumulation) against the
-float64 oracle at north_star's 1e-4 and against the exact-f32 kernels to f32 rounding."""
+"""The fp32 Fisher product on the bf16 matrix cores -- the split-operand JVP rows
+(csrc/mlp_split.hip: fp32 operands split exactly into three bf16 parts, the part products
+on bf16 MFMA with f32 accumulation) and the hybrid cached VJP (mlp_vjp16_kernel<HYB>: its
+two 64x64 products on split operands) -- against the float64 oracle at north_star's 1e-4
+and against the exact-f32 kernels to f32 rounding."""
 import numpy as np
 import pytest
 import torch
@@ -22,11 +24,8 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("head,nin,nout", CASES)
 @pytest.mark.parametrize("N", [1, 33, 3001])
-@pytest.mark.parametrize("form", ["1", "2"])
-def test_split_fisher_product(head, nin, nout, N, form, monkeypatch):
+def test_split_fisher_product(head, nin, nout, N, monkeypatch):
     monkeypatch.setenv("MRL_FISHER", "split")
-    monkeypatch.setenv("MRL_VJP_SPLIT", "1")
-    monkeypatch.setenv("MRL_VJP_SPLIT_FORM", form)  # the VJP kernel (mlp_split.hip)
     from modular_rl_amd import _lib
     from modular_rl_amd.nets import MlpNet
     rng = np.random.default_rng(nin * 7 + N)
@@ -63,14 +62,14 @@ def test_split_fisher_product(head, nin, nout, N, form, monkeypatch):
     # the same rows to f32 rounding (different summation order of exact products)
     np.testing.assert_allclose(asp, a32, rtol=2e-5, atol=2e-6 * np.abs(a32).max())
     fv = torch.zeros(net.P, dtype=torch.float32, device="cuda")
-    net.vjp_flat(x, N, ghs, fv)  # the split VJP (policy net, cached)
+    net.vjp_flat(x, N, ghs, fv)  # the hybrid cached VJP (policy net)
     want = T.fisher_vector_product(spec, th, v.astype(np.float64), ob)
     assert _rel(fv.cpu().numpy(), want) < 1e-4
-    # the split VJP against the exact-f32 VJP on the same head rows: f32 rounding apart
+    # the hybrid VJP against the exact-f32 VJP (the uncached kernel: an explicit image
+    # bypasses the activation cache) on the same head rows: f32 rounding apart
     fs, f32 = torch.zeros_like(fv), torch.zeros_like(fv)
     net.vjp_flat(x, N, gh32, fs)
-    monkeypatch.setenv("MRL_VJP_SPLIT", "0")
-    net.vjp_flat(x, N, gh32, f32)
+    net.vjp_flat(x, N, gh32, f32, image=net.image)
     assert _rel(fs.cpu().numpy(), f32.cpu().numpy()) < 1e-5
     assert _rel(f32.cpu().numpy(), want) < 1e-4
 
@@ -86,21 +85,20 @@ def test_split_image_parts_sum_to_the_f32_weights(monkeypatch):
     th = (rng.standard_normal(net.P) * np.exp(rng.uniform(-20, 5, net.P))).astype(np.float32)
     net.set_flat(th)
     img = net.image_s.cpu().numpy().view(np.uint32)
-    w = int(net.lib.mrl_mlp_image_words_bf16(__import__("ctypes").byref(net.desc)))
     fa0 = 64 + 64 + 2 * 8 * 32 + 16
     fwd_words = fa0 + 2 * 1 * 64 * 4 + 2 * 4 * 64 * 4
-    FW, BW = fwd_words - fa0, w - fwd_words
+    FW = fwd_words - fa0
+    assert img.size == fa0 + 3 * FW  # the forward section only (the VJP half splits its own operands)
+
     def bf(u):  # bf16 bits (low / high halves of the words) -> f32
         return (u.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
-    for lo, n in ((fa0, FW), (fa0 + 3 * FW, BW)):
-        stride = FW if lo == fa0 else BW
-        parts = [img[lo + p * stride: lo + p * stride + n] for p in range(3)]
-        for half in (0, 1):
-            vals = [bf((pp >> (16 * half)) & 0xFFFF) for pp in parts]
-            tot = vals[0] + vals[1] + vals[2]
-            # every weight is an f32 value and the three parts reproduce it exactly
-            assert np.array_equal(tot.astype(np.float32).astype(np.float64), tot)
-            assert np.all(np.abs(vals[1]) <= np.abs(vals[0]) * 2.0 ** -7 + 1e-45)
+    parts = [img[fa0 + p * FW: fa0 + (p + 1) * FW] for p in range(3)]
+    for half in (0, 1):
+        vals = [bf((pp >> (16 * half)) & 0xFFFF) for pp in parts]
+        tot = vals[0] + vals[1] + vals[2]
+        # every weight is an f32 value and the three parts reproduce it exactly
+        assert np.array_equal(tot.astype(np.float32).astype(np.float64), tot)
+        assert np.all(np.abs(vals[1]) <= np.abs(vals[0]) * 2.0 ** -7 + 1e-45)
     w32 = set(np.abs(th).astype(np.float64).tolist()) | {0.0}
     tot0 = np.abs(bf(img[fa0:fa0 + FW] & 0xFFFF) + bf(img[fa0 + FW:fa0 + 2 * FW] & 0xFFFF) +
                   bf(img[fa0 + 2 * FW:fa0 + 3 * FW] & 0xFFFF))
@@ -138,111 +136,20 @@ def test_split_fisher_product_is_deterministic(monkeypatch):
         outs.append(gh.clone())
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
-    # and the split VJP of those rows, both kernel forms
-    monkeypatch.setenv("MRL_VJP_SPLIT", "1")
-    for form in ("1", "2"):
-        monkeypatch.setenv("MRL_VJP_SPLIT_FORM", form)
-        fv = [torch.zeros(net.P, device="cuda") for _ in range(3)]
-        for f in fv:
-            net.vjp_flat(x, N, gh, f)
-        for f in fv[1:]:
-            assert torch.equal(f, fv[0]), form
-
-
-@pytest.mark.parametrize("head,nin,nout", CASES)
-@pytest.mark.parametrize("N", [1, 33, 3001, 70001])
-def test_fused_fisher_product_equals_two_passes(head, nin, nout, N, monkeypatch):
-    """mrl_mlp_fisher_split (JVP, KL metric and VJP per tile in one kernel) gives the
-    two-pass split product bit for bit -- the split JVP rows, then the split VJP (form 2)
-    of the rows they wrote -- and its optional head rows equal the JVP kernel's; the
-    product holds the float64 oracle at 1e-4."""
-    monkeypatch.setenv("MRL_FISHER", "split")
-    monkeypatch.setenv("MRL_FISHER_FUSED", "1")
-    from modular_rl_amd import _lib
-    from modular_rl_amd.nets import MlpNet
-    rng = np.random.default_rng(nin * 11 + N)
-    spec = T.Spec(nin, [64, 64], nout, head)
-    th = T.mlp_init(rng, spec.shapes, head == "gauss") + 0.05 * rng.standard_normal(spec.P)
-    if head == "gauss":
-        th[-nout:] = 0.3 * rng.standard_normal(nout)
-    th = th.astype(np.float32).astype(np.float64)
-    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
-    oldprob = T.policy_prob(spec, th + 0.01 * rng.standard_normal(spec.P), ob).astype(np.float32).astype(np.float64)
-    act = T.sample(spec, oldprob, rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N))
-    adv = rng.standard_normal(N).astype(np.float32).astype(np.float64)
-    v = rng.standard_normal(spec.P).astype(np.float32)
-    net = MlpNet(nin, nout, _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX)
-    net.set_flat(th)
-    x, vt = _dev(ob), _dev(v)
-    a = _dev(act, torch.int32 if head == "softmax" else torch.float32)
-    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
-    gh = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
-    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(adv), oldprob=_dev(oldprob), ghead=gh,
-             partial=partial)
-    imgs = net.new_tangent_image()
-    net.pack_tangent(vt, imgs)
-    assert net.fisher_fusable(x, N, imgs)
-    # two passes: split JVP rows, split VJP form 2
-    monkeypatch.setenv("MRL_VJP_SPLIT", "1")
-    monkeypatch.setenv("MRL_VJP_SPLIT_FORM", "2")
-    gh2 = torch.full_like(gh, float("nan"))
-    net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=gh2, tangent=vt, image_t=imgs)
-    f2 = torch.zeros(net.P, dtype=torch.float32, device="cuda")
-    net.vjp_flat(x, N, gh2, f2)
-    # one pass, with the diagnostic head rows
-    ghf = torch.full_like(gh, float("nan"))
-    ff = torch.full((net.P,), float("nan"), dtype=torch.float32, device="cuda")
-    assert net.fisher_product(x, N, 1.0 / N, vt, imgs, ff, ghead=ghf)
-    torch.cuda.synchronize()
-    assert torch.equal(ghf, gh2)
-    assert torch.equal(ff, f2)
-    want = T.fisher_vector_product(spec, th, v.astype(np.float64), ob)
-    assert _rel(ff.cpu().numpy(), want) < 1e-4
-
-
-def test_fused_fisher_product_grid_for_a_cu_subset(monkeypatch):
-    """The fused kernel sizes its grid (and so its slab rows) like the VJP for the net's
-    CU count; with a CU subset it stays equal to the two-pass product."""
-    monkeypatch.setenv("MRL_FISHER", "split")
-    monkeypatch.setenv("MRL_FISHER_FUSED", "1")
-    monkeypatch.setenv("MRL_VJP_SPLIT", "1")
-    monkeypatch.setenv("MRL_VJP_SPLIT_FORM", "2")
-    from modular_rl_amd import _lib
-    from modular_rl_amd.nets import MlpNet, glorot_init
-    N = 200003
-    rng = np.random.default_rng(5)
-    net = MlpNet(11, 3, _lib.HEAD_GAUSS)
-    net.set_flat(glorot_init(rng, 11, 3, _lib.HEAD_GAUSS))
-    net.size_for_cus(48)
-    g = torch.Generator(device="cuda").manual_seed(1)
-    x = torch.randn(N, 11, device="cuda", generator=g)
-    act = torch.randn(N, 3, device="cuda", generator=g)
-    adv = torch.randn(N, device="cuda", generator=g)
-    prob = net.forward(x, N).clone()
-    gh = torch.zeros(N * net.gh, device="cuda")
-    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
-    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=act, adv=adv, oldprob=prob, ghead=gh, partial=partial)
-    v = torch.randn(net.P, device="cuda", generator=g) * 1e-2
-    imgt = net.new_tangent_image()
-    net.pack_tangent(v, imgt)
-    net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=gh, tangent=v, image_t=imgt)
-    f2 = torch.zeros(net.P, device="cuda")
-    net.vjp_flat(x, N, gh, f2)
-    ff = torch.zeros(net.P, device="cuda")
-    outs = []
-    for _ in range(3):
-        assert net.fisher_product(x, N, 1.0 / N, v, imgt, ff)
-        outs.append(ff.clone())
-    for o in outs:
-        assert torch.equal(o, f2)
+    # and the hybrid cached VJP of those rows
+    fv = [torch.zeros(net.P, device="cuda") for _ in range(3)]
+    for f in fv:
+        net.vjp_flat(x, N, gh, f)
+    for f in fv[1:]:
+        assert torch.equal(f, fv[0])
 
 
 @pytest.mark.parametrize("head,nin,nout", [("gauss", 11, 3), ("softmax", 4, 2), ("linear", 12, 1), ("gauss", 17, 4)])
 @pytest.mark.parametrize("N", [1, 33, 70001])
-def test_vjp16_valu_head_gradient(head, nin, nout, N, monkeypatch):
-    """The cached 16-row VJP with the head-weight gradient on the VALU (MRL_VJP16_VG2=1,
-    heads of <= 4 outputs) against its MFMA form: the same sums in another order (f32
-    rounding apart), and against the float64 J^T g of the oracle at 1e-4."""
+def test_vjp16_hybrid_against_exact_f32_and_oracle(head, nin, nout, N):
+    """The cached 16-row VJP (its two 64x64 products on split bf16 operands) against the
+    exact-f32 uncached VJP on the same head rows (f32 rounding apart) and against the
+    float64 J^T g of the oracle at 1e-4."""
     from modular_rl_amd import _lib
     from modular_rl_amd.nets import MlpNet
     rng = np.random.default_rng(nin + N)
@@ -269,16 +176,16 @@ def test_vjp16_valu_head_gradient(head, nin, nout, N, monkeypatch):
         net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(rng.standard_normal(N)),
                  oldprob=_dev(oldprob), ghead=gh, partial=part)
     outs = {}
-    for v in ("0", "1"):
-        monkeypatch.setenv("MRL_VJP16_VG2", v)
+    for v, image in (("hyb", None), ("f32", net.image)):
         o = torch.zeros(net.P, dtype=torch.float32, device="cuda")
-        net.vjp_flat(x, N, gh, o)
+        net.vjp_flat(x, N, gh, o, image=image)
         outs[v] = o.cpu().numpy().astype(np.float64)
-    assert _rel(outs["1"], outs["0"]) < 1e-5
+    assert _rel(outs["hyb"], outs["f32"]) < 1e-5
     g = gh.cpu().numpy().astype(np.float64).reshape(N, -1)
     _, acts = T.mlp_forward(spec, th, ob)
     parts = [p.ravel() for p in T.mlp_vjp(spec, th, acts, g[:, :nout])]
     if head == "gauss":
         parts.append(g[:, nout:].sum(axis=0))  # the logstd slot: the rows' own log-std gradients
     want = np.concatenate(parts)
-    assert _rel(outs["1"], want) < 1e-4
+    assert _rel(outs["hyb"], want) < 1e-4
+    assert _rel(outs["f32"], want) < 1e-4

@@ -14,9 +14,7 @@ import os
 
 # role -> kernel-name substring (first match wins, most specific first)
 ROLES = [
-    ("fvp_fused", "mlp_fisher_split_kernel"),        # the one-pass split Fisher product (round 4)
     ("fvp_jvp_rows_split", "mlp_fvp_split_kernel"),
-    ("vjp_split", "mlp_vjp_split"),
     ("fvp_jvp_rows", "mlp_rows_kernel<100"),
     ("fvp_vjp", "mlp_vjp16_kernel<false, false"),  # the cached VJP (16-row kernel)
     ("fvp_vjp_r02", "mlp_vjp_kernel<true"),          # its round-2 32-row predecessor

@@ -2,7 +2,7 @@
 (mlp_rows_kernel<EPI_FVP_CACHED>) against the split-operand bf16 kernel
 (mlp_fvp_split_kernel), both reading the f32 activation cache of one SURRGRAD pass;
 prints ms per launch and the max relative difference of the head-gradient rows and of
-the whole Fisher product (f32 VJP of each)."""
+the whole Fisher product (the same cached VJP of each)."""
 import os
 import sys
 
@@ -61,19 +61,8 @@ for nin, nout, head in CASES[:int(os.environ.get("MRL_PROBE_NCASES", len(CASES))
     t32, ts = timed(jvp32), timed(jvps)
     f32 = torch.zeros(net.P, device='cuda')
     fs = torch.zeros(net.P, device='cuda')
-    os.environ["MRL_VJP_SPLIT"] = "0"
-    tv32 = timed(lambda: net.vjp_flat(x, N, gh, f32))
-    os.environ["MRL_VJP_SPLIT"] = "1"  # the kernel form: MRL_VJP_SPLIT_FORM (1 | 2)
-    tvs = timed(lambda: net.vjp_flat(x, N, gh_s, fs))
-    fss = torch.zeros(net.P, device='cuda')
-    net.vjp_flat(x, N, gh, fss)  # split VJP of the f32 head rows
+    tv = timed(lambda: net.vjp_flat(x, N, gh, f32))  # the cached VJP (mlp_vjp16_kernel, hybrid)
+    net.vjp_flat(x, N, gh_s, fs)
     torch.cuda.synchronize()
-    print(f"[{nin},{nout},{head}] fvp rows: f32 {t32:.4f} ms  split {ts:.4f} ms | vjp(+reduce): f32 {tv32:.4f} ms  "
-          f"split {tvs:.4f} ms | ghead rel diff {rel(gh_s, gh):.3e}  split-VJP rel diff {rel(fss, f32):.3e}  "
-          f"Fv (both split) rel diff {rel(fs, f32):.3e}", flush=True)
-    os.environ["MRL_FISHER_FUSED"] = "1"
-    ff = torch.zeros(net.P, device='cuda')
-    tf = timed(lambda: net.fisher_product(x, N, 1.0 / N, v, imgs, ff))
-    torch.cuda.synchronize()
-    print(f"[{nin},{nout},{head}] fused one-pass Fisher product (+reduce) {tf:.4f} ms vs f32 pair {t32 + tv32:.4f} ms "
-          f"| rel diff vs the f32 pair {rel(ff, f32):.3e}  vs two-pass split {rel(ff, fs):.3e}", flush=True)
+    print(f"[{nin},{nout},{head}] fvp rows: f32 {t32:.4f} ms  split {ts:.4f} ms | vjp(+reduce) {tv:.4f} ms | "
+          f"ghead rel diff {rel(gh_s, gh):.3e}  Fv (split rows vs f32 rows) rel diff {rel(fs, f32):.3e}", flush=True)

@@ -1,8 +1,7 @@
-"""A/B of the cached VJP kernels at the Hopper C3 size (4,194,304 rows): the VJP launch
-alone (no slab reduction), HIP events on the launch stream.  Run once per kernel:
-MRL_VJP16=1 (16-row transpose-free) / MRL_VJP16=0 (32-row LDS-transpose)."""
+"""Time the cached VJP kernel (mlp_vjp16_kernel, hybrid form) at the Hopper C3 size
+(4,194,304 rows): the VJP launch alone (no slab reduction), HIP events on the launch
+stream."""
 import ctypes
-import os
 import sys
 
 import numpy as np
@@ -49,5 +48,5 @@ for nin, nout, head in [(11, 3, _lib.HEAD_GAUSS), (4, 2, _lib.HEAD_SOFTMAX), (12
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 10
     flop = 2.0 * (2 * 64 * 64 + 64 * nout * 2 + nin * 64) * N
-    print(f"MRL_VJP16={os.environ.get('MRL_VJP16', '1')} nin={nin} nout={nout}: {ms:.3f} ms/launch "
+    print(f"vjp16 nin={nin} nout={nout}: {ms:.3f} ms/launch "
           f"{flop / ms / 1e9:.1f} TFLOP/s = {flop / ms / 1e9 / 157.3:.3f} of fp32 MFMA", flush=True)
