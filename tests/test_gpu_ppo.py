@@ -176,11 +176,18 @@ def test_ppo_lbfgs_matches_reference_golden(k, layered):
     got = np.array([info[x] for x in keys])
     ok = np.abs(got - want_i) <= np.maximum(1e-4 * np.abs(want_i) + 1e-6, 2 * floor_i)
     if not ok.all() and not split:
-        # the default maxiter 25 (lbg2) ends L-BFGS at its iteration limit on a chaotic
-        # path: theta is held above at the reference's own float32 floor, and an "after"
-        # entry may then sit off the reference's by more than its own f32-f64 distance.
-        # Such entries are held instead to the reference's loss functions (ppo.py:47-49,
-        # the oracle pinned to them) evaluated at the device's theta, at 1e-4.
+        # PARITY UNPINNED for these entries.  The default maxiter 25 (lbg2) ends L-BFGS at
+        # its iteration limit on a chaotic path: the reference's own float32 run lands 21 %
+        # (surr after) to 44 % (kl change) off its float64 run (lbg2f_info vs lbg2_info),
+        # so no fixture pins an "after" entry tighter than that.  theta is held above at
+        # the reference's own float32 floor; an "after" entry outside 2x the fixture's
+        # f32-f64 distance is reported (warning) and checked only for self-consistency:
+        # the reference's loss functions (ppo.py:47-49, the oracle pinned to them)
+        # evaluated at the device's theta, at 1e-4.  A float32 L-BFGS fixture that tracks
+        # the device path would pin them; scipy's float64 L-BFGS-B has no float32 mode.
+        import warnings
+        warnings.warn(f"{k}: after-entries {[keys[i] for i in np.flatnonzero(~ok)]} parity unpinned "
+                      f"(outside 2x the reference's own f32-f64 distance; self-consistency checked)")
         from oracle import ppo_np as PO
         from oracle import trpo_np as T
         w = d[k + "_oldprob"].shape[1]
