@@ -47,8 +47,8 @@ def flops_per_row(net):
     fwd = 2 * sum(mm)
     if getattr(net, "layered", False) or getattr(net, "use_cache", False):
         # the primal forward comes from the activation cache / recorded tape
-        return {"fvp_jvp_rows": jvp, "fvp_vjp": vjp, "policy_forward": fwd}
-    return {"fvp_jvp_rows": fwd + jvp, "fvp_vjp": vjp, "policy_forward": fwd}
+        return {"fvp_jvp_rows": jvp, "fvp_vjp": vjp, "fvp_onepass": jvp + vjp, "policy_forward": fwd}
+    return {"fvp_jvp_rows": fwd + jvp, "fvp_vjp": vjp, "fvp_onepass": fwd + jvp + vjp, "policy_forward": fwd}
 
 
 def vjp_binary_entry(kern, policy_vjp_flop, vf_vjp_flop, rows, iters):
@@ -260,6 +260,9 @@ def fisher_arith(net):
         if getattr(net, "fisher_split", False) else "exact f32 MFMA"
     vjp = ("hybrid: the two 64x64 products of each 16-row tile (gh1, gW1) on split-operand bf16 MFMA, "
            "the rest exact f32 MFMA (mlp_vjp16_kernel<HYB>)")
+    if getattr(net, "fisher_onepass", False):
+        return {"pass": "one kernel per product (mlp_fisher_hyb_kernel: per block 4 waves of JVP rows + KL metric "
+                        "and 4 waves of the hybrid VJP, the head rows through LDS)", "jvp_rows": jvp, "vjp": vjp}
     return {"pass": "two kernels per product (JVP + metric rows, then the VJP)", "jvp_rows": jvp, "vjp": vjp}
 
 
@@ -272,7 +275,8 @@ def policy_gemm_roofline(kern, kinfo, net, dtype, n_rows, K, pmc, gemm_pmc):
     dense MFMA peak, and the PMC traffic / algorithmic bytes ratio where a pass measured it."""
     peak = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_FP32_TFLOPS
     if not net.layered:
-        cands = {k: v for k, v in kinfo.items() if k in ("fvp_jvp_rows",) + tuple(VJP_BINARY.values())}
+        cands = {k: v for k, v in kinfo.items()
+                 if k in ("fvp_onepass", "fvp_jvp_rows") + tuple(VJP_BINARY.values())}
         if not cands:
             return None
         name = max(cands, key=lambda k: cands[k]["total_ms"])
@@ -286,7 +290,9 @@ def policy_gemm_roofline(kern, kinfo, net, dtype, n_rows, K, pmc, gemm_pmc):
                 "algorithmic_bytes": alg or None,
                 "kernel": {"fvp_jvp_rows": ("mlp_fvp_split_kernel (JVP + KL metric)"
                                             if getattr(net, "fisher_split", False)
-                                            else "mlp_rows_kernel (JVP + KL metric)")}.get(name, name),
+                                            else "mlp_rows_kernel (JVP + KL metric)"),
+                           "fvp_onepass": "mlp_fisher_hyb_kernel (JVP + KL metric + hybrid VJP, one launch)"
+                           }.get(name, name),
                 "flop_per_row": ki["flop_per_row"], "rows_per_launch": ki["rows_per_launch"],
                 "mean_launch_ms": round(ki["mean_ms"], 5), "launches_timed": ki["launches"],
                 "ms_per_iter": round(ki["total_ms"] / K, 3),
@@ -416,14 +422,16 @@ def main():
         if "fvp_jvp_rows" not in pmc and "fvp_jvp_rows_split" in pmc:  # the JVP half's kernel this round
             pmc["fvp_jvp_rows"] = pmc["fvp_jvp_rows_split"]
     kinfo = {}
-    for name in ("fvp_jvp_rows", "fvp_vjp"):
+    for name in ("fvp_onepass", "fvp_jvp_rows", "fvp_vjp"):
         if name in kern:
             cnt, mean_ms, tot_ms = kern[name]
             kinfo[name] = dict(launches=cnt, mean_ms=mean_ms, total_ms=tot_ms, rows_per_launch=n_local,
                                flop_per_row=fpr[name])
             if not net.layered:
-                kinfo[name]["bytes_per_row"] = row_b
-                kinfo[name]["hbm_gbs_alg"] = row_b * n_local / (mean_ms * 1e-3) / 1e9
+                # one pass: the cache and the obs row cross HBM, the head rows stay in LDS
+                rb = cache_b + 4 * net.n_in if name == "fvp_onepass" else row_b
+                kinfo[name]["bytes_per_row"] = rb
+                kinfo[name]["hbm_gbs_alg"] = rb * n_local / (mean_ms * 1e-3) / 1e9
     if not net.layered:
         # the same kernel binary (the cached VJP) also serves the policy gradient and every
         # VF L-BFGS evaluation (the VF fit's launches run beside the next rollout on the

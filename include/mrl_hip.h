@@ -167,6 +167,17 @@ int64_t mrl_mlp_image_words_split(const mrl_mlp_desc* d);
 int mrl_mlp_pack_split(const mrl_mlp_desc* d, const float* theta, float* image, const int32_t* skip, void* stream);
 int mrl_mlp_fvp_split(const mrl_mlp_desc* d, const float* theta, const float* image, const float* tangent,
                       const float* image_t, const mrl_rows_io* io, const int32_t* skip, void* stream);
+/* The whole Fisher product in one launch (trpo.py:45-58, Fvp = J^T M J v): per block,
+ * four waves run the split JVP rows above on 32-row tiles and leave the KL-metric head
+ * rows in LDS, four waves run the hybrid cached VJP (mrl_mlp_vjp) on them; the activation
+ * cache crosses HBM once.  Slab rows as mrl_mlp_vjp (mrl_mlp_slab_rows(d, n)), then
+ * mrl_reduce_rows_f32.  image: the f32 image (its W1 / W2 fragments); image_s / image_t_s:
+ * split images of theta and of the tangent.  E_UNSUPPORTED unless
+ * mrl_mlp_fisher_hyb_fits(d) (policy nets of <= 15 inputs; the split images fit LDS). */
+int32_t mrl_mlp_fisher_hyb_fits(const mrl_mlp_desc* d);
+int mrl_mlp_fisher_hyb(const mrl_mlp_desc* d, const float* theta, const float* image, const float* image_s,
+                       const float* tangent, const float* image_t_s, const mrl_rows_io* io, float* slab,
+                       const int32_t* skip, void* stream);
 
 int mrl_reduce_rows_f32(const float* slab, int64_t rows, int64_t cols, float* out, const int32_t* skip, void* stream);
 int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* out, const int32_t* skip, void* stream);

@@ -98,6 +98,8 @@ SIGNATURES = {
     "mrl_mlp_vjp_bf16": (i32, [vp, vp, vp, vp, f64, vp, i64, vp, vp, vp, vp]),
     "mrl_mlp_image_words_split": (i64, [vp]),
     "mrl_mlp_pack_split": (i32, [vp, vp, vp, vp, vp]),
+    "mrl_mlp_fisher_hyb_fits": (i32, [vp]),
+    "mrl_mlp_fisher_hyb": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_mlp_fvp_split": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_reduce_rows_f32": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_reduce_rows_f64": (i32, [vp, i64, i64, vp, vp, vp]),

@@ -22,6 +22,7 @@
 #include "../../include/mrl_hip.h"
 #include "mlp_device.h"
 #include "rows_epilogue.h"
+#include "fvp_split_role.h"
 
 namespace mrl {
 
@@ -1061,6 +1062,412 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
   }
 }
 
+// The one-pass Fisher product (mlp_fisher_hyb_kernel): the hybrid VJP above with the
+// Fisher product's JVP half beside it in the block.  Waves 0-3 (one per SIMD) run the
+// split-operand JVP rows of 32-row tiles (JvpSplitRole, fvp_split_role.h) and leave each
+// tile's KL-metric head-gradient rows in an LDS mailbox; waves 4-7 (the partner wave of
+// each SIMD) run this VJP on them one round later -- the tile's h1 / h2 / x re-read from
+// L2, where the JVP wave's loads of the same CU just put them, so the activation cache
+// crosses HBM once per product instead of twice, and each SIMD interleaves the JVP's VALU
+// work with the VJP's MFMA chains.  One s_barrier per round (two mailbox slots); the
+// head-gradient rows never reach HBM.
+constexpr int MBOX_GH = 2 * MAX_OUT;  // mailbox row pitch (floats): the widest head-gradient row
+
+struct FisherFusedIn {
+  RowsArgs ra;        // the JVP rows' arguments (x, n, inv_ng, logstd / dlogstd, cache)
+  BDims rb;
+  const float* img_s; // split images of theta and of the tangent (mrl_mlp_pack_split)
+  const float* imt_s;
+};
+
+template <int SH>
+__global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(VjpArgs a, const float* __restrict__ img,
+                                                                           const int32_t* __restrict__ skip,
+                                                                           FisherFusedIn fz) {
+  constexpr int MT0 = 1;
+  // LDS: the W2 fragments (the split W1^T of gh1 is in wbs), h1 staging of the four VJP
+  // waves, wbs, the mailbox and (dynamic) the two split images: 148 KB for Hopper
+  __shared__ __attribute__((aligned(16))) float lds[2 * 4 * 64];
+  __shared__ __attribute__((aligned(16))) float sH[4 * 2 * VJP16_H1_FLOATS];
+  // B fragments of gh1 = ga2 W1^T, [k-step s][tile nt][part p][lane], 24 KB
+  __shared__ __attribute__((aligned(16))) bf16x8 wbs[2 * 4 * 3 * 64];
+  // head-gradient rows of the JVP waves' tiles, [slot][JVP wave][row][MBOX_GH]
+  __shared__ __attribute__((aligned(16))) float mbox[2 * 4 * 32 * MBOX_GH];
+  extern __shared__ __attribute__((aligned(16))) float ldsx[];  // the two split images
+  if (skip != nullptr && *skip != 0) return;
+  const MlpDims& d = a.d;
+  for (int i = threadIdx.x; i < 2 * 4 * 64 / 4; i += 64 * VJP16_WAVES)  // BA2 of the image
+    reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img + d.ba1 + 2 * 32 * 64)[i];
+  const int WS = split_fwd_words(fz.rb);
+  for (int i = threadIdx.x; i < WS / 4; i += 64 * VJP16_WAVES) {
+    reinterpret_cast<float4*>(ldsx)[i] = reinterpret_cast<const float4*>(fz.img_s)[i];
+    reinterpret_cast<float4*>(ldsx + WS)[i] = reinterpret_cast<const float4*>(fz.imt_s)[i];
+  }
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform tile bases
+  const int A = d.A, gh = a.gh;
+  const int KS2 = (A + 3) >> 2;  // head k-steps (A <= 8)
+  // W2 fragment (nt, ks) = W2[16 nt + c][4 ks + g] (zero past A): BA2 holds W2[i][o] at
+  // ((i >> 5) * 64 + 32 (o >> 2) + (i & 31)) * 4 + (o & 3)
+  const float* w2l = lds + 4 * c + g;
+  auto w2frag = [&](int nt, int ks) { return w2l[((nt >> 1) * 64 + 32 * ks + 16 * (nt & 1)) * 4]; };
+  __syncthreads();
+  // W1 fragment (nt, mt): W1[16 nt + c][16 mt + 4 g + 0..3] as one float4 of BA1 (read
+  // from the image in global memory, only to build wbs)
+  const float* w1l = img + d.ba1 + (32 * (g & 1) + c) * 4;
+  auto w1frag = [&](int nt, int mt) {
+    const int s4 = 4 * (mt >> 1) + 2 * (mt & 1) + (g >> 1);
+    return ld4(w1l + (((nt >> 1) * 8 + s4) * 64 + 16 * (nt & 1)) * 4);
+  };
+  // per-lane parts of the cache offsets (cache_off): T gathers (unit 16 p + c, row 4 g + r)
+  // and R float4s (row c, units 16 p + 4 g .. + 3); the (slot, p, r) parts are constants
+  const int offT = ((c >> 3) * 64 + 32 * ((c >> 2) & 1) + 4 * g) * 4 + (c & 3);
+  const int offR = ((g >> 1) * 64 + 32 * (g & 1) + c) * 4;
+  {
+    // wave w builds (k-step s = w >> 2, tile nt = w & 3): lane (c, g) element e is
+    // W1[16 nt + c][16 (2 s + (e >> 2)) + 4 g + (e & 3)], i.e. w1frag(nt, 2 s + (e >> 2))
+    static_assert(VJP16_WAVES == 8, "one (s, nt) per wave");
+    const int s = wave >> 2, nt = wave & 3;
+    const float4 u = w1frag(nt, 2 * s), v = w1frag(nt, 2 * s + 1);
+    bf16x4 pu[3], pv[3];
+    split4(f32x4{u.x, u.y, u.z, u.w}, pu);
+    split4(f32x4{v.x, v.y, v.z, v.w}, pv);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) wbs[((s * 4 + nt) * 3 + p) * 64 + lane] = cat4(pu[p], pv[p]);
+    __syncthreads();
+  }
+  // Rounds: in round r the JVP waves fill mailbox slot r & 1 with the rows of their
+  // round-r tiles (32-row tile T = (r G + block) 4 + w) and the VJP waves consume slot
+  // (r - 1) & 1; every wave passes the same number of barriers (one per round)
+  const int64_t nt32 = (a.n + 31) / 32, stride32 = (int64_t)gridDim.x * 4;
+  const int64_t rounds = (nt32 + stride32 - 1) / stride32 + 1;
+  auto fused_barrier = []() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's mailbox writes / reads are done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  {
+    if (wave < 4) {
+      RowsArgs ra = fz.ra;
+      BDims rb = fz.rb;
+      split_shape<SH>(ra, rb);
+      JvpSplitRole role;
+      role.init(ra, rb, ldsx, ldsx + WS, lane);
+      float sd[MAX_OUT], dls[MAX_OUT];
+#pragma unroll
+      for (int j = 0; j < MAX_OUT; ++j) {
+        sd[j] = expf((ra.logstd != nullptr && j < ra.A) ? ra.logstd[j] : 0.f);
+        dls[j] = (ra.dlogstd != nullptr && j < ra.A) ? ra.dlogstd[j] : 0.f;
+      }
+      int64_t T = (int64_t)blockIdx.x * 4 + wave;
+      if (T < nt32) role.prologue(T);
+      for (int64_t r = 0; r < rounds; ++r) {
+        if (r + 1 < rounds && T < nt32) {
+          const int64_t tn = T + stride32 < nt32 ? T + stride32 : T;  // the last tile re-reads itself
+          float* mb = mbox + ((r & 1) * 4 + wave) * 32 * MBOX_GH + (lane & 31) * MBOX_GH;
+          role.tile(T, tn, [&](bool valid, int64_t, const float (&z)[MAX_OUT], const float (&dz)[MAX_OUT]) {
+            if ((lane >> 5) == 0) {
+              // the KL-metric head-gradient row (row_epilogue FVP); rows past n hold 0
+              float gg[MAX_OUT], gl[MAX_OUT];
+              fvp_metric_row<MAX_OUT>(ra, z, dz, sd, dls, gg, gl);
+#pragma unroll
+              for (int j = 0; j < MAX_OUT; ++j)
+                if (j < ra.A) {
+                  mb[j] = valid ? gg[j] : 0.f;
+                  if (ra.head == MRL_HEAD_GAUSS) mb[ra.A + j] = valid ? gl[j] : 0.f;
+                }
+            }
+          });
+          T += stride32;
+        }
+        fused_barrier();
+      }
+      return;
+    }
+  }
+
+  f32x4 gW1[4][4], gW2[4], gW0[MT0][4];
+  f32x4 zero4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    gW2[m] = zero4;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) gW1[m][n] = zero4;
+#pragma unroll
+    for (int m0 = 0; m0 < MT0; ++m0) gW0[m0][m] = zero4;
+  }
+  float pb1[4] = {0.f, 0.f, 0.f, 0.f}, pG = 0.f;
+
+  const int64_t last = a.n - 1;
+  // Tile inputs, loaded one tile ahead (software pipeline at two waves per SIMD): the
+  // head-gradient operands and h2 of tile t+1 are issued once tile t's chain has consumed
+  // half of ga2_R (its registers are free), h1 and x once the chain is done.  The loads
+  // keep raw values; the row / column masks are applied when the tile uses them (a mask
+  // at load time would wait for the load there).  Every load is unconditional (clamped
+  // addresses) and masked by opaque 0 / 1 factors: a select on a loaded value lets hipcc
+  // sink the load into a branch and drain every outstanding load at the join.
+  float gq[2], GB[4], xA[MT0][4], xN[MT0][4];  // xN: the next tile's x, moved to xA after gW0
+  f32x4 h2R[4], h2T[4], h1T[4];
+  // h2 in R and T layouts
+  auto load_h2 = [&](int64_t t) {
+    const float* ct = a.cache + (t >> 1) * CACHE_TILE_FLOATS + 16 * (int)(t & 1) * 4;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const float4 v = ld4(ct + (2 + (nt >> 1)) * 1024 + 512 * (nt & 1) + offR);
+      h2R[nt] = f32x4{v.x, v.y, v.z, v.w};
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h2T[nt][r] = ct[(2 + (nt >> 1)) * 1024 + 512 * (nt & 1) + 4 * r + offT];
+  };
+  // G of 16-row tile t from its 32-row tile's mailbox rows mbt: G[row0 + c][4 ks + g]
+  // (operand of both gh2 products), G[row0 + 4 g + r][c] (B operand of gW2, bias / logstd sums)
+  const float* mbt = mbox;
+  auto load_g_mbox = [&](int64_t t) {
+    const float* m = mbt + 16 * (int)(t & 1) * MBOX_GH;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int o = 4 * ks + g;
+      gq[ks] = m[c * MBOX_GH + (o < gh ? o : gh - 1)];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) GB[r] = m[(4 * g + r) * MBOX_GH + (c < gh ? c : gh - 1)];
+  };
+  auto mask_g = [&](int64_t t) {
+    const int64_t row0 = t * 16;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) gq[ks] *= opaque((row0 + c < a.n && 4 * ks + g < A && ks < KS2) ? 1.f : 0.f);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) GB[r] *= opaque((row0 + 4 * g + r < a.n && c < gh) ? 1.f : 0.f);
+  };
+  // x[row0 + 4 g + r][16 m0 + c] (A operand of gW0; rows past n: any finite value, their
+  // ga1 is 0)
+  auto take_x = [&]() {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int m0 = 0; m0 < MT0; ++m0) xA[m0][r] = xN[m0][r];
+    }
+  };
+  auto load_x = [&](int64_t t) {
+    const int64_t row0 = t * 16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t rr = row0 + 4 * g + r, rc = rr < last ? rr : last;
+#pragma unroll
+      for (int m0 = 0; m0 < MT0; ++m0) {
+        const int col = 16 * m0 + c;
+        xN[m0][r] = a.x[rc * a.n_obs + (col < a.n_obs ? col : a.n_obs - 1)];
+      }
+    }
+  };
+  // h1 of a tile staged in LDS by four LDS-DMA instructions (no registers while in
+  // flight).  The 16-B chunks (run = (slot * 4 + q) * 2 + h, row j) of the cache tile land
+  // at (run * 16 + jj) * 4 with the rows of each 4-row group rotated by k = 2 (q & 1) + h,
+  // jj = 4 (j >> 2) + ((j + k) & 3): the T reads below (lane (c, g): run of unit 16 p + c,
+  // row 4 g + r) then hit 64 distinct banks.  The rotation is applied on the source side
+  // (an LDS-DMA destination is lane-linear).
+  float* const h1s = sH + (wave - 4) * 2 * VJP16_H1_FLOATS;
+  auto dma_h1 = [&](int64_t t, int b) {
+    const float* ct = a.cache + (t >> 1) * CACHE_TILE_FLOATS + 16 * (int)(t & 1) * 4;
+    const int jj = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int run = 4 * i + (lane >> 4), sq = run >> 1, hh = run & 1, k = 2 * (sq & 1) + hh;
+      const int j = 4 * (jj >> 2) + ((jj - k) & 3);
+      glds16(ct + (sq * 64 + 32 * hh + j) * 4, h1s + b * VJP16_H1_FLOATS + i * 256);
+    }
+  };
+  // lane parts of the T read offsets: run bits from c, rotated row 4 g + ((r + (c >> 2)) & 3)
+  int offH[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    offH[r] = ((c >> 3) * 2 + ((c >> 2) & 1)) * 64 + 16 * g + 4 * ((r + (c >> 2)) & 3) + (c & 3);
+  auto read_h1 = [&](int b, int nt) {
+    const float* p = h1s + b * VJP16_H1_FLOATS + (nt >> 1) * 512 + (nt & 1) * 256;
+    h1T[nt] = f32x4{p[offH[0]], p[offH[1]], p[offH[2]], p[offH[3]]};
+  };
+  // column O reads 1 (a ones column: gW0's row O is the bias gradient sum_rows ga1)
+  auto mask_x = [&]() {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int m0 = 0; m0 < MT0; ++m0) {
+        const int col = 16 * m0 + c;
+        float xv = xA[m0][r] * opaque(col < a.n_obs ? 1.f : 0.f) + (col == d.O ? 1.f : 0.f);
+        xA[m0][r] = xv;
+      }
+  };
+  int buf = 0;
+  // one 16-row tile t, the loads of tile tn issued under its chain
+  auto vjp_tile = [&](int64_t t, int64_t tn) {
+    load_g_mbox(t);
+    mask_g(t);
+    // ---- gh2 in both layouts (K = head outputs), then ga2 = gh2 (1 - h2^2)
+    f32x4 ga2R[4], ga2T[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const float w = w2frag(nt, 0);
+      ga2R[nt] = MFMA16(w, gq[0], zero4);
+      ga2T[nt] = MFMA16(gq[0], w, zero4);
+    }
+    if (KS2 > 1) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const float w = w2frag(nt, 1);
+        ga2R[nt] = MFMA16(w, gq[1], ga2R[nt]);
+        ga2T[nt] = MFMA16(gq[1], w, ga2T[nt]);
+      }
+    }
+    // gW2 += h2_T^T G  (k-step r: rows 4 g + r)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) gW2[nt] = MFMA16(h2T[nt][r], GB[r], gW2[nt]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pG += GB[r];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ga2R[nt][r] *= dtanh(h2R[nt][r]);
+        ga2T[nt][r] *= dtanh(h2T[nt][r]);
+      }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) pb1[nt] += (ga2T[nt][0] + ga2T[nt][1]) + (ga2T[nt][2] + ga2T[nt][3]);
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- gh1_T = ga2_R . W1^T (K = units, k-step (mt, r)) interleaved with
+    //      gW1 += h1_T^T ga2_T (K = rows): independent chains, one MFMA stream
+    f32x4 g1T[4] = {zero4, zero4, zero4, zero4};
+    // this tile's h1 (its DMA was issued with the loads phase 1 waited for): all of it is
+    // read before the next tile's DMA is issued
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) read_h1(buf, nt);
+    {
+      // gW1 += h1_T^T ga2_T first (ga2_T's registers are free after it): K = 16 rows, two
+      // part products per MFMA
+      {
+        bf16x4 gp[4][3];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) split4(ga2T[nt], gp[nt]);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          bf16x4 hp[3];
+          split4(h1T[mt], hp);
+          const bf16x8 H21 = cat4(hp[2], hp[1]), H01 = cat4(hp[0], hp[1]), H00 = cat4(hp[0], hp[0]);
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            gW1[mt][nt] = MFMAB16(H21, cat4(gp[nt][0], gp[nt][1]), gW1[mt][nt]);  // h2 g0 + h1 g1
+            gW1[mt][nt] = MFMAB16(H01, cat4(gp[nt][2], gp[nt][0]), gW1[mt][nt]);  // h0 g2 + h1 g0
+            gW1[mt][nt] = MFMAB16(H00, cat4(gp[nt][1], gp[nt][0]), gW1[mt][nt]);  // h0 g1 + h0 g0
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // the next tile's h2 / x / h1 loads, under the gh1 chain
+      load_h2(tn);
+      load_x(tn);
+      dma_h1(tn, buf ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+      // gh1_T = ga2_R W1^T: two k-steps of 32 units, six part products each (smallest first)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x4 pa[3], pb[3];
+        split4(ga2R[2 * s], pa);
+        split4(ga2R[2 * s + 1], pb);
+        const bf16x8 A0 = cat4(pa[0], pb[0]), A1 = cat4(pa[1], pb[1]), A2 = cat4(pa[2], pb[2]);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const bf16x8* w = wbs + (s * 4 + nt) * 3 * 64 + lane;
+          const bf16x8 B0 = w[0], B1 = w[64], B2 = w[128];
+          g1T[nt] = MFMAB16(A2, B0, g1T[nt]);
+          g1T[nt] = MFMAB16(A0, B2, g1T[nt]);
+          g1T[nt] = MFMAB16(A1, B1, g1T[nt]);
+          g1T[nt] = MFMAB16(A1, B0, g1T[nt]);
+          g1T[nt] = MFMAB16(A0, B1, g1T[nt]);
+          g1T[nt] = MFMAB16(A0, B0, g1T[nt]);
+        }
+      }
+    }
+    // ---- ga1 = gh1 (1 - h1^2) in T;  gW0 += x^T ga1
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g1T[nt][r] *= dtanh(h1T[nt][r]);
+    mask_x();
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int m0 = 0; m0 < MT0; ++m0)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) gW0[m0][nt] = MFMA16(xA[m0][r], g1T[nt][r], gW0[m0][nt]);
+    take_x();
+    buf ^= 1;
+  };
+  {
+    const int vw = wave - 4;
+    int64_t T = (int64_t)blockIdx.x * 4 + vw;
+    if (T < nt32) {
+      load_h2(2 * T);
+      load_x(2 * T);
+      dma_h1(2 * T, 0);
+      take_x();
+    }
+    fused_barrier();  // round 0: the JVP waves fill slot 0
+    for (int64_t r = 1; r < rounds; ++r) {
+      if (T < nt32) {
+        mbt = mbox + (((r - 1) & 1) * 4 + vw) * 32 * MBOX_GH;
+        const int64_t Tn = T + stride32 < nt32 ? T + stride32 : T;  // the last tile re-reads itself
+#pragma unroll 1
+        for (int hf = 0; hf < 2; ++hf) vjp_tile(2 * T + hf, hf ? 2 * Tn : 2 * T + 1);
+        T += stride32;
+      }
+      fused_barrier();
+    }
+  }
+
+  // ---- bias / logstd partials: sum over the four lane groups (rows)
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) pb1[nt] = xor32_add(xor16_add(pb1[nt]));
+  pG = xor32_add(xor16_add(pG));
+
+  // ---- the four VJP waves store one slab row each (mrl_slab_rows = 4 per block)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (unused) h1 DMA has landed
+  float* out = a.slab + ((int64_t)blockIdx.x * 4 + (wave - 4)) * d.P;
+  // gW1 [in][out]: in = 16 mt + 4 g + r, out = 16 nt + c
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[d.tW1 + (16 * m + 4 * g + r) * HID + 16 * n + c] = gW1[m][n][r];
+  // gW2 [u][o]: u = 16 nt + 4 g + r, o = c
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (c < A) out[d.tW2 + (16 * n + 4 * g + r) * A + c] = gW2[n][r];
+  // gW0 [i][u]: i = 16 m0 + 4 g + r, u = 16 nt + c; row O (the ones column) is b0's
+#pragma unroll
+  for (int m0 = 0; m0 < MT0; ++m0)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * m0 + 4 * g + r;
+        if (i < d.O) out[d.tW0 + i * HID + 16 * n + c] = gW0[m0][n][r];
+        else if (i == d.O) out[d.tb0 + 16 * n + c] = gW0[m0][n][r];
+      }
+  if (g == 0) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) out[d.tb1 + 16 * n + c] = pb1[n];
+    if (c < A) out[d.tb2 + c] = pG;
+    else if (c < gh) out[d.tls + (c - A)] = pG;
+  }
+}
+
 // ------------------------------------------------------------------ pack / reduce
 __global__ void mlp_pack_kernel(MlpDims d, const float* __restrict__ th, float* __restrict__ image, int count,
                                 const int32_t* __restrict__ skip) {
@@ -1235,6 +1642,21 @@ int64_t mrl_mlp_image_floats(const mrl_mlp_desc* d) {
 int64_t mrl_partial_rows(int64_t n) { return rows_blocks(n) * 4; }
 int64_t mrl_act_cache_floats(int64_t n) { return ceil_div(n, 32) * CACHE_TILE_FLOATS; }
 int64_t mrl_slab_rows(int64_t n) { return vjp_blocks(n) * 4; }
+// 1 when the one-pass Fisher product applies to the net's shape: a policy MLP of a static
+// shape (Hopper-v2, CartPole-v0) whose input fits the 16-row VJP (O % 16 != 0, O <= 16)
+// and whose two split images fit one block's LDS beside the VJP's (W2 fragments, h1
+// staging, split W1^T, mailbox)
+int32_t mrl_mlp_fisher_hyb_fits(const mrl_mlp_desc* d) {
+  if (d == nullptr || d->n_hidden != HID || d->n_layers != 2 || d->head == MRL_HEAD_LINEAR) return 0;
+  if (d->n_out < 1 || d->n_out > MAX_OUT || d->n_in < 1 || d->n_in > MAX_IN) return 0;
+  const MlpDims m = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
+  if (m.O > 16 || m.O % 16 == 0) return 0;
+  // the static shapes only (the run-time-shape instantiation spills at 256 registers)
+  if (static_shape_of(d, false) == 0) return 0;
+  const size_t lds = (size_t)split_fwd_words(bf16_dims(d->n_in, d->n_out)) * 4 * 2 + 2 * 4 * 64 * 4 +
+                     4 * 2 * VJP16_H1_FLOATS * 4 + 2 * 4 * 3 * 64 * 16 + 2 * 4 * 32 * MBOX_GH * 4;
+  return lds <= 160 * 1024 ? 1 : 0;
+}
 int64_t mrl_mlp_partial_rows(const mrl_mlp_desc* d, int64_t n) {
   if (check_desc(d) != OK) return -1;
   return rows_blocks(n, desc_cus(d)) * 4;
@@ -1412,6 +1834,59 @@ int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const
   else MRL_VJP_LAUNCH(false);
 #undef MRL_VJP_LAUNCH
   return hip_check(hipGetLastError(), "mrl_mlp_vjp");
+}
+
+int mrl_mlp_fisher_hyb(const mrl_mlp_desc* d, const float* theta, const float* image, const float* image_s,
+                       const float* tangent, const float* image_t_s, const mrl_rows_io* io, float* slab,
+                       const int32_t* skip, void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (!io || !image || !image_s || !image_t_s || !tangent || !io->x || !slab) return fail(E_ARG, "null pointer");
+  if (!io->act_cache || io->cache_mode != MRL_CACHE_READ)
+    return fail(E_ARG, "mrl_mlp_fisher_hyb reads the f32 activation cache (MRL_CACHE_READ)");
+  if (io->ep_t) return fail(E_ARG, "mrl_mlp_fisher_hyb: policy rows only (no time feature)");
+  if (d->head == MRL_HEAD_LINEAR) return fail(E_ARG, "Fisher product of a value net");
+  if (d->head == MRL_HEAD_GAUSS && !theta) return fail(E_ARG, "DiagGauss needs theta (logstd)");
+  if (mrl_mlp_fisher_hyb_fits(d) != 1) return fail(E_UNSUPPORTED, "mrl_mlp_fisher_hyb: shape does not fit one block's LDS");
+  if (io->n <= 0) return OK;
+  VjpArgs a;
+  a.d = dims_of(d);
+  a.n_obs = d->n_in;
+  a.n_sum = d->head == MRL_HEAD_GAUSS ? d->n_out : 0;
+  a.gh = d->n_out + a.n_sum;
+  a.x = io->x;
+  a.ept = nullptr;
+  a.ts_limit = 1.0;
+  a.n = io->n;
+  a.ghead = nullptr;
+  a.slab = slab;
+  a.cache = io->act_cache;
+  FisherFusedIn fz{};
+  RowsArgs& r = fz.ra;
+  r.d = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
+  r.head = d->head;
+  r.n_obs = d->n_in;
+  r.gh = a.gh;
+  r.A = d->n_out;
+  r.x = io->x;
+  r.n = io->n;
+  r.inv_ng = io->inv_n_global;
+  r.logstd = d->head == MRL_HEAD_GAUSS ? theta + r.d.tls : nullptr;
+  r.dlogstd = d->head == MRL_HEAD_GAUSS ? tangent + r.d.tls : nullptr;
+  r.cache = io->act_cache;
+  r.cache_mode = MRL_CACHE_READ;
+  fz.rb = bf16_dims(d->n_in, d->n_out);
+  fz.img_s = image_s;
+  fz.imt_s = image_t_s;
+  // the VJP's grid and slab rows (mrl_mlp_slab_rows): one slab row per VJP wave
+  const dim3 grid(vjp_blocks(io->n, desc_cus(d))), blk(64 * VJP16_WAVES);
+  const size_t shm = (size_t)split_fwd_words(fz.rb) * 4 * 2;
+  hipStream_t s = (hipStream_t)stream;
+  switch (static_shape_of(d, false)) {
+    case 1: hipLaunchKernelGGL((mlp_fisher_hyb_kernel<1>), grid, blk, shm, s, a, image, skip, fz); break;
+    default: hipLaunchKernelGGL((mlp_fisher_hyb_kernel<2>), grid, blk, shm, s, a, image, skip, fz); break;
+  }
+  return hip_check(hipGetLastError(), "mrl_mlp_fisher_hyb");
 }
 
 int mrl_probtype_rows(int32_t head, int32_t k, int64_t n, const float* prob, const float* prob2, const void* x,

@@ -29,15 +29,9 @@
 #include "bf16_frag.h"
 #include "mlp_device.h"
 #include "rows_epilogue.h"
+#include "fvp_split_role.h"
 
 namespace mrl {
-
-// Split image: the f32 section [0, fa0), then the three parts of the forward fragments
-// (fa0, fa1: FW words each, part p of a forward segment at its bf16-image offset + p FW).
-// Only the JVP half runs on split operands (the VJP half is mlp_vjp16_kernel's hybrid
-// form, which splits its f32 image fragments itself), so there is no backward section.
-__host__ __device__ constexpr int split_fw(const BDims& b) { return b.fwd_words - b.fa0; }
-__host__ __device__ constexpr int split_fwd_words(const BDims& b) { return b.fa0 + 3 * split_fw(b); }
 
 // part p (0, 1, 2) of an f32 value's exact three-way bf16 split
 __device__ inline float bf16_part(float v, int p) {
@@ -76,64 +70,6 @@ __global__ void mlp_pack_split_kernel(MlpDims d, BDims b, const float* __restric
   image[w] = __uint_as_float(v);
 }
 
-// The exact three-way split of 8 values, two at a time: one v_cvt_pk_bf16_f32 per part
-// pair, the widening and the remainders on packed f32 (v_pk_add_f32) -- the same RNE
-// conversions and exact subtractions as the element-wise form, about 4.5 VALU per value
-// instead of 7 (the split is most of these kernels' VALU work).  Explicit vector types, so
-// the packing does not depend on the SLP vectoriser.
-// (split2: mlp_device.h)
-__device__ inline void split8v(const float* v, bf16x8* out) {
-#pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    bf16x2 a, c, e;
-    split2(f32x2{v[j], v[j + 1]}, a, c, e);
-    out[0][j] = a[0];
-    out[0][j + 1] = a[1];
-    out[1][j] = c[0];
-    out[1][j + 1] = c[1];
-    out[2][j] = e[0];
-    out[2][j + 1] = e[1];
-  }
-}
-// the three parts of registers 8 sp .. 8 sp + 7 of an F tile (the B fragment pack8 forms)
-__device__ inline void split8(const f32x16& t, int sp, bf16x8* out) {
-  float v[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = t[8 * sp + j];
-  split8v(v, out);
-}
-
-// acc += W . X for one k-step: W = the image fragment f of segment `seg` (parts at
-// +p * PS), X = three parts; smallest products first
-__device__ inline void mfma_split(const float* img, int seg, int PS, int f, int lane, const bf16x8* x, f32x16& acc) {
-  const bf16x8 w0 = frag_at(img, seg, f, lane), w1 = frag_at(img, seg + PS, f, lane);
-  const bf16x8 w2 = frag_at(img, seg + 2 * PS, f, lane);
-  acc = MFMA32B(w2, x[0], acc);
-  acc = MFMA32B(w0, x[2], acc);
-  acc = MFMA32B(w1, x[1], acc);
-  acc = MFMA32B(w1, x[0], acc);
-  acc = MFMA32B(w0, x[1], acc);
-  acc = MFMA32B(w0, x[0], acc);
-}
-
-// scheduling fence between the JVP's phases (one phase's VALU splits are not
-// interleaved into the previous phase's MFMA chain)
-#define FVP_SPLIT_FENCE() __builtin_amdgcn_sched_barrier(0)
-
-template <int SH>
-__device__ inline void split_shape(RowsArgs& a, BDims& b) {
-  if constexpr (SH != 0) {
-    constexpr StaticShape S = STATIC_SHAPES[SH];
-    a.d = static_dims(SH);
-    a.A = S.A;
-    a.head = S.head;
-    a.n_obs = S.O;
-    a.gh = S.head == MRL_HEAD_GAUSS ? 2 * S.A : S.A;
-    a.ept = nullptr;
-    b = bf16_dims(S.O, S.A);
-  }
-}
-
 // waves per block of the JVP rows kernel: 4 (two blocks per CU at 2 waves per SIMD: the
 // staged images take 67 KB of LDS per block) or 12 (one block per CU at 3 waves per SIMD)
 #ifndef MRL_SPLIT_ROWS_WAVES
@@ -151,24 +87,21 @@ constexpr int SPLIT_ROWS_BLOCK = 64 * SPLIT_ROWS_WAVES;
 template <int SH>
 __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, (4 * MRL_SPLIT_FVP_OCC / SPLIT_ROWS_WAVES > 0
                                                  ? 4 * MRL_SPLIT_FVP_OCC / SPLIT_ROWS_WAVES : 1))
-    void mlp_fvp_split_kernel(RowsArgs a, BDims b,
-                                                                           const float* __restrict__ img_g,
-                                                                           const float* __restrict__ imt_g,
-                                                                           const int32_t* __restrict__ skip) {
+    void mlp_fvp_split_kernel(RowsArgs a, BDims b, const float* __restrict__ img_g, const float* __restrict__ imt_g,
+                              const int32_t* __restrict__ skip) {
   split_shape<SH>(a, b);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if (skip != nullptr && *skip != 0) return;
-  const int W = split_fwd_words(b), PS = split_fw(b);  // forward segments only
+  const int W = split_fwd_words(b);  // forward segments only
   for (int i = threadIdx.x; i < W / 4; i += SPLIT_ROWS_BLOCK) {
     reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img_g)[i];
     reinterpret_cast<float4*>(lds + W)[i] = reinterpret_cast<const float4*>(imt_g)[i];
   }
   __syncthreads();
-  const float* img = lds;
-  const float* imt = lds + W;
-  const MlpDims dd = head_dims(a.d, b);
-  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform tile indices
+  JvpSplitRole role;
+  role.init(a, b, lds, lds + W, lane);
   const int A = a.A;
   float ls[MAX_OUT], sd[MAX_OUT], dls[MAX_OUT];
 #pragma unroll
@@ -177,106 +110,22 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, (4 * MRL_SPLIT_FVP_OCC / SPLIT_RO
     sd[j] = expf(ls[j]);
     dls[j] = (a.dlogstd != nullptr && j < A) ? a.dlogstd[j] : 0.f;
   }
-  const bool need_z = a.head != MRL_HEAD_GAUSS;  // the DiagGauss metric does not use the mean
   double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
   const int64_t ntiles = (a.n + 31) / 32;
   const int64_t stride = (int64_t)gridDim.x * SPLIT_ROWS_WAVES;
-  // Software pipeline (SQ, round 4: 0.39 of the wave time parked on s_waitcnt): a tile's
-  // inputs x and h1 are loaded during the previous tile; at a tile's start its h2 loads
-  // are issued first, then the next tile's x / h1 (vmcnt retires in order, so the wait
-  // for h2 before the head leaves the prefetch in flight)
+  const int h = lane >> 5;
   int64_t tile = (int64_t)blockIdx.x * SPLIT_ROWS_WAVES + wave;
-  float xv[MAX_KS0B][8];
-  f32x16 h1[2];
-  auto load_xh1 = [&](int64_t t, float (&x)[MAX_KS0B][8], f32x16* hh) {
-    const int64_t r = t * 32 + (lane & 31);
-    XGlobalNB xl{a.x, a.ept, a.ts_limit, a.n_obs, r, r < a.n};
-#pragma unroll
-    for (int s0 = 0; s0 < MAX_KS0B; ++s0)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[s0][j] = s0 < b.KS0B ? xl(16 * s0 + 8 * h + j) : 0.f;
-    cache_load(a.cache + t * CACHE_TILE_FLOATS, lane, 0, hh[0]);
-    cache_load(a.cache + t * CACHE_TILE_FLOATS, lane, 1, hh[1]);
-  };
-  if (tile < ntiles) load_xh1(tile, xv, h1);
+  if (tile < ntiles) role.prologue(tile);
   for (; tile < ntiles; tile += stride) {
-    const int64_t row = tile * 32 + (lane & 31);
-    const bool valid = row < a.n;
-    const float* ct = a.cache + tile * CACHE_TILE_FLOATS;
-    f32x16 h2[2];
-    cache_load(ct, lane, 2, h2[0]);
-    cache_load(ct, lane, 3, h2[1]);
-    __builtin_amdgcn_sched_barrier(0);
     const int64_t tn = tile + stride < ntiles ? tile + stride : tile;  // the last tile re-reads itself
-    float xn[MAX_KS0B][8];
-    f32x16 h1n[2];
-    load_xh1(tn, xn, h1n);
-    __builtin_amdgcn_sched_barrier(0);
-    f32x16 dh[2];
-    // layer 0 tangent: dh = (x dW0 + db0) (1 - h1^2)
-    dh[0] = load_bias16(imt, b.fb0, 0, h);
-    dh[1] = load_bias16(imt, b.fb0, 1, h);
-#pragma unroll
-    for (int s0 = 0; s0 < MAX_KS0B; ++s0) {
-      if (s0 < b.KS0B) {
-        bf16x8 xs[3];
-        split8v(xv[s0], xs);
-        mfma_split(imt, b.fa0, PS, 0 * b.KS0B + s0, lane, xs, dh[0]);
-        mfma_split(imt, b.fa0, PS, 1 * b.KS0B + s0, lane, xs, dh[1]);
-      }
-    }
-    mul_dtanh16(dh[0], h1[0]);
-    mul_dtanh16(dh[1], h1[1]);
-    // layer 1 tangent: da = (dh W1 + h1 dW1 + db1) (1 - h2^2); each input fragment is
-    // split once and feeds both output tiles (per tile the k order is unchanged: the four
-    // dh fragments, then the four h1 fragments)
-    float z[MAX_OUT], dz[MAX_OUT], dzt[MAX_OUT];
-#pragma unroll
-    for (int o = 0; o < MAX_OUT; ++o) z[o] = dz[o] = dzt[o] = 0.f;
-    f32x16 da2[2] = {load_bias16(imt, b.fb1, 0, h), load_bias16(imt, b.fb1, 1, h)};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf16x8 ps[3];
-      split8(dh[s >> 1], s & 1, ps);
-      mfma_split(img, b.fa1, PS, 0 * 4 + s, lane, ps, da2[0]);
-      mfma_split(img, b.fa1, PS, 1 * 4 + s, lane, ps, da2[1]);
-    }
-    FVP_SPLIT_FENCE();
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf16x8 ps[3];
-      split8(h1[s >> 1], s & 1, ps);
-      mfma_split(imt, b.fa1, PS, 0 * 4 + s, lane, ps, da2[0]);
-      mfma_split(imt, b.fa1, PS, 1 * 4 + s, lane, ps, da2[1]);
-    }
-    FVP_SPLIT_FENCE();
-#pragma unroll
-    for (int mo = 0; mo < 2; ++mo) {
-      f32x16& da = da2[mo];
-      mul_dtanh16(da, h2[mo]);
-      // the head on the f32 VALU: dz = da . W2 + h2 . dW2 (+ db2 in head_finish), z = h2 . W2
-      if (need_z) head_partial_mt(img, dd, h2[mo], mo, h, z);
-      head_partial_mt(img, dd, da, mo, h, dz);
-      head_partial_mt(imt, dd, h2[mo], mo, h, dzt);
-      FVP_SPLIT_FENCE();
-    }
-    if (need_z) head_finish(img, dd, z);
-#pragma unroll
-    for (int o = 0; o < MAX_OUT; ++o) dz[o] += dzt[o];
-    head_finish(imt, dd, dz);
-    if (valid && h == 0) row_epilogue<MRL_EPI_FVP, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
-#pragma unroll
-    for (int s0 = 0; s0 < MAX_KS0B; ++s0)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) xv[s0][j] = xn[s0][j];
-    h1[0] = h1n[0];
-    h1[1] = h1n[1];
+    role.tile(tile, tn, [&](bool valid, int64_t row, const float (&z)[MAX_OUT], const float (&dz)[MAX_OUT]) {
+      if (valid && h == 0) row_epilogue<MRL_EPI_FVP, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+    });
   }
   (void)acc0;
   (void)acc1;
   (void)acc2;
 }
-
 
 }  // namespace mrl
 

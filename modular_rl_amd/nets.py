@@ -131,6 +131,10 @@ class MlpNet:
         # the fp32 Fisher product's JVP half on bf16 MFMA with exactly split operands
         # (csrc/mlp_split.hip): MRL_FISHER=split (default) | f32 (the exact-f32 MFMA rows kernel)
         self.fisher_split = (not self.bf16) and os.environ.get("MRL_FISHER", "split") == "split"
+        # the whole Fisher product in one launch (mrl_mlp_fisher_hyb) where the shape allows
+        # it; MRL_FISHER_ONEPASS=0: the split JVP rows + hybrid VJP pair
+        self.fisher_onepass = (self.fisher_split and os.environ.get("MRL_FISHER_ONEPASS", "1") != "0"
+                               and bool(self.lib.mrl_mlp_fisher_hyb_fits(ctypes.byref(self.desc))))
         self.image_s = None
         if self.fisher_split:
             w = int(self.lib.mrl_mlp_image_words_split(ctypes.byref(self.desc)))
@@ -241,6 +245,27 @@ class MlpNet:
         call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
         return out
 
+    def fisher_onepass_applies(self, x, n, image_t):
+        return bool(self.fisher_onepass and getattr(image_t, "_mrl_split", False) and self.use_cache
+                    and self._cache_key == self._key(x, n, None, 1.0))
+
+    def fisher_product(self, x, n, inv_n_global, tangent, image_t, out, skip=None):
+        """out[P] <- the Fisher product along ``tangent`` over the n cached rows in ONE
+        launch (mrl_mlp_fisher_hyb: split JVP rows and hybrid VJP side by side in each
+        block, the head-gradient rows through LDS) when it applies -- a split tangent image,
+        a current activation cache of these rows, a shape mrl_mlp_fisher_hyb_fits accepts.
+        False: not applicable (the caller runs rows(EPI_FVP) + vjp_flat)."""
+        if not self.fisher_onepass_applies(x, n, image_t):
+            return False
+        rows = int(self.lib.mrl_mlp_slab_rows(ctypes.byref(self.desc), int(n)))
+        slab = self.ws.get("slab", rows * self.P, torch.float32)
+        io = _lib.RowsIO(ptr(x), None, 1.0, int(n), float(inv_n_global), None, None, None, None, None, None,
+                         None, 0.0, 0.0, 0.0, 0, _lib.CACHE_READ, ptr(self._cache(n)), None)
+        call("mrl_mlp_fisher_hyb", ctypes.byref(self.desc), ptr(self.theta), ptr(self.image), ptr(self.image_s),
+             ptr(tangent), ptr(image_t), ctypes.byref(io), ptr(slab), ptr(skip), stream())
+        call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
+        return True
+
     def reduce_partial(self, partial, n, out):
         rows = self.partial_rows(n)
         call("mrl_reduce_rows_f64", ptr(partial), rows, 4, ptr(out), None, stream())
@@ -336,6 +361,27 @@ class LayeredMlpNet:
 
     def partial_rows(self, n):
         return int(self.lib.mrl_partial_rows(int(n)))
+
+    def fisher_onepass_applies(self, x, n, image_t):
+        return bool(self.fisher_onepass and getattr(image_t, "_mrl_split", False) and self.use_cache
+                    and self._cache_key == self._key(x, n, None, 1.0))
+
+    def fisher_product(self, x, n, inv_n_global, tangent, image_t, out, skip=None):
+        """out[P] <- the Fisher product along ``tangent`` over the n cached rows in ONE
+        launch (mrl_mlp_fisher_hyb: split JVP rows and hybrid VJP side by side in each
+        block, the head-gradient rows through LDS) when it applies -- a split tangent image,
+        a current activation cache of these rows, a shape mrl_mlp_fisher_hyb_fits accepts.
+        False: not applicable (the caller runs rows(EPI_FVP) + vjp_flat)."""
+        if not self.fisher_onepass_applies(x, n, image_t):
+            return False
+        rows = int(self.lib.mrl_mlp_slab_rows(ctypes.byref(self.desc), int(n)))
+        slab = self.ws.get("slab", rows * self.P, torch.float32)
+        io = _lib.RowsIO(ptr(x), None, 1.0, int(n), float(inv_n_global), None, None, None, None, None, None,
+                         None, 0.0, 0.0, 0.0, 0, _lib.CACHE_READ, ptr(self._cache(n)), None)
+        call("mrl_mlp_fisher_hyb", ctypes.byref(self.desc), ptr(self.theta), ptr(self.image), ptr(self.image_s),
+             ptr(tangent), ptr(image_t), ctypes.byref(io), ptr(slab), ptr(skip), stream())
+        call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
+        return True
 
     def reduce_partial(self, partial, n, out):
         call("mrl_reduce_rows_f64", ptr(partial), self.partial_rows(n), 4, ptr(out), None, stream())

@@ -92,6 +92,12 @@ class HipTrpoOps:
     def fvp(self, v32, skip=None):
         b, net = self.batch, self.net
         net.pack_tangent(v32, self.tan_image, skip=skip)
+        if getattr(net, "fisher_onepass", False) and net.fisher_onepass_applies(b.obs, b.n, self.tan_image):
+            # the whole product in one launch (JVP rows and VJP side by side per block)
+            timing.start("fvp_onepass")
+            net.fisher_product(b.obs, b.n, self.inv_ng, v32, self.tan_image, self.fv, skip=skip)
+            timing.stop("fvp_onepass")
+            return self.fv
         timing.start("fvp_jvp_rows")
         net.rows(_lib.EPI_FVP, b.obs, b.n, inv_n_global=self.inv_ng, ghead=self.ghead, tangent=v32,
                  image_t=self.tan_image, skip=skip)
@@ -275,6 +281,7 @@ class TrpoUpdater:
                 skipped = self.CG_ITERS - int(host[10])  # Fisher products after convergence
                 timing.drop_last("fvp_jvp_rows", skipped)
                 timing.drop_last("fvp_vjp", skipped)
+                timing.drop_last("fvp_onepass", skipped)
             fval = losses_before[0]
             trace = []
             if self.LS_BATCHES:

@@ -182,7 +182,7 @@ from modular_rl_amd import _lib
 lib = _lib.load()
 # every status-returning entry point with null buffers: an error status, no fault
 for name, (res, args) in _lib.SIGNATURES.items():
-    if name in ("mrl_last_error", "mrl_version", "mrl_stream_destroy"):
+    if name in ("mrl_last_error", "mrl_version", "mrl_stream_destroy", "mrl_mlp_fisher_hyb_fits"):
         continue
     r = getattr(lib, name)(*[None if a is ctypes.c_void_p else 0 for a in args])
     if res is ctypes.c_int:
@@ -196,7 +196,7 @@ for n_in in (1, 4, 11, 16, 17, 32, 33):
                     d = _lib.MlpDesc(n_in, n_out, head, hid, 2, cus)
                     b = ctypes.byref(d)
                     for f in ("mrl_mlp_num_params", "mrl_mlp_image_floats", "mrl_mlp_image_words_bf16",
-                              "mrl_mlp_image_words_split"):
+                              "mrl_mlp_image_words_split", "mrl_mlp_fisher_hyb_fits"):
                         getattr(lib, f)(b)
                     for n in (0, 1, 31, 33, 4194304, 1 << 31):
                         lib.mrl_mlp_partial_rows(b, n); lib.mrl_mlp_slab_rows(b, n)

@@ -2,10 +2,11 @@
 
 C3 (BASELINE configs[2]) runs the update over 4096 envs x 1024 steps = 4,194,304 Hopper
 rows (11-64-64-3 DiagGauss policy).  The golden and oracle tests elsewhere use 400 to
-70,001 rows; here the device path the headline runs -- split JVP rows + exact-f32 VJP,
+70,001 rows; here the device path the headline runs -- split JVP rows + hybrid VJP in one launch,
 per-wave slabs reduced over 4 M rows, device fp64 CG, batched line search -- is held to
 the float64 oracle at north_star's 1e-4 on exactly that row count: the policy gradient
-(`trpo.py:42-43`), one Fisher-vector product (`trpo.py:45-58`) and a whole
+(`trpo.py:42-43`), one Fisher-vector product (`trpo.py:45-58`: the one-pass kernel, the
+split pair and the exact-f32 pair) and a whole
 `TrpoUpdater.__call__` (`trpo.py:72-140`: k exact; lm, shs, the step, the six stats).
 The oracle is oracle/mlp_c.c (the numpy restatement's per-row math in C, pinned to it by
 tests/test_oracle_c.py) driven by trpo_np.trpo_update, so the CG / line-search control
@@ -72,12 +73,12 @@ def _net(b):
     return net
 
 
-@pytest.mark.parametrize("fisher", ["split", "f32"])
+@pytest.mark.parametrize("fisher", ["onepass", "split", "f32"])
 def test_fullsize_gradient_and_fisher_product(batch, fisher, monkeypatch):
     """g and one Fisher product F v over all 4,194,304 rows, each within 1e-4 (max error
-    relative to the vector's max) of the float64 oracle; both fp32 Fisher paths (the
-    default split JVP + exact-f32 VJP, and the exact-f32 pair)."""
-    monkeypatch.setenv("MRL_FISHER", fisher)
+    relative to the vector's max) of the float64 oracle; every fp32 Fisher path (the
+    default one-pass kernel, the split JVP rows + hybrid VJP pair, the exact-f32 pair)."""
+    monkeypatch.setenv("MRL_FISHER", "f32" if fisher == "f32" else "split")
     from modular_rl_amd import _lib
     b, spec = batch, batch["spec"]
     net = _net(b)
@@ -96,29 +97,41 @@ def test_fullsize_gradient_and_fisher_product(batch, fisher, monkeypatch):
     vt = _dev(v)
     imgt = net.new_tangent_image()
     net.pack_tangent(vt, imgt)
-    fgh = torch.full((N * net.gh,), float("nan"), device="cuda")
-    net.rows(_lib.EPI_FVP, b["x"], N, inv_n_global=1.0 / N, ghead=fgh, tangent=vt, image_t=imgt)
     fv = torch.zeros(net.P, device="cuda")
-    net.vjp_flat(b["x"], N, fgh, fv)
+    if fisher == "onepass":
+        assert net.fisher_product(b["x"], N, 1.0 / N, vt, imgt, fv)
+    else:
+        fgh = torch.full((N * net.gh,), float("nan"), device="cuda")
+        net.rows(_lib.EPI_FVP, b["x"], N, inv_n_global=1.0 / N, ghead=fgh, tangent=vt, image_t=imgt)
+        net.vjp_flat(b["x"], N, fgh, fv)
     fv_want = b["crows"].fvp(spec, b["th"], v.astype(np.float64))
     print(f"[fullsize] oracle g + Fv in {time.time() - t0:.1f} s", flush=True)
     assert _rel(fv.cpu().numpy().astype(np.float64), fv_want) < 1e-4
 
 
-def test_fullsize_trpo_update_matches_float64_oracle(batch):
+_ORACLE_UPDATE = {}
+
+
+@pytest.mark.parametrize("onepass", ["1", "0"])
+def test_fullsize_trpo_update_matches_float64_oracle(batch, onepass, monkeypatch):
     """One whole TrpoUpdater.update at 4,194,304 rows (the bench's cg_damping 0.1,
     max_kl 0.01): accepted backtrack k exactly; lm, shs, the expected improve rate and
-    the six loss stats within 1e-4 relative; theta within 1e-4 of the step."""
+    the six loss stats within 1e-4 relative; theta within 1e-4 of the step -- with the
+    one-pass Fisher product (default) and with the two-kernel pair."""
+    monkeypatch.setenv("MRL_FISHER_ONEPASS", onepass)
     from modular_rl_amd.collector import Batch
     from modular_rl_amd.core import StochPolicyMLP
     from modular_rl_amd.trpo import TrpoUpdater
     b, spec = batch, batch["spec"]
     t0 = time.time()
-    th_w, stats_w, diag_w = T.trpo_update(spec, b["th"], b["ob"], b["act"], b["adv"], b["oldprob"], cg_damping=0.1,
-                                          max_kl=0.01, rows=b["crows"])
+    if not _ORACLE_UPDATE:
+        _ORACLE_UPDATE["w"] = T.trpo_update(spec, b["th"], b["ob"], b["act"], b["adv"], b["oldprob"],
+                                            cg_damping=0.1, max_kl=0.01, rows=b["crows"])
+    th_w, stats_w, diag_w = _ORACLE_UPDATE["w"]
     print(f"[fullsize] oracle update in {time.time() - t0:.1f} s (k={diag_w['k']}, cg iters {diag_w['cg_iters']})",
           flush=True)
     pol = StochPolicyMLP(_net(b), b["pt"])
+    assert pol.net.fisher_onepass == (onepass == "1")
     up = TrpoUpdater(pol, dict(cg_damping=0.1, max_kl=0.01))
     bt = Batch(N, b["x"], b["a"], b["oldprobd"])
     bt.adv = b["advd"]
@@ -135,11 +148,11 @@ def test_fullsize_trpo_update_matches_float64_oracle(batch):
         np.testing.assert_allclose(stats[k], stats_w[k], rtol=1e-4, atol=1e-7, err_msg=k)
 
 
-@pytest.mark.parametrize("path", ["split", "f32", "bf16"])
+@pytest.mark.parametrize("path", ["onepass", "split", "f32", "bf16"])
 def test_fullsize_fisher_product_is_deterministic(batch, path, monkeypatch):
-    """The Fisher product's row and VJP kernels repeated on the same 4,194,304 rows give
-    the same bits every time (the split JVP rows once did not: DESIGN §3, the packed-f32
-    hazard), for the default split pair, the exact-f32 pair and the bf16 pair."""
+    """The Fisher product's kernels repeated on the same 4,194,304 rows give the same bits
+    every time (the split JVP rows once did not: DESIGN §3, the packed-f32 hazard), for
+    the one-pass kernel, the split pair, the exact-f32 pair and the bf16 pair."""
     monkeypatch.setenv("MRL_FISHER", "f32" if path == "f32" else "split")
     from modular_rl_amd import _lib
     from modular_rl_amd.nets import MlpNet
@@ -154,6 +167,14 @@ def test_fullsize_fisher_product_is_deterministic(batch, path, monkeypatch):
     imgt = net.new_tangent_image()
     net.pack_tangent(v, imgt)
     rows, fvs = [], []
+    if path == "onepass":
+        for _ in range(4):
+            f = torch.zeros(net.P, device="cuda")
+            assert net.fisher_product(b["x"], N, 1.0 / N, v, imgt, f)
+            fvs.append(f)
+        for f in fvs[1:]:
+            assert torch.equal(f, fvs[0])
+        return
     for _ in range(4):
         net.rows(_lib.EPI_FVP, b["x"], N, inv_n_global=1.0 / N, ghead=gh, tangent=v, image_t=imgt)
         rows.append(gh.clone())

@@ -189,3 +189,57 @@ def test_vjp16_hybrid_against_exact_f32_and_oracle(head, nin, nout, N):
     want = np.concatenate(parts)
     assert _rel(outs["hyb"], want) < 1e-4
     assert _rel(outs["f32"], want) < 1e-4
+
+
+@pytest.mark.parametrize("head,nin,nout", [("gauss", 11, 3), ("softmax", 4, 2)])
+@pytest.mark.parametrize("N", [1, 33, 3001, 70001])
+@pytest.mark.parametrize("cus", [0, 48])
+def test_onepass_fisher_product(head, nin, nout, N, cus, monkeypatch):
+    """mrl_mlp_fisher_hyb (JVP rows and hybrid VJP side by side in one launch, the head
+    rows through LDS) against the two-kernel pair on the same split tangent image (the same
+    per-row values, summed over another row partition: f32 rounding apart), against the
+    float64 oracle at 1e-4, and bit-identical run to run -- on the whole device and on a
+    48-CU subset (the grid and slab rows follow the net's CU count)."""
+    monkeypatch.setenv("MRL_FISHER", "split")
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import MlpNet
+    rng = np.random.default_rng(nin * 13 + N)
+    spec = T.Spec(nin, [64, 64], nout, head)
+    th = T.mlp_init(rng, spec.shapes, head == "gauss") + 0.05 * rng.standard_normal(spec.P)
+    if head == "gauss":
+        th[-nout:] = 0.3 * rng.standard_normal(nout)
+    th = th.astype(np.float32).astype(np.float64)
+    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
+    oldprob = T.policy_prob(spec, th + 0.01 * rng.standard_normal(spec.P), ob).astype(np.float32).astype(np.float64)
+    act = T.sample(spec, oldprob, rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N))
+    adv = rng.standard_normal(N).astype(np.float32).astype(np.float64)
+    v = rng.standard_normal(spec.P).astype(np.float32)
+    net = MlpNet(nin, nout, _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX)
+    assert net.fisher_onepass
+    net.set_flat(th)
+    if cus:
+        net.size_for_cus(cus)
+    x, vt = _dev(ob), _dev(v)
+    a = _dev(act, torch.int32 if head == "softmax" else torch.float32)
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    gh = torch.zeros(N * net.gh, dtype=torch.float32, device="cuda")
+    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(adv), oldprob=_dev(oldprob), ghead=gh,
+             partial=partial)
+    imgs = net.new_tangent_image()
+    net.pack_tangent(vt, imgs)
+    assert net.fisher_onepass_applies(x, N, imgs)
+    f1 = [torch.full((net.P,), float("nan"), dtype=torch.float32, device="cuda") for _ in range(3)]
+    for f in f1:
+        assert net.fisher_product(x, N, 1.0 / N, vt, imgs, f)
+    torch.cuda.synchronize()
+    for f in f1[1:]:
+        assert torch.equal(f, f1[0])
+    gh2 = torch.full_like(gh, float("nan"))
+    net.rows(_lib.EPI_FVP, x, N, inv_n_global=1.0 / N, ghead=gh2, tangent=vt, image_t=imgs)
+    f2 = torch.zeros(net.P, dtype=torch.float32, device="cuda")
+    net.vjp_flat(x, N, gh2, f2)
+    one, two = f1[0].cpu().numpy().astype(np.float64), f2.cpu().numpy().astype(np.float64)
+    assert np.isfinite(one).all()
+    assert _rel(one, two) < 1e-5
+    want = T.fisher_vector_product(spec, th, v.astype(np.float64), ob)
+    assert _rel(one, want) < 1e-4

@@ -14,6 +14,7 @@ import os
 
 # role -> kernel-name substring (first match wins, most specific first)
 ROLES = [
+    ("fvp_onepass", "mlp_fisher_hyb_kernel"),        # the one-pass Fisher product (round 5)
     ("fvp_jvp_rows_split", "mlp_fvp_split_kernel"),
     ("fvp_jvp_rows", "mlp_rows_kernel<100"),
     ("fvp_vjp", "mlp_vjp16_kernel<false, false"),  # the cached VJP (16-row kernel)
