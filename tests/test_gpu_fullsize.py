@@ -82,7 +82,7 @@ def test_fullsize_gradient_and_fisher_product(batch, fisher, monkeypatch):
     from modular_rl_amd import _lib
     b, spec = batch, batch["spec"]
     net = _net(b)
-    assert net.fisher_split == (fisher == "split")
+    assert net.fisher_split == (fisher != "f32")
     gh = torch.zeros(N * net.gh, device="cuda")
     partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
     net.rows(_lib.EPI_SURRGRAD, b["x"], N, inv_n_global=1.0 / N, act=b["a"], adv=b["advd"], oldprob=b["oldprobd"],

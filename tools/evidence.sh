@@ -9,6 +9,10 @@
 #   issue        SQ issue floor of the persistent rollout per bench line (tools/rollout_issue.py)
 #   stamps       per-phase stamps of the persistent Hopper rollout (tools/persistent_stamps.py)
 #   det          run-to-run determinism of the Fisher-product kernels (tools/det_locate.py)
+#   fisher       one Fisher product at 4.19 M rows: one-pass kernel vs the two-kernel pair
+#   fisher_tests the Fisher-product GPU tests only (split / one-pass / full size)
+#   gae          mrl_gae alone, the default build and every tools/gvar/*.so variant
+#   pair         the default bench line with the two-kernel Fisher product (MRL_FISHER_ONEPASS=0)
 # Every GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
 tag=${1:?tag}
@@ -68,6 +72,24 @@ for step in "$@"; do
       timeout -k 10 300 python -u tools/persistent_stamps.py Hopper-v2 > gpurun_out/${tag}_stamps.txt 2>&1 ||
         { tail -5 gpurun_out/${tag}_stamps.txt; exit 1; }
       grep -v amdgpu.ids gpurun_out/${tag}_stamps.txt | tail -20 ;;
+    fisher)
+      timeout -k 10 200 python -u tools/fisher_probe.py > gpurun_out/${tag}_fisher.log 2>&1 ||
+        { tail -5 gpurun_out/${tag}_fisher.log; exit 1; }
+      grep -v amdgpu.ids gpurun_out/${tag}_fisher.log ;;
+    fisher_tests)
+      timeout -k 10 900 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_fullsize.py -m gpu -x -q \
+        --timeout 300 --timeout-method thread > gpurun_out/${tag}_fisher_tests.log 2>&1 ||
+        { echo FISHER_TESTS_FAILED; tail -40 gpurun_out/${tag}_fisher_tests.log; exit 1; }
+      tail -1 gpurun_out/${tag}_fisher_tests.log ;;
+    gae)
+      for lib in default tools/gvar/*.so; do
+        if [ $lib = default ]; then unset MRL_LIB_PATH; else export MRL_LIB_PATH=$GRAFT_REPO_ROOT/$lib; fi
+        timeout -k 10 120 python -u tools/gae_probe.py >> gpurun_out/${tag}_gae.log 2>&1 ||
+          { tail -5 gpurun_out/${tag}_gae.log; exit 1; }
+      done
+      unset MRL_LIB_PATH
+      grep -v amdgpu.ids gpurun_out/${tag}_gae.log ;;
+    pair) MRL_FISHER_ONEPASS=0 bench pair 400 --no-cpu-baseline ;;
     det)
       REPS=8 timeout -k 10 200 python -u tools/det_locate.py > gpurun_out/${tag}_det.log 2>&1 ||
         { tail -5 gpurun_out/${tag}_det.log; exit 1; }
