@@ -174,6 +174,13 @@ int mrl_mlp_fvp_split(const mrl_mlp_desc* d, const float* theta, const float* im
  * mrl_reduce_rows_f32.  image: the f32 image (its W1 / W2 fragments); image_s / image_t_s:
  * split images of theta and of the tangent.  E_UNSUPPORTED unless
  * mrl_mlp_fisher_hyb_fits(d) (policy nets of <= 15 inputs; the split images fit LDS). */
+/* The forward row passes PROB / LOSSES / SURRGRAD / VFLOSS of mrl_mlp_rows (same io, same
+ * grid and partial rows, MRL_CACHE_WRITE stores the same activation-cache layout) on the
+ * split image of theta (mrl_mlp_pack_split): both layers as six bf16 part products, f32
+ * accumulation -- the f32 kernel's per-row values to f32 rounding (core.py:261-270,
+ * 611-617, 648-650; trpo.py:42-43, 60-64). */
+int mrl_mlp_rows_split(const mrl_mlp_desc* d, int32_t epi, const float* theta, const float* image_s,
+                       const mrl_rows_io* io, const int32_t* skip, void* stream);
 int32_t mrl_mlp_fisher_hyb_fits(const mrl_mlp_desc* d);
 int mrl_mlp_fisher_hyb(const mrl_mlp_desc* d, const float* theta, const float* image, const float* image_s,
                        const float* tangent, const float* image_t_s, const mrl_rows_io* io, float* slab,
@@ -197,6 +204,7 @@ int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* 
  * bf16 is the throughput mode: operands rounded to bf16 RNE, f32 accumulation) */
 #define MRL_COMPUTE_F32 0
 #define MRL_COMPUTE_BF16 1
+#define MRL_COMPUTE_SPLIT 2 /* fp32 on split bf16 operands (mrl_mlp_rows_split; mrl_linesearch_eval) */
 #define MRL_GEMM_SLAB 3   /* c + z*slab_stride = sum over K-split z of AB  (weight grads) */
 
 typedef struct {

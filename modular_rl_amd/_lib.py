@@ -19,7 +19,7 @@ EPI_PROB, EPI_LOSSES, EPI_SURRGRAD, EPI_VFLOSS, EPI_FVP, EPI_PPOGRAD, EPI_PPOSGD
 PPO_BLOCK_ROWS = 128
 ENV_CARTPOLE, ENV_HOPPER, ENV_HUMANOID = 0, 1, 2
 GEMM_STORE, GEMM_TANH, GEMM_DTANH, GEMM_SLAB = 0, 1, 2, 3
-COMPUTE_F32, COMPUTE_BF16 = 0, 1
+COMPUTE_F32, COMPUTE_BF16, COMPUTE_SPLIT = 0, 1, 2
 COMPUTE = {"fp32": COMPUTE_F32, "bf16": COMPUTE_BF16}
 
 vp = ctypes.c_void_p
@@ -99,6 +99,7 @@ SIGNATURES = {
     "mrl_mlp_image_words_split": (i64, [vp]),
     "mrl_mlp_pack_split": (i32, [vp, vp, vp, vp, vp]),
     "mrl_mlp_fisher_hyb_fits": (i32, [vp]),
+    "mrl_mlp_rows_split": (i32, [vp, i32, vp, vp, vp, vp, vp]),
     "mrl_mlp_fisher_hyb": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_mlp_fvp_split": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_reduce_rows_f32": (i32, [vp, i64, i64, vp, vp, vp]),

@@ -192,4 +192,8 @@ struct JvpSplitRole {
   }
 };
 
+// launch mlp_rows_split_kernel<epi, sh> (mlp_split.hip) for mrl_mlp_rows_split
+int launch_rows_split(int epi, int sh, const RowsArgs& a, const BDims& b, const float* image_s, int64_t blocks,
+                      const int32_t* skip, void* stream);
+
 }  // namespace mrl

@@ -182,6 +182,24 @@ __device__ inline void split4(const f32x4& v, bf16x4* p) {
 __device__ inline bf16x8 cat4(const bf16x4& lo, const bf16x4& hi) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
+// The three parts of four values laid out [p0 | p1 | p2 | p0] (8 registers): its 8-element
+// windows at 0 (p0, p1) and 8 (p2, p0) are K-stacked operands of a 16x16x32 product whose
+// K is 4 rows x 2 parts, so the six part products i + j <= 2 of two such operands h, g take
+// three MFMAs on register windows, no operand copies:
+//   W8(h) W0(g) = h2 g0 + h0 g1,   W0(h) W8(g) = h0 g2 + h1 g0,   W0(h) W0(g) = h0 g0 + h1 g1
+typedef __bf16 bf16x16 __attribute__((ext_vector_type(16)));
+__device__ inline bf16x16 split4w(const f32x4& v) {
+  bf16x2 a0, c0, e0, a1, c1, e1;
+  split2(f32x2{v[0], v[1]}, a0, c0, e0);
+  split2(f32x2{v[2], v[3]}, a1, c1, e1);
+  const bf16x4 p0 = __builtin_shufflevector(a0, a1, 0, 1, 2, 3);
+  const bf16x4 p1 = __builtin_shufflevector(c0, c1, 0, 1, 2, 3);
+  const bf16x4 p2 = __builtin_shufflevector(e0, e1, 0, 1, 2, 3);
+  return __builtin_shufflevector(cat4(p0, p1), cat4(p2, p0), 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14,
+                                 15);
+}
+__device__ inline bf16x8 W0(const bf16x16& w) { return __builtin_shufflevector(w, w, 0, 1, 2, 3, 4, 5, 6, 7); }
+__device__ inline bf16x8 W8(const bf16x16& w) { return __builtin_shufflevector(w, w, 8, 9, 10, 11, 12, 13, 14, 15); }
 
 // tanh' from the activation, 1 - h^2, as one explicit fma (see tanh_fast)
 __device__ inline float dtanh(float h) { return fmaf(-h, h, 1.f); }

@@ -880,7 +880,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
     if constexpr (HYB) {
       // gW1 += h1_T^T ga2_T first (ga2_T's registers are free after it): K = 16 rows, two
       // part products per MFMA
-      {
+      if constexpr (EPT) {  // the VF net's form (the window layout below spills there)
         bf16x4 gp[4][3];
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) split4(ga2T[nt], gp[nt]);
@@ -894,6 +894,20 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
             gW1[mt][nt] = MFMAB16(H21, cat4(gp[nt][0], gp[nt][1]), gW1[mt][nt]);  // h2 g0 + h1 g1
             gW1[mt][nt] = MFMAB16(H01, cat4(gp[nt][2], gp[nt][0]), gW1[mt][nt]);  // h0 g2 + h1 g0
             gW1[mt][nt] = MFMAB16(H00, cat4(gp[nt][1], gp[nt][0]), gW1[mt][nt]);  // h0 g1 + h0 g0
+          }
+        }
+      } else {
+        bf16x16 gw[4];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) gw[nt] = split4w(ga2T[nt]);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const bf16x16 hw = split4w(h1T[mt]);
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            gW1[mt][nt] = MFMAB16(W8(hw), W0(gw[nt]), gW1[mt][nt]);  // h2 g0 + h0 g1
+            gW1[mt][nt] = MFMAB16(W0(hw), W8(gw[nt]), gW1[mt][nt]);  // h0 g2 + h1 g0
+            gW1[mt][nt] = MFMAB16(W0(hw), W0(gw[nt]), gW1[mt][nt]);  // h0 g0 + h1 g1
           }
         }
       }
@@ -1349,19 +1363,17 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
       // gW1 += h1_T^T ga2_T first (ga2_T's registers are free after it): K = 16 rows, two
       // part products per MFMA
       {
-        bf16x4 gp[4][3];
+        bf16x16 gw[4];
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) split4(ga2T[nt], gp[nt]);
+        for (int nt = 0; nt < 4; ++nt) gw[nt] = split4w(ga2T[nt]);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
-          bf16x4 hp[3];
-          split4(h1T[mt], hp);
-          const bf16x8 H21 = cat4(hp[2], hp[1]), H01 = cat4(hp[0], hp[1]), H00 = cat4(hp[0], hp[0]);
+          const bf16x16 hw = split4w(h1T[mt]);
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
-            gW1[mt][nt] = MFMAB16(H21, cat4(gp[nt][0], gp[nt][1]), gW1[mt][nt]);  // h2 g0 + h1 g1
-            gW1[mt][nt] = MFMAB16(H01, cat4(gp[nt][2], gp[nt][0]), gW1[mt][nt]);  // h0 g2 + h1 g0
-            gW1[mt][nt] = MFMAB16(H00, cat4(gp[nt][1], gp[nt][0]), gW1[mt][nt]);  // h0 g1 + h0 g0
+            gW1[mt][nt] = MFMAB16(W8(hw), W0(gw[nt]), gW1[mt][nt]);  // h2 g0 + h0 g1
+            gW1[mt][nt] = MFMAB16(W0(hw), W8(gw[nt]), gW1[mt][nt]);  // h0 g2 + h1 g0
+            gW1[mt][nt] = MFMAB16(W0(hw), W0(gw[nt]), gW1[mt][nt]);  // h0 g0 + h1 g1
           }
         }
       }
@@ -1678,13 +1690,14 @@ int mrl_mlp_pack(const mrl_mlp_desc* d, const float* theta, float* image, int32_
   return hip_check(hipGetLastError(), "mrl_mlp_pack");
 }
 
-int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const float* image, const float* tangent,
-                 const float* image_t, const mrl_rows_io* io, const int32_t* skip, void* stream) {
+// the RowsArgs of one row pass and the argument checks of its epilogue (mrl_mlp_rows,
+// mrl_mlp_rows_split); 1 = nothing to do (n <= 0)
+static int rows_args(const mrl_mlp_desc* d, int32_t epi, const float* theta, const float* image, const float* tangent,
+                     const float* image_t, const mrl_rows_io* io, RowsArgs& a) {
   int rc = check_desc(d);
   if (rc) return rc;
   if (!io || !image || !io->x) return fail(E_ARG, "null pointer");
-  if (io->n <= 0) return OK;
-  RowsArgs a;
+  if (io->n <= 0) return 1;
   a.d = dims_of(d);
   a.head = d->head;
   a.n_obs = d->n_in - (io->ep_t ? 1 : 0);
@@ -1742,6 +1755,14 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
     default:
       return fail(E_ARG, "unknown epilogue");
   }
+  return OK;
+}
+
+int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const float* image, const float* tangent,
+                 const float* image_t, const mrl_rows_io* io, const int32_t* skip, void* stream) {
+  RowsArgs a;
+  int rc = rows_args(d, epi, theta, image, tangent, image_t, io, a);
+  if (rc) return rc > 0 ? OK : rc;
   // cus sizes the passes whose sums follow the grid (per-wave partials); the others
   // (forward / PROB / FVP rows) keep the device-wide grid wherever they run
   const int64_t blocks = rows_blocks(io->n, io->partial != nullptr ? desc_cus(d) : 256);
@@ -1776,6 +1797,21 @@ int mrl_mlp_rows(const mrl_mlp_desc* d, int32_t epi, const float* theta, const f
   }
 #undef MRL_ROWS_LAUNCH
   return hip_check(hipGetLastError(), "mrl_mlp_rows");
+}
+
+int mrl_mlp_rows_split(const mrl_mlp_desc* d, int32_t epi, const float* theta, const float* image_s,
+                       const mrl_rows_io* io, const int32_t* skip, void* stream) {
+  if (epi != MRL_EPI_PROB && epi != MRL_EPI_LOSSES && epi != MRL_EPI_SURRGRAD && epi != MRL_EPI_VFLOSS)
+    return fail(E_UNSUPPORTED, "mrl_mlp_rows_split: PROB, LOSSES, SURRGRAD or VFLOSS");
+  if (d != nullptr && (d->n_in > MAX_IN || d->n_out > MAX_OUT || d->n_hidden != HID || d->n_layers != 2))
+    return fail(E_UNSUPPORTED, "mrl_mlp_rows_split: the 64-wide fused shape only");
+  RowsArgs a;
+  int rc = rows_args(d, epi, theta, image_s, nullptr, nullptr, io, a);
+  if (rc) return rc > 0 ? OK : rc;
+  // the grid (and so the partial rows) of mrl_mlp_rows: mrl_mlp_partial_rows holds for both
+  const int64_t blocks = rows_blocks(io->n, io->partial != nullptr ? desc_cus(d) : 256);
+  const int sh = static_shape_of(d, io->ep_t != nullptr, epi == MRL_EPI_PROB);
+  return launch_rows_split(epi, sh, a, bf16_dims(d->n_in, d->n_out), image_s, blocks, skip, stream);
 }
 
 int mrl_mlp_vjp(const mrl_mlp_desc* d, const float* image, const float* x, const int32_t* ep_t, double ts_limit,
@@ -1936,10 +1972,11 @@ int mrl_linesearch_eval(const mrl_mlp_desc* pol, int32_t compute, const float* t
   int rc = check_desc(pol);
   if (rc) return rc;
   if (!io || !cand || !images || !partials || !out) return fail(E_ARG, "mrl_linesearch_eval: null pointer");
-  if (compute != MRL_COMPUTE_F32 && compute != MRL_COMPUTE_BF16) return fail(E_ARG, "bad compute");
-  const bool bf = compute == MRL_COMPUTE_BF16;
+  if (compute != MRL_COMPUTE_F32 && compute != MRL_COMPUTE_BF16 && compute != MRL_COMPUTE_SPLIT)
+    return fail(E_ARG, "bad compute");
+  const bool bf = compute == MRL_COMPUTE_BF16, sp = compute == MRL_COMPUTE_SPLIT;
   const int64_t P = mrl_mlp_num_params(pol);
-  const int64_t img = bf ? mrl_mlp_image_words_bf16(pol) : mrl_mlp_image_floats(pol);
+  const int64_t img = bf ? mrl_mlp_image_words_bf16(pol) : sp ? mrl_mlp_image_words_split(pol) : mrl_mlp_image_floats(pol);
   // the LOSSES pass sizes its grid (and so its partial rows) by the desc's CU count
   const int64_t prow = bf ? mrl_mlp_partial_rows_bf16(pol, io->n) : mrl_mlp_partial_rows(pol, io->n);
   if (image_stride < img || partial_stride < prow * 4) return fail(E_ARG, "mrl_linesearch_eval: strides too small");
@@ -1951,10 +1988,12 @@ int mrl_linesearch_eval(const mrl_mlp_desc* pol, int32_t compute, const float* t
     iok.partial = partials + (int64_t)k * partial_stride;
     iok.cache_mode = MRL_CACHE_NONE;
     iok.act_cache = nullptr;
-    rc = bf ? mrl_mlp_pack_bf16(pol, th, im, 1, nullptr, stream) : mrl_mlp_pack(pol, th, im, 1, nullptr, stream);
+    rc = bf ? mrl_mlp_pack_bf16(pol, th, im, 1, nullptr, stream)
+            : sp ? mrl_mlp_pack_split(pol, th, im, nullptr, stream) : mrl_mlp_pack(pol, th, im, 1, nullptr, stream);
     if (rc == OK)
       rc = bf ? mrl_mlp_rows_bf16(pol, MRL_EPI_LOSSES, th, im, nullptr, nullptr, &iok, nullptr, stream)
-              : mrl_mlp_rows(pol, MRL_EPI_LOSSES, th, im, nullptr, nullptr, &iok, nullptr, stream);
+            : sp ? mrl_mlp_rows_split(pol, MRL_EPI_LOSSES, th, im, &iok, nullptr, stream)
+                 : mrl_mlp_rows(pol, MRL_EPI_LOSSES, th, im, nullptr, nullptr, &iok, nullptr, stream);
     if (rc == OK) rc = mrl_reduce_rows_f64(iok.partial, prow, 4, out + 4 * (int64_t)k, nullptr, stream);
   }
   return rc;

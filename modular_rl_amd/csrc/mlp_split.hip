@@ -127,6 +127,158 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, (4 * MRL_SPLIT_FVP_OCC / SPLIT_RO
   (void)acc2;
 }
 
+
+// ------------------------------------------------------------------ forward rows
+// The primal row passes of the fp32 update -- TRPO losses and surrogate-gradient rows
+// (trpo.py:42-43, 60-64), the value prediction and the VF loss rows (core.py:611-617,
+// 648-650) -- on the same split operands: layer 0 and layer 1 as six bf16 part products
+// each, f32 accumulation, tanh and the A-output head on the f32 VALU.  Same per-row values
+// as mlp_rows_kernel<EPI> to f32 rounding (the products are exact, the summation order
+// differs); the activation cache it writes (SURRGRAD / VFLOSS, MRL_CACHE_WRITE) has the
+// f32 kernel's layout, so the Fisher products and VJPs read it unchanged.
+template <int SH>
+__device__ inline void split_rows_shape(RowsArgs& a, BDims& b) {
+  if constexpr ((SH & ~SH_TIME) != 0) {
+    constexpr int B = SH & ~SH_TIME;
+    constexpr StaticShape S = STATIC_SHAPES[B];
+    a.d = static_dims(B);
+    a.A = S.A;
+    a.head = S.head;
+    a.n_obs = (SH & SH_TIME) ? S.O - 1 : S.O;
+    a.gh = S.head == MRL_HEAD_GAUSS ? 2 * S.A : S.A;
+    if constexpr (!(SH & SH_TIME)) a.ept = nullptr;
+    b = bf16_dims(S.O, S.A);
+  }
+}
+
+template <int EPI, int SH>
+__global__ __launch_bounds__(SPLIT_ROWS_BLOCK, 2) void mlp_rows_split_kernel(RowsArgs a, BDims b,
+                                                                            const float* __restrict__ img_g,
+                                                                            const int32_t* __restrict__ skip) {
+  split_rows_shape<SH>(a, b);
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (skip != nullptr && *skip != 0) return;
+  const int W = split_fwd_words(b), PS = split_fw(b);
+  for (int i = threadIdx.x; i < W / 4; i += SPLIT_ROWS_BLOCK)
+    reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img_g)[i];
+  __syncthreads();
+  const float* img = lds;
+  const MlpDims dd = head_dims(a.d, b);
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int A = a.A;
+  float ls[MAX_OUT], sd[MAX_OUT], dls[MAX_OUT];
+#pragma unroll
+  for (int j = 0; j < MAX_OUT; ++j) {
+    ls[j] = (a.logstd != nullptr && j < A) ? a.logstd[j] : 0.f;
+    sd[j] = expf(ls[j]);
+    dls[j] = 0.f;
+  }
+  const bool store = a.cache != nullptr && a.cache_mode == MRL_CACHE_WRITE;
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+  const int64_t ntiles = (a.n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * SPLIT_ROWS_WAVES + wave; tile < ntiles;
+       tile += (int64_t)gridDim.x * SPLIT_ROWS_WAVES) {
+    const int64_t row = tile * 32 + (lane & 31);
+    const bool valid = row < a.n;
+    XGlobalNB xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
+    float* ct = store ? a.cache + tile * CACHE_TILE_FLOATS : nullptr;
+    // layer 0: h1 = tanh(x W0 + b0)
+    f32x16 h1[2] = {load_bias16(img, b.fb0, 0, h), load_bias16(img, b.fb0, 1, h)};
+#pragma unroll
+    for (int s0 = 0; s0 < MAX_KS0B; ++s0) {
+      if (s0 < b.KS0B) {
+        float xv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = xl(16 * s0 + 8 * h + j);
+        bf16x8 xs[3];
+        split8v(xv, xs);
+        mfma_split(img, b.fa0, PS, 0 * b.KS0B + s0, lane, xs, h1[0]);
+        mfma_split(img, b.fa0, PS, 1 * b.KS0B + s0, lane, xs, h1[1]);
+      }
+    }
+    tanh16(h1[0]);
+    tanh16(h1[1]);
+    if (store) {
+      cache_store(ct, lane, 0, h1[0]);
+      cache_store(ct, lane, 1, h1[1]);
+    }
+    // layer 1: h2 = tanh(h1 W1 + b1), each input fragment split once for both output tiles
+    f32x16 a2[2] = {load_bias16(img, b.fb1, 0, h), load_bias16(img, b.fb1, 1, h)};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 ps[3];
+      split8(h1[s >> 1], s & 1, ps);
+      mfma_split(img, b.fa1, PS, 0 * 4 + s, lane, ps, a2[0]);
+      mfma_split(img, b.fa1, PS, 1 * 4 + s, lane, ps, a2[1]);
+    }
+    FVP_SPLIT_FENCE();
+    float z[MAX_OUT], dz[MAX_OUT];
+#pragma unroll
+    for (int o = 0; o < MAX_OUT; ++o) z[o] = dz[o] = 0.f;
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo) {
+      tanh16(a2[mo]);
+      if (store) cache_store(ct, lane, 2 + mo, a2[mo]);
+      head_partial_mt(img, dd, a2[mo], mo, h, z);
+    }
+    head_finish(img, dd, z);
+    if constexpr (EPI == MRL_EPI_PROB)
+      if (a.feat != nullptr && valid) write_feature_row(a, row, h, xl);
+    if (valid && h == 0) row_epilogue<EPI, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+  }
+  if (a.partial != nullptr) {
+    acc0 = wave_sum(acc0);
+    acc1 = wave_sum(acc1);
+    acc2 = wave_sum(acc2);
+    if (lane == 0) {
+      double* p = a.partial + ((int64_t)blockIdx.x * SPLIT_ROWS_WAVES + wave) * 4;
+      p[0] = acc0;
+      p[1] = acc1;
+      p[2] = acc2;
+      p[3] = 0.0;
+    }
+  }
+}
+
+int launch_rows_split(int epi, int sh, const RowsArgs& a, const BDims& b, const float* image_s, int64_t blocks,
+                      const int32_t* skip, void* stream) {
+  const dim3 grid(blocks), blk(SPLIT_ROWS_BLOCK);
+  const size_t shm = (size_t)split_fwd_words(b) * 4;
+  hipStream_t s = (hipStream_t)stream;
+#define MRL_RS(E, S) hipLaunchKernelGGL((mlp_rows_split_kernel<E, S>), grid, blk, shm, s, a, b, image_s, skip)
+  switch (epi) {
+    case MRL_EPI_PROB:
+      if (sh == 1) MRL_RS(MRL_EPI_PROB, 1);
+      else if (sh == 2) MRL_RS(MRL_EPI_PROB, 2);
+      else if (sh == 3) MRL_RS(MRL_EPI_PROB, 3);
+      else if (sh == 4) MRL_RS(MRL_EPI_PROB, 4);
+      else if (sh == (3 | SH_TIME)) MRL_RS(MRL_EPI_PROB, 3 | SH_TIME);
+      else if (sh == (4 | SH_TIME)) MRL_RS(MRL_EPI_PROB, 4 | SH_TIME);
+      else MRL_RS(MRL_EPI_PROB, 0);
+      break;
+    case MRL_EPI_LOSSES:
+      if (sh == 1) MRL_RS(MRL_EPI_LOSSES, 1);
+      else if (sh == 2) MRL_RS(MRL_EPI_LOSSES, 2);
+      else MRL_RS(MRL_EPI_LOSSES, 0);
+      break;
+    case MRL_EPI_SURRGRAD:
+      if (sh == 1) MRL_RS(MRL_EPI_SURRGRAD, 1);
+      else if (sh == 2) MRL_RS(MRL_EPI_SURRGRAD, 2);
+      else MRL_RS(MRL_EPI_SURRGRAD, 0);
+      break;
+    case MRL_EPI_VFLOSS:
+      if (sh == 3) MRL_RS(MRL_EPI_VFLOSS, 3);
+      else if (sh == 4) MRL_RS(MRL_EPI_VFLOSS, 4);
+      else MRL_RS(MRL_EPI_VFLOSS, 0);
+      break;
+    default:
+      return fail(E_UNSUPPORTED, "mrl_mlp_rows_split: epilogue");
+  }
+#undef MRL_RS
+  return hip_check(hipGetLastError(), "mrl_mlp_rows_split");
+}
+
 }  // namespace mrl
 
 using namespace mrl;

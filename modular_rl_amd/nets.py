@@ -99,6 +99,9 @@ class Workspace:
         return t[:numel]
 
 
+_SPLIT_ROWS_EPIS = (_lib.EPI_PROB, _lib.EPI_LOSSES, _lib.EPI_SURRGRAD, _lib.EPI_VFLOSS)
+
+
 class MlpNet:
     """tanh MLP n_in -> 64 -> 64 -> n_out with a linear / softmax / DiagGauss head."""
 
@@ -135,6 +138,9 @@ class MlpNet:
         # it; MRL_FISHER_ONEPASS=0: the split JVP rows + hybrid VJP pair
         self.fisher_onepass = (self.fisher_split and os.environ.get("MRL_FISHER_ONEPASS", "1") != "0"
                                and bool(self.lib.mrl_mlp_fisher_hyb_fits(ctypes.byref(self.desc))))
+        # the forward row passes (PROB / LOSSES / SURRGRAD / VFLOSS) of the net's own theta
+        # on the same split operands (mrl_mlp_rows_split); MRL_ROWS_SPLIT=0: exact-f32 kernel
+        self.rows_split = self.fisher_split and os.environ.get("MRL_ROWS_SPLIT", "1") != "0"
         self.image_s = None
         if self.fisher_split:
             w = int(self.lib.mrl_mlp_image_words_split(ctypes.byref(self.desc)))
@@ -207,6 +213,10 @@ class MlpNet:
         io = _lib.RowsIO(ptr(x), ptr(ep_t), float(timestep_limit), int(n), float(inv_n_global), ptr(act), ptr(adv),
                          ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial), float(kl_coeff),
                          float(kl_cutoff), float(cutoff_coeff), int(reverse_kl), mode, ptr(cache), ptr(feat_out))
+        if self.rows_split and own and epi in _SPLIT_ROWS_EPIS:
+            call("mrl_mlp_rows_split", ctypes.byref(self.desc), int(epi), ptr(theta), ptr(self.image_s),
+                 ctypes.byref(io), ptr(skip), stream())
+            return
         call("mrl_mlp_rows" + self._sfx, ctypes.byref(self.desc), int(epi), ptr(theta), ptr(image), ptr(tangent),
              ptr(image_t), ctypes.byref(io), ptr(skip), stream())
 

@@ -135,7 +135,8 @@ class HipTrpoOps:
         if self._ls is None or self._ls[0] < K or self._ls[3].shape[1] < prow:
             Kc = max(K, self._ls[0] if self._ls is not None else 0)
             dev = net.device
-            imgs = (torch.zeros(Kc, net.image.numel(), dtype=torch.float32, device=dev)
+            iw = max(net.image.numel(), net.image_s.numel() if getattr(net, "rows_split", False) else 0)
+            imgs = (torch.zeros(Kc, iw, dtype=torch.float32, device=dev)
                     if not getattr(net, "layered", False) else None)
             self._ls = (Kc, torch.zeros(Kc, self.P, dtype=torch.float32, device=dev), imgs,
                         torch.zeros(Kc, prow, dtype=torch.float64, device=dev),
@@ -151,7 +152,8 @@ class HipTrpoOps:
         if not getattr(net, "layered", False):
             io = _lib.RowsIO(ptr(b.obs), None, 1.0, int(b.n), float(self.inv_ng), ptr(b.act), ptr(b.adv), ptr(b.prob),
                              None, None, None, None, 0.0, 0.0, 0.0, 0, _lib.CACHE_NONE, None)
-            call("mrl_linesearch_eval", ctypes.byref(net.desc), _lib.COMPUTE[net.dtype], ptr(theta_old),
+            compute = _lib.COMPUTE_SPLIT if getattr(net, "rows_split", False) else _lib.COMPUTE[net.dtype]
+            call("mrl_linesearch_eval", ctypes.byref(net.desc), compute, ptr(theta_old),
                  ptr(self.fullstep), int(k0), int(K), ctypes.byref(io), ptr(cand), ptr(imgs), int(imgs.shape[1]),
                  ptr(partials), int(partials.shape[1]), ptr(sums), stream())
         else:

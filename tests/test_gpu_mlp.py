@@ -138,13 +138,16 @@ def test_value_forward_and_loss_grad_with_time_feature(nin, cus):
 
 
 @pytest.mark.parametrize("head,nin,nout", [("gauss", 11, 3), ("softmax", 4, 2)])
-def test_activation_cache_is_bitwise_transparent(head, nin, nout):
+def test_activation_cache_is_bitwise_transparent(head, nin, nout, monkeypatch):
     """SURRGRAD stores h1/h2; the FVP rows pass that follows reads them instead of
-    recomputing the forward -- its head rows must equal the uncached kernel's bit for bit.
+    recomputing the forward -- its head rows must equal the uncached kernel's bit for bit
+    (the exact-f32 row kernels: MRL_ROWS_SPLIT=0; the split forward's cache holds its own
+    rounding, tests/test_gpu_split.py).
     The cached VJP is the transpose-free 16-row kernel (mlp_vjp16_kernel): the same sums
     in another row order, so its gradients agree with the uncached 32-row kernel to fp32
     rounding and both with the float64 oracle."""
     from modular_rl_amd import _lib
+    monkeypatch.setenv("MRL_ROWS_SPLIT", "0")
     N = 3000
     spec, th, ob, act, adv, oldprob = _setup(head, nin, nout, N, seed=9)
     v = np.random.default_rng(2).standard_normal(spec.P).astype(np.float32)

@@ -243,3 +243,117 @@ def test_onepass_fisher_product(head, nin, nout, N, cus, monkeypatch):
     assert _rel(one, two) < 1e-5
     want = T.fisher_vector_product(spec, th, v.astype(np.float64), ob)
     assert _rel(one, want) < 1e-4
+
+
+def _rows_pair(monkeypatch, head, nin, nout, th, build):
+    """build(net) on a split-forward net and on an exact-f32 one (MRL_ROWS_SPLIT=0)."""
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import MlpNet
+    kind = {"gauss": _lib.HEAD_GAUSS, "softmax": _lib.HEAD_SOFTMAX, "linear": _lib.HEAD_LINEAR}[head]
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("MRL_ROWS_SPLIT", flag)
+        net = MlpNet(nin, nout, kind)
+        assert net.rows_split == (flag == "1")
+        net.set_flat(th)
+        out.append(build(net))
+    return out
+
+
+@pytest.mark.parametrize("head,nin,nout", CASES)
+@pytest.mark.parametrize("N", [1, 33, 3001, 70001])
+def test_split_forward_rows(head, nin, nout, N, monkeypatch):
+    """mrl_mlp_rows_split (the forward row passes on split bf16 operands) against the
+    exact-f32 row kernel (per-row values to f32 rounding: rows 2e-5, loss sums 1e-6, the
+    activation cache it writes 2e-6 absolute on tanh outputs) and against the float64
+    oracle at 1e-4: prob rows, the TRPO losses, the surrogate-gradient rows and the policy
+    gradient from the cache they wrote."""
+    monkeypatch.setenv("MRL_FISHER", "split")
+    from modular_rl_amd import _lib
+    rng = np.random.default_rng(nin * 3 + N)
+    spec = T.Spec(nin, [64, 64], nout, head)
+    th = T.mlp_init(rng, spec.shapes, head == "gauss") + 0.05 * rng.standard_normal(spec.P)
+    if head == "gauss":
+        th[-nout:] = 0.3 * rng.standard_normal(nout)
+    th = th.astype(np.float32).astype(np.float64)
+    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
+    oldprob = T.policy_prob(spec, th + 0.01 * rng.standard_normal(spec.P), ob).astype(np.float32).astype(np.float64)
+    act = T.sample(spec, oldprob, rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N))
+    if head == "gauss":
+        act = act.astype(np.float32).astype(np.float64)
+    adv = rng.standard_normal(N).astype(np.float32).astype(np.float64)
+    x, a = _dev(ob), _dev(act, torch.int32 if head == "softmax" else torch.float32)
+
+    def build(net):
+        prob = net.forward(x, N).clone()
+        partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+        gh = torch.full((N * net.gh,), float("nan"), device="cuda")
+        net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(adv), oldprob=_dev(oldprob),
+                 ghead=gh, partial=partial)
+        sums = torch.zeros(4, dtype=torch.float64, device="cuda")
+        net.reduce_partial(partial, N, sums)
+        cache = net._cache(N)[: ((N + 31) // 32) * 64 * 64].clone()
+        g = torch.zeros(net.P, device="cuda")
+        net.vjp_flat(x, N, gh, g)
+        lp = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+        net.rows(_lib.EPI_LOSSES, x, N, inv_n_global=1.0 / N, act=a, adv=_dev(adv), oldprob=_dev(oldprob),
+                 partial=lp)
+        ls = torch.zeros(4, dtype=torch.float64, device="cuda")
+        net.reduce_partial(lp, N, ls)
+        return [t.cpu().numpy().astype(np.float64) for t in (prob, gh, sums, cache, g, ls)]
+
+    (p1, gh1, s1, c1, g1, l1), (p0, gh0, s0, c0, g0, l0) = _rows_pair(monkeypatch, head, nin, nout, th, build)
+    np.testing.assert_allclose(p1, p0, rtol=2e-5, atol=2e-6 * np.abs(p0).max())
+    np.testing.assert_allclose(gh1, gh0, rtol=2e-5, atol=2e-6 * np.abs(gh0).max())
+    np.testing.assert_allclose(s1[:3], s0[:3], rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(l1[:3], s1[:3], rtol=1e-12, atol=0)  # LOSSES == SURRGRAD's sums
+    assert np.abs(c1 - c0).max() < 2e-6
+    assert _rel(g1, g0) < 1e-5
+    np.testing.assert_allclose(p1, T.policy_prob(spec, th, ob), rtol=2e-5, atol=2e-6)
+    want = T.surr_kl_ent(spec, th, ob, act, adv, oldprob)
+    np.testing.assert_allclose(np.array([-s1[0] / N, s1[1] / N, s1[2] / N]), want, rtol=1e-4, atol=1e-6)
+    assert _rel(g1, T.policy_gradient(spec, th, ob, act, adv, oldprob)) < 1e-4
+
+
+@pytest.mark.parametrize("nin", [5, 12])
+@pytest.mark.parametrize("N", [1, 1500, 70001])
+def test_split_forward_value_rows(nin, N, monkeypatch):
+    """The value net's passes on split operands: the prediction with the time feature
+    (and the feature rows it writes) and the VF loss / gradient rows, against the exact-f32
+    kernel and the float64 oracle (core.py:611-617, 648-660)."""
+    monkeypatch.setenv("MRL_FISHER", "split")
+    from modular_rl_amd import _lib
+    limit = 200.0
+    rng = np.random.default_rng(nin + N)
+    spec = T.Spec(nin, [64, 64], 1, "linear")
+    th = (T.mlp_init(rng, spec.shapes, False) + 0.05 * rng.standard_normal(spec.P)).astype(np.float32).astype(np.float64)
+    obs = rng.standard_normal((N, nin - 1)).astype(np.float32)
+    ept = rng.integers(0, 200, size=N).astype(np.int32)
+    X = np.concatenate([obs.astype(np.float64), (ept / limit).astype(np.float32).astype(np.float64)[:, None]], axis=1)
+    y = rng.standard_normal(N).astype(np.float32)
+    xo, et, yd = _dev(obs), _dev(ept, torch.int32), _dev(y)
+
+    def build(net):
+        feat = torch.full((N, nin), float("nan"), device="cuda")
+        v = net.forward(xo, N, ep_t=et, timestep_limit=limit, feat_out=feat).clone()
+        xf = feat.clone()
+        partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+        gh = torch.zeros(N, device="cuda")
+        net.rows(_lib.EPI_VFLOSS, xf, N, inv_n_global=1.0 / N, target=yd, ghead=gh, partial=partial)
+        sums = torch.zeros(4, dtype=torch.float64, device="cuda")
+        net.reduce_partial(partial, N, sums)
+        g = torch.zeros(net.P, device="cuda")
+        net.vjp_flat(xf, N, gh, g)
+        return [t.cpu().numpy().astype(np.float64) for t in (v, xf, gh, sums, g)]
+
+    (v1, f1, gh1, s1, g1), (v0, f0, gh0, s0, g0) = _rows_pair(monkeypatch, "linear", nin, 1, th, build)
+    assert np.array_equal(f1, f0)
+    np.testing.assert_allclose(f1, X, rtol=0, atol=0)
+    np.testing.assert_allclose(v1, v0, rtol=2e-5, atol=2e-6 * np.abs(v0).max())
+    np.testing.assert_allclose(gh1, gh0, rtol=2e-5, atol=2e-6 * np.abs(gh0).max())
+    np.testing.assert_allclose(s1[0], s0[0], rtol=1e-5)
+    assert _rel(g1, g0) < 1e-5
+    np.testing.assert_allclose(v1, T.mlp_forward(spec, th, X)[0][:, 0], rtol=2e-5, atol=2e-6)
+    loss, gw, mse, l2 = T.vf_loss_grad(spec, th, X, y.astype(np.float64))
+    np.testing.assert_allclose(s1[0] / N, mse, rtol=1e-5)
+    assert _rel(g1 + 2e-3 * th, gw) < 1e-4

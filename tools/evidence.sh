@@ -5,7 +5,7 @@
 #   prof         rocprofv3 --kernel-trace --stats of the default line + host gaps
 #   pmc          separate FETCH_SIZE / WRITE_SIZE passes of the default line -> TAG_pmc.json
 #   lines        C3 bf16, C2 bf16 / fp32, C5 bf16 / fp32 lines
-#   sq           SQ wave-time split of the Fisher-product kernels (tools/sq_split.py)
+#   sq           SQ wave-time split of the Fisher-product kernels (tools/fisher_probe.py, tools/sq_split.py)
 #   issue        SQ issue floor of the persistent rollout per bench line (tools/rollout_issue.py)
 #   stamps       per-phase stamps of the persistent Hopper rollout (tools/persistent_stamps.py)
 #   det          run-to-run determinism of the Fisher-product kernels (tools/det_locate.py)
@@ -55,9 +55,9 @@ for step in "$@"; do
     sq)  # SQ wave-time split of the Fisher-product kernels (one 8-counter pass of the probe)
       timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
         SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_BUSY_CYCLES --output-format csv \
-        -d gpurun_out/${tag}_sq -o run -- python3 tools/split_probe.py > gpurun_out/${tag}_sq.log 2>&1 ||
+        -d gpurun_out/${tag}_sq -o run -- python3 tools/fisher_probe.py > gpurun_out/${tag}_sq.log 2>&1 ||
         { echo SQ_FAILED; tail -5 gpurun_out/${tag}_sq.log; exit 1; }
-      python tools/sq_split.py gpurun_out/${tag}_sq mlp_fvp_split_kernel mlp_vjp16_kernel \
+      python tools/sq_split.py gpurun_out/${tag}_sq mlp_fisher_hyb_kernel mlp_fvp_split_kernel mlp_vjp16_kernel \
         > gpurun_out/${tag}_sq.txt && cat gpurun_out/${tag}_sq.txt ;;
     issue)  # the persistent rollout's SQ issue floor per step -> profiles-style TAG_rollout_issue.json
       for line in "Hopper-v2 fp32" "Hopper-v2 bf16" "CartPole-v0 bf16" "CartPole-v0 fp32"; do
