@@ -176,6 +176,21 @@ class MlpNet:
             return t
         return torch.zeros_like(self.image)
 
+    def new_candidate_image(self):
+        """Image buffer for a candidate theta's forward passes (pack_candidate): a split
+        image (marked) when the row passes run on split operands, else an f32 image."""
+        if self.rows_split:
+            t = torch.zeros_like(self.image_s)
+            t._mrl_split_fwd = True  # rows() takes the split kernel for images marked so
+            return t
+        return torch.zeros_like(self.image)
+
+    def pack_candidate(self, theta, image, skip=None):
+        if getattr(image, "_mrl_split_fwd", False):
+            call("mrl_mlp_pack_split", ctypes.byref(self.desc), ptr(theta), ptr(image), ptr(skip), stream())
+        else:
+            self.pack(theta=theta, image=image, fwd_only=True, skip=skip)
+
     def pack_tangent(self, v, image, skip=None):
         if self.fisher_split:
             call("mrl_mlp_pack_split", ctypes.byref(self.desc), ptr(v), ptr(image), ptr(skip), stream())
@@ -213,9 +228,9 @@ class MlpNet:
         io = _lib.RowsIO(ptr(x), ptr(ep_t), float(timestep_limit), int(n), float(inv_n_global), ptr(act), ptr(adv),
                          ptr(oldprob), ptr(target), ptr(out), ptr(ghead), ptr(partial), float(kl_coeff),
                          float(kl_cutoff), float(cutoff_coeff), int(reverse_kl), mode, ptr(cache), ptr(feat_out))
-        if self.rows_split and own and epi in _SPLIT_ROWS_EPIS:
-            call("mrl_mlp_rows_split", ctypes.byref(self.desc), int(epi), ptr(theta), ptr(self.image_s),
-                 ctypes.byref(io), ptr(skip), stream())
+        if self.rows_split and epi in _SPLIT_ROWS_EPIS and (own or getattr(image, "_mrl_split_fwd", False)):
+            call("mrl_mlp_rows_split", ctypes.byref(self.desc), int(epi), ptr(theta),
+                 ptr(self.image_s if own else image), ctypes.byref(io), ptr(skip), stream())
             return
         call("mrl_mlp_rows" + self._sfx, ctypes.byref(self.desc), int(epi), ptr(theta), ptr(image), ptr(tangent),
              ptr(image_t), ctypes.byref(io), ptr(skip), stream())

@@ -55,7 +55,8 @@ class HipTrpoOps:
         self.p32 = torch.zeros(P, **f32)
         self.fullstep = torch.zeros(P, **f64)
         self.cand = torch.zeros(P, **f32)
-        self.cand_image = torch.zeros_like(net.image)
+        self.cand_image = (net.new_candidate_image() if hasattr(net, "new_candidate_image")
+                           else torch.zeros_like(net.image))
         self.tan_image = net.new_tangent_image()
         ns = int(_lib.load().mrl_cg_state_doubles(self.P))  # scalars + block partials (wide nets)
         self.state = torch.zeros(ns, **f64)
@@ -84,7 +85,10 @@ class HipTrpoOps:
 
     def losses(self, theta):
         b, net = self.batch, self.net
-        net.pack(theta=theta, image=self.cand_image, fwd_only=True)
+        if hasattr(net, "pack_candidate"):
+            net.pack_candidate(theta, self.cand_image)
+        else:
+            net.pack(theta=theta, image=self.cand_image, fwd_only=True)
         net.rows(_lib.EPI_LOSSES, b.obs, b.n, inv_n_global=self.inv_ng, act=b.act, adv=b.adv, oldprob=b.prob,
                  partial=self.partial, theta=theta, image=self.cand_image)
         return net.reduce_partial(self.partial, b.n, self.sums)
