@@ -305,7 +305,9 @@ def test_split_forward_rows(head, nin, nout, N, monkeypatch):
     (p1, gh1, s1, c1, g1, l1), (p0, gh0, s0, c0, g0, l0) = _rows_pair(monkeypatch, head, nin, nout, th, build)
     np.testing.assert_allclose(p1, p0, rtol=2e-5, atol=2e-6 * np.abs(p0).max())
     np.testing.assert_allclose(gh1, gh0, rtol=2e-5, atol=2e-6 * np.abs(gh0).max())
-    np.testing.assert_allclose(s1[:3], s0[:3], rtol=1e-5, atol=1e-9)
+    # the KL sum is a difference of near-equal terms: f32 rounding of the rows moves it by
+    # ~1e-7 of the largest sum, whichever kernel rounds
+    np.testing.assert_allclose(s1[:3], s0[:3], rtol=1e-5, atol=1e-6 * np.abs(s0[:3]).max())
     np.testing.assert_allclose(l1[:3], s1[:3], rtol=1e-12, atol=0)  # LOSSES == SURRGRAD's sums
     assert np.abs(c1 - c0).max() < 2e-6
     assert _rel(g1, g0) < 1e-5
