@@ -154,7 +154,7 @@ __host__ __device__ inline float image_value(const MlpDims& d, const float* th, 
 struct RDims {
   int KS0, KS0p;  // input-layer k-steps (4 inputs each), padded to a multiple of 4
   int a0, a1, b0, b1, hv, hb, f32_size;
-  int ba0, ba1, size;  // bf16 fragments (v_mfma_f32_16x16x32_bf16) of the bf16 compute mode
+  int ba0, ba1, bs1, size;  // bf16 fragments (v_mfma_f32_16x16x32_bf16): bf16 mode; bs1: split W1 (fp32)
 };
 
 __host__ __device__ constexpr RDims rollout_dims(int O) {
@@ -175,6 +175,9 @@ __host__ __device__ constexpr RDims rollout_dims(int O) {
   // group g holds in registers r of the 16-unit activation tiles 2p, 2p+1.
   r.ba0 = o; o += 4 * 64 * 4;
   r.ba1 = o; o += 4 * 2 * 64 * 4;
+  // fp32 mode: the three exact bf16 parts of the ba1 fragments, [part][mo][p][lane]: layer 1
+  // of the rollout forward on split operands (six part products, f32 accumulation)
+  r.bs1 = o; o += 3 * 4 * 2 * 64 * 4;
   r.size = o;
   return r;
 }

@@ -133,7 +133,7 @@ template <int O, int A>
 struct RWeights {
   static constexpr RDims R = rollout_dims(O);
   float4 a0[4][R.KS0p / 4];
-  float4 a1[4][4];
+  const bf16x8* w1s = nullptr;  // the split W1 fragments (image section bs1), staged in LDS
   float4 b0[4], b1[4];
   float4 hv[A][4];
   float hb[A];
@@ -144,10 +144,6 @@ struct RWeights {
     for (int mo = 0; mo < 4; ++mo)
 #pragma unroll
       for (int s4 = 0; s4 < R.KS0p / 4; ++s4) a0[mo][s4] = f[(R.a0 >> 2) + (mo * (R.KS0p / 4) + s4) * 64 + lane];
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) a1[mo][mt] = f[(R.a1 >> 2) + (mo * 4 + mt) * 64 + lane];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       b0[mt] = f[(R.b0 >> 2) + g * 4 + mt];
@@ -252,44 +248,54 @@ __device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane
 #pragma unroll
     for (int mo = 0; mo < 4; ++mo) h1[mo] = MFMA16(f4get(w.a0[mo][ks >> 2], ks & 3), xb[ks], h1[mo]);
   if (st != nullptr) st[9] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  // layer 1: input tile mt needs only tanh(h1[mt]): the tanh of tile mt+1 issues
-  // under the MFMAs of tile mt
+  // layer 1 on split operands (fp32-accurate: h1 and W1 split exactly into three bf16
+  // parts, six part products on v_mfma_f32_16x16x32_bf16, f32 accumulation): k-step s
+  // covers tiles 2s, 2s+1 -- the lane's own registers, unit rb_unit(s, g, e) for element e
+  // -- against the W1 fragments the rollout image holds split (section bs1)
   tanh4r<BF>(h1[0]);
+  tanh4r<BF>(h1[1]);
 #pragma unroll
-  for (int mt = 0; mt < 3; ++mt) {
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 hp[3];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int r = 0; r < 4; r += 2) {
+      bf16x2 a, c, e, a2, c2, e2;
+      split2(f32x2{h1[2 * s][r], h1[2 * s][r + 1]}, a, c, e);
+      split2(f32x2{h1[2 * s + 1][r], h1[2 * s + 1][r + 1]}, a2, c2, e2);
+      hp[0][r] = a[0]; hp[0][r + 1] = a[1]; hp[0][4 + r] = a2[0]; hp[0][4 + r + 1] = a2[1];
+      hp[1][r] = c[0]; hp[1][r + 1] = c[1]; hp[1][4 + r] = c2[0]; hp[1][4 + r + 1] = c2[1];
+      hp[2][r] = e[0]; hp[2][r + 1] = e[1]; hp[2][4 + r] = e2[0]; hp[2][4 + r + 1] = e2[1];
+    }
 #pragma unroll
-      for (int mo = 0; mo < 4; ++mo) {
-#ifdef MRL_ABL_NOL1  // diagnostic timing build only (results are wrong)
-        if (q == 0) h2[mo][mt] += h1[mt][q];
-        continue;
-#endif
-        h2[mo] = MFMA16(f4get(w.a1[mo][mt], q), h1[mt][q], h2[mo]);
-      }
-    tanh4r<BF>(h1[mt + 1]);
+    for (int mo = 0; mo < 4; ++mo) {
+      const bf16x8 w0 = w.w1s[(0 * 8 + mo * 2 + s) * 64 + lane], w1 = w.w1s[(1 * 8 + mo * 2 + s) * 64 + lane];
+      const bf16x8 w2 = w.w1s[(2 * 8 + mo * 2 + s) * 64 + lane];
+      h2[mo] = MFMAB16(w2, hp[0], h2[mo]);  // smallest products first
+      h2[mo] = MFMAB16(w0, hp[2], h2[mo]);
+      h2[mo] = MFMAB16(w1, hp[1], h2[mo]);
+      h2[mo] = MFMAB16(w1, hp[0], h2[mo]);
+      h2[mo] = MFMAB16(w0, hp[1], h2[mo]);
+      h2[mo] = MFMAB16(w0, hp[0], h2[mo]);
+    }
+    if (s == 0) {  // the second k-step's activations, under the first one's MFMAs
+      tanh4r<BF>(h1[2]);
+      tanh4r<BF>(h1[3]);
+    }
   }
   if (st != nullptr) st[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  // last input tile output-tile major: tanh + head of output tile mo issue under the
-  // MFMAs of tile mo+1.  Head on VALU: 16 units per lane, then the column's 4 rows.
+  // tanh + head of output tile mo (head on VALU: 16 units per lane, then the column's 4 rows)
   float acc[A];
 #pragma unroll
   for (int o = 0; o < A; ++o) acc[o] = 0.f;
-  auto head_tile = [&](int mo) {
+#pragma unroll
+  for (int mo = 0; mo < 4; ++mo) {
     tanh4r<BF>(h2[mo]);
 #pragma unroll
     for (int o = 0; o < A; ++o) {
       const float4 hv = w.hv[o][mo];
       acc[o] += hv.x * h2[mo][0] + hv.y * h2[mo][1] + hv.z * h2[mo][2] + hv.w * h2[mo][3];
     }
-  };
-#pragma unroll
-  for (int mo = 0; mo < 4; ++mo) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) h2[mo] = MFMA16(f4get(w.a1[mo][3], q), h1[3][q], h2[mo]);
-    if (mo > 0) head_tile(mo - 1);
   }
-  head_tile(3);
 #pragma unroll
   for (int o = 0; o < A; ++o) z[o] = quad_sum(acc[o]) + w.hb[o];
 }
@@ -631,12 +637,30 @@ __global__ __launch_bounds__(RB) void rollout_reset_kernel(RollArgs a) {
 }
 
 // rollout image: rimage_value (mlp_layout.h) of every element
+// part p (0, 1, 2) of an f32 value's exact three-way bf16 split (mlp_split.hip)
+__device__ inline float rb_part(float v, int p) {
+  const __bf16 a = (__bf16)v;
+  if (p == 0) return (float)a;
+  const float r = v - (float)a;
+  const __bf16 c = (__bf16)r;
+  if (p == 1) return (float)c;
+  return r - (float)c;
+}
+
 __global__ void rollout_pack_kernel(RDims r, MlpDims d, const float* __restrict__ th, float* __restrict__ out,
                                     int bf) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < r.f32_size) {
     const float v = rimage_value(r, d, th, i);
     out[i] = (bf && i < r.b0) ? bf16r(v) : v;  // bf16 mode: the MFMA weights W0, W1
+  } else if (i >= r.bs1 && i < r.size) {
+    // split W1 fragments (fp32 mode): part p of the ba1 fragment elements, two per word
+    const int rel = i - r.bs1, part = rel / (4 * 2 * 64 * 4), rr = rel % (4 * 2 * 64 * 4);
+    const int frag = rr >> 2, q = rr & 3;
+    const __bf16 lo = (__bf16)rb_part(rimage_bf16_elem(d, th, true, frag, 2 * q), part);
+    const __bf16 hi = (__bf16)rb_part(rimage_bf16_elem(d, th, true, frag, 2 * q + 1), part);
+    out[i] = __uint_as_float((uint32_t)__builtin_bit_cast(uint16_t, lo) |
+                             ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16));
   } else if (i < r.size) {
     // bf16 fragments: two bf16 per word
     const bool l1 = i >= r.ba1;
@@ -699,6 +723,12 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, const floa
   if (valid) load_noise<ENV>(a, row, zn);
   RollWeights<O, A, BF> wt;
   wt.load(rimg, lane);
+  __shared__ bf16x8 w1s_l[BF ? 1 : 3 * 8 * 64];  // fp32 mode: the split W1 fragments (24 KB)
+  if constexpr (!BF) {
+    constexpr RDims R = rollout_dims(O);
+    for (int i = threadIdx.x; i < 3 * 8 * 64; i += RB) w1s_l[i] = reinterpret_cast<const bf16x8*>(rimg + R.bs1)[i];
+    wt.w1s = w1s_l;
+  }
   float lsd[A];
 #pragma unroll
   for (int q = 0; q < A; ++q) lsd[q] = EC::DISCRETE ? 0.f : logstd[q];
@@ -940,6 +970,12 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
 
   RollWeights<O, A, BF> wt;
   wt.load(rimg, lane);
+  __shared__ bf16x8 w1s_l[BF ? 1 : 3 * 8 * 64];  // fp32 mode: the split W1 fragments (24 KB)
+  if constexpr (!BF) {
+    constexpr RDims R = rollout_dims(O);
+    for (int i = threadIdx.x; i < 3 * 8 * 64; i += RB) w1s_l[i] = reinterpret_cast<const bf16x8*>(rimg + R.bs1)[i];
+    wt.w1s = w1s_l;
+  }
   float lsd[A];
 #pragma unroll
   for (int q = 0; q < A; ++q) lsd[q] = EC::DISCRETE ? 0.f : logstd[q];
