@@ -307,10 +307,16 @@ def policy_gemm_roofline(kern, kinfo, net, dtype, n_rows, K, pmc, gemm_pmc):
     m = timing.meta.get(name, {})
     tf = m["flop"] / (mean_ms * 1e-3) / 1e12
     gemm_peak = PEAK_BF16_TFLOPS if m.get("dtype") == "bf16" else PEAK_FP32_TFLOPS
+    split = m.get("dtype") == "split"
+    if split:
+        # fp32 on split operands: six bf16 part products per fp32 product on the bf16 MFMA,
+        # so the MFMA work is 6x the algorithmic FLOP, priced against the bf16 peak
+        tf, gemm_peak = 6 * tf, PEAK_BF16_TFLOPS
     traffic = gemm_pmc.get(name, {}).get("hbm_bytes_per_launch") if gemm_pmc else None
     by_shape = {k: {"launches": c, "mean_ms": round(mm, 4), "ms_per_iter": round(t / K, 3),
-                    "frac_mfma": round(timing.meta[k]["flop"] / (mm * 1e-3) / 1e12 /
-                                       (PEAK_BF16_TFLOPS if timing.meta[k].get("dtype") == "bf16"
+                    "frac_mfma": round(timing.meta[k]["flop"] / (mm * 1e-3) / 1e12 *
+                                       (6 if timing.meta[k].get("dtype") == "split" else 1) /
+                                       (PEAK_BF16_TFLOPS if timing.meta[k].get("dtype") in ("bf16", "split")
                                         else PEAK_FP32_TFLOPS), 4)}
                 for k, (c, mm, t) in sorted(g.items(), key=lambda kv: -kv[1][2])}
     return {"bound": "mfma", "achieved": round(tf, 3), "peak": gemm_peak, "unit": "TFLOP/s",
@@ -322,7 +328,9 @@ def policy_gemm_roofline(kern, kinfo, net, dtype, n_rows, K, pmc, gemm_pmc):
             "mean_launch_ms": round(mean_ms, 5), "launches_timed": cnt, "ms_per_iter": round(tot_ms / K, 3),
             "gemms": by_shape,
             "note": "layered path: every GEMM launch over >= 65,536 rows timed on its own (HIP events on its stream); "
-                    "the shape with the largest device time per iteration; flop = 2mnk per product"}
+                    "the shape with the largest device time per iteration; flop = 2mnk per product"
+                    + ("; fp32 on split bf16 operands: achieved = 6 x 2mnk / time (the six part products on bf16 "
+                       "MFMA) against the bf16 peak" if split else "")}
 
 
 def main():

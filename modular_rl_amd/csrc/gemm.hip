@@ -116,6 +116,24 @@ __device__ inline void store_tile(float* dst, const float4 (&r)[TW / 32]) {
     *reinterpret_cast<float4*>(dst + S::c_of(t, w) * LDP + S::k_of(t, w)) = r[w];
 }
 
+// split compute (MRL_COMPUTE_SPLIT): the tile's three exact bf16 parts (split2, mlp_device.h),
+// part p at dst + p * part_stride, each in the bf16 tile layout
+template <bool K_CONTIG, int TW>
+__device__ inline void store_tile_split(__bf16* dst, int part_stride, const float4 (&r)[TW / 32]) {
+  using S = Stage<K_CONTIG, TW>;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int w = 0; w < S::NV; ++w) {
+    bf16x2 a0, c0, e0, a1, c1, e1;
+    split2(f32x2{r[w].x, r[w].y}, a0, c0, e0);
+    split2(f32x2{r[w].z, r[w].w}, a1, c1, e1);
+    __bf16* d = dst + S::c_of(t, w) * LDPB + S::k_of(t, w);
+    *reinterpret_cast<bf16x4*>(d) = __builtin_shufflevector(a0, a1, 0, 1, 2, 3);
+    *reinterpret_cast<bf16x4*>(d + part_stride) = __builtin_shufflevector(c0, c1, 0, 1, 2, 3);
+    *reinterpret_cast<bf16x4*>(d + 2 * part_stride) = __builtin_shufflevector(e0, e1, 0, 1, 2, 3);
+  }
+}
+
 template <bool K_CONTIG, int TW>
 __device__ inline void store_tile_bf16(__bf16* dst, const float4 (&r)[TW / 32]) {
   using S = Stage<K_CONTIG, TW>;
@@ -132,13 +150,19 @@ __device__ inline void store_tile_bf16(__bf16* dst, const float4 (&r)[TW / 32]) 
 }
 
 // BN = 128: 2x2 waves, each a 64x64 tile (2x2 MFMA tiles).  BN = 32 (narrow heads,
-// small M): 4x1 waves, each a 32x32 tile.  BF: bf16 operands (v_mfma_f32_32x32x16_bf16,
-// two k-steps per 32-deep tile), f32 accumulation and epilogue.
-template <bool AT, bool BT, int BN, bool BF>
+// small M): 4x1 waves, each a 32x32 tile.  MODE 1 (bf16): bf16 operands
+// (v_mfma_f32_32x32x16_bf16, two k-steps per 32-deep tile), f32 accumulation and
+// epilogue.  MODE 2 (split, fp32-accurate): both operands split exactly into three bf16
+// parts on the way into LDS, the six part products i + j <= 2 per k-step on the same bf16
+// MFMA (mlp_split.hip header), f32 accumulation -- the exact-f32 kernel's results to f32
+// rounding at 6 bf16 MFMAs per 16-deep k-step instead of 16 f32 ones.
+template <bool AT, bool BT, int BN, int MODE>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
+  constexpr bool BF = MODE != 0;
+  constexpr int NP = MODE == 2 ? 3 : 1;  // bf16 parts per operand tile
   constexpr int MI = BN == 128 ? 2 : 1, NI = BN == 128 ? 2 : 1;
-  // tile sizes in floats (fp32) or in 4-byte words holding two bf16 (BF)
-  constexpr int A_FL = BF ? GBM * LDPB / 2 : GBM * LDP, B_FL = BF ? BN * LDPB / 2 : BN * LDP;
+  // tile sizes in floats (fp32) or in 4-byte words holding two bf16 (BF; NP parts)
+  constexpr int A_FL = BF ? NP * GBM * LDPB / 2 : GBM * LDP, B_FL = BF ? NP * BN * LDPB / 2 : BN * LDP;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if (g.skip != nullptr && *g.skip != 0) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, j = lane & 31;
@@ -193,7 +217,10 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
   for (int64_t t = 0; t < nt; ++t) {
     float* As = smem + (t & 1) * (A_FL + B_FL);
     float* Bs = As + A_FL;
-    if constexpr (BF) {
+    if constexpr (MODE == 2) {
+      store_tile_split<!AT, GBM>(reinterpret_cast<__bf16*>(As), GBM * LDPB, ra);
+      store_tile_split<BT, BN>(reinterpret_cast<__bf16*>(Bs), BN * LDPB, rb);
+    } else if constexpr (BF) {
       store_tile_bf16<!AT, GBM>(reinterpret_cast<__bf16*>(As), ra);
       store_tile_bf16<BT, BN>(reinterpret_cast<__bf16*>(Bs), rb);
     } else {
@@ -202,6 +229,37 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
     }
     __syncthreads();
     if (t + 1 < nt) load(t + 1);  // next tile's global loads overlap this tile's MFMAs
+    if constexpr (MODE == 2) {
+      const __bf16* Ab = reinterpret_cast<const __bf16*>(As);
+      const __bf16* Bb = reinterpret_cast<const __bf16*>(Bs);
+#pragma unroll
+      for (int ks = 0; ks < GBK / 16; ++ks) {
+        bf16x8 av[3][MI], bv[3][NI];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+            av[p][mi] = *reinterpret_cast<const bf16x8*>(Ab + p * GBM * LDPB + (wm * 32 * MI + 32 * mi + j) * LDPB +
+                                                         16 * ks + 8 * h);
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            bv[p][ni] = *reinterpret_cast<const bf16x8*>(Bb + p * BN * LDPB + (wn * 32 * NI + 32 * ni + j) * LDPB +
+                                                         16 * ks + 8 * h);
+        }
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) {  // smallest products first
+            acc[mi][ni] = MFMA32B(av[2][mi], bv[0][ni], acc[mi][ni]);
+            acc[mi][ni] = MFMA32B(av[0][mi], bv[2][ni], acc[mi][ni]);
+            acc[mi][ni] = MFMA32B(av[1][mi], bv[1][ni], acc[mi][ni]);
+            acc[mi][ni] = MFMA32B(av[1][mi], bv[0][ni], acc[mi][ni]);
+            acc[mi][ni] = MFMA32B(av[0][mi], bv[1][ni], acc[mi][ni]);
+            acc[mi][ni] = MFMA32B(av[0][mi], bv[0][ni], acc[mi][ni]);
+          }
+      }
+      continue;
+    }
     if constexpr (BF) {
       // k-step s of lane half h: tile k = 16s + 8h + j (A and B agree, any order is valid)
       const __bf16* Ab = reinterpret_cast<const __bf16*>(As);
@@ -444,7 +502,8 @@ int mrl_gemm(const mrl_gemm_desc* d, const int32_t* skip, void* stream) {
   if ((d->a2 == nullptr) != (d->b2 == nullptr)) return fail(E_ARG, "mrl_gemm: a2/b2 must be both set or both null");
   if (d->epilogue < MRL_GEMM_STORE || d->epilogue > MRL_GEMM_SLAB) return fail(E_ARG, "mrl_gemm: bad epilogue");
   if (d->epilogue == MRL_GEMM_DTANH && !d->h) return fail(E_ARG, "mrl_gemm: DTANH needs h");
-  if (d->compute != MRL_COMPUTE_F32 && d->compute != MRL_COMPUTE_BF16) return fail(E_ARG, "mrl_gemm: bad compute");
+  if (d->compute != MRL_COMPUTE_F32 && d->compute != MRL_COMPUTE_BF16 && d->compute != MRL_COMPUTE_SPLIT)
+    return fail(E_ARG, "mrl_gemm: bad compute");
   if (d->m <= 0 || d->n <= 0) return OK;
   GemmArgs g;
   g.M = d->m;
@@ -475,33 +534,34 @@ int mrl_gemm(const mrl_gemm_desc* d, const int32_t* skip, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const unsigned gm = (unsigned)((g.M + GBM - 1) / GBM);
   const int64_t wide_blocks = (g.N + GBN - 1) / GBN * (int64_t)gm * splits;
-  const bool bf = d->compute == MRL_COMPUTE_BF16;
-#define MRL_GEMM_LAUNCH(BNW, SHM)                                                                                   \
-  do {                                                                                                              \
-    const dim3 grid((unsigned)((g.N + BNW - 1) / BNW), gm, (unsigned)splits);                                       \
-    if (!d->a_trans && !d->b_trans) {                                                                               \
-      if (bf) hipLaunchKernelGGL((gemm_f32_kernel<false, false, BNW, true>), grid, dim3(256), SHM, s, g);           \
-      else hipLaunchKernelGGL((gemm_f32_kernel<false, false, BNW, false>), grid, dim3(256), SHM, s, g);             \
-    } else if (!d->a_trans && d->b_trans) {                                                                         \
-      if (bf) hipLaunchKernelGGL((gemm_f32_kernel<false, true, BNW, true>), grid, dim3(256), SHM, s, g);            \
-      else hipLaunchKernelGGL((gemm_f32_kernel<false, true, BNW, false>), grid, dim3(256), SHM, s, g);              \
-    } else if (d->a_trans && !d->b_trans) {                                                                         \
-      if (bf) hipLaunchKernelGGL((gemm_f32_kernel<true, false, BNW, true>), grid, dim3(256), SHM, s, g);            \
-      else hipLaunchKernelGGL((gemm_f32_kernel<true, false, BNW, false>), grid, dim3(256), SHM, s, g);              \
-    } else {                                                                                                        \
-      if (bf) hipLaunchKernelGGL((gemm_f32_kernel<true, true, BNW, true>), grid, dim3(256), SHM, s, g);             \
-      else hipLaunchKernelGGL((gemm_f32_kernel<true, true, BNW, false>), grid, dim3(256), SHM, s, g);               \
-    }                                                                                                               \
+  const int mode = d->compute == MRL_COMPUTE_BF16 ? 1 : d->compute == MRL_COMPUTE_SPLIT ? 2 : 0;
+#define MRL_GEMM_KERNEL(AT, BT, BNW, SHM, grid)                                                     \
+  do {                                                                                              \
+    if (mode == 1) hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, BNW, 1>), grid, dim3(256), SHM, s, g);     \
+    else if (mode == 2) hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, BNW, 2>), grid, dim3(256), SHM, s, g); \
+    else hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, BNW, 0>), grid, dim3(256), SHM, s, g);               \
   } while (0)
+#define MRL_GEMM_LAUNCH(BNW, SHM)                                                                  \
+  do {                                                                                             \
+    const dim3 grid((unsigned)((g.N + BNW - 1) / BNW), gm, (unsigned)splits);                      \
+    if (!d->a_trans && !d->b_trans) MRL_GEMM_KERNEL(false, false, BNW, SHM, grid);                 \
+    else if (!d->a_trans && d->b_trans) MRL_GEMM_KERNEL(false, true, BNW, SHM, grid);              \
+    else if (d->a_trans && !d->b_trans) MRL_GEMM_KERNEL(true, false, BNW, SHM, grid);              \
+    else MRL_GEMM_KERNEL(true, true, BNW, SHM, grid);                                              \
+  } while (0)
+  // LDS per block: two stages of the A and B tiles (fp32 pitch 36; bf16 pitch 40; split: 3 parts)
+  auto shm_of = [&](int bn) -> size_t {
+    return mode == 0 ? 2 * (GBM + bn) * LDP * sizeof(float)
+                     : (size_t)(mode == 2 ? 3 : 1) * 2 * (GBM + bn) * LDPB * sizeof(__bf16);
+  };
   if (g.N <= 32 || wide_blocks < 160) {
     // narrow 128x32 tiles: head layers (n_out <= 32) without 128-wide MFMA waste, and
     // small-M launches (the rollout's per-step forward over E rows) with 4x the blocks
-    const size_t shm = bf ? 2 * (GBM + 32) * LDPB * sizeof(__bf16) : 2 * (GBM + 32) * LDP * sizeof(float);
-    MRL_GEMM_LAUNCH(32, shm);
+    MRL_GEMM_LAUNCH(32, shm_of(32));
   } else {
-    const size_t shm = bf ? 2 * (GBM + GBN) * LDPB * sizeof(__bf16) : 2 * (GBM + GBN) * LDP * sizeof(float);
-    MRL_GEMM_LAUNCH(128, shm);
+    MRL_GEMM_LAUNCH(128, shm_of(128));
   }
+#undef MRL_GEMM_KERNEL
 #undef MRL_GEMM_LAUNCH
   return hip_check(hipGetLastError(), "mrl_gemm");
 }

@@ -333,6 +333,10 @@ class LayeredMlpNet:
         self.lib = _lib.load(require_gpu=True)
         self.dtype = check_dtype(dtype)
         self.compute = _lib.COMPUTE[dtype]
+        # fp32 GEMMs on split bf16 operands (mrl_gemm MRL_COMPUTE_SPLIT: fp32-accurate, six
+        # bf16 part products per k-step); MRL_GEMM_SPLIT=0: the exact-f32 MFMA kernel
+        if self.compute == _lib.COMPUTE_F32 and os.environ.get("MRL_GEMM_SPLIT", "1") != "0":
+            self.compute = _lib.COMPUTE_SPLIT
         if not 1 <= n_out <= MAX_OUT_LAYERED:
             raise MrlError(f"n_out={n_out}: the layered head supports 1..{MAX_OUT_LAYERED} outputs")
         if head == _lib.HEAD_LINEAR and n_out != 1:
@@ -387,27 +391,6 @@ class LayeredMlpNet:
     def partial_rows(self, n):
         return int(self.lib.mrl_partial_rows(int(n)))
 
-    def fisher_onepass_applies(self, x, n, image_t):
-        return bool(self.fisher_onepass and getattr(image_t, "_mrl_split", False) and self.use_cache
-                    and self._cache_key == self._key(x, n, None, 1.0))
-
-    def fisher_product(self, x, n, inv_n_global, tangent, image_t, out, skip=None):
-        """out[P] <- the Fisher product along ``tangent`` over the n cached rows in ONE
-        launch (mrl_mlp_fisher_hyb: split JVP rows and hybrid VJP side by side in each
-        block, the head-gradient rows through LDS) when it applies -- a split tangent image,
-        a current activation cache of these rows, a shape mrl_mlp_fisher_hyb_fits accepts.
-        False: not applicable (the caller runs rows(EPI_FVP) + vjp_flat)."""
-        if not self.fisher_onepass_applies(x, n, image_t):
-            return False
-        rows = int(self.lib.mrl_mlp_slab_rows(ctypes.byref(self.desc), int(n)))
-        slab = self.ws.get("slab", rows * self.P, torch.float32)
-        io = _lib.RowsIO(ptr(x), None, 1.0, int(n), float(inv_n_global), None, None, None, None, None, None,
-                         None, 0.0, 0.0, 0.0, 0, _lib.CACHE_READ, ptr(self._cache(n)), None)
-        call("mrl_mlp_fisher_hyb", ctypes.byref(self.desc), ptr(self.theta), ptr(self.image), ptr(self.image_s),
-             ptr(tangent), ptr(image_t), ctypes.byref(io), ptr(slab), ptr(skip), stream())
-        call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
-        return True
-
     def reduce_partial(self, partial, n, out):
         call("mrl_reduce_rows_f64", ptr(partial), self.partial_rows(n), 4, ptr(out), None, stream())
         return out
@@ -429,8 +412,10 @@ class LayeredMlpNet:
             S = int(self.lib.mrl_gemm_slab_splits(k, splits)) if epi == _lib.GEMM_SLAB else 1
             nbytes = 4 * (prods * (m * k + k * n) + S * m * n + (m * n if epi == _lib.GEMM_DTANH else 0))
             kind = "TN" if a_trans else ("NT" if b_trans else ("NN_dual" if a2 is not None else "NN"))
-            timing.region(f"gemm:f32:{kind}:{m}x{n}x{k}", call, "mrl_gemm", ctypes.byref(g), ptr(skip), stream(),
-                          flop=2 * prods * m * n * k, bytes=nbytes, kernel="gemm_f32_kernel", dtype="fp32")
+            mode = "split" if self.compute == _lib.COMPUTE_SPLIT else "f32"
+            timing.region(f"gemm:{mode}:{kind}:{m}x{n}x{k}", call, "mrl_gemm", ctypes.byref(g), ptr(skip), stream(),
+                          flop=2 * prods * m * n * k, bytes=nbytes, kernel="gemm_f32_kernel",
+                          dtype="split" if mode == "split" else "fp32")
             return
         call("mrl_gemm", ctypes.byref(g), ptr(skip), stream())
 

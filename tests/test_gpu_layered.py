@@ -177,9 +177,11 @@ def test_value_forward_and_loss_grad_with_time_feature(nin, hid):
     assert _rel(g.cpu().numpy() + 2e-3 * th, gw) < 1e-4
 
 
-@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (130, 70, 33), (257, 129, 300), (300, 17, 520)])
-def test_gemm_orientations_and_epilogues(M, N, K):
-    """mrl_gemm against torch fp64 for every operand orientation and epilogue."""
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (130, 70, 33), (257, 129, 300), (300, 17, 520), (1024, 512, 512)])
+@pytest.mark.parametrize("compute", ["f32", "split"])
+def test_gemm_orientations_and_epilogues(M, N, K, compute):
+    """mrl_gemm against torch fp64 for every operand orientation and epilogue, on the
+    exact-f32 MFMA and on split bf16 operands (MRL_COMPUTE_SPLIT: fp32-accurate)."""
     import ctypes
     from modular_rl_amd import _lib
     from modular_rl_amd._lib import call, stream
@@ -192,6 +194,7 @@ def test_gemm_orientations_and_epilogues(M, N, K):
     bias = torch.randn(N, generator=g)
     H = torch.rand(M, N, generator=g)
     addr = lambda t: ctypes.c_void_p(t.data_ptr())
+    cm = _lib.COMPUTE_SPLIT if compute == "split" else _lib.COMPUTE_F32
     bias_d, H_d = bias.cuda(), H.cuda()  # keep the device copies alive while the kernels read them
     for at in (0, 1):
         for bt in (0, 1):
@@ -205,7 +208,7 @@ def test_gemm_orientations_and_epilogues(M, N, K):
                 C = torch.zeros(M, N, device="cuda")
                 d = _lib.GemmDesc(m=M, n=N, k=K, a=addr(Ad), lda=lda, a_trans=at, b=addr(Bd), ldb=ldb, b_trans=bt,
                                   epilogue=epi, a2=addr(A2d), b2=addr(B2d), c=addr(C), ldc=N, bias=addr(bias_d),
-                                  h=addr(H_d), ldh=N)
+                                  h=addr(H_d), ldh=N, compute=cm)
                 call("mrl_gemm", ctypes.byref(d), None, stream())
                 ref = (A.double() @ B.double() + A2.double() @ B2.double() + bias.double())
                 scale = ref.abs().max().item()  # fp32 rounding of the pre-activation sets the error scale
@@ -222,7 +225,7 @@ def test_gemm_orientations_and_epilogues(M, N, K):
     stride = (M + 1) * N + 5
     slab = torch.zeros(S * stride, device="cuda")
     d = _lib.GemmDesc(m=M + 1, n=N, k=K, a=addr(Ad), lda=M, a_trans=1, ones_row=1, b=addr(Bd), ldb=N,
-                      epilogue=_lib.GEMM_SLAB, c=addr(slab), ldc=N, splits=4, slab_stride=stride)
+                      epilogue=_lib.GEMM_SLAB, c=addr(slab), ldc=N, splits=4, slab_stride=stride, compute=cm)
     call("mrl_gemm", ctypes.byref(d), None, stream())
     got = slab.view(S, stride)[:, :(M + 1) * N].sum(0).view(M + 1, N).cpu().double()
     ref = torch.cat([A.double(), torch.ones(1, K, dtype=torch.float64)], 0) @ B.double()
