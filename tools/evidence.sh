@@ -13,6 +13,8 @@
 #   fisher_tests the Fisher-product GPU tests only (split / one-pass / full size)
 #   gae          mrl_gae alone, the default build and every tools/gvar/*.so variant
 #   pair         the default bench line with the two-kernel Fisher product (MRL_FISHER_ONEPASS=0)
+#   layered_tests  the layered-path / Humanoid GPU tests only
+#   c5 / c5_f32  C5 Humanoid fp32 line (split GEMMs / exact-f32 GEMMs: MRL_GEMM_SPLIT=0)
 # Every GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
 tag=${1:?tag}
@@ -90,6 +92,14 @@ for step in "$@"; do
       unset MRL_LIB_PATH
       grep -v amdgpu.ids gpurun_out/${tag}_gae.log ;;
     pair) MRL_FISHER_ONEPASS=0 bench pair 400 --no-cpu-baseline ;;
+    layered_tests)
+      timeout -k 10 900 python -u -m pytest tests/test_gpu_layered.py tests/test_gpu_humanoid.py -m gpu -x -q \
+        --timeout 300 --timeout-method thread > gpurun_out/${tag}_layered_tests.log 2>&1 ||
+        { echo LAYERED_TESTS_FAILED; tail -40 gpurun_out/${tag}_layered_tests.log; exit 1; }
+      tail -1 gpurun_out/${tag}_layered_tests.log ;;
+    c5) bench humanoid 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    c5_f32) MRL_GEMM_SPLIT=0 bench humanoid_f32gemm 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 5 \
+      --warmup 1 --no-cpu-baseline ;;
     det)
       REPS=8 timeout -k 10 200 python -u tools/det_locate.py > gpurun_out/${tag}_det.log 2>&1 ||
         { tail -5 gpurun_out/${tag}_det.log; exit 1; }
