@@ -333,10 +333,14 @@ class LayeredMlpNet:
         self.lib = _lib.load(require_gpu=True)
         self.dtype = check_dtype(dtype)
         self.compute = _lib.COMPUTE[dtype]
-        # fp32 GEMMs on split bf16 operands (mrl_gemm MRL_COMPUTE_SPLIT: fp32-accurate, six
-        # bf16 part products per k-step); MRL_GEMM_SPLIT=0: the exact-f32 MFMA kernel
-        if self.compute == _lib.COMPUTE_F32 and os.environ.get("MRL_GEMM_SPLIT", "1") != "0":
-            self.compute = _lib.COMPUTE_SPLIT
+        # fp32: the policy's weight-gradient (TN) and JVP (NN, two products) GEMMs on split
+        # bf16 operands (mrl_gemm MRL_COMPUTE_SPLIT: fp32-accurate, six bf16 part products per
+        # k-step), where they measured faster than the exact-f32 kernel at 1 M rows (C5: TN
+        # 4.77 -> 4.06 ms, JVP 9.44 -> 8.56); the single-product NN / NT GEMMs and the value
+        # net (its fit runs beside the rollout) measured slower on them and stay exact f32
+        # (profiles/r05o_bench_humanoid*.json).  MRL_GEMM_SPLIT=0: exact f32 everywhere.
+        self.split_gemms = (self.compute == _lib.COMPUTE_F32 and head != _lib.HEAD_LINEAR
+                            and os.environ.get("MRL_GEMM_SPLIT", "1") != "0")
         if not 1 <= n_out <= MAX_OUT_LAYERED:
             raise MrlError(f"n_out={n_out}: the layered head supports 1..{MAX_OUT_LAYERED} outputs")
         if head == _lib.HEAD_LINEAR and n_out != 1:
@@ -402,9 +406,12 @@ class LayeredMlpNet:
 
     def _gemm(self, m, n, k, a, lda, b, ldb, c, ldc, a_trans=0, b_trans=0, epi=0, a2=None, b2=None, bias=None,
               h=None, ldh=0, ones_row=0, splits=1, slab_stride=0, skip=None):
+        compute = self.compute
+        if self.split_gemms and (a_trans or a2 is not None) and max(m, k) >= GEMM_TIMING_MIN_ROWS:
+            compute = _lib.COMPUTE_SPLIT
         g = _lib.GemmDesc(m=m, n=n, k=k, a=a, lda=lda, a_trans=a_trans, ones_row=ones_row, b=b, ldb=ldb,
                           b_trans=b_trans, epilogue=epi, a2=a2, b2=b2, c=c, ldc=ldc, bias=bias, h=h, ldh=ldh,
-                          splits=splits, slab_stride=slab_stride, compute=self.compute)
+                          splits=splits, slab_stride=slab_stride, compute=compute)
         if timing.enabled() and max(m, k) >= GEMM_TIMING_MIN_ROWS:
             # algorithmic work of the launch: 2mnk per product; bytes = f32 operands read
             # once, C written once (SLAB: one [m, n] slab per K split), H read (DTANH)
@@ -412,7 +419,7 @@ class LayeredMlpNet:
             S = int(self.lib.mrl_gemm_slab_splits(k, splits)) if epi == _lib.GEMM_SLAB else 1
             nbytes = 4 * (prods * (m * k + k * n) + S * m * n + (m * n if epi == _lib.GEMM_DTANH else 0))
             kind = "TN" if a_trans else ("NT" if b_trans else ("NN_dual" if a2 is not None else "NN"))
-            mode = "split" if self.compute == _lib.COMPUTE_SPLIT else "f32"
+            mode = "split" if compute == _lib.COMPUTE_SPLIT else "f32"
             timing.region(f"gemm:{mode}:{kind}:{m}x{n}x{k}", call, "mrl_gemm", ctypes.byref(g), ptr(skip), stream(),
                           flop=2 * prods * m * n * k, bytes=nbytes, kernel="gemm_f32_kernel",
                           dtype="split" if mode == "split" else "fp32")
