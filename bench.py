@@ -87,7 +87,7 @@ PMC_FILE = "pmc_r04.json"  # tools/prof_pmc_run.sh r04l (the split JVP rows kern
 GEMM_PMC_FILE = "pmc_gemm_r04.json"  # tools/pmc_traffic.py --gemm: HBM bytes per layered GEMM launch
 # SQ issue cycles per rollout step (tools/rollout_issue.py: persistent kernel; tools/step_issue.py: the
 # layered Humanoid step's launch chain), newest first: the first file holding the line's key is used
-ROLLOUT_ISSUE_FILES = ("rollout_issue_r04.json", "rollout_issue_r03.json")
+ROLLOUT_ISSUE_FILES = ("rollout_issue_r05.json", "rollout_issue_r04.json", "rollout_issue_r03.json")
 CLOCK_GHZ = 2.4  # MI355X max shader clock (MI355X_MICROARCH.md)
 
 
