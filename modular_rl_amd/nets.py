@@ -333,12 +333,13 @@ class LayeredMlpNet:
         self.lib = _lib.load(require_gpu=True)
         self.dtype = check_dtype(dtype)
         self.compute = _lib.COMPUTE[dtype]
-        # fp32: the policy's weight-gradient (TN) and JVP (NN, two products) GEMMs on split
-        # bf16 operands (mrl_gemm MRL_COMPUTE_SPLIT: fp32-accurate, six bf16 part products per
-        # k-step), where they measured faster than the exact-f32 kernel at 1 M rows (C5: TN
-        # 4.77 -> 4.06 ms, JVP 9.44 -> 8.56); the single-product NN / NT GEMMs and the value
-        # net (its fit runs beside the rollout) measured slower on them and stay exact f32
-        # (profiles/r05o_bench_humanoid*.json).  MRL_GEMM_SPLIT=0: exact f32 everywhere.
+        # fp32: the policy's weight-gradient (TN) and JVP (NN, two products) GEMMs and its
+        # small-M rollout forward on split bf16 operands (mrl_gemm MRL_COMPUTE_SPLIT:
+        # fp32-accurate, six bf16 part products per k-step), where they measured faster than
+        # the exact-f32 kernel (C5: TN 4.77 -> 4.06 ms, JVP 9.44 -> 8.56 at 1 M rows; the
+        # rollout 405 -> 363 ms per iteration); the single-product NN / NT GEMMs over 1 M rows
+        # and the value net (its fit runs beside the rollout) measured slower on them and stay
+        # exact f32 (profiles/r05o_bench_humanoid*.json).  MRL_GEMM_SPLIT=0: exact f32.
         self.split_gemms = (self.compute == _lib.COMPUTE_F32 and head != _lib.HEAD_LINEAR
                             and os.environ.get("MRL_GEMM_SPLIT", "1") != "0")
         if not 1 <= n_out <= MAX_OUT_LAYERED:
@@ -407,7 +408,7 @@ class LayeredMlpNet:
     def _gemm(self, m, n, k, a, lda, b, ldb, c, ldc, a_trans=0, b_trans=0, epi=0, a2=None, b2=None, bias=None,
               h=None, ldh=0, ones_row=0, splits=1, slab_stride=0, skip=None):
         compute = self.compute
-        if self.split_gemms and (a_trans or a2 is not None) and max(m, k) >= GEMM_TIMING_MIN_ROWS:
+        if self.split_gemms and (a_trans or a2 is not None or max(m, k) < GEMM_TIMING_MIN_ROWS):
             compute = _lib.COMPUTE_SPLIT
         g = _lib.GemmDesc(m=m, n=n, k=k, a=a, lda=lda, a_trans=a_trans, ones_row=ones_row, b=b, ldb=ldb,
                           b_trans=b_trans, epilogue=epi, a2=a2, b2=b2, c=c, ldc=ldc, bias=bias, h=h, ldh=ldh,
