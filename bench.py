@@ -83,7 +83,7 @@ def dominant_kernel(kinfo):
 DYNAMICS = {"Hopper-v2": "hopper.xml articulated-body dynamics", "Humanoid-v2": "humanoid.xml articulated-body dynamics",
             "CartPole-v0": "gym equations"}
 GAE_BYTES_PER_ROW = 17  # read r 4 + v 4 + flags 1, write adv 4 + ret 4
-PMC_FILE = "pmc_r04.json"  # tools/prof_pmc_run.sh r04l (the split JVP rows kernel as fvp_jvp_rows_split)
+PMC_FILE = "pmc_r05.json"  # tools/evidence.sh pmc (FETCH_SIZE x2 + WRITE_SIZE per launch, separate passes)
 GEMM_PMC_FILE = "pmc_gemm_r04.json"  # tools/pmc_traffic.py --gemm: HBM bytes per layered GEMM launch
 # SQ issue cycles per rollout step (tools/rollout_issue.py: persistent kernel; tools/step_issue.py: the
 # layered Humanoid step's launch chain), newest first: the first file holding the line's key is used
