@@ -314,6 +314,13 @@ int mrl_cg_init(const double* b, int64_t n, double* x, double* r, double* p, flo
                 double* state, int32_t* flag, void* stream);
 int mrl_cg_update(const float* fvp, double damping, double residual_tol, int64_t n, double* x, double* r,
                   double* p, float* p32, double* ax, double* state, int32_t* flag, void* stream);
+/* mrl_cg_update that also writes the next Fisher product's split tangent image of p32
+ * (what mrl_mlp_pack_split(d, p32, image_t) writes), so the CG loop issues one launch
+ * fewer per iteration; the single-block update only (n <= 8192, else E_UNSUPPORTED),
+ * n must be d's parameter count */
+int mrl_cg_update_pack(const float* fvp, double damping, double residual_tol, int64_t n, double* x, double* r,
+                       double* p, float* p32, double* ax, double* state, int32_t* flag, const mrl_mlp_desc* d,
+                       float* image_t, void* stream);
 /* step scaling (trpo.py:119-124): shs = .5 x.(fvp + damping x), lm = sqrt(shs/max_kl),
  * fullstep = x/lm, out[0]=shs out[1]=lm out[2]=-g.x out[3]=-g.x/lm (expected rate) */
 int mrl_trpo_step(const float* fvp, const double* x, const float* g, double damping, double max_kl,

@@ -116,6 +116,7 @@ SIGNATURES = {
     "mrl_cg_state_doubles": (i64, [i64]),
     "mrl_cg_init": (i32, [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_cg_update": (i32, [vp, f64, f64, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "mrl_cg_update_pack": (i32, [vp, f64, f64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_trpo_step": (i32, [vp, vp, vp, f64, f64, i64, vp, vp, vp]),
     "mrl_trpo_step_ax": (i32, [vp, vp, vp, f64, i64, vp, vp, vp]),
     "mrl_device_cu_count": (i32, [vp]),

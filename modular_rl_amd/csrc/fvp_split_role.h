@@ -17,6 +17,40 @@ namespace mrl {
 __host__ __device__ constexpr int split_fw(const BDims& b) { return b.fwd_words - b.fa0; }
 __host__ __device__ constexpr int split_fwd_words(const BDims& b) { return b.fa0 + 3 * split_fw(b); }
 
+// part p (0, 1, 2) of an f32 value's exact three-way bf16 split
+__device__ inline float bf16_part(float v, int p) {
+  const __bf16 a = (__bf16)v;
+  if (p == 0) return (float)a;
+  const float r = v - (float)a;
+  const __bf16 c = (__bf16)r;
+  if (p == 1) return (float)c;
+  return r - (float)c;
+}
+
+// word w of the split image of th (mlp_pack_split_kernel; the CG update writes the next
+// tangent's image with it, mrl_cg_update_pack): the f32 section [0, fa0) -- biases and
+// the VALU head in the bf16 image's order -- then part p of the forward fragments
+__device__ inline float split_image_word(const MlpDims& d, const BDims& b, const float* th, int w) {
+  if (w < b.fa0) {
+    int idx;
+    if (w < b.fb1) idx = d.fb0 + (w - b.fb0);
+    else if (w < b.hv) idx = d.fb1 + (w - b.fb1);
+    else if (w < b.hb) idx = d.hv + (w - b.hv);
+    else idx = d.hb + (w - b.hb);
+    return image_value(d, th, idx);
+  }
+  const int FW = split_fw(b);
+  const int part = (w - b.fa0) / FW;
+  const int wp = b.fa0 + (w - b.fa0) % FW;
+  int seg, rel;
+  if (wp < b.fa1) { seg = 0; rel = wp - b.fa0; }
+  else { seg = 1; rel = wp - b.fa1; }
+  const int frag = rel >> 2, q = rel & 3;
+  const __bf16 lo = (__bf16)bf16_part(bimage_elem(d, b, th, seg, frag, 2 * q), part);
+  const __bf16 hi = (__bf16)bf16_part(bimage_elem(d, b, th, seg, frag, 2 * q + 1), part);
+  return __uint_as_float((uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16));
+}
+
 // The exact three-way split of 8 values, two at a time: one v_cvt_pk_bf16_f32 per part
 // pair, the widening and the remainders on packed f32 (v_pk_add_f32) -- the same RNE
 // conversions and exact subtractions as the element-wise form, about 4.5 VALU per value

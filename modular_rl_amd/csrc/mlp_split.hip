@@ -33,41 +33,11 @@
 
 namespace mrl {
 
-// part p (0, 1, 2) of an f32 value's exact three-way bf16 split
-__device__ inline float bf16_part(float v, int p) {
-  const __bf16 a = (__bf16)v;
-  if (p == 0) return (float)a;
-  const float r = v - (float)a;
-  const __bf16 c = (__bf16)r;
-  if (p == 1) return (float)c;
-  return r - (float)c;
-}
-
 __global__ void mlp_pack_split_kernel(MlpDims d, BDims b, const float* __restrict__ th, float* __restrict__ image,
                                       int words, const int32_t* __restrict__ skip) {
   if (skip != nullptr && *skip != 0) return;
   const int w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= words) return;
-  if (w < b.fa0) {  // f32 section: biases and the VALU head, the bf16 image's order
-    int idx;
-    if (w < b.fb1) idx = d.fb0 + (w - b.fb0);
-    else if (w < b.hv) idx = d.fb1 + (w - b.fb1);
-    else if (w < b.hb) idx = d.hv + (w - b.hv);
-    else idx = d.hb + (w - b.hb);
-    image[w] = image_value(d, th, idx);
-    return;
-  }
-  const int FW = split_fw(b);
-  const int part = (w - b.fa0) / FW;
-  const int wp = b.fa0 + (w - b.fa0) % FW;
-  int seg, rel;
-  if (wp < b.fa1) { seg = 0; rel = wp - b.fa0; }
-  else { seg = 1; rel = wp - b.fa1; }
-  const int frag = rel >> 2, q = rel & 3;
-  const __bf16 lo = (__bf16)bf16_part(bimage_elem(d, b, th, seg, frag, 2 * q), part);
-  const __bf16 hi = (__bf16)bf16_part(bimage_elem(d, b, th, seg, frag, 2 * q + 1), part);
-  const uint32_t v = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
-  image[w] = __uint_as_float(v);
+  if (w < words) image[w] = split_image_word(d, b, th, w);
 }
 
 // waves per block of the JVP rows kernel: 4 (two blocks per CU at 2 waves per SIMD: the

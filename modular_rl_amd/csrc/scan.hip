@@ -12,6 +12,7 @@
 
 #include "../../include/mrl_hip.h"
 #include "mrl_common.h"
+#include "fvp_split_role.h"
 
 namespace mrl {
 
@@ -321,10 +322,20 @@ __global__ __launch_bounds__(CG_T) void cg_update_kernel(const float* __restrict
 // registers: every operand is loaded once, up front, instead of once per pass
 // (three dependent global passes of the plain kernel).  Per-thread accumulation
 // order and the block_sum tree are the plain kernel's, so the results are identical.
-template <int K>
+// PACK: the next Fisher product's tangent image too -- the split image of p32
+// (split_image_word, as mlp_pack_split_kernel writes it), one launch instead of two
+struct CgPack {
+  MlpDims d;
+  BDims b;
+  float* image;
+  int words;
+};
+
+template <int K, bool PACK = false>
 __global__ __launch_bounds__(CG_T) void cg_update_reg_kernel(const float* __restrict__ fvp, double damping, double tol,
                                                              int64_t n, double* x, double* r, double* p, float* p32,
-                                                             double* ax, double* state, int32_t* flag) {
+                                                             double* ax, double* state, int32_t* flag,
+                                                             CgPack pk = CgPack{}) {
   __shared__ double red[CG_T];
   if (flag[0] != 0) return;
   const double rdotr = state[0];
@@ -376,6 +387,10 @@ __global__ __launch_bounds__(CG_T) void cg_update_reg_kernel(const float* __rest
     state[1] = pz;
     state[2] += 1.0;
     if (newr < tol) flag[0] = 1;
+  }
+  if constexpr (PACK) {
+    __syncthreads();  // p32 of the whole block is written (global, visible to the block)
+    for (int w = threadIdx.x; w < pk.words; w += CG_T) pk.image[w] = split_image_word(pk.d, pk.b, p32, w);
   }
 }
 
@@ -893,6 +908,25 @@ int mrl_cg_update(const float* fvp, double damping, double residual_tol, int64_t
                        state, flag);
   }
   return hip_check(hipGetLastError(), "mrl_cg_update");
+}
+
+int mrl_cg_update_pack(const float* fvp, double damping, double residual_tol, int64_t n, double* x, double* r,
+                       double* p, float* p32, double* ax, double* state, int32_t* flag, const mrl_mlp_desc* d,
+                       float* image_t, void* stream) {
+  if (!fvp || !x || !r || !p || !p32 || !state || !flag || !d || !image_t) return fail(E_ARG, "null pointer");
+  if (!(MRL_CG_REG && n <= CG_SMALL_N && n <= 8 * CG_T))
+    return fail(E_UNSUPPORTED, "mrl_cg_update_pack: the single-block register CG update only (n <= 8192)");
+  const int64_t words = mrl_mlp_image_words_split(d);
+  if (words < 0) return fail(E_UNSUPPORTED, "mrl_cg_update_pack: no split image for this net");
+  if (mrl_mlp_num_params(d) != n) return fail(E_ARG, "mrl_cg_update_pack: n is not the net's parameter count");
+  CgPack pk;
+  pk.d = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
+  pk.b = bf16_dims(d->n_in, d->n_out);
+  pk.image = image_t;
+  pk.words = (int)words;
+  hipLaunchKernelGGL((cg_update_reg_kernel<8, true>), dim3(1), dim3(CG_T), 0, (hipStream_t)stream, fvp, damping,
+                     residual_tol, n, x, r, p, p32, ax, state, flag, pk);
+  return hip_check(hipGetLastError(), "mrl_cg_update_pack");
 }
 
 int mrl_trpo_step(const float* fvp, const double* x, const float* g, double damping, double max_kl, int64_t n,

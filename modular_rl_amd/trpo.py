@@ -25,6 +25,7 @@ In data-parallel mode every sum above is all-reduced over ranks (dist.Comm)
 before it is used, so all ranks take the identical step.
 """
 import ctypes
+import os
 from collections import OrderedDict
 
 import numpy as np
@@ -58,6 +59,11 @@ class HipTrpoOps:
         self.cand_image = (net.new_candidate_image() if hasattr(net, "new_candidate_image")
                            else torch.zeros_like(net.image))
         self.tan_image = net.new_tangent_image()
+        # the CG update writes the next tangent's split image itself (mrl_cg_update_pack):
+        # the Fisher product then skips its pack launch
+        self.cg_pack = (getattr(net, "fisher_split", False) and P <= 8192
+                        and os.environ.get("MRL_CG_PACK", "1") != "0")
+        self._tan_packed = False
         ns = int(_lib.load().mrl_cg_state_doubles(self.P))  # scalars + block partials (wide nets)
         self.state = torch.zeros(ns, **f64)
         self.flag = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -95,7 +101,8 @@ class HipTrpoOps:
 
     def fvp(self, v32, skip=None):
         b, net = self.batch, self.net
-        net.pack_tangent(v32, self.tan_image, skip=skip)
+        if not (self._tan_packed and v32 is self.p32):
+            net.pack_tangent(v32, self.tan_image, skip=skip)
         if getattr(net, "fisher_onepass", False) and net.fisher_onepass_applies(b.obs, b.n, self.tan_image):
             # the whole product in one launch (JVP rows and VJP side by side per block)
             timing.start("fvp_onepass")
@@ -118,8 +125,15 @@ class HipTrpoOps:
     def cg_init(self, b):
         call("mrl_cg_init", ptr(b), self.P, ptr(self.x), ptr(self.r), ptr(self.p), ptr(self.p32), ptr(self.ax),
              ptr(self.state), ptr(self.flag), stream())
+        self._tan_packed = False
 
     def cg_update(self, fv, damping, tol):
+        if self.cg_pack:
+            call("mrl_cg_update_pack", ptr(fv), float(damping), float(tol), self.P, ptr(self.x), ptr(self.r),
+                 ptr(self.p), ptr(self.p32), ptr(self.ax), ptr(self.state), ptr(self.flag),
+                 ctypes.byref(self.net.desc), ptr(self.tan_image), stream())
+            self._tan_packed = True
+            return
         call("mrl_cg_update", ptr(fv), float(damping), float(tol), self.P, ptr(self.x), ptr(self.r), ptr(self.p),
              ptr(self.p32), ptr(self.ax), ptr(self.state), ptr(self.flag), stream())
 

@@ -359,3 +359,64 @@ def test_split_forward_value_rows(nin, N, monkeypatch):
     loss, gw, mse, l2 = T.vf_loss_grad(spec, th, X, y.astype(np.float64))
     np.testing.assert_allclose(s1[0] / N, mse, rtol=1e-5)
     assert _rel(g1 + 2e-3 * th, gw) < 1e-4
+
+
+@pytest.mark.parametrize("head,nin,nout", [("gauss", 11, 3), ("softmax", 4, 2), ("gauss", 17, 6)])
+def test_cg_update_pack_writes_the_split_tangent_image(head, nin, nout, monkeypatch):
+    """mrl_cg_update_pack (the CG update that also writes the next tangent's split image)
+    leaves x / r / p / p32 / ax / state bit-identical to mrl_cg_update, and its image is
+    mrl_mlp_pack_split's of the new p32 word for word; converged (flag set) it touches
+    nothing."""
+    monkeypatch.setenv("MRL_FISHER", "split")
+    from modular_rl_amd import _lib
+    from modular_rl_amd._lib import call, ptr
+    from modular_rl_amd.nets import MlpNet
+    from modular_rl_amd.trpo import HipTrpoOps
+    net = MlpNet(nin, nout, _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX)
+    rng = np.random.default_rng(nin)
+    P = net.P
+    outs = []
+    for fused in (False, True):
+        ops = HipTrpoOps(net)
+        ops.cg_pack = fused
+        b = _dev(rng.standard_normal(P) if not outs else outs[0]["b"], torch.float64)
+        ops.cg_init(b)
+        fv = _dev(np.random.default_rng(5).standard_normal(P))
+        ops.tan_image.fill_(float("nan"))
+        for _ in range(3):
+            ops.cg_update(fv, 1e-3, 1e-10)
+        torch.cuda.synchronize()
+        outs.append(dict(b=b.cpu().numpy(), **{k: getattr(ops, k).cpu().numpy().copy()
+                                             for k in ("x", "r", "p", "p32", "ax", "state", "tan_image")}))
+        if fused:
+            ref = net.new_tangent_image()
+            net.pack_tangent(ops.p32, ref)
+            got = ops.tan_image.cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, ref.cpu().numpy().view(np.uint32))
+            # converged: the update (and its pack) leaves everything as it is
+            ops.flag.fill_(1)
+            ops.tan_image.fill_(7.0)
+            ops.cg_update(fv, 1e-3, 1e-10)
+            assert bool((ops.tan_image == 7.0).all())
+    for k in ("x", "r", "p", "p32", "ax", "state"):
+        assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+def test_cg_update_pack_refuses_wide_nets_and_mismatched_sizes(monkeypatch):
+    monkeypatch.setenv("MRL_FISHER", "split")
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import MlpNet
+    net = MlpNet(11, 3, _lib.HEAD_GAUSS)
+    lib = _lib.load()
+    P = net.P
+    z = torch.zeros(P + 8, dtype=torch.float64, device="cuda")
+    f = torch.zeros(P + 8, dtype=torch.float32, device="cuda")
+    st = torch.zeros(4, dtype=torch.float64, device="cuda")
+    fl = torch.zeros(2, dtype=torch.int32, device="cuda")
+    img = net.new_tangent_image()
+    import ctypes
+    args = lambda n: (f.data_ptr(), 1e-3, 1e-10, n, z.data_ptr(), z.data_ptr(), z.data_ptr(), f.data_ptr(),
+                      z.data_ptr(), st.data_ptr(), fl.data_ptr(), ctypes.byref(net.desc), img.data_ptr(), None)
+    assert lib.mrl_cg_update_pack(*args(P + 1)) == -1  # MRL_E_ARG
+    assert lib.mrl_cg_update_pack(*args(9000)) == -2  # MRL_E_UNSUPPORTED
+    torch.cuda.synchronize()
