@@ -59,12 +59,13 @@ def _host(v):
     return v.detach().cpu().numpy().copy() if torch.is_tensor(v) else np.array(v, copy=True)
 
 
-def capture_state(agent, with_vf=True, host=True):
+def capture_state(agent, with_vf=True, host=True, theta=True):
     """Device-side copies (stream-ordered, no host sync) of everything agent_state
     saves; the pipelined runner takes one at the end of each iteration.  host=False:
     only the state the next rollout advances (taken before that rollout is issued; the
-    rest, capture_host_state, after it)."""
-    cap = {"policy/theta": agent.policy.net.theta.detach().clone()}
+    rest, capture_host_state, after it); theta=False: without the policy parameters
+    (the runner clones them after issuing that rollout, which only reads them)."""
+    cap = {"policy/theta": agent.policy.net.theta.detach().clone()} if theta else {}
     if with_vf:
         cap["vf/theta"] = agent.baseline.net.theta.detach().clone()
     col = agent._filter_owner()

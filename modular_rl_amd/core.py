@@ -319,13 +319,15 @@ class IterationRunner:
         Python then run under that rollout instead of in front of it."""
         return self._on_main(lambda: self._step(prelaunch_next))
 
-    def _launch_rollout(self):
-        """Issue one iteration's rollout (the noise fill and the step chain); its events."""
+    def _launch_rollout(self, noise_ready=False):
+        """Issue one iteration's rollout (the noise fill and the step chain); its events.
+        ``noise_ready``: the noise fill was issued already (under the update's readback)."""
         col, ev = self.col, {}
         ev["rollout0"] = self._event()
         if self.pipeline:
             main = torch.cuda.current_stream()
-            col.fill_noise()  # one wide kernel: on every CU, ahead of the step chain
+            if not noise_ready:
+                col.fill_noise()  # one wide kernel: on every CU, ahead of the step chain
             self.rollout_stream.wait_stream(main)
             with torch.cuda.stream(self.rollout_stream):
                 col.launch(fill_noise=False)
@@ -368,19 +370,30 @@ class IterationRunner:
             ev["upd1"] = self._event()
             # pipelined: the VF of this iteration is fitted during the next step and added
             # to the capture then; in order it is final already
-            post["cap"] = capture_state(agent, with_vf=not self.pipeline, host=False)
+            post["cap"] = capture_state(agent, with_vf=not self.pipeline, host=False, theta=False)
             if prelaunch_next:
-                self._prelaunched = self._launch_rollout()
-            # numpy's RNG and the updater's arrays: nothing the rollout touches, so taken
-            # under it (≈30 us of host time off the update-to-rollout seam)
+                self._prelaunched = self._launch_rollout(noise_ready=post.pop("noise", False))
+            # theta (the rollout only reads it), numpy's RNG and the updater's arrays:
+            # nothing the rollout writes, so taken under it (off the update-to-rollout seam)
+            post["cap"]["policy/theta"] = agent.policy.net.theta.detach().clone()
             post["cap"].update(capture_host_state(agent))
+
+        def before_readback():
+            """The next rollout's noise (a function of the collector's iteration counter,
+            which this iteration's rollout has advanced already): issued behind the
+            update's readback, it runs while the host decides the line search."""
+            if prelaunch_next and self.pipeline and "cap" not in post:
+                col.fill_noise()
+                post["noise"] = True
 
         upd = agent.updater
         upd.after_theta = after_theta
+        upd.before_readback = before_readback
         try:
             pol_stats = upd.update(batch)
         finally:
             upd.after_theta = None
+            upd.before_readback = None
         after_theta()  # updaters without the hook
         if self.pipeline:
             # read back with the deferred VF fit's stats (no host sync here); the state at

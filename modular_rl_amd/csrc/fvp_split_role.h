@@ -27,28 +27,36 @@ __device__ inline float bf16_part(float v, int p) {
   return r - (float)c;
 }
 
-// word w of the split image of th (mlp_pack_split_kernel; the CG update writes the next
-// tangent's image with it, mrl_cg_update_pack): the f32 section [0, fa0) -- biases and
-// the VALU head in the bf16 image's order -- then part p of the forward fragments
-__device__ inline float split_image_word(const MlpDims& d, const BDims& b, const float* th, int w) {
-  if (w < b.fa0) {
+// The split image of th (mlp_pack_split_kernel; the CG update writes the next tangent's
+// image with it, mrl_cg_update_pack), item u of split_image_items(b): items [0, fa0) are
+// the f32 section's words (biases and the VALU head in the bf16 image's order), item
+// fa0 + j is forward-fragment word j of all three parts (its two weights read and split
+// once, the three part words written)
+__device__ inline int split_image_items(const BDims& b) { return b.fa0 + split_fw(b); }
+
+__device__ inline void split_image_item(const MlpDims& d, const BDims& b, const float* th, float* image, int u) {
+  if (u < b.fa0) {
     int idx;
-    if (w < b.fb1) idx = d.fb0 + (w - b.fb0);
-    else if (w < b.hv) idx = d.fb1 + (w - b.fb1);
-    else if (w < b.hb) idx = d.hv + (w - b.hv);
-    else idx = d.hb + (w - b.hb);
-    return image_value(d, th, idx);
+    if (u < b.fb1) idx = d.fb0 + (u - b.fb0);
+    else if (u < b.hv) idx = d.fb1 + (u - b.fb1);
+    else if (u < b.hb) idx = d.hv + (u - b.hv);
+    else idx = d.hb + (u - b.hb);
+    image[u] = image_value(d, th, idx);
+    return;
   }
   const int FW = split_fw(b);
-  const int part = (w - b.fa0) / FW;
-  const int wp = b.fa0 + (w - b.fa0) % FW;
+  const int wp = u;  // word of the bf16 image's forward section
   int seg, rel;
   if (wp < b.fa1) { seg = 0; rel = wp - b.fa0; }
   else { seg = 1; rel = wp - b.fa1; }
   const int frag = rel >> 2, q = rel & 3;
-  const __bf16 lo = (__bf16)bf16_part(bimage_elem(d, b, th, seg, frag, 2 * q), part);
-  const __bf16 hi = (__bf16)bf16_part(bimage_elem(d, b, th, seg, frag, 2 * q + 1), part);
-  return __uint_as_float((uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16));
+  const float lo = bimage_elem(d, b, th, seg, frag, 2 * q), hi = bimage_elem(d, b, th, seg, frag, 2 * q + 1);
+#pragma unroll
+  for (int part = 0; part < 3; ++part) {
+    const __bf16 l = (__bf16)bf16_part(lo, part), h = (__bf16)bf16_part(hi, part);
+    image[u + part * FW] =
+        __uint_as_float((uint32_t)__builtin_bit_cast(uint16_t, l) | ((uint32_t)__builtin_bit_cast(uint16_t, h) << 16));
+  }
 }
 
 // The exact three-way split of 8 values, two at a time: one v_cvt_pk_bf16_f32 per part

@@ -34,10 +34,10 @@
 namespace mrl {
 
 __global__ void mlp_pack_split_kernel(MlpDims d, BDims b, const float* __restrict__ th, float* __restrict__ image,
-                                      int words, const int32_t* __restrict__ skip) {
+                                      int items, const int32_t* __restrict__ skip) {
   if (skip != nullptr && *skip != 0) return;
-  const int w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w < words) image[w] = split_image_word(d, b, th, w);
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < items) split_image_item(d, b, th, image, u);
 }
 
 // waves per block of the JVP rows kernel: 4 (two blocks per CU at 2 waves per SIMD: the
@@ -302,9 +302,9 @@ int mrl_mlp_pack_split(const mrl_mlp_desc* d, const float* theta, float* image, 
   if (!theta || !image) return fail(E_ARG, "null pointer");
   const MlpDims m = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
   const BDims b = bf16_dims(d->n_in, d->n_out);
-  const int words = split_fwd_words(b);
-  hipLaunchKernelGGL(mlp_pack_split_kernel, dim3((words + 255) / 256), dim3(256), 0, (hipStream_t)stream, m, b, theta,
-                     image, words, skip);
+  const int items = b.fa0 + split_fw(b);
+  hipLaunchKernelGGL(mlp_pack_split_kernel, dim3((items + 255) / 256), dim3(256), 0, (hipStream_t)stream, m, b, theta,
+                     image, items, skip);
   return hip_check(hipGetLastError(), "mrl_mlp_pack_split");
 }
 

@@ -244,22 +244,41 @@ constexpr int CG_T = 1024;
 #define MRL_CG_REG 1
 #endif
 
+// The sum of the block's CG_T values as the pairwise tree red[i] += red[i + o],
+// o = CG_T/2 .. 1, adds them (the tree every CG kernel's results are defined by), in
+// two barriers instead of eleven: wave 0 lane i gathers its 16 values v[i + 64 k] and
+// adds them in the tree's cross-wave order (o = 512 .. 64: k with k + 8, k + 4, k + 2,
+// k + 1), then o = 32 .. 1 as lane shuffles.  red: CG_T + 1 doubles (the result slot
+// red[CG_T] is only written after the first barrier, so back-to-back sums need no third).
 __device__ inline double block_sum(double v, double* red) {
+  static_assert(CG_T == 1024, "the cross-wave tree below is CG_T = 16 x 64");
   red[threadIdx.x] = v;
   __syncthreads();
-  for (int o = CG_T / 2; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
+  if (threadIdx.x < 64) {
+    const double* q = red + threadIdx.x;
+    // b[k] = (v[k] + v[k + 8]) + (v[k + 4] + v[k + 12]) (in units of 64), one k at a time
+    auto quad = [&](int k) { return (q[64 * k] + q[64 * (k + 8)]) + (q[64 * (k + 4)] + q[64 * (k + 12)]); };
+    // (the fences keep the gathers one quad at a time: four doubles in flight, not
+    // sixteen, beside the CG kernels' register-resident vectors)
+    const double b0 = quad(0);
+    asm volatile("" ::: "memory");
+    const double c0 = b0 + quad(2);
+    asm volatile("" ::: "memory");
+    const double b1 = quad(1);
+    asm volatile("" ::: "memory");
+    double t = c0 + (b1 + quad(3));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_down(t, o, 64);
+    if (threadIdx.x == 0) red[CG_T] = t;
   }
-  const double r = red[0];
   __syncthreads();
-  return r;
+  return red[CG_T];
 }
 
 __global__ __launch_bounds__(CG_T) void cg_init_kernel(const double* __restrict__ b, int64_t n, double* x, double* r,
                                                        double* p, float* p32, double* ax, double* state,
                                                        int32_t* flag) {
-  __shared__ double red[CG_T];
+  __shared__ double red[CG_T + 1];
   double s = 0.0;
   for (int64_t i = threadIdx.x; i < n; i += CG_T) {
     const double bi = b[i];
@@ -283,7 +302,7 @@ __global__ __launch_bounds__(CG_T) void cg_init_kernel(const double* __restrict_
 __global__ __launch_bounds__(CG_T) void cg_update_kernel(const float* __restrict__ fvp, double damping, double tol,
                                                          int64_t n, double* x, double* r, double* p, float* p32,
                                                          double* ax, double* state, int32_t* flag) {
-  __shared__ double red[CG_T];
+  __shared__ double red[CG_T + 1];
   if (flag[0] != 0) return;
   const double rdotr = state[0];
   double s = 0.0;
@@ -323,12 +342,11 @@ __global__ __launch_bounds__(CG_T) void cg_update_kernel(const float* __restrict
 // (three dependent global passes of the plain kernel).  Per-thread accumulation
 // order and the block_sum tree are the plain kernel's, so the results are identical.
 // PACK: the next Fisher product's tangent image too -- the split image of p32
-// (split_image_word, as mlp_pack_split_kernel writes it), one launch instead of two
+// (split_image_item, as mlp_pack_split_kernel writes it), one launch instead of two
 struct CgPack {
   MlpDims d;
   BDims b;
   float* image;
-  int words;
 };
 
 template <int K, bool PACK = false>
@@ -336,20 +354,24 @@ __global__ __launch_bounds__(CG_T) void cg_update_reg_kernel(const float* __rest
                                                              int64_t n, double* x, double* r, double* p, float* p32,
                                                              double* ax, double* state, int32_t* flag,
                                                              CgPack pk = CgPack{}) {
-  __shared__ double red[CG_T];
+  __shared__ double red[CG_T + 1];
   if (flag[0] != 0) return;
   const double rdotr = state[0];
-  double pr[K], zr[K], rr[K], xr[K], ar[K];
+  // z = fvp + damping p is recomputed where it is used (the same value) from the f32 fvp
+  // kept in registers: 8 VGPRs fewer than a double z, no spills at CG_T threads
+  double pr[K], rr[K], xr[K], ar[K];
+  float fr[K];
   double s = 0.0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int64_t i = threadIdx.x + (int64_t)k * CG_T;
-    pr[k] = zr[k] = rr[k] = xr[k] = ar[k] = 0.0;
+    pr[k] = rr[k] = xr[k] = ar[k] = 0.0;
+    fr[k] = 0.f;
     if (i < n) {
       const double pi = p[i];
-      const double z = (double)fvp[i] + damping * pi;
+      fr[k] = fvp[i];
+      const double z = (double)fr[k] + damping * pi;
       pr[k] = pi;
-      zr[k] = z;
       rr[k] = r[i];
       xr[k] = x[i];
       if (ax) ar[k] = ax[i];
@@ -363,9 +385,10 @@ __global__ __launch_bounds__(CG_T) void cg_update_reg_kernel(const float* __rest
   for (int k = 0; k < K; ++k) {
     const int64_t i = threadIdx.x + (int64_t)k * CG_T;
     if (i < n) {
+      const double z = (double)fr[k] + damping * pr[k];
       x[i] = xr[k] + v * pr[k];
-      if (ax) ax[i] = ar[k] + v * zr[k];
-      const double ri = rr[k] - v * zr[k];
+      if (ax) ax[i] = ar[k] + v * z;
+      const double ri = rr[k] - v * z;
       r[i] = ri;
       rr[k] = ri;
       s += ri * ri;
@@ -389,15 +412,20 @@ __global__ __launch_bounds__(CG_T) void cg_update_reg_kernel(const float* __rest
     if (newr < tol) flag[0] = 1;
   }
   if constexpr (PACK) {
-    __syncthreads();  // p32 of the whole block is written (global, visible to the block)
-    for (int w = threadIdx.x; w < pk.words; w += CG_T) pk.image[w] = split_image_word(pk.d, pk.b, p32, w);
+    // the new p32 staged in LDS (8192 floats), read there by the image gathers
+    __shared__ float sp[8 * CG_T];
+#pragma unroll
+    for (int k = 0; k < K; ++k) sp[threadIdx.x + k * CG_T] = (float)(rr[k] + mu * pr[k]);
+    __syncthreads();
+    const int items = split_image_items(pk.b);
+    for (int u = threadIdx.x; u < items; u += CG_T) split_image_item(pk.d, pk.b, sp, pk.image, u);
   }
 }
 
 __global__ __launch_bounds__(CG_T) void trpo_step_kernel(const float* __restrict__ fvp, const double* __restrict__ x,
                                                          const float* __restrict__ g, double damping, double max_kl,
                                                          int64_t n, double* fullstep, double* out) {
-  __shared__ double red[CG_T];
+  __shared__ double red[CG_T + 1];
   double s = 0.0, sg = 0.0;
   for (int64_t i = threadIdx.x; i < n; i += CG_T) {
     s += x[i] * ((double)fvp[i] + damping * x[i]);
@@ -420,7 +448,7 @@ __global__ __launch_bounds__(CG_T) void trpo_step_kernel(const float* __restrict
 __global__ __launch_bounds__(CG_T) void trpo_step_ax_kernel(const double* __restrict__ ax, const double* __restrict__ x,
                                                             const float* __restrict__ g, double max_kl, int64_t n,
                                                             double* fullstep, double* out) {
-  __shared__ double red[CG_T];
+  __shared__ double red[CG_T + 1];
   double s = 0.0, sg = 0.0;
   for (int64_t i = threadIdx.x; i < n; i += CG_T) {
     s += x[i] * ax[i];
@@ -923,7 +951,6 @@ int mrl_cg_update_pack(const float* fvp, double damping, double residual_tol, in
   pk.d = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
   pk.b = bf16_dims(d->n_in, d->n_out);
   pk.image = image_t;
-  pk.words = (int)words;
   hipLaunchKernelGGL((cg_update_reg_kernel<8, true>), dim3(1), dim3(CG_T), 0, (hipStream_t)stream, fvp, damping,
                      residual_tol, n, x, r, p, p32, ax, state, flag, pk);
   return hip_check(hipGetLastError(), "mrl_cg_update_pack");

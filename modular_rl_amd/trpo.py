@@ -231,6 +231,26 @@ class TrpoUpdater:
         # set by core.IterationRunner: called once theta (and its image) is final, so the
         # next iteration's rollout is issued before the stats / host bookkeeping
         self.after_theta = None
+        # set by core.IterationRunner: device work that may run while the host waits for
+        # the update's readback (the next rollout's noise fill); issued after the copy
+        self.before_readback = None
+        self._host_buf = None
+
+    def _readback(self, dev):
+        """dev (float64, 1-D) to the host through a pinned buffer: the copy is ordered
+        first, then before_readback's work is issued behind it, and only the copy is
+        waited for -- that work runs under the host's line-search decision."""
+        n = dev.numel()
+        if self._host_buf is None or self._host_buf.numel() < n:
+            self._host_buf = torch.empty(max(n, 64), dtype=torch.float64, pin_memory=True)
+        h = self._host_buf[:n]
+        h.copy_(dev, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record()
+        if self.before_readback is not None:
+            self.before_readback()
+        done.synchronize()
+        return h.numpy().copy()
 
     # EzFlat surface (core.py:544-554)
     def get_params_flat(self):
@@ -282,7 +302,7 @@ class TrpoUpdater:
             ls_sums, ls_cand = ops.losses_batch(thprev, 0, K0)
             comm.allreduce_(ls_sums)
             parts.append(ls_sums.reshape(-1))
-        host = torch.cat(parts).cpu().numpy()
+        host = self._readback(torch.cat(parts)) if net.theta.is_cuda else torch.cat(parts).cpu().numpy()
         if abort is not None and host[11] != 0:
             raise _lib.MrlError("policy update on an aborted rollout: " + getattr(batch, "abort_msg", ""))
         if self.LS_BATCHES:
