@@ -64,6 +64,9 @@ class HipTrpoOps:
         self.cg_pack = (getattr(net, "fisher_split", False) and P <= 8192
                         and os.environ.get("MRL_CG_PACK", "1") != "0")
         self._tan_packed = False
+        # the product's slab reduction folded into the CG update (fvp_cg; single process)
+        self.cg_reduce = self.cg_pack and os.environ.get("MRL_CG_REDUCE", "1") != "0"
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         ns = int(_lib.load().mrl_cg_state_doubles(self.P))  # scalars + block partials (wide nets)
         self.state = torch.zeros(ns, **f64)
         self.flag = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -103,6 +106,7 @@ class HipTrpoOps:
         b, net = self.batch, self.net
         if not (self._tan_packed and v32 is self.p32):
             net.pack_tangent(v32, self.tan_image, skip=skip)
+            self._tan_packed = v32 is self.p32
         if getattr(net, "fisher_onepass", False) and net.fisher_onepass_applies(b.obs, b.n, self.tan_image):
             # the whole product in one launch (JVP rows and VJP side by side per block)
             timing.start("fvp_onepass")
@@ -117,6 +121,30 @@ class HipTrpoOps:
         net.vjp_flat(b.obs, b.n, self.ghead, self.fv, skip=skip)
         timing.stop("fvp_vjp")
         return self.fv
+
+    def fvp_cg(self, damping, tol):
+        """One CG iteration -- the Fisher product along p and the CG update -- as two
+        launches when the one-pass product applies (its slab rows reduced by the CG update
+        kernel, mrl_fvp_reduce_cg, which also packs the next tangent); otherwise False
+        (the caller runs fvp + cg_update).  Single process only: the product is not
+        all-reduced in between."""
+        b, net = self.batch, self.net
+        if not (self.cg_reduce and getattr(net, "fisher_onepass", False)):
+            return False
+        if not self._tan_packed:
+            net.pack_tangent(self.p32, self.tan_image, skip=self.flag)
+            self._tan_packed = True
+        if not net.fisher_onepass_applies(b.obs, b.n, self.tan_image):
+            return False
+        timing.start("fvp_onepass")
+        slab, rows = net.fisher_product(b.obs, b.n, self.inv_ng, self.p32, self.tan_image, self.fv, skip=self.flag,
+                                        reduce=False)
+        timing.stop("fvp_onepass")
+        call("mrl_fvp_reduce_cg", ptr(slab), int(rows), ptr(self.fv), ptr(self.ticket), float(damping), float(tol),
+             self.P, ptr(self.x), ptr(self.r), ptr(self.p), ptr(self.p32), ptr(self.ax), ptr(self.state),
+             ptr(self.flag), ctypes.byref(net.desc), ptr(self.tan_image), stream())
+        self._tan_packed = True
+        return True
 
     def neg_g64(self, g):
         call("mrl_cast_scale_f32_f64", ptr(g), -1.0, self.P, ptr(self.b), stream())
@@ -136,6 +164,7 @@ class HipTrpoOps:
             return
         call("mrl_cg_update", ptr(fv), float(damping), float(tol), self.P, ptr(self.x), ptr(self.r), ptr(self.p),
              ptr(self.p32), ptr(self.ax), ptr(self.state), ptr(self.flag), stream())
+        self._tan_packed = False
 
     def trpo_step(self, g, max_kl):
         """shs / lm / fullstep from the A x the CG updates accumulated (trpo.py:119-124)."""
@@ -281,6 +310,10 @@ class TrpoUpdater:
         damping, max_kl = float(cfg["cg_damping"]), float(cfg["max_kl"])
         ops.cg_init(ops.neg_g64(g))
         for _ in range(self.CG_ITERS):
+            # single process: the product's reduction, the CG update and the next tangent's
+            # pack in one launch after the product's
+            if not comm.enabled and hasattr(ops, "fvp_cg") and ops.fvp_cg(damping, self.RESIDUAL_TOL):
+                continue
             fv = ops.fvp(ops.p32, skip=ops.flag)
             comm.allreduce_(fv)
             ops.cg_update(fv, damping, self.RESIDUAL_TOL)
