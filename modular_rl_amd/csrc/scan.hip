@@ -349,7 +349,8 @@ struct CgPack {
   float* image;
 };
 
-template <int K, bool PACK>
+// COHERENT: fvp was written by other blocks of this launch (agent-scope atomic loads)
+template <int K, bool PACK, bool COHERENT = false>
 __device__ inline void cg_update_reg_body(const float* fvp, double damping, double tol, int64_t n, double* x,
                                           double* r, double* p, float* p32, double* ax, double* state, int32_t* flag,
                                           const CgPack& pk, double* red) {
@@ -366,7 +367,7 @@ __device__ inline void cg_update_reg_body(const float* fvp, double damping, doub
     fr[k] = 0.f;
     if (i < n) {
       const double pi = p[i];
-      fr[k] = fvp[i];
+      fr[k] = COHERENT ? __hip_atomic_load(fvp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : fvp[i];
       const double z = (double)fr[k] + damping * pi;
       pr[k] = pi;
       rr[k] = r[i];
@@ -464,17 +465,20 @@ __global__ __launch_bounds__(CG_T) void fvp_reduce_cg_kernel(const float* __rest
     if (g < w) part[g][c] += part[g + w][c];
     __syncthreads();
   }
-  if (g == 0 && col < n) fvp[col] = (float)part[0][c];
+  // The columns cross XCDs (each XCD has its own L2) without a device-scope fence (a
+  // fence writes back the whole L2, dirty with the product's slab): agent-scope atomic
+  // stores / loads of the columns go to the device's coherence point, the ticket is taken
+  // only once this block's stores have completed (vmcnt 0), and the last block reads the
+  // columns only after its ticket came back
+  if (g == 0 && col < n) __hip_atomic_store(fvp + col, (float)part[0][c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();  // this block's fvp columns, visible device-wide before its ticket
-    is_last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
-  }
+  if (threadIdx.x == 0)
+    is_last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
   __syncthreads();
   if (!is_last) return;
-  __threadfence();  // every block's columns (they were released before their tickets)
   if (threadIdx.x == 0) ticket[0] = 0;
-  cg_update_reg_body<8, PACK>(fvp, damping, tol, n, x, r, p, p32, ax, state, flag, pk, red);
+  cg_update_reg_body<8, PACK, true>(fvp, damping, tol, n, x, r, p, p32, ax, state, flag, pk, red);
 }
 
 __global__ __launch_bounds__(CG_T) void trpo_step_kernel(const float* __restrict__ fvp, const double* __restrict__ x,
