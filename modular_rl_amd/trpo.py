@@ -64,8 +64,11 @@ class HipTrpoOps:
         self.cg_pack = (getattr(net, "fisher_split", False) and P <= 8192
                         and os.environ.get("MRL_CG_PACK", "1") != "0")
         self._tan_packed = False
-        # the product's slab reduction folded into the CG update (fvp_cg; single process)
-        self.cg_reduce = self.cg_pack and os.environ.get("MRL_CG_REDUCE", "1") != "0"
+        # the product's slab reduction folded into the CG update too (fvp_cg; single
+        # process; MRL_CG_REDUCE=1).  Off by default: the CG iteration measures the same
+        # with two, three or four launches (tools/cg_probe.py, 1216 us at C3 size) -- the
+        # small launches' cost hides under the product's -- and three is the simpler layout
+        self.cg_reduce = self.cg_pack and os.environ.get("MRL_CG_REDUCE", "0") == "1"
         self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         ns = int(_lib.load().mrl_cg_state_doubles(self.P))  # scalars + block partials (wide nets)
         self.state = torch.zeros(ns, **f64)
