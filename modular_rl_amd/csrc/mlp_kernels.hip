@@ -1086,6 +1086,11 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
 // work with the VJP's MFMA chains.  One s_barrier per round (two mailbox slots); the
 // head-gradient rows never reach HBM.
 constexpr int MBOX_GH = 2 * MAX_OUT;  // mailbox row pitch (floats): the widest head-gradient row
+// diagnostic builds only (tools/role_probe.sh): 1 = the VJP role skips its tiles, 2 = the
+// JVP role does -- the launch time of the other role alone at the same barriers
+#ifndef MRL_FISHER_ROLE_PROBE
+#define MRL_FISHER_ROLE_PROBE 0
+#endif
 
 struct FisherFusedIn {
   RowsArgs ra;        // the JVP rows' arguments (x, n, inv_ng, logstd / dlogstd, cache)
@@ -1176,7 +1181,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
       int64_t T = (int64_t)blockIdx.x * 4 + wave;
       if (T < nt32) role.prologue(T);
       for (int64_t r = 0; r < rounds; ++r) {
-        if (r + 1 < rounds && T < nt32) {
+        if (MRL_FISHER_ROLE_PROBE != 2 && r + 1 < rounds && T < nt32) {
           const int64_t tn = T + stride32 < nt32 ? T + stride32 : T;  // the last tile re-reads itself
           float* mb = mbox + ((r & 1) * 4 + wave) * 32 * MBOX_GH + (lane & 31) * MBOX_GH;
           role.tile(T, tn, [&](bool valid, int64_t, const float (&z)[MAX_OUT], const float (&dz)[MAX_OUT]) {
@@ -1429,7 +1434,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
     }
     fused_barrier();  // round 0: the JVP waves fill slot 0
     for (int64_t r = 1; r < rounds; ++r) {
-      if (T < nt32) {
+      if (MRL_FISHER_ROLE_PROBE != 1 && T < nt32) {
         mbt = mbox + (((r - 1) & 1) * 4 + vw) * 32 * MBOX_GH;
         const int64_t Tn = T + stride32 < nt32 ? T + stride32 : T;  // the last tile re-reads itself
 #pragma unroll 1
