@@ -455,6 +455,7 @@ def test_fvp_reduce_cg_matches_reduce_then_update(head, nin, nout, N, monkeypatc
     outs = []
     for fused in (False, True):
         ops = HipTrpoOps(net)
+        ops.cg_reduce = fused  # opt-in layout (MRL_CG_REDUCE=1)
         ops.bind(bt, 1.0 / N)
         ops.surrgrad()  # the SURRGRAD pass records the activation cache of these rows
         ops.cg_init(g)
