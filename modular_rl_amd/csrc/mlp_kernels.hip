@@ -1087,7 +1087,8 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 2) void mlp_vjp16_kernel(VjpArgs 
 // head-gradient rows never reach HBM.
 constexpr int MBOX_GH = 2 * MAX_OUT;  // mailbox row pitch (floats): the widest head-gradient row
 // diagnostic builds only (tools/role_probe.sh): 1 = the VJP role skips its tiles, 2 = the
-// JVP role does -- the launch time of the other role alone at the same barriers
+// JVP role does -- the launch time of the other role alone at the same barriers; 3 = no
+// barrier between the rounds (wrong results: the cost of the rounds' lockstep)
 #ifndef MRL_FISHER_ROLE_PROBE
 #define MRL_FISHER_ROLE_PROBE 0
 #endif
@@ -1162,7 +1163,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
   const int64_t rounds = (nt32 + stride32 - 1) / stride32 + 1;
   auto fused_barrier = []() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's mailbox writes / reads are done
-    __builtin_amdgcn_s_barrier();
+    if (MRL_FISHER_ROLE_PROBE != 3) __builtin_amdgcn_s_barrier();  // 3: timing build without the rounds' barrier
     asm volatile("" ::: "memory");
   };
   {
