@@ -370,7 +370,11 @@ class IterationRunner:
             ev["upd1"] = self._event()
             # pipelined: the VF of this iteration is fitted during the next step and added
             # to the capture then; in order it is final already
-            post["cap"] = capture_state(agent, with_vf=not self.pipeline, host=False, theta=False)
+            # the state the next rollout advances: taken under the readback already when
+            # before_readback ran (nothing changes it in between), else here
+            early = post.pop("cap_early", None)
+            post["cap"] = early if early is not None else capture_state(agent, with_vf=not self.pipeline,
+                                                                       host=False, theta=False)
             if prelaunch_next:
                 self._prelaunched = self._launch_rollout(noise_ready=post.pop("noise", False))
             # theta (the rollout only reads it), numpy's RNG and the updater's arrays:
@@ -380,11 +384,14 @@ class IterationRunner:
 
         def before_readback():
             """The next rollout's noise (a function of the collector's iteration counter,
-            which this iteration's rollout has advanced already): issued behind the
-            update's readback, it runs while the host decides the line search."""
+            which this iteration's rollout has advanced already) and the snapshot copies of
+            the state that rollout advances (filter state, RNG counters: final since this
+            iteration's rollout): issued behind the update's readback, they run while the
+            host decides the line search."""
             if prelaunch_next and self.pipeline and "cap" not in post:
                 col.fill_noise()
                 post["noise"] = True
+                post["cap_early"] = capture_state(agent, with_vf=False, host=False, theta=False)
 
         upd = agent.updater
         upd.after_theta = after_theta
