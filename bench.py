@@ -383,7 +383,10 @@ def main():
         for i in range(args.warmup):
             runner.step(prelaunch_next=i + 1 < args.warmup)
         runner.drain()
-    timing.enable(True)
+    # the many per-iteration launch regions (Fisher products, VJPs, GEMMs) on every 4th
+    # timed iteration (each event is a queue marker that delays the next kernel), the
+    # rollout and the GAE scan on every one (modular_rl_amd/timing.py)
+    timing.enable(True, detail_every=4)
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -391,6 +394,7 @@ def main():
     # VF fit drains inside the timed region)
     with runner.loop_stream():
         for i in range(args.steps):
+            timing.tick()
             runner.step(prelaunch_next=i + 1 < args.steps)  # the next rollout issued as theta is final
             recs.append(runner.last_phase_events)
         runner.drain()
@@ -404,10 +408,15 @@ def main():
         elapsed = float(t.item())
     kern = timing.summary()
     timing.enable(False)
+    nph = {k: 0 for k in phases}
     for ev in recs:
         for k, (a, b) in spans.items():
-            if a in ev and b in ev:
+            # (the first timed iteration's rollout was issued in the warmup, untimed)
+            if ev.get(a) is not None and ev.get(b) is not None:
                 phases[k] += ev[a].elapsed_time(ev[b])
+                nph[k] += 1
+    # per-iteration phase times over the iterations that timed them, scaled to K
+    phases = {k: (v / nph[k] * args.steps if nph[k] else 0.0) for k, v in phases.items()}
     K = args.steps
     n_local = E * Tn
     total_steps = n_local * world * K

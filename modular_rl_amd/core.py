@@ -227,6 +227,7 @@ class IterationRunner:
         self._prelaunched = None  # events of a rollout issued by the previous step
         self.pipeline = False
         self.last_phase_events = None
+        self.record_phases = False
         self.last_drain_events = {}
         if torch.cuda.is_available():
             from . import streams
@@ -284,6 +285,11 @@ class IterationRunner:
         return stats
 
     def _event(self):
+        """A phase boundary's timing event -- only while timing is enabled (bench.py's timed
+        region) or record_phases is set: each one is a queue marker that delays the next
+        kernel by ≈6 µs (modular_rl_amd/timing.py)."""
+        if not (self.record_phases or timing.enabled()):
+            return None
         e = torch.cuda.Event(enable_timing=True)
         e.record()
         return e

@@ -90,7 +90,7 @@ class HipTrpoOps:
         net.rows(_lib.EPI_SURRGRAD, b.obs, b.n, inv_n_global=self.inv_ng, act=b.act, adv=b.adv, oldprob=b.prob,
                  ghead=self.ghead, partial=self.partial)
         net.reduce_partial(self.partial, b.n, self.sums)
-        timing.start("pg_vjp")
+        timing.start("pg_vjp", detail=True)
         net.vjp_flat(b.obs, b.n, self.ghead, self.g)
         timing.stop("pg_vjp")
         return self.g, self.sums
@@ -112,15 +112,15 @@ class HipTrpoOps:
             self._tan_packed = v32 is self.p32
         if getattr(net, "fisher_onepass", False) and net.fisher_onepass_applies(b.obs, b.n, self.tan_image):
             # the whole product in one launch (JVP rows and VJP side by side per block)
-            timing.start("fvp_onepass")
+            timing.start("fvp_onepass", detail=True)
             net.fisher_product(b.obs, b.n, self.inv_ng, v32, self.tan_image, self.fv, skip=skip)
             timing.stop("fvp_onepass")
             return self.fv
-        timing.start("fvp_jvp_rows")
+        timing.start("fvp_jvp_rows", detail=True)
         net.rows(_lib.EPI_FVP, b.obs, b.n, inv_n_global=self.inv_ng, ghead=self.ghead, tangent=v32,
                  image_t=self.tan_image, skip=skip)
         timing.stop("fvp_jvp_rows")
-        timing.start("fvp_vjp")
+        timing.start("fvp_vjp", detail=True)
         net.vjp_flat(b.obs, b.n, self.ghead, self.fv, skip=skip)
         timing.stop("fvp_vjp")
         return self.fv
@@ -139,7 +139,7 @@ class HipTrpoOps:
             self._tan_packed = True
         if not net.fisher_onepass_applies(b.obs, b.n, self.tan_image):
             return False
-        timing.start("fvp_onepass")
+        timing.start("fvp_onepass", detail=True)
         slab, rows = net.fisher_product(b.obs, b.n, self.inv_ng, self.p32, self.tan_image, self.fv, skip=self.flag,
                                         reduce=False)
         timing.stop("fvp_onepass")

@@ -72,7 +72,7 @@ class LbfgsOptimizer:
                  ghead=ghead, partial=partial)
         net.reduce_partial(partial, n, self.sums)
         if with_grad:
-            timing.start("vf_vjp")
+            timing.start("vf_vjp", detail=True)
             net.vjp_flat(x, n, ghead, self.g, ep_t=ep_t, timestep_limit=limit)
             timing.stop("vf_vjp")
             self.comm.allreduce_(self.g)

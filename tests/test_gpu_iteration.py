@@ -19,6 +19,7 @@ def _run(env_id, pipeline, n_iter=3, agent_cls="TrpoAgent", prelaunch=False, **k
     agent = getattr(agentzoo, agent_cls)(env.observation_space, env.action_space, cfg)
     col = agent.make_collector(env, cfg)
     runner = IterationRunner(agent, col, cfg, pipeline=pipeline)
+    runner.record_phases = True  # the phase events (off by default outside timed measurements)
     stats = []
     with runner.loop_stream():
         for i in range(n_iter):
