@@ -92,7 +92,7 @@ def compute_advantage_batch(vf, batch, gamma, lam, comm=None):
         batch.adv = torch.empty(n, dtype=torch.float32, device=dev)
         batch.ret = torch.empty(n, dtype=torch.float32, device=dev)
     ws, moments = _GAE.get(batch.T, batch.E, dev)
-    timing.start("gae_scan")
+    timing.start("gae_scan", detail=True)
     call("mrl_gae", ptr(batch.rew), ptr(batch.vpred), ptr(batch.flags), int(batch.T), int(batch.E), float(gamma),
          float(lam), ptr(batch.adv), ptr(batch.ret), ptr(moments), ptr(ws), stream())
     timing.stop("gae_scan")
@@ -285,10 +285,10 @@ class IterationRunner:
         return stats
 
     def _event(self):
-        """A phase boundary's timing event -- only while timing is enabled (bench.py's timed
-        region) or record_phases is set: each one is a queue marker that delays the next
-        kernel by ≈6 µs (modular_rl_amd/timing.py)."""
-        if not (self.record_phases or timing.enabled()):
+        """A phase boundary's timing event -- only on the iterations timing samples (bench.py's
+        timed region) or when record_phases is set: each one is a queue marker that delays
+        the next kernel by ≈6 µs (modular_rl_amd/timing.py)."""
+        if not (self.record_phases or timing.detail_now()):
             return None
         e = torch.cuda.Event(enable_timing=True)
         e.record()

@@ -6,9 +6,9 @@ device duration of the dominant kernels live inside the timed region.
 Every recorded event is a marker packet in the stream's queue, and the kernel after it
 starts ≈6 µs later (rocprofv3: the CG loop's launches run back to back untimed, 6 µs apart
 with a region around each product).  Regions marked ``detail`` (the many per-iteration
-launches: Fisher products, VJPs, layered GEMMs) are therefore recorded only on every
-``detail_every``-th iteration (``tick()`` once per iteration), and summary() scales their
-totals to all iterations; the other regions (the rollout, the GAE scan) every iteration.
+launches: Fisher products, VJPs, layered GEMMs, the GAE scan) are therefore recorded only
+on every ``detail_every``-th iteration (``tick()`` once per iteration), and summary()
+scales their totals to all iterations; the rollout's region every iteration.
 """
 import collections
 
@@ -51,6 +51,11 @@ def tick():
 
 def _detail_now():
     return _iters == 0 or (_iters - 1) % _every == 0
+
+
+def detail_now():
+    """Timing is on and this iteration records detail regions."""
+    return _ENABLED and _detail_now()
 
 
 def start(name, detail=False):
