@@ -321,16 +321,6 @@ int mrl_cg_update(const float* fvp, double damping, double residual_tol, int64_t
 int mrl_cg_update_pack(const float* fvp, double damping, double residual_tol, int64_t n, double* x, double* r,
                        double* p, float* p32, double* ax, double* state, int32_t* flag, const mrl_mlp_desc* d,
                        float* image_t, void* stream);
-/* One CG iteration's tail in one launch (single process: no all-reduce of the product):
- * fvp[n] <- the column sums of slab[rows][n] (the one-pass Fisher product's per-wave
- * rows, summed as mrl_reduce_rows_f32 sums them), then the mrl_cg_update step on it
- * (the last block to finish its columns runs it), and -- d != NULL -- the next tangent's
- * split image as mrl_cg_update_pack writes it.  ticket: one int32, 0 before the first
- * call (every call leaves it 0).  n <= 8192, else E_UNSUPPORTED.  Skipped entirely once
- * flag[0] is set (cg.py's early exit). */
-int mrl_fvp_reduce_cg(const float* slab, int64_t rows, float* fvp, int32_t* ticket, double damping,
-                      double residual_tol, int64_t n, double* x, double* r, double* p, float* p32, double* ax,
-                      double* state, int32_t* flag, const mrl_mlp_desc* d, float* image_t, void* stream);
 /* step scaling (trpo.py:119-124): shs = .5 x.(fvp + damping x), lm = sqrt(shs/max_kl),
  * fullstep = x/lm, out[0]=shs out[1]=lm out[2]=-g.x out[3]=-g.x/lm (expected rate) */
 int mrl_trpo_step(const float* fvp, const double* x, const float* g, double damping, double max_kl,

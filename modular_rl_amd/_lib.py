@@ -117,7 +117,6 @@ SIGNATURES = {
     "mrl_cg_init": (i32, [vp, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_cg_update": (i32, [vp, f64, f64, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_cg_update_pack": (i32, [vp, f64, f64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
-    "mrl_fvp_reduce_cg": (i32, [vp, i64, vp, vp, f64, f64, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_trpo_step": (i32, [vp, vp, vp, f64, f64, i64, vp, vp, vp]),
     "mrl_trpo_step_ax": (i32, [vp, vp, vp, f64, i64, vp, vp, vp]),
     "mrl_device_cu_count": (i32, [vp]),

@@ -349,8 +349,7 @@ struct CgPack {
   float* image;
 };
 
-// COHERENT: fvp was written by other blocks of this launch (agent-scope atomic loads)
-template <int K, bool PACK, bool COHERENT = false>
+template <int K, bool PACK>
 __device__ inline void cg_update_reg_body(const float* fvp, double damping, double tol, int64_t n, double* x,
                                           double* r, double* p, float* p32, double* ax, double* state, int32_t* flag,
                                           const CgPack& pk, double* red) {
@@ -367,7 +366,7 @@ __device__ inline void cg_update_reg_body(const float* fvp, double damping, doub
     fr[k] = 0.f;
     if (i < n) {
       const double pi = p[i];
-      fr[k] = COHERENT ? __hip_atomic_load(fvp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : fvp[i];
+      fr[k] = fvp[i];
       const double z = (double)fr[k] + damping * pi;
       pr[k] = pi;
       rr[k] = r[i];
@@ -430,56 +429,6 @@ __global__ __launch_bounds__(CG_T) void cg_update_reg_kernel(const float* __rest
   cg_update_reg_body<K, PACK>(fvp, damping, tol, n, x, r, p, p32, ax, state, flag, pk, red);
 }
 
-// The Fisher product's slab reduction (per-wave rows of the one-pass product, rows x n)
-// and the CG update in one launch: every block sums its 64 columns over the rows as
-// reduce_rows_kernel<float, float, 16> does (the same order: the same fvp bits), writes
-// them to fvp and takes a ticket; the block that takes the last ticket runs the CG update
-// (and the tangent pack) on the whole fvp -- one dependent launch boundary fewer per CG
-// iteration.  Single process only (a multi-process product is all-reduced in between).
-// ticket: one int32, 0 at launch, left 0.
-template <bool PACK>
-__global__ __launch_bounds__(CG_T) void fvp_reduce_cg_kernel(const float* __restrict__ slab, int64_t rows,
-                                                             float* fvp, int32_t* ticket, double damping, double tol,
-                                                             int64_t n, double* x, double* r, double* p, float* p32,
-                                                             double* ax, double* state, int32_t* flag, CgPack pk) {
-  constexpr int RG = CG_T / 64;
-  __shared__ double part[RG][64];
-  __shared__ double red[CG_T + 1];
-  __shared__ int is_last;
-  if (flag[0] != 0) return;
-  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int64_t col = (int64_t)blockIdx.x * 64 + c;
-  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (col < n) {
-    int64_t rr = g;
-    for (; rr + 7 * RG < rows; rr += 8 * RG) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) s[q] += (double)slab[(rr + RG * q) * n + col];
-    }
-    for (; rr < rows; rr += RG) s[0] += (double)slab[rr * n + col];
-  }
-  part[g][c] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-  __syncthreads();
-#pragma unroll
-  for (int w = RG / 2; w >= 1; w >>= 1) {
-    if (g < w) part[g][c] += part[g + w][c];
-    __syncthreads();
-  }
-  // The columns cross XCDs (each XCD has its own L2) without a device-scope fence (a
-  // fence writes back the whole L2, dirty with the product's slab): agent-scope atomic
-  // stores / loads of the columns go to the device's coherence point, the ticket is taken
-  // only once this block's stores have completed (vmcnt 0), and the last block reads the
-  // columns only after its ticket came back
-  if (g == 0 && col < n) __hip_atomic_store(fvp + col, (float)part[0][c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    is_last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!is_last) return;
-  if (threadIdx.x == 0) ticket[0] = 0;
-  cg_update_reg_body<8, PACK, true>(fvp, damping, tol, n, x, r, p, p32, ax, state, flag, pk, red);
-}
 
 __global__ __launch_bounds__(CG_T) void trpo_step_kernel(const float* __restrict__ fvp, const double* __restrict__ x,
                                                          const float* __restrict__ g, double damping, double max_kl,
@@ -1013,33 +962,6 @@ int mrl_cg_update_pack(const float* fvp, double damping, double residual_tol, in
   hipLaunchKernelGGL((cg_update_reg_kernel<8, true>), dim3(1), dim3(CG_T), 0, (hipStream_t)stream, fvp, damping,
                      residual_tol, n, x, r, p, p32, ax, state, flag, pk);
   return hip_check(hipGetLastError(), "mrl_cg_update_pack");
-}
-
-int mrl_fvp_reduce_cg(const float* slab, int64_t rows, float* fvp, int32_t* ticket, double damping,
-                      double residual_tol, int64_t n, double* x, double* r, double* p, float* p32, double* ax,
-                      double* state, int32_t* flag, const mrl_mlp_desc* d, float* image_t, void* stream) {
-  if (!slab || !fvp || !ticket || !x || !r || !p || !p32 || !state || !flag) return fail(E_ARG, "null pointer");
-  if (rows <= 0) return fail(E_ARG, "mrl_fvp_reduce_cg: no slab rows");
-  if (!(MRL_CG_REG && n > 0 && n <= CG_SMALL_N && n <= 8 * CG_T))
-    return fail(E_UNSUPPORTED, "mrl_fvp_reduce_cg: the single-block register CG update only (n <= 8192)");
-  CgPack pk{};
-  const bool pack = d != nullptr;
-  if (pack) {
-    if (!image_t) return fail(E_ARG, "mrl_fvp_reduce_cg: null tangent image");
-    if (mrl_mlp_image_words_split(d) < 0) return fail(E_UNSUPPORTED, "mrl_fvp_reduce_cg: no split image for this net");
-    if (mrl_mlp_num_params(d) != n) return fail(E_ARG, "mrl_fvp_reduce_cg: n is not the net's parameter count");
-    pk.d = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
-    pk.b = bf16_dims(d->n_in, d->n_out);
-    pk.image = image_t;
-  }
-  const dim3 grid((unsigned)((n + 63) / 64));
-  if (pack)
-    hipLaunchKernelGGL(fvp_reduce_cg_kernel<true>, grid, dim3(CG_T), 0, (hipStream_t)stream, slab, rows, fvp, ticket,
-                       damping, residual_tol, n, x, r, p, p32, ax, state, flag, pk);
-  else
-    hipLaunchKernelGGL(fvp_reduce_cg_kernel<false>, grid, dim3(CG_T), 0, (hipStream_t)stream, slab, rows, fvp,
-                       ticket, damping, residual_tol, n, x, r, p, p32, ax, state, flag, pk);
-  return hip_check(hipGetLastError(), "mrl_fvp_reduce_cg");
 }
 
 int mrl_trpo_step(const float* fvp, const double* x, const float* g, double damping, double max_kl, int64_t n,

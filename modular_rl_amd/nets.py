@@ -274,14 +274,12 @@ class MlpNet:
         return bool(self.fisher_onepass and getattr(image_t, "_mrl_split", False) and self.use_cache
                     and self._cache_key == self._key(x, n, None, 1.0))
 
-    def fisher_product(self, x, n, inv_n_global, tangent, image_t, out, skip=None, reduce=True):
+    def fisher_product(self, x, n, inv_n_global, tangent, image_t, out, skip=None):
         """out[P] <- the Fisher product along ``tangent`` over the n cached rows in ONE
         launch (mrl_mlp_fisher_hyb: split JVP rows and hybrid VJP side by side in each
         block, the head-gradient rows through LDS) when it applies -- a split tangent image,
         a current activation cache of these rows, a shape mrl_mlp_fisher_hyb_fits accepts.
-        False: not applicable (the caller runs rows(EPI_FVP) + vjp_flat).  reduce=False:
-        the per-wave slab rows are left unreduced and (slab, rows) returned (the CG update
-        reduces them itself, mrl_fvp_reduce_cg)."""
+        False: not applicable (the caller runs rows(EPI_FVP) + vjp_flat)."""
         if not self.fisher_onepass_applies(x, n, image_t):
             return False
         rows = int(self.lib.mrl_mlp_slab_rows(ctypes.byref(self.desc), int(n)))
@@ -290,8 +288,6 @@ class MlpNet:
                          None, 0.0, 0.0, 0.0, 0, _lib.CACHE_READ, ptr(self._cache(n)), None)
         call("mrl_mlp_fisher_hyb", ctypes.byref(self.desc), ptr(self.theta), ptr(self.image), ptr(self.image_s),
              ptr(tangent), ptr(image_t), ctypes.byref(io), ptr(slab), ptr(skip), stream())
-        if not reduce:
-            return slab, rows
         call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
         return True
 

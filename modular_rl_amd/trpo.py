@@ -61,15 +61,8 @@ class HipTrpoOps:
         self.tan_image = net.new_tangent_image()
         # the CG update writes the next tangent's split image itself (mrl_cg_update_pack):
         # the Fisher product then skips its pack launch
-        self.cg_pack = (getattr(net, "fisher_split", False) and P <= 8192
-                        and os.environ.get("MRL_CG_PACK", "1") != "0")
+        self.cg_pack = getattr(net, "fisher_split", False) and P <= 8192
         self._tan_packed = False
-        # the product's slab reduction folded into the CG update too (fvp_cg; single
-        # process; MRL_CG_REDUCE=1).  Off by default: the CG iteration measures the same
-        # with two, three or four launches (tools/cg_probe.py, 1216 us at C3 size) -- the
-        # small launches' cost hides under the product's -- and three is the simpler layout
-        self.cg_reduce = self.cg_pack and os.environ.get("MRL_CG_REDUCE", "0") == "1"
-        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         ns = int(_lib.load().mrl_cg_state_doubles(self.P))  # scalars + block partials (wide nets)
         self.state = torch.zeros(ns, **f64)
         self.flag = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -124,30 +117,6 @@ class HipTrpoOps:
         net.vjp_flat(b.obs, b.n, self.ghead, self.fv, skip=skip)
         timing.stop("fvp_vjp")
         return self.fv
-
-    def fvp_cg(self, damping, tol):
-        """One CG iteration -- the Fisher product along p and the CG update -- as two
-        launches when the one-pass product applies (its slab rows reduced by the CG update
-        kernel, mrl_fvp_reduce_cg, which also packs the next tangent); otherwise False
-        (the caller runs fvp + cg_update).  Single process only: the product is not
-        all-reduced in between."""
-        b, net = self.batch, self.net
-        if not (self.cg_reduce and getattr(net, "fisher_onepass", False)):
-            return False
-        if not self._tan_packed:
-            net.pack_tangent(self.p32, self.tan_image, skip=self.flag)
-            self._tan_packed = True
-        if not net.fisher_onepass_applies(b.obs, b.n, self.tan_image):
-            return False
-        timing.start("fvp_onepass", detail=True)
-        slab, rows = net.fisher_product(b.obs, b.n, self.inv_ng, self.p32, self.tan_image, self.fv, skip=self.flag,
-                                        reduce=False)
-        timing.stop("fvp_onepass")
-        call("mrl_fvp_reduce_cg", ptr(slab), int(rows), ptr(self.fv), ptr(self.ticket), float(damping), float(tol),
-             self.P, ptr(self.x), ptr(self.r), ptr(self.p), ptr(self.p32), ptr(self.ax), ptr(self.state),
-             ptr(self.flag), ctypes.byref(net.desc), ptr(self.tan_image), stream())
-        self._tan_packed = True
-        return True
 
     def neg_g64(self, g):
         call("mrl_cast_scale_f32_f64", ptr(g), -1.0, self.P, ptr(self.b), stream())
@@ -313,10 +282,6 @@ class TrpoUpdater:
         damping, max_kl = float(cfg["cg_damping"]), float(cfg["max_kl"])
         ops.cg_init(ops.neg_g64(g))
         for _ in range(self.CG_ITERS):
-            # single process: the product's reduction, the CG update and the next tangent's
-            # pack in one launch after the product's
-            if not comm.enabled and hasattr(ops, "fvp_cg") and ops.fvp_cg(damping, self.RESIDUAL_TOL):
-                continue
             fv = ops.fvp(ops.p32, skip=ops.flag)
             comm.allreduce_(fv)
             ops.cg_update(fv, damping, self.RESIDUAL_TOL)

@@ -420,55 +420,3 @@ def test_cg_update_pack_refuses_wide_nets_and_mismatched_sizes(monkeypatch):
     assert lib.mrl_cg_update_pack(*args(P + 1)) == -1  # MRL_E_ARG
     assert lib.mrl_cg_update_pack(*args(9000)) == -2  # MRL_E_UNSUPPORTED
     torch.cuda.synchronize()
-
-
-@pytest.mark.parametrize("head,nin,nout", [("gauss", 11, 3), ("softmax", 4, 2)])
-@pytest.mark.parametrize("N", [33, 70001])
-def test_fvp_reduce_cg_matches_reduce_then_update(head, nin, nout, N, monkeypatch):
-    """mrl_fvp_reduce_cg (the one-pass product's slab reduction, the CG update and the
-    tangent pack in one launch, the last block to finish running the update) against
-    mrl_reduce_rows_f32 + mrl_cg_update_pack: every output bit-identical over three CG
-    iterations (the ticket is left 0 by every launch)."""
-    monkeypatch.setenv("MRL_FISHER", "split")
-    from modular_rl_amd import _lib
-    from modular_rl_amd.nets import MlpNet
-    from modular_rl_amd.trpo import HipTrpoOps
-    rng = np.random.default_rng(N + nin)
-    spec = T.Spec(nin, [64, 64], nout, head)
-    th = T.mlp_init(rng, spec.shapes, head == "gauss") + 0.05 * rng.standard_normal(spec.P)
-    net = MlpNet(nin, nout, _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX)
-    if not net.fisher_onepass:
-        pytest.skip("one-pass product not available for this shape")
-    th = th.astype(np.float32).astype(np.float64)
-    net.set_flat(th)
-    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
-    oldprob = T.policy_prob(spec, th + 0.01 * rng.standard_normal(spec.P), ob).astype(np.float32).astype(np.float64)
-    act = T.sample(spec, oldprob, rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N))
-
-    class B:
-        pass
-    bt = B()
-    bt.obs, bt.n = _dev(ob), N
-    bt.act = _dev(act, torch.int32 if head == "softmax" else torch.float32)
-    bt.adv, bt.prob = _dev(rng.standard_normal(N)), _dev(oldprob)
-    g = _dev(rng.standard_normal(net.P), torch.float64)
-    outs = []
-    for fused in (False, True):
-        ops = HipTrpoOps(net)
-        ops.cg_reduce = fused  # opt-in layout (MRL_CG_REDUCE=1)
-        ops.bind(bt, 1.0 / N)
-        ops.surrgrad()  # the SURRGRAD pass records the activation cache of these rows
-        ops.cg_init(g)
-        for _ in range(3):
-            if fused:
-                assert ops.fvp_cg(1e-3, 1e-10)
-            else:
-                ops.cg_update(ops.fvp(ops.p32, skip=ops.flag), 1e-3, 1e-10)
-        torch.cuda.synchronize()
-        outs.append({k: getattr(ops, k).cpu().numpy().copy()
-                     for k in ("fv", "x", "r", "p", "p32", "ax", "state", "tan_image")})
-        if fused:
-            assert int(ops.ticket.item()) == 0
-    for k in outs[0]:
-        a, b = outs[0][k], outs[1][k]
-        assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), k

@@ -1,8 +1,9 @@
 """Time the conjugate-gradient loop's iteration at the Hopper C3 size (4,194,304 rows):
-one-pass Fisher product + CG update in the three launch layouts -- product, slab
-reduction, CG update, tangent pack (four launches); the CG update packing the tangent
-(three, mrl_cg_update_pack); the reduction inside the CG update (two,
-mrl_fvp_reduce_cg) -- HIP events on the launch stream over many iterations, no profiler.
+one-pass Fisher product + CG update in two launch layouts -- product, slab reduction,
+CG update, tangent pack (four launches); the CG update packing the tangent (three,
+mrl_cg_update_pack) -- HIP events on the launch stream over many iterations, no profiler.
+(Round 5 also measured a two-launch form with the reduction inside the CG update:
+1218 us, the same; not kept, profiles/r05w_cg_probe.txt.)
 Also a chain of tiny kernels (pack launches) to show the per-launch cost of a dependent
 launch on this runtime."""
 import os
@@ -55,26 +56,24 @@ ops.surrgrad()
 g64 = ops.g.double()
 
 
-def layout(pack, red):
-    ops.cg_pack, ops.cg_reduce = pack, red
+def layout(pack):
+    ops.cg_pack = pack
 
     def it():
-        # restart CG so the flag never stops the loop (tol 0: never converges)
-        if not ops.fvp_cg(1e-3, 0.0):
-            ops.cg_update(ops.fvp(ops.p32, skip=ops.flag), 1e-3, 0.0)
+        # tol 0: CG never converges, so the flag never stops the loop
+        ops.cg_update(ops.fvp(ops.p32, skip=ops.flag), 1e-3, 0.0)
     ops.cg_init(g64)
     return it
 
 
-LAYOUTS = (("4 launches (pack, product, reduce, update)", False, False),
-           ("3 launches (update packs)", True, False),
-           ("2 launches (update reduces and packs)", True, True))
-res = {name: [] for name, _, _ in LAYOUTS}
-timed(layout(True, True), 50)  # clocks up
+LAYOUTS = (("4 launches (pack, product, reduce, update)", False),
+           ("3 launches (update packs)", True))
+res = {name: [] for name, _ in LAYOUTS}
+timed(layout(True), 50)  # clocks up
 for rnd in range(4):  # rotated, so clock drift does not favour one layout
-    for name, pack, red in LAYOUTS:
-        res[name].append(timed(layout(pack, red), 8) * 1e3)  # CG stays finite over a few iterations
-for name, _, _ in LAYOUTS:
+    for name, pack in LAYOUTS:
+        res[name].append(timed(layout(pack), 8) * 1e3)  # CG stays finite over a few iterations
+for name, _ in LAYOUTS:
     print(f"{name:45s} median {np.median(res[name]):8.1f} us per CG iteration  "
           f"({' '.join(f'{v:.1f}' for v in res[name])})", flush=True)
 
