@@ -25,7 +25,6 @@ In data-parallel mode every sum above is all-reduced over ranks (dist.Comm)
 before it is used, so all ranks take the identical step.
 """
 import ctypes
-import os
 from collections import OrderedDict
 
 import numpy as np
