@@ -124,3 +124,29 @@ def test_rollout_cu_split(monkeypatch):
     monkeypatch.setenv("MRL_FIT_CUS", "96")
     r, f = rollout_cu_split(64, 256)
     assert r == list(range(64)) and f == list(range(64, 160))
+
+
+def test_timing_samples_detail_regions_every_nth_iteration():
+    """bench.py's timing: per-launch ("detail") regions and the phase events only on every
+    detail_every-th iteration (each HIP timing event is a queue marker that delays the
+    next kernel); the bookkeeping alone, no events recorded (no GPU here)."""
+    from modular_rl_amd import timing
+    timing.enable(True, detail_every=4)
+    try:
+        seen = []
+        for _ in range(9):
+            timing.tick()
+            seen.append(timing.detail_now())
+        assert seen == [True, False, False, False, True, False, False, False, True]
+        assert timing._iters == 9 and timing._detail_iters == 3
+        # an unsampled iteration records nothing for a detail region and drop_last leaves
+        # the sampled iterations' records alone
+        timing.tick()
+        assert not timing.detail_now()
+        timing._events["fvp_onepass"].append(("a", "b"))
+        timing._detail_names.add("fvp_onepass")
+        timing.drop_last("fvp_onepass", 1)
+        assert len(timing._events["fvp_onepass"]) == 1
+    finally:
+        timing.enable(False)
+    assert not timing.detail_now()
