@@ -510,6 +510,12 @@ int mrl_device_cu_count(int32_t* out);
 int mrl_stream_create_cu_mask(const uint32_t* mask, int32_t words, void** stream_out);
 int mrl_stream_get_cu_mask(void* stream, int32_t words, uint32_t* mask);
 int mrl_stream_destroy(void* stream);
+/* cross-stream ordering on a memory value: mrl_stream_signal enqueues "flag = value" on the
+ * producer's stream (after its prior work), mrl_stream_wait makes the consumer's stream
+ * wait until flag >= value.  flag: device memory written by one producer stream only, with
+ * increasing values; the signal is enqueued before the wait. */
+int mrl_stream_signal(void* stream, uint32_t* flag, uint32_t value);
+int mrl_stream_wait(void* stream, uint32_t* flag, uint32_t value);
 
 #ifdef __cplusplus
 }

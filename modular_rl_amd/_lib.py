@@ -123,6 +123,8 @@ SIGNATURES = {
     "mrl_stream_create_cu_mask": (i32, [vp, i32, vp]),
     "mrl_stream_get_cu_mask": (i32, [vp, i32, vp]),
     "mrl_stream_destroy": (i32, [vp]),
+    "mrl_stream_signal": (i32, [vp, vp, ctypes.c_uint32]),
+    "mrl_stream_wait": (i32, [vp, vp, ctypes.c_uint32]),
     "mrl_axpy_cast": (i32, [vp, vp, f64, i64, vp, vp]),
     "mrl_linesearch_candidates": (i32, [vp, vp, i32, i32, i64, vp, vp]),
     "mrl_linesearch_eval": (i32, [vp, i32, vp, vp, i32, i32, vp, vp, vp, i64, vp, i64, vp, vp]),

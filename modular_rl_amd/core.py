@@ -229,6 +229,7 @@ class IterationRunner:
         self.last_phase_events = None
         self.record_phases = False
         self.last_drain_events = {}
+        self._vorder = None  # streams.ValueOrder of the pipelined loop (set below)
         if torch.cuda.is_available():
             from . import streams
             need = rollout_cus_needed(collector)
@@ -267,6 +268,8 @@ class IterationRunner:
                 # serialise the fit behind it
                 self.main_stream = torch.cuda.Stream()
                 self.pipeline = True
+                if os.environ.get("MRL_XSTREAM_EVENT", "0") != "1":
+                    self._vorder = streams.ValueOrder()
                 # data-parallel: the fit's per-evaluation reductions go over a host group
                 # while it overlaps the persistent rollout (RCCL's kernels would land on
                 # the rollout's CUs and delay its hand-off polls).  The
@@ -283,6 +286,14 @@ class IterationRunner:
         add_prefixed_stats(stats, "vf", vf_stats)
         add_prefixed_stats(stats, "pol", pol_stats)
         return stats
+
+    def _order(self, producer, consumer):
+        """consumer's later work after producer's prior work: on a memory value (the
+        rollout <-> iteration streams; streams.ValueOrder, ~10 us less per crossing than
+        an event) unless MRL_XSTREAM_EVENT=1."""
+        if self._vorder is None:
+            return consumer.wait_stream(producer)
+        self._vorder.order(producer, consumer)
 
     def _event(self):
         """A phase boundary's timing event -- only on the iterations timing samples (bench.py's
@@ -334,7 +345,7 @@ class IterationRunner:
             main = torch.cuda.current_stream()
             if not noise_ready:
                 col.fill_noise()  # one wide kernel: on every CU, ahead of the step chain
-            self.rollout_stream.wait_stream(main)
+            self._order(main, self.rollout_stream)
             with torch.cuda.stream(self.rollout_stream):
                 col.launch(fill_noise=False)
                 ev["rollout1"] = self._event()
@@ -352,7 +363,7 @@ class IterationRunner:
         if self.pipeline:
             if self.pending is not None:
                 done = self._fit_pending(self.fit_stream, ev)
-            main.wait_stream(self.rollout_stream)
+            self._order(self.rollout_stream, main)
         batch = col.finish()
         ev["adv0"] = self._event()
         compute_advantage_batch(agent.baseline, batch, cfg["gamma"], cfg["lam"], self.comm)

@@ -80,3 +80,30 @@ def launch_cus(s=None):
         if st.cuda_stream == s.cuda_stream:
             return len(cus)
     return cu_count()
+
+
+class ValueOrder:
+    """Cross-stream ordering on a memory value instead of an event (tools/xstream_probe.py:
+    a hop ordered by hipStreamWaitValue32 costs 5.6 us against 15.7 with
+    hipStreamWaitEvent).  One int32 slot per producer stream, written by that stream only
+    with increasing values; order(producer, consumer) enqueues the producer's write and
+    then the consumer's wait, so the awaited value is always on its way."""
+
+    def __init__(self, device="cuda"):
+        self.flags = torch.zeros(8, dtype=torch.int32, device=device)
+        torch.cuda.synchronize()  # the zeros are in place before any stream waits on them
+        self.slot = {}
+        self.value = {}
+
+    def order(self, producer, consumer):
+        key = producer.cuda_stream
+        if key not in self.slot:
+            if len(self.slot) >= self.flags.numel():
+                raise _lib.MrlError("ValueOrder: too many producer streams")
+            self.slot[key] = len(self.slot)
+            self.value[key] = 0
+        self.value[key] += 1
+        v = self.value[key]
+        addr = ctypes.c_void_p(self.flags.data_ptr() + 4 * self.slot[key])
+        call("mrl_stream_signal", ctypes.c_void_p(producer.cuda_stream), addr, v)
+        call("mrl_stream_wait", ctypes.c_void_p(consumer.cuda_stream), addr, v)
