@@ -110,3 +110,27 @@ def test_fit_runs_beside_the_prelaunched_rollout():
     ev = runner.last_phase_events
     assert "vf0" in ev and "rollout1" in ev
     assert ev["vf0"].elapsed_time(ev["rollout1"]) > 0.5  # ms of the rollout left when the fit began
+
+
+def test_value_order_sequences_two_streams():
+    """streams.ValueOrder (the pipelined loop's rollout <-> iteration ordering on a memory
+    value): a ping-pong of dependent read-modify-writes between a CU-masked stream and a
+    plain one, each hop behind a long kernel on the producer, ends with every update
+    applied in order (x = 2 N), as an event-ordered ping-pong does."""
+    from modular_rl_amd import streams
+    n_cu = streams.cu_count()
+    a = streams.masked_stream(list(range(min(64, n_cu))))
+    b = torch.cuda.Stream()
+    order = streams.ValueOrder()
+    x = torch.zeros(1 << 20, device="cuda")
+    N = 50
+    for i in range(N):
+        with torch.cuda.stream(a):
+            torch.cuda._sleep(20000)  # the producer's work finishes after the host enqueued the wait
+            x.mul_(1.0).add_(1.0)
+        order.order(a, b)
+        with torch.cuda.stream(b):
+            x.add_(1.0)
+        order.order(b, a)
+    torch.cuda.synchronize()
+    assert torch.all(x == 2 * N)
