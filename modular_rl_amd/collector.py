@@ -315,7 +315,12 @@ class Collector:
         # the stream of this call (a captured graph replays here, not on its capture stream)
         from . import streams
         self.desc.launch_cus = -1 if self.force_persistent else streams.launch_cus()
-        if self.use_graph and self.noise is None:
+        # the persistent fused rollout is a handful of launches: replaying them as a graph
+        # only adds the graph's launch latency (MRL_ROLLOUT_GRAPH=1 keeps it); the step-
+        # launch rollouts (layered, or persistent off) replay their T x k launches
+        graph = self.use_graph and self.noise is None and (
+            self.layered or not self.persistent or os.environ.get("MRL_ROLLOUT_GRAPH", "auto") == "1")
+        if graph:
             if self.graph is not None and self._graph_cus != self.desc.launch_cus:
                 self.graph = None  # captured for another CU set
             if self.graph is None:

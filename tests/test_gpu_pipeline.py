@@ -162,11 +162,13 @@ def test_full_size_rollout_invariants():
 @pytest.mark.parametrize("env_id,E,Tn,graph", [("Hopper-v2", 4096, 64, True), ("Hopper-v2", 100, 300, False),
                                                ("CartPole-v0", 1, 250, False), ("CartPole-v0", 8256, 12, False),
                                                ("Hopper-v2", 8256, 8, True)])
-def test_persistent_rollout_equals_step_launches(env_id, E, Tn, graph):
+def test_persistent_rollout_equals_step_launches(env_id, E, Tn, graph, monkeypatch):
     """mrl_rollout_run as ONE persistent launch (blocks resident, per-step running-stat
     hand-off through memory) vs T step launches: every trajectory row, the filter
     state, env state and counters bit-identical over two iterations.  E = 8256 takes
-    the multi-round record merge (129 blocks > 128)."""
+    the multi-round record merge (129 blocks > 128).  graph: both replayed from captured
+    graphs (MRL_ROLLOUT_GRAPH=1; by default the persistent launch is not captured)."""
+    monkeypatch.setenv("MRL_ROLLOUT_GRAPH", "1" if graph else "auto")
     from modular_rl_amd.collector import Collector
     from modular_rl_amd.envs import make
     env = make(env_id)
@@ -188,7 +190,11 @@ def test_persistent_rollout_equals_step_launches(env_id, E, Tn, graph):
         assert torch.equal(a, b), i
 
 
-def test_rollout_graph_replay_equals_eager():
+@pytest.mark.parametrize("persistent_graph", ["1", "auto"])
+def test_rollout_graph_replay_equals_eager(persistent_graph, monkeypatch):
+    """use_graph: the rollout replayed from a captured graph (the persistent launch too
+    with MRL_ROLLOUT_GRAPH=1; by default it is launched directly) equals eager launches."""
+    monkeypatch.setenv("MRL_ROLLOUT_GRAPH", persistent_graph)
     from modular_rl_amd.collector import Collector
     from modular_rl_amd.envs import make
     env = make("Hopper-v2")
