@@ -228,8 +228,9 @@ class TrpoUpdater:
         self.ops = ops if ops is not None else HipTrpoOps(stochpol.net)
         self.loss_names = ["surr", "kl", "ent"]
         self.last_diag = {}
-        # set by core.IterationRunner: called once theta (and its image) is final, so the
-        # next iteration's rollout is issued before the stats / host bookkeeping
+        # set by core.IterationRunner: called once theta is final (before its packed images,
+        # which the rollout does not read), so the next iteration's rollout is issued before
+        # the stats / host bookkeeping
         self.after_theta = None
         # set by core.IterationRunner: device work that may run while the host waits for
         # the update's readback (the next rollout's noise fill); issued after the copy
@@ -339,9 +340,11 @@ class TrpoUpdater:
                 losses_after = laux
             else:
                 net.theta.copy_(thprev)
-            net.pack()
+            # the next rollout is issued first: it packs its own image from theta, and the
+            # net's images are for this stream's next passes (off the update-to-rollout seam)
             if self.after_theta is not None:
                 self.after_theta()
+            net.pack()
             diag.update(skipped=False, shs=shs, lm=lm, neggdotstepdir=neggdotstepdir, expected_rate=rate,
                         success=success, k=k, stepfrac=frac, cg_iters=int(host[10]), rdotr=float(host[8]),
                         ls=np.array(trace, dtype=np.float64))
