@@ -12,8 +12,9 @@ starts from state already resident in HBM.
 
 Rank 0 prints ONE JSON line.  value = env-steps/s summed over ranks (weak scaling:
 E x T envs-steps per GPU per iteration).  Also reported: TRPO-iters/s, per-phase
-times, the live HIP-event roofline of the dominant kernel (Fisher-vector product)
-and of the GAE scan, and the CPU oracle timed on a bounded sample of the workload.
+times, the live HIP-event roofline of the dominant kernel (by device time per iteration:
+the persistent rollout on C3) and of the GAE scan, and the CPU oracle timed on a bounded
+sample of the workload.  Defaults: N = 1, K = 20, W = 5 (well under a minute of GPU time).
 """
 import argparse
 import gc
@@ -336,8 +337,10 @@ def policy_gemm_roofline(kern, kinfo, net, dtype, n_rows, K, pmc, gemm_pmc):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=1)
+    # defaults: 20 timed iterations after 5 warmup ones (the last VF fit's drain, timed as
+    # part of iteration K, amortised over 20; the per-launch timing samples 5 of them)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--env", default="Hopper-v2")
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--horizon", type=int, default=1024)
