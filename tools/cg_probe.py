@@ -6,6 +6,7 @@ mrl_cg_update_pack) -- HIP events on the launch stream over many iterations, no 
 1218 us, the same; not kept, profiles/r05w_cg_probe.txt.)
 Also a chain of tiny kernels (pack launches) to show the per-launch cost of a dependent
 launch on this runtime."""
+import ctypes
 import os
 import sys
 
@@ -86,6 +87,5 @@ def chain():
         call("mrl_mlp_pack_split", ctypes_desc, ptr(ops.p32), ptr(img), None, stream())
 
 
-import ctypes  # noqa: E402
 ctypes_desc = ctypes.byref(net.desc)
 print(f"tiny dependent launches: {timed(chain, 5) * 1e3 / 100:.2f} us per launch", flush=True)
