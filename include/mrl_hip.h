@@ -230,6 +230,9 @@ typedef struct {
 } mrl_gemm_desc;
 
 int mrl_gemm(const mrl_gemm_desc* g, const int32_t* skip, void* stream);
+/* column-tile width mrl_gemm launches for this descriptor: 32 (narrow 128x32 tiles: n <= 32
+ * or fewer than 160 128x128 blocks) or 128 (0 for an empty product); host-only query */
+int32_t mrl_gemm_tile_n(const mrl_gemm_desc* g);
 
 /* bf16-operand GEMMs of the layered path's bf16 mode (csrc/gemm_bf16.hip): operands in
  * HBM as bf16 (a bf16 tape and packed bf16 weight images), f32 accumulation.  The

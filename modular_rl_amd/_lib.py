@@ -106,6 +106,7 @@ SIGNATURES = {
     "mrl_reduce_rows_f64": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_gemm": (i32, [vp, vp, vp]),
     "mrl_gemm_slab_splits": (i64, [i64, i32]),
+    "mrl_gemm_tile_n": (i32, [vp]),
     "mrl_gemm_bf16": (i32, [vp, vp, vp]),
     "mrl_gemm_bf16_tn": (i32, [vp, vp, vp]),
     "mrl_cast_rows_bf16": (i32, [vp, i64, i64, i64, vp, i64, vp]),

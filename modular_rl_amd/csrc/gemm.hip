@@ -497,6 +497,23 @@ int64_t mrl_gemm_slab_splits(int64_t k, int32_t max_splits) {
   return (k + chunk - 1) / chunk;
 }
 
+// column-tile width mrl_gemm launches for a descriptor: 32 (narrow 128x32 tiles: the heads,
+// n <= 32, and small-M launches with fewer than 160 wide blocks) or 128
+static int gemm_tile_n(int64_t m, int64_t n, int64_t k, int32_t epilogue, int32_t req_splits) {
+  int64_t splits = 1;
+  if (epilogue == MRL_GEMM_SLAB) {
+    const int64_t chunk = slab_chunk(k, req_splits);
+    splits = k > 0 ? (k + chunk - 1) / chunk : 1;
+  }
+  const int64_t wide_blocks = (n + GBN - 1) / GBN * ((m + GBM - 1) / GBM) * splits;
+  return (n <= 32 || wide_blocks < 160) ? 32 : 128;
+}
+
+int32_t mrl_gemm_tile_n(const mrl_gemm_desc* d) {
+  if (!d || d->m <= 0 || d->n <= 0) return 0;
+  return gemm_tile_n(d->m, d->n, d->k, d->epilogue, d->splits);
+}
+
 int mrl_gemm(const mrl_gemm_desc* d, const int32_t* skip, void* stream) {
   if (!d || !d->b || !d->c || (!d->a && d->m > (d->ones_row ? 1 : 0))) return fail(E_ARG, "mrl_gemm: null pointer");
   if ((d->a2 == nullptr) != (d->b2 == nullptr)) return fail(E_ARG, "mrl_gemm: a2/b2 must be both set or both null");
@@ -533,7 +550,6 @@ int mrl_gemm(const mrl_gemm_desc* d, const int32_t* skip, void* stream) {
   if (splits > 65535) return fail(E_ARG, "mrl_gemm: too many splits");
   hipStream_t s = (hipStream_t)stream;
   const unsigned gm = (unsigned)((g.M + GBM - 1) / GBM);
-  const int64_t wide_blocks = (g.N + GBN - 1) / GBN * (int64_t)gm * splits;
   const int mode = d->compute == MRL_COMPUTE_BF16 ? 1 : d->compute == MRL_COMPUTE_SPLIT ? 2 : 0;
 #define MRL_GEMM_KERNEL(AT, BT, BNW, SHM, grid)                                                     \
   do {                                                                                              \
@@ -554,7 +570,7 @@ int mrl_gemm(const mrl_gemm_desc* d, const int32_t* skip, void* stream) {
     return mode == 0 ? 2 * (GBM + bn) * LDP * sizeof(float)
                      : (size_t)(mode == 2 ? 3 : 1) * 2 * (GBM + bn) * LDPB * sizeof(__bf16);
   };
-  if (g.N <= 32 || wide_blocks < 160) {
+  if (gemm_tile_n(d->m, d->n, d->k, d->epilogue, d->splits) == 32) {
     // narrow 128x32 tiles: head layers (n_out <= 32) without 128-wide MFMA waste, and
     // small-M launches (the rollout's per-step forward over E rows) with 4x the blocks
     MRL_GEMM_LAUNCH(32, shm_of(32));

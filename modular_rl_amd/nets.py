@@ -28,6 +28,11 @@ from ._lib import MrlError, call, ptr, stream
 # GEMM launches over at least this many rows are timed one by one when bench.py enables
 # timing (the update's and the VF fit's passes; not the rollout's per-step GEMMs)
 GEMM_TIMING_MIN_ROWS = 1 << 16
+# fp32 policy GEMMs below this many rows (the rollout's per-step forward over E rows and
+# the small-M launches) run on split bf16 operands (MRL_COMPUTE_SPLIT): on the C5 rollout
+# 405 -> 363 ms per iteration against the exact-f32 kernel (profiles/r05o_bench_humanoid*.json);
+# the single-product NN / NT launches above it measured faster in exact f32
+SPLIT_SMALL_M_ROWS = 1 << 16
 
 HIDDEN = 64
 N_LAYERS = 2
@@ -408,7 +413,7 @@ class LayeredMlpNet:
     def _gemm(self, m, n, k, a, lda, b, ldb, c, ldc, a_trans=0, b_trans=0, epi=0, a2=None, b2=None, bias=None,
               h=None, ldh=0, ones_row=0, splits=1, slab_stride=0, skip=None):
         compute = self.compute
-        if self.split_gemms and (a_trans or a2 is not None or max(m, k) < GEMM_TIMING_MIN_ROWS):
+        if self.split_gemms and (a_trans or a2 is not None or max(m, k) < SPLIT_SMALL_M_ROWS):
             compute = _lib.COMPUTE_SPLIT
         g = _lib.GemmDesc(m=m, n=n, k=k, a=a, lda=lda, a_trans=a_trans, ones_row=ones_row, b=b, ldb=ldb,
                           b_trans=b_trans, epilogue=epi, a2=a2, b2=b2, c=c, ldc=ldc, bias=bias, h=h, ldh=ldh,

@@ -174,6 +174,14 @@ def test_gemm_refuses_bad_descriptors():
     rc = lib.mrl_gemm(ctypes.byref(d), None, None)
     assert rc < 0 and b"null" in lib.mrl_last_error()
     assert lib.mrl_gemm_slab_splits(1000, 4) == 4 and lib.mrl_gemm_slab_splits(10, 64) == 1
+    # the column-tile choice (host query): 128-wide tiles from 160 blocks of 128x128 up
+    tile = lambda **kw: lib.mrl_gemm_tile_n(ctypes.byref(_lib.GemmDesc(**kw)))
+    assert tile(m=0, n=4, k=4) == 0 and lib.mrl_gemm_tile_n(None) == 0
+    assert tile(m=1024, n=512, k=512) == 32          # 32 blocks: small-M launch
+    assert tile(m=8192, n=512, k=512) == 128         # 256 blocks: the C5 layers' production tile
+    assert tile(m=8192, n=17, k=512) == 32           # head layer
+    assert tile(m=513, n=512, k=65536, epilogue=_lib.GEMM_SLAB, splits=64) == 128   # TN weight grads
+    assert tile(m=513, n=512, k=65536, epilogue=_lib.GEMM_SLAB, splits=4) == 32
 
 
 _UBSAN_PROBE = r"""
@@ -182,7 +190,8 @@ from modular_rl_amd import _lib
 lib = _lib.load()
 # every status-returning entry point with null buffers: an error status, no fault
 for name, (res, args) in _lib.SIGNATURES.items():
-    if name in ("mrl_last_error", "mrl_version", "mrl_stream_destroy", "mrl_mlp_fisher_hyb_fits"):
+    if name in ("mrl_last_error", "mrl_version", "mrl_stream_destroy", "mrl_mlp_fisher_hyb_fits",
+                "mrl_gemm_tile_n"):
         continue
     r = getattr(lib, name)(*[None if a is ctypes.c_void_p else 0 for a in args])
     if res is ctypes.c_int:
@@ -207,6 +216,8 @@ for n in (0, 1, 31, 32, 33, 4194304, 1 << 31):
     lib.mrl_gae_workspace_bytes(n, 1024)
     for s in (1, 8, 64):
         lib.mrl_gemm_slab_splits(n, s)
+        for m in (1, 513, 1 << 20):
+            lib.mrl_gemm_tile_n(ctypes.byref(_lib.GemmDesc(m=m, n=512, k=n, epilogue=3, splits=s)))
 for e in (-1, 0, 1, 2, 3, 99):
     lib.mrl_env_state_doubles(e); lib.mrl_filter_doubles(e); lib.mrl_record_doubles(e); lib.mrl_rollout_blocks(e)
 print("UBSAN_PROBE_OK")
@@ -232,9 +243,10 @@ def test_host_code_under_ubsan():
 
 
 def test_built_code_has_no_packed_f32_to_lds_reads():
-    """The gfx950 code objects in libmrl_hip.so: no LDS instruction reads, as data, a VGPR
-    that a packed-f32 VALU op wrote fewer than two wait states earlier (the round-4 split
-    Fisher product's run-to-run hazard).  A compiler or flag change that
+    """The gfx950 code objects in libmrl_hip.so: no cross-lane LDS read (ds_bpermute /
+    ds_permute / ds_swizzle) of a VGPR a packed-f32 VALU op wrote earlier in the same basic
+    block, and no other LDS data read of one within 8 wait states (four times the count
+    proven insufficient; the round-4 split Fisher product's run-to-run hazard).  A compiler or flag change that
     reintroduces the pattern fails here, on the CPU, before any GPU run."""
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -249,4 +261,19 @@ def test_built_code_has_no_packed_f32_to_lds_reads():
     # and the checker does see the pattern: a packed-f32 sum read by ds_bpermute next
     lines = ["0000 <k>:", "v_pk_add_f32 v[4:5], v[0:1], v[34:35]", "v_add_f32_e32 v3, v2, v3",
              "ds_bpermute_b32 v6, v56, v4", "ds_bpermute_b32 v7, v56, v5"]
-    assert [(f, st) for f, _, _, st in H.scan(lines)] == [("k", 1)]
+    assert [(f, st) for f, _, _, st in H.scan(lines)] == [("k", 1), ("k", 2)]
+    # the build proven bad: two wait states (s_nop 1) before the bpermute; and a cross-lane
+    # read far down the same block -- both flagged (whole-block rule for permutes)
+    far = ["v_mul_f32_e32 v9, v8, v8"] * 40
+    lines = ["0000 <k>:", "v_pk_add_f32 v[4:5], v[0:1], v[34:35]", "s_nop 1", "ds_bpermute_b32 v6, v56, v4"]
+    assert [st for _, _, _, st in H.scan(lines)] == [2]
+    lines = ["0000 <k>:", "v_pk_add_f32 v[4:5], v[0:1], v[34:35]"] + far + ["ds_swizzle_b32 v6, v5 offset:0x1f"]
+    assert [st for _, _, _, st in H.scan(lines)] == [40]
+    # other LDS data reads: flagged under 8 wait states, not beyond; a branch ends the block
+    pk = ["0000 <k>:", "v_pk_mul_f32 v[4:5], v[0:1], v[34:35]"]
+    assert [st for _, _, _, st in H.scan(pk + ["s_nop 5", "ds_write_b32 v6, v5"])] == [6]
+    assert H.scan(pk + far[:8] + ["ds_write_b32 v6, v5"]) == []
+    assert H.scan(pk + far[:8] + ["ds_write_b32 v6, v5"], min_states=None) != []
+    assert H.scan(pk + ["s_branch 4", "ds_bpermute_b32 v6, v56, v4"]) == []
+    # an overwrite in between clears the register
+    assert H.scan(pk + ["v_mov_b32_e32 v4, 0", "ds_bpermute_b32 v6, v56, v4"]) == []

@@ -177,11 +177,14 @@ def test_value_forward_and_loss_grad_with_time_feature(nin, hid):
     assert _rel(g.cpu().numpy() + 2e-3 * th, gw) < 1e-4
 
 
-@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (130, 70, 33), (257, 129, 300), (300, 17, 520), (1024, 512, 512)])
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (130, 70, 33), (257, 129, 300), (300, 17, 520), (1024, 512, 512),
+                                   (8192, 512, 512), (8192, 512, 376)])
 @pytest.mark.parametrize("compute", ["f32", "split"])
 def test_gemm_orientations_and_epilogues(M, N, K, compute):
     """mrl_gemm against torch fp64 for every operand orientation and epilogue, on the
-    exact-f32 MFMA and on split bf16 operands (MRL_COMPUTE_SPLIT: fp32-accurate)."""
+    exact-f32 MFMA and on split bf16 operands (MRL_COMPUTE_SPLIT: fp32-accurate); the
+    8192-row cases run the 128-column tile the C5 layers use (asserted via
+    mrl_gemm_tile_n), the others the narrow 128x32 one."""
     import ctypes
     from modular_rl_amd import _lib
     from modular_rl_amd._lib import call, stream
@@ -209,6 +212,7 @@ def test_gemm_orientations_and_epilogues(M, N, K, compute):
                 d = _lib.GemmDesc(m=M, n=N, k=K, a=addr(Ad), lda=lda, a_trans=at, b=addr(Bd), ldb=ldb, b_trans=bt,
                                   epilogue=epi, a2=addr(A2d), b2=addr(B2d), c=addr(C), ldc=N, bias=addr(bias_d),
                                   h=addr(H_d), ldh=N, compute=cm)
+                assert _lib.load().mrl_gemm_tile_n(ctypes.byref(d)) == (128 if M >= 8192 else 32)
                 call("mrl_gemm", ctypes.byref(d), None, stream())
                 ref = (A.double() @ B.double() + A2.double() @ B2.double() + bias.double())
                 scale = ref.abs().max().item()  # fp32 rounding of the pre-activation sets the error scale
@@ -230,6 +234,41 @@ def test_gemm_orientations_and_epilogues(M, N, K, compute):
     got = slab.view(S, stride)[:, :(M + 1) * N].sum(0).view(M + 1, N).cpu().double()
     ref = torch.cat([A.double(), torch.ones(1, K, dtype=torch.float64)], 0) @ B.double()
     assert (got - ref).abs().max().item() < 1e-4 * max(ref.abs().max().item(), 1.0)
+
+
+@pytest.mark.parametrize("din", [376, 512])
+@pytest.mark.parametrize("compute", ["f32", "split"])
+def test_gemm_weight_gradient_slabs_at_production_tile(din, compute):
+    """The TN weight-gradient GEMM as the C5 VJP issues it (LayeredMlpNet.vjp_flat):
+    dW = X^T G over K = 65,536 rows in 64 split-K slabs, with the bias gradient as the
+    ones-row when din is not a multiple of 128 -- >= 160 blocks, so the 128-column tile
+    (mrl_gemm_tile_n) -- against the float64 product, summed over the slabs."""
+    import ctypes
+    from modular_rl_amd import _lib
+    from modular_rl_amd._lib import call, stream
+    lib = _lib.load(require_gpu=True)
+    rows, dout = 65536, 512
+    gen = torch.Generator(device="cuda").manual_seed(din)
+    X = torch.randn(rows, din, device="cuda", generator=gen)
+    G = torch.randn(rows, dout, device="cuda", generator=gen) * 1e-3
+    ones = din % 128 != 0
+    m = din + ones
+    S = int(lib.mrl_gemm_slab_splits(rows, 64))
+    stride = m * dout + 7
+    slab = torch.full((S * stride,), float("nan"), device="cuda")
+    cm = _lib.COMPUTE_SPLIT if compute == "split" else _lib.COMPUTE_F32
+    addr = lambda t: ctypes.c_void_p(t.data_ptr())
+    d = _lib.GemmDesc(m=m, n=dout, k=rows, a=addr(X), lda=din, a_trans=1, ones_row=int(ones), b=addr(G), ldb=dout,
+                      epilogue=_lib.GEMM_SLAB, c=addr(slab), ldc=dout, splits=64, slab_stride=stride, compute=cm)
+    assert S == 64 and lib.mrl_gemm_tile_n(ctypes.byref(d)) == 128
+    call("mrl_gemm", ctypes.byref(d), None, stream())
+    got = slab.view(S, stride)[:, :m * dout].double().sum(0).view(m, dout)
+    Xd = X.double()
+    if ones:
+        Xd = torch.cat([Xd, torch.ones(rows, 1, dtype=torch.float64, device="cuda")], 1)
+    ref = Xd.t() @ G.double()
+    err = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-5, err
 
 
 @pytest.mark.parametrize("M,N,ldg,S", [(5000, 17, 34, 3), (1048576, 17, 34, 256), (777, 70, 70, 5), (40, 3, 3, 7)])

@@ -6,10 +6,18 @@ stale values for the last quarter of the wave (lanes 48-63) -- run to run, a few
 groups per 4 M rows (tools/det_locate.py, gpurun_out/r05_det*.log).  hipcc pads a
 packed-f32 write before a VALU consumer (s_nop 0) but not before an LDS consumer.  This
 tool disassembles every gfx950 code object bundled in the library and reports each LDS
-instruction that reads a VGPR written by a packed-f32 VALU op fewer than MIN_STATES wait
-states earlier in the same basic block.
+instruction that reads as data a VGPR written by a packed-f32 VALU op:
+  * a cross-lane LDS read (ds_bpermute / ds_permute / ds_swizzle, the failing pattern)
+    anywhere earlier in the same basic block -- no wait-state count is trusted there;
+  * any other LDS data read (ds_write / ds_add ...) fewer than MIN_STATES = 8 wait states
+    earlier: four times the two wait states (s_nop 1) proven insufficient by a build that
+    still corrupted 1,024 rows (profiles/r05_det_slp_bpermute_nop.txt; one wait state:
+    24.8-33.1 k rows).  The library's nearest such site is 12 states away
+    (mlp_vjp_kernel's dtanh products into its LDS transposes; `--strict` lists them).
+No ISA document available here states the hazard's window.
+--min-states N replaces the 8; --strict applies the whole-block rule to every LDS read.
 
-usage: python tools/isa_hazard_check.py [lib.so] [--min-states N] [--all]
+usage: python tools/isa_hazard_check.py [lib.so] [--min-states N | --strict] [--all]
 exit status 1 if a hazard is found (tests/test_abi.py runs it on the built library)."""
 import os
 import re
@@ -21,7 +29,8 @@ import tempfile
 LLVM = "/opt/rocm/lib/llvm/bin"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
-MIN_STATES = 2  # wait states required between the packed-f32 write and the LDS read
+MIN_STATES = 8  # wait states required before a non-permute LDS data read (None: whole block)
+CROSS_LANE = ("ds_bpermute", "ds_permute", "ds_swizzle")  # whole-block rule always
 
 
 def code_objects(lib):
@@ -67,7 +76,9 @@ def _lds_data_regs(op, ops):
     """VGPRs an LDS instruction reads as data (not the address)."""
     if op.startswith(("ds_bpermute", "ds_permute")):
         return _regs(ops[2]) if len(ops) > 2 else set()
-    if op.startswith(("ds_read", "ds_load", "ds_swizzle", "ds_consume", "ds_append", "ds_nop")):
+    if op.startswith("ds_swizzle"):  # ds_swizzle_b32 vdst, vsrc offset:...
+        return _regs(ops[1]) if len(ops) > 1 else set()
+    if op.startswith(("ds_read", "ds_load", "ds_consume", "ds_append", "ds_nop")):
         return set()
     # stores / atomics: every operand after the address
     return set().union(*[_regs(o) for o in ops[1:]]) if len(ops) > 1 else set()
@@ -89,8 +100,9 @@ def scan(lines, min_states=MIN_STATES):
         if op.startswith("ds_"):
             data = _lds_data_regs(op, ops)
             states = 0
+            limit = None if op.startswith(CROSS_LANE) else min_states
             for pop, pops, ps in reversed(win):
-                if states >= min_states or not data:
+                if (limit is not None and states >= limit) or not data:
                     break
                 written = _regs(pops[0]) if pops and pop.startswith("v_") else set()
                 if pop.startswith("v_pk_") and pop.endswith("_f32") and written & data:
@@ -100,7 +112,7 @@ def scan(lines, min_states=MIN_STATES):
         if op.startswith(("s_branch", "s_cbranch", "s_setpc", "s_endpgm")):
             win = []
         else:
-            win = (win + [(op, ops, s)])[-8:]
+            win.append((op, ops, s))
     return found
 
 
@@ -112,12 +124,22 @@ def check(lib, min_states=MIN_STATES):
 
 
 def main():
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    argv, args, ms = sys.argv[1:], [], MIN_STATES
+    i = 0
+    while i < len(argv):
+        if argv[i] == "--strict":
+            ms = None
+        elif argv[i] == "--min-states":
+            if i + 1 >= len(argv):
+                sys.exit("--min-states needs a value")
+            ms = int(argv[i + 1])
+            i += 2
+            continue
+        if not argv[i].startswith("--"):
+            args.append(argv[i])
+        i += 1
     lib = args[0] if args else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                             "modular_rl_amd", "libmrl_hip.so")
-    ms = MIN_STATES
-    if "--min-states" in sys.argv:
-        ms = int(sys.argv[sys.argv.index("--min-states") + 1])
     hz = check(lib, ms)
     by_fn = {}
     for fn, pk, ds, st in hz:
@@ -126,7 +148,8 @@ def main():
         print(f"{fn}: {len(v)}")
         for pk, ds, st in v[: (None if "--all" in sys.argv else 2)]:
             print(f"    {pk}  ->  {ds}   ({st} wait states)")
-    print(f"{len(hz)} packed-f32 -> LDS data reads under {ms} wait states in {len(by_fn)} kernels")
+    rule = "in the same basic block" if ms is None else f"under {ms} wait states (cross-lane: whole block)"
+    print(f"{len(hz)} packed-f32 -> LDS data reads {rule} in {len(by_fn)} kernels")
     return 1 if hz else 0
 
 
