@@ -386,9 +386,11 @@ def main():
         for i in range(args.warmup):
             runner.step(prelaunch_next=i + 1 < args.warmup)
         runner.drain()
-    # the many per-iteration launch regions (Fisher products, VJPs, GEMMs) on every 4th
-    # timed iteration (each event is a queue marker that delays the next kernel), the
-    # rollout and the GAE scan on every one (modular_rl_amd/timing.py)
+    # the per-launch regions (Fisher products, VJPs, GEMMs, the GAE scan) and the phase
+    # spans are recorded on every 4th timed iteration only (each event is a queue marker
+    # that delays the next kernel); their per-iteration figures are the sampled
+    # iterations' means, scaled to K (modular_rl_amd/timing.py).  The rollout region is
+    # recorded on every iteration.
     timing.enable(True, detail_every=4)
     comm.barrier()
     torch.cuda.synchronize()

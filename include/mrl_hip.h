@@ -373,7 +373,10 @@ int mrl_probtype_rows(int32_t head, int32_t k, int64_t n, const float* prob, con
  * GAE + discounted return over time-major [T, E] rows (core.py:63-75 with
  * misc_utils.py:9-27 discount): flags bit0 = episode ends at this row, bit1 = the
  * env terminated (bootstrap 0) else bootstrap with the row's own baseline (core.py:73).
- * moments (fp64 [3]) <- (sum adv, sum adv^2, count)  (for core.py:100-105). */
+ * moments (fp64 [3]) <- (sum adv, sum adv^2, count)  (for core.py:100-105).
+ * workspace: mrl_gae_workspace_bytes(T, E) bytes, ZEROED before its first mrl_gae and
+ * not written by anything else between calls (it holds a completion counter that each
+ * call returns to 0); one workspace per stream of concurrent calls. */
 int mrl_gae(const float* rew, const float* vpred, const uint8_t* flags, int64_t T, int64_t E, double gamma,
             double lam, float* adv, float* ret, double* moments, void* workspace, void* stream);
 int64_t mrl_gae_workspace_bytes(int64_t T, int64_t E);

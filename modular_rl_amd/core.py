@@ -63,17 +63,23 @@ def add_prefixed_stats(stats, prefix, d):
 
 # ================================================================ advantage
 class _GaeWorkspace:
+    """mrl_gae's own workspace (zeroed once: it carries a completion counter between calls)
+    and the moments passes' scratch, kept apart."""
+
     def __init__(self):
-        self.ws = None
+        self.ws = self.ws_gae = None
         self.moments = None
 
     def get(self, T, E, device):
         lib = _lib.load()
-        nbytes = max(int(lib.mrl_gae_workspace_bytes(int(T), int(E))), int(lib.mrl_moments_workspace_bytes(int(T * E))))
-        if self.ws is None or self.ws.numel() < nbytes or self.ws.device != device:
+        nbytes = int(lib.mrl_moments_workspace_bytes(int(T * E)))
+        gbytes = int(lib.mrl_gae_workspace_bytes(int(T), int(E)))
+        if (self.ws is None or self.ws.numel() < nbytes or self.ws_gae.numel() < gbytes
+                or self.ws.device != device):
             self.ws = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+            self.ws_gae = torch.zeros(gbytes, dtype=torch.uint8, device=device)
             self.moments = torch.zeros(2, 3, dtype=torch.float64, device=device)  # first pass, centred pass
-        return self.ws, self.moments
+        return self.ws_gae, self.ws, self.moments
 
 
 _GAE = _GaeWorkspace()
@@ -91,10 +97,10 @@ def compute_advantage_batch(vf, batch, gamma, lam, comm=None):
     if batch.adv is None or batch.adv.numel() != n:
         batch.adv = torch.empty(n, dtype=torch.float32, device=dev)
         batch.ret = torch.empty(n, dtype=torch.float32, device=dev)
-    ws, moments = _GAE.get(batch.T, batch.E, dev)
+    ws_gae, ws, moments = _GAE.get(batch.T, batch.E, dev)
     timing.start("gae_scan", detail=True)
     call("mrl_gae", ptr(batch.rew), ptr(batch.vpred), ptr(batch.flags), int(batch.T), int(batch.E), float(gamma),
-         float(lam), ptr(batch.adv), ptr(batch.ret), ptr(moments), ptr(ws), stream())
+         float(lam), ptr(batch.adv), ptr(batch.ret), ptr(moments), ptr(ws_gae), stream())
     timing.stop("gae_scan")
     # numpy's two-pass std (core.py:100-105): global mean first, then the centred sums
     comm.allreduce_(moments[0])

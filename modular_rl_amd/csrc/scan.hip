@@ -9,6 +9,7 @@
 // One pass: r / v / flags are read once, adv / ret written once (17 B per row).
 // Scans run in fp64 like lfilter; outputs are fp32.
 #include <math.h>
+#include <stdlib.h>
 
 #include "../../include/mrl_hip.h"
 #include "mrl_common.h"
@@ -184,6 +185,186 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_scan_kernel(const float* __re
     }
     part[blk * 2 + 0] = t1;
     part[blk * 2 + 1] = t2;
+  }
+}
+
+// The exact-fit form (round 6): T = GAE_NC * L (one segment) and E a multiple of GAE_EB
+// -- the benchmark's 1024 x 4096.  Same per-row arithmetic and summation order as
+// gae_scan_kernel, rebuilt for instruction count (that kernel issues ~100 instructions per
+// row: per-lane bounds clamps, 64-bit address arithmetic per load, the delta recomputed
+// in the second pass; at 16 K rows per CU its VALU time alone is ~10 us):
+//  * no bounds: every load / store is a uniform row base (SGPR) + one per-lane 32-bit
+//    offset fixed for the thread's chunk;
+//  * loads issued in consumption order (the chunk's last step first), so the summary pass
+//    starts on the first rows to land instead of the last;
+//  * delta_t kept in registers (fp64) for the second pass; the chunk maps' multipliers
+//    B, C are gl^L / gamma^L unless the chunk breaks (0): no per-row products;
+//  * the moments' final sum rides in the last block to finish (a ticket counter; the
+//    partials handed over as sc1 granules, MI355X_MICROARCH.md's hand-off table, row 1),
+//    so there is no second launch.
+typedef uint32_t gran4_t __attribute__((ext_vector_type(4)));  // one 16-B granule
+
+template <int L>
+__global__ __launch_bounds__(GAE_THREADS) void gae_full_kernel(const float* __restrict__ rew,
+                                                               const float* __restrict__ v,
+                                                               const uint8_t* __restrict__ flags, int64_t E,
+                                                               double gamma, double lam, float* __restrict__ adv,
+                                                               float* __restrict__ ret, double* __restrict__ part,
+                                                               uint32_t* __restrict__ ticket,
+                                                               double* __restrict__ moments, double count) {
+  __shared__ double sA[GAE_NC * GAE_PITCH], sB[GAE_NC * GAE_PITCH], sR[GAE_NC * GAE_PITCH],
+      sC[GAE_NC * GAE_PITCH];
+  __shared__ double red[2][GAE_THREADS];
+  __shared__ int is_last;
+  const int tid = threadIdx.x;
+  const int el = tid % GAE_EB, c = tid / GAE_EB;
+  const int64_t blk = xcd_segment(blockIdx.x, gridDim.x);
+  const double gl = gamma * lam;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int sc = tid % GAE_NC, se = tid / GAE_NC;
+  // byte offset of (row c*L, env) -- the same for every step j of the chunk; step j adds
+  // the uniform j * E * 4 to the base pointer (T * E * 4 < 2^31, checked on the host)
+  const uint32_t E4 = (uint32_t)E * 4u;
+  const uint32_t o4 = ((uint32_t)(c * L) * (uint32_t)E + (uint32_t)(blk * GAE_EB + el)) * 4u;
+  const bool lastc = c == GAE_NC - 1;
+  // buffer resources: per access one VGPR offset (o4) + the row's uniform SGPR offset
+  const int nbytes = (int)(GAE_NC * L * E4);
+  const __amdgpu_buffer_rsrc_t rr_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rew), 0, nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vv_rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(v), 0, nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ff_rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(flags), 0, nbytes / 4, 0x00020000);
+  float rr[L], vv[L];
+  uint32_t ff[L];
+#pragma unroll
+  for (int j = L - 1; j >= 0; --j) {
+    const uint32_t rowb = (uint32_t)j * E4;
+    rr[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr_rs, o4, rowb, 0));
+    vv[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vv_rs, o4, rowb, 0));
+    ff[j] = __builtin_amdgcn_raw_buffer_load_b8(ff_rs, o4 >> 2, rowb >> 2, 0);
+  }
+  // v of the next chunk's first row (the last chunk's is never used: t + 1 = T)
+  const float vnext = __builtin_bit_cast(
+      float, __builtin_amdgcn_raw_buffer_load_b32(vv_rs, lastc ? o4 : o4 + (uint32_t)L * E4, 0, 0));
+  double glL = 1.0, gL = 1.0;  // B, C of an unbroken chunk: the products gae_scan_kernel forms
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    glL = gl * glL;
+    gL = gamma * gL;
+  }
+  double dd[L];
+  double A = 0.0, R = 0.0;
+  bool brk = false;
+  double vn = (double)vnext;
+  uint32_t fl[(L + 15) / 16] = {};  // the flags again, 2 bits per step, for the second pass
+#pragma unroll
+  for (int j = L - 1; j >= 0; --j) {
+    fl[j >> 4] |= ff[j] << (2 * (j & 15));
+    const bool cont = !(ff[j] & 1u) && !(lastc && j == L - 1);
+    const double vt = (double)vv[j], rj = (double)rr[j];
+    // bootstrap b1[t+1]: next baseline inside the episode, 0 if terminated, else b[-1] (core.py:73)
+    const double boot = cont ? vn : ((ff[j] & 2u) ? 0.0 : vt);
+    const double d = rj + gamma * boot - vt;
+    dd[j] = d;
+    A = d + (cont ? gl : 0.0) * A;
+    R = rj + (cont ? gamma : 0.0) * R;
+    brk = brk || !cont;
+    vn = vt;
+  }
+  sA[c * GAE_PITCH + el] = A;
+  sB[c * GAE_PITCH + el] = brk ? 0.0 : glL;
+  sR[c * GAE_PITCH + el] = R;
+  sC[c * GAE_PITCH + el] = brk ? 0.0 : gL;
+  __syncthreads();
+  {
+    // reverse inclusive scan of env slot se's chunk maps (lane = chunk), as gae_scan_kernel
+    double a = sA[sc * GAE_PITCH + se], b = sB[sc * GAE_PITCH + se];
+    double r = sR[sc * GAE_PITCH + se], cc = sC[sc * GAE_PITCH + se];
+#pragma unroll
+    for (int off = 1; off < GAE_NC; off <<= 1) {
+      const double a2 = __shfl_down(a, off), b2 = __shfl_down(b, off);
+      const double r2 = __shfl_down(r, off), c2 = __shfl_down(cc, off);
+      if (sc + off < GAE_NC) {
+        a = a + b * a2;
+        b = b * b2;
+        r = r + cc * r2;
+        cc = cc * c2;
+      }
+    }
+    double xa = __shfl_down(a, 1), xb = __shfl_down(b, 1), xr = __shfl_down(r, 1), xc = __shfl_down(cc, 1);
+    if (sc == GAE_NC - 1) { xa = 0.0; xb = 1.0; xr = 0.0; xc = 1.0; }
+    const double in_a = xa + xb * 0.0, in_r = xr + xc * 0.0;
+    __syncthreads();
+    sA[sc * GAE_PITCH + se] = in_a;
+    sR[sc * GAE_PITCH + se] = in_r;
+  }
+  __syncthreads();
+  double a = sA[c * GAE_PITCH + el], r = sR[c * GAE_PITCH + el];
+  double s1 = 0.0, s2 = 0.0;
+  const __amdgpu_buffer_rsrc_t adv_rs = __builtin_amdgcn_make_buffer_rsrc(adv, 0, nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ret_rs = __builtin_amdgcn_make_buffer_rsrc(ret, 0, nbytes, 0x00020000);
+#pragma unroll
+  for (int j = L - 1; j >= 0; --j) {
+    const bool cont = !((fl[j >> 4] >> (2 * (j & 15))) & 1u) && !(lastc && j == L - 1);
+    a = dd[j] + (cont ? gl : 0.0) * a;
+    r = (double)rr[j] + (cont ? gamma : 0.0) * r;
+    const float af = (float)a;
+    const uint32_t rowb = (uint32_t)j * E4;
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, af), adv_rs, o4, rowb, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, (float)r), ret_rs, o4, rowb, 0);
+    s1 += (double)af;
+    s2 += (double)af * (double)af;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_down(s1, off);
+    s2 += __shfl_down(s2, off);
+  }
+  if (lane == 0) {
+    red[0][wave] = s1;
+    red[1][wave] = s2;
+  }
+  __syncthreads();
+  const int64_t nb = gridDim.x;
+  __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(part, 0, (int)(nb * 16), 0x00020000);
+  if (tid == 0) {
+    double t1 = 0.0, t2 = 0.0;
+    for (int w = 0; w < GAE_THREADS / 64; ++w) {
+      t1 += red[0][w];
+      t2 += red[1][w];
+    }
+    // the block's partial as one sc1 granule, waited for, then the ticket (agent scope)
+    const uint64_t b1 = (uint64_t)__double_as_longlong(t1), b2 = (uint64_t)__double_as_longlong(t2);
+    const gran4_t g = {(uint32_t)b1, (uint32_t)(b1 >> 32), (uint32_t)b2, (uint32_t)(b2 >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(g, prs, (uint32_t)(blk * 16), 0, 16);  // aux 16 = sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t done = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = done == (uint32_t)(nb - 1);
+  }
+  __syncthreads();
+  if (!is_last) return;
+  // the last block: every partial through sc1 loads, summed in block order in a fixed
+  // tree (the order moments_final_kernel uses, over GAE_THREADS lanes)
+  double t1 = 0.0, t2 = 0.0;
+  for (int64_t i = tid; i < nb; i += GAE_THREADS) {
+    const gran4_t g = __builtin_amdgcn_raw_buffer_load_b128(prs, (uint32_t)(i * 16), 0, 16);
+    t1 += __longlong_as_double((long long)(((uint64_t)g.y << 32) | g.x));
+    t2 += __longlong_as_double((long long)(((uint64_t)g.w << 32) | g.z));
+  }
+  red[0][tid] = t1;
+  red[1][tid] = t2;
+  __syncthreads();
+  for (int o = GAE_THREADS / 2; o > 0; o >>= 1) {
+    if (tid < o) {
+      red[0][tid] += red[0][tid + o];
+      red[1][tid] += red[1][tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    moments[0] = red[0][0];
+    moments[1] = red[1][0];
+    moments[2] = count;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
   }
 }
 
@@ -863,10 +1044,16 @@ using namespace mrl;
 
 extern "C" {
 
+// workspace: [nb fp64 (sum, sumsq) block partials][pad to 64 B][u32 completion ticket]
+static int64_t gae_ticket_offset(int64_t E) {
+  const int64_t nb = (E + GAE_EB - 1) / GAE_EB;
+  return (nb * 2 * (int64_t)sizeof(double) + 63) / 64 * 64;
+}
+
 int64_t mrl_gae_workspace_bytes(int64_t T, int64_t E) {
   (void)T;
-  const int64_t nb = (E + GAE_EB - 1) / GAE_EB;
-  return nb * 2 * (int64_t)sizeof(double) + 64;
+  if (E <= 0) return 128;
+  return gae_ticket_offset(E) + 64;
 }
 
 int mrl_gae(const float* rew, const float* vpred, const uint8_t* flags, int64_t T, int64_t E, double gamma, double lam,
@@ -881,6 +1068,25 @@ int mrl_gae(const float* rew, const float* vpred, const uint8_t* flags, int64_t 
   // chunk length: the smallest power of two that covers T in one segment, at most GAE_LMAX
   int L = 1;
   while (L < GAE_LMAX && (int64_t)GAE_NC * L < T) L <<= 1;
+  // MRL_GAE_GENERAL=1 (tests / A-B probes): the general kernel for every shape
+  static const bool general_only = getenv("MRL_GAE_GENERAL") && getenv("MRL_GAE_GENERAL")[0] == '1';
+  if (!general_only && T == (int64_t)GAE_NC * L && E % GAE_EB == 0 && T * E * 4 < ((int64_t)1 << 31)) {
+    // exact fit: one pass, the moments finished by the last block (gae_full_kernel)
+    uint32_t* ticket = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(workspace) + gae_ticket_offset(E));
+#define MRL_GAE_FULL(LL)                                                                                          \
+  hipLaunchKernelGGL(gae_full_kernel<LL>, dim3(nb), dim3(GAE_THREADS), 0, s, rew, vpred, flags, E, gamma, lam, adv, \
+                     ret, part, ticket, moments, (double)(T * E))
+    switch (L) {
+      case 1: MRL_GAE_FULL(1); break;
+      case 2: MRL_GAE_FULL(2); break;
+      case 4: MRL_GAE_FULL(4); break;
+      case 8: MRL_GAE_FULL(8); break;
+      case 16: MRL_GAE_FULL(16); break;
+      default: MRL_GAE_FULL(32); break;
+    }
+#undef MRL_GAE_FULL
+    return hip_check(hipGetLastError(), "mrl_gae");
+  }
 #define MRL_GAE_LAUNCH(LL)                                                                                      \
   hipLaunchKernelGGL(gae_scan_kernel<LL>, dim3(nb), dim3(GAE_THREADS), 0, s, rew, vpred, flags, T, E, gamma, lam, \
                      adv, ret, part)

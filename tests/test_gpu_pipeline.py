@@ -18,7 +18,8 @@ def _dev(a, dtype=torch.float32):
     return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).cuda()
 
 
-@pytest.mark.parametrize("Tn,E", [(1, 1), (33, 5), (100, 37), (257, 64), (1024, 4096), (2500, 19), (4097, 3)])
+@pytest.mark.parametrize("Tn,E", [(1, 1), (33, 5), (100, 37), (257, 64), (1024, 4096), (2500, 19), (4097, 3),
+                                  (32, 16), (64, 48), (512, 32), (1024, 64)])
 def test_gae_and_standardize(Tn, E):
     from modular_rl_amd import core
     from modular_rl_amd.collector import Batch
@@ -41,6 +42,53 @@ def test_gae_and_standardize(Tn, E):
     np.testing.assert_allclose(b.ret.cpu().numpy().reshape(Tn, E), ret_w, rtol=1e-5, atol=1e-5)
     if Tn * E > 1:
         np.testing.assert_allclose(b.adv.cpu().numpy().reshape(Tn, E), T.standardize(adv_w), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("Tn,E", [(1024, 4096), (64, 48), (32, 16), (256, 160)])
+def test_gae_exact_fit_kernel_equals_general_kernel(Tn, E, tmp_path):
+    """mrl_gae's exact-fit kernel (T = 32 chunks x L, E a multiple of 16: one pass, the
+    moments finished by the last block through a completion ticket) gives the general
+    kernel's adv / ret / moments bit for bit, and its ticket returns to zero: repeated
+    calls on one workspace keep finishing the moments (MRL_GAE_GENERAL=1 selects the
+    general kernel, read once per process, so the two run in child processes)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for general in ("0", "1"):
+        env = dict(os.environ, MRL_GAE_GENERAL=general, PYTHONPATH=root)
+        path = os.path.join(str(tmp_path), f"gae{general}.npz")
+        r = subprocess.run([sys.executable, "-c", _GAE_CHILD, str(Tn), str(E), path], env=env, capture_output=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr.decode()[-3000:]
+        outs.append(np.load(path))
+    for k in ("adv", "ret", "mom"):
+        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+
+
+_GAE_CHILD = r"""
+import sys
+import numpy as np, torch
+from modular_rl_amd import _lib
+from modular_rl_amd._lib import call, ptr, stream
+Tn, E = int(sys.argv[1]), int(sys.argv[2])
+rng = np.random.default_rng(Tn + E)
+last = rng.random((Tn, E)) < 0.01
+term = last & (rng.random((Tn, E)) < 0.5)
+flags = torch.as_tensor((last.astype(np.uint8) | (term.astype(np.uint8) << 1)).reshape(-1)).cuda()
+rew = torch.as_tensor(rng.standard_normal(Tn * E).astype(np.float32)).cuda()
+v = torch.as_tensor(rng.standard_normal(Tn * E).astype(np.float32)).cuda()
+adv, ret = torch.empty_like(rew), torch.empty_like(rew)
+ws = torch.zeros(int(_lib.load(require_gpu=True).mrl_gae_workspace_bytes(Tn, E)), dtype=torch.uint8, device="cuda")
+moms = []
+for rep in range(3):
+    mom = torch.full((3,), float("nan"), dtype=torch.float64, device="cuda")
+    call("mrl_gae", ptr(rew), ptr(v), ptr(flags), Tn, E, 0.995, 0.97, ptr(adv), ptr(ret), ptr(mom), ptr(ws), stream())
+    moms.append(mom.cpu().numpy())
+assert all(np.array_equal(m, moms[0]) for m in moms), moms
+assert ws.view(torch.int32)[-16:].abs().sum().item() == 0  # the ticket is back at 0
+np.savez(sys.argv[3], adv=adv.cpu().numpy(), ret=ret.cpu().numpy(), mom=moms[0])
+"""
 
 
 def _policy(head, nin, nout, seed):

@@ -11,7 +11,7 @@
 #   det          run-to-run determinism of the Fisher-product kernels (tools/det_locate.py)
 #   fisher       one Fisher product at 4.19 M rows: one-pass kernel vs the two-kernel pair
 #   fisher_tests the Fisher-product GPU tests only (split / one-pass / full size)
-#   gae          mrl_gae alone, the default build and every tools/gvar/*.so variant
+#   gae          mrl_gae alone: exact-fit vs general kernel (MRL_GAE_GENERAL=1) + rocprof stats
 #   pair         the default bench line with the two-kernel Fisher product (MRL_FISHER_ONEPASS=0)
 #   layered_tests  the layered-path / Humanoid GPU tests only
 #   c5 / c5_f32  C5 Humanoid fp32 line (split GEMMs / exact-f32 GEMMs: MRL_GEMM_SPLIT=0)
@@ -83,14 +83,13 @@ for step in "$@"; do
         --timeout 300 --timeout-method thread > gpurun_out/${tag}_fisher_tests.log 2>&1 ||
         { echo FISHER_TESTS_FAILED; tail -40 gpurun_out/${tag}_fisher_tests.log; exit 1; }
       tail -1 gpurun_out/${tag}_fisher_tests.log ;;
-    gae)
-      for lib in default tools/gvar/*.so; do
-        if [ $lib = default ]; then unset MRL_LIB_PATH; else export MRL_LIB_PATH=$GRAFT_REPO_ROOT/$lib; fi
-        timeout -k 10 120 python -u tools/gae_probe.py >> gpurun_out/${tag}_gae.log 2>&1 ||
-          { tail -5 gpurun_out/${tag}_gae.log; exit 1; }
-      done
-      unset MRL_LIB_PATH
-      grep -v amdgpu.ids gpurun_out/${tag}_gae.log ;;
+    gae)  # mrl_gae alone: the exact-fit kernel, the general one (MRL_GAE_GENERAL=1), and a rocprof pass
+      timeout -k 10 120 python -u tools/gae_probe.py > gpurun_out/${tag}_gae.log 2>&1 &&
+        MRL_GAE_GENERAL=1 timeout -k 10 120 python -u tools/gae_probe.py >> gpurun_out/${tag}_gae.log 2>&1 &&
+        timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_gae_prof -o run --output-format csv \
+          -- python3 tools/gae_probe.py >> gpurun_out/${tag}_gae.log 2>&1 || { tail -5 gpurun_out/${tag}_gae.log; exit 1; }
+      grep -v amdgpu.ids gpurun_out/${tag}_gae.log | grep gae
+      grep -h gae gpurun_out/${tag}_gae_prof/run_kernel_stats.csv ;;
     pair) MRL_FISHER_ONEPASS=0 bench pair 400 --no-cpu-baseline ;;
     layered_tests)
       timeout -k 10 900 python -u -m pytest tests/test_gpu_layered.py tests/test_gpu_humanoid.py -m gpu -x -q \

@@ -35,6 +35,8 @@ def main(T=1024, E=4096, reps=50):
     ms = e0.elapsed_time(e1) / reps
     gbs = 17 * T * E / (ms * 1e-3) / 1e9
     lib = os.path.basename(os.environ.get("MRL_LIB_PATH", "default"))
+    if os.environ.get("MRL_GAE_GENERAL") == "1":
+        lib += ", general kernel"
     print(f"[{lib}] gae T={T} E={E}: {ms * 1e3:.1f} us/call back-to-back, {gbs:.0f} GB/s algorithmic, "
           f"mean adv {float(mom[0]) / (T * E):.5f}", flush=True)
 
