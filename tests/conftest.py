@@ -12,4 +12,4 @@ def pytest_configure(config):
     # the HIP library is a build artefact (git-ignored): build it in-tree if absent
     libs = [os.path.join(ROOT, "modular_rl_amd", "libmrl_hip.so"), os.path.join(ROOT, "oracle", "libmrl_oracle.so")]
     if not all(os.path.exists(p) for p in libs):
-        subprocess.run(["make", "-C", ROOT, "-j8"], check=True, stdout=subprocess.DEVNULL)
+        subprocess.run(["make", "-C", ROOT, "-j8", "all", "oracle"], check=True, stdout=subprocess.DEVNULL)
