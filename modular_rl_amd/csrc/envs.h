@@ -116,16 +116,33 @@ __device__ inline double clampd(double v, double lo, double hi) { return v < lo 
 // emulation (oracle/fma.py) -- the GPU and numpy dynamics stay bit-identical.
 __device__ inline double fmad(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
+// capsule k's contact constants: radius, friction, the two end-spheres' offsets (u, w)
+// in the segment frame -- [field][k] in HP_CAP (the fused rollout keeps this table in LDS:
+// its lanes' k is their row, so a select per constant per substep became one LDS read)
+struct CapsuleC {
+  double rad, mu, u0, u1, w0, w1;
+};
+constexpr double HP_CAP[24] = {0.05, 0.05, 0.04, 0.06,  1.0, 1.0, 1.0, 2.0,  0.0, 0.0, 0.0, -0.13,
+                               0.0, 0.0, 0.0, 0.26,      0.2, 0.0, 0.0, 0.0,  -0.2, -0.45, -0.5, 0.0};
+__device__ inline CapsuleC capsule_const(int k) {
+  return CapsuleC{sel4(k, HP_CAP[0], HP_CAP[1], HP_CAP[2], HP_CAP[3]),
+                  sel4(k, HP_CAP[4], HP_CAP[5], HP_CAP[6], HP_CAP[7]),
+                  sel4(k, HP_CAP[8], HP_CAP[9], HP_CAP[10], HP_CAP[11]),
+                  sel4(k, HP_CAP[12], HP_CAP[13], HP_CAP[14], HP_CAP[15]),
+                  sel4(k, HP_CAP[16], HP_CAP[17], HP_CAP[18], HP_CAP[19]),
+                  sel4(k, HP_CAP[20], HP_CAP[21], HP_CAP[22], HP_CAP[23])};
+}
+
 // capsule k's two end-spheres against the floor: contact force sum (x, z) and
-// moment about pivot k (oracle hopper_contacts); k may differ per lane
-__device__ inline void hopper_contacts(int k, double pz, double pvx, double pvz, double om, double sk, double ck,
-                                       double* out) {
-  const double rad = sel4(k, 0.05, 0.05, 0.04, 0.06), mu = sel4(k, 1.0, 1.0, 1.0, 2.0);
+// moment about pivot k (oracle hopper_contacts); cc = capsule k's constants
+__device__ inline void hopper_contacts(const CapsuleC& cc, double pz, double pvx, double pvz, double om, double sk,
+                                       double ck, double* out) {
+  const double rad = cc.rad, mu = cc.mu;
   double fcx = 0.0, fcz = 0.0, ncm = 0.0;
 #pragma unroll
   for (int n = 0; n < 2; ++n) {
-    const double u = n == 0 ? sel4(k, 0.0, 0.0, 0.0, -0.13) : sel4(k, 0.0, 0.0, 0.0, 0.26);
-    const double w = n == 0 ? sel4(k, 0.2, 0.0, 0.0, 0.0) : sel4(k, -0.2, -0.45, -0.5, 0.0);
+    const double u = n == 0 ? cc.u0 : cc.u1;
+    const double w = n == 0 ? cc.w0 : cc.w1;
     const double ox = fmad(u, ck, w * sk);
     const double oz = fmad(w, ck, -(u * sk)) - rad;
     const double pen = -(pz + oz);
@@ -148,6 +165,7 @@ __device__ inline void hopper_contacts(int k, double pz, double pvx, double pvz,
 
 // every lane evaluates the whole env (layered rollout)
 struct HopperSerial {
+  __device__ CapsuleC capsule(int k) const { return capsule_const(k); }
   __device__ void sincos4(const double* phi, double* s, double* c) const {
 #pragma unroll
     for (int k = 0; k < 4; ++k) sincos(phi[k], &s[k], &c[k]);
@@ -251,7 +269,7 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
 #endif
   par.contacts(
       [&](int k, double* out) {
-        hopper_contacts(k, sel4(k, pz[0], pz[1], pz[2], pz[3]), sel4(k, pvx[0], pvx[1], pvx[2], pvx[3]),
+        hopper_contacts(par.capsule(k), sel4(k, pz[0], pz[1], pz[2], pz[3]), sel4(k, pvx[0], pvx[1], pvx[2], pvx[3]),
                         sel4(k, pvz[0], pvz[1], pvz[2], pvz[3]), sel4(k, om[0], om[1], om[2], om[3]),
                         sel4(k, sg[0], sg[1], sg[2], sg[3]), sel4(k, cg[0], cg[1], cg[2], cg[3]), out);
       },

@@ -36,8 +36,17 @@ constexpr int MAXD = 16;  // obs dims + 1 (reward)
 // the SAME 16 envs: row g evaluates sincos of segment angle g and the contacts of
 // capsule g, and the rows exchange the results, so every row continues with the
 // identical state.  All lanes must be active.
+#ifndef MRL_HP_CAP_LDS  // 0: the capsule constants by per-substep selects (A/B build)
+#define MRL_HP_CAP_LDS 1
+#endif
 struct HopperQuad {
   int g;
+  const double* capc;  // HP_CAP in LDS ([field][k]; the persistent kernel), or null
+  __device__ CapsuleC capsule(int) const {
+    if (MRL_HP_CAP_LDS && capc != nullptr)
+      return CapsuleC{capc[g], capc[4 + g], capc[8 + g], capc[12 + g], capc[16 + g], capc[20 + g]};
+    return capsule_const(g);
+  }
   __device__ void sincos4(const double* phi, double* s, double* c) const {
     double sx, cx;
     sincos(sel4(g, phi[0], phi[1], phi[2], phi[3]), &sx, &cx);
@@ -66,7 +75,7 @@ struct EnvC<MRL_ENV_CARTPOLE> {
   __device__ static void obs(const double* s, double* o) { cartpole_obs(s, o); }
   __device__ static void step_disc(double* s, int a, double& rew, bool& done) { cartpole_step(s, a, rew, done); }
   __device__ static void step_cont(double*, const float*, double&, bool&) {}
-  __device__ static void step_cont_quad(double*, const float*, double&, bool&, int) {}
+  __device__ static void step_cont_quad(double*, const float*, double&, bool&, int, const double*) {}
   template <class Out>
   __device__ static void obs_out(const double* s, Out out) {
     double o[OBS];
@@ -83,8 +92,9 @@ struct EnvC<MRL_ENV_HOPPER> {
   __device__ static void obs(const double* s, double* o) { hopper_obs(s, o); }
   __device__ static void step_disc(double*, int, double&, bool&) {}
   __device__ static void step_cont(double* s, const float* a, double& rew, bool& done) { hopper_step(s, a, rew, done); }
-  __device__ static void step_cont_quad(double* s, const float* a, double& rew, bool& done, int g) {
-    hopper_step(s, a, rew, done, HopperQuad{g});
+  __device__ static void step_cont_quad(double* s, const float* a, double& rew, bool& done, int g,
+                                        const double* capc) {
+    hopper_step(s, a, rew, done, HopperQuad{g, capc});
   }
   template <class Out>
   __device__ static void obs_out(const double* s, Out out) {
@@ -545,7 +555,7 @@ __global__ void noise_fill_kernel(RollArgs a, double* __restrict__ out) {
 template <int ENV, bool QUAD = false>
 __device__ inline void sample_and_step(const RollArgs& a, int64_t row, const float* z, const float* logstd,
                                        const double* zn, double* s, double& rew, bool& done, bool store = true,
-                                       int h = 0) {
+                                       int h = 0, const double* capc = nullptr) {
   using EC = EnvC<ENV>;
   constexpr int A = EC::ACT;
   if constexpr (EC::DISCRETE) {
@@ -590,7 +600,7 @@ __device__ inline void sample_and_step(const RollArgs& a, int64_t row, const flo
         a.b.prob[row * 2 * A + A + q] = sd;
       }
     }
-    if constexpr (QUAD) EC::step_cont_quad(s, av, rew, done, h);
+    if constexpr (QUAD) EC::step_cont_quad(s, av, rew, done, h, capc);
     else EC::step_cont(s, av, rew, done);
   }
 }
@@ -950,6 +960,9 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
   __shared__ double fmean[MAXD], fden[MAXD];
   __shared__ float xt[4][16][MAX_IN + 1];  // +1: conflict-free column reads
   __shared__ int s_fail;
+  // HP_CAP: the capsule constants, one LDS read per constant per substep instead of a
+  // select chain on the lane's row (rollout 14.30 -> 14.05 ms, profiles/r06d_ab.txt)
+  __shared__ double hp_cap[24];
   const int E = a.d.n_envs, T = a.d.horizon, nb = a.nb;
   // diagnostic phase stamps (100 MHz realtime) of block 0 -- never set in production
 #define PSTAMP(tt, k)                                                                  \
@@ -967,6 +980,7 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
   const int nvalid = min(ENVS_PER_BLOCK, E - (int)blockIdx.x * ENVS_PER_BLOCK);
   const Granules gr(sync, nb, D);
   if (threadIdx.x == 0) s_fail = 0;
+  if (threadIdx.x < 24) hp_cap[threadIdx.x] = HP_CAP[threadIdx.x];
 
   RollWeights<O, A, BF> wt;
   wt.load(rimg, lane);
@@ -1097,7 +1111,7 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
     // sample + env step on every row (split angle functions); row 0 stores
     double rew = 0.0;
     bool done = false;
-    sample_and_step<ENV, true>(a, row, z, lsd, zn, s, rew, done, valid && g == 0, g);
+    sample_and_step<ENV, true>(a, row, z, lsd, zn, s, rew, done, valid && g == 0, g, hp_cap);
     PSTAMP(t, 4);
     // episode bookkeeping on every row, so the rows keep identical env state
     // (finish_env_step: gym TimeLimit => terminated; limit / horizon cut => not)
