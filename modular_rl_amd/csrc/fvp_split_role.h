@@ -158,8 +158,11 @@ struct JvpSplitRole {
   }
   // the first tile's x / h1
   __device__ __forceinline__ void prologue(int64_t tile) { load_xh1(tile, xv, h1); }
-  // tile `tile` (its x / h1 already loaded), prefetching tile tn's (tn == tile: re-read)
-  template <class Sink>
+  // tile `tile` (its x / h1 already loaded), prefetching tile tn's (tn == tile: re-read);
+  // PF = false: no prefetch -- the tile's own x / h1 are loaded here, after its h2 (and no
+  // prologue), so the tile's bytes all enter L2 within one round (the one-pass product's
+  // VJP role re-reads them a round later: MRL_FISHER_JVP_PF)
+  template <bool PF = true, class Sink>
   __device__ __forceinline__ void tile(int64_t tile, int64_t tn, Sink&& sink) {
     const int64_t row = tile * 32 + (lane & 31);
     const bool valid = row < a.n;
@@ -170,7 +173,8 @@ struct JvpSplitRole {
     __builtin_amdgcn_sched_barrier(0);
     float xn[MAX_KS0B][8];
     f32x16 h1n[2];
-    load_xh1(tn, xn, h1n);
+    if constexpr (PF) load_xh1(tn, xn, h1n);
+    else load_xh1(tile, xv, h1);
     __builtin_amdgcn_sched_barrier(0);
     f32x16 dh[2];
     // layer 0 tangent: dh = (x dW0 + db0) (1 - h1^2)
@@ -225,12 +229,14 @@ struct JvpSplitRole {
     for (int o = 0; o < MAX_OUT; ++o) dz[o] += dzt[o];
     head_finish(imt, dd, dz);
     sink(valid, row, z, dz);
+    if constexpr (PF) {
 #pragma unroll
-    for (int s0 = 0; s0 < MAX_KS0B; ++s0)
+      for (int s0 = 0; s0 < MAX_KS0B; ++s0)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xv[s0][j] = xn[s0][j];
-    h1[0] = h1n[0];
-    h1[1] = h1n[1];
+        for (int j = 0; j < 8; ++j) xv[s0][j] = xn[s0][j];
+      h1[0] = h1n[0];
+      h1[1] = h1n[1];
+    }
   }
 };
 

@@ -634,9 +634,10 @@ __device__ inline float opaque(float m) {
 }
 // 16 B per lane global -> LDS (global_load_lds_dwordx4): lane L's bytes land at l + 16 L
 // (l wave-uniform); no VGPR destination
+template <int AUX = 0>  // AUX: cache-policy bits of the load (2 = nt)
 __device__ inline void glds16(const float* g, float* l) {
   __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, AUX);
 }
 constexpr int VJP16_W_FLOATS = 2 * 32 * 64 + 2 * 4 * 64;  // BA1 + BA2 of the image
 constexpr int VJP16_H1_FLOATS = 16 * 64;                  // h1 of one 16-row tile
@@ -1092,6 +1093,26 @@ constexpr int MBOX_GH = 2 * MAX_OUT;  // mailbox row pitch (floats): the widest 
 #ifndef MRL_FISHER_ROLE_PROBE
 #define MRL_FISHER_ROLE_PROBE 0
 #endif
+// L2 reuse of the activation cache between the roles (round 6): each role alone reads the
+// algorithmic 2.33 GB per Hopper product, the pair 4.36 GB -- the VJP role's re-reads of a
+// tile a round after the JVP role's miss the XCD's 4 MB L2 (profiles/r06f_fisher_pmc.txt).
+// MRL_FISHER_JVP_PF 0: the JVP role loads a tile's x / h1 in its own round (no prefetch a
+// round ahead); MRL_FISHER_VJP_NT 1: the VJP role's loads (the last use of those bytes) are
+// non-temporal, so they do not displace the lines still to be re-read
+#ifndef MRL_FISHER_JVP_PF
+#define MRL_FISHER_JVP_PF 1
+#endif
+#ifndef MRL_FISHER_VJP_NT
+#define MRL_FISHER_VJP_NT 0
+#endif
+__device__ inline f32x4 ldv4(const f32x4* p) {
+  if constexpr (MRL_FISHER_VJP_NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+__device__ inline float ldv1(const float* p) {
+  if constexpr (MRL_FISHER_VJP_NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
 
 struct FisherFusedIn {
   RowsArgs ra;        // the JVP rows' arguments (x, n, inv_ng, logstd / dlogstd, cache)
@@ -1180,12 +1201,13 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
         dls[j] = (ra.dlogstd != nullptr && j < ra.A) ? ra.dlogstd[j] : 0.f;
       }
       int64_t T = (int64_t)blockIdx.x * 4 + wave;
-      if (T < nt32) role.prologue(T);
+      if (MRL_FISHER_JVP_PF && T < nt32) role.prologue(T);
       for (int64_t r = 0; r < rounds; ++r) {
         if (MRL_FISHER_ROLE_PROBE != 2 && r + 1 < rounds && T < nt32) {
           const int64_t tn = T + stride32 < nt32 ? T + stride32 : T;  // the last tile re-reads itself
           float* mb = mbox + ((r & 1) * 4 + wave) * 32 * MBOX_GH + (lane & 31) * MBOX_GH;
-          role.tile(T, tn, [&](bool valid, int64_t, const float (&z)[MAX_OUT], const float (&dz)[MAX_OUT]) {
+          role.template tile<MRL_FISHER_JVP_PF != 0>(T, tn, [&](bool valid, int64_t, const float (&z)[MAX_OUT],
+                                                                  const float (&dz)[MAX_OUT]) {
             if ((lane >> 5) == 0) {
               // the KL-metric head-gradient row (row_epilogue FVP); rows past n hold 0
               float gg[MAX_OUT], gl[MAX_OUT];
@@ -1232,14 +1254,12 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
   auto load_h2 = [&](int64_t t) {
     const float* ct = a.cache + (t >> 1) * CACHE_TILE_FLOATS + 16 * (int)(t & 1) * 4;
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const float4 v = ld4(ct + (2 + (nt >> 1)) * 1024 + 512 * (nt & 1) + offR);
-      h2R[nt] = f32x4{v.x, v.y, v.z, v.w};
-    }
+    for (int nt = 0; nt < 4; ++nt)
+      h2R[nt] = ldv4(reinterpret_cast<const f32x4*>(ct + (2 + (nt >> 1)) * 1024 + 512 * (nt & 1) + offR));
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h2T[nt][r] = ct[(2 + (nt >> 1)) * 1024 + 512 * (nt & 1) + 4 * r + offT];
+      for (int r = 0; r < 4; ++r) h2T[nt][r] = ldv1(ct + (2 + (nt >> 1)) * 1024 + 512 * (nt & 1) + 4 * r + offT);
   };
   // G of 16-row tile t from its 32-row tile's mailbox rows mbt: G[row0 + c][4 ks + g]
   // (operand of both gh2 products), G[row0 + 4 g + r][c] (B operand of gW2, bias / logstd sums)
@@ -1278,7 +1298,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
 #pragma unroll
       for (int m0 = 0; m0 < MT0; ++m0) {
         const int col = 16 * m0 + c;
-        xN[m0][r] = a.x[rc * a.n_obs + (col < a.n_obs ? col : a.n_obs - 1)];
+        xN[m0][r] = ldv1(a.x + rc * a.n_obs + (col < a.n_obs ? col : a.n_obs - 1));
       }
     }
   };
@@ -1296,7 +1316,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
     for (int i = 0; i < 4; ++i) {
       const int run = 4 * i + (lane >> 4), sq = run >> 1, hh = run & 1, k = 2 * (sq & 1) + hh;
       const int j = 4 * (jj >> 2) + ((jj - k) & 3);
-      glds16(ct + (sq * 64 + 32 * hh + j) * 4, h1s + b * VJP16_H1_FLOATS + i * 256);
+      glds16<MRL_FISHER_VJP_NT ? 2 : 0>(ct + (sq * 64 + 32 * hh + j) * 4, h1s + b * VJP16_H1_FLOATS + i * 256);
     }
   };
   // lane parts of the T read offsets: run bits from c, rotated row 4 g + ((r + (c >> 2)) & 3)

@@ -26,6 +26,7 @@ ROLES = [
     ("rows_vfloss", "mlp_rows_kernel<3,"),
     ("rollout_persistent", "rollout_persistent_kernel"),
     ("rollout_step", "rollout_step_kernel"),
+    ("gae_scan", "gae_full_kernel"),                  # the exact-fit GAE kernel (round 6)
     ("gae_scan", "gae_scan_kernel"),
     ("episode_stats", "episode_stats_kernel<"),
     ("gemm_nn", "gemm_f32_kernel<false, false, 128>"),
