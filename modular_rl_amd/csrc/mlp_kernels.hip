@@ -1094,13 +1094,15 @@ constexpr int MBOX_GH = 2 * MAX_OUT;  // mailbox row pitch (floats): the widest 
 #define MRL_FISHER_ROLE_PROBE 0
 #endif
 // L2 reuse of the activation cache between the roles (round 6): each role alone reads the
-// algorithmic 2.33 GB per Hopper product, the pair 4.36 GB -- the VJP role's re-reads of a
-// tile a round after the JVP role's miss the XCD's 4 MB L2 (profiles/r06f_fisher_pmc.txt).
-// MRL_FISHER_JVP_PF 0: the JVP role loads a tile's x / h1 in its own round (no prefetch a
-// round ahead); MRL_FISHER_VJP_NT 1: the VJP role's loads (the last use of those bytes) are
-// non-temporal, so they do not displace the lines still to be re-read
+// algorithmic 2.33 GB per Hopper product, the pair 4.35 GB -- the VJP role's re-reads of a
+// tile a round after the JVP role's miss the XCD's 4 MB L2 (each round brings ~4.5 MB per
+// XCD: both roles' reads plus the JVP's prefetch of the next tile; profiles/r06g_fisher_l2.txt).
+// MRL_FISHER_JVP_PF 0 (the default): the JVP role loads a tile's x / h1 in the tile's own
+// round, not a round ahead -- 4.35 -> 3.98 GB and 1.309 -> 1.277 ms per product;
+// MRL_FISHER_VJP_NT 1: the VJP role's loads (the last use of those bytes) non-temporal --
+// 3.57 GB (3.34 with both) but 1.32 ms: not kept
 #ifndef MRL_FISHER_JVP_PF
-#define MRL_FISHER_JVP_PF 1
+#define MRL_FISHER_JVP_PF 0
 #endif
 #ifndef MRL_FISHER_VJP_NT
 #define MRL_FISHER_VJP_NT 0
