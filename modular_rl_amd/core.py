@@ -85,6 +85,16 @@ class _GaeWorkspace:
 _GAE = _GaeWorkspace()
 
 
+def gae_scan(batch, gamma, lam):
+    """The GAE + discounted-return scan of a time-major batch (mrl_gae: adv / ret rows and
+    the first-pass moments into the module workspace) -- compute_advantage_batch's scan,
+    also timed on its own by bench.py."""
+    ws_gae, _, moments = _GAE.get(batch.T, batch.E, batch.rew.device)
+    call("mrl_gae", ptr(batch.rew), ptr(batch.vpred), ptr(batch.flags), int(batch.T), int(batch.E), float(gamma),
+         float(lam), ptr(batch.adv), ptr(batch.ret), ptr(moments), ptr(ws_gae), stream())
+    return moments
+
+
 def compute_advantage_batch(vf, batch, gamma, lam, comm=None):
     """Device form of `core.py:63-105` on a time-major batch: baseline forward,
     GAE + discounted return scan (mrl_gae), then standardisation with the global
@@ -97,10 +107,9 @@ def compute_advantage_batch(vf, batch, gamma, lam, comm=None):
     if batch.adv is None or batch.adv.numel() != n:
         batch.adv = torch.empty(n, dtype=torch.float32, device=dev)
         batch.ret = torch.empty(n, dtype=torch.float32, device=dev)
-    ws_gae, ws, moments = _GAE.get(batch.T, batch.E, dev)
+    ws, moments = _GAE.get(batch.T, batch.E, dev)[1:]
     timing.start("gae_scan", detail=True)
-    call("mrl_gae", ptr(batch.rew), ptr(batch.vpred), ptr(batch.flags), int(batch.T), int(batch.E), float(gamma),
-         float(lam), ptr(batch.adv), ptr(batch.ret), ptr(moments), ptr(ws_gae), stream())
+    gae_scan(batch, gamma, lam)
     timing.stop("gae_scan")
     # numpy's two-pass std (core.py:100-105): global mean first, then the centred sums
     comm.allreduce_(moments[0])
@@ -371,6 +380,7 @@ class IterationRunner:
                 done = self._fit_pending(self.fit_stream, ev)
             self._order(self.rollout_stream, main)
         batch = col.finish()
+        self.last_batch = batch
         ev["adv0"] = self._event()
         compute_advantage_batch(agent.baseline, batch, cfg["gamma"], cfg["lam"], self.comm)
         ev["adv1"] = self._event()

@@ -41,13 +41,17 @@ for step in "$@"; do
         { echo PROF_FAILED; tail -5 gpurun_out/${tag}_prof.log; exit 1; }
       python tools/host_gap.py gpurun_out/${tag}_prof/run_kernel_trace.csv > gpurun_out/${tag}_host_gap.txt &&
         tail -4 gpurun_out/${tag}_host_gap.txt ;;
-    pmc)
+    pmc)  # counter passes serialise the dispatches: the rollout <-> iteration streams are ordered
+          # by events there (MRL_XSTREAM_EVENT=1); a stream waiting on a memory value written by a
+          # packet queued behind it would never run (r06i: the FETCH pass hung)
+      export MRL_XSTREAM_EVENT=1
       timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${tag}_pmc_fetch -o run \
         -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${tag}_pmc_f.log 2>&1 || exit 1
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${tag}_pmc_write -o run \
         -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${tag}_pmc_w.log 2>&1 || exit 1
       python tools/pmc_traffic.py gpurun_out/${tag}_pmc_fetch gpurun_out/${tag}_pmc_write \
-        --out gpurun_out/${tag}_pmc.json > /dev/null && echo PMC_OK ;;
+        --out gpurun_out/${tag}_pmc.json > /dev/null && echo PMC_OK
+      unset MRL_XSTREAM_EVENT ;;
     lines)
       bench hopper_bf16 400 --dtype bf16 --no-cpu-baseline
       bench cartpole_bf16 400 --env CartPole-v0 --dtype bf16 --no-cpu-baseline
@@ -62,6 +66,7 @@ for step in "$@"; do
       python tools/sq_split.py gpurun_out/${tag}_sq mlp_fisher_hyb_kernel mlp_fvp_split_kernel mlp_vjp16_kernel \
         > gpurun_out/${tag}_sq.txt && cat gpurun_out/${tag}_sq.txt ;;
     issue)  # the persistent rollout's SQ issue floor per step -> profiles-style TAG_rollout_issue.json
+      export MRL_XSTREAM_EVENT=1  # counter passes: event ordering (see pmc)
       for line in "Hopper-v2 fp32" "Hopper-v2 bf16" "CartPole-v0 bf16" "CartPole-v0 fp32"; do
         set -- $line
         timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY \
@@ -69,7 +74,8 @@ for step in "$@"; do
           -- python3 bench.py --env $1 --dtype $2 --steps 2 --warmup 1 --no-cpu-baseline \
           > gpurun_out/${tag}_issue_$1_$2.log 2>&1 || { echo ISSUE_FAILED $1 $2; tail -5 gpurun_out/${tag}_issue_$1_$2.log; exit 1; }
         python tools/rollout_issue.py gpurun_out/${tag}_issue_$1_$2 $1/$2 1024 --out gpurun_out/${tag}_rollout_issue.json
-      done ;;
+      done
+      unset MRL_XSTREAM_EVENT ;;
     stamps)
       timeout -k 10 300 python -u tools/persistent_stamps.py Hopper-v2 > gpurun_out/${tag}_stamps.txt 2>&1 ||
         { tail -5 gpurun_out/${tag}_stamps.txt; exit 1; }
