@@ -385,6 +385,18 @@ __device__ inline double dpp_d(double v) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
+// x / n for an env count n >= 0 (a mean of n values): when every active lane's n is a power
+// of two -- a full 64-env block, E = 4096 -- the multiply by the exact 2^-k instead, which is
+// the same correctly rounded value as the division (x 2^-k and x / 2^k round the same real
+// number once), without the division's dependent v_div_scale / v_rcp / fma chain on the
+// step's critical path; the branch is wave-uniform (a ballot)
+__device__ inline double div_count(double x, double n) {
+  int e;
+  const double m = frexp(n, &e);
+  if (__builtin_amdgcn_ballot_w64(m != 0.5) == 0) return x * ldexp(1.0, 1 - e);
+  return x / n;
+}
+
 __device__ inline double sum16(double v) {
   v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
@@ -401,7 +413,7 @@ __device__ inline void publish_partial(const RollArgs& a, const double* vals, in
   double s = 0.0;
   if (k < D)
     for (int i = j; i < nvalid; i += 16) s += vals[i * D + k];
-  const double mean = nvalid > 0 ? sum16(s) / (double)nvalid : 0.0;
+  const double mean = nvalid > 0 ? div_count(sum16(s), (double)nvalid) : 0.0;
   double m2 = 0.0;
   if (k < D)
     for (int i = j; i < nvalid; i += 16) {
@@ -453,7 +465,7 @@ struct RecRoundT {
     accumulate(n, sm, raw);
     n = sum16(n);
     sm = sum16(sm);
-    const double mean = n > 0.0 ? sm / n : 0.0;
+    const double mean = n > 0.0 ? div_count(sm, n) : 0.0;
     double m2 = 0.0;
 #pragma unroll
     for (int q = 0; q < R; ++q)
@@ -487,7 +499,7 @@ __device__ inline void batch_of_records(const double* rec, int nb, int RS, int D
   }
   n = sum16(n);
   sm = sum16(sm);
-  const double mean = n > 0.0 ? sm / n : 0.0;
+  const double mean = n > 0.0 ? div_count(sm, n) : 0.0;
   bn = n;
   bm = mean;
   bs = sum16(raw) - n * mean * mean;
@@ -885,7 +897,7 @@ __device__ inline void publish_granules(const Granules& gr, const double* vals, 
   double s = 0.0;
   if (k < gr.D)
     for (int i = j; i < nvalid; i += 16) s += vals[i * gr.D + k];
-  const double mean = nvalid > 0 ? sum16(s) / (double)nvalid : 0.0;
+  const double mean = nvalid > 0 ? div_count(sum16(s), (double)nvalid) : 0.0;
   double m2 = 0.0;
   if (k < gr.D)
     for (int i = j; i < nvalid; i += 16) {
@@ -1058,7 +1070,7 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
         }
         n = sum16(n);
         sm = sum16(sm);
-        bm = n > 0.0 ? sm / n : 0.0;
+        bm = n > 0.0 ? div_count(sm, n) : 0.0;
         bn = n;
         bs = sum16(raw) - n * bm * bm;
       }
@@ -1202,7 +1214,7 @@ __global__ __launch_bounds__(RB) void lrollout_partials_kernel(RollArgs a, int D
   double tot = 0.0;
 #pragma unroll
   for (int q = 0; q < 8; ++q) tot += red[q][c];
-  const double mean = nvalid > 0 ? tot / (double)nvalid : 0.0;
+  const double mean = nvalid > 0 ? div_count(tot, (double)nvalid) : 0.0;
   __syncthreads();
   double m2 = 0.0;
   if (k < D)
