@@ -185,6 +185,15 @@ int32_t mrl_mlp_fisher_hyb_fits(const mrl_mlp_desc* d);
 int mrl_mlp_fisher_hyb(const mrl_mlp_desc* d, const float* theta, const float* image, const float* image_s,
                        const float* tangent, const float* image_t_s, const mrl_rows_io* io, float* slab,
                        const int32_t* skip, void* stream);
+/* The policy gradient in ONE launch (trpo.py:42-43, the surrogate's flat gradient; round
+ * 6): mrl_mlp_rows_split's SURRGRAD pass (io: x, n, inv_n_global, act, adv, oldprob,
+ * partial; act_cache with MRL_CACHE_WRITE, written as that pass writes it) beside the
+ * hybrid VJP of mrl_mlp_vjp in each block, the head-gradient rows through LDS (no ghead in
+ * HBM).  slab: mrl_mlp_slab_rows(d, n) rows of P floats (reduce with mrl_reduce_rows_f32);
+ * partial: the same number of rows of 4 doubles (surr, kl, ent, 0 sums; reduce with
+ * mrl_reduce_rows_f64).  Same shapes as mrl_mlp_fisher_hyb (mrl_mlp_fisher_hyb_fits). */
+int mrl_mlp_grad_hyb(const mrl_mlp_desc* d, const float* theta, const float* image, const float* image_s,
+                     const mrl_rows_io* io, float* slab, const int32_t* skip, void* stream);
 
 int mrl_reduce_rows_f32(const float* slab, int64_t rows, int64_t cols, float* out, const int32_t* skip, void* stream);
 int mrl_reduce_rows_f64(const double* slab, int64_t rows, int64_t cols, double* out, const int32_t* skip, void* stream);

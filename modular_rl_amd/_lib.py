@@ -10,7 +10,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # MRL_LIB_PATH: diagnostic override (ablation builds under tools/); the default is the in-tree build
-LIB_PATH = os.environ.get("MRL_LIB_PATH") or os.path.join(_HERE, "libmrl_hip.so")
+_DEFAULT_PATH = os.path.join(_HERE, "libmrl_hip.so")
+LIB_PATH = os.environ.get("MRL_LIB_PATH") or _DEFAULT_PATH
 
 OK = 0
 HEAD_LINEAR, HEAD_SOFTMAX, HEAD_GAUSS = 0, 1, 2
@@ -101,6 +102,7 @@ SIGNATURES = {
     "mrl_mlp_fisher_hyb_fits": (i32, [vp]),
     "mrl_mlp_rows_split": (i32, [vp, i32, vp, vp, vp, vp, vp]),
     "mrl_mlp_fisher_hyb": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "mrl_mlp_grad_hyb": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_mlp_fvp_split": (i32, [vp, vp, vp, vp, vp, vp, vp, vp]),
     "mrl_reduce_rows_f32": (i32, [vp, i64, i64, vp, vp, vp]),
     "mrl_reduce_rows_f64": (i32, [vp, i64, i64, vp, vp, vp]),
@@ -174,6 +176,8 @@ def load(require_gpu=False):
                            "modular_rl_amd has no CPU fallback")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if LIB_PATH != _DEFAULT_PATH and not hasattr(lib, name):
+                continue  # an ablation build that predates this entry point
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

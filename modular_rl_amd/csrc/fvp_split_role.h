@@ -240,6 +240,69 @@ struct JvpSplitRole {
   }
 };
 
+// One 32-row tile of the forward row passes on split operands (mlp_rows_split_kernel's
+// per-tile body; also the one-pass policy gradient's forward role, mlp_fisher_hyb_kernel
+// PROD 1): h1 = tanh(x W0 + b0), h2 = tanh(h1 W1 + b1) with six bf16 part products per
+// k-step, the head on the f32 VALU, the activation cache stored when `store`; then the
+// row epilogue of lane half 0 with its arguments / row index `ae`, `erow` (the pass's own
+// `a`, row -- or tile-local ones: the one-pass gradient points ghead at its LDS mailbox,
+// LDSHEAD)
+template <int EPI, bool LDSHEAD = false>
+__device__ __forceinline__ void split_rows_tile(const RowsArgs& a, const BDims& b, const float* img, const MlpDims& dd,
+                                                int lane, int64_t tile, bool store, const float (&ls)[MAX_OUT],
+                                                const float (&sd)[MAX_OUT], const float (&dls)[MAX_OUT],
+                                                double& acc0, double& acc1, double& acc2, const RowsArgs& ae,
+                                                int64_t erow) {
+  const int h = lane >> 5, PS = split_fw(b);
+  const int64_t row = tile * 32 + (lane & 31);
+  const bool valid = row < a.n;
+  XGlobalNB xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
+  float* ct = store ? a.cache + tile * CACHE_TILE_FLOATS : nullptr;
+  // layer 0: h1 = tanh(x W0 + b0)
+  f32x16 h1[2] = {load_bias16(img, b.fb0, 0, h), load_bias16(img, b.fb0, 1, h)};
+#pragma unroll
+  for (int s0 = 0; s0 < MAX_KS0B; ++s0) {
+    if (s0 < b.KS0B) {
+      float xv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xv[j] = xl(16 * s0 + 8 * h + j);
+      bf16x8 xs[3];
+      split8v(xv, xs);
+      mfma_split(img, b.fa0, PS, 0 * b.KS0B + s0, lane, xs, h1[0]);
+      mfma_split(img, b.fa0, PS, 1 * b.KS0B + s0, lane, xs, h1[1]);
+    }
+  }
+  tanh16(h1[0]);
+  tanh16(h1[1]);
+  if (store) {
+    cache_store(ct, lane, 0, h1[0]);
+    cache_store(ct, lane, 1, h1[1]);
+  }
+  // layer 1: h2 = tanh(h1 W1 + b1), each input fragment split once for both output tiles
+  f32x16 a2[2] = {load_bias16(img, b.fb1, 0, h), load_bias16(img, b.fb1, 1, h)};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    bf16x8 ps[3];
+    split8(h1[s >> 1], s & 1, ps);
+    mfma_split(img, b.fa1, PS, 0 * 4 + s, lane, ps, a2[0]);
+    mfma_split(img, b.fa1, PS, 1 * 4 + s, lane, ps, a2[1]);
+  }
+  FVP_SPLIT_FENCE();
+  float z[MAX_OUT], dz[MAX_OUT];
+#pragma unroll
+  for (int o = 0; o < MAX_OUT; ++o) z[o] = dz[o] = 0.f;
+#pragma unroll
+  for (int mo = 0; mo < 2; ++mo) {
+    tanh16(a2[mo]);
+    if (store) cache_store(ct, lane, 2 + mo, a2[mo]);
+    head_partial_mt(img, dd, a2[mo], mo, h, z);
+  }
+  head_finish(img, dd, z);
+  if constexpr (EPI == MRL_EPI_PROB)
+    if (a.feat != nullptr && valid) write_feature_row(a, row, h, xl);
+  if (valid && h == 0) row_epilogue<EPI, MAX_OUT, LDSHEAD>(ae, erow, z, dz, ls, sd, dls, acc0, acc1, acc2);
+}
+
 // launch mlp_rows_split_kernel<epi, sh> (mlp_split.hip) for mrl_mlp_rows_split
 int launch_rows_split(int epi, int sh, const RowsArgs& a, const BDims& b, const float* image_s, int64_t blocks,
                       const int32_t* skip, void* stream);

@@ -1117,13 +1117,20 @@ __device__ inline float ldv1(const float* p) {
 }
 
 struct FisherFusedIn {
-  RowsArgs ra;        // the JVP rows' arguments (x, n, inv_ng, logstd / dlogstd, cache)
+  RowsArgs ra;        // the producer rows' arguments (x, n, inv_ng, logstd / dlogstd, cache;
+                      // PROD 1: act / adv / oldprob / partial, the cache written)
   BDims rb;
   const float* img_s; // split images of theta and of the tangent (mrl_mlp_pack_split)
-  const float* imt_s;
+  const float* imt_s; // (PROD 1: unused)
 };
 
-template <int SH>
+// PROD: what waves 0-3 produce for the VJP role.  0: the Fisher product's JVP rows (the KL
+// metric's head-gradient rows along a tangent, reading the activation cache); 1: the
+// policy gradient's forward rows (round 6, mrl_mlp_grad_hyb) -- the SURRGRAD pass of
+// mlp_rows_split_kernel (split_rows_tile, the same per-row code), which writes the
+// activation cache the VJP role then reads and the surrogate head-gradient rows into the
+// mailbox, and leaves the surr / KL / entropy sums per producer wave in the partial rows
+template <int SH, int PROD = 0>
 __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(VjpArgs a, const float* __restrict__ img,
                                                                            const int32_t* __restrict__ skip,
                                                                            FisherFusedIn fz) {
@@ -1135,7 +1142,10 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
   // B fragments of gh1 = ga2 W1^T, [k-step s][tile nt][part p][lane], 24 KB
   __shared__ __attribute__((aligned(16))) bf16x8 wbs[2 * 4 * 3 * 64];
   // head-gradient rows of the JVP waves' tiles, [slot][JVP wave][row][MBOX_GH]
-  __shared__ __attribute__((aligned(16))) float mbox[2 * 4 * 32 * MBOX_GH];
+  // PROD 1 runs the VJP two rounds behind (LAG): its prefetch of the next tile then reads
+  // cache rows the producer finished a round earlier; NSLOT mailbox slots per JVP wave
+  constexpr int LAG = PROD == 1 ? 2 : 1, NSLOT = LAG + 1;
+  __shared__ __attribute__((aligned(16))) float mbox[NSLOT * 4 * 32 * MBOX_GH];
   extern __shared__ __attribute__((aligned(16))) float ldsx[];  // the two split images
   if (skip != nullptr && *skip != 0) return;
   const MlpDims& d = a.d;
@@ -1144,7 +1154,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
   const int WS = split_fwd_words(fz.rb);
   for (int i = threadIdx.x; i < WS / 4; i += 64 * VJP16_WAVES) {
     reinterpret_cast<float4*>(ldsx)[i] = reinterpret_cast<const float4*>(fz.img_s)[i];
-    reinterpret_cast<float4*>(ldsx + WS)[i] = reinterpret_cast<const float4*>(fz.imt_s)[i];
+    if constexpr (PROD == 0) reinterpret_cast<float4*>(ldsx + WS)[i] = reinterpret_cast<const float4*>(fz.imt_s)[i];
   }
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform tile bases
@@ -1183,13 +1193,63 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
   // round-r tiles (32-row tile T = (r G + block) 4 + w) and the VJP waves consume slot
   // (r - 1) & 1; every wave passes the same number of barriers (one per round)
   const int64_t nt32 = (a.n + 31) / 32, stride32 = (int64_t)gridDim.x * 4;
-  const int64_t rounds = (nt32 + stride32 - 1) / stride32 + 1;
+  const int64_t rounds = (nt32 + stride32 - 1) / stride32 + LAG;
   auto fused_barrier = []() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's mailbox writes / reads are done
     if (MRL_FISHER_ROLE_PROBE != 3) __builtin_amdgcn_s_barrier();  // 3: timing build without the rounds' barrier
     asm volatile("" ::: "memory");
   };
-  {
+  if constexpr (PROD == 1) {
+    if (wave < 4) {
+      RowsArgs ra = fz.ra;
+      BDims rb = fz.rb;
+      split_shape<SH>(ra, rb);
+      const MlpDims dd = head_dims(ra.d, rb);
+      float ls[MAX_OUT], sd[MAX_OUT], dls[MAX_OUT];
+#pragma unroll
+      for (int j = 0; j < MAX_OUT; ++j) {
+        ls[j] = (ra.logstd != nullptr && j < ra.A) ? ra.logstd[j] : 0.f;
+        sd[j] = expf(ls[j]);
+        dls[j] = 0.f;
+      }
+      const int A = ra.A, actw = ra.head == MRL_HEAD_SOFTMAX ? 1 : A, opw = ra.head == MRL_HEAD_SOFTMAX ? A : 2 * A;
+      double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
+      int64_t T = (int64_t)blockIdx.x * 4 + wave;
+      for (int64_t r = 0; r < rounds; ++r) {
+        if (r + LAG < rounds && T < nt32) {
+          // the row epilogue's inputs at this tile's rows and its head-gradient row in the
+          // mailbox (pitch MBOX_GH; rows past n get zeros, as the JVP role's)
+          float* mb = mbox + ((r % NSLOT) * 4 + wave) * 32 * MBOX_GH;
+          const int64_t row0 = T * 32;
+          RowsArgs ae = ra;
+          ae.adv = ra.adv + row0;
+          ae.act = ra.head == MRL_HEAD_SOFTMAX ? (const void*)(reinterpret_cast<const int32_t*>(ra.act) + row0)
+                                               : (const void*)(reinterpret_cast<const float*>(ra.act) + row0 * actw);
+          ae.oldprob = ra.oldprob + row0 * opw;
+          ae.ghead = mb;
+          ae.gh = MBOX_GH;
+          if ((lane >> 5) == 0 && row0 + (lane & 31) >= ra.n)
+            for (int j = 0; j < MBOX_GH; ++j) mb[(lane & 31) * MBOX_GH + j] = 0.f;
+          split_rows_tile<MRL_EPI_SURRGRAD, true>(ra, rb, ldsx, dd, lane, T, true, ls, sd, dls, acc0, acc1, acc2, ae,
+                                            lane & 31);
+          T += stride32;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's cache rows are in L2 for the VJP waves
+        fused_barrier();
+      }
+      acc0 = wave_sum(acc0);
+      acc1 = wave_sum(acc1);
+      acc2 = wave_sum(acc2);
+      if (lane == 0) {
+        double* p = ra.partial + ((int64_t)blockIdx.x * 4 + wave) * 4;
+        p[0] = acc0;
+        p[1] = acc1;
+        p[2] = acc2;
+        p[3] = 0.0;
+      }
+      return;
+    }
+  } else {
     if (wave < 4) {
       RowsArgs ra = fz.ra;
       BDims rb = fz.rb;
@@ -1449,16 +1509,20 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
   {
     const int vw = wave - 4;
     int64_t T = (int64_t)blockIdx.x * 4 + vw;
-    if (T < nt32) {
-      load_h2(2 * T);
-      load_x(2 * T);
-      dma_h1(2 * T, 0);
-      take_x();
+    // the first tile's inputs: before round 0's barrier (PROD 0: the cache is read-only
+    // here), or after it (PROD 1: the producer wrote them in round 0)
+    for (int64_t r = 0; r < LAG; ++r) {
+      if (r == LAG - 1 && T < nt32) {
+        load_h2(2 * T);
+        load_x(2 * T);
+        dma_h1(2 * T, 0);
+        take_x();
+      }
+      fused_barrier();  // round r: the producer waves fill slot r
     }
-    fused_barrier();  // round 0: the JVP waves fill slot 0
-    for (int64_t r = 1; r < rounds; ++r) {
+    for (int64_t r = LAG; r < rounds; ++r) {
       if (MRL_FISHER_ROLE_PROBE != 1 && T < nt32) {
-        mbt = mbox + (((r - 1) & 1) * 4 + vw) * 32 * MBOX_GH;
+        mbt = mbox + (((r - LAG) % NSLOT) * 4 + vw) * 32 * MBOX_GH;
         const int64_t Tn = T + stride32 < nt32 ? T + stride32 : T;  // the last tile re-reads itself
 #pragma unroll 1
         for (int hf = 0; hf < 2; ++hf) vjp_tile(2 * T + hf, hf ? 2 * Tn : 2 * T + 1);
@@ -1951,6 +2015,63 @@ int mrl_mlp_fisher_hyb(const mrl_mlp_desc* d, const float* theta, const float* i
     default: hipLaunchKernelGGL((mlp_fisher_hyb_kernel<2>), grid, blk, shm, s, a, image, skip, fz); break;
   }
   return hip_check(hipGetLastError(), "mrl_mlp_fisher_hyb");
+}
+
+int mrl_mlp_grad_hyb(const mrl_mlp_desc* d, const float* theta, const float* image, const float* image_s,
+                     const mrl_rows_io* io, float* slab, const int32_t* skip, void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (!io || !image || !image_s || !io->x || !slab) return fail(E_ARG, "null pointer");
+  if (!io->act || !io->adv || !io->oldprob || !io->partial) return fail(E_ARG, "mrl_mlp_grad_hyb needs act/adv/oldprob/partial");
+  if (!io->act_cache || io->cache_mode != MRL_CACHE_WRITE)
+    return fail(E_ARG, "mrl_mlp_grad_hyb writes the f32 activation cache (MRL_CACHE_WRITE)");
+  if (io->ep_t) return fail(E_ARG, "mrl_mlp_grad_hyb: policy rows only (no time feature)");
+  if (d->head == MRL_HEAD_LINEAR) return fail(E_ARG, "policy gradient of a value net");
+  if (d->head == MRL_HEAD_GAUSS && !theta) return fail(E_ARG, "DiagGauss needs theta (logstd)");
+  if (mrl_mlp_fisher_hyb_fits(d) != 1) return fail(E_UNSUPPORTED, "mrl_mlp_grad_hyb: shape does not fit one block's LDS");
+  if (io->n <= 0) return OK;
+  VjpArgs a;
+  a.d = dims_of(d);
+  a.n_obs = d->n_in;
+  a.n_sum = d->head == MRL_HEAD_GAUSS ? d->n_out : 0;
+  a.gh = d->n_out + a.n_sum;
+  a.x = io->x;
+  a.ept = nullptr;
+  a.ts_limit = 1.0;
+  a.n = io->n;
+  a.ghead = nullptr;
+  a.slab = slab;
+  a.cache = io->act_cache;
+  FisherFusedIn fz{};
+  RowsArgs& r = fz.ra;
+  r.d = mlp_dims(d->n_in, d->n_out, d->head == MRL_HEAD_GAUSS);
+  r.head = d->head;
+  r.n_obs = d->n_in;
+  r.gh = a.gh;
+  r.A = d->n_out;
+  r.x = io->x;
+  r.n = io->n;
+  r.inv_ng = io->inv_n_global;
+  r.act = io->act;
+  r.adv = io->adv;
+  r.oldprob = io->oldprob;
+  r.partial = io->partial;
+  r.logstd = d->head == MRL_HEAD_GAUSS ? theta + r.d.tls : nullptr;
+  r.cache = io->act_cache;
+  r.cache_mode = MRL_CACHE_WRITE;
+  fz.rb = bf16_dims(d->n_in, d->n_out);
+  fz.img_s = image_s;
+  fz.imt_s = nullptr;
+  // the VJP's grid and slab rows (mrl_mlp_slab_rows): one slab row per VJP wave, and one
+  // partial row (surr, kl, ent, 0) per producer wave -- the same count
+  const dim3 grid(vjp_blocks(io->n, desc_cus(d))), blk(64 * VJP16_WAVES);
+  const size_t shm = (size_t)split_fwd_words(fz.rb) * 4;
+  hipStream_t s = (hipStream_t)stream;
+  switch (static_shape_of(d, false)) {
+    case 1: hipLaunchKernelGGL((mlp_fisher_hyb_kernel<1, 1>), grid, blk, shm, s, a, image, skip, fz); break;
+    default: hipLaunchKernelGGL((mlp_fisher_hyb_kernel<2, 1>), grid, blk, shm, s, a, image, skip, fz); break;
+  }
+  return hip_check(hipGetLastError(), "mrl_mlp_grad_hyb");
 }
 
 int mrl_probtype_rows(int32_t head, int32_t k, int64_t n, const float* prob, const float* prob2, const void* x,

@@ -128,13 +128,13 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, 2) void mlp_rows_split_kernel(Row
   split_rows_shape<SH>(a, b);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if (skip != nullptr && *skip != 0) return;
-  const int W = split_fwd_words(b), PS = split_fw(b);
+  const int W = split_fwd_words(b);
   for (int i = threadIdx.x; i < W / 4; i += SPLIT_ROWS_BLOCK)
     reinterpret_cast<float4*>(lds)[i] = reinterpret_cast<const float4*>(img_g)[i];
   __syncthreads();
   const float* img = lds;
   const MlpDims dd = head_dims(a.d, b);
-  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int A = a.A;
   float ls[MAX_OUT], sd[MAX_OUT], dls[MAX_OUT];
@@ -150,52 +150,7 @@ __global__ __launch_bounds__(SPLIT_ROWS_BLOCK, 2) void mlp_rows_split_kernel(Row
   for (int64_t tile = (int64_t)blockIdx.x * SPLIT_ROWS_WAVES + wave; tile < ntiles;
        tile += (int64_t)gridDim.x * SPLIT_ROWS_WAVES) {
     const int64_t row = tile * 32 + (lane & 31);
-    const bool valid = row < a.n;
-    XGlobalNB xl{a.x, a.ept, a.ts_limit, a.n_obs, row, valid};
-    float* ct = store ? a.cache + tile * CACHE_TILE_FLOATS : nullptr;
-    // layer 0: h1 = tanh(x W0 + b0)
-    f32x16 h1[2] = {load_bias16(img, b.fb0, 0, h), load_bias16(img, b.fb0, 1, h)};
-#pragma unroll
-    for (int s0 = 0; s0 < MAX_KS0B; ++s0) {
-      if (s0 < b.KS0B) {
-        float xv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xv[j] = xl(16 * s0 + 8 * h + j);
-        bf16x8 xs[3];
-        split8v(xv, xs);
-        mfma_split(img, b.fa0, PS, 0 * b.KS0B + s0, lane, xs, h1[0]);
-        mfma_split(img, b.fa0, PS, 1 * b.KS0B + s0, lane, xs, h1[1]);
-      }
-    }
-    tanh16(h1[0]);
-    tanh16(h1[1]);
-    if (store) {
-      cache_store(ct, lane, 0, h1[0]);
-      cache_store(ct, lane, 1, h1[1]);
-    }
-    // layer 1: h2 = tanh(h1 W1 + b1), each input fragment split once for both output tiles
-    f32x16 a2[2] = {load_bias16(img, b.fb1, 0, h), load_bias16(img, b.fb1, 1, h)};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf16x8 ps[3];
-      split8(h1[s >> 1], s & 1, ps);
-      mfma_split(img, b.fa1, PS, 0 * 4 + s, lane, ps, a2[0]);
-      mfma_split(img, b.fa1, PS, 1 * 4 + s, lane, ps, a2[1]);
-    }
-    FVP_SPLIT_FENCE();
-    float z[MAX_OUT], dz[MAX_OUT];
-#pragma unroll
-    for (int o = 0; o < MAX_OUT; ++o) z[o] = dz[o] = 0.f;
-#pragma unroll
-    for (int mo = 0; mo < 2; ++mo) {
-      tanh16(a2[mo]);
-      if (store) cache_store(ct, lane, 2 + mo, a2[mo]);
-      head_partial_mt(img, dd, a2[mo], mo, h, z);
-    }
-    head_finish(img, dd, z);
-    if constexpr (EPI == MRL_EPI_PROB)
-      if (a.feat != nullptr && valid) write_feature_row(a, row, h, xl);
-    if (valid && h == 0) row_epilogue<EPI, MAX_OUT>(a, row, z, dz, ls, sd, dls, acc0, acc1, acc2);
+    split_rows_tile<EPI>(a, b, img, dd, lane, tile, store, ls, sd, dls, acc0, acc1, acc2, a, row);
   }
   if (a.partial != nullptr) {
     acc0 = wave_sum(acc0);

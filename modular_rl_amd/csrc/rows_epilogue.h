@@ -93,7 +93,18 @@ __device__ __forceinline__ void fvp_metric_row(const RowsArgs& a, const float (&
   }
 }
 
-template <int EPI, int MA>
+// a head-gradient store.  LDS destinations (the one-pass policy gradient's mailbox,
+// mlp_fisher_hyb_kernel PROD 1) take the value through an identity DPP move first: an LDS
+// op must not read a packed-f32 VALU result within 8 wait states (mlp_device.h; hipcc
+// pads packed-f32 -> VALU / DPP dependencies but not -> LDS ones), and the categorical
+// head's w * (onehot - p) pairs are SLP-vectorised into v_pk_mul_f32.
+template <bool LDSHEAD>
+__device__ __forceinline__ void st_head(float* p, float v) {
+  if constexpr (LDSHEAD) v = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xE4, 0xF, 0xF, false));
+  *p = v;
+}
+
+template <int EPI, int MA, bool LDSHEAD = false>
 __device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, const float (&z)[MA],
                                              const float (&dz)[MA], const float (&ls)[MA], const float (&sd)[MA],
                                              const float (&dls)[MA], double& acc0, double& acc1, double& acc2) {
@@ -143,7 +154,7 @@ __device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, con
           float gj = w * ((j == act ? 1.f : 0.f) - p[j]);
           if (EPI == MRL_EPI_PPOGRAD)
             gj += c * (a.reverse_kl ? p[j] * (logf(p[j] / op[j]) - kl) : p[j] - op[j]);
-          a.ghead[row * a.gh + j] = gj;
+          st_head<LDSHEAD>(a.ghead + row * a.gh + j, gj);
         }
       }
     } else {
@@ -183,25 +194,25 @@ __device__ __forceinline__ void row_epilogue(const RowsArgs& a, int64_t row, con
               gs += c * (1.f - (s0 * s0 + dm * dm) / (sd[j] * sd[j]));
             }
           }
-          a.ghead[row * a.gh + j] = gm;
-          a.ghead[row * a.gh + A + j] = gs;
+          st_head<LDSHEAD>(a.ghead + row * a.gh + j, gm);
+          st_head<LDSHEAD>(a.ghead + row * a.gh + A + j, gs);
         }
       }
     }
   } else if (EPI == MRL_EPI_VFLOSS) {
     const float err = z[0] - a.target[row];
     acc0 += (double)err * (double)err;
-    a.ghead[row] = (float)(2.0 * a.inv_ng) * err;
+    st_head<LDSHEAD>(a.ghead + row, (float)(2.0 * a.inv_ng) * err);
   } else if (EPI == MRL_EPI_FVP) {
     float g[MA], gl[MA];
     fvp_metric_row<MA>(a, z, dz, sd, dls, g, gl);
     if (a.head == MRL_HEAD_GAUSS) {
       for (int j = 0; j < A; ++j) {
-        a.ghead[row * a.gh + j] = g[j];
-        a.ghead[row * a.gh + A + j] = gl[j];
+        st_head<LDSHEAD>(a.ghead + row * a.gh + j, g[j]);
+        st_head<LDSHEAD>(a.ghead + row * a.gh + A + j, gl[j]);
       }
     } else {
-      for (int j = 0; j < A; ++j) a.ghead[row * a.gh + j] = g[j];
+      for (int j = 0; j < A; ++j) st_head<LDSHEAD>(a.ghead + row * a.gh + j, g[j]);
     }
   }
 }

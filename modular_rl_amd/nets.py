@@ -146,6 +146,10 @@ class MlpNet:
         # the forward row passes (PROB / LOSSES / SURRGRAD / VFLOSS) of the net's own theta
         # on the same split operands (mrl_mlp_rows_split); MRL_ROWS_SPLIT=0: exact-f32 kernel
         self.rows_split = self.fisher_split and os.environ.get("MRL_ROWS_SPLIT", "1") != "0"
+        # the policy gradient (SURRGRAD rows + VJP) in one launch (mrl_mlp_grad_hyb), on the
+        # one-pass Fisher product's shapes; MRL_GRAD_ONEPASS=0: the rows + VJP pair
+        self.grad_onepass = (self.fisher_onepass and self.rows_split
+                             and os.environ.get("MRL_GRAD_ONEPASS", "1") != "0")
         self.image_s = None
         if self.fisher_split:
             w = int(self.lib.mrl_mlp_image_words_split(ctypes.byref(self.desc)))
@@ -294,6 +298,29 @@ class MlpNet:
         call("mrl_mlp_fisher_hyb", ctypes.byref(self.desc), ptr(self.theta), ptr(self.image), ptr(self.image_s),
              ptr(tangent), ptr(image_t), ctypes.byref(io), ptr(slab), ptr(skip), stream())
         call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), ptr(skip), stream())
+        return True
+
+    def grad_onepass_applies(self, ep_t=None):
+        return bool(self.grad_onepass and self.use_cache and ep_t is None)
+
+    def policy_gradient(self, x, n, inv_n_global, act, adv, oldprob, out, sums):
+        """out[P] <- the surrogate's gradient and sums[4] <- (surr, kl, ent, 0) summed over
+        the n rows in ONE launch (mrl_mlp_grad_hyb: the SURRGRAD rows of
+        mrl_mlp_rows_split and the hybrid VJP side by side in each block, the head-gradient
+        rows through LDS), recording the activation cache as the rows pass does.  False:
+        not applicable (the caller runs rows(EPI_SURRGRAD) + vjp_flat)."""
+        if not self.grad_onepass_applies():
+            return False
+        rows = int(self.lib.mrl_mlp_slab_rows(ctypes.byref(self.desc), int(n)))
+        slab = self.ws.get("slab", rows * self.P, torch.float32)
+        partial = self.ws.get("grad_partial", rows * 4, torch.float64)  # one row per producer wave
+        self._cache_key = self._key(x, n, None, 1.0)
+        io = _lib.RowsIO(ptr(x), None, 1.0, int(n), float(inv_n_global), ptr(act), ptr(adv), ptr(oldprob), None,
+                         None, None, ptr(partial), 0.0, 0.0, 0.0, 0, _lib.CACHE_WRITE, ptr(self._cache(n)), None)
+        call("mrl_mlp_grad_hyb", ctypes.byref(self.desc), ptr(self.theta), ptr(self.image), ptr(self.image_s),
+             ctypes.byref(io), ptr(slab), None, stream())
+        call("mrl_reduce_rows_f32", ptr(slab), rows, self.P, ptr(out), None, stream())
+        call("mrl_reduce_rows_f64", ptr(partial), rows, 4, ptr(sums), None, stream())
         return True
 
     def reduce_partial(self, partial, n, out):

@@ -79,6 +79,12 @@ class HipTrpoOps:
 
     def surrgrad(self):
         b, net = self.batch, self.net
+        if getattr(net, "grad_onepass", False):
+            timing.start("pg_onepass", detail=True)
+            done = net.policy_gradient(b.obs, b.n, self.inv_ng, b.act, b.adv, b.prob, self.g, self.sums)
+            timing.stop("pg_onepass")
+            if done:
+                return self.g, self.sums
         net.rows(_lib.EPI_SURRGRAD, b.obs, b.n, inv_n_global=self.inv_ng, act=b.act, adv=b.adv, oldprob=b.prob,
                  ghead=self.ghead, partial=self.partial)
         net.reduce_partial(self.partial, b.n, self.sums)

@@ -77,18 +77,23 @@ def _net(b):
 def test_fullsize_gradient_and_fisher_product(batch, fisher, monkeypatch):
     """g and one Fisher product F v over all 4,194,304 rows, each within 1e-4 (max error
     relative to the vector's max) of the float64 oracle; every fp32 Fisher path (the
-    default one-pass kernel, the split JVP rows + hybrid VJP pair, the exact-f32 pair)."""
+    default one-pass kernel, the split JVP rows + hybrid VJP pair, the exact-f32 pair); the
+    one-pass case takes g from the one-launch policy gradient too."""
     monkeypatch.setenv("MRL_FISHER", "f32" if fisher == "f32" else "split")
     from modular_rl_amd import _lib
     b, spec = batch, batch["spec"]
     net = _net(b)
     assert net.fisher_split == (fisher != "f32")
-    gh = torch.zeros(N * net.gh, device="cuda")
-    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
-    net.rows(_lib.EPI_SURRGRAD, b["x"], N, inv_n_global=1.0 / N, act=b["a"], adv=b["advd"], oldprob=b["oldprobd"],
-             ghead=gh, partial=partial)
     g = torch.zeros(net.P, device="cuda")
-    net.vjp_flat(b["x"], N, gh, g)
+    if fisher == "onepass":  # the one-launch policy gradient (mrl_mlp_grad_hyb) records the cache
+        assert net.policy_gradient(b["x"], N, 1.0 / N, b["a"], b["advd"], b["oldprobd"], g,
+                                   torch.zeros(4, dtype=torch.float64, device="cuda"))
+    else:
+        gh = torch.zeros(N * net.gh, device="cuda")
+        partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+        net.rows(_lib.EPI_SURRGRAD, b["x"], N, inv_n_global=1.0 / N, act=b["a"], adv=b["advd"],
+                 oldprob=b["oldprobd"], ghead=gh, partial=partial)
+        net.vjp_flat(b["x"], N, gh, g)
     t0 = time.time()
     g_want = b["crows"].pg(spec, b["th"])
     assert _rel(g.cpu().numpy().astype(np.float64), g_want) < 1e-4
@@ -117,8 +122,9 @@ def test_fullsize_trpo_update_matches_float64_oracle(batch, onepass, monkeypatch
     """One whole TrpoUpdater.update at 4,194,304 rows (the bench's cg_damping 0.1,
     max_kl 0.01): accepted backtrack k exactly; lm, shs, the expected improve rate and
     the six loss stats within 1e-4 relative; theta within 1e-4 of the step -- with the
-    one-pass Fisher product (default) and with the two-kernel pair."""
+    one-pass Fisher product and policy gradient (default) and with the two-kernel pairs."""
     monkeypatch.setenv("MRL_FISHER_ONEPASS", onepass)
+    monkeypatch.setenv("MRL_GRAD_ONEPASS", onepass)
     from modular_rl_amd.collector import Batch
     from modular_rl_amd.core import StochPolicyMLP
     from modular_rl_amd.trpo import TrpoUpdater
@@ -131,7 +137,7 @@ def test_fullsize_trpo_update_matches_float64_oracle(batch, onepass, monkeypatch
     print(f"[fullsize] oracle update in {time.time() - t0:.1f} s (k={diag_w['k']}, cg iters {diag_w['cg_iters']})",
           flush=True)
     pol = StochPolicyMLP(_net(b), b["pt"])
-    assert pol.net.fisher_onepass == (onepass == "1")
+    assert pol.net.fisher_onepass == pol.net.grad_onepass == (onepass == "1")
     up = TrpoUpdater(pol, dict(cg_damping=0.1, max_kl=0.01))
     bt = Batch(N, b["x"], b["a"], b["oldprobd"])
     bt.adv = b["advd"]
@@ -146,6 +152,25 @@ def test_fullsize_trpo_update_matches_float64_oracle(batch, onepass, monkeypatch
     assert np.abs(th1 - th_w).max() <= 1e-4 * step, np.abs(th1 - th_w).max() / step
     for k in stats_w:
         np.testing.assert_allclose(stats[k], stats_w[k], rtol=1e-4, atol=1e-7, err_msg=k)
+
+
+def test_fullsize_onepass_policy_gradient_is_deterministic(batch):
+    """The one-launch policy gradient (mrl_mlp_grad_hyb) repeated on the 4,194,304 rows:
+    g, the loss sums and the activation cache it records, the same bits every time."""
+    b = batch
+    net = _net(b)
+    assert net.grad_onepass
+    outs = []
+    for _ in range(3):
+        g = torch.zeros(net.P, device="cuda")
+        s = torch.zeros(4, dtype=torch.float64, device="cuda")
+        assert net.policy_gradient(b["x"], N, 1.0 / N, b["a"], b["advd"], b["oldprobd"], g, s)
+        outs.append((g, s))
+        if len(outs) == 1:
+            cache0 = net._cache(N).clone()
+    assert torch.equal(net._cache(N), cache0)
+    for g, s in outs[1:]:
+        assert torch.equal(g, outs[0][0]) and torch.equal(s, outs[0][1])
 
 
 @pytest.mark.parametrize("path", ["onepass", "split", "f32", "bf16"])

@@ -245,6 +245,84 @@ def test_onepass_fisher_product(head, nin, nout, N, cus, monkeypatch):
     assert _rel(one, want) < 1e-4
 
 
+@pytest.mark.parametrize("head,nin,nout", [("gauss", 11, 3), ("softmax", 4, 2)])  # the static shapes
+@pytest.mark.parametrize("N", [1, 33, 3001, 70001])
+@pytest.mark.parametrize("cus", [0, 48])
+def test_onepass_policy_gradient(head, nin, nout, N, cus, monkeypatch):
+    """mrl_mlp_grad_hyb (the SURRGRAD rows of mrl_mlp_rows_split and the hybrid VJP side
+    by side in one launch, the head-gradient rows through LDS, trpo.py:42-43) against the
+    two-kernel pair: the activation cache it records bit for bit (the same per-row code),
+    g to f32 rounding (the same head rows, summed over another row partition), the
+    surr / KL / entropy sums to 1e-12; against the float64 oracle at 1e-4; bit-identical
+    run to run; the Fisher product that reads its cache equals the one after the pair's."""
+    monkeypatch.setenv("MRL_FISHER", "split")
+    from modular_rl_amd import _lib
+    from modular_rl_amd.nets import MlpNet
+    rng = np.random.default_rng(nin * 17 + N)
+    spec = T.Spec(nin, [64, 64], nout, head)
+    th = T.mlp_init(rng, spec.shapes, head == "gauss") + 0.05 * rng.standard_normal(spec.P)
+    if head == "gauss":
+        th[-nout:] = 0.3 * rng.standard_normal(nout)
+    th = th.astype(np.float32).astype(np.float64)
+    ob = rng.standard_normal((N, nin)).astype(np.float32).astype(np.float64)
+    oldprob = T.policy_prob(spec, th + 0.01 * rng.standard_normal(spec.P), ob).astype(np.float32).astype(np.float64)
+    act = T.sample(spec, oldprob, rng.standard_normal((N, nout)) if head == "gauss" else rng.random(N))
+    if head == "gauss":
+        act = act.astype(np.float32).astype(np.float64)
+    adv = rng.standard_normal(N).astype(np.float32).astype(np.float64)
+    v = (0.1 * rng.standard_normal(spec.P)).astype(np.float32)
+    monkeypatch.setenv("MRL_GRAD_ONEPASS", "1")
+    net = MlpNet(nin, nout, _lib.HEAD_GAUSS if head == "gauss" else _lib.HEAD_SOFTMAX)
+    assert net.grad_onepass
+    net.set_flat(th)
+    if cus:
+        net.size_for_cus(cus)
+    x, vt, advd, opd = _dev(ob), _dev(v), _dev(adv), _dev(oldprob)
+    a = _dev(act, torch.int32 if head == "softmax" else torch.float32)
+    ncache = ((N + 31) // 32) * 64 * 64
+    imgs = net.new_tangent_image()
+    net.pack_tangent(vt, imgs)
+
+    def fisher():
+        f = torch.zeros(net.P, device="cuda")
+        assert net.fisher_product(x, N, 1.0 / N, vt, imgs, f)
+        return f.cpu().numpy().astype(np.float64)
+
+    # the two-kernel pair
+    net._cache(N).fill_(float("nan"))
+    partial = torch.zeros(net.partial_rows(N) * 4, dtype=torch.float64, device="cuda")
+    gh = torch.full((N * net.gh,), float("nan"), device="cuda")
+    net.rows(_lib.EPI_SURRGRAD, x, N, inv_n_global=1.0 / N, act=a, adv=advd, oldprob=opd, ghead=gh, partial=partial)
+    s2 = torch.zeros(4, dtype=torch.float64, device="cuda")
+    net.reduce_partial(partial, N, s2)
+    c2 = net._cache(N)[:ncache].clone()
+    g2 = torch.zeros(net.P, device="cuda")
+    net.vjp_flat(x, N, gh, g2)
+    f2 = fisher()
+    # the one launch, three times
+    runs = []
+    for _ in range(3):
+        net._cache(N).fill_(float("nan"))
+        g1 = torch.full((net.P,), float("nan"), device="cuda")
+        s1 = torch.full((4,), float("nan"), dtype=torch.float64, device="cuda")
+        assert net.policy_gradient(x, N, 1.0 / N, a, advd, opd, g1, s1)
+        runs.append((g1, s1, net._cache(N)[:ncache].clone()))
+    f1 = fisher()
+    torch.cuda.synchronize()
+    for g1, s1, c1 in runs[1:]:
+        assert torch.equal(g1, runs[0][0]) and torch.equal(s1, runs[0][1]) and torch.equal(c1, runs[0][2])
+    g1, s1, c1 = (t.cpu().numpy().astype(np.float64) for t in runs[0])
+    assert np.array_equal(c1, c2.cpu().numpy().astype(np.float64), equal_nan=True)
+    assert np.isfinite(g1).all()
+    assert _rel(g1, g2.cpu().numpy().astype(np.float64)) < 1e-5
+    np.testing.assert_allclose(s1[:3], s2.cpu().numpy()[:3], rtol=1e-12, atol=1e-12 * np.abs(s1[:3]).max())
+    assert s1[3] == 0.0
+    np.testing.assert_array_equal(f1, f2)
+    want = T.surr_kl_ent(spec, th, ob, act, adv, oldprob)
+    np.testing.assert_allclose(np.array([-s1[0] / N, s1[1] / N, s1[2] / N]), want, rtol=1e-4, atol=1e-6)
+    assert _rel(g1, T.policy_gradient(spec, th, ob, act, adv, oldprob)) < 1e-4
+
+
 def _rows_pair(monkeypatch, head, nin, nout, th, build):
     """build(net) on a split-forward net and on an exact-f32 one (MRL_ROWS_SPLIT=0)."""
     from modular_rl_amd import _lib
