@@ -239,10 +239,25 @@ __device__ inline void tanh4r(f32x4& a) {
 // BF (MRL_COMPUTE_BF16): x, h1, h2 rounded to bf16 (W0, W1 are rounded in the image),
 // the operands mlp_rows_bf16 multiplies -- the products and sums stay f32, so the prob
 // rows equal the update's bf16 forward up to f32 summation order.
+#ifndef MRL_FWD_WPF  // 1: a k-step's twelve split W1 fragments read from LDS ahead of its MFMAs
+#define MRL_FWD_WPF 1
+#endif
 template <int O, int A, bool BF, class XL>
 __device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane, float* z, int64_t* st = nullptr) {
   constexpr RDims R = RWeights<O, A>::R;
   const int g = lane >> 4;
+  // the split W1 fragments of k-step s, [tile mo][part p]: k-step 0's issued before layer 0,
+  // k-step 1's once k-step 0's MFMAs are issued -- each lands under other work instead of
+  // an LDS round trip in front of every MFMA group (the persistent kernel's registers are
+  // held by the fp64 dynamics, not here)
+  bf16x8 wf[4][3];
+  auto load_wf = [&](int s) {
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) wf[mo][p] = w.w1s[(p * 8 + mo * 2 + s) * 64 + lane];
+  };
+  if (MRL_FWD_WPF) load_wf(0);
   float xb[R.KS0p];
 #pragma unroll
   for (int ks = 0; ks < R.KS0p; ++ks) xb[ks] = ks < R.KS0 ? (BF ? bf16r(xl(4 * ks + g)) : xl(4 * ks + g)) : 0.f;
@@ -276,10 +291,16 @@ __device__ inline void forward16(const RWeights<O, A>& w, const XL& xl, int lane
       hp[1][r] = c[0]; hp[1][r + 1] = c[1]; hp[1][4 + r] = c2[0]; hp[1][4 + r + 1] = c2[1];
       hp[2][r] = e[0]; hp[2][r + 1] = e[1]; hp[2][4 + r] = e2[0]; hp[2][4 + r + 1] = e2[1];
     }
+    bf16x8 wc[4][3];
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        wc[mo][p] = MRL_FWD_WPF ? wf[mo][p] : w.w1s[(p * 8 + mo * 2 + s) * 64 + lane];
+    if (MRL_FWD_WPF && s == 0) load_wf(1);
 #pragma unroll
     for (int mo = 0; mo < 4; ++mo) {
-      const bf16x8 w0 = w.w1s[(0 * 8 + mo * 2 + s) * 64 + lane], w1 = w.w1s[(1 * 8 + mo * 2 + s) * 64 + lane];
-      const bf16x8 w2 = w.w1s[(2 * 8 + mo * 2 + s) * 64 + lane];
+      const bf16x8 w0 = wc[mo][0], w1 = wc[mo][1], w2 = wc[mo][2];
       h2[mo] = MFMAB16(w2, hp[0], h2[mo]);  // smallest products first
       h2[mo] = MFMAB16(w0, hp[2], h2[mo]);
       h2[mo] = MFMAB16(w1, hp[1], h2[mo]);
