@@ -527,6 +527,43 @@ __device__ inline void batch_of_records(const double* rec, int nb, int RS, int D
 }
 
 // Chan merge of (nb, mb, m2b) into (n, M, S); for nb == 1 this is RunningStat.push
+// the filtered observation columns 4i + g of one env row (core.py:191-192: clip((o - mean)
+// / (std + 1e-8), -5, 5)), as f32.  Every column's statistics are read from LDS before any
+// arithmetic and the stores are left to the caller, so the (O + 3) / 4 divisions are
+// independent chains rather than one LDS round trip + division per branchy store block
+// (the same operations per value)
+template <int ENV>
+__device__ inline void filtered_obs(const double* s, int g, bool filter, const double* fmean, const double* fden,
+                                    float* vf) {
+  constexpr int O = EnvC<ENV>::OBS, NI = (O + 3) / 4;
+  double o[O];
+  EnvC<ENV>::obs(s, o);
+  double v[NI], mu[NI], den[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    v[i] = o[4 * i];
+#pragma unroll
+    for (int q = 1; q < 4; ++q)
+      if (4 * i + q < O && g == q) v[i] = o[4 * i + q < O ? 4 * i + q : O - 1];
+  }
+  if (filter) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int kc = 4 * i + g, kk = kc < O ? kc : O - 1;
+      mu[i] = fmean[kk];
+      den[i] = fden[kk];
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      double x = v[i] - mu[i];
+      x = x / den[i];
+      v[i] = x < -5.0 ? -5.0 : (x > 5.0 ? 5.0 : x);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i) vf[i] = (float)v[i];
+}
+
 __device__ inline void chan_merge(double& n, double& M, double& S, double nb, double mb, double m2b) {
   if (nb <= 0.0) return;
   const double na = n;
@@ -801,25 +838,14 @@ __global__ __launch_bounds__(RB) void rollout_step_kernel(RollArgs a, const floa
 
   // 3. filtered observation (core.py:191-192); row g takes columns 4i + g
   {
-    double o[O];
-    EC::obs(s, o);
+    float vf[(O + 3) / 4];
+    filtered_obs<ENV>(s, g, a.d.filter != 0, fmean, fden, vf);
 #pragma unroll
     for (int i = 0; i < (O + 3) / 4; ++i) {
       const int kc = 4 * i + g;
-      double v = o[4 * i];
-#pragma unroll
-      for (int q = 1; q < 4; ++q)
-        if (4 * i + q < O && g == q) v = o[4 * i + q < O ? 4 * i + q : O - 1];
-      if (a.d.filter) {
-        const int kk = kc < O ? kc : O - 1;
-        v = v - fmean[kk];
-        v = v / fden[kk];
-        v = v < -5.0 ? -5.0 : (v > 5.0 ? 5.0 : v);
-      }
-      const float vf = (float)v;
       if (kc < O) {
-        if (valid) a.b.obs[row * O + kc] = vf;
-        xt[wave][j][kc] = vf;
+        if (valid) a.b.obs[row * O + kc] = vf[i];
+        xt[wave][j][kc] = vf[i];
       }
     }
   }
@@ -1109,25 +1135,14 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
     PSTAMP(t, 1);
     // filtered observation (core.py:191-192); row g takes columns 4i + g
     {
-      double o[O];
-      EC::obs(s, o);
+      float vf[(O + 3) / 4];
+      filtered_obs<ENV>(s, g, a.d.filter != 0, fmean, fden, vf);
 #pragma unroll
       for (int i = 0; i < (O + 3) / 4; ++i) {
         const int kc = 4 * i + g;
-        double v = o[4 * i];
-#pragma unroll
-        for (int q = 1; q < 4; ++q)
-          if (4 * i + q < O && g == q) v = o[4 * i + q < O ? 4 * i + q : O - 1];
-        if (a.d.filter) {
-          const int kk = kc < O ? kc : O - 1;
-          v = v - fmean[kk];
-          v = v / fden[kk];
-          v = v < -5.0 ? -5.0 : (v > 5.0 ? 5.0 : v);
-        }
-        const float vf = (float)v;
         if (kc < O) {
-          if (valid) a.b.obs[row * O + kc] = vf;
-          xt[wave][j][kc] = vf;
+          if (valid) a.b.obs[row * O + kc] = vf[i];
+          xt[wave][j][kc] = vf[i];
         }
       }
     }
