@@ -428,20 +428,41 @@ __device__ inline double sum16(double v) {
 
 // per-block two-pass (mean, M2) partial of vals[ENVS_PER_BLOCK][D] (doubles in LDS):
 // thread (k = tid/16, j = tid%16) covers envs j, j+16, ...; 16-lane butterflies.
+// column k's (mean, M2) over the block's nvalid envs: lane j adds envs j, j + 16, j + 32,
+// j + 48 in that order, then the 16-lane butterflies.  The four values are read from LDS
+// together and kept for the M2 pass (one LDS round trip instead of eight dependent ones);
+// a term past nvalid is skipped, as the loop over i < nvalid did
+__device__ inline void block_moments(const double* vals, int nvalid, int D, int k, int j, double& mean, double& m2) {
+  constexpr int Q = ENVS_PER_BLOCK / 16;
+  const int kk = k < D ? k : D - 1;
+  double v[Q];
+  bool in[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int i = j + 16 * q;
+    in[q] = k < D && i < nvalid;
+    v[q] = vals[(i < nvalid ? i : 0) * D + kk];
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    if (in[q]) s += v[q];
+  mean = nvalid > 0 ? div_count(sum16(s), (double)nvalid) : 0.0;
+  double m = 0.0;
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    if (in[q]) {
+      const double dv = v[q] - mean;
+      m += dv * dv;
+    }
+  m2 = sum16(m);
+}
+
 __device__ inline void publish_partial(const RollArgs& a, const double* vals, int nvalid, int D, bool with_rew,
                                        double* rec_out) {
   const int k = threadIdx.x >> 4, j = threadIdx.x & 15;
-  double s = 0.0;
-  if (k < D)
-    for (int i = j; i < nvalid; i += 16) s += vals[i * D + k];
-  const double mean = nvalid > 0 ? div_count(sum16(s), (double)nvalid) : 0.0;
-  double m2 = 0.0;
-  if (k < D)
-    for (int i = j; i < nvalid; i += 16) {
-      const double dv = vals[i * D + k] - mean;
-      m2 += dv * dv;
-    }
-  m2 = sum16(m2);
+  double mean, m2;
+  block_moments(vals, nvalid, D, k, j, mean, m2);
   if (k < D && j == 0) {
     double* r = rec_out + (int64_t)blockIdx.x * a.RS;
     r[2 + k] = mean;
@@ -941,17 +962,8 @@ __device__ inline bool g_tag_is(gran_t g, int step) { return (g.w >> 31) == step
 // the granules of gather step `step`; lane 0 of column group k writes column k's
 __device__ inline void publish_granules(const Granules& gr, const double* vals, int nvalid, int step) {
   const int k = threadIdx.x >> 4, j = threadIdx.x & 15;
-  double s = 0.0;
-  if (k < gr.D)
-    for (int i = j; i < nvalid; i += 16) s += vals[i * gr.D + k];
-  const double mean = nvalid > 0 ? div_count(sum16(s), (double)nvalid) : 0.0;
-  double m2 = 0.0;
-  if (k < gr.D)
-    for (int i = j; i < nvalid; i += 16) {
-      const double dv = vals[i * gr.D + k] - mean;
-      m2 += dv * dv;
-    }
-  m2 = sum16(m2);
+  double mean, m2;
+  block_moments(vals, nvalid, gr.D, k, j, mean, m2);
   if (k < gr.D && j == 0) gr.put(step, k, blockIdx.x, mean, m2);
 }
 
