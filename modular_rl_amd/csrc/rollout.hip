@@ -36,14 +36,19 @@ constexpr int MAXD = 16;  // obs dims + 1 (reward)
 // the SAME 16 envs: row g evaluates sincos of segment angle g and the contacts of
 // capsule g, and the rows exchange the results, so every row continues with the
 // identical state.  All lanes must be active.
-#ifndef MRL_HP_CAP_LDS  // 0: the capsule constants by per-substep selects (A/B build)
-#define MRL_HP_CAP_LDS 1
+// the persistent kernel's capsule constants: 2 -- the row's own six, read from the LDS
+// table once per launch and held in registers; 1 -- read from the LDS table every substep;
+// 0 -- per-substep selects (A/B builds)
+#ifndef MRL_HP_CAP_LDS
+#define MRL_HP_CAP_LDS 2
 #endif
 struct HopperQuad {
   int g;
-  const double* capc;  // HP_CAP in LDS ([field][k]; the persistent kernel), or null
+  const double* capc;  // mode 2: the row's capsule {rad, mu, u0, u1, w0, w1}; mode 1: HP_CAP
+                       // in LDS ([field][k]); or null
   __device__ CapsuleC capsule(int) const {
-    if (MRL_HP_CAP_LDS && capc != nullptr)
+    if (MRL_HP_CAP_LDS == 2 && capc != nullptr) return CapsuleC{capc[0], capc[1], capc[2], capc[3], capc[4], capc[5]};
+    if (MRL_HP_CAP_LDS == 1 && capc != nullptr)
       return CapsuleC{capc[g], capc[4 + g], capc[8 + g], capc[12 + g], capc[16 + g], capc[20 + g]};
     return capsule_const(g);
   }
@@ -1090,6 +1095,9 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
   }
   __syncthreads();
   publish_granules(gr, vals, nvalid, 0);  // gather step 0's partials
+  double capr[6];  // row g's capsule constants (MRL_HP_CAP_LDS 2)
+#pragma unroll
+  for (int f = 0; f < 6; ++f) capr[f] = hp_cap[4 * f + g];
 
   for (int t = 0; t < T; ++t) {
     const int64_t row = (int64_t)t * E + e;
@@ -1171,7 +1179,8 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
     // sample + env step on every row (split angle functions); row 0 stores
     double rew = 0.0;
     bool done = false;
-    sample_and_step<ENV, true>(a, row, z, lsd, zn, s, rew, done, valid && g == 0, g, hp_cap);
+    sample_and_step<ENV, true>(a, row, z, lsd, zn, s, rew, done, valid && g == 0, g,
+                               MRL_HP_CAP_LDS == 2 ? capr : hp_cap);
     PSTAMP(t, 4);
     // episode bookkeeping on every row, so the rows keep identical env state
     // (finish_env_step: gym TimeLimit => terminated; limit / horizon cut => not)
