@@ -166,10 +166,12 @@ __device__ inline void hopper_contacts(const CapsuleC& cc, double pz, double pvx
 // every lane evaluates the whole env (layered rollout)
 struct HopperSerial {
   __device__ CapsuleC capsule(int k) const { return capsule_const(k); }
-  __device__ void sincos4(const double* phi, double* s, double* c) const {
+  __device__ void sincos4(const double* phi, double* s, double* c, double&, double&) const {
 #pragma unroll
     for (int k = 0; k < 4; ++k) sincos(phi[k], &s[k], &c[k]);
   }
+  // segment k's value of a per-segment array (k a compile-time index here)
+  __device__ double own(int k, const double* a4, double) const { return a4[k]; }
   template <class F>
   __device__ void contacts(F f, double (*ct)[3]) const {
 #pragma unroll
@@ -226,7 +228,8 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
     cg[k] = 1.0 - phi[k] * phi[k] * 0.5;
   }
 #else
-  par.sincos4(phi, sg, cg);
+  double s_own = 0.0, c_own = 0.0;  // HopperQuad: the row's own segment's sin / cos
+  par.sincos4(phi, sg, cg, s_own, c_own);
 #endif
   om[0] = v[2];
 #pragma unroll
@@ -271,7 +274,7 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
       [&](int k, double* out) {
         hopper_contacts(par.capsule(k), sel4(k, pz[0], pz[1], pz[2], pz[3]), sel4(k, pvx[0], pvx[1], pvx[2], pvx[3]),
                         sel4(k, pvz[0], pvz[1], pvz[2], pvz[3]), sel4(k, om[0], om[1], om[2], om[3]),
-                        sel4(k, sg[0], sg[1], sg[2], sg[3]), sel4(k, cg[0], cg[1], cg[2], cg[3]), out);
+                        par.own(k, sg, s_own), par.own(k, cg, c_own), out);
       },
       ct);
   // per body: inertial + gravity force minus contact force, moment about its pivot
@@ -386,7 +389,10 @@ __device__ inline void hopper_step(double* s, const float* a, double& rew, bool&
   for (int k = 0; k < HP_FRAME_SKIP; ++k) hopper_substep(q, v, tau, par);
   rew = (q[0] - x_before) / (HP_DT * HP_FRAME_SKIP) + 1.0 - 1e-3 * asq;
   bool healthy = true;
-#if MRL_HP_LIM_BITS  // every test evaluated and combined with & (the && chain: nested branches)
+#ifndef MRL_HP_HEALTH_BITS  // 1: the health test's comparisons combined with & (no branches)
+#define MRL_HP_HEALTH_BITS 1
+#endif
+#if MRL_HP_LIM_BITS || MRL_HP_HEALTH_BITS  // every test evaluated and combined with & (the && chain: nested branches)
   for (int i = 0; i < 12; ++i) healthy = healthy & (bool)isfinite(s[i]);
   for (int i = 2; i < 12; ++i) healthy = healthy & (fabs(s[i]) < 100.0);
   healthy = healthy & (q[1] > 0.7) & (fabs(q[2]) < 0.2);

@@ -52,12 +52,17 @@ struct HopperQuad {
       return CapsuleC{capc[g], capc[4 + g], capc[8 + g], capc[12 + g], capc[16 + g], capc[20 + g]};
     return capsule_const(g);
   }
-  __device__ void sincos4(const double* phi, double* s, double* c) const {
+  __device__ void sincos4(const double* phi, double* s, double* c, double& so, double& co) const {
     double sx, cx;
     sincos(sel4(g, phi[0], phi[1], phi[2], phi[3]), &sx, &cx);
     quads(sx, s);
     quads(cx, c);
+    so = sx;
+    co = cx;
   }
+  // segment k == g's value: the row's own (sel4(g, quads(x)) is x, bit for bit), with no
+  // wait for the row exchange and no select
+  __device__ double own(int, const double*, double v) const { return v; }
   template <class F>
   __device__ void contacts(F f, double (*ct)[3]) const {
     double own[3], x[4];
