@@ -96,6 +96,12 @@ __device__ inline double pick_bits(uint32_t m, double x, double y) {  // m ? y :
 #ifndef MRL_HP_LIM_BITS  // 1: joint limits and the health test without branches as well (measured
 #define MRL_HP_LIM_BITS 0  // slower: 14.56 ms, the extra live values spill)
 #endif
+#ifndef MRL_HP_LIM_SEL  // 1: joint limits as selects over both evaluated forms (0: the ternary)
+#define MRL_HP_LIM_SEL 1
+#endif
+#ifndef MRL_HP_HEALTH_BITS  // 1: the health test's comparisons combined with & (no branches)
+#define MRL_HP_HEALTH_BITS 1
+#endif
 __device__ inline double sel4(int k, double a0, double a1, double a2, double a3) {
   if (!MRL_HP_SEL_BITS || __builtin_constant_p(k)) return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
   uint32_t m0 = 0u - (uint32_t)(k & 1), m1 = 0u - (uint32_t)((k >> 1) & 1);
@@ -337,7 +343,14 @@ __device__ inline void hopper_substep(double* q, double* v, const double* tau, c
   for (int i = 1; i < 4; ++i) {
     const int jj = i - 1, j = 2 + i;
     C[i][i] = C[i][i] + HP_ARM;
-#if MRL_HP_LIM_BITS
+#if MRL_HP_LIM_SEL
+    // joint-limit force: both one-sided forms evaluated, the active one picked by a plain
+    // select (v_cndmask) -- the ternary over the fmas was an exec-masked branch pair per
+    // joint, both arms issued by divergent rows
+    const double cv = -(HP_CL * v[j]);
+    const double flo = fmad(HP_KL, HP_LO[jj] - q[j], cv), fhi = fmad(HP_KL, HP_HI[jj] - q[j], cv);
+    const double lim = q[j] < HP_LO[jj] ? flo : (q[j] > HP_HI[jj] ? fhi : 0.0);
+#elif MRL_HP_LIM_BITS
     // joint-limit force: both one-sided forms evaluated, the active one selected by bit
     // masks (divergent rows make the ternary an exec-masked branch pair per joint)
     const double cv = -(HP_CL * v[j]);
@@ -389,9 +402,6 @@ __device__ inline void hopper_step(double* s, const float* a, double& rew, bool&
   for (int k = 0; k < HP_FRAME_SKIP; ++k) hopper_substep(q, v, tau, par);
   rew = (q[0] - x_before) / (HP_DT * HP_FRAME_SKIP) + 1.0 - 1e-3 * asq;
   bool healthy = true;
-#ifndef MRL_HP_HEALTH_BITS  // 1: the health test's comparisons combined with & (no branches)
-#define MRL_HP_HEALTH_BITS 1
-#endif
 #if MRL_HP_LIM_BITS || MRL_HP_HEALTH_BITS  // every test evaluated and combined with & (the && chain: nested branches)
   for (int i = 0; i < 12; ++i) healthy = healthy & (bool)isfinite(s[i]);
   for (int i = 2; i < 12; ++i) healthy = healthy & (fabs(s[i]) < 100.0);

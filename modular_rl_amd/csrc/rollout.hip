@@ -653,7 +653,9 @@ __global__ void noise_fill_kernel(RollArgs a, double* __restrict__ out) {
 // core.py:432-435), write act/prob rows, step the env (fp64)
 // QUAD: the four 16-lane rows of the wave hold this env (fused step kernel); every
 // lane steps it (row h = lane >> 4 of the angle functions), lanes with `store` write
-template <int ENV, bool QUAD = false>
+// SD: `logstd` holds the standard deviations exp(logstd) already (the persistent kernel
+// forms them once per launch: the same expf, not one per step)
+template <int ENV, bool QUAD = false, bool SD = false>
 __device__ inline void sample_and_step(const RollArgs& a, int64_t row, const float* z, const float* logstd,
                                        const double* zn, double* s, double& rew, bool& done, bool store = true,
                                        int h = 0, const double* capc = nullptr) {
@@ -693,7 +695,7 @@ __device__ inline void sample_and_step(const RollArgs& a, int64_t row, const flo
     float av[A];
 #pragma unroll
     for (int q = 0; q < A; ++q) {
-      const float sd = expf(logstd[q]);
+      const float sd = SD ? logstd[q] : expf(logstd[q]);
       av[q] = __fadd_rn(__fmul_rn((float)zn[q], sd), z[q]);
       if (store) {
         reinterpret_cast<float*>(a.b.act)[row * A + q] = av[q];
@@ -1071,9 +1073,12 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
     for (int i = threadIdx.x; i < 3 * 8 * 64; i += RB) w1s_l[i] = reinterpret_cast<const bf16x8*>(rimg + R.bs1)[i];
     wt.w1s = w1s_l;
   }
-  float lsd[A];
+  float lsd[A], sdv[A];
 #pragma unroll
-  for (int q = 0; q < A; ++q) lsd[q] = EC::DISCRETE ? 0.f : logstd[q];
+  for (int q = 0; q < A; ++q) {
+    lsd[q] = EC::DISCRETE ? 0.f : logstd[q];
+    sdv[q] = expf(lsd[q]);
+  }
   // the running stat at the start of the iteration (every block keeps the same copy)
   double fn = 0.0, fM = 0.0, fS = 0.0;
   if (kcol) {
@@ -1184,8 +1189,8 @@ __global__ __launch_bounds__(RB) void rollout_persistent_kernel(RollArgs a, cons
     // sample + env step on every row (split angle functions); row 0 stores
     double rew = 0.0;
     bool done = false;
-    sample_and_step<ENV, true>(a, row, z, lsd, zn, s, rew, done, valid && g == 0, g,
-                               MRL_HP_CAP_LDS == 2 ? capr : hp_cap);
+    sample_and_step<ENV, true, true>(a, row, z, sdv, zn, s, rew, done, valid && g == 0, g,
+                                     MRL_HP_CAP_LDS == 2 ? capr : hp_cap);
     PSTAMP(t, 4);
     // episode bookkeeping on every row, so the rows keep identical env state
     // (finish_env_step: gym TimeLimit => terminated; limit / horizon cut => not)
