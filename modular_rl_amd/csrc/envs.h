@@ -90,8 +90,8 @@ __device__ inline double pick_bits(uint32_t m, double x, double y) {  // m ? y :
   const uint32_t hi = ((uint32_t)(yb >> 32) & m) | ((uint32_t)(xb >> 32) & ~m);
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
-#ifndef MRL_HP_SEL_BITS  // 0: the plain ternary chain (A/B: r04x rollout 13.87 ms with, 14.05 without)
-#define MRL_HP_SEL_BITS 1
+#ifndef MRL_HP_SEL_BITS  // 0: the plain ternary chain (A/B: r04x rollout 13.87 ms with, 14.05 without);
+#define MRL_HP_SEL_BITS 2  // 1: bit masks made opaque per call; 2: selects on k's bits
 #endif
 #ifndef MRL_HP_LIM_BITS  // 1: joint limits and the health test without branches as well (measured
 #define MRL_HP_LIM_BITS 0  // slower: 14.56 ms, the extra live values spill)
@@ -104,6 +104,11 @@ __device__ inline double pick_bits(uint32_t m, double x, double y) {  // m ? y :
 #endif
 __device__ inline double sel4(int k, double a0, double a1, double a2, double a3) {
   if (!MRL_HP_SEL_BITS || __builtin_constant_p(k)) return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
+  if (MRL_HP_SEL_BITS == 2) {  // selects on k's two bits (v_cndmask on loop-invariant lane masks)
+    const bool b0 = (k & 1) != 0, b1 = (k & 2) != 0;
+    const double lo = b0 ? a1 : a0, hi = b0 ? a3 : a2;
+    return b1 ? hi : lo;
+  }
   uint32_t m0 = 0u - (uint32_t)(k & 1), m1 = 0u - (uint32_t)((k >> 1) & 1);
   asm volatile("" : "+v"(m0), "+v"(m1));
   return pick_bits(m1, pick_bits(m0, a0, a1), pick_bits(m0, a2, a3));
