@@ -14,6 +14,8 @@ import os
 
 # role -> kernel-name substring (first match wins, most specific first)
 ROLES = [
+    ("pg_onepass", "mlp_fisher_hyb_kernel<1, 1>"),  # the one-launch policy gradient (round 6)
+    ("pg_onepass", "mlp_fisher_hyb_kernel<2, 1>"),
     ("fvp_onepass", "mlp_fisher_hyb_kernel"),        # the one-pass Fisher product (round 5)
     ("fvp_jvp_rows_split", "mlp_fvp_split_kernel"),
     ("fvp_jvp_rows", "mlp_rows_kernel<100"),
