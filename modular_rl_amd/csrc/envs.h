@@ -408,9 +408,21 @@ __device__ inline void hopper_step(double* s, const float* a, double& rew, bool&
   rew = (q[0] - x_before) / (HP_DT * HP_FRAME_SKIP) + 1.0 - 1e-3 * asq;
   bool healthy = true;
 #if MRL_HP_LIM_BITS || MRL_HP_HEALTH_BITS  // every test evaluated and combined with & (the && chain: nested branches)
-  for (int i = 0; i < 12; ++i) healthy = healthy & (bool)isfinite(s[i]);
-  for (int i = 2; i < 12; ++i) healthy = healthy & (fabs(s[i]) < 100.0);
-  healthy = healthy & (q[1] > 0.7) & (fabs(q[2]) < 0.2);
+  // |s_i| < 100 is false for a NaN or an infinity, so isfinite(s_i) adds nothing for
+  // i >= 2: the same truth value from 14 comparisons instead of 24, combined as a
+  // balanced tree (depth 4) instead of a chain
+  bool t[14];
+  t[0] = isfinite(s[0]);
+  t[1] = isfinite(s[1]);
+#pragma unroll
+  for (int i = 2; i < 12; ++i) t[i] = fabs(s[i]) < 100.0;
+  t[12] = q[1] > 0.7;
+  t[13] = fabs(q[2]) < 0.2;
+#pragma unroll
+  for (int w = 1; w < 14; w *= 2)
+#pragma unroll
+    for (int i = 0; i + w < 14; i += 2 * w) t[i] = t[i] & t[i + w];
+  healthy = t[0];
 #else
   for (int i = 0; i < 12; ++i) healthy = healthy && isfinite(s[i]);
   for (int i = 2; i < 12; ++i) healthy = healthy && (fabs(s[i]) < 100.0);
