@@ -169,8 +169,8 @@ constexpr bool topo_fits() {
   }
   for (int k = 0; k < NV; ++k)
     if (LDL_START[k + 1] - LDL_START[k] > 128) return false;
-  for (int lv = 0; lv < NLEVEL; ++lv)
-    if (LEVEL_START[lv + 1] - LEVEL_START[lv] > 64) return false;
+  for (int lv = 0; lv < NLEVEL; ++lv)  // the subtree sums take four parents of a level per wave
+    if (LEVEL_START[lv + 1] - LEVEL_START[lv] > 4) return false;
   return NV <= 32 && NB <= 32 && NSPH <= 64 && NACT <= 64 && NHINGE <= 32 && n_entries() <= N_ENT;
 }
 static_assert(topo_fits(), "humanoid tree exceeds the wave layout");
@@ -468,44 +468,61 @@ HM_INLINE void forward(Wave& W, const Shared& S, int lane, int64_t* st = nullptr
   }
   WAVE_SYNC();
   HM_STAMP(3);
-  // cvel and cdof_dot (MuJoCo mj_comVel order): body `lane` accumulates its path
-  if (lane < NB) {
-    double cv[6];
+  // cvel and cdof_dot (MuJoCo mj_comVel order).  The velocity walk down body b's path is
+  // element-wise (cv += cdof qd), so one lane per (body b, element pair ep) carries two of
+  // its six elements; the walk leaves the velocity in front of each of the body's own
+  // hinges in scratch (W.L, free until the mass matrix), and then one lane per (body,
+  // own hinge) forms that hinge's cdof_dot = cv x cdof -- the same operations per element
+  // as a body-per-lane walk that crosses every dof of its path and keeps its own
+  {
+    double* const X = &W.L[0][0];  // [NB][3][6] cv in front of own hinge c; [234..240) cv after the root's translation
+    const int b = lane & 15, ep = lane >> 4;
+    if (b < NB && ep < 3) {
+      double cv[2];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) cv[i] = 0.0 + ((W.cdof[0][i] * qd[0] + W.cdof[1][i] * qd[1]) + W.cdof[2][i] * qd[2]);
-    if (lane == 0) {
-#pragma unroll
-      for (int i = 0; i < 6; ++i) W.cdof_dot[0][i] = W.cdof_dot[1][i] = W.cdof_dot[2][i] = 0.0;
-#pragma unroll
-      for (int k = 3; k < 6; ++k) cross_motion(cv, W.cdof[k], W.cdof_dot[k]);
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) cv[i] = cv[i] + ((W.cdof[3][i] * qd[3] + W.cdof[4][i] * qd[4]) + W.cdof[5][i] * qd[5]);
-    const uint32_t p0 = S.w[W_PATH][lane], p1 = S.w[W_PATH + 1][lane];
-#pragma unroll
-    for (int s = 0; s < PATH_LEN; ++s) {
-      const int a = path_body(p0, p1, s);
-      const int ac = a == (int)NONE ? 0 : a;
-      const int h0 = S.hinge0[ac], nh = a == (int)NONE ? 0 : S.nhinge[ac];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const bool has = c < nh;
-        const int d = 6 + (has ? h0 + c : 0);
-        double cd[6], cdd[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) cd[i] = W.cdof[d][i];
-        const double qdd = qd[d];
-        cross_motion(cv, cd, cdd);
-        if (has && a == lane) {
-#pragma unroll
-          for (int i = 0; i < 6; ++i) W.cdof_dot[d][i] = cdd[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) cv[i] = has ? cv[i] + cd[i] * qdd : cv[i];
+      for (int i = 0; i < 2; ++i) {
+        const int e = 2 * ep + i;
+        cv[i] = 0.0 + ((W.cdof[0][e] * qd[0] + W.cdof[1][e] * qd[1]) + W.cdof[2][e] * qd[2]);
+        if (b == 0) X[NB * 18 + e] = cv[i];
+        cv[i] = cv[i] + ((W.cdof[3][e] * qd[3] + W.cdof[4][e] * qd[4]) + W.cdof[5][e] * qd[5]);
       }
-    }
+      const uint32_t p0 = S.w[W_PATH][b], p1 = S.w[W_PATH + 1][b];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) W.cvel[lane][i] = cv[i];
+      for (int s = 0; s < PATH_LEN; ++s) {
+        const int a = path_body(p0, p1, s);
+        const int ac = a == (int)NONE ? 0 : a;
+        const int h0 = S.hinge0[ac], nh = a == (int)NONE ? 0 : S.nhinge[ac];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const bool has = c < nh;
+          const int d = 6 + (has ? h0 + c : 0);
+          const double qdd = qd[d];
+          if (has && a == b) {
+            X[(b * 3 + c) * 6 + 2 * ep] = cv[0];
+            X[(b * 3 + c) * 6 + 2 * ep + 1] = cv[1];
+          }
+#pragma unroll
+          for (int i = 0; i < 2; ++i) cv[i] = has ? cv[i] + W.cdof[d][2 * ep + i] * qdd : cv[i];
+        }
+      }
+      W.cvel[b][2 * ep] = cv[0];
+      W.cvel[b][2 * ep + 1] = cv[1];
+    }
+    WAVE_SYNC();
+    // lane (b, c < 3): own hinge c of body b; lanes 48..50: the root's rotational dofs
+    // 3..5 (from the velocity after its translation); lanes 51..53: dofs 0..2 (zero)
+    const int c = lane >> 4;
+    if (c < 3) {
+      if (b < NB && c < (int)S.nhinge[b]) {
+        const int d = 6 + S.hinge0[b] + c;
+        cross_motion(X + (b * 3 + c) * 6, W.cdof[d], W.cdof_dot[d]);
+      }
+    } else if (b < 3) {
+      cross_motion(X + NB * 18, W.cdof[3 + b], W.cdof_dot[3 + b]);
+    } else if (b < 6) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) W.cdof_dot[b - 3][i] = 0.0;
+    }
   }
   WAVE_SYNC();
   HM_STAMP(4);
@@ -568,29 +585,44 @@ HM_INLINE void accelerations(Wave& W, const Shared& S, int lane, int64_t* st = n
   const double* q = W.s;
   const double* qd = W.s + NQ;
   const double* ctrl = W.s + NQ + NV;
-  // cacc along body `lane`'s path, then its bias force (RNEA forward pass)
+  // cacc along body b's path, one lane per (body b, element pair ep): the path walk's
+  // multiply-adds are element-wise, so each lane carries two of the six elements through
+  // the same operation sequence (a third of the body-per-lane walk's instructions); the
+  // pairs meet in W.F (free until the F phase) for the bias force on body lanes
+  {
+    const int b = lane & 15, ep = lane >> 4;
+    if (b < NB && ep < 3) {
+      double ca[2] = {0.0, ep == 2 ? 0.0 + GRAV : 0.0};
+#pragma unroll
+      for (int k = 3; k < 6; ++k)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) ca[i] = ca[i] + W.cdof_dot[k][2 * ep + i] * qd[k];
+      const uint32_t p0 = S.w[W_PATH][b], p1 = S.w[W_PATH + 1][b];
+#pragma unroll
+      for (int s = 0; s < PATH_LEN; ++s) {
+        const int a = path_body(p0, p1, s);
+        const int ac = a == (int)NONE ? 0 : a;
+        const int h0 = S.hinge0[ac], nh = a == (int)NONE ? 0 : S.nhinge[ac];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const bool has = c < nh;
+          const int d = 6 + (has ? h0 + c : 0);
+          const double qdd = qd[d];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) ca[i] = has ? ca[i] + W.cdof_dot[d][2 * ep + i] * qdd : ca[i];
+        }
+      }
+      W.F[b][2 * ep] = ca[0];
+      W.F[b][2 * ep + 1] = ca[1];
+    }
+  }
+  WAVE_SYNC();
+  // the bias force of body `lane` (RNEA forward pass)
   if (lane < NB) {
     const int b = lane;
-    double ca[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0 + GRAV};
+    double ca[6];
 #pragma unroll
-    for (int k = 3; k < 6; ++k)
-#pragma unroll
-      for (int i = 0; i < 6; ++i) ca[i] = ca[i] + W.cdof_dot[k][i] * qd[k];
-    const uint32_t p0 = S.w[W_PATH][lane], p1 = S.w[W_PATH + 1][lane];
-#pragma unroll
-    for (int s = 0; s < PATH_LEN; ++s) {
-      const int a = path_body(p0, p1, s);
-      const int ac = a == (int)NONE ? 0 : a;
-      const int h0 = S.hinge0[ac], nh = a == (int)NONE ? 0 : S.nhinge[ac];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const bool has = c < nh;
-        const int d = 6 + (has ? h0 + c : 0);
-        const double qdd = qd[d];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) ca[i] = has ? ca[i] + W.cdof_dot[d][i] * qdd : ca[i];
-      }
-    }
+    for (int i = 0; i < 6; ++i) ca[i] = W.F[b][i];
     double Ia[6], Iv[6], cf[6];
     mul_inert(W.cinert[b], ca, Ia);
     mul_inert(W.cinert[b], W.cvel[b], Iv);
@@ -602,43 +634,34 @@ HM_INLINE void accelerations(Wave& W, const Shared& S, int lane, int64_t* st = n
   }
   WAVE_SYNC();
   HM_STAMP(6);
-  // subtree sums, leaves -> root: a parent adds its children in descending index
+  // subtree sums, leaves -> root: a parent adds its children in descending index.  One
+  // lane per (parent slot, element): a level's (at most four) parents x the 16 elements
+  // of fb (6) ++ crb (10) fill the wave, so each lane adds its element's three child
+  // values -- the same adds in the same order per element as a parent-per-lane loop over
+  // all 16, at a sixteenth of the instructions (subtree phase 10.6 k -> see DESIGN §3b)
+  {
+    const int slot = lane >> 4, el = lane & 15;
+    double* const eb = el < 6 ? &W.fb[0][el] : &W.crb[0][el - 6];  // element el of body 0
+    const int es = el < 6 ? 6 : 10;                                 // its stride over bodies
 #pragma unroll 1
-  for (int lv = NLEVEL - 2; lv >= 0; --lv) {
-    const uint32_t ts = S.w[W_SUB + lv][lane];
-    const int p = (int)byte_of(ts, 0);
-    if (p != (int)NONE) {
-      double f[6], c[10];
+    for (int lv = NLEVEL - 2; lv >= 0; --lv) {
+      const uint32_t ts = S.w[W_SUB + lv][slot];
+      const int p = (int)byte_of(ts, 0);
+      if (p != (int)NONE) {
+        // every child slot loads (a missing child reads the parent) so the loads batch;
+        // only existing children add
+        double v = eb[p * es], cv[3];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) f[i] = W.fb[p][i];
+        for (int k = 0; k < 3; ++k) {
+          const int ch = (int)byte_of(ts, k + 1);
+          cv[k] = eb[(ch == (int)NONE ? p : ch) * es];
+        }
 #pragma unroll
-      for (int i = 0; i < 10; ++i) c[i] = W.crb[p][i];
-      // every child slot loads (a missing child reads the parent) so the loads batch;
-      // only existing children add
-      double fc[3][6], cc[3][10];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int ch = (int)byte_of(ts, k + 1);
-        const int chc = ch == (int)NONE ? p : ch;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) fc[k][i] = W.fb[chc][i];
-#pragma unroll
-        for (int i = 0; i < 10; ++i) cc[k][i] = W.crb[chc][i];
+        for (int k = 0; k < 3; ++k) v = byte_of(ts, k + 1) != NONE ? v + cv[k] : v;
+        eb[p * es] = v;
       }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const bool has = byte_of(ts, k + 1) != NONE;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) f[i] = has ? f[i] + fc[k][i] : f[i];
-#pragma unroll
-        for (int i = 0; i < 10; ++i) c[i] = has ? c[i] + cc[k][i] : c[i];
-      }
-#pragma unroll
-      for (int i = 0; i < 6; ++i) W.fb[p][i] = f[i];
-#pragma unroll
-      for (int i = 0; i < 10; ++i) W.crb[p][i] = c[i];
+      WAVE_SYNC();
     }
-    WAVE_SYNC();
   }
   HM_STAMP(7);
   // per dof i: F_i = crb(body(i)) cdof_i and the generalised force

@@ -79,6 +79,70 @@ def test_layered_rollout_matches_oracle(env_id, hid, E, Tn, limit, inject):
         np.testing.assert_allclose(mr, fs.M[-1], rtol=1e-4, atol=1e-5)
 
 
+def test_humanoid_step_matches_oracle_twin():
+    """The wave-per-env Humanoid step (hm_act_kernel) against oracle/humanoid.py on the
+    same controls: with the policy means given as z rows, logstd 0 and injected noise the
+    action a = z + noise is the same fp32 value on both sides, and the fp64 env state
+    (qpos ++ qvel ++ ctrl) and the raw 376-d observation + reward after every one of 40
+    steps (auto-resets included) follow the oracle's operation sequence per value.  Not
+    bit for bit: the device sin / cos and numpy's libm differ in the last bit for some
+    angles (about half the words differ after 40 steps, by <= ~1e-9 relative, r06s2d).
+    Bit-identity of a kernel change against the previous build is tools/hm_twin_ab.py."""
+    from modular_rl_amd import _lib
+    from modular_rl_amd.collector import Collector
+    from modular_rl_amd.envs import make
+    from modular_rl_amd._lib import call, ptr, stream
+    import ctypes
+    env = make("Humanoid-v2")
+    E, Tn, A, O = 96, 40, env.act_dim, env.obs_dim
+    _, _, pol = _layered_policy("gauss", O, A, [32], seed=4)
+    seed = 4242
+    col = Collector(env, pol, E, Tn, 1000, filter=1, seed=seed, use_graph=False)
+    rng = np.random.default_rng(11)
+    noise = rng.standard_normal((Tn, E, A))
+    z = (0.4 * rng.standard_normal((Tn, E, A))).astype(np.float32)
+    col.set_noise(noise.reshape(Tn * E, A))
+    logstd = torch.zeros(A, dtype=torch.float32, device="cuda")
+    d, bufs = ctypes.byref(col.desc), col._bufs()
+    envs = RO.Envs(RO.HUMANOID, E, seed)
+    envs.reset(np.arange(E))
+    call("mrl_rollout_reset_rows", d, ctypes.byref(bufs), stream())
+    ns = envs.ns
+
+    worst = [0.0, 0, 0]  # max relative difference, differing words, compared words
+
+    def cmp(got, want):
+        worst[1] += int((got.view(np.uint64) != want.view(np.uint64)).sum())
+        worst[2] += got.size
+        worst[0] = max(worst[0], float((np.abs(got - want) / np.maximum(np.abs(want), 1e-6)).max()))
+
+    def check(t, rew=None):
+        torch.cuda.synchronize()
+        cmp(col.env_state.view(ns, E).cpu().numpy().T, envs.state)
+        raw = col.raw_obs.view(O + 1, E).cpu().numpy().T
+        cmp(raw[:, :O], envs.obs())
+        if rew is not None:
+            cmp(raw[:, O], rew)
+
+    check(-1)
+    resets = 0
+    for t in range(Tn):
+        zt = torch.as_tensor(z[t]).cuda().contiguous()
+        call("mrl_rollout_act", d, int(_lib.HEAD_GAUSS), A, ptr(zt), ptr(logstd), ctypes.byref(bufs), t, stream())
+        act = noise[t].astype(np.float32) * np.float32(1.0) + z[t]
+        rew, done = envs.step(act)
+        ept = envs.ep_t.copy()
+        last = done | (ept + 1 >= envs.max_steps) | (t == Tn - 1)
+        envs.ep_t = ept + 1
+        if t < Tn - 1 and last.any():
+            envs.reset(np.nonzero(last)[0])
+            resets += int(last.sum())
+        check(t, rew)
+    assert resets > 0  # the auto-reset path ran
+    print("humanoid step twin: max rel diff %.3g, %d of %d words differ" % tuple(worst))
+    assert worst[0] <= 1e-7
+
+
 def test_layered_rollout_graph_replay_equals_eager():
     from modular_rl_amd.collector import Collector
     from modular_rl_amd.envs import make

@@ -14,6 +14,7 @@
 #   gae          mrl_gae alone: exact-fit vs general kernel (MRL_GAE_GENERAL=1) + rocprof stats
 #   pair         the default bench line with the two-kernel Fisher product (MRL_FISHER_ONEPASS=0)
 #   layered_tests  the layered-path / Humanoid GPU tests only
+#   c5prof       rocprofv3 kernel trace of the C5 bf16 line + the per-step timeline (tools/step_timeline.py)
 #   c5 / c5_f32  C5 Humanoid fp32 line (split GEMMs / exact-f32 GEMMs: MRL_GEMM_SPLIT=0)
 # Every GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
@@ -102,6 +103,12 @@ for step in "$@"; do
         --timeout 300 --timeout-method thread > gpurun_out/${tag}_layered_tests.log 2>&1 ||
         { echo LAYERED_TESTS_FAILED; tail -40 gpurun_out/${tag}_layered_tests.log; exit 1; }
       tail -1 gpurun_out/${tag}_layered_tests.log ;;
+    c5prof)  # kernel trace of the C5 bf16 line: the layered rollout's per-step timeline
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_c5prof -o run --output-format csv \
+        -- python3 bench.py --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 2 --warmup 1 --dtype bf16 \
+        --no-cpu-baseline > gpurun_out/${tag}_c5prof.log 2>&1 || { echo C5PROF_FAILED; tail -5 gpurun_out/${tag}_c5prof.log; exit 1; }
+      python tools/step_timeline.py gpurun_out/${tag}_c5prof/run_kernel_trace.csv > gpurun_out/${tag}_c5_timeline.txt &&
+        cat gpurun_out/${tag}_c5_timeline.txt ;;
     c5) bench humanoid 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 5 --warmup 1 --no-cpu-baseline ;;
     c5_f32) MRL_GEMM_SPLIT=0 bench humanoid_f32gemm 600 --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 5 \
       --warmup 1 --no-cpu-baseline ;;
