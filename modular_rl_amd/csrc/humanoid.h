@@ -335,63 +335,78 @@ HM_INLINE void forward(Wave& W, const Shared& S, int lane, int64_t* st = nullptr
     W.xpos[0][2] = q[2];
   }
   WAVE_SYNC();
-  // each body's pose in its parent's frame (after its hinges), all bodies at once
-  if (lane >= 1 && lane < NB) {
-    const int b = lane;
-    double Q[9], o[3];
-    quat_mat(S.quat[b][0], S.quat[b][1], S.quat[b][2], S.quat[b][3], Q);
+  // each body's pose in its parent's frame (after its hinges), one lane per (body b, row
+  // r): every product here takes row r of the body's running rotation Q times constant /
+  // LDS matrices and vectors, so a row's lane carries the row through the same operations
+  // (mm3 / mv3 row r) as a body-per-lane loop over all three
+  {
+    const int b = lane & 15, r = lane >> 4;
+    if (b >= 1 && b < NB && r < 3) {
+      double Q[3], o;
+      {
+        double Qf[9];
+        quat_mat(S.quat[b][0], S.quat[b][1], S.quat[b][2], S.quat[b][3], Qf);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) o[i] = S.pos[b][i];
-    const int h0 = S.hinge0[b], nh = S.nhinge[b];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      if (c < nh) {
-        const int j = h0 + c;
-        double ra[3], Qn[9], rb[3];
-        mv3(Q, S.hpos[j], ra);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) W.lanc[j][i] = o[i] + ra[i];
-        mv3(Q, S.hax[j], W.lax[j]);
-        mm3(Q, W.rot[j], Qn);
-#pragma unroll
-        for (int i = 0; i < 9; ++i) Q[i] = Qn[i];
-        mv3(Q, S.hpos[j], rb);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) o[i] = W.lanc[j][i] - rb[i];
+        for (int c = 0; c < 3; ++c) Q[c] = r == 0 ? Qf[c] : (r == 1 ? Qf[3 + c] : Qf[6 + c]);
       }
+      o = S.pos[b][r];
+      const int h0 = S.hinge0[b], nh = S.nhinge[b];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        if (c < nh) {
+          const int j = h0 + c;
+          const double* hp = S.hpos[j];
+          const double* hx = S.hax[j];
+          const double* rt = W.rot[j];
+          const double ra = (Q[0] * hp[0] + Q[1] * hp[1]) + Q[2] * hp[2];
+          const double la = o + ra;
+          W.lanc[j][r] = la;
+          W.lax[j][r] = (Q[0] * hx[0] + Q[1] * hx[1]) + Q[2] * hx[2];
+          double Qn[3];
+#pragma unroll
+          for (int jj = 0; jj < 3; ++jj) Qn[jj] = (Q[0] * rt[jj] + Q[1] * rt[3 + jj]) + Q[2] * rt[6 + jj];
+#pragma unroll
+          for (int jj = 0; jj < 3; ++jj) Q[jj] = Qn[jj];
+          const double rb = (Q[0] * hp[0] + Q[1] * hp[1]) + Q[2] * hp[2];
+          o = la - rb;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) W.Qloc[b][3 * r + c] = Q[c];
+      W.oloc[b][r] = o;
     }
-#pragma unroll
-    for (int i = 0; i < 9; ++i) W.Qloc[b][i] = Q[i];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) W.oloc[b][i] = o[i];
   }
   WAVE_SYNC();
   HM_STAMP(1);
-  // world poses: body `lane` composes its path from the root
-  if (lane >= 1 && lane < NB) {
-    const uint32_t p0 = S.w[W_PATH][lane], p1 = S.w[W_PATH + 1][lane];
-    double R[9], x[3];
+  // world poses: body b composes its path from the root, one lane per (body b, row r):
+  // row r of R Qloc and of R oloc need row r of R only
+  {
+    const int b = lane & 15, r = lane >> 4;
+    if (b >= 1 && b < NB && r < 3) {
+      const uint32_t p0 = S.w[W_PATH][b], p1 = S.w[W_PATH + 1][b];
+      double R[3], x;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) R[i] = W.R[0][i];
+      for (int c = 0; c < 3; ++c) R[c] = W.R[0][3 * r + c];
+      x = W.xpos[0][r];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) x[i] = W.xpos[0][i];
+      for (int s = 0; s < PATH_LEN; ++s) {
+        const int a = path_body(p0, p1, s);
+        const bool has = a != (int)NONE;
+        const int ac = has ? a : 0;
+        const double* Ql = W.Qloc[ac];
+        const double* ol = W.oloc[ac];
+        double Rn[3];
 #pragma unroll
-    for (int s = 0; s < PATH_LEN; ++s) {
-      const int a = path_body(p0, p1, s);
-      const bool has = a != (int)NONE;
-      const int ac = has ? a : 0;
-      double Rn[9], off[3];
-      mm3(R, W.Qloc[ac], Rn);
-      mv3(R, W.oloc[ac], off);
+        for (int c = 0; c < 3; ++c) Rn[c] = (R[0] * Ql[c] + R[1] * Ql[3 + c]) + R[2] * Ql[6 + c];
+        const double off = (R[0] * ol[0] + R[1] * ol[1]) + R[2] * ol[2];
+        x = has ? x + off : x;
 #pragma unroll
-      for (int i = 0; i < 3; ++i) x[i] = has ? x[i] + off[i] : x[i];
+        for (int c = 0; c < 3; ++c) R[c] = has ? Rn[c] : R[c];
+      }
 #pragma unroll
-      for (int i = 0; i < 9; ++i) R[i] = has ? Rn[i] : R[i];
+      for (int c = 0; c < 3; ++c) W.R[b][3 * r + c] = R[c];
+      W.xpos[b][r] = x;
     }
-#pragma unroll
-    for (int i = 0; i < 9; ++i) W.R[lane][i] = R[i];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) W.xpos[lane][i] = x[i];
   }
   WAVE_SYNC();
   HM_STAMP(2);
@@ -417,32 +432,39 @@ HM_INLINE void forward(Wave& W, const Shared& S, int lane, int64_t* st = nullptr
     W.com[lane] = acc / TOTAL_MASS;
   }
   WAVE_SYNC();
-  if (lane < NB) {  // cinert
-    const int b = lane;
-    const double* I6 = S.inertia[b];
-    const double Ib[9] = {I6[0], I6[3], I6[4], I6[3], I6[1], I6[5], I6[4], I6[5], I6[2]};
-    double Rt[9], T[9], Iw[9], d[3];
+  {  // cinert, one lane per (body b, row r): row r of T = R Ib and of Iw = T R^T, and the
+     // cinert entries on that row of Iw (the same expressions as a body-per-lane mm3 pair)
+    const int b = lane & 15, r = lane >> 4;
+    if (b < NB && r < 3) {
+      const double* I6 = S.inertia[b];
+      const double Ib[9] = {I6[0], I6[3], I6[4], I6[3], I6[1], I6[5], I6[4], I6[5], I6[2]};
+      const double* R = W.R[b];
+      double T[3], Iw[3], d[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) T[j] = (R[3 * r] * Ib[j] + R[3 * r + 1] * Ib[3 + j]) + R[3 * r + 2] * Ib[6 + j];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) Rt[3 * i + j] = W.R[b][3 * j + i];
-    mm3(W.R[b], Ib, T);
-    mm3(T, Rt, Iw);
-    const double m = S.mass[b];
+      for (int j = 0; j < 3; ++j) Iw[j] = (T[0] * R[3 * j] + T[1] * R[3 * j + 1]) + T[2] * R[3 * j + 2];
+      const double m = S.mass[b];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) d[i] = W.xipos[b][i] - W.com[i];
-    double* ci = W.cinert[b];
-    ci[0] = Iw[0] + m * (d[1] * d[1] + d[2] * d[2]);
-    ci[1] = Iw[4] + m * (d[0] * d[0] + d[2] * d[2]);
-    ci[2] = Iw[8] + m * (d[0] * d[0] + d[1] * d[1]);
-    ci[3] = Iw[1] - m * (d[0] * d[1]);
-    ci[4] = Iw[2] - m * (d[0] * d[2]);
-    ci[5] = Iw[5] - m * (d[1] * d[2]);
-    ci[6] = m * d[0];
-    ci[7] = m * d[1];
-    ci[8] = m * d[2];
-    ci[9] = m;
-  } else if (lane >= 32 && lane < 32 + NV) {  // cdof
+      for (int i = 0; i < 3; ++i) d[i] = W.xipos[b][i] - W.com[i];
+      double* ci = W.cinert[b];
+      if (r == 0) {
+        ci[0] = Iw[0] + m * (d[1] * d[1] + d[2] * d[2]);
+        ci[3] = Iw[1] - m * (d[0] * d[1]);
+        ci[4] = Iw[2] - m * (d[0] * d[2]);
+      } else if (r == 1) {
+        ci[1] = Iw[1] + m * (d[0] * d[0] + d[2] * d[2]);
+        ci[5] = Iw[2] - m * (d[1] * d[2]);
+      } else {
+        ci[2] = Iw[2] + m * (d[0] * d[0] + d[1] * d[1]);
+        ci[6] = m * d[0];
+        ci[7] = m * d[1];
+        ci[8] = m * d[2];
+        ci[9] = m;
+      }
+    }
+  }
+  if (lane >= 32 && lane < 32 + NV) {  // cdof
     const int i = lane - 32;
     double* cd = W.cdof[i];
     if (i < 3) {
