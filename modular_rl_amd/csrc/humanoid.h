@@ -16,6 +16,8 @@
 // need compiler fences only (WAVE_SYNC), no barriers.
 // Model constants: humanoid_model.h (generated from modular_rl_amd/humanoid_model.py).
 #pragma once
+#include <cstddef>
+
 #include "humanoid_model.h"
 #include "mrl_common.h"
 
@@ -126,8 +128,78 @@ constexpr int W_PAIR = W_MISC + 1;            // [NV] pivot k's (i, j) pairs at 
 constexpr int W_KANC = W_PAIR + NV;           // [(NV+3)/4] pivot k's lane-th strict ancestor: byte k % 4 of word k / 4
 constexpr int W_ENT = W_KANC + (NV + 3) / 4;  // [ceil(N_ENT/128)] mass-matrix entries r, r+64: i | j << 8 (, << 16, 24)
 constexpr int N_ENT_WORDS = (N_ENT + 127) / 128;
-constexpr int TOPO_WORDS = W_ENT + N_ENT_WORDS;
 constexpr int PATH_LEN = NLEVEL - 1;
+
+// Branch-parallel L^T D L schedule.  The dof tree is a trunk (a chain 0 .. NT-1 of dofs
+// with two or more leaves below) carrying branches (chains NT .. NV-1 hanging off trunk
+// dofs: the legs and the arms).  A branch pivot k updates pairs (i, j) of its ancestors:
+// entries with i in k's branch belong to that branch alone, entries with i in the trunk
+// are shared by every branch below i.  So the branches' pivots run in lockstep (step s:
+// each branch's s-th pivot from its leaf, 16 lanes per branch), updating their branch
+// entries in place and leaving their trunk-entry products p_k(i, j) in C; one gather then
+// subtracts them from each trunk entry in descending k, and the trunk pivots follow in
+// sequence -- every entry sees the same operations in the same order as the pivot-by-pivot
+// loop.  Item words (dst | a1 << 11 | a2 << 21 | sub << 31, offsets in doubles from
+// W.L): dst = dst - a1 (a2 invd) if sub, else dst = a1 (a2 invd); a row scaling is
+// a1 = L[k][a] times a2 = the ONE slot (1 invd = invd exactly).
+constexpr int dof_leaves(int d) {
+  int n = 0;
+  for (int c = d + 1; c < NV; ++c)
+    if (DOF_PARENT[c] == d) n += dof_leaves(c);
+  return n > 0 ? n : 1;
+}
+constexpr int trunk_len() {
+  int n = 0;
+  while (n < NV && dof_leaves(n) >= 2) ++n;
+  return n;
+}
+constexpr int NT = trunk_len();                  // trunk dofs 0 .. NT-1
+constexpr int NTP = NT * (NT + 1) / 2;           // trunk entries (i, j <= i)
+constexpr int NCONTRIB = (NV - NT) * NTP;        // C: [branch pivot k - NT][trunk entry]
+constexpr int OFF_ONE = NV * NV, OFF_C = OFF_ONE + 1, OFF_JUNK = OFF_C + NCONTRIB;
+constexpr int branch_count() {
+  int n = 0;
+  for (int d = NT; d < NV; ++d) n += DOF_PARENT[d] < NT ? 1 : 0;
+  return n;
+}
+constexpr int NBRANCH = branch_count();
+constexpr int branch_root(int b) {
+  for (int d = NT; d < NV; ++d)
+    if (DOF_PARENT[d] < NT && b-- == 0) return d;
+  return -1;
+}
+constexpr int branch_leaf(int b) { return b + 1 < NBRANCH ? branch_root(b + 1) - 1 : NV - 1; }
+constexpr int anc_count(int k) {
+  int n = 0;
+  for (int l = 0; l < 16; ++l) n += ANC[16 * k + l] >= 0 ? 1 : 0;
+  return n;
+}
+constexpr int ldl_items(int k) { return (LDL_START[k + 1] - LDL_START[k]) + anc_count(k); }
+constexpr int branch_steps() {
+  int n = 0;
+  for (int b = 0; b < NBRANCH; ++b) n = branch_leaf(b) - branch_root(b) + 1 > n ? branch_leaf(b) - branch_root(b) + 1 : n;
+  return n;
+}
+constexpr int NBSTEP = branch_steps();
+constexpr int branch_slots() {
+  int n = 0;
+  for (int k = NT; k < NV; ++k) n = (ldl_items(k) + 15) / 16 > n ? (ldl_items(k) + 15) / 16 : n;
+  return n;
+}
+constexpr int NBSLOT = branch_slots();         // item words per lane and step (+1: the pivot's diagonal)
+constexpr int W_BR = W_ENT + N_ENT_WORDS;      // [NBSTEP][NBSLOT + 1] branch-step item words, then k NV + k
+constexpr int W_TG = W_BR + NBSTEP * (NBSLOT + 1);  // trunk entry `lane`: i NV + j | branch pivots below i << 16
+constexpr int TOPO_WORDS = W_TG + 1;
+constexpr bool ldl_schedule_fits() {
+  for (int d = 0; d < NT; ++d)
+    if (d > 0 && DOF_PARENT[d] != d - 1) return false;  // the trunk is a chain
+  for (int d = NT; d < NV; ++d) {
+    if (dof_leaves(d) != 1) return false;
+    if (DOF_PARENT[d] >= NT && DOF_PARENT[d] != d - 1) return false;  // branches are chains
+  }
+  return NT >= 1 && NBRANCH >= 1 && NBRANCH <= 4 && NV - NT <= 16 && NTP <= 64 && OFF_JUNK + 64 <= 2048 &&
+         OFF_ONE < 1024;
+}
 
 struct Shared {
   uint32_t w[TOPO_WORDS][64];
@@ -174,6 +246,15 @@ constexpr bool topo_fits() {
   return NV <= 32 && NB <= 32 && NSPH <= 64 && NACT <= 64 && NHINGE <= 32 && n_entries() <= N_ENT;
 }
 static_assert(topo_fits(), "humanoid tree exceeds the wave layout");
+static_assert(ldl_schedule_fits(), "humanoid dof tree does not fit the branch-parallel L^T D L schedule");
+constexpr uint32_t ldl_item(int dst, int a1, int a2, int sub) {
+  return (uint32_t)dst | (uint32_t)a1 << 11 | (uint32_t)a2 << 21 | (uint32_t)sub << 31;
+}
+constexpr bool dof_is_anc(int i, int k) {  // i a strict ancestor of k
+  for (int a = DOF_PARENT[k]; a >= 0; a = DOF_PARENT[a])
+    if (a == i) return true;
+  return false;
+}
 
 struct MaskTable {
   uint32_t anc[NV], desc[NV];
@@ -247,6 +328,41 @@ constexpr Shared make_shared() {
   }
   for (int q = 0; q < N_ENT_WORDS; ++q)
     for (int lane = 0; lane < 64; ++lane) t.w[W_ENT + q][lane] = ent[128 * q + lane] | ent[128 * q + 64 + lane] << 16;
+  // branch-parallel L^T D L: step st, lane 16 b + l runs items l, l + 16, ... of branch b's
+  // st-th pivot from its leaf (pairs in LDL order, then the row scalings); idle slots
+  // write the lane's junk slot
+  for (int st = 0; st < NBSTEP; ++st)
+    for (int lane = 0; lane < 64; ++lane) {
+      for (int q = 0; q < NBSLOT; ++q) t.w[W_BR + st * (NBSLOT + 1) + q][lane] = ldl_item(OFF_JUNK + lane, 0, 0, 0);
+      t.w[W_BR + st * (NBSLOT + 1) + NBSLOT][lane] = 0u;
+    }
+  for (int b = 0; b < NBRANCH; ++b)
+    for (int st = 0; st < NBSTEP; ++st) {
+      const int k = branch_leaf(b) - st;
+      if (k < branch_root(b)) continue;
+      int q = 0;
+      for (int pp = LDL_START[k]; pp < LDL_START[k + 1]; ++pp, ++q) {
+        const int i = LDL_I[pp], j = LDL_J[pp];
+        t.w[W_BR + st * (NBSLOT + 1) + q / 16][16 * b + q % 16] =
+            i >= NT ? ldl_item(i * NV + j, k * NV + i, k * NV + j, 1)
+                    : ldl_item(OFF_C + (k - NT) * NTP + i * (i + 1) / 2 + j, k * NV + i, k * NV + j, 0);
+      }
+      for (int l = 0; l < 16; ++l) {
+        const int a = ANC[16 * k + l];
+        if (a < 0) continue;
+        t.w[W_BR + st * (NBSLOT + 1) + q / 16][16 * b + q % 16] = ldl_item(k * NV + a, k * NV + a, OFF_ONE, 0);
+        ++q;
+      }
+      for (int l = 0; l < 16; ++l) t.w[W_BR + st * (NBSLOT + 1) + NBSLOT][16 * b + l] = (uint32_t)(k * NV + k);
+    }
+  // trunk entry (i, j) at lane i (i + 1) / 2 + j: its offset and the branch pivots below i
+  for (int lane = 0; lane < 64; ++lane) t.w[W_TG][lane] = 0u;
+  for (int i = 0, tp = 0; i < NT; ++i)
+    for (int j = 0; j <= i; ++j, ++tp) {
+      uint32_t m = 0;
+      for (int k = NT; k < NV; ++k) m |= dof_is_anc(i, k) ? 1u << (k - NT) : 0u;
+      t.w[W_TG][tp] = (uint32_t)(i * NV + j) | m << 16;
+    }
   for (int b = 0; b < NB; ++b) {
     for (int i = 0; i < 4; ++i) t.quat[b][i] = BODY_QUAT[4 * b + i];
     for (int i = 0; i < 3; ++i) {
@@ -308,9 +424,16 @@ struct Wave {
   double cinert[NB][10], cdof[NV][6], cdof_dot[NV][6], cvel[NB][6];
   double fsph[NSPH][6], cfrc[NB][6], fb[NB][6], crb[NB][10];
   double F[NV][6];
-  double L[NV][NV], junk[64], x[NV];  // junk: the target of lanes with no entry (branch-free stores)
+  // L, then (contiguous, addressed as offsets from L: OFF_ONE, OFF_C, OFF_JUNK) the 1.0 of
+  // the row scalings, the branch pivots' trunk products, and the target of lanes with no
+  // entry (branch-free stores)
+  double L[NV][NV], one, C[NCONTRIB], junk[64], x[NV];
   double red[2];
 };
+static_assert(offsetof(Wave, one) - offsetof(Wave, L) == OFF_ONE * sizeof(double) &&
+                  offsetof(Wave, C) - offsetof(Wave, L) == OFF_C * sizeof(double) &&
+                  offsetof(Wave, junk) - offsetof(Wave, L) == OFF_JUNK * sizeof(double),
+              "W.L offsets of the L^T D L items");
 
 HM_INLINE int path_body(uint32_t p0, uint32_t p1, int s) { return (int)byte_of(s < 4 ? p0 : p1, s & 3); }
 
@@ -707,7 +830,7 @@ HM_INLINE void accelerations(Wave& W, const Shared& S, int lane, int64_t* st = n
   HM_STAMP(8);
   // mass-matrix entries M_ij = cdof_j . F_i (j = i or an ancestor), all lanes at once
   double* Lf = &W.L[0][0];
-  const int junk = NV * NV + lane;  // W.junk[lane]
+  const int junk = OFF_JUNK + lane;  // W.junk[lane]
 #pragma unroll
   for (int r = 0; r < 2 * N_ENT_WORDS; ++r) {
     const uint32_t e = (S.w[W_ENT + (r >> 1)][lane] >> (16 * (r & 1))) & 0xffffu;
@@ -720,14 +843,52 @@ HM_INLINE void accelerations(Wave& W, const Shared& S, int lane, int64_t* st = n
   if (lane >= 6 && lane < NV) W.L[lane][lane] = W.L[lane][lane] + S.arm[lane - 6];
   WAVE_SYNC();
   HM_STAMP(9);
-  // L^T D L, leaves first: pivot k updates every (ancestor i, ancestor-or-self j of i)
-  // pair from its still unscaled row, then scales its row (reads before writes: one
-  // phase per pivot)
-  // the next pivot's table words are loaded a pivot ahead (constants: no ordering)
-  uint32_t pr = S.w[W_PAIR + NV - 1][lane];
-  uint32_t ka = S.w[W_KANC + ((NV - 1) >> 2)][lane];
+  // L^T D L, leaves first (the branch-parallel schedule above).  Branch steps: each lane
+  // reads its items' operands and its pivot's diagonal, then writes (reads before writes:
+  // one phase per step)
+  if (lane == 0) W.one = 1.0;
+  WAVE_SYNC();
 #pragma unroll 1
-  for (int k = NV - 1; k >= 0; --k) {
+  for (int st = 0; st < NBSTEP; ++st) {
+    uint32_t it[NBSLOT];
+#pragma unroll
+    for (int q = 0; q < NBSLOT; ++q) it[q] = S.w[W_BR + st * (NBSLOT + 1) + q][lane];
+    const double lkk = Lf[S.w[W_BR + st * (NBSLOT + 1) + NBSLOT][lane]];
+    double vd[NBSLOT], v1[NBSLOT], v2[NBSLOT];
+#pragma unroll
+    for (int q = 0; q < NBSLOT; ++q) {
+      vd[q] = Lf[it[q] & 0x7ffu];
+      v1[q] = Lf[(it[q] >> 11) & 0x3ffu];
+      v2[q] = Lf[(it[q] >> 21) & 0x3ffu];
+    }
+    const double invd = 1.0 / lkk;
+#pragma unroll
+    for (int q = 0; q < NBSLOT; ++q) {
+      const double p = v1[q] * (v2[q] * invd);
+      Lf[it[q] & 0x7ffu] = (it[q] >> 31) ? vd[q] - p : p;
+    }
+    WAVE_SYNC();
+  }
+  // trunk gather: entry (i, j) minus the branch pivots' products, in descending pivot order
+  if (lane < NTP) {
+    const uint32_t tg = S.w[W_TG][lane];
+    const int off = (int)(tg & 0xffffu);
+    const uint32_t m = tg >> 16;
+    double v = Lf[off], c[NV - NT];
+#pragma unroll
+    for (int q = 0; q < NV - NT; ++q) c[q] = Lf[OFF_C + q * NTP + lane];
+#pragma unroll
+    for (int q = NV - NT - 1; q >= 0; --q) v = ((m >> q) & 1u) ? v - c[q] : v;
+    Lf[off] = v;
+  }
+  WAVE_SYNC();
+  // trunk pivots in sequence: pivot k updates every (ancestor i, ancestor-or-self j of i)
+  // pair from its still unscaled row, then scales its row (reads before writes: one
+  // phase per pivot); the next pivot's table words are loaded a pivot ahead
+  uint32_t pr = S.w[W_PAIR + NT - 1][lane];
+  uint32_t ka = S.w[W_KANC + ((NT - 1) >> 2)][lane];
+#pragma unroll 1
+  for (int k = NT - 1; k >= 0; --k) {
     const int a = (int)byte_of(ka, k & 3);
     const int i0 = (int)byte_of(pr, 0), j0 = (int)byte_of(pr, 1), i1 = (int)byte_of(pr, 2), j1 = (int)byte_of(pr, 3);
     // no-entry lanes read harmless in-range elements and write their junk slot
