@@ -440,7 +440,8 @@ typedef struct {
 } mrl_rollout_desc;
 
 typedef struct {
-  double* env_state;       /* [state_doubles, E] SoA                             */
+  double* env_state;       /* [state_doubles, E]: SoA state rows (Humanoid: the NS state rows,
+                              then each env's kinematics cache, AoS)             */
   int32_t* env_int;        /* [2, E]: steps in episode, episodes started         */
   double* filter_state;    /* [2, filter_doubles] ping-pong running stats        */
   double* records;         /* [2, n_blocks, record_doubles] per-block partials   */
@@ -460,6 +461,8 @@ typedef struct {
                               obs_dim.. left as they are (caller zeroes them once); NULL: none */
 } mrl_rollout_bufs;
 
+/* env_state doubles per env (Humanoid: qpos ++ qvel ++ ctrl, 64, plus the 565-double
+   kinematics cache the step kernels keep of the stored state) */
 int64_t mrl_env_state_doubles(int32_t env_id);
 int64_t mrl_filter_doubles(int32_t env_id);
 int64_t mrl_record_doubles(int32_t env_id);

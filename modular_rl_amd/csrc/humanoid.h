@@ -420,9 +420,11 @@ HM_INLINE double read_lane(double v, int l) {
 struct Wave {
   double s[NQ + NV + NACT];  // qpos ++ qvel ++ ctrl
   double rot[NHINGE][9], Qloc[NB][9], oloc[NB][3], lax[NHINGE][3], lanc[NHINGE][3];
-  double R[NB][9], xpos[NB][3], xipos[NB][3], haxis[NHINGE][3], hanchor[NHINGE][3], com[3];
-  double cinert[NB][10], cdof[NV][6], cdof_dot[NV][6], cvel[NB][6];
-  double fsph[NSPH][6], cfrc[NB][6], fb[NB][6], crb[NB][10];
+  double R[NB][9], xpos[NB][3], xipos[NB][3], haxis[NHINGE][3], hanchor[NHINGE][3], fsph[NSPH][6];
+  // forward()'s outputs that accelerations() and the reward read, contiguous: the
+  // kinematics cache (KCACHE doubles, com .. cfrc) a step leaves beside the env state
+  double com[3], cinert[NB][10], cdof[NV][6], cdof_dot[NV][6], cvel[NB][6], cfrc[NB][6];
+  double fb[NB][6], crb[NB][10];
   double F[NV][6];
   // L, then (contiguous, addressed as offsets from L: OFF_ONE, OFF_C, OFF_JUNK) the 1.0 of
   // the row scalings, the branch pivots' trunk products, and the target of lanes with no
@@ -430,6 +432,24 @@ struct Wave {
   double L[NV][NV], one, C[NCONTRIB], junk[64], x[NV];
   double red[2];
 };
+constexpr int KCACHE = 3 + NB * 10 + NV * 6 * 2 + NB * 6 * 2;
+static_assert(offsetof(Wave, fb) - offsetof(Wave, com) == KCACHE * sizeof(double), "kinematics cache span");
+// The kinematics cache of an env: what forward() computed from the state the step left
+// (env_state's per-env tail, AoS: the wave's lanes read / write consecutive doubles).
+// The next step starts from it instead of its first substep's forward() -- the same
+// values, so bit-identical (every writer of a Humanoid env state writes its cache).
+HM_INLINE void save_kcache(const Wave& W, double* dst, int lane) {
+  const double* src = W.com;
+#pragma unroll
+  for (int i = 0; i < (KCACHE + 63) / 64; ++i)
+    if (lane + 64 * i < KCACHE) dst[lane + 64 * i] = src[lane + 64 * i];
+}
+HM_INLINE void load_kcache(Wave& W, const double* src, int lane) {
+  double* dst = W.com;
+#pragma unroll
+  for (int i = 0; i < (KCACHE + 63) / 64; ++i)
+    if (lane + 64 * i < KCACHE) dst[lane + 64 * i] = src[lane + 64 * i];
+}
 static_assert(offsetof(Wave, one) - offsetof(Wave, L) == OFF_ONE * sizeof(double) &&
                   offsetof(Wave, C) - offsetof(Wave, L) == OFF_C * sizeof(double) &&
                   offsetof(Wave, junk) - offsetof(Wave, L) == OFF_JUNK * sizeof(double),
@@ -1044,5 +1064,6 @@ __device__ inline void observation(const Wave& W, const Shared& S, int lane, Out
 }  // namespace hm
 
 constexpr int HM_NQ = hm::NQ, HM_NV = hm::NV, HM_ACT = hm::NACT, HM_NS = hm::NS, HM_OBS = hm::OBS, HM_NU = hm::NU;
+constexpr int HM_KCACHE = hm::KCACHE;
 
 }  // namespace mrl

@@ -1516,6 +1516,7 @@ __global__ __launch_bounds__(64 * WPB) void hm_reset_kernel(RollArgs a) {
   double* raw = a.b.raw_obs;
   hm::observation(W, S, lane, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
   if (lane < HM_NS) a.b.env_state[(int64_t)lane * E + e] = W.s[lane];
+  hm::save_kcache(W, a.b.env_state + (int64_t)HM_NS * E + (int64_t)e * HM_KCACHE, lane);
   if (lane == 0) {
     raw[(int64_t)HM_OBS * E + e] = 0.0;
     a.b.env_int[E + e] = (int32_t)(w + 1);
@@ -1570,6 +1571,9 @@ __global__ __launch_bounds__(64 * WPB) void hm_act_kernel(RollArgs a, const floa
   if (e >= E) return;  // after the tables' barrier
   const int64_t row = (int64_t)t * E + e;
   if (lane < HM_NS) W.s[lane] = a.b.env_state[(int64_t)lane * E + e];
+  // the kinematics of that state, as the step that left it computed them (first substep)
+  double* const kc = a.b.env_state + (int64_t)HM_NS * E + (int64_t)e * HM_KCACHE;
+  hm::load_kcache(W, kc, lane);
   const bool fused = hr.hid != nullptr || hr.hid16 != nullptr;
   const float zh = fused ? head_z(hr, e, lane) : 0.f;
   WAVE_SYNC();
@@ -1599,7 +1603,7 @@ __global__ __launch_bounds__(64 * WPB) void hm_act_kernel(RollArgs a, const floa
   for (int pass = 0;; ++pass) {
     int64_t* sp = pass == 1 ? st : nullptr;
     if (sp != nullptr && lane == 0) sp[0] = (int64_t)__builtin_amdgcn_s_memtime();
-    hm::forward(W, S, lane, sp);
+    if (pass > 0) hm::forward(W, S, lane, sp);  // pass 0: the kinematics cache
     if (pass < hm::FRAME_SKIP) {
       if (pass == 0) x_before = W.com[0];
       hm::accelerations(W, S, lane, sp);
@@ -1630,6 +1634,7 @@ __global__ __launch_bounds__(64 * WPB) void hm_act_kernel(RollArgs a, const floa
     }
   }
   if (lane < HM_NS) a.b.env_state[(int64_t)lane * E + e] = W.s[lane];
+  hm::save_kcache(W, kc, lane);  // W holds forward() of the state just stored
   double* raw = a.b.raw_obs;
   hm::observation(W, S, lane, [&](int k, double v) { raw[(int64_t)k * E + e] = v; });
   if (lane == 0) raw[(int64_t)HM_OBS * E + e] = rew;
@@ -1742,7 +1747,11 @@ static RollArgs make_args(const mrl_rollout_desc* d, const mrl_rollout_bufs* b) 
 
 extern "C" {
 
-int64_t mrl_env_state_doubles(int32_t env_id) { return env_info(env_id).ns; }
+// Humanoid: the state (SoA [NS][E]) and then each env's kinematics cache (AoS [E][KCACHE],
+// humanoid.h save_kcache) -- the forward kinematics of the stored state
+int64_t mrl_env_state_doubles(int32_t env_id) {
+  return env_info(env_id).ns + (env_id == MRL_ENV_HUMANOID ? HM_KCACHE : 0);
+}
 int64_t mrl_filter_doubles(int32_t env_id) { return filt_doubles(env_info(env_id).obs); }
 int64_t mrl_record_doubles(int32_t env_id) { return filt_doubles(env_info(env_id).obs); }
 int64_t mrl_rollout_blocks(int32_t n_envs) { return (n_envs + ENVS_PER_BLOCK - 1) / ENVS_PER_BLOCK; }

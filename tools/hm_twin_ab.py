@@ -37,7 +37,7 @@ def run(out, E=256, T=64):
     for t in range(T):
         zt = torch.as_tensor(z[t]).cuda().contiguous()
         call("mrl_rollout_act", d, int(_lib.HEAD_GAUSS), A, ptr(zt), ptr(logstd), ctypes.byref(bufs), t, stream())
-        states.append(col.env_state.clone())
+        states.append(col.env_state[:64 * E].clone())  # the state rows (not the kinematics cache)
         raws.append(col.raw_obs.clone())
     torch.cuda.synchronize()
     np.savez(out, state=torch.stack(states).cpu().numpy(), raw=torch.stack(raws).cpu().numpy(),
