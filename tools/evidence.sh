@@ -105,7 +105,7 @@ for step in "$@"; do
       tail -1 gpurun_out/${tag}_layered_tests.log ;;
     c5prof)  # kernel trace of the C5 bf16 line: the layered rollout's per-step timeline
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_c5prof -o run --output-format csv \
-        -- python3 bench.py --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 2 --warmup 1 --dtype bf16 \
+        -- python3 bench.py --env Humanoid-v2 --envs 1024 --hid 512,512,512 --steps 2 --warmup 1 --dtype ${C5DT:-bf16} \
         --no-cpu-baseline > gpurun_out/${tag}_c5prof.log 2>&1 || { echo C5PROF_FAILED; tail -5 gpurun_out/${tag}_c5prof.log; exit 1; }
       python tools/step_timeline.py gpurun_out/${tag}_c5prof/run_kernel_trace.csv > gpurun_out/${tag}_c5_timeline.txt &&
         cat gpurun_out/${tag}_c5_timeline.txt ;;
