@@ -129,6 +129,20 @@ constexpr int W_KANC = W_PAIR + NV;           // [(NV+3)/4] pivot k's lane-th st
 constexpr int W_ENT = W_KANC + (NV + 3) / 4;  // [ceil(N_ENT/128)] mass-matrix entries r, r+64: i | j << 8 (, << 16, 24)
 constexpr int N_ENT_WORDS = (N_ENT + 127) / 128;
 constexpr int PATH_LEN = NLEVEL - 1;
+// The hinge dofs along body b's path below the root (root side first, each body's hinges
+// in order) as bytes: dof | own << 5 | own hinge index << 6, padding 0xff (dof field 31)
+constexpr int path_dof_count(int b) {
+  int n = 0;
+  for (int a = b; a > 0; a = BODY_PARENT[a]) n += BODY_NHINGE[a];
+  return n;
+}
+constexpr int max_path_dofs() {
+  int n = 0;
+  for (int b = 0; b < NB; ++b) n = path_dof_count(b) > n ? path_dof_count(b) : n;
+  return n;
+}
+constexpr int MAXPD = max_path_dofs();
+constexpr int PD_WORDS = (MAXPD + 3) / 4;
 
 // Branch-parallel L^T D L schedule.  The dof tree is a trunk (a chain 0 .. NT-1 of dofs
 // with two or more leaves below) carrying branches (chains NT .. NV-1 hanging off trunk
@@ -189,7 +203,8 @@ constexpr int branch_slots() {
 constexpr int NBSLOT = branch_slots();         // item words per lane and step (+1: the pivot's diagonal)
 constexpr int W_BR = W_ENT + N_ENT_WORDS;      // [NBSTEP][NBSLOT + 1] branch-step item words, then k NV + k
 constexpr int W_TG = W_BR + NBSTEP * (NBSLOT + 1);  // trunk entry `lane`: i NV + j | branch pivots below i << 16
-constexpr int TOPO_WORDS = W_TG + 1;
+constexpr int W_PDOF = W_TG + 1;                    // [PD_WORDS] body (lane & 15)'s path dofs (bytes)
+constexpr int TOPO_WORDS = W_PDOF + PD_WORDS;
 constexpr bool ldl_schedule_fits() {
   for (int d = 0; d < NT; ++d)
     if (d > 0 && DOF_PARENT[d] != d - 1) return false;  // the trunk is a chain
@@ -328,6 +343,19 @@ constexpr Shared make_shared() {
   }
   for (int q = 0; q < N_ENT_WORDS; ++q)
     for (int lane = 0; lane < 64; ++lane) t.w[W_ENT + q][lane] = ent[128 * q + lane] | ent[128 * q + 64 + lane] << 16;
+  for (int lane = 0; lane < 64; ++lane) {
+    uint8_t pd[PD_WORDS * 4] = {};
+    for (int t = 0; t < PD_WORDS * 4; ++t) pd[t] = 0xff;
+    const int b = lane & 15;
+    if (b < NB) {
+      int chain[8] = {}, n = 0, t = 0;
+      for (int a = b; a > 0; a = BODY_PARENT[a]) chain[n++] = a;
+      for (int s = n - 1; s >= 0; --s)
+        for (int c = 0; c < BODY_NHINGE[chain[s]]; ++c)
+          pd[t++] = (uint8_t)((6 + BODY_HINGE0[chain[s]] + c) | (chain[s] == b ? 0x20 | c << 6 : 0));
+    }
+    for (int q = 0; q < PD_WORDS; ++q) t.w[W_PDOF + q][lane] = bytes4(pd[4 * q], pd[4 * q + 1], pd[4 * q + 2], pd[4 * q + 3]);
+  }
   // branch-parallel L^T D L: step st, lane 16 b + l runs items l, l + 16, ... of branch b's
   // st-th pivot from its leaf (pairs in LDL order, then the row scalings); idle slots
   // write the lane's junk slot
@@ -651,24 +679,22 @@ HM_INLINE void forward(Wave& W, const Shared& S, int lane, int64_t* st = nullptr
         if (b == 0) X[NB * 18 + e] = cv[i];
         cv[i] = cv[i] + ((W.cdof[3][e] * qd[3] + W.cdof[4][e] * qd[4]) + W.cdof[5][e] * qd[5]);
       }
-      const uint32_t p0 = S.w[W_PATH][b], p1 = S.w[W_PATH + 1][b];
+      uint32_t pw[PD_WORDS];
 #pragma unroll
-      for (int s = 0; s < PATH_LEN; ++s) {
-        const int a = path_body(p0, p1, s);
-        const int ac = a == (int)NONE ? 0 : a;
-        const int h0 = S.hinge0[ac], nh = a == (int)NONE ? 0 : S.nhinge[ac];
+      for (int q = 0; q < PD_WORDS; ++q) pw[q] = S.w[W_PDOF + q][lane];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const bool has = c < nh;
-          const int d = 6 + (has ? h0 + c : 0);
-          const double qdd = qd[d];
-          if (has && a == b) {
-            X[(b * 3 + c) * 6 + 2 * ep] = cv[0];
-            X[(b * 3 + c) * 6 + 2 * ep + 1] = cv[1];
-          }
-#pragma unroll
-          for (int i = 0; i < 2; ++i) cv[i] = has ? cv[i] + W.cdof[d][2 * ep + i] * qdd : cv[i];
+      for (int t = 0; t < MAXPD; ++t) {  // the path's hinge dofs in order (W_PDOF)
+        const uint32_t pb = byte_of(pw[t >> 2], t & 3);
+        const bool has = (pb & 31u) != 31u;
+        const int d = has ? (int)(pb & 31u) : 6;
+        const double qdd = qd[d];
+        if (has && (pb & 0x20u)) {  // own hinge c: the velocity in front of it
+          const int c = (int)(pb >> 6);
+          X[(b * 3 + c) * 6 + 2 * ep] = cv[0];
+          X[(b * 3 + c) * 6 + 2 * ep + 1] = cv[1];
         }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) cv[i] = has ? cv[i] + W.cdof[d][2 * ep + i] * qdd : cv[i];
       }
       W.cvel[b][2 * ep] = cv[0];
       W.cvel[b][2 * ep + 1] = cv[1];
@@ -762,20 +788,17 @@ HM_INLINE void accelerations(Wave& W, const Shared& S, int lane, int64_t* st = n
       for (int k = 3; k < 6; ++k)
 #pragma unroll
         for (int i = 0; i < 2; ++i) ca[i] = ca[i] + W.cdof_dot[k][2 * ep + i] * qd[k];
-      const uint32_t p0 = S.w[W_PATH][b], p1 = S.w[W_PATH + 1][b];
+      uint32_t pw[PD_WORDS];
 #pragma unroll
-      for (int s = 0; s < PATH_LEN; ++s) {
-        const int a = path_body(p0, p1, s);
-        const int ac = a == (int)NONE ? 0 : a;
-        const int h0 = S.hinge0[ac], nh = a == (int)NONE ? 0 : S.nhinge[ac];
+      for (int q = 0; q < PD_WORDS; ++q) pw[q] = S.w[W_PDOF + q][lane];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const bool has = c < nh;
-          const int d = 6 + (has ? h0 + c : 0);
-          const double qdd = qd[d];
+      for (int t = 0; t < MAXPD; ++t) {  // the path's hinge dofs in order (W_PDOF)
+        const uint32_t pb = byte_of(pw[t >> 2], t & 3);
+        const bool has = (pb & 31u) != 31u;
+        const int d = has ? (int)(pb & 31u) : 6;
+        const double qdd = qd[d];
 #pragma unroll
-          for (int i = 0; i < 2; ++i) ca[i] = has ? ca[i] + W.cdof_dot[d][2 * ep + i] * qdd : ca[i];
-        }
+        for (int i = 0; i < 2; ++i) ca[i] = has ? ca[i] + W.cdof_dot[d][2 * ep + i] * qdd : ca[i];
       }
       W.F[b][2 * ep] = ca[0];
       W.F[b][2 * ep + 1] = ca[1];
