@@ -124,9 +124,7 @@ constexpr int W_SUB = 0;                      // [NLEVEL] level lv's body at thi
 constexpr int W_PATH = W_SUB + NLEVEL;        // [2] body `lane`'s path below the root, root side first (bytes)
 constexpr int W_OWN = W_PATH + 2;             // body `lane`: hinge0 | nhinge << 8 | sph0 << 16 | nsph << 24
 constexpr int W_MISC = W_OWN + 1;             // dof `lane`'s body | sphere `lane`'s body << 8 | hinge `lane - 32`'s parent body << 16
-constexpr int W_PAIR = W_MISC + 1;            // [NV] pivot k's (i, j) pairs at this lane: i0 | j0 << 8 | i1 << 16 | j1 << 24
-constexpr int W_KANC = W_PAIR + NV;           // [(NV+3)/4] pivot k's lane-th strict ancestor: byte k % 4 of word k / 4
-constexpr int W_ENT = W_KANC + (NV + 3) / 4;  // [ceil(N_ENT/128)] mass-matrix entries r, r+64: i | j << 8 (, << 16, 24)
+constexpr int W_ENT = W_MISC + 1;             // [ceil(N_ENT/128)] mass-matrix entries r, r+64: i | j << 8 (, << 16, 24)
 constexpr int N_ENT_WORDS = (N_ENT + 127) / 128;
 constexpr int PATH_LEN = NLEVEL - 1;
 // The hinge dofs along body b's path below the root (root side first, each body's hinges
@@ -204,7 +202,8 @@ constexpr int NBSLOT = branch_slots();         // item words per lane and step (
 constexpr int W_BR = W_ENT + N_ENT_WORDS;      // [NBSTEP][NBSLOT + 1] branch-step item words, then k NV + k
 constexpr int W_TG = W_BR + NBSTEP * (NBSLOT + 1);  // trunk entry `lane`: i NV + j | branch pivots below i << 16
 constexpr int W_PDOF = W_TG + 1;                    // [PD_WORDS] body (lane & 15)'s path dofs (bytes)
-constexpr int TOPO_WORDS = W_PDOF + PD_WORDS;
+constexpr int W_TR = W_PDOF + PD_WORDS;             // [NT] trunk pivot k's item at this lane (one per lane)
+constexpr int TOPO_WORDS = W_TR + NT;
 constexpr bool ldl_schedule_fits() {
   for (int d = 0; d < NT; ++d)
     if (d > 0 && DOF_PARENT[d] != d - 1) return false;  // the trunk is a chain
@@ -212,6 +211,8 @@ constexpr bool ldl_schedule_fits() {
     if (dof_leaves(d) != 1) return false;
     if (DOF_PARENT[d] >= NT && DOF_PARENT[d] != d - 1) return false;  // branches are chains
   }
+  for (int k = 0; k < NT; ++k)
+    if (ldl_items(k) > 64) return false;  // a trunk pivot's items take one lane each
   return NT >= 1 && NBRANCH >= 1 && NBRANCH <= 4 && NV - NT <= 16 && NTP <= 64 && OFF_JUNK + 64 <= 2048 &&
          OFF_ONE < 1024;
 }
@@ -318,20 +319,6 @@ constexpr Shared make_shared() {
                                  : 0u;
     t.w[W_MISC][lane] = (lane < NV ? (uint32_t)DOF_BODY[lane] : 0u) | (lane < NSPH ? (uint32_t)SPHERE_BODY[lane] : 0u) << 8 |
                         (lane >= 32 && lane < 32 + NHINGE ? nb(BODY_PARENT[hinge_body(lane - 32)]) : 0u) << 16;
-    for (int k = 0; k < NV; ++k) {
-      uint32_t v = 0;
-      for (int h = 0; h < 2; ++h) {
-        const int pp = LDL_START[k] + lane + 64 * h;
-        const uint32_t ij = pp < LDL_START[k + 1] ? ((uint32_t)LDL_I[pp] | (uint32_t)LDL_J[pp] << 8) : (NONE | NONE << 8);
-        v |= ij << (16 * h);
-      }
-      t.w[W_PAIR + k][lane] = v;
-    }
-    for (int q = 0; q < (NV + 3) / 4; ++q) {
-      uint32_t v = 0;
-      for (int c = 0; c < 4 && 4 * q + c < NV; ++c) v |= nb(lane < 16 ? ANC[16 * (4 * q + c) + lane] : -1) << (8 * c);
-      t.w[W_KANC + q][lane] = v;
-    }
   }
   // mass-matrix entries, row by row (diagonal first, then the ancestors nearest first)
   uint32_t ent[N_ENT_WORDS * 128] = {};
@@ -383,6 +370,15 @@ constexpr Shared make_shared() {
       }
       for (int l = 0; l < 16; ++l) t.w[W_BR + st * (NBSLOT + 1) + NBSLOT][16 * b + l] = (uint32_t)(k * NV + k);
     }
+  // trunk pivot k: its pairs, then its row scalings, one item per lane
+  for (int k = 0; k < NT; ++k) {
+    for (int lane = 0; lane < 64; ++lane) t.w[W_TR + k][lane] = ldl_item(OFF_JUNK + lane, 0, 0, 0);
+    int q = 0;
+    for (int pp = LDL_START[k]; pp < LDL_START[k + 1]; ++pp, ++q)
+      t.w[W_TR + k][q] = ldl_item(LDL_I[pp] * NV + LDL_J[pp], k * NV + LDL_I[pp], k * NV + LDL_J[pp], 1);
+    for (int l = 0; l < 16; ++l)
+      if (ANC[16 * k + l] >= 0) t.w[W_TR + k][q++] = ldl_item(k * NV + ANC[16 * k + l], k * NV + ANC[16 * k + l], OFF_ONE, 0);
+  }
   // trunk entry (i, j) at lane i (i + 1) / 2 + j: its offset and the branch pivots below i
   for (int lane = 0; lane < 64; ++lane) t.w[W_TG][lane] = 0u;
   for (int i = 0, tp = 0; i < NT; ++i)
@@ -925,33 +921,19 @@ HM_INLINE void accelerations(Wave& W, const Shared& S, int lane, int64_t* st = n
     Lf[off] = v;
   }
   WAVE_SYNC();
-  // trunk pivots in sequence: pivot k updates every (ancestor i, ancestor-or-self j of i)
-  // pair from its still unscaled row, then scales its row (reads before writes: one
-  // phase per pivot); the next pivot's table words are loaded a pivot ahead
-  uint32_t pr = S.w[W_PAIR + NT - 1][lane];
-  uint32_t ka = S.w[W_KANC + ((NT - 1) >> 2)][lane];
+  // trunk pivots in sequence, one item per lane (W_TR): pivot k updates every (ancestor i,
+  // ancestor-or-self j of i) pair from its still unscaled row, then scales its row (reads
+  // before writes: one phase per pivot); the next pivot's item word is loaded a pivot ahead
+  uint32_t it = S.w[W_TR + NT - 1][lane];
 #pragma unroll 1
   for (int k = NT - 1; k >= 0; --k) {
-    const int a = (int)byte_of(ka, k & 3);
-    const int i0 = (int)byte_of(pr, 0), j0 = (int)byte_of(pr, 1), i1 = (int)byte_of(pr, 2), j1 = (int)byte_of(pr, 3);
-    // no-entry lanes read harmless in-range elements and write their junk slot
-    const int r0 = i0 == (int)NONE ? 0 : i0, c0 = j0 == (int)NONE ? 0 : j0;
-    const int r1 = i1 == (int)NONE ? 0 : i1, c1 = j1 == (int)NONE ? 0 : j1;
-    const int ca = a == (int)NONE ? 0 : a;
-    const double lkk = W.L[k][k];
-    const double l00 = Lf[r0 * NV + c0], lk0 = Lf[k * NV + r0], lkc0 = Lf[k * NV + c0];
-    const double l11 = Lf[r1 * NV + c1], lk1 = Lf[k * NV + r1], lkc1 = Lf[k * NV + c1];
-    const double lka = Lf[k * NV + ca];
-    const int kn = k > 0 ? k - 1 : 0;
-    pr = S.w[W_PAIR + kn][lane];
-    ka = S.w[W_KANC + (kn >> 2)][lane];
+    const double lkk = Lf[k * NV + k];
+    const double vd = Lf[it & 0x7ffu], v1 = Lf[(it >> 11) & 0x3ffu], v2 = Lf[(it >> 21) & 0x3ffu];
+    const uint32_t cur = it;
+    it = S.w[W_TR + (k > 0 ? k - 1 : 0)][lane];
     const double invd = 1.0 / lkk;
-    const double u0 = l00 - lk0 * (lkc0 * invd);
-    const double u1 = l11 - lk1 * (lkc1 * invd);
-    const double sc = lka * invd;
-    Lf[i0 == (int)NONE ? junk : r0 * NV + c0] = u0;
-    Lf[i1 == (int)NONE ? junk : r1 * NV + c1] = u1;
-    Lf[a == (int)NONE ? junk : k * NV + ca] = sc;
+    const double p = v1 * (v2 * invd);
+    Lf[cur & 0x7ffu] = (cur >> 31) ? vd - p : p;
     WAVE_SYNC();
   }
   HM_STAMP(10);
