@@ -1537,8 +1537,72 @@ struct HeadRows {
   const uint16_t* hid16;  // the hidden rows as bf16 bits instead of hid (the bf16 tape's)
 };
 
+// lane l takes the KPL consecutive hidden units KPL l .. KPL l + KPL - 1: their head-kernel
+// rows are one contiguous, 16-B aligned run of KPL A floats (KPL % 4 == 0), loaded as
+// float4s -- a quarter of the strided lane-per-unit loads' instructions (nh = 64 KPL)
+template <int KPL>
+__device__ inline float head_z_runs(const HeadRows& hr, int e, int lane) {
+  constexpr int A = HM_ACT;
+  static_assert(KPL % 4 == 0, "16-B aligned runs");
+  float acc[A], hv[KPL];
+#pragma unroll
+  for (int o = 0; o < A; ++o) acc[o] = 0.f;
+  if (hr.hid16) {
+    const uint4* h = reinterpret_cast<const uint4*>(hr.hid16 + (int64_t)e * hr.nh + KPL * lane);
+#pragma unroll
+    for (int q = 0; q < KPL / 8; ++q) {
+      const uint4 u = h[q];
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hv[8 * q + 2 * r] = __uint_as_float(w[r] << 16);
+        hv[8 * q + 2 * r + 1] = __uint_as_float(w[r] & 0xffff0000u);
+      }
+    }
+    if constexpr (KPL % 8 != 0) {
+      const uint2 u = reinterpret_cast<const uint2*>(hr.hid16 + (int64_t)e * hr.nh + KPL * lane)[KPL / 4 - 1];
+      hv[KPL - 4] = __uint_as_float(u.x << 16);
+      hv[KPL - 3] = __uint_as_float(u.x & 0xffff0000u);
+      hv[KPL - 2] = __uint_as_float(u.y << 16);
+      hv[KPL - 1] = __uint_as_float(u.y & 0xffff0000u);
+    }
+  } else {
+    const float4* h = reinterpret_cast<const float4*>(hr.hid + (int64_t)e * hr.nh + KPL * lane);
+#pragma unroll
+    for (int q = 0; q < KPL / 4; ++q) {
+      const float4 u = h[q];
+      hv[4 * q] = hr.bf ? bf16r(u.x) : u.x;
+      hv[4 * q + 1] = hr.bf ? bf16r(u.y) : u.y;
+      hv[4 * q + 2] = hr.bf ? bf16r(u.z) : u.z;
+      hv[4 * q + 3] = hr.bf ? bf16r(u.w) : u.w;
+    }
+  }
+  const float4* w4 = reinterpret_cast<const float4*>(hr.w + (int64_t)KPL * lane * A);
+#pragma unroll
+  for (int q = 0; q < KPL * A / 4; ++q) {
+    const float4 w = w4[q];
+    const float ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 4 * q + r;
+      acc[f % A] = fmaf(hv[f / A], hr.bf ? bf16r(ws[r]) : ws[r], acc[f % A]);
+    }
+  }
+  float z = 0.f;
+#pragma unroll
+  for (int o = 0; o < A; ++o) {
+    const float sum = wave_sumf(acc[o]);
+    if (lane == o) z = sum + hr.b[o];
+  }
+  return z;
+}
+
 __device__ inline float head_z(const HeadRows& hr, int e, int lane) {
   constexpr int A = HM_ACT;
+  const bool al = (reinterpret_cast<uintptr_t>(hr.w) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(hr.hid16 ? (const void*)hr.hid16 : (const void*)hr.hid) & 15) == 0;
+  if (al && hr.nh == 512) return head_z_runs<8>(hr, e, lane);
+  if (al && hr.nh == 256) return head_z_runs<4>(hr, e, lane);
   float acc[A];
 #pragma unroll
   for (int o = 0; o < A; ++o) acc[o] = 0.f;
@@ -1567,15 +1631,41 @@ __global__ __launch_bounds__(64 * WPB) void hm_act_kernel(RollArgs a, const floa
   hm::Wave& W = hm_block<WPB>(e, lane);
   constexpr int A = HM_ACT;
   const int E = a.d.n_envs;
-  hm_load_tables<WPB>(S, lane);
-  if (e >= E) return;  // after the tables' barrier
-  const int64_t row = (int64_t)t * E + e;
-  if (lane < HM_NS) W.s[lane] = a.b.env_state[(int64_t)lane * E + e];
-  // the kinematics of that state, as the step that left it computed them (first substep)
-  double* const kc = a.b.env_state + (int64_t)HM_NS * E + (int64_t)e * HM_KCACHE;
-  hm::load_kcache(W, kc, lane);
+  const bool live = e < E;
+  const int ec = live ? e : E - 1;  // a block's waves past E load a valid env, store nothing
+  double* const kc = a.b.env_state + (int64_t)HM_NS * E + (int64_t)ec * HM_KCACHE;
   const bool fused = hr.hid != nullptr || hr.hid16 != nullptr;
-  const float zh = fused ? head_z(hr, e, lane) : 0.f;
+  float zh = 0.f;
+  if constexpr (WPB == 4) {
+    // the model tables' global loads first, held in registers while the env's own loads
+    // (state, kinematics cache) and the head's dot products run, stored behind them:
+    // one load latency for the launch's prologue instead of three in sequence
+    constexpr int NW = (int)(sizeof(hm::Shared) / 8), PER = (NW + 64 * WPB - 1) / (64 * WPB);
+    const double* src = reinterpret_cast<const double*>(&hm::SHARED);
+    double tv[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int k = (int)threadIdx.x + 64 * WPB * i;
+      tv[i] = src[k < NW ? k : 0];
+    }
+    if (lane < HM_NS) W.s[lane] = a.b.env_state[(int64_t)lane * E + ec];
+    hm::load_kcache(W, kc, lane);
+    if (fused) zh = head_z(hr, ec, lane);
+    double* dst = reinterpret_cast<double*>(&S);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int k = (int)threadIdx.x + 64 * WPB * i;
+      if (k < NW) dst[k] = tv[i];
+    }
+    __syncthreads();
+  } else {
+    hm_load_tables<WPB>(S, lane);
+    if (lane < HM_NS) W.s[lane] = a.b.env_state[(int64_t)lane * E + ec];
+    hm::load_kcache(W, kc, lane);
+    if (fused) zh = head_z(hr, ec, lane);
+  }
+  if (!live) return;  // after the tables' barrier
+  const int64_t row = (int64_t)t * E + e;
   WAVE_SYNC();
   // sample (DiagGauss, core.py:432-435): a = z + sd * noise in fp32; the action is the ctrl
   if (lane < A) {

@@ -537,7 +537,8 @@ def test_bf16_rollout_prob_rows_equal_update_forward(env_id):
     assert d32 > 1e-4, d32
 
 
-def test_bf16_humanoid_rollout_hidden_rows_on_bf16_gemms():
+@pytest.mark.parametrize("hid", [[128, 64], [256, 512]])  # 512: the head's contiguous-run loads
+def test_bf16_humanoid_rollout_hidden_rows_on_bf16_gemms(hid):
     """bf16 mode, Humanoid (wave-per-env step, head fused into the step): the rollout's
     hidden layers run on mrl_gemm_bf16 with bf16 rows (mrl_rollout_act_head_bf16), the
     same kernels and rounding points as the update's bf16 tape, so the prob rows the
@@ -547,7 +548,7 @@ def test_bf16_humanoid_rollout_hidden_rows_on_bf16_gemms():
     from modular_rl_amd.envs import make
     env = make("Humanoid-v2")
     cfg = dict(timestep_limit=env.spec.max_episode_steps, n_envs=256, horizon=16, seed=3, mlp_dtype="bf16",
-               hid_sizes=[128, 64])
+               hid_sizes=hid)
     agent = TrpoAgent(env.observation_space, env.action_space, cfg)
     net = agent.policy.net
     col = agent.make_collector(env, cfg)
