@@ -1339,6 +1339,17 @@ __global__ __launch_bounds__(RB) void lrollout_obs_kernel(RollArgs a, int t) {
   double* fs_out = a.b.filter_state + ((t + 1) & 1) * a.FS;
   const double* rec = a.b.records + (int64_t)(t & 1) * a.nb * a.RS;
   const int kbase = blockIdx.y * LCOLS;
+  // this block's raw observation values, loaded first: their latency runs under the
+  // record loads and the merge below (they do not depend on it)
+  const int e0 = blockIdx.x * ENVS_PER_BLOCK;
+  const int nvalid = min(ENVS_PER_BLOCK, E - e0);
+  const int el = threadIdx.x % ENVS_PER_BLOCK, kb = threadIdx.x / ENVS_PER_BLOCK;
+  double v[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    const int k = kbase + kb + G * q;
+    v[q] = (k < O && el < nvalid) ? a.b.raw_obs[(int64_t)k * E + e0 + el] : 0.0;
+  }
   if (threadIdx.x < LCOLS && kbase + (int)threadIdx.x < D) {
     const int k = kbase + threadIdx.x;
     const bool isr = (k == O);
@@ -1346,43 +1357,71 @@ __global__ __launch_bounds__(RB) void lrollout_obs_kernel(RollArgs a, int t) {
     // chunk's sums (the sums themselves stay sequential in block order, as the oracle's);
     // one dependent global load per block per pass had made this launch ~14 us of waiting
     constexpr int LREC = 16;
-    double bn = 0.0, sm = 0.0;
-    for (int b0 = 0; b0 < a.nb; b0 += LREC) {
-      double rn[LREC], rm[LREC];
+    double bn = 0.0, sm = 0.0, bm = 0.0, bs = 0.0;
+    // the filter's M2 terms and the fs_in state loaded with the first chunk (one record
+    // round trip when nb <= LREC: the second pass reuses the first's loads)
+    double rn1[LREC], rm1[LREC], rs1[LREC];
+    const double n0 = fs_in[isr ? 1 : 0], M0 = fs_in[2 + k], S0 = fs_in[2 + D + k];
+    if (a.nb <= LREC) {
 #pragma unroll
       for (int q = 0; q < LREC; ++q) {
-        const double* r = rec + (int64_t)min(b0 + q, a.nb - 1) * a.RS;
-        rn[q] = r[isr ? 1 : 0];
-        rm[q] = r[2 + k];
+        const double* r = rec + (int64_t)min(q, a.nb - 1) * a.RS;
+        rn1[q] = r[isr ? 1 : 0];
+        rm1[q] = r[2 + k];
+        rs1[q] = r[2 + D + k];
       }
 #pragma unroll
       for (int q = 0; q < LREC; ++q)
-        if (b0 + q < a.nb) {
-          bn += rn[q];
-          sm += rn[q] * rm[q];
+        if (q < a.nb) {
+          bn += rn1[q];
+          sm += rn1[q] * rm1[q];
         }
-    }
-    double bm = 0.0, bs = 0.0;
-    if (bn > 0.0) {
-      bm = sm / bn;
+      if (bn > 0.0) {
+        bm = sm / bn;
+#pragma unroll
+        for (int q = 0; q < LREC; ++q)
+          if (q < a.nb && rn1[q] > 0.0) {
+            const double dm = rm1[q] - bm;
+            bs += rs1[q] + rn1[q] * dm * dm;
+          }
+      }
+    } else {
       for (int b0 = 0; b0 < a.nb; b0 += LREC) {
-        double rn[LREC], rm[LREC], rs[LREC];
+        double rn[LREC], rm[LREC];
 #pragma unroll
         for (int q = 0; q < LREC; ++q) {
           const double* r = rec + (int64_t)min(b0 + q, a.nb - 1) * a.RS;
           rn[q] = r[isr ? 1 : 0];
           rm[q] = r[2 + k];
-          rs[q] = r[2 + D + k];
         }
 #pragma unroll
         for (int q = 0; q < LREC; ++q)
-          if (b0 + q < a.nb && rn[q] > 0.0) {
-            const double dm = rm[q] - bm;
-            bs += rs[q] + rn[q] * dm * dm;
+          if (b0 + q < a.nb) {
+            bn += rn[q];
+            sm += rn[q] * rm[q];
           }
       }
+      if (bn > 0.0) {
+        bm = sm / bn;
+        for (int b0 = 0; b0 < a.nb; b0 += LREC) {
+          double rn[LREC], rm[LREC], rs[LREC];
+#pragma unroll
+          for (int q = 0; q < LREC; ++q) {
+            const double* r = rec + (int64_t)min(b0 + q, a.nb - 1) * a.RS;
+            rn[q] = r[isr ? 1 : 0];
+            rm[q] = r[2 + k];
+            rs[q] = r[2 + D + k];
+          }
+#pragma unroll
+          for (int q = 0; q < LREC; ++q)
+            if (b0 + q < a.nb && rn[q] > 0.0) {
+              const double dm = rm[q] - bm;
+              bs += rs[q] + rn[q] * dm * dm;
+            }
+        }
+      }
     }
-    double n = fs_in[isr ? 1 : 0], M = fs_in[2 + k], S = fs_in[2 + D + k];
+    double n = n0, M = M0, S = S0;
     chan_merge(n, M, S, bn, bm, bs);
     if (blockIdx.x == 0) {
       if (k == 0) fs_out[0] = n;
@@ -1396,17 +1435,8 @@ __global__ __launch_bounds__(RB) void lrollout_obs_kernel(RollArgs a, int t) {
   }
   __syncthreads();
   // normalised obs rows (core.py:191-192): SoA raw -> LDS tile -> row-major fp32 rows
-  const int e0 = blockIdx.x * ENVS_PER_BLOCK;
-  const int nvalid = min(ENVS_PER_BLOCK, E - e0);
   const int64_t row0 = (int64_t)t * E + e0;
   {
-    const int el = threadIdx.x % ENVS_PER_BLOCK, kb = threadIdx.x / ENVS_PER_BLOCK;
-    double v[CPT];
-#pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-      const int k = kbase + kb + G * q;
-      v[q] = (k < O && el < nvalid) ? a.b.raw_obs[(int64_t)k * E + e0 + el] : 0.0;
-    }
 #pragma unroll
     for (int q = 0; q < CPT; ++q) {
       const int kl = kb + G * q;
