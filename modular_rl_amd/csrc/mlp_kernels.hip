@@ -1107,6 +1107,11 @@ constexpr int MBOX_GH = 2 * MAX_OUT;  // mailbox row pitch (floats): the widest 
 #ifndef MRL_FISHER_VJP_NT
 #define MRL_FISHER_VJP_NT 0
 #endif
+// diagnostic builds only: issue priority of one role's waves (s_setprio 1; 1 = the VJP
+// role, 2 = the JVP role) -- 0, the default, leaves both at the same priority
+#ifndef MRL_FISHER_PRIO
+#define MRL_FISHER_PRIO 0
+#endif
 __device__ inline f32x4 ldv4(const f32x4* p) {
   if constexpr (MRL_FISHER_VJP_NT) return __builtin_nontemporal_load(p);
   return *p;
@@ -1256,6 +1261,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
       split_shape<SH>(ra, rb);
       JvpSplitRole role;
       role.init(ra, rb, ldsx, ldsx + WS, lane);
+      if constexpr (MRL_FISHER_PRIO == 2) __builtin_amdgcn_s_setprio(1);
       float sd[MAX_OUT], dls[MAX_OUT];
 #pragma unroll
       for (int j = 0; j < MAX_OUT; ++j) {
@@ -1290,6 +1296,7 @@ __global__ __launch_bounds__(64 * VJP16_WAVES, 1) void mlp_fisher_hyb_kernel(Vjp
     }
   }
 
+  if constexpr (MRL_FISHER_PRIO == 1 && PROD == 0) __builtin_amdgcn_s_setprio(1);
   f32x4 gW1[4][4], gW2[4], gW0[MT0][4];
   f32x4 zero4 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
