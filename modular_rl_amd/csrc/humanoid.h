@@ -203,6 +203,16 @@ constexpr int W_BR = W_ENT + N_ENT_WORDS;      // [NBSTEP][NBSLOT + 1] branch-st
 constexpr int W_TG = W_BR + NBSTEP * (NBSLOT + 1);  // trunk entry `lane`: i NV + j | branch pivots below i << 16
 constexpr int W_PDOF = W_TG + 1;                    // [PD_WORDS] body (lane & 15)'s path dofs (bytes)
 constexpr int W_TR = W_PDOF + PD_WORDS;             // [NT] trunk pivot k's item at this lane (one per lane)
+// the lane of trunk pivot k's item on the next pivot's diagonal (k - 1, k - 1), packed 6
+// bits per pivot (k >= 1; the trunk is a chain, so k - 1 is k's parent)
+constexpr uint64_t trunk_diag_lanes() {
+  uint64_t m = 0;
+  for (int k = 1; k < NT; ++k)
+    for (int pp = LDL_START[k]; pp < LDL_START[k + 1]; ++pp)
+      if (LDL_I[pp] == k - 1 && LDL_J[pp] == k - 1) m |= (uint64_t)(pp - LDL_START[k]) << (6 * k);
+  return m;
+}
+constexpr uint64_t TRUNK_DIAG_LANES = trunk_diag_lanes();
 constexpr int TOPO_WORDS = W_TR + NT;
 constexpr bool ldl_schedule_fits() {
   for (int d = 0; d < NT; ++d)
@@ -923,19 +933,29 @@ HM_INLINE void accelerations(Wave& W, const Shared& S, int lane, int64_t* st = n
   WAVE_SYNC();
   // trunk pivots in sequence, one item per lane (W_TR): pivot k updates every (ancestor i,
   // ancestor-or-self j of i) pair from its still unscaled row, then scales its row (reads
-  // before writes: one phase per pivot); the next pivot's item word is loaded a pivot ahead
+  // before writes: one phase per pivot).  The next pivot's reciprocal diagonal is formed
+  // from the value pivot k just computed for (k - 1, k - 1) -- its final value, pivot k
+  // being the last to update it -- on the lane that holds it, while the next pivot's LDS
+  // operands are in flight, and broadcast by readlane: the division leaves the chain.
   uint32_t it = S.w[W_TR + NT - 1][lane];
+  double invd = 1.0 / Lf[(NT - 1) * NV + NT - 1];
+  double vd = Lf[it & 0x7ffu], v1 = Lf[(it >> 11) & 0x3ffu], v2 = Lf[(it >> 21) & 0x3ffu];
 #pragma unroll 1
   for (int k = NT - 1; k >= 0; --k) {
-    const double lkk = Lf[k * NV + k];
-    const double vd = Lf[it & 0x7ffu], v1 = Lf[(it >> 11) & 0x3ffu], v2 = Lf[(it >> 21) & 0x3ffu];
     const uint32_t cur = it;
-    it = S.w[W_TR + (k > 0 ? k - 1 : 0)][lane];
-    const double invd = 1.0 / lkk;
     const double p = v1 * (v2 * invd);
-    Lf[cur & 0x7ffu] = (cur >> 31) ? vd - p : p;
-    WAVE_SYNC();
+    const double r = (cur >> 31) ? vd - p : p;
+    Lf[cur & 0x7ffu] = r;
+    if (k > 0) {
+      WAVE_SYNC();
+      it = S.w[W_TR + k - 1][lane];
+      vd = Lf[it & 0x7ffu];
+      v1 = Lf[(it >> 11) & 0x3ffu];
+      v2 = Lf[(it >> 21) & 0x3ffu];
+      invd = read_lane(1.0 / r, (int)((TRUNK_DIAG_LANES >> (6 * k)) & 63u));
+    }
   }
+  WAVE_SYNC();
   HM_STAMP(10);
   // the solves with x in registers (lane j holds x_j), the pivot broadcast by readlane:
   // L^T y = x (leaves first), D z = y, L x = z (column by column)
