@@ -368,6 +368,13 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run the VF fit in the reference order instead of beside the next rollout")
     args = ap.parse_args()
+    # stdout carries exactly the one JSON line: whatever else reaches file descriptor 1 --
+    # native libraries' banners (RCCL prints its version block there when a communicator
+    # is created) or a stray print -- is sent to stderr, and the line goes to a duplicate
+    # of the original stdout
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     from modular_rl_amd import timing
     from modular_rl_amd.agentzoo import TrpoAgent
@@ -554,7 +561,8 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(cpu_E, cpu_T, args.env, hid)
         line["cpu_baseline"]["serial_c1"] = cpu_serial_c1()
-    print(json.dumps(line), flush=True)
+    json_out.write(json.dumps(line) + "\n")
+    json_out.flush()
     return runner
 
 
